@@ -1,0 +1,157 @@
+/*
+ * skv.h — C ABI of the MI355X compaction path for skyvault v1 runs.
+ *
+ * This is the drop-in boundary for skyvault's byte-heavy compaction core:
+ *
+ *     runs::read_run_stream   (src/runs.rs:517-628)     decode every input run
+ *  -> k_way::merge            (src/k_way.rs:113-179)    newest seq_no wins per key
+ *  -> [Delete filter]         (src/jobs/table_tree_compaction.rs:139-145)
+ *  -> [WAL table split]       (src/jobs/wal_compaction.rs:66-174)
+ *  -> runs::build_runs        (src/runs.rs:166-282)     greedy split into <= max-byte runs
+ *
+ * One skv_compact() call replaces that whole composition as it appears in the three
+ * compaction jobs (table_buffer_compaction.rs:224-279, table_tree_compaction.rs:81-147,
+ * wal_compaction.rs:207-347). The jobs keep doing everything around it (forest
+ * snapshot, get_run/put_run, metadata commit), so the Rust side binds this header through
+ * a thin `extern "C"` block called from `tokio::task::spawn_blocking`.
+ *
+ * Conventions
+ *  - Blocking calls. One skv_ctx per GPU; calls on one ctx are serialised by the caller,
+ *    different ctxs (GPUs) may run concurrently from different threads.
+ *  - Inputs are borrowed for the duration of the call and never modified.
+ *  - All-or-nothing: on error no result is produced. (The reference streams finished
+ *    output runs to S3 before a later error surfaces; those orphans are invisible to the
+ *    forest, so "job failed" is the only observable outcome and is what we model.)
+ *  - The result owns its memory; free it with skv_result_free().
+ *  - Error messages are the reference's Display text of RunError / JobError.
+ */
+#ifndef SKV_H
+#define SKV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SKV_ABI_VERSION 1
+
+typedef struct skv_ctx skv_ctx;
+
+/*
+ * One input stream of k_way::merge: a (SeqNo, stream) pair (k_way.rs:113). The stream is
+ * the flattened concatenation of its member runs, each decoded separately by
+ * read_run_stream — exactly how the jobs build their inputs (table_buffer_compaction.rs
+ * :243-275 concatenates all L0 runs into one stream at SeqNo 0; table_tree_compaction.rs
+ * :105-135 does the same for the overlapping next-level runs). A stream with n_runs == 0
+ * yields nothing (k_way.rs:138); a member run of 0 bytes yields RunError::EmptyInput.
+ * seq_no values must be pairwise distinct (k_way.rs:121 keys streams by SeqNo).
+ */
+typedef struct {
+    const uint8_t* const* runs; /* member runs, in order (host or device pointers, see below) */
+    const uint64_t* run_lens;   /* byte length of each member run */
+    uint32_t n_runs;
+    int64_t seq_no;
+} skv_stream;
+
+/*
+ * One output run, as yielded by build_runs (runs.rs:221-228, :271-280) together with
+ * its Stats::StatsV1 (runs.rs:102-109). len == StatsV1.size_bytes (the version byte is
+ * counted, runs.rs:241-244). min_key / max_key point into the result bytes.
+ */
+typedef struct {
+    uint64_t off;          /* byte offset of the run within skv_result.bytes */
+    uint64_t len;          /* run size in bytes == StatsV1.size_bytes */
+    uint64_t put_count;    /* StatsV1.put_count */
+    uint64_t delete_count; /* StatsV1.delete_count */
+    uint64_t min_key_off;  /* StatsV1.min_key = bytes[min_key_off .. +min_key_len] */
+    uint64_t min_key_len;
+    uint64_t max_key_off;  /* StatsV1.max_key = bytes[max_key_off .. +max_key_len] */
+    uint64_t max_key_len;
+    int64_t table_id;      /* SKV_SPLIT_BY_TABLE: owning table (wal_compaction.rs:248-252); else 0 */
+    uint64_t reserved;
+} skv_run_desc;
+
+typedef struct {
+    uint8_t* bytes;      /* concatenated output runs (host memory, or device memory for skv_compact_dev) */
+    uint64_t n_bytes;
+    skv_run_desc* runs;  /* host memory, n_runs entries, in emission order */
+    uint64_t n_runs;
+    /* diagnostics */
+    uint64_t in_bytes;       /* total input run bytes (the metric's I) */
+    uint64_t in_records;     /* records decoded from the inputs */
+    uint64_t out_records;    /* records written to the output runs */
+    uint64_t dropped_tables; /* SKV_SPLIT_BY_TABLE: tables whose build the reference discards
+                                (wal_compaction.rs:276, :341 swallow a failed table task) */
+} skv_result;
+
+/* Status codes. The first five mirror the reference's error variants. */
+enum {
+    SKV_OK = 0,
+    SKV_E_EMPTY_INPUT = 1,         /* RunError::EmptyInput          (runs.rs:93, :537-540) */
+    SKV_E_UNSUPPORTED_VERSION = 2, /* RunError::UnsupportedVersion  (runs.rs:91, :553-556) */
+    SKV_E_IO = 3,                  /* RunError::Io, UnexpectedEof   (runs.rs:85, :570-576, :598-604) */
+    SKV_E_FORMAT = 4,              /* RunError::Format(..)          (runs.rs:87; :194, :581, :588, :609, :622) */
+    SKV_E_INVALID_INPUT = 5,       /* JobError::InvalidInput, WAL key (jobs/mod.rs:26; wal_compaction.rs:244-251) */
+    SKV_E_INVALID_ARG = 6,         /* API misuse: NULL pointers, duplicate seq_no, bad device */
+    SKV_E_DEVICE = 7,              /* HIP runtime failure or device capacity exceeded */
+    SKV_E_UNSUPPORTED = 8          /* input shape outside what this build supports (message says which) */
+};
+
+/* skv_compact flags */
+enum {
+    SKV_DROP_TOMBSTONES = 1, /* drop Delete ops after the merge: compaction into Level::max()
+                                (table_tree_compaction.rs:139-145, metadata.rs:117-126) */
+    SKV_SPLIT_BY_TABLE = 2   /* WAL compaction: split merged ops by "{table_id}." key prefix, strip
+                                it, one build_runs per table with the reference's exactly-one-run
+                                rule and error swallowing (wal_compaction.rs:239-347) */
+};
+
+/* Per-phase device timings of the last call (HIP events on the ctx stream), when enabled. */
+typedef struct {
+    double total_ms;    /* first kernel -> last kernel of the compaction */
+    double parse_ms;    /* record-boundary discovery + key extraction */
+    double check_ms;    /* in-stream order / error triggers */
+    double merge_ms;    /* splitters + tile merge + dedup/filter + prefix sums */
+    double chain_ms;    /* greedy max-size split (run boundaries + stats) */
+    double gather_ms;   /* byte gather of surviving records into output runs */
+    uint64_t gather_read_bytes;  /* algorithmic bytes read by the gather (surviving input records) */
+    uint64_t gather_write_bytes; /* algorithmic bytes written by the gather (== output bytes) */
+    uint64_t host_syncs;
+} skv_timings;
+
+int skv_abi_version(void);
+int skv_device_count(int* out);
+
+/* device >= 0: HIP device ordinal. There is no CPU mode: the CPU restatement under oracle/
+ * is test infrastructure and is not reachable through this ABI. */
+int skv_ctx_create(int device, skv_ctx** out);
+void skv_ctx_destroy(skv_ctx* ctx);
+const char* skv_last_error(const skv_ctx* ctx); /* reference Display text of the last error */
+int skv_ctx_set_profiling(skv_ctx* ctx, int enable);
+int skv_ctx_get_timings(const skv_ctx* ctx, skv_timings* out);
+
+/*
+ * Host-memory entry point: the shape skyvault's jobs have (Bytes in from get_run,
+ * Bytes out to put_run). Inputs are staged to HBM, compacted on the GPU, and the output
+ * runs come back in pinned host memory.
+ */
+int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams,
+                uint64_t max_run_size, uint32_t flags, skv_result** out);
+
+/*
+ * Device-resident entry point: every runs[i] is a device pointer on the ctx's GPU, and the
+ * returned result->bytes is a device pointer owned by the ctx (valid until the next call
+ * on the ctx or skv_result_free). Descriptors are host memory.
+ */
+int skv_compact_dev(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams,
+                    uint64_t max_run_size, uint32_t flags, skv_result** out);
+
+void skv_result_free(skv_result* r);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SKV_H */

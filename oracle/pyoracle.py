@@ -1,0 +1,195 @@
+"""ctypes wrapper of oracle/libskv_oracle.so — the CPU restatement of skyvault's compaction
+path. TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product package (skyvault-rs_amd/skv).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+from typing import List, Sequence, Tuple
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "skyvault-rs_amd"))
+
+from skv._abi import (  # noqa: E402
+    SKV_OK,
+    RunError,
+    SkvResult,
+    StreamArgs,
+    result_to_runs,
+)
+
+LIB = os.path.join(HERE, "libskv_oracle.so")
+
+
+class SkvoOp(C.Structure):
+    _fields_ = [
+        ("is_put", C.c_uint32),
+        ("key_len", C.c_uint32),
+        ("key", C.c_void_p),
+        ("val_len", C.c_uint64),
+        ("val", C.c_void_p),
+    ]
+
+
+class SkvoOpList(C.Structure):
+    _fields_ = [("ops", C.POINTER(SkvoOp)), ("n_ops", C.c_uint64), ("arena", C.c_void_p)]
+
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB):
+        subprocess.check_call(["make", "-s", "-C", HERE, "libskv_oracle.so"])
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        l = C.CDLL(LIB)
+        l.skvo_compact.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
+                                   C.POINTER(C.POINTER(SkvResult)), C.c_char_p, C.c_size_t]
+        l.skvo_compact.restype = C.c_int
+        l.skvo_build_runs.argtypes = [C.POINTER(SkvoOp), C.c_uint64, C.c_uint64,
+                                      C.POINTER(C.POINTER(SkvResult)), C.c_char_p, C.c_size_t]
+        l.skvo_build_runs.restype = C.c_int
+        l.skvo_decode_run.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.POINTER(SkvoOpList)),
+                                      C.c_char_p, C.c_size_t]
+        l.skvo_decode_run.restype = C.c_int
+        l.skvo_merge_ops.argtypes = [C.POINTER(C.POINTER(SkvoOp)), C.POINTER(C.c_uint64),
+                                     C.POINTER(C.c_int64), C.c_uint32,
+                                     C.POINTER(C.POINTER(SkvoOpList)), C.c_char_p, C.c_size_t]
+        l.skvo_merge_ops.restype = C.c_int
+        l.skvo_result_free.argtypes = [C.POINTER(SkvResult)]
+        l.skvo_op_list_free.argtypes = [C.POINTER(SkvoOpList)]
+        _lib = l
+    return _lib
+
+
+# ops are tuples: (True, key_bytes, value_bytes) for Put, (False, key_bytes, None) for Delete
+Op = Tuple[bool, bytes, object]
+
+
+def _ops_array(ops: Sequence[Op]):
+    keep = []
+    arr = (SkvoOp * max(1, len(ops)))()
+    for i, (is_put, k, v) in enumerate(ops):
+        kb = C.create_string_buffer(bytes(k), max(1, len(k)))
+        keep.append(kb)
+        arr[i].is_put = 1 if is_put else 0
+        arr[i].key_len = len(k)
+        arr[i].key = C.cast(kb, C.c_void_p)
+        if is_put:
+            vb = C.create_string_buffer(bytes(v), max(1, len(v)))
+            keep.append(vb)
+            arr[i].val_len = len(v)
+            arr[i].val = C.cast(vb, C.c_void_p)
+    return arr, keep
+
+
+def _op_list(ptr) -> List[Op]:
+    l = ptr.contents
+    out = []
+    for i in range(l.n_ops):
+        o = l.ops[i]
+        k = C.string_at(o.key, o.key_len) if o.key_len else b""
+        if o.is_put:
+            v = C.string_at(o.val, o.val_len) if o.val_len else b""
+            out.append((True, k, v))
+        else:
+            out.append((False, k, None))
+    return out
+
+
+def compact(streams: Sequence[tuple], max_run_size: int, flags: int = 0, with_result: bool = False):
+    """streams: [(seq_no, [run_bytes, ...])]. Returns [OutRun] or raises RunError."""
+    sa = StreamArgs(streams)
+    res = C.POINTER(SkvResult)()
+    eb = C.create_string_buffer(512)
+    rc = lib().skvo_compact(C.cast(sa.arr, C.c_void_p), sa.n, max_run_size, flags, C.byref(res), eb, 512)
+    if rc != SKV_OK:
+        raise RunError(rc, eb.value.decode("utf-8", "replace"))
+    try:
+        runs = result_to_runs(res.contents)
+        info = dict(in_bytes=res.contents.in_bytes, out_records=res.contents.out_records,
+                    dropped_tables=res.contents.dropped_tables, n_bytes=res.contents.n_bytes)
+    finally:
+        lib().skvo_result_free(res)
+    return (runs, info) if with_result else runs
+
+
+def compact_bytes(streams: Sequence[tuple], max_run_size: int, flags: int = 0):
+    """Like compact() but returns (concatenated output bytes, [descriptor tuples])."""
+    sa = StreamArgs(streams)
+    res = C.POINTER(SkvResult)()
+    eb = C.create_string_buffer(512)
+    rc = lib().skvo_compact(C.cast(sa.arr, C.c_void_p), sa.n, max_run_size, flags, C.byref(res), eb, 512)
+    if rc != SKV_OK:
+        raise RunError(rc, eb.value.decode("utf-8", "replace"))
+    try:
+        r = res.contents
+        data = C.string_at(r.bytes, r.n_bytes) if r.n_bytes else b""
+        descs = [(d.off, d.len, d.put_count, d.delete_count, d.min_key_off, d.min_key_len,
+                  d.max_key_off, d.max_key_len, d.table_id) for d in (r.runs[i] for i in range(r.n_runs))]
+    finally:
+        lib().skvo_result_free(res)
+    return data, descs
+
+
+def build_runs(ops: Sequence[Op], max_run_size: int):
+    arr, keep = _ops_array(ops)
+    res = C.POINTER(SkvResult)()
+    eb = C.create_string_buffer(512)
+    rc = lib().skvo_build_runs(arr, len(ops), max_run_size, C.byref(res), eb, 512)
+    if rc != SKV_OK:
+        raise RunError(rc, eb.value.decode("utf-8", "replace"))
+    try:
+        return result_to_runs(res.contents)
+    finally:
+        lib().skvo_result_free(res)
+
+
+def decode_run(data: bytes):
+    """read_run_stream: returns (ops, error_or_None)."""
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    out = C.POINTER(SkvoOpList)()
+    eb = C.create_string_buffer(512)
+    rc = lib().skvo_decode_run(C.cast(buf, C.c_void_p), len(data), C.byref(out), eb, 512)
+    try:
+        ops = _op_list(out)
+    finally:
+        lib().skvo_op_list_free(out)
+    err = None if rc == SKV_OK else RunError(rc, eb.value.decode("utf-8", "replace"))
+    return ops, err
+
+
+def merge_ops(streams: Sequence[Tuple[int, Sequence[Op]]]):
+    """k_way::merge over decoded op lists: returns (emitted ops, error_or_None)."""
+    n = len(streams)
+    keep = []
+    ptrs = (C.POINTER(SkvoOp) * max(1, n))()
+    lens = (C.c_uint64 * max(1, n))()
+    seqs = (C.c_int64 * max(1, n))()
+    for i, (seq, ops) in enumerate(streams):
+        arr, k = _ops_array(ops)
+        keep += [arr, k]
+        ptrs[i] = C.cast(arr, C.POINTER(SkvoOp))
+        lens[i] = len(ops)
+        seqs[i] = seq
+    out = C.POINTER(SkvoOpList)()
+    eb = C.create_string_buffer(512)
+    rc = lib().skvo_merge_ops(ptrs, lens, seqs, n, C.byref(out), eb, 512)
+    ops = []
+    if out:
+        try:
+            ops = _op_list(out)
+        finally:
+            lib().skvo_op_list_free(out)
+    err = None if rc == SKV_OK else RunError(rc, eb.value.decode("utf-8", "replace"))
+    return ops, err

@@ -1,0 +1,180 @@
+"""ctypes mirror of include/skv.h (the C ABI of the compaction path).
+
+Shared by the product wrapper (skv.runs / skv.jobs, which load libskv.so) and by the test
+tooling that loads the CPU restatement under oracle/. Only plain pointers and sizes cross
+the boundary — no torch types.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT_DIR = os.path.dirname(os.path.dirname(PKG_DIR))
+LIB_PATH = os.path.join(PKG_DIR, "libskv.so")
+
+SKV_OK = 0
+SKV_E_EMPTY_INPUT = 1
+SKV_E_UNSUPPORTED_VERSION = 2
+SKV_E_IO = 3
+SKV_E_FORMAT = 4
+SKV_E_INVALID_INPUT = 5
+SKV_E_INVALID_ARG = 6
+SKV_E_DEVICE = 7
+SKV_E_UNSUPPORTED = 8
+
+SKV_DROP_TOMBSTONES = 1
+SKV_SPLIT_BY_TABLE = 2
+
+ERROR_NAMES = {
+    SKV_E_EMPTY_INPUT: "EmptyInput",
+    SKV_E_UNSUPPORTED_VERSION: "UnsupportedVersion",
+    SKV_E_IO: "Io",
+    SKV_E_FORMAT: "Format",
+    SKV_E_INVALID_INPUT: "InvalidInput",
+    SKV_E_INVALID_ARG: "InvalidArgument",
+    SKV_E_DEVICE: "Device",
+    SKV_E_UNSUPPORTED: "Unsupported",
+}
+
+
+class SkvStream(C.Structure):
+    _fields_ = [
+        ("runs", C.POINTER(C.c_void_p)),
+        ("run_lens", C.POINTER(C.c_uint64)),
+        ("n_runs", C.c_uint32),
+        ("seq_no", C.c_int64),
+    ]
+
+
+class SkvRunDesc(C.Structure):
+    _fields_ = [
+        ("off", C.c_uint64),
+        ("len", C.c_uint64),
+        ("put_count", C.c_uint64),
+        ("delete_count", C.c_uint64),
+        ("min_key_off", C.c_uint64),
+        ("min_key_len", C.c_uint64),
+        ("max_key_off", C.c_uint64),
+        ("max_key_len", C.c_uint64),
+        ("table_id", C.c_int64),
+        ("reserved", C.c_uint64),
+    ]
+
+
+class SkvResult(C.Structure):
+    _fields_ = [
+        ("bytes", C.c_void_p),
+        ("n_bytes", C.c_uint64),
+        ("runs", C.POINTER(SkvRunDesc)),
+        ("n_runs", C.c_uint64),
+        ("in_bytes", C.c_uint64),
+        ("in_records", C.c_uint64),
+        ("out_records", C.c_uint64),
+        ("dropped_tables", C.c_uint64),
+    ]
+
+
+class SkvTimings(C.Structure):
+    _fields_ = [
+        ("total_ms", C.c_double),
+        ("parse_ms", C.c_double),
+        ("check_ms", C.c_double),
+        ("merge_ms", C.c_double),
+        ("chain_ms", C.c_double),
+        ("gather_ms", C.c_double),
+        ("gather_read_bytes", C.c_uint64),
+        ("gather_write_bytes", C.c_uint64),
+        ("host_syncs", C.c_uint64),
+    ]
+
+
+# Every symbol include/skv.h declares (tests/test_abi.py checks the built library exports them).
+EXPORTED_SYMBOLS = [
+    "skv_abi_version",
+    "skv_device_count",
+    "skv_ctx_create",
+    "skv_ctx_destroy",
+    "skv_last_error",
+    "skv_ctx_set_profiling",
+    "skv_ctx_get_timings",
+    "skv_compact",
+    "skv_compact_dev",
+    "skv_result_free",
+]
+
+
+@dataclass
+class Stats:
+    """Stats::StatsV1 (runs.rs:102-109)."""
+
+    min_key: str
+    max_key: str
+    size_bytes: int
+    put_count: int
+    delete_count: int
+
+
+@dataclass
+class OutRun:
+    data: bytes
+    stats: Stats
+    table_id: int = 0
+
+
+class RunError(Exception):
+    """RunError / JobError surfaced through the ABI. `kind` names the reference variant,
+    `message` is the reference's Display text."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(message)
+        self.code = code
+        self.kind = ERROR_NAMES.get(code, str(code))
+        self.message = message
+
+
+class StreamArgs:
+    """Keeps the ctypes arrays of one skv_stream[] alive for a call."""
+
+    def __init__(self, streams: Sequence[tuple], device: bool = False):
+        # streams: [(seq_no, [run_ptr_or_bytes, ...], [len, ...]?)]
+        self._keep: List[object] = []
+        self.arr = (SkvStream * max(1, len(streams)))()
+        self.n = len(streams)
+        for i, st in enumerate(streams):
+            seq, runs = st[0], st[1]
+            n = len(runs)
+            ptrs = (C.c_void_p * max(1, n))()
+            lens = (C.c_uint64 * max(1, n))()
+            for j, r in enumerate(runs):
+                if device:
+                    ptr, ln = r
+                    ptrs[j] = C.c_void_p(int(ptr))
+                    lens[j] = int(ln)
+                else:
+                    b = bytes(r)
+                    buf = C.create_string_buffer(b, max(1, len(b)))
+                    self._keep.append(buf)
+                    ptrs[j] = C.cast(buf, C.c_void_p)
+                    lens[j] = len(b)
+            self._keep += [ptrs, lens]
+            self.arr[i].runs = C.cast(ptrs, C.POINTER(C.c_void_p))
+            self.arr[i].run_lens = C.cast(lens, C.POINTER(C.c_uint64))
+            self.arr[i].n_runs = n
+            self.arr[i].seq_no = int(seq)
+
+
+def result_to_runs(res: SkvResult, host_bytes: Optional[bytes] = None) -> List[OutRun]:
+    """Turn an skv_result (host bytes) into [(run bytes, StatsV1)]."""
+    if host_bytes is None:
+        host_bytes = C.string_at(res.bytes, res.n_bytes) if res.n_bytes else b""
+    out = []
+    for i in range(res.n_runs):
+        d = res.runs[i]
+        data = host_bytes[d.off : d.off + d.len]
+        mn = host_bytes[d.min_key_off : d.min_key_off + d.min_key_len].decode("utf-8")
+        mx = host_bytes[d.max_key_off : d.max_key_off + d.max_key_len].decode("utf-8")
+        out.append(OutRun(data, Stats(mn, mx, d.len, d.put_count, d.delete_count), d.table_id))
+    return out
