@@ -1,0 +1,210 @@
+// skv_dev.hpp — shared definitions of the MI355X compaction path (device + host side).
+//
+// Data layout in HBM (one compaction, see DESIGN.md "Data layout"):
+//   runs[]          RunInfo per input member run, in "rank order": streams sorted by seq_no
+//                   descending, members in stream order. Record index (rec_idx) follows the same
+//                   order, so for equal keys "smaller rec_idx" == "newer seq_no" == the record
+//                   k_way::merge keeps (k_way.rs:20-27, :146-151).
+//   chunk arrays    per CHUNK bytes of run body: speculative walk summaries.
+//   record arrays   per record (rec_idx): absolute address, 16-byte BE key prefix, key length,
+//                   meta = size | is_delete<<31.
+//   merged arrays   per surviving record in output order: source address, output-byte prefix P,
+//                   delete-count prefix, rec_idx.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace skv {
+
+constexpr uint64_t CHUNK = 4096;          // bytes of run body per speculative walk lane
+constexpr int TILE_CAP = 4096;            // max elements a merge tile sorts in LDS
+constexpr int TILE_TARGET = 2048;         // target elements per merge tile
+constexpr int TILE_THREADS = 1024;
+constexpr int GATHER_SEG = 256;           // surviving records per gather workgroup
+constexpr int GATHER_THREADS = 256;
+constexpr uint32_t NO_POS32 = 0xFFFFFFFFu;
+constexpr uint64_t NO_POS = ~0ull;
+
+// device-side error codes of a record walk (mapped to skv.h codes + reference text on the host)
+enum : uint32_t {
+    DERR_NONE = 0,
+    DERR_EMPTY = 1,        // RunError::EmptyInput                     runs.rs:537-540
+    DERR_VERSION = 2,      // RunError::UnsupportedVersion(v)          runs.rs:553-556
+    DERR_IO = 3,           // RunError::Io (read_u32 past the end)     runs.rs:570-576, :598-604
+    DERR_KEY = 4,          // Format("Incomplete key data")            runs.rs:580-583
+    DERR_UTF8 = 5,         // Format("Invalid UTF-8 in key")           runs.rs:585-591
+    DERR_VAL = 6,          // Format("Incomplete value data")          runs.rs:608-611
+    DERR_MARKER = 7,       // Format("Invalid marker byte: {m}")       runs.rs:621-624
+};
+// err word = code | extra_byte << 8
+
+struct RunInfo {
+    uint64_t ptr;         // absolute device address of the run's first byte (version byte)
+    uint64_t len;         // run length in bytes
+    uint64_t chunk_base;  // first global chunk index of this run
+    uint32_t n_chunks;
+    uint32_t stream;      // stream rank (seq_no descending)
+};
+
+struct RunSummary {       // per run, read back by the host after the parse
+    uint64_t records;     // records decoded before the first error of the run
+    uint32_t err;         // DERR_* | extra << 8 (0 = none)
+    uint32_t pad;
+};
+
+struct TileOut {
+    // level > 0: sorted elements
+    uint64_t* ohi;
+    uint64_t* olo;
+    uint64_t* oc;
+    // level 0: surviving records of the tile, in merged order, at tile_base + rank
+    uint32_t* t_rec;
+    uint32_t* t_meta;
+    uint64_t* tile_kept;
+    uint64_t* tile_bytes;
+    uint64_t* tile_dels;
+    // global scratch for tiles larger than TILE_CAP
+    uint64_t* xhi;
+    uint64_t* xlo;
+    uint64_t* xc;
+    uint32_t* xmeta;
+};
+
+struct DevRunDesc {       // == skv_run_desc layout
+    uint64_t off, len, put_count, delete_count;
+    uint64_t min_key_off, min_key_len, max_key_off, max_key_len;
+    int64_t table_id;
+    uint64_t reserved;
+};
+
+// ------------------------------------------------------------------------------------------
+#ifdef __HIPCC__
+
+__device__ __forceinline__ uint32_t ld_u8(const uint8_t* p) { return *p; }
+
+__device__ __forceinline__ uint32_t ld_be32(const uint8_t* p) {
+    return (ld_u8(p) << 24) | (ld_u8(p + 1) << 16) | (ld_u8(p + 2) << 8) | ld_u8(p + 3);
+}
+
+// core::str::from_utf8 acceptance (runs.rs:585), streaming over global memory.
+__device__ inline bool utf8_valid(const uint8_t* s, uint64_t n) {
+    uint64_t i = 0;
+    while (i < n) {
+        uint32_t c = s[i];
+        if (c < 0x80) { ++i; continue; }
+        uint32_t need, lo = 0x80, hi = 0xBF;
+        if (c >= 0xC2 && c <= 0xDF) need = 1;
+        else if (c == 0xE0) { need = 2; lo = 0xA0; }
+        else if (c >= 0xE1 && c <= 0xEC) need = 2;
+        else if (c == 0xED) { need = 2; hi = 0x9F; }
+        else if (c >= 0xEE && c <= 0xEF) need = 2;
+        else if (c == 0xF0) { need = 3; lo = 0x90; }
+        else if (c >= 0xF1 && c <= 0xF3) need = 3;
+        else if (c == 0xF4) { need = 3; hi = 0x8F; }
+        else return false;
+        if (n - i - 1 < need) return false;
+        uint32_t c1 = s[i + 1];
+        if (c1 < lo || c1 > hi) return false;
+        for (uint32_t k = 2; k <= need; ++k) {
+            uint32_t ck = s[i + k];
+            if (ck < 0x80 || ck > 0xBF) return false;
+        }
+        i += need + 1;
+    }
+    return true;
+}
+
+struct WalkRes {
+    uint64_t end;   // first record start >= stop, or the erroring record's start
+    uint32_t cnt;   // records decoded
+    uint32_t err;   // DERR_* | extra << 8
+};
+
+// runs::read_run_stream's per-record loop (runs.rs:559-626) over [p, stop) of one run, in the
+// reference's check order. max_recs bounds the walk (probe mode).
+__device__ inline WalkRes walk_checked(const uint8_t* run, uint64_t len, uint64_t p, uint64_t stop,
+                                       uint32_t max_recs) {
+    uint32_t cnt = 0;
+    while (p < stop && cnt < max_recs) {
+        uint32_t marker = run[p];
+        if (p + 5 > len) return {p, cnt, DERR_IO};
+        uint64_t klen = ld_be32(run + p + 1);
+        uint64_t kp = p + 5;
+        if (kp + klen > len) return {p, cnt, DERR_KEY};
+        if (!utf8_valid(run + kp, klen)) return {p, cnt, DERR_UTF8};
+        uint64_t size;
+        if (marker == 1) {
+            if (kp + klen + 4 > len) return {p, cnt, DERR_IO};
+            uint64_t vlen = ld_be32(run + kp + klen);
+            if (kp + klen + 4 + vlen > len) return {p, cnt, DERR_VAL};
+            size = 9 + klen + vlen;
+        } else if (marker == 2) {
+            size = 5 + klen;
+        } else {
+            return {p, cnt, DERR_MARKER | (marker << 8)};
+        }
+        ++cnt;
+        p += size;
+    }
+    return {p, cnt, DERR_NONE};
+}
+
+// big-endian 16-byte key prefix (zero padded) of a key of klen bytes at k
+__device__ inline void key_prefix(const uint8_t* k, uint64_t klen, uint64_t& hi, uint64_t& lo) {
+    uint64_t h = 0, l = 0;
+    uint32_t n = klen < 16 ? (uint32_t)klen : 16u;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+        uint64_t b = j < n ? (uint64_t)k[j] : 0ull;
+        if (j < 8) h |= b << (56 - 8 * j);
+        else l |= b << (56 - 8 * (j - 8));
+    }
+    hi = h;
+    lo = l;
+}
+
+// Ordering of two keys given their 16-byte prefixes, lengths and (for keys > 16 B) their bytes:
+// bytewise lexicographic, proper prefix first (Rust str Ord). Returns <0, 0, >0.
+__device__ inline int key_cmp(uint64_t ahi, uint64_t alo, uint32_t alen, const uint8_t* akey,
+                              uint64_t bhi, uint64_t blo, uint32_t blen, const uint8_t* bkey) {
+    if (ahi != bhi) return ahi < bhi ? -1 : 1;
+    if (alo != blo) return alo < blo ? -1 : 1;
+    if (alen > 16 && blen > 16) {
+        uint32_t n = (alen < blen ? alen : blen);
+        for (uint32_t i = 16; i < n; ++i) {
+            uint32_t x = akey[i], y = bkey[i];
+            if (x != y) return x < y ? -1 : 1;
+        }
+    }
+    return alen < blen ? -1 : (alen > blen ? 1 : 0);
+}
+
+// 16 bytes from an arbitrary (unaligned) address using two aligned 16-byte loads. The second
+// aligned block contains p+15, so it holds at least one byte the caller owns and never crosses
+// into an unmapped page.
+__device__ __forceinline__ uint4 load16_unaligned(const uint8_t* p) {
+    uintptr_t a = (uintptr_t)p;
+    const uint4* base = (const uint4*)(a & ~(uintptr_t)15);
+    uint32_t sh = (uint32_t)(a & 15);
+    uint4 x = base[0];
+    if (sh == 0) return x;
+    uint4 y = base[1];
+    uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+    uint32_t q = sh >> 2, r = sh & 3;
+    uint32_t s[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        uint32_t v0 = w[i], v1 = w[i + 1], v2 = w[i + 2], v3 = (i + 3 < 8) ? w[i + 3] : 0u;
+        s[i] = q == 0 ? v0 : (q == 1 ? v1 : (q == 2 ? v2 : v3));
+    }
+    uint4 o;
+    o.x = __builtin_amdgcn_alignbyte(s[1], s[0], r);
+    o.y = __builtin_amdgcn_alignbyte(s[2], s[1], r);
+    o.z = __builtin_amdgcn_alignbyte(s[3], s[2], r);
+    o.w = __builtin_amdgcn_alignbyte(s[4], s[3], r);
+    return o;
+}
+
+#endif  // __HIPCC__
+
+}  // namespace skv

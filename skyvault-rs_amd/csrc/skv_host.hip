@@ -1,0 +1,708 @@
+// skv_host.hip — C ABI (include/skv.h) and host orchestration of the MI355X compaction path.
+//
+// One skv_compact call = the decode -> merge -> [filter] -> build_runs composition of the
+// compaction jobs (table_buffer_compaction.rs:224-279, table_tree_compaction.rs:81-147). The
+// device does all per-record work; the host only sequences kernels, sizes buffers and turns
+// per-run / per-stream summaries into the reference's error (which error surfaces first is a
+// property of k_way::merge's pull order, resolved here from a handful of candidate records).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cinttypes>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/skv.h"
+#include "skv_dev.hpp"
+
+namespace skv {
+void launch_run_header(hipStream_t, const RunInfo*, uint32_t, uint32_t*);
+void launch_spec(hipStream_t, const RunInfo*, uint32_t, uint64_t, const uint32_t*, uint64_t*, uint64_t*, uint32_t*,
+                 uint32_t*);
+void launch_validate(hipStream_t, const RunInfo*, uint32_t, uint64_t, const uint32_t*, const uint64_t*, const uint64_t*,
+                     const uint32_t*, unsigned long long*, uint32_t*);
+void launch_fixup(hipStream_t, const RunInfo*, uint32_t, const uint32_t*, const uint32_t*, const unsigned long long*,
+                  uint64_t*, uint64_t*, uint32_t*, uint32_t*);
+void launch_err_chunk(hipStream_t, const RunInfo*, uint32_t, uint64_t, const uint32_t*, const uint32_t*, uint32_t*);
+void launch_mask(hipStream_t, const RunInfo*, uint32_t, uint64_t, const uint32_t*, const uint32_t*, const uint32_t*,
+                 uint64_t*);
+void launch_run_summary(hipStream_t, const RunInfo*, uint32_t, const uint32_t*, const uint32_t*, const uint32_t*,
+                        const uint64_t*, RunSummary*);
+void launch_emit(hipStream_t, const RunInfo*, uint32_t, uint64_t, const uint64_t*, const uint64_t*, uint64_t*, uint64_t*,
+                 uint64_t*, uint32_t*, uint32_t*, uint32_t*);
+void launch_order_check(hipStream_t, uint64_t, const uint64_t*, uint32_t, const uint64_t*, const uint64_t*,
+                        const uint64_t*, const uint32_t*, unsigned long long*, uint32_t*);
+void launch_sample(hipStream_t, bool, const uint64_t*, const uint64_t*, const uint64_t*, const uint32_t*, const uint64_t*,
+                   const uint64_t*, uint32_t, uint64_t, uint64_t, uint64_t*, uint64_t*, uint64_t*);
+void launch_bounds(hipStream_t, bool, const uint64_t*, const uint64_t*, const uint64_t*, const uint32_t*,
+                   const uint64_t*, uint32_t, const uint64_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t,
+                   const uint64_t*, uint64_t*);
+void launch_tile_n(hipStream_t, const uint64_t*, uint32_t, uint64_t, uint64_t*);
+
+hipError_t launch_tile(hipStream_t, bool, const uint64_t*, const uint64_t*, const uint64_t*, const uint32_t*,
+                       const uint64_t*, uint32_t, uint64_t, const uint64_t*, const uint32_t*, const uint64_t*, uint32_t,
+                       TileOut);
+void launch_finalize(hipStream_t, uint64_t, const uint64_t*, const uint64_t*, const uint64_t*, const uint64_t*,
+                     const uint64_t*, const uint32_t*, const uint32_t*, const uint64_t*, uint32_t*, uint64_t*, uint64_t*,
+                     uint64_t*, uint32_t*);
+void launch_chain(hipStream_t, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
+void launch_run_stats(hipStream_t, const uint64_t*, const uint64_t*, const uint64_t*, const uint64_t*, const uint32_t*,
+                      const uint32_t*, DevRunDesc*, uint64_t);
+void launch_gather(hipStream_t, const uint64_t*, const uint64_t*, const uint64_t*, const uint64_t*, const uint64_t*,
+                   uint8_t*, uint64_t);
+uint64_t scan_tmp_words(uint64_t);
+void launch_scan(hipStream_t, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
+}  // namespace skv
+
+using namespace skv;
+
+// ------------------------------------------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+enum Phase { PH_START = 0, PH_PARSE, PH_CHECK, PH_MERGE, PH_CHAIN, PH_GATHER, PH_N };
+
+struct skv_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    bool profiling = false;
+    skv_timings timings{};
+    std::map<std::string, DevBuf> bufs;
+    hipEvent_t ev[PH_N] = {};
+    void* pinned = nullptr;  // small readback staging
+    size_t pinned_cap = 0;
+    uint64_t syncs = 0;
+};
+
+struct ResultBox {  // skv_result + how to free it
+    skv_result pub;
+    int host_bytes;  // 1: bytes malloc'd by us
+};
+
+static int set_err(skv_ctx* ctx, int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    return code;
+}
+
+#define HIPCHK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess)                                                                       \
+            throw DevError(std::string(#x) + ": " + hipGetErrorString(e_));                         \
+    } while (0)
+
+struct DevError {
+    std::string msg;
+    explicit DevError(std::string m) : msg(std::move(m)) {}
+};
+struct ApiError {
+    int code;
+    std::string msg;
+};
+
+template <typename T>
+static T* dbuf(skv_ctx* ctx, const char* name, size_t count) {
+    size_t bytes = count * sizeof(T);
+    if (bytes == 0) bytes = 16;
+    bytes = (bytes + 255) & ~(size_t)255;
+    DevBuf& b = ctx->bufs[name];
+    if (b.cap < bytes) {
+        if (b.p) HIPCHK(hipFree(b.p));
+        b.p = nullptr;
+        b.cap = 0;
+        size_t cap = bytes + bytes / 8;
+        HIPCHK(hipMalloc(&b.p, cap));
+        b.cap = cap;
+    }
+    return (T*)b.p;
+}
+
+static void* pinned(skv_ctx* ctx, size_t bytes) {
+    if (ctx->pinned_cap < bytes) {
+        if (ctx->pinned) HIPCHK(hipHostFree(ctx->pinned));
+        ctx->pinned = nullptr;
+        size_t cap = std::max<size_t>(bytes, 1 << 16);
+        HIPCHK(hipHostMalloc(&ctx->pinned, cap, hipHostMallocDefault));
+        ctx->pinned_cap = cap;
+    }
+    return ctx->pinned;
+}
+
+static void d2h(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!bytes) return;
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+}
+static void h2d(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!bytes) return;
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+}
+static void sync(skv_ctx* ctx) {
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->syncs++;
+}
+static void mark(skv_ctx* ctx, Phase p) {
+    if (ctx->profiling) HIPCHK(hipEventRecord(ctx->ev[p], ctx->stream));
+}
+
+// reference Display text of a device error word (runs.rs:83-95, :537-624)
+static int derr_to_api(uint32_t e, std::string& msg) {
+    uint32_t code = e & 0xFF, extra = e >> 8;
+    char buf[128];
+    switch (code) {
+        case DERR_EMPTY: msg = "Input list of operations cannot be empty"; return SKV_E_EMPTY_INPUT;
+        case DERR_VERSION: snprintf(buf, sizeof buf, "Unsupported run version: %u", extra); msg = buf; return SKV_E_UNSUPPORTED_VERSION;
+        case DERR_IO: msg = "I/O error: failed to fill whole buffer"; return SKV_E_IO;
+        case DERR_KEY: msg = "Data format error: Incomplete key data"; return SKV_E_FORMAT;
+        case DERR_UTF8: msg = "Data format error: Invalid UTF-8 in key"; return SKV_E_FORMAT;
+        case DERR_VAL: msg = "Data format error: Incomplete value data"; return SKV_E_FORMAT;
+        case DERR_MARKER: snprintf(buf, sizeof buf, "Data format error: Invalid marker byte: %u", extra); msg = buf; return SKV_E_FORMAT;
+        default: snprintf(buf, sizeof buf, "internal: unknown device error %u", e); msg = buf; return SKV_E_DEVICE;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+struct InStream {
+    int64_t seq;
+    uint32_t vec_idx;  // position in the caller's vector (merge pulls first items in this order)
+    std::vector<uint64_t> ptrs, lens;
+};
+
+struct Job {
+    std::vector<InStream> ranked;  // streams sorted by seq_no descending
+    uint64_t max_run_size = 0;
+    uint32_t flags = 0;
+    uint64_t in_bytes = 0;
+};
+
+// a record's key bytes (host copy) for error-trigger comparisons
+static std::string fetch_key(skv_ctx* ctx, const uint64_t* d_rec_addr, const uint32_t* d_rec_klen, uint64_t rec) {
+    uint64_t addr = 0;
+    uint32_t klen = 0;
+    HIPCHK(hipMemcpy(&addr, d_rec_addr + rec, 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&klen, d_rec_klen + rec, 4, hipMemcpyDeviceToHost));
+    std::string k(klen, '\0');
+    if (klen) HIPCHK(hipMemcpy(&k[0], (const void*)(addr + 5), klen, hipMemcpyDeviceToHost));
+    return k;
+}
+
+static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
+    hipStream_t st = ctx->stream;
+    ctx->syncs = 0;
+    mark(ctx, PH_START);
+    const uint32_t k = (uint32_t)job.ranked.size();
+    // ---- run table ------------------------------------------------------------------------
+    std::vector<RunInfo> runs;
+    std::vector<uint32_t> stream_first_run(k + 1, 0);
+    uint64_t n_chunks = 0;
+    for (uint32_t s = 0; s < k; ++s) {
+        stream_first_run[s] = (uint32_t)runs.size();
+        const InStream& S = job.ranked[s];
+        for (size_t m = 0; m < S.ptrs.size(); ++m) {
+            RunInfo R;
+            R.ptr = S.ptrs[m];
+            R.len = S.lens[m];
+            R.chunk_base = n_chunks;
+            R.n_chunks = R.len >= 2 ? (uint32_t)((R.len - 1 + CHUNK - 1) / CHUNK) : 0;
+            R.stream = s;
+            n_chunks += R.n_chunks;
+            runs.push_back(R);
+        }
+    }
+    stream_first_run[k] = (uint32_t)runs.size();
+    const uint32_t n_runs = (uint32_t)runs.size();
+
+    RunInfo* d_runs = dbuf<RunInfo>(ctx, "runs", n_runs);
+    uint32_t* d_hdr = dbuf<uint32_t>(ctx, "hdr_err", n_runs);
+    uint64_t* ch_start = dbuf<uint64_t>(ctx, "ch_start", n_chunks);
+    uint64_t* ch_end = dbuf<uint64_t>(ctx, "ch_end", n_chunks);
+    uint32_t* ch_cnt = dbuf<uint32_t>(ctx, "ch_cnt", n_chunks);
+    uint32_t* ch_err = dbuf<uint32_t>(ctx, "ch_err", n_chunks);
+    unsigned long long* bad_bits = dbuf<unsigned long long>(ctx, "bad_bits", n_chunks / 64 + 1);
+    uint32_t* first_bad = dbuf<uint32_t>(ctx, "first_bad", n_runs);
+    uint32_t* err_chunk = dbuf<uint32_t>(ctx, "err_chunk", n_runs);
+    uint64_t* cnt64 = dbuf<uint64_t>(ctx, "cnt64", n_chunks);
+    uint64_t* ch_rec_base = dbuf<uint64_t>(ctx, "ch_rec_base", n_chunks + 1);
+    uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "scan_tmp", scan_tmp_words(std::max<uint64_t>(n_chunks, 1 << 20)) + 64);
+    RunSummary* d_sum = dbuf<RunSummary>(ctx, "run_sum", n_runs);
+
+    h2d(ctx, d_runs, runs.data(), n_runs * sizeof(RunInfo));
+    HIPCHK(hipMemsetAsync(bad_bits, 0, (n_chunks / 64 + 1) * 8, st));
+    HIPCHK(hipMemsetAsync(first_bad, 0xFF, n_runs * 4, st));
+    HIPCHK(hipMemsetAsync(err_chunk, 0xFF, n_runs * 4, st));
+    launch_run_header(st, d_runs, n_runs, d_hdr);
+    launch_spec(st, d_runs, n_runs, n_chunks, d_hdr, ch_start, ch_end, ch_cnt, ch_err);
+    launch_validate(st, d_runs, n_runs, n_chunks, d_hdr, ch_start, ch_end, ch_err, bad_bits, first_bad);
+    launch_fixup(st, d_runs, n_runs, d_hdr, first_bad, bad_bits, ch_start, ch_end, ch_cnt, ch_err);
+    launch_err_chunk(st, d_runs, n_runs, n_chunks, d_hdr, ch_err, err_chunk);
+    launch_mask(st, d_runs, n_runs, n_chunks, d_hdr, err_chunk, ch_cnt, cnt64);
+    launch_scan(st, cnt64, n_chunks, ch_rec_base, scan_tmp);
+    launch_run_summary(st, d_runs, n_runs, d_hdr, err_chunk, ch_err, ch_rec_base, d_sum);
+    HIPCHK(hipGetLastError());
+
+    std::vector<RunSummary> sum(n_runs);
+    uint64_t R = 0;
+    {
+        RunSummary* hs = (RunSummary*)pinned(ctx, n_runs * sizeof(RunSummary) + 16);
+        d2h(ctx, hs, d_sum, n_runs * sizeof(RunSummary));
+        d2h(ctx, (uint8_t*)hs + n_runs * sizeof(RunSummary), ch_rec_base + n_chunks, 8);
+        sync(ctx);
+        memcpy(sum.data(), hs, n_runs * sizeof(RunSummary));
+        memcpy(&R, (uint8_t*)hs + n_runs * sizeof(RunSummary), 8);
+    }
+    // per stream (rank order): valid record count n_s and the first error
+    std::vector<uint64_t> stream_base(k + 1, 0), stream_valid(k, 0);
+    std::vector<uint32_t> stream_err(k, 0);
+    bool any_err = false;
+    {
+        uint64_t acc = 0;
+        for (uint32_t s = 0; s < k; ++s) {
+            stream_base[s] = acc;
+            uint64_t valid = 0;
+            bool dead = false;
+            for (uint32_t r = stream_first_run[s]; r < stream_first_run[s + 1]; ++r) {
+                acc += sum[r].records;
+                if (!dead) {
+                    valid += sum[r].records;
+                    if (sum[r].err) {
+                        stream_err[s] = sum[r].err;
+                        dead = true;
+                        any_err = true;
+                    }
+                }
+            }
+            stream_valid[s] = valid;
+        }
+        stream_base[k] = acc;
+        if (acc != R) throw DevError("internal: record count mismatch");
+    }
+    // ---- record arrays ---------------------------------------------------------------------
+    uint64_t* rec_addr = dbuf<uint64_t>(ctx, "rec_addr", R);
+    uint64_t* rec_hi = dbuf<uint64_t>(ctx, "rec_hi", R);
+    uint64_t* rec_lo = dbuf<uint64_t>(ctx, "rec_lo", R);
+    uint32_t* rec_klen = dbuf<uint32_t>(ctx, "rec_klen", R);
+    uint32_t* rec_meta = dbuf<uint32_t>(ctx, "rec_meta", R);
+    uint32_t* d_flags = dbuf<uint32_t>(ctx, "flags", 4);
+    uint64_t* d_stream_base = dbuf<uint64_t>(ctx, "stream_base", k + 1);
+    unsigned long long* d_first_dec = dbuf<unsigned long long>(ctx, "first_dec", k);
+    HIPCHK(hipMemsetAsync(d_flags, 0, 16, st));
+    HIPCHK(hipMemsetAsync(d_first_dec, 0xFF, (size_t)k * 8, st));
+    h2d(ctx, d_stream_base, stream_base.data(), (k + 1) * 8);
+    launch_emit(st, d_runs, n_runs, n_chunks, ch_start, ch_rec_base, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
+                d_flags);
+    mark(ctx, PH_PARSE);
+    launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
+    HIPCHK(hipGetLastError());
+    std::vector<uint64_t> first_dec(k);
+    uint32_t hflags[4];
+    {
+        uint8_t* hp = (uint8_t*)pinned(ctx, k * 8 + 16);
+        d2h(ctx, hp, d_first_dec, (size_t)k * 8);
+        d2h(ctx, hp + (size_t)k * 8, d_flags, 16);
+        sync(ctx);
+        memcpy(first_dec.data(), hp, (size_t)k * 8);
+        memcpy(hflags, hp + (size_t)k * 8, 16);
+    }
+    mark(ctx, PH_CHECK);
+    bool any_dec = false;
+    for (uint32_t s = 0; s < k; ++s)
+        if (first_dec[s] != ~0ull && first_dec[s] + 1 < stream_valid[s]) any_dec = true;
+
+    // ---- errors: which one k_way::merge surfaces first --------------------------------------
+    if (any_err || any_dec) {
+        // (1) first items are pulled in the caller's vector order (k_way.rs:126-140)
+        std::vector<uint32_t> by_vec(k);
+        for (uint32_t s = 0; s < k; ++s) by_vec[job.ranked[s].vec_idx] = s;
+        for (uint32_t v = 0; v < k; ++v) {
+            uint32_t s = by_vec[v];
+            if (stream_valid[s] == 0 && stream_err[s]) {
+                std::string msg;
+                int code = derr_to_api(stream_err[s], msg);
+                throw ApiError{code, msg};
+            }
+        }
+        // (2) each stream's earliest trigger item; the one popped first wins
+        struct Cand { uint32_t s; uint64_t idx; bool order; std::string key; };
+        std::vector<Cand> cands;
+        bool any_order = false;
+        for (uint32_t s = 0; s < k; ++s) {
+            uint64_t trig = ~0ull;
+            bool order = false;
+            if (first_dec[s] != ~0ull && first_dec[s] + 1 < stream_valid[s]) { trig = first_dec[s]; order = true; }
+            if (stream_err[s] && stream_valid[s] > 0) {
+                uint64_t t2 = stream_valid[s] - 1;
+                if (t2 < trig) { trig = t2; order = false; }
+            }
+            if (trig == ~0ull) continue;
+            any_order |= order;
+            cands.push_back({s, trig, order, fetch_key(ctx, rec_addr, rec_klen, stream_base[s] + trig)});
+        }
+        if (cands.empty()) throw DevError("internal: error without trigger");
+        // pop order: key ascending, then seq_no descending (== smaller rank)
+        std::sort(cands.begin(), cands.end(), [](const Cand& a, const Cand& b) {
+            if (a.key != b.key) return a.key < b.key;
+            return a.s < b.s;
+        });
+        const Cand& w = cands[0];
+        if (any_order && (job.flags & SKV_DROP_TOMBSTONES))
+            throw ApiError{SKV_E_UNSUPPORTED,
+                           "unsorted input stream with SKV_DROP_TOMBSTONES: the reference's outcome depends on the "
+                           "Delete filter's interleaving; not resolved on device in this build"};
+        if (w.order) throw ApiError{SKV_E_FORMAT, "Data format error: Operations must be sorted by key"};
+        std::string msg;
+        int code = derr_to_api(stream_err[w.s], msg);
+        throw ApiError{code, msg};
+    }
+    if (hflags[0]) throw ApiError{SKV_E_UNSUPPORTED, "record of 2 GiB or more: unsupported by this build"};
+    if (R >= 0xFFFFFFFFull) throw ApiError{SKV_E_UNSUPPORTED, "more than 2^32-1 records in one compaction"};
+
+    // ---- merge ------------------------------------------------------------------------------
+    struct Level {
+        uint64_t N = 0, S = 1;
+        std::vector<uint64_t> off;  // k+1 list offsets
+        uint64_t* hi = nullptr;
+        uint64_t* lo = nullptr;
+        uint64_t* c = nullptr;       // level > 0
+        uint64_t* d_off = nullptr;
+        // sorted output (level > 0)
+        uint64_t* shi = nullptr;
+        uint64_t* slo = nullptr;
+        uint64_t* sc = nullptr;
+    };
+    std::vector<Level> lv(1);
+    lv[0].N = R;
+    lv[0].off = stream_base;
+    lv[0].hi = rec_hi;
+    lv[0].lo = rec_lo;
+    lv[0].d_off = d_stream_base;
+    const uint64_t S_step = std::max<uint64_t>(2, (uint64_t)TILE_TARGET / std::max<uint32_t>(k, 1));
+    if (k > (uint32_t)TILE_TARGET / 2 && R > (uint64_t)TILE_CAP)
+        throw ApiError{SKV_E_UNSUPPORTED, "merge fan-in above 1024 streams is not supported by this build yet"};
+    while (lv.back().N > (uint64_t)TILE_CAP) {
+        const Level& P = lv.back();
+        Level L;
+        L.S = S_step;
+        L.off.resize(k + 1);
+        uint64_t acc = 0;
+        for (uint32_t j = 0; j < k; ++j) {
+            L.off[j] = acc;
+            uint64_t nj = P.off[j + 1] - P.off[j];
+            acc += (nj + L.S - 1) / L.S;
+        }
+        L.off[k] = acc;
+        L.N = acc;
+        char nm[64];
+        int li = (int)lv.size();
+        snprintf(nm, sizeof nm, "lv%d_hi", li); L.hi = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "lv%d_lo", li); L.lo = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "lv%d_c", li); L.c = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "lv%d_off", li); L.d_off = dbuf<uint64_t>(ctx, nm, k + 1);
+        h2d(ctx, L.d_off, L.off.data(), (k + 1) * 8);
+        launch_sample(st, li == 1, P.hi, P.lo, P.c, rec_klen, P.d_off, L.d_off, k, L.S, L.N, L.hi, L.lo, L.c);
+        lv.push_back(L);
+    }
+    // top-down: sort each sample level, derive splitters for the level below
+    uint64_t T0 = 1;
+    uint64_t* d_tile_base0 = nullptr;
+    TileOut O0{};
+    for (int li = (int)lv.size() - 1; li >= 0; --li) {
+        Level& L = lv[li];
+        const bool l0 = li == 0;
+        uint64_t T = 1, m = 1;
+        if (li + 1 < (int)lv.size()) {
+            m = std::max<uint64_t>(1, (uint64_t)TILE_TARGET / lv[li + 1].S);
+            T = std::max<uint64_t>(1, (lv[li + 1].N + m - 1) / m);
+        }
+        char nm[64];
+        snprintf(nm, sizeof nm, "bounds%d", li);
+        uint64_t* bounds = dbuf<uint64_t>(ctx, nm, (T + 1) * k);
+        const Level* U = li + 1 < (int)lv.size() ? &lv[li + 1] : nullptr;
+        launch_bounds(st, l0, L.hi, L.lo, L.c, rec_klen, L.d_off, k, U ? U->shi : nullptr, U ? U->slo : nullptr,
+                      U ? U->sc : nullptr, m, T, rec_addr, bounds);
+        snprintf(nm, sizeof nm, "tile_n%d", li);
+        uint64_t* tile_n = dbuf<uint64_t>(ctx, nm, T);
+        snprintf(nm, sizeof nm, "tile_base%d", li);
+        uint64_t* tile_base = dbuf<uint64_t>(ctx, nm, T + 1);
+        launch_tile_n(st, bounds, k, T, tile_n);
+        launch_scan(st, tile_n, T, tile_base, scan_tmp);
+        TileOut O{};
+        snprintf(nm, sizeof nm, "x%d_hi", li); O.xhi = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "x%d_lo", li); O.xlo = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "x%d_c", li); O.xc = dbuf<uint64_t>(ctx, nm, L.N);
+        if (l0) {
+            O.xmeta = dbuf<uint32_t>(ctx, "x0_meta", L.N);
+            O.t_rec = dbuf<uint32_t>(ctx, "t_rec", L.N);
+            O.t_meta = dbuf<uint32_t>(ctx, "t_meta", L.N);
+            O.tile_kept = dbuf<uint64_t>(ctx, "tile_kept", T);
+            O.tile_bytes = dbuf<uint64_t>(ctx, "tile_bytes", T);
+            O.tile_dels = dbuf<uint64_t>(ctx, "tile_dels", T);
+        } else {
+            snprintf(nm, sizeof nm, "s%d_hi", li); L.shi = O.ohi = dbuf<uint64_t>(ctx, nm, L.N);
+            snprintf(nm, sizeof nm, "s%d_lo", li); L.slo = O.olo = dbuf<uint64_t>(ctx, nm, L.N);
+            snprintf(nm, sizeof nm, "s%d_c", li); L.sc = O.oc = dbuf<uint64_t>(ctx, nm, L.N);
+        }
+        HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, rec_klen, bounds, k, T, tile_base, rec_meta, rec_addr,
+                           (job.flags & SKV_DROP_TOMBSTONES) ? 1u : 0u, O));
+        if (l0) {
+            T0 = T;
+            d_tile_base0 = tile_base;
+            O0 = O;
+        }
+    }
+    // dense merged arrays
+    uint64_t* kept_base = dbuf<uint64_t>(ctx, "kept_base", T0 + 1);
+    uint64_t* byte_base = dbuf<uint64_t>(ctx, "byte_base", T0 + 1);
+    uint64_t* del_base = dbuf<uint64_t>(ctx, "del_base", T0 + 1);
+    launch_scan(st, O0.tile_kept, T0, kept_base, scan_tmp);
+    launch_scan(st, O0.tile_bytes, T0, byte_base, scan_tmp);
+    launch_scan(st, O0.tile_dels, T0, del_base, scan_tmp);
+    uint32_t* m_rec = dbuf<uint32_t>(ctx, "m_rec", R + 1);
+    uint64_t* m_src = dbuf<uint64_t>(ctx, "m_src", R + 1);
+    uint64_t* m_P = dbuf<uint64_t>(ctx, "m_P", R + 1);
+    uint64_t* m_Dp = dbuf<uint64_t>(ctx, "m_Dp", R + 1);
+    uint32_t* max_rec = d_flags + 2;
+    if (R == 0) {
+        HIPCHK(hipMemsetAsync(m_P, 0, 8, st));
+        HIPCHK(hipMemsetAsync(m_Dp, 0, 8, st));
+    }
+    launch_finalize(st, T0, d_tile_base0, O0.tile_kept, kept_base, byte_base, del_base, O0.t_rec, O0.t_meta, rec_addr,
+                    m_rec, m_src, m_P, m_Dp, max_rec);
+    HIPCHK(hipGetLastError());
+    mark(ctx, PH_MERGE);
+    // ---- chain + stats ----------------------------------------------------------------------
+    const uint64_t* d_K = kept_base + T0;
+    uint64_t* run_b = dbuf<uint64_t>(ctx, "run_b", R + 2);
+    uint64_t* d_nruns = dbuf<uint64_t>(ctx, "n_runs", 2);
+    DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", R + 1);
+    launch_chain(st, d_K, m_P, job.max_run_size, run_b, d_nruns);
+    launch_run_stats(st, d_nruns, run_b, m_P, m_Dp, m_rec, rec_klen, d_desc, R);
+    mark(ctx, PH_CHAIN);
+    // ---- gather -----------------------------------------------------------------------------
+    uint64_t total_rec_bytes = 0;
+    for (const InStream& S : job.ranked)
+        for (uint64_t l : S.lens) total_rec_bytes += l;
+    uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + R + 16);
+    launch_gather(st, d_K, d_nruns, run_b, m_P, m_src, d_out, R);
+    HIPCHK(hipGetLastError());
+    mark(ctx, PH_GATHER);
+    // ---- readback ---------------------------------------------------------------------------
+    uint64_t h3[4];
+    {
+        uint64_t* hp = (uint64_t*)pinned(ctx, 64);
+        d2h(ctx, hp, d_nruns, 8);
+        d2h(ctx, hp + 1, d_K, 8);
+        sync(ctx);
+        memcpy(h3, hp, 16);
+    }
+    const uint64_t n_out_runs = h3[0], K = h3[1];
+    uint64_t kept_bytes = 0;
+    HIPCHK(hipMemcpy(&kept_bytes, m_P + K, 8, hipMemcpyDeviceToHost));
+    ResultBox* box = (ResultBox*)calloc(1, sizeof(ResultBox));
+    skv_result* res = &box->pub;
+    res->runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, n_out_runs) * sizeof(skv_run_desc));
+    static_assert(sizeof(skv_run_desc) == sizeof(DevRunDesc), "desc layout");
+    if (n_out_runs) HIPCHK(hipMemcpy(res->runs, d_desc, n_out_runs * sizeof(DevRunDesc), hipMemcpyDeviceToHost));
+    res->n_runs = n_out_runs;
+    res->bytes = d_out;
+    res->n_bytes = kept_bytes + n_out_runs;
+    res->in_bytes = job.in_bytes;
+    res->in_records = R;
+    res->out_records = K;
+    res->dropped_tables = 0;
+    box->host_bytes = 0;
+    if (ctx->profiling) {
+        HIPCHK(hipEventSynchronize(ctx->ev[PH_GATHER]));
+        float ms[PH_N] = {};
+        for (int p = PH_PARSE; p < PH_N; ++p) HIPCHK(hipEventElapsedTime(&ms[p], ctx->ev[p - 1], ctx->ev[p]));
+        float tot = 0;
+        HIPCHK(hipEventElapsedTime(&tot, ctx->ev[PH_START], ctx->ev[PH_GATHER]));
+        skv_timings& t = ctx->timings;
+        t.total_ms = tot;
+        t.parse_ms = ms[PH_PARSE];
+        t.check_ms = ms[PH_CHECK];
+        t.merge_ms = ms[PH_MERGE];
+        t.chain_ms = ms[PH_CHAIN];
+        t.gather_ms = ms[PH_GATHER];
+        t.gather_read_bytes = kept_bytes;
+        t.gather_write_bytes = kept_bytes + n_out_runs;
+    }
+    ctx->timings.host_syncs = ctx->syncs;
+    *out = res;
+    return SKV_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+static int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t max_run_size, uint32_t flags,
+                     Job& job) {
+    if (n && !streams) return set_err(ctx, SKV_E_INVALID_ARG, "streams is NULL");
+    if (flags & ~(uint32_t)(SKV_DROP_TOMBSTONES | SKV_SPLIT_BY_TABLE))
+        return set_err(ctx, SKV_E_INVALID_ARG, "unknown flags 0x%x", flags);
+    if ((flags & SKV_SPLIT_BY_TABLE) && (flags & SKV_DROP_TOMBSTONES))
+        return set_err(ctx, SKV_E_INVALID_ARG, "SKV_SPLIT_BY_TABLE and SKV_DROP_TOMBSTONES are exclusive");
+    job.max_run_size = max_run_size;
+    job.flags = flags;
+    for (uint32_t i = 0; i < n; ++i) {
+        const skv_stream& s = streams[i];
+        if (s.n_runs && (!s.runs || !s.run_lens))
+            return set_err(ctx, SKV_E_INVALID_ARG, "stream %u: runs/run_lens is NULL", i);
+        InStream S;
+        S.seq = s.seq_no;
+        S.vec_idx = i;
+        for (uint32_t r = 0; r < s.n_runs; ++r) {
+            if (s.run_lens[r] && !s.runs[r]) return set_err(ctx, SKV_E_INVALID_ARG, "stream %u run %u: NULL data", i, r);
+            S.ptrs.push_back((uint64_t)(uintptr_t)s.runs[r]);
+            S.lens.push_back(s.run_lens[r]);
+            job.in_bytes += s.run_lens[r];
+        }
+        job.ranked.push_back(std::move(S));
+    }
+    std::stable_sort(job.ranked.begin(), job.ranked.end(), [](const InStream& a, const InStream& b) { return a.seq > b.seq; });
+    for (size_t i = 1; i < job.ranked.size(); ++i)
+        if (job.ranked[i].seq == job.ranked[i - 1].seq)
+            return set_err(ctx, SKV_E_INVALID_ARG, "duplicate seq_no %" PRId64, job.ranked[i].seq);
+    if (flags & SKV_SPLIT_BY_TABLE)
+        return set_err(ctx, SKV_E_UNSUPPORTED, "SKV_SPLIT_BY_TABLE (WAL compaction) is not on the device path in this build");
+    return SKV_OK;
+}
+
+static int run_guarded(skv_ctx* ctx, const Job& job, skv_result** out) {
+    try {
+        return compact_device(ctx, job, out);
+    } catch (const ApiError& e) {
+        (void)hipStreamSynchronize(ctx->stream);
+        return set_err(ctx, e.code, "%s", e.msg.c_str());
+    } catch (const DevError& e) {
+        (void)hipStreamSynchronize(ctx->stream);
+        return set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());
+    }
+}
+
+extern "C" {
+
+int skv_abi_version(void) { return SKV_ABI_VERSION; }
+
+int skv_device_count(int* out) {
+    if (!out) return SKV_E_INVALID_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *out = n;
+    return SKV_OK;
+}
+
+int skv_ctx_create(int device, skv_ctx** out) {
+    if (!out) return SKV_E_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return SKV_E_DEVICE;
+    if (device < 0 || device >= n) return SKV_E_INVALID_ARG;
+    skv_ctx* ctx = new skv_ctx();
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return SKV_E_DEVICE;
+    }
+    for (int i = 0; i < PH_N; ++i) (void)hipEventCreate(&ctx->ev[i]);
+    *out = ctx;
+    return SKV_OK;
+}
+
+void skv_ctx_destroy(skv_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->bufs)
+        if (kv.second.p) (void)hipFree(kv.second.p);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    for (int i = 0; i < PH_N; ++i)
+        if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* skv_last_error(const skv_ctx* ctx) { return ctx ? ctx->err.c_str() : "ctx is NULL"; }
+
+int skv_ctx_set_profiling(skv_ctx* ctx, int enable) {
+    if (!ctx) return SKV_E_INVALID_ARG;
+    ctx->profiling = enable != 0;
+    return SKV_OK;
+}
+
+int skv_ctx_get_timings(const skv_ctx* ctx, skv_timings* out) {
+    if (!ctx || !out) return SKV_E_INVALID_ARG;
+    *out = ctx->timings;
+    return SKV_OK;
+}
+
+int skv_compact_dev(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uint64_t max_run_size, uint32_t flags,
+                    skv_result** out) {
+    if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
+    *out = nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    Job job;
+    int rc = build_job(ctx, streams, n_streams, max_run_size, flags, job);
+    if (rc) return rc;
+    return run_guarded(ctx, job, out);
+}
+
+int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uint64_t max_run_size, uint32_t flags,
+                skv_result** out) {
+    if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
+    *out = nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    Job job;
+    int rc = build_job(ctx, streams, n_streams, max_run_size, flags, job);
+    if (rc) return rc;
+    try {
+        // stage inputs into HBM (16-byte aligned per run)
+        uint64_t total = 0;
+        for (const InStream& S : job.ranked)
+            for (uint64_t l : S.lens) total += (l + 15) & ~15ull;
+        uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", total + 16);
+        uint64_t off = 0;
+        for (InStream& S : job.ranked) {
+            for (size_t m = 0; m < S.ptrs.size(); ++m) {
+                if (S.lens[m]) h2d(ctx, d_in + off, (const void*)S.ptrs[m], S.lens[m]);
+                S.ptrs[m] = (uint64_t)(uintptr_t)(d_in + off);
+                off += (S.lens[m] + 15) & ~15ull;
+            }
+        }
+    } catch (const DevError& e) {
+        return set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());
+    }
+    skv_result* dres = nullptr;
+    rc = run_guarded(ctx, job, &dres);
+    if (rc) return rc;
+    ResultBox* box = (ResultBox*)dres;
+    uint8_t* hb = (uint8_t*)malloc(std::max<uint64_t>(1, dres->n_bytes));
+    if (dres->n_bytes && hipMemcpy(hb, dres->bytes, dres->n_bytes, hipMemcpyDeviceToHost) != hipSuccess) {
+        free(hb);
+        skv_result_free(dres);
+        return set_err(ctx, SKV_E_DEVICE, "device-to-host copy of the output failed");
+    }
+    dres->bytes = hb;
+    box->host_bytes = 1;
+    *out = dres;
+    return SKV_OK;
+}
+
+void skv_result_free(skv_result* r) {
+    if (!r) return;
+    ResultBox* box = (ResultBox*)r;
+    if (box->host_bytes) free(r->bytes);
+    free(r->runs);
+    free(box);
+}
+
+}  // extern "C"

@@ -1,0 +1,1130 @@
+// skv_kernels.hip — HIP/CDNA4 (gfx950) kernels of the skyvault compaction path.
+//
+// Pipeline (one compaction; host orchestration in skv_host.hip):
+//   parse   k_run_header, k_spec, k_validate, k_fixup, k_err_chunk, k_mask, scan, k_run_summary,
+//           k_emit           — runs::read_run_stream (runs.rs:517-628) for every input run at once
+//   check   k_order_check    — first in-stream key decrease (what build_runs rejects, runs.rs:190-198)
+//   merge   k_sample, k_bounds, k_tile_n, k_tile<L0>, k_finalize
+//                            — k_way::merge (k_way.rs:113-179): order by (key asc, seq_no desc),
+//                              keep the first record per key, drop Deletes at Level::max
+//                              (table_tree_compaction.rs:139-145)
+//   chain   k_chain, k_run_stats — build_runs' greedy size split + StatsV1 (runs.rs:202-280)
+//   gather  k_gather         — output bytes: version byte per run + surviving records verbatim
+//
+// Everything is integer/byte work: no MFMA. The HBM-bound kernel is k_gather (reads the
+// surviving input records once, writes the output once, 16-byte vector stores).
+#include "skv_dev.hpp"
+
+namespace skv {
+
+// ---------------------------------------------------------------------------------------
+// small helpers
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+
+// exclusive scan across the block (blockDim multiple of 64, <= 1024); ws: >= 16 T of LDS
+template <typename T>
+__device__ T block_excl_scan(T v, T* ws, T& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    T inc = wave_incl_scan(v);
+    if (lane == 63) ws[wid] = inc;
+    __syncthreads();
+    if (wid == 0) {
+        T w = lane < nw ? ws[lane] : (T)0;
+        w = wave_incl_scan(w);
+        if (lane < nw) ws[lane] = w;
+    }
+    __syncthreads();
+    T off = wid ? ws[wid - 1] : (T)0;
+    total = ws[nw - 1];
+    __syncthreads();
+    return off + inc - v;
+}
+
+template <typename T>
+__device__ T block_reduce_sum(T v, T* ws) {
+    T total;
+    block_excl_scan(v, ws, total);
+    return total;
+}
+
+// last index i in [0, n) with a[i] <= x (a sorted ascending, a[0] <= x assumed)
+template <typename T>
+__device__ __forceinline__ uint32_t upper_idx(const T* a, uint32_t n, T x) {
+    uint32_t lo = 0, hi = n;  // answer in [lo, hi)
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] <= x) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint32_t find_run(const RunInfo* runs, uint32_t n_runs, uint64_t c) {
+    uint32_t lo = 0, hi = n_runs;
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (runs[mid].chunk_base <= c) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// ---------------------------------------------------------------------------------------
+// parse: run headers (runs.rs:537-556)
+
+__global__ void k_run_header(const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_runs) return;
+    RunInfo R = runs[r];
+    uint32_t e = 0;
+    if (R.len == 0) e = DERR_EMPTY;
+    else {
+        uint32_t v = ((const uint8_t*)R.ptr)[0];
+        if (v != 1) e = DERR_VERSION | (v << 8);
+    }
+    hdr_err[r] = e;
+}
+
+// Speculative start of chunk `local` (> 0): a record start must lie in [cs, ce). Try the
+// position a fixed record stride predicts, then scan for the first position whose next three
+// records decode cleanly. Wrong guesses are caught by k_validate and repaired by k_fixup.
+__device__ uint64_t spec_start(const uint8_t* run, uint64_t len, uint64_t cs, uint64_t ce) {
+    WalkRes f = walk_checked(run, len, 1, len, 1);
+    if (f.err == DERR_NONE && f.cnt == 1) {
+        uint64_t S = f.end - 1;
+        uint64_t p0 = 1 + ((cs - 1 + S - 1) / S) * S;
+        if (p0 < ce) {
+            uint32_t m = run[p0];
+            if (m == 1 || m == 2) {
+                WalkRes w = walk_checked(run, len, p0, len, 3);
+                if (w.err == DERR_NONE) return p0;
+            }
+        }
+    }
+    for (uint64_t p = cs; p < ce; ++p) {
+        uint32_t m = run[p];
+        if (m != 1 && m != 2) continue;
+        WalkRes w = walk_checked(run, len, p, len, 3);
+        if (w.err == DERR_NONE) return p;
+    }
+    return NO_POS;
+}
+
+__global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
+                       const uint32_t* __restrict__ hdr_err, uint64_t* ch_start, uint64_t* ch_end,
+                       uint32_t* ch_cnt, uint32_t* ch_err) {
+    uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_chunks) return;
+    uint32_t r = find_run(runs, n_runs, c);
+    RunInfo R = runs[r];
+    uint64_t local = c - R.chunk_base;
+    const uint8_t* run = (const uint8_t*)R.ptr;
+    uint64_t cs = 1 + local * CHUNK;
+    uint64_t ce = cs + CHUNK < R.len ? cs + CHUNK : R.len;
+    if (hdr_err[r]) {
+        ch_start[c] = cs;
+        ch_end[c] = cs;
+        ch_cnt[c] = 0;
+        ch_err[c] = 0;
+        return;
+    }
+    uint64_t start = local == 0 ? 1 : spec_start(run, R.len, cs, ce);
+    if (start == NO_POS) {
+        ch_start[c] = NO_POS;
+        ch_end[c] = NO_POS;
+        ch_cnt[c] = 0;
+        ch_err[c] = 0;
+        return;
+    }
+    WalkRes w = walk_checked(run, R.len, start, ce, 0xFFFFFFFFu);
+    ch_start[c] = start;
+    ch_end[c] = w.end;
+    ch_cnt[c] = w.cnt;
+    ch_err[c] = w.err;
+}
+
+// A chunk is "bad" when its speculative start is not the exit of its predecessor.
+__global__ void k_validate(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
+                           const uint32_t* __restrict__ hdr_err, const uint64_t* ch_start,
+                           const uint64_t* ch_end, const uint32_t* ch_err, unsigned long long* bad_bits,
+                           uint32_t* run_first_bad) {
+    uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_chunks) return;
+    uint32_t r = find_run(runs, n_runs, c);
+    RunInfo R = runs[r];
+    uint64_t local = c - R.chunk_base;
+    if (local == 0 || hdr_err[r]) return;
+    bool ok = ch_err[c - 1] == 0 && ch_end[c - 1] == ch_start[c];
+    if (!ok) {
+        atomicOr(&bad_bits[c >> 6], 1ull << (c & 63));
+        atomicMin(&run_first_bad[r], (uint32_t)local);
+    }
+}
+
+__device__ uint64_t next_bad(const unsigned long long* bits, uint64_t from, uint64_t to) {
+    uint64_t c = from;
+    while (c < to) {
+        unsigned long long w = bits[c >> 6] >> (c & 63);
+        if (w) {
+            uint64_t r = c + __builtin_ctzll(w);
+            return r < to ? r : to;
+        }
+        c = (c | 63) + 1;
+    }
+    return to;
+}
+
+// Sequential repair of each run's bad chunks from the true chain (exact; rare on real data).
+__global__ void k_fixup(const RunInfo* __restrict__ runs, uint32_t n_runs, const uint32_t* __restrict__ hdr_err,
+                        const uint32_t* __restrict__ run_first_bad, const unsigned long long* __restrict__ bad_bits,
+                        uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_runs) return;
+    uint32_t fb = run_first_bad[r];
+    if (fb == NO_POS32 || hdr_err[r]) return;
+    RunInfo R = runs[r];
+    const uint8_t* run = (const uint8_t*)R.ptr;
+    uint64_t n = R.n_chunks, base = R.chunk_base;
+    uint64_t c = fb;
+    while (c < n) {
+        uint64_t g = base + c;
+        if (ch_err[g - 1]) break;  // a real error in a valid chunk ends the run
+        uint64_t E = ch_end[g - 1];
+        uint64_t cs = 1 + c * CHUNK;
+        uint64_t ce = cs + CHUNK < R.len ? cs + CHUNK : R.len;
+        uint64_t end = E;
+        uint32_t cnt = 0, err = 0;
+        if (E < ce) {
+            WalkRes w = walk_checked(run, R.len, E, ce, 0xFFFFFFFFu);
+            end = w.end;
+            cnt = w.cnt;
+            err = w.err;
+        }
+        ch_start[g] = E;
+        ch_end[g] = end;
+        ch_cnt[g] = cnt;
+        ch_err[g] = err;
+        if (err) break;
+        ++c;
+        if (c >= n) break;
+        if (ch_start[base + c] == end) c = next_bad(bad_bits, base + c + 1, base + n) - base;
+    }
+}
+
+__global__ void k_err_chunk(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
+                            const uint32_t* __restrict__ hdr_err, const uint32_t* __restrict__ ch_err,
+                            uint32_t* run_err_chunk) {
+    uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_chunks) return;
+    if (!ch_err[c]) return;
+    uint32_t r = find_run(runs, n_runs, c);
+    if (hdr_err[r]) return;
+    atomicMin(&run_err_chunk[r], (uint32_t)(c - runs[r].chunk_base));
+}
+
+__global__ void k_mask(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
+                       const uint32_t* __restrict__ hdr_err, const uint32_t* __restrict__ run_err_chunk,
+                       const uint32_t* __restrict__ ch_cnt, uint64_t* cnt64) {
+    uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_chunks) return;
+    uint32_t r = find_run(runs, n_runs, c);
+    uint64_t local = c - runs[r].chunk_base;
+    uint32_t ec = run_err_chunk[r];
+    cnt64[c] = (hdr_err[r] || (ec != NO_POS32 && local > ec)) ? 0 : ch_cnt[c];
+}
+
+__global__ void k_run_summary(const RunInfo* __restrict__ runs, uint32_t n_runs, const uint32_t* __restrict__ hdr_err,
+                              const uint32_t* __restrict__ run_err_chunk, const uint32_t* __restrict__ ch_err,
+                              const uint64_t* __restrict__ ch_rec_base, RunSummary* out) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_runs) return;
+    RunInfo R = runs[r];
+    RunSummary s;
+    s.records = ch_rec_base[R.chunk_base + R.n_chunks] - ch_rec_base[R.chunk_base];
+    uint32_t ec = run_err_chunk[r];
+    s.err = hdr_err[r] ? hdr_err[r] : (ec != NO_POS32 ? ch_err[R.chunk_base + ec] : 0u);
+    s.pad = 0;
+    out[r] = s;
+}
+
+// Emit the record arrays for every validated chunk: address, 16 B key prefix, key length, meta.
+__global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
+                       const uint64_t* __restrict__ ch_start, const uint64_t* __restrict__ ch_rec_base,
+                       uint64_t* __restrict__ rec_addr, uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
+                       uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags) {
+    uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_chunks) return;
+    uint64_t b0 = ch_rec_base[c], cnt = ch_rec_base[c + 1] - b0;
+    if (!cnt) return;
+    uint32_t r = find_run(runs, n_runs, c);
+    const uint8_t* run = (const uint8_t*)runs[r].ptr;
+    uint64_t p = ch_start[c];
+    for (uint64_t i = 0; i < cnt; ++i) {
+        const uint8_t* rp = run + p;
+        uint32_t marker = rp[0];
+        uint64_t klen = ld_be32(rp + 1);
+        uint64_t size = marker == 1 ? 9 + klen + ld_be32(rp + 5 + klen) : 5 + klen;
+        uint64_t hi, lo;
+        key_prefix(rp + 5, klen, hi, lo);
+        uint64_t o = b0 + i;
+        rec_addr[o] = (uint64_t)rp;
+        rec_hi[o] = hi;
+        rec_lo[o] = lo;
+        rec_klen[o] = (uint32_t)klen;
+        if (size >= (1ull << 31)) atomicOr(flags, 1u);  // record too large for this build
+        rec_meta[o] = (uint32_t)size | (marker == 2 ? 0x80000000u : 0u);
+        p += size;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// check: first key decrease inside each stream (rank order)
+
+__global__ void k_order_check(uint64_t R, const uint64_t* __restrict__ stream_base, uint32_t k,
+                              const uint64_t* __restrict__ rec_addr, const uint64_t* __restrict__ rec_hi,
+                              const uint64_t* __restrict__ rec_lo, const uint32_t* __restrict__ rec_klen,
+                              unsigned long long* first_dec, uint32_t* any_dec) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0 || i >= R) return;
+    uint32_t lo = 0, hi = k;  // stream s with base[s] <= i < base[s+1]
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (stream_base[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    if (stream_base[lo] == i) return;
+    int c = key_cmp(rec_hi[i - 1], rec_lo[i - 1], rec_klen[i - 1], (const uint8_t*)rec_addr[i - 1] + 5, rec_hi[i],
+                    rec_lo[i], rec_klen[i], (const uint8_t*)rec_addr[i] + 5);
+    if (c > 0) {
+        atomicMin(&first_dec[lo], (unsigned long long)(i - 1 - stream_base[lo]));
+        atomicOr(any_dec, 1u);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// merge: recursive sampled splitters + LDS tile merge
+//
+// An element is (hi, lo, c) with c = key_len << 32 | rec_idx. Total order: key bytes (prefix,
+// then suffix from the record when both keys exceed 16 B), key length, rec_idx — and rec_idx
+// order == seq_no descending for equal keys, which is exactly HeapItem's pop order.
+
+struct Elems {
+    const uint64_t* hi;
+    const uint64_t* lo;
+    const uint64_t* c;       // null at level 0 (c = klen << 32 | position)
+    const uint32_t* klen;    // level 0 only
+};
+
+template <bool L0>
+__device__ __forceinline__ void load_elem(const Elems& E, uint64_t pos, uint64_t& hi, uint64_t& lo, uint64_t& c) {
+    hi = E.hi[pos];
+    lo = E.lo[pos];
+    c = L0 ? (((uint64_t)E.klen[pos] << 32) | pos) : E.c[pos];
+}
+
+__device__ __forceinline__ int suffix_cmp(const uint64_t* rec_addr, uint64_t ca, uint64_t cb) {
+    uint32_t la = (uint32_t)(ca >> 32), lb = (uint32_t)(cb >> 32);
+    if (la > 16 && lb > 16) {
+        const uint8_t* a = (const uint8_t*)rec_addr[(uint32_t)ca] + 5;
+        const uint8_t* b = (const uint8_t*)rec_addr[(uint32_t)cb] + 5;
+        uint32_t n = la < lb ? la : lb;
+        for (uint32_t i = 16; i < n; ++i) {
+            uint32_t x = a[i], y = b[i];
+            if (x != y) return x < y ? -1 : 1;
+        }
+    }
+    return 0;
+}
+
+// key-only comparison (<0, 0, >0)
+__device__ __forceinline__ int ekey_cmp(const uint64_t* rec_addr, uint64_t ha, uint64_t la_, uint64_t ca,
+                                        uint64_t hb, uint64_t lb_, uint64_t cb) {
+    if (ha != hb) return ha < hb ? -1 : 1;
+    if (la_ != lb_) return la_ < lb_ ? -1 : 1;
+    int s = suffix_cmp(rec_addr, ca, cb);
+    if (s) return s;
+    uint32_t la = (uint32_t)(ca >> 32), lb = (uint32_t)(cb >> 32);
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+// total order (key, then rec_idx)
+__device__ __forceinline__ bool elem_less(const uint64_t* rec_addr, uint64_t ha, uint64_t la_, uint64_t ca,
+                                          uint64_t hb, uint64_t lb_, uint64_t cb) {
+    int k = ekey_cmp(rec_addr, ha, la_, ca, hb, lb_, cb);
+    if (k) return k < 0;
+    return (uint32_t)ca < (uint32_t)cb;
+}
+
+// samples: every S-th element of each list
+template <bool L0>
+__global__ void k_sample(Elems src, const uint64_t* __restrict__ off_src, const uint64_t* __restrict__ off_dst,
+                         uint32_t k, uint64_t S, uint64_t n_dst, uint64_t* dhi, uint64_t* dlo, uint64_t* dc) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_dst) return;
+    uint32_t lo = 0, hi = k;
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (off_dst[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    // skip empty lists sharing this offset: want the last list j with off_dst[j] <= i
+    uint64_t pos = off_src[lo] + (i - off_dst[lo]) * S;
+    uint64_t h, l, c;
+    load_elem<L0>(src, pos, h, l, c);
+    dhi[i] = h;
+    dlo[i] = l;
+    dc[i] = c;
+}
+
+// bounds[t*k + j] = first position of list j whose key >= splitter t's key
+template <bool L0>
+__global__ void k_bounds(Elems E, const uint64_t* __restrict__ off, uint32_t k, const uint64_t* __restrict__ shi,
+                         const uint64_t* __restrict__ slo, const uint64_t* __restrict__ sc, uint64_t m, uint64_t T,
+                         const uint64_t* __restrict__ rec_addr, uint64_t* bounds) {
+    uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (T + 1) * k) return;
+    uint64_t t = g / k;
+    uint32_t j = (uint32_t)(g - t * k);
+    uint64_t a = off[j], b = off[j + 1];
+    if (t == 0) { bounds[g] = a; return; }
+    if (t == T) { bounds[g] = b; return; }
+    uint64_t sp = t * m;
+    uint64_t h = shi[sp], l = slo[sp], c = sc[sp];
+    while (a < b) {
+        uint64_t mid = (a + b) >> 1;
+        uint64_t eh, el, ec;
+        load_elem<L0>(E, mid, eh, el, ec);
+        if (ekey_cmp(rec_addr, eh, el, ec, h, l, c) < 0) a = mid + 1;
+        else b = mid;
+    }
+    bounds[g] = a;
+}
+
+__global__ void k_tile_n(const uint64_t* __restrict__ bounds, uint32_t k, uint64_t T, uint64_t* tile_n) {
+    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    uint64_t s = 0;
+    for (uint32_t j = 0; j < k; ++j) s += bounds[(t + 1) * k + j] - bounds[t * k + j];
+    tile_n[t] = s;
+}
+
+
+
+// LDS layout of k_tile (dynamic): hi[CAP] lo[CAP] c[CAP] u64 | meta[CAP] u32 | pA[CAP] pB[CAP] u16
+// | cbA[k+1] cbB[k+1] u32 | ws[16] u64
+__device__ __forceinline__ uint32_t seg_of(const uint32_t* cb, uint32_t m, uint32_t i) {
+    uint32_t lo = 0, hi = m;  // last s in [0, m) with cb[s] <= i
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (cb[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+template <bool L0>
+__device__ void tile_output(uint32_t n, const uint64_t* hi, const uint64_t* lo, const uint64_t* c, const uint32_t* meta,
+                            const uint16_t* perm, uint64_t base, uint64_t t, bool drop_deletes,
+                            const uint64_t* rec_addr, const TileOut& O, uint64_t* ws) {
+    if (!L0) {
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+            uint32_t e = perm[i];
+            O.ohi[base + i] = hi[e];
+            O.olo[base + i] = lo[e];
+            O.oc[base + i] = c[e];
+        }
+        return;
+    }
+    // dedup (first per key survives: k_way.rs:146-151) + Delete filter, order-preserving compaction
+    constexpr int PER = TILE_CAP / TILE_THREADS;
+    uint32_t i0 = threadIdx.x * PER;
+    uint32_t keep_mask = 0, nk = 0;
+    uint64_t bytes = 0, dels = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        uint32_t i = i0 + q;
+        if (i < n) {
+            uint32_t e = perm[i];
+            bool first = true;
+            if (i > 0) {
+                uint32_t p = perm[i - 1];
+                first = ekey_cmp(rec_addr, hi[p], lo[p], c[p], hi[e], lo[e], c[e]) != 0;
+            }
+            bool del = (meta[e] >> 31) != 0;
+            bool keep = first && !(drop_deletes && del);
+            if (keep) {
+                keep_mask |= 1u << q;
+                ++nk;
+                bytes += meta[e] & 0x7FFFFFFFu;
+                dels += del ? 1 : 0;
+            }
+        }
+    }
+    uint64_t tot;
+    uint64_t rank = block_excl_scan<uint64_t>(nk, ws, tot);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (keep_mask & (1u << q)) {
+            uint32_t e = perm[i0 + q];
+            O.t_rec[base + rank] = (uint32_t)c[e];
+            O.t_meta[base + rank] = meta[e];
+            ++rank;
+        }
+    }
+    uint64_t tb = block_reduce_sum<uint64_t>(bytes, ws);
+    uint64_t td = block_reduce_sum<uint64_t>(dels, ws);
+    if (threadIdx.x == 0) {
+        O.tile_kept[t] = tot;
+        O.tile_bytes[t] = tb;
+        O.tile_dels[t] = td;
+    }
+}
+
+// Tiles larger than TILE_CAP: bitonic sort in global scratch (ascending-comparator form, so
+// virtual +inf padding never moves), then the same output stage in blocks of TILE_CAP.
+template <bool L0>
+__device__ void tile_big(Elems E, const uint64_t* bounds, uint32_t k, uint64_t t, uint64_t base, uint32_t n,
+                         const uint32_t* sb, const uint32_t* rec_meta, const uint64_t* rec_addr, bool drop_deletes,
+                         const TileOut& O, uint64_t* ws, uint32_t* s_flag) {
+    uint64_t* xh = O.xhi + base;
+    uint64_t* xl = O.xlo + base;
+    uint64_t* xc = O.xc + base;
+    uint32_t* xm = O.xmeta + base;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        uint32_t j = seg_of(sb, k + 1, i);
+        uint64_t pos = bounds[t * k + j] + (i - sb[j]);
+        uint64_t h, l, c;
+        load_elem<L0>(E, pos, h, l, c);
+        xh[i] = h;
+        xl[i] = l;
+        xc[i] = c;
+        if (L0) xm[i] = rec_meta[pos];
+    }
+    __syncthreads();
+    uint32_t P = 1;
+    while (P < n) P <<= 1;
+    for (uint32_t kk = 2; kk <= P; kk <<= 1) {
+        for (uint32_t jj = kk >> 1; jj >= 1; jj >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P / 2; i += blockDim.x) {
+                uint32_t a, b;
+                if (jj == (kk >> 1)) {
+                    uint32_t blk = i / jj, off = i % jj;
+                    a = blk * kk + off;
+                    b = blk * kk + kk - 1 - off;
+                } else {
+                    uint32_t blk = i / jj, off = i % jj;
+                    a = blk * 2 * jj + off;
+                    b = a + jj;
+                }
+                if (b < n) {
+                    if (elem_less(rec_addr, xh[b], xl[b], xc[b], xh[a], xl[a], xc[a])) {
+                        uint64_t th = xh[a], tl = xl[a], tc = xc[a];
+                        xh[a] = xh[b]; xl[a] = xl[b]; xc[a] = xc[b];
+                        xh[b] = th; xl[b] = tl; xc[b] = tc;
+                        if (L0) { uint32_t tm = xm[a]; xm[a] = xm[b]; xm[b] = tm; }
+                    }
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+    }
+    if (!L0) {
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+            O.ohi[base + i] = xh[i];
+            O.olo[base + i] = xl[i];
+            O.oc[base + i] = xc[i];
+        }
+        return;
+    }
+    uint64_t kept = 0, bytes = 0, dels = 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += blockDim.x) {
+        uint32_t i = b0 + threadIdx.x;
+        bool keep = false;
+        uint32_t m = 0;
+        if (i < n) {
+            bool first = i == 0 || ekey_cmp(rec_addr, xh[i - 1], xl[i - 1], xc[i - 1], xh[i], xl[i], xc[i]) != 0;
+            m = xm[i];
+            keep = first && !(drop_deletes && (m >> 31));
+        }
+        uint64_t tot;
+        uint64_t r = block_excl_scan<uint64_t>(keep ? 1 : 0, ws, tot);
+        // all reads of this block are done before any writes of it (output region == base..)
+        __syncthreads();
+        if (keep) {
+            O.t_rec[base + kept + r] = (uint32_t)xc[i];
+            O.t_meta[base + kept + r] = m;
+        }
+        kept += tot;
+        bytes += block_reduce_sum<uint64_t>(keep ? (m & 0x7FFFFFFFu) : 0, ws);
+        dels += block_reduce_sum<uint64_t>(keep && (m >> 31) ? 1 : 0, ws);
+    }
+    if (threadIdx.x == 0) {
+        O.tile_kept[t] = kept;
+        O.tile_bytes[t] = bytes;
+        O.tile_dels[t] = dels;
+    }
+    (void)s_flag;
+}
+
+template <bool L0>
+__global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* __restrict__ bounds, uint32_t k,
+                                                      const uint64_t* __restrict__ tile_base,
+                                                      const uint32_t* __restrict__ rec_meta,
+                                                      const uint64_t* __restrict__ rec_addr, uint32_t drop_deletes,
+                                                      TileOut O) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint64_t* s_hi = (uint64_t*)smem;
+    uint64_t* s_lo = s_hi + TILE_CAP;
+    uint64_t* s_c = s_lo + TILE_CAP;
+    uint32_t* s_meta = (uint32_t*)(s_c + TILE_CAP);
+    uint16_t* pA = (uint16_t*)(s_meta + TILE_CAP);
+    uint16_t* pB = pA + TILE_CAP;
+    uint32_t* cbA = (uint32_t*)(pB + TILE_CAP);
+    uint32_t* cbB = cbA + (k + 1);
+    uint64_t* ws = (uint64_t*)(((uintptr_t)(cbB + (k + 1)) + 15) & ~(uintptr_t)15);
+    uint32_t* s_flag = (uint32_t*)(ws + 16);
+
+    const uint64_t t = blockIdx.x;
+    const uint64_t base = tile_base[t];
+    const uint64_t n64 = tile_base[t + 1] - base;
+    // segment starts
+    uint64_t segtot = 0;
+    for (uint32_t j0 = 0; j0 < k; j0 += blockDim.x) {
+        uint32_t j = j0 + threadIdx.x;
+        uint64_t len = j < k ? bounds[(t + 1) * k + j] - bounds[t * k + j] : 0;
+        uint64_t tot;
+        uint64_t ex = block_excl_scan<uint64_t>(len, ws, tot);
+        if (j < k) cbA[j] = (uint32_t)(segtot + ex);
+        segtot += tot;
+    }
+    if (threadIdx.x == 0) cbA[k] = (uint32_t)segtot;
+    __syncthreads();
+    const uint32_t n = (uint32_t)n64;
+    if (n64 > TILE_CAP) {
+        tile_big<L0>(E, bounds, k, t, base, n, cbA, rec_meta, rec_addr, drop_deletes != 0, O, ws, s_flag);
+        return;
+    }
+    if (n == 0) {
+        if (L0 && threadIdx.x == 0) {
+            O.tile_kept[t] = 0;
+            O.tile_bytes[t] = 0;
+            O.tile_dels[t] = 0;
+        }
+        return;
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        uint32_t j = seg_of(cbA, k + 1, i);
+        uint64_t pos = bounds[t * k + j] + (i - cbA[j]);
+        uint64_t h, l, c;
+        load_elem<L0>(E, pos, h, l, c);
+        s_hi[i] = h;
+        s_lo[i] = l;
+        s_c[i] = c;
+        s_meta[i] = L0 ? rec_meta[pos] : 0u;
+        pA[i] = (uint16_t)i;
+    }
+    __syncthreads();
+    // pairwise merge rounds: each element finds its rank in the partner segment
+    uint32_t m = k;
+    uint32_t* cb = cbA;
+    uint32_t* cbn = cbB;
+    while (m > 1) {
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+            uint32_t s = seg_of(cb, m + 1, i);
+            uint32_t e = pA[i];
+            uint32_t local = i - cb[s];
+            uint32_t ps = s ^ 1u;
+            uint32_t newpos;
+            if (ps >= m) {
+                newpos = i;
+            } else {
+                uint32_t a = cb[ps], b = cb[ps + 1];
+                uint64_t eh = s_hi[e], el = s_lo[e], ec = s_c[e];
+                while (a < b) {  // count partner elements < e
+                    uint32_t mid = (a + b) >> 1;
+                    uint32_t x = pA[mid];
+                    if (elem_less(rec_addr, s_hi[x], s_lo[x], s_c[x], eh, el, ec)) a = mid + 1;
+                    else b = mid;
+                }
+                newpos = cb[s & ~1u] + local + (a - cb[ps]);
+            }
+            pB[newpos] = (uint16_t)e;
+        }
+        __syncthreads();
+        uint32_t mn = (m + 1) >> 1;
+        for (uint32_t p = threadIdx.x; p <= mn; p += blockDim.x) cbn[p] = p < mn ? cb[2 * p] : cb[m];
+        __syncthreads();
+        uint16_t* tp = pA; pA = pB; pB = tp;
+        uint32_t* tc = cb; cb = cbn; cbn = tc;
+        m = mn;
+    }
+    tile_output<L0>(n, s_hi, s_lo, s_c, s_meta, pA, base, t, drop_deletes != 0, rec_addr, O, ws);
+}
+
+// dense merged arrays: rec_idx, source address, output-byte prefix P, delete-count prefix
+__global__ void __launch_bounds__(1024) k_finalize(uint64_t T, const uint64_t* __restrict__ tile_base,
+                                                   const uint64_t* __restrict__ tile_kept,
+                                                   const uint64_t* __restrict__ kept_base,
+                                                   const uint64_t* __restrict__ byte_base,
+                                                   const uint64_t* __restrict__ del_base,
+                                                   const uint32_t* __restrict__ t_rec, const uint32_t* __restrict__ t_meta,
+                                                   const uint64_t* __restrict__ rec_addr, uint32_t* m_rec,
+                                                   uint64_t* m_src, uint64_t* m_P, uint64_t* m_Dp, uint32_t* max_rec) {
+    __shared__ uint64_t ws[16];
+    const uint64_t t = blockIdx.x;
+    const uint64_t n = tile_kept[t], src = tile_base[t];
+    uint64_t g = kept_base[t], pb = byte_base[t], pd = del_base[t];
+    uint32_t mx = 0;
+    for (uint64_t b0 = 0; b0 < n; b0 += blockDim.x) {
+        uint64_t i = b0 + threadIdx.x;
+        uint32_t meta = i < n ? t_meta[src + i] : 0u;
+        uint64_t sz = meta & 0x7FFFFFFFu, dl = meta >> 31;
+        uint64_t tb, td;
+        uint64_t eb = block_excl_scan<uint64_t>(sz, ws, tb);
+        uint64_t ed = block_excl_scan<uint64_t>(dl, ws, td);
+        if (i < n) {
+            uint32_t r = t_rec[src + i];
+            m_rec[g + i] = r;
+            m_src[g + i] = rec_addr[r];
+            m_P[g + i] = pb + eb;
+            m_Dp[g + i] = pd + ed;
+            mx = (uint32_t)sz > mx ? (uint32_t)sz : mx;
+        }
+        g += 0;
+        pb += tb;
+        pd += td;
+        (void)0;
+    }
+    if (mx) atomicMax(max_rec, mx);
+    if (t == T - 1 && threadIdx.x == 0) {
+        m_P[kept_base[t] + n] = pb;
+        m_Dp[kept_base[t] + n] = pd;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// chain: build_runs' greedy split (runs.rs:211-238). A run starting at surviving record b
+// holds records b..e-1 where e is the largest index with 1 + P[e] - P[b] <= max (at least b+1).
+// One wave walks the chain; each step checks a window around the predicted end first.
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        uint64_t o = __shfl_xor(v, d, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+__global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ P,
+                                              uint64_t max_size, uint64_t* run_b, uint64_t* n_runs_out) {
+    const uint64_t K = *Kp;
+    const int lane = threadIdx.x;
+    if (K == 0) {
+        if (lane == 0) { run_b[0] = 0; *n_runs_out = 0; }
+        return;
+    }
+    uint64_t b = 0, m = 0;
+    uint64_t Pb = P[0];
+    const uint64_t total = P[K];
+    uint64_t L = 1;
+    if (max_size > 1) {
+        uint64_t avg = total / K;
+        if (avg == 0) avg = 1;
+        L = (max_size - 1) / avg;
+        if (L == 0) L = 1;
+    }
+    while (b < K) {
+        uint64_t e;
+        if (max_size == 0 || P[b + 1] - Pb + 1 > max_size) {
+            e = b + 1;  // the first record never splits: a run of one oversized record
+        } else {
+            const uint64_t v = Pb + max_size - 1;  // record j fits iff P[j+1] <= v
+            // window of 256 positions around b + L
+            uint64_t ws = b + L > 128 ? b + L - 128 : 0;
+            if (ws < b + 1) ws = b + 1;
+            uint64_t best = 0;
+            bool any_gt = false;
+            for (int q = 0; q < 4; ++q) {
+                uint64_t pos = ws + (uint64_t)lane * 4 + q;
+                if (pos <= K) {
+                    uint64_t pv = P[pos];
+                    if (pv <= v) best = pos > best ? pos : best;
+                    else any_gt = true;
+                }
+            }
+            best = wave_max_u64(best);
+            bool gt = __any(any_gt);
+            uint64_t wend = ws + 256;  // exclusive
+            bool ok = best >= ws && (best == K || (gt && best + 1 < wend));
+            if (ok) {
+                e = best;
+            } else {
+                // 64-ary search on [lo, hi]: P[lo] <= v holds for lo = b+1
+                uint64_t lo = b + 1, hi = K;
+                while (lo < hi) {
+                    uint64_t span = hi - lo;
+                    uint64_t step = (span + 63) / 64;
+                    uint64_t pos = lo + (uint64_t)(lane + 1) * step;
+                    if (pos > hi) pos = hi;
+                    bool f = P[pos] <= v;
+                    uint64_t cand = f ? pos : lo;
+                    uint64_t nlo = wave_max_u64(cand);
+                    // smallest probed position with P > v bounds hi
+                    uint64_t gtpos = f ? ~0ull : pos;
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) {
+                        uint64_t o = __shfl_xor(gtpos, d, 64);
+                        gtpos = o < gtpos ? o : gtpos;
+                    }
+                    lo = nlo;
+                    if (gtpos != ~0ull) hi = gtpos - 1;
+                    if (step == 1) break;
+                }
+                e = lo;
+            }
+            uint64_t len = e - b;
+            L = len;
+        }
+        if (lane == 0) run_b[m] = b;
+        ++m;
+        b = e;
+        Pb = P[b];
+    }
+    if (lane == 0) {
+        run_b[m] = K;
+        *n_runs_out = m;
+    }
+}
+
+__global__ void k_run_stats(const uint64_t* __restrict__ n_runs_p, const uint64_t* __restrict__ run_b,
+                            const uint64_t* __restrict__ P, const uint64_t* __restrict__ Dp,
+                            const uint32_t* __restrict__ m_rec, const uint32_t* __restrict__ rec_klen,
+                            DevRunDesc* descs) {
+    const uint64_t n_runs = *n_runs_p;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_runs; r += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t b = run_b[r], e = run_b[r + 1];
+        DevRunDesc d;
+        d.off = P[b] + r;
+        d.len = 1 + P[e] - P[b];
+        d.delete_count = Dp[e] - Dp[b];
+        d.put_count = (e - b) - d.delete_count;
+        d.min_key_off = d.off + 1 + 5;
+        d.min_key_len = rec_klen[m_rec[b]];
+        d.max_key_off = d.off + 1 + (P[e - 1] - P[b]) + 5;
+        d.max_key_len = rec_klen[m_rec[e - 1]];
+        d.table_id = 0;
+        d.reserved = 0;
+        descs[r] = d;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// gather: workgroup per GATHER_SEG surviving records. Output byte x of the job is covered by a
+// "piece": a record (copied verbatim from its input address) or a run's version byte. Record j
+// of run r lands at P[j] + r + 1; run r's version byte at P[b_r] + r. Each lane produces whole
+// 16-byte aligned output blocks with one vector store; blocks shared with a neighbouring
+// workgroup (segment edges) are written bytewise.
+
+__global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __restrict__ Kp,
+                                                           const uint64_t* __restrict__ n_runs_p,
+                                                           const uint64_t* __restrict__ run_b,
+                                                           const uint64_t* __restrict__ P,
+                                                           const uint64_t* __restrict__ m_src, uint8_t* __restrict__ out) {
+    __shared__ uint64_t s_dst[2 * GATHER_SEG];
+    __shared__ uint64_t s_src[2 * GATHER_SEG];  // 0 => version byte
+    __shared__ uint32_t s_len[2 * GATHER_SEG];
+    __shared__ uint64_t s_rb[GATHER_SEG + 2];
+    __shared__ uint64_t ws[16];
+    __shared__ uint64_t s_r0, s_nrb;
+    const uint64_t K = *Kp;
+    const uint64_t j0 = (uint64_t)blockIdx.x * GATHER_SEG;
+    if (j0 >= K) return;
+    const uint64_t j1 = j0 + GATHER_SEG < K ? j0 + GATHER_SEG : K;
+    const uint64_t n_runs = *n_runs_p;
+    if (threadIdx.x == 0) {
+        uint64_t lo = 0, hi = n_runs;  // last run with run_b <= j0
+        while (hi - lo > 1) {
+            uint64_t mid = (lo + hi) >> 1;
+            if (run_b[mid] <= j0) lo = mid;
+            else hi = mid;
+        }
+        s_r0 = lo;
+    }
+    __syncthreads();
+    const uint64_t r0 = s_r0;
+    // run starts r0 .. r0+nrb-1 that are <= j1-1
+    for (uint32_t i = threadIdx.x; i < GATHER_SEG + 1; i += blockDim.x) {
+        uint64_t r = r0 + i;
+        s_rb[i] = r <= n_runs ? run_b[r] : ~0ull;
+    }
+    __syncthreads();
+    // pieces: per record 1 or 2
+    const uint32_t nrec = (uint32_t)(j1 - j0);
+    uint32_t cntp = 0;
+    uint64_t j = j0 + threadIdx.x;
+    uint64_t rr = 0;
+    bool start = false;
+    if (threadIdx.x < nrec) {
+        uint32_t q = upper_idx<uint64_t>(s_rb, GATHER_SEG + 1, j);
+        rr = r0 + q;
+        start = s_rb[q] == j;
+        cntp = start ? 2 : 1;
+    }
+    uint64_t tot;
+    uint32_t pi = (uint32_t)block_excl_scan<uint64_t>(cntp, ws, tot);
+    const uint32_t npieces = (uint32_t)tot;
+    if (threadIdx.x < nrec) {
+        uint64_t dst = P[j] + rr + 1;
+        if (start) {
+            s_dst[pi] = dst - 1;
+            s_src[pi] = 0;
+            s_len[pi] = 1;
+            ++pi;
+        }
+        s_dst[pi] = dst;
+        s_src[pi] = m_src[j];
+        s_len[pi] = (uint32_t)(P[j + 1] - P[j]);
+    }
+    __syncthreads();
+    const uint64_t lo_b = s_dst[0];
+    const uint64_t hi_b = s_dst[npieces - 1] + s_len[npieces - 1];
+    const uint64_t q0 = lo_b >> 4, q1 = (hi_b + 15) >> 4;
+    uint32_t hint = 0;
+    for (uint64_t q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+        const uint64_t B = q << 4;
+        const uint64_t x0 = B > lo_b ? B : lo_b;
+        const uint64_t x1 = B + 16 < hi_b ? B + 16 : hi_b;
+        // piece containing x0
+        uint32_t p;
+        {
+            uint32_t lo = 0, hi = npieces;
+            while (hi - lo > 1) {
+                uint32_t mid = (lo + hi) >> 1;
+                if (s_dst[mid] <= x0) lo = mid;
+                else hi = mid;
+            }
+            p = lo;
+        }
+        (void)hint;
+        const bool full = x0 == B && x1 == B + 16;
+        if (full && s_src[p] != 0 && s_dst[p] + s_len[p] >= B + 16) {
+            uint4 v = load16_unaligned((const uint8_t*)s_src[p] + (B - s_dst[p]));
+            *(uint4*)(out + B) = v;
+            continue;
+        }
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint64_t x = x0; x < x1; ++x) {
+            while (s_dst[p] + s_len[p] <= x) ++p;
+            uint32_t byte = s_src[p] ? ((const uint8_t*)s_src[p])[x - s_dst[p]] : 1u;
+            uint32_t k = (uint32_t)(x - B);
+            if (full) {
+#pragma unroll
+                for (int wi = 0; wi < 4; ++wi)
+                    if ((k >> 2) == (uint32_t)wi) w[wi] |= byte << (8 * (k & 3));
+            } else {
+                out[x] = (uint8_t)byte;
+            }
+        }
+        if (full) *(uint4*)(out + B) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// device-wide exclusive scan of u64 (reduce -> scan partials -> apply), total at out[n]
+
+constexpr int SCAN_THREADS = 1024;
+constexpr int SCAN_PER = 4;
+constexpr uint64_t SCAN_BLOCK = SCAN_THREADS * SCAN_PER;
+
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_reduce(const uint64_t* in, uint64_t n, uint64_t* partial) {
+    __shared__ uint64_t ws[16];
+    uint64_t b0 = blockIdx.x * SCAN_BLOCK;
+    uint64_t s = 0;
+#pragma unroll
+    for (int q = 0; q < SCAN_PER; ++q) {
+        uint64_t i = b0 + (uint64_t)threadIdx.x * SCAN_PER + q;
+        if (i < n) s += in[i];
+    }
+    uint64_t t = block_reduce_sum<uint64_t>(s, ws);
+    if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(const uint64_t* in, uint64_t n, const uint64_t* partial_ex,
+                                                             uint64_t* out) {
+    __shared__ uint64_t ws[16];
+    uint64_t b0 = blockIdx.x * SCAN_BLOCK;
+    uint64_t v[SCAN_PER];
+    uint64_t s = 0;
+#pragma unroll
+    for (int q = 0; q < SCAN_PER; ++q) {
+        uint64_t i = b0 + (uint64_t)threadIdx.x * SCAN_PER + q;
+        v[q] = i < n ? in[i] : 0;
+        s += v[q];
+    }
+    uint64_t tot;
+    uint64_t ex = block_excl_scan<uint64_t>(s, ws, tot) + partial_ex[blockIdx.x];
+#pragma unroll
+    for (int q = 0; q < SCAN_PER; ++q) {
+        uint64_t i = b0 + (uint64_t)threadIdx.x * SCAN_PER + q;
+        if (i < n) out[i] = ex;
+        ex += v[q];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == blockDim.x - 1) out[n] = ex;
+}
+
+// ---------------------------------------------------------------------------------------
+// launch wrappers (C++ linkage, used by skv_host.hip)
+
+static inline unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+void launch_run_header(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err) {
+    if (n_runs) k_run_header<<<blocks_for(n_runs, 256), 256, 0, s>>>(runs, n_runs, hdr_err);
+}
+void launch_spec(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
+                 uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err) {
+    if (n_chunks) k_spec<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, ch_start, ch_end, ch_cnt, ch_err);
+}
+void launch_validate(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
+                     const uint64_t* ch_start, const uint64_t* ch_end, const uint32_t* ch_err,
+                     unsigned long long* bad_bits, uint32_t* run_first_bad) {
+    if (n_chunks)
+        k_validate<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, ch_start, ch_end, ch_err,
+                                                             bad_bits, run_first_bad);
+}
+void launch_fixup(hipStream_t s, const RunInfo* runs, uint32_t n_runs, const uint32_t* hdr_err,
+                  const uint32_t* run_first_bad, const unsigned long long* bad_bits, uint64_t* ch_start,
+                  uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err) {
+    if (n_runs)
+        k_fixup<<<blocks_for(n_runs, 64), 64, 0, s>>>(runs, n_runs, hdr_err, run_first_bad, bad_bits, ch_start, ch_end,
+                                                       ch_cnt, ch_err);
+}
+void launch_err_chunk(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
+                      const uint32_t* ch_err, uint32_t* run_err_chunk) {
+    if (n_chunks) k_err_chunk<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, ch_err, run_err_chunk);
+}
+void launch_mask(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
+                 const uint32_t* run_err_chunk, const uint32_t* ch_cnt, uint64_t* cnt64) {
+    if (n_chunks) k_mask<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, run_err_chunk, ch_cnt, cnt64);
+}
+void launch_run_summary(hipStream_t s, const RunInfo* runs, uint32_t n_runs, const uint32_t* hdr_err,
+                        const uint32_t* run_err_chunk, const uint32_t* ch_err, const uint64_t* ch_rec_base,
+                        RunSummary* out) {
+    if (n_runs)
+        k_run_summary<<<blocks_for(n_runs, 256), 256, 0, s>>>(runs, n_runs, hdr_err, run_err_chunk, ch_err, ch_rec_base, out);
+}
+void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint64_t* ch_start,
+                 const uint64_t* ch_rec_base, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
+                 uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags) {
+    if (n_chunks)
+        k_emit<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, ch_start, ch_rec_base, rec_addr, rec_hi,
+                                                         rec_lo, rec_klen, rec_meta, flags);
+}
+void launch_order_check(hipStream_t s, uint64_t R, const uint64_t* stream_base, uint32_t k, const uint64_t* rec_addr,
+                        const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,
+                        unsigned long long* first_dec, uint32_t* any_dec) {
+    if (R > 1)
+        k_order_check<<<blocks_for(R, 256), 256, 0, s>>>(R, stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, first_dec,
+                                                         any_dec);
+}
+void launch_sample(hipStream_t s, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
+                   const uint32_t* klen, const uint64_t* off_src, const uint64_t* off_dst, uint32_t k, uint64_t S,
+                   uint64_t n_dst, uint64_t* dhi, uint64_t* dlo, uint64_t* dc) {
+    if (!n_dst) return;
+    Elems E{hi, lo, c, klen};
+    if (l0) k_sample<true><<<blocks_for(n_dst, 256), 256, 0, s>>>(E, off_src, off_dst, k, S, n_dst, dhi, dlo, dc);
+    else k_sample<false><<<blocks_for(n_dst, 256), 256, 0, s>>>(E, off_src, off_dst, k, S, n_dst, dhi, dlo, dc);
+}
+void launch_bounds(hipStream_t s, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
+                   const uint32_t* klen, const uint64_t* off, uint32_t k, const uint64_t* shi, const uint64_t* slo,
+                   const uint64_t* sc, uint64_t m, uint64_t T, const uint64_t* rec_addr, uint64_t* bounds) {
+    Elems E{hi, lo, c, klen};
+    uint64_t n = (T + 1) * k;
+    if (l0) k_bounds<true><<<blocks_for(n, 256), 256, 0, s>>>(E, off, k, shi, slo, sc, m, T, rec_addr, bounds);
+    else k_bounds<false><<<blocks_for(n, 256), 256, 0, s>>>(E, off, k, shi, slo, sc, m, T, rec_addr, bounds);
+}
+void launch_tile_n(hipStream_t s, const uint64_t* bounds, uint32_t k, uint64_t T, uint64_t* tile_n) {
+    k_tile_n<<<blocks_for(T, 256), 256, 0, s>>>(bounds, k, T, tile_n);
+}
+size_t tile_lds_bytes(uint32_t k) {
+    size_t b = (size_t)TILE_CAP * (3 * 8 + 4 + 2 + 2) + 2 * (size_t)(k + 1) * 4;
+    b = (b + 15) & ~(size_t)15;
+    return b + 16 * 8 + 16;
+}
+hipError_t launch_tile(hipStream_t s, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
+                       const uint32_t* klen, const uint64_t* bounds, uint32_t k, uint64_t T, const uint64_t* tile_base,
+                       const uint32_t* rec_meta, const uint64_t* rec_addr, uint32_t drop, TileOut O) {
+    Elems E{hi, lo, c, klen};
+    size_t lds = tile_lds_bytes(k);
+    if (l0) {
+        (void)hipFuncSetAttribute((const void*)k_tile<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        k_tile<true><<<(unsigned)T, TILE_THREADS, lds, s>>>(E, bounds, k, tile_base, rec_meta, rec_addr, drop, O);
+    } else {
+        (void)hipFuncSetAttribute((const void*)k_tile<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        k_tile<false><<<(unsigned)T, TILE_THREADS, lds, s>>>(E, bounds, k, tile_base, rec_meta, rec_addr, drop, O);
+    }
+    return hipGetLastError();
+}
+void launch_finalize(hipStream_t s, uint64_t T, const uint64_t* tile_base, const uint64_t* tile_kept,
+                     const uint64_t* kept_base, const uint64_t* byte_base, const uint64_t* del_base, const uint32_t* t_rec,
+                     const uint32_t* t_meta, const uint64_t* rec_addr, uint32_t* m_rec, uint64_t* m_src, uint64_t* m_P,
+                     uint64_t* m_Dp, uint32_t* max_rec) {
+    k_finalize<<<(unsigned)T, 1024, 0, s>>>(T, tile_base, tile_kept, kept_base, byte_base, del_base, t_rec, t_meta,
+                                              rec_addr, m_rec, m_src, m_P, m_Dp, max_rec);
+}
+void launch_chain(hipStream_t s, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, uint64_t* run_b,
+                  uint64_t* n_runs) {
+    k_chain<<<1, 64, 0, s>>>(Kp, P, max_size, run_b, n_runs);
+}
+void launch_run_stats(hipStream_t s, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
+                      const uint64_t* Dp, const uint32_t* m_rec, const uint32_t* rec_klen, DevRunDesc* descs,
+                      uint64_t max_runs) {
+    unsigned blocks = blocks_for(max_runs ? max_runs : 1, 256);
+    if (blocks > 4096) blocks = 4096;
+    k_run_stats<<<blocks, 256, 0, s>>>(n_runs, run_b, P, Dp, m_rec, rec_klen, descs);
+}
+void launch_gather(hipStream_t s, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
+                   const uint64_t* m_src, uint8_t* out, uint64_t max_K) {
+    if (!max_K) return;
+    k_gather<<<blocks_for(max_K, GATHER_SEG), GATHER_THREADS, 0, s>>>(Kp, n_runs, run_b, P, m_src, out);
+}
+// exclusive scan of n u64 values into out[0..n] (out[n] = total); tmp needs scan_tmp_words(n)
+uint64_t scan_tmp_words(uint64_t n) {
+    uint64_t w = 0;
+    while (true) {
+        uint64_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
+        w += 2 * nb + 2;
+        if (nb <= 1) break;
+        n = nb;
+    }
+    return w;
+}
+void launch_scan(hipStream_t s, const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tmp) {
+    uint64_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
+    if (nb == 0) {
+        (void)hipMemsetAsync(out, 0, 8, s);
+        return;
+    }
+    uint64_t* partial = tmp;
+    uint64_t* partial_ex = tmp + nb;
+    k_scan_reduce<<<(unsigned)nb, SCAN_THREADS, 0, s>>>(in, n, partial);
+    if (nb == 1) {
+        (void)hipMemsetAsync(partial_ex, 0, 8, s);
+    } else {
+        launch_scan(s, partial, nb, partial_ex, tmp + 2 * nb + 2);
+    }
+    k_scan_apply<<<(unsigned)nb, SCAN_THREADS, 0, s>>>(in, n, partial_ex, out);
+}
+
+}  // namespace skv

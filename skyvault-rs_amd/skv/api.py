@@ -1,0 +1,159 @@
+"""Host-side binding of libskv.so (include/skv.h) — the MI355X compaction path.
+
+`Compactor` owns one skv_ctx (one GPU). Its `compact()` is the drop-in for the
+read_run_stream -> k_way::merge -> [filter] -> build_runs composition the reference's jobs
+perform (see skv.jobs for the job-level stream assembly). There is no CPU mode: if the
+library or the GPU is missing this raises, it never falls back.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import List, Optional, Sequence, Tuple
+
+from ._abi import (
+    EXPORTED_SYMBOLS,
+    LIB_PATH,
+    PKG_DIR,
+    SKV_OK,
+    OutRun,
+    RunError,
+    SkvResult,
+    SkvTimings,
+    StreamArgs,
+    result_to_runs,
+)
+
+MAX_RUN_SIZE = 4 * 1024 * 1024  # the jobs' build_runs limit (table_buffer_compaction.rs:279)
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile skv/libskv.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    src_dir = os.path.dirname(PKG_DIR)
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", src_dir] + (["-B"] if force else []))
+    return LIB_PATH
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is not built (run skv.api.build() / __graft_entry__.build())")
+    l = C.CDLL(LIB_PATH)
+    l.skv_abi_version.restype = C.c_int
+    l.skv_device_count.argtypes = [C.POINTER(C.c_int)]
+    l.skv_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+    l.skv_ctx_destroy.argtypes = [C.c_void_p]
+    l.skv_ctx_destroy.restype = None
+    l.skv_last_error.argtypes = [C.c_void_p]
+    l.skv_last_error.restype = C.c_char_p
+    l.skv_ctx_set_profiling.argtypes = [C.c_void_p, C.c_int]
+    l.skv_ctx_get_timings.argtypes = [C.c_void_p, C.POINTER(SkvTimings)]
+    for fn in (l.skv_compact, l.skv_compact_dev):
+        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.POINTER(C.POINTER(SkvResult))]
+        fn.restype = C.c_int
+    l.skv_result_free.argtypes = [C.POINTER(SkvResult)]
+    l.skv_result_free.restype = None
+    _lib = l
+    return l
+
+
+def exported_symbols_present() -> List[str]:
+    l = load()
+    return [s for s in EXPORTED_SYMBOLS if hasattr(l, s)]
+
+
+class DeviceResult:
+    """Output of compact_dev: run bytes stay in HBM (device pointer owned by the ctx)."""
+
+    def __init__(self, lib, res_ptr):
+        self._lib = lib
+        self._res = res_ptr
+        r = res_ptr.contents
+        self.dev_ptr = int(r.bytes or 0)
+        self.n_bytes = int(r.n_bytes)
+        self.n_runs = int(r.n_runs)
+        self.in_bytes = int(r.in_bytes)
+        self.in_records = int(r.in_records)
+        self.out_records = int(r.out_records)
+        self.descs = [(d.off, d.len, d.put_count, d.delete_count, d.min_key_off, d.min_key_len, d.max_key_off,
+                       d.max_key_len, d.table_id) for d in (r.runs[i] for i in range(r.n_runs))]
+
+    def free(self):
+        if self._res:
+            self._lib.skv_result_free(self._res)
+            self._res = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Compactor:
+    def __init__(self, device: int = 0, profiling: bool = False):
+        self.lib = load()
+        self.ctx = C.c_void_p()
+        rc = self.lib.skv_ctx_create(device, C.byref(self.ctx))
+        if rc != SKV_OK:
+            raise RunError(rc, f"skv_ctx_create(device={device}) failed: no usable HIP device")
+        if profiling:
+            self.lib.skv_ctx_set_profiling(self.ctx, 1)
+
+    def close(self):
+        if self.ctx:
+            self.lib.skv_ctx_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self, rc):
+        return RunError(rc, self.lib.skv_last_error(self.ctx).decode("utf-8", "replace"))
+
+    def compact(self, streams: Sequence[Tuple[int, Sequence[bytes]]], max_run_size: int = MAX_RUN_SIZE,
+                flags: int = 0, with_info: bool = False):
+        """streams: [(seq_no, [run_bytes, ...])] (host memory). Returns [OutRun]."""
+        sa = StreamArgs(streams)
+        res = C.POINTER(SkvResult)()
+        rc = self.lib.skv_compact(self.ctx, C.cast(sa.arr, C.c_void_p), sa.n, max_run_size, flags, C.byref(res))
+        if rc != SKV_OK:
+            raise self._err(rc)
+        try:
+            runs = result_to_runs(res.contents)
+            info = dict(in_bytes=res.contents.in_bytes, in_records=res.contents.in_records,
+                        out_records=res.contents.out_records, dropped_tables=res.contents.dropped_tables,
+                        n_bytes=res.contents.n_bytes)
+        finally:
+            self.lib.skv_result_free(res)
+        return (runs, info) if with_info else runs
+
+    def compact_dev(self, streams: Sequence[Tuple[int, Sequence[Tuple[int, int]]]],
+                    max_run_size: int = MAX_RUN_SIZE, flags: int = 0) -> DeviceResult:
+        """streams: [(seq_no, [(device_ptr, length), ...])] with inputs resident in HBM."""
+        sa = StreamArgs(streams, device=True)
+        res = C.POINTER(SkvResult)()
+        rc = self.lib.skv_compact_dev(self.ctx, C.cast(sa.arr, C.c_void_p), sa.n, max_run_size, flags, C.byref(res))
+        if rc != SKV_OK:
+            raise self._err(rc)
+        return DeviceResult(self.lib, res)
+
+    def timings(self) -> dict:
+        t = SkvTimings()
+        self.lib.skv_ctx_get_timings(self.ctx, C.byref(t))
+        return {f: getattr(t, f) for f, _ in SkvTimings._fields_}
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    load().skv_device_count(C.byref(n))
+    return n.value
