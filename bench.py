@@ -133,7 +133,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(device)
 
-    gather_ms, total_ms = [], []
+    gather_ms, total_ms, phases = [], [], []
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -141,6 +141,7 @@ def main():
         t = comp.timings()
         gather_ms.append(t["gather_ms"])
         total_ms.append(t["total_ms"])
+        phases.append([t[k] for k in ("parse_ms", "check_ms", "merge_ms", "chain_ms", "gather_ms")])
         gread, gwrite = t["gather_read_bytes"], t["gather_write_bytes"]
         out_bytes, n_out_runs = res.n_bytes, res.n_runs
         res.free()
@@ -191,6 +192,8 @@ def main():
                 "parallelism": f"{world} independent compactions (one per GPU), no collective",
             },
             "device_ms_per_compaction": round(float(np.mean(total_ms)), 4),
+            "phases_ms": dict(zip(("parse", "check", "merge", "chain", "gather"),
+                                  [round(float(x), 4) for x in np.mean(np.array(phases), axis=0)])),
             "roofline": {
                 "bound": "hbm",
                 "kernel": "k_gather",

@@ -366,6 +366,19 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
         throw ApiError{code, msg};
     }
     if (hflags[0]) throw ApiError{SKV_E_UNSUPPORTED, "record of 2 GiB or more: unsupported by this build"};
+    if (R == 0) {  // nothing survives: build_runs yields no run (runs.rs:270-271)
+        ResultBox* box = (ResultBox*)calloc(1, sizeof(ResultBox));
+        box->pub.runs = (skv_run_desc*)malloc(sizeof(skv_run_desc));
+        box->pub.bytes = dbuf<uint8_t>(ctx, "out", 16);
+        box->pub.in_bytes = job.in_bytes;
+        mark(ctx, PH_MERGE);
+        mark(ctx, PH_CHAIN);
+        mark(ctx, PH_GATHER);
+        ctx->timings = skv_timings{};
+        ctx->timings.host_syncs = ctx->syncs;
+        *out = &box->pub;
+        return SKV_OK;
+    }
     if (R >= 0xFFFFFFFFull) throw ApiError{SKV_E_UNSUPPORTED, "more than 2^32-1 records in one compaction"};
 
     // ---- merge ------------------------------------------------------------------------------

@@ -847,7 +847,7 @@ __global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __res
     __shared__ uint32_t s_len[2 * GATHER_SEG];
     __shared__ uint64_t s_rb[GATHER_SEG + 2];
     __shared__ uint64_t ws[16];
-    __shared__ uint64_t s_r0, s_nrb;
+    __shared__ uint64_t s_r0;
     const uint64_t K = *Kp;
     const uint64_t j0 = (uint64_t)blockIdx.x * GATHER_SEG;
     if (j0 >= K) return;
@@ -1051,10 +1051,12 @@ void launch_bounds(hipStream_t s, bool l0, const uint64_t* hi, const uint64_t* l
                    const uint64_t* sc, uint64_t m, uint64_t T, const uint64_t* rec_addr, uint64_t* bounds) {
     Elems E{hi, lo, c, klen};
     uint64_t n = (T + 1) * k;
+    if (!n) return;
     if (l0) k_bounds<true><<<blocks_for(n, 256), 256, 0, s>>>(E, off, k, shi, slo, sc, m, T, rec_addr, bounds);
     else k_bounds<false><<<blocks_for(n, 256), 256, 0, s>>>(E, off, k, shi, slo, sc, m, T, rec_addr, bounds);
 }
 void launch_tile_n(hipStream_t s, const uint64_t* bounds, uint32_t k, uint64_t T, uint64_t* tile_n) {
+    if (!T) return;
     k_tile_n<<<blocks_for(T, 256), 256, 0, s>>>(bounds, k, T, tile_n);
 }
 size_t tile_lds_bytes(uint32_t k) {

@@ -26,6 +26,10 @@ KiB, MiB = 1 << 10, 1 << 20
 
 @pytest.fixture(scope="module")
 def dev():
+    # torch bundles its own HIP runtime under the same SONAME; initialise it first so that
+    # libskv.so binds to that one runtime instead of loading a second copy.
+    torch = pytest.importorskip("torch")
+    torch.cuda.init()
     c = Compactor(0, profiling=True)
     yield c
     c.close()
