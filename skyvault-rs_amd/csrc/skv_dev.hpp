@@ -46,6 +46,11 @@ struct RunInfo {
     uint32_t stream;      // stream rank (seq_no descending)
 };
 
+struct RunFmt {           // fixed-stride hypothesis of a run (S == 0: none)
+    uint64_t S;           // record size
+    uint32_t K, V;        // key / value length
+};
+
 struct RunSummary {       // per run, read back by the host after the parse
     uint64_t records;     // records decoded before the first error of the run
     uint32_t err;         // DERR_* | extra << 8 (0 = none)
@@ -203,6 +208,187 @@ __device__ __forceinline__ uint4 load16_unaligned(const uint8_t* p) {
     o.z = __builtin_amdgcn_alignbyte(s[3], s[2], r);
     o.w = __builtin_amdgcn_alignbyte(s[4], s[3], r);
     return o;
+}
+
+// bytes [sh, sh+16) of the 32-byte little-endian concatenation x|y (sh in 0..15)
+__device__ __forceinline__ uint4 funnel16(uint4 x, uint4 y, uint32_t sh) {
+    if (sh == 0) return x;
+    uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+    uint32_t q = sh >> 2, r = sh & 3;
+    uint32_t s[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        uint32_t v3 = (i + 3 < 8) ? w[i + 3] : 0u;
+        s[i] = q == 0 ? w[i] : (q == 1 ? w[i + 1] : (q == 2 ? w[i + 2] : v3));
+    }
+    uint4 o;
+    o.x = __builtin_amdgcn_alignbyte(s[1], s[0], r);
+    o.y = __builtin_amdgcn_alignbyte(s[2], s[1], r);
+    o.z = __builtin_amdgcn_alignbyte(s[3], s[2], r);
+    o.w = __builtin_amdgcn_alignbyte(s[4], s[3], r);
+    return o;
+}
+
+// bytes [p, p+n) (1 <= n <= 16) at bytes 0..n-1 of the result (the rest unspecified). Only the
+// aligned 16-byte blocks holding a requested byte are read, so no page beyond them is touched.
+__device__ __forceinline__ uint4 load_window16(const uint8_t* p, uint32_t n) {
+    uintptr_t a = (uintptr_t)p;
+    const uint4* b0 = (const uint4*)(a & ~(uintptr_t)15);
+    uint32_t sh = (uint32_t)(a & 15);
+    uint4 x = b0[0];
+    uint4 y = make_uint4(0, 0, 0, 0);
+    if (sh + n > 16) y = b0[1];
+    return funnel16(x, y, sh);
+}
+
+// move byte j to j + a (a in 0..15), zero fill
+__device__ __forceinline__ uint4 shl_bytes(uint4 w, uint32_t a) {
+    return a ? funnel16(make_uint4(0, 0, 0, 0), w, 16 - a) : w;
+}
+
+__device__ __forceinline__ uint32_t dword_mask(uint32_t a, uint32_t b, uint32_t i) {
+    uint32_t lo = a > 4 * i ? a : 4 * i, hi = b < 4 * i + 4 ? b : 4 * i + 4;
+    if (lo >= hi) return 0u;
+    uint64_t m = ((1ull << (8 * (hi - lo))) - 1) << (8 * (lo - 4 * i));
+    return (uint32_t)m;
+}
+
+// ---- vectorized record headers --------------------------------------------------------------
+
+// 32 bytes at run+p into w[0..7] (bytes at or past run+len read as zero). Only aligned 16-byte
+// blocks holding a byte below run+len are loaded.
+__device__ __forceinline__ void window32(const uint8_t* run, uint64_t len, uint64_t p, uint32_t w[8]) {
+    uintptr_t a = (uintptr_t)(run + p);
+    uintptr_t end = (uintptr_t)(run + len);
+    uintptr_t base = a & ~(uintptr_t)15;
+    uint32_t sh = (uint32_t)(a & 15);
+    const uint4* b = (const uint4*)base;
+    uint4 z = make_uint4(0, 0, 0, 0);
+    uint4 b0 = b[0];
+    uint4 b1 = base + 16 < end ? b[1] : z;
+    uint4 b2 = (sh && base + 32 < end) ? b[2] : z;
+    uint4 lo = funnel16(b0, b1, sh), hi = funnel16(b1, b2, sh);
+    w[0] = lo.x; w[1] = lo.y; w[2] = lo.z; w[3] = lo.w;
+    w[4] = hi.x; w[5] = hi.y; w[6] = hi.z; w[7] = hi.w;
+    // zero bytes at or past the run end (the window may extend past it)
+    if (p + 32 > len) {
+        uint32_t valid = (uint32_t)(len - p);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] &= dword_mask(0, valid, i) | (4u * i + 4 <= valid ? 0xFFFFFFFFu : 0u);
+    }
+}
+
+__device__ __forceinline__ uint32_t sel8(const uint32_t w[8], uint32_t i) {
+    uint32_t r = w[0];
+#pragma unroll
+    for (uint32_t k = 1; k < 8; ++k) r = i == k ? w[k] : r;
+    return i < 8 ? r : 0u;
+}
+
+// big-endian u32 at byte offset o (o <= 28) of the window
+__device__ __forceinline__ uint32_t win_be32(const uint32_t w[8], uint32_t o) {
+    uint32_t q = o >> 2, r = o & 3;
+    return __builtin_bswap32(__builtin_amdgcn_alignbyte(sel8(w, q + 1), sel8(w, q), r));
+}
+
+// key bytes 5.. of the window as 7 dwords (28 bytes), little-endian byte order
+__device__ __forceinline__ void win_key(const uint32_t w[8], uint32_t kd[7]) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) kd[i] = __builtin_amdgcn_alignbyte(i + 2 < 8 ? w[i + 2] : 0u, w[i + 1], 1);
+}
+
+__device__ __forceinline__ bool ascii_prefix(const uint32_t kd[7], uint32_t n /* <= 28 */) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 7; ++i) acc |= kd[i] & dword_mask(0, n, i);
+    return (acc & 0x80808080u) == 0;
+}
+
+// UTF-8 validity with an all-ASCII vector fast path (16 bytes per step)
+__device__ inline bool utf8_valid_fast(const uint8_t* s, uint64_t n) {
+    for (uint64_t i = 0; i < n; i += 16) {
+        uint32_t m = (uint32_t)(n - i < 16 ? n - i : 16);
+        uint4 v = load_window16(s + i, m);
+        uint32_t acc = (v.x & dword_mask(0, m, 0)) | (v.y & dword_mask(0, m, 1)) | (v.z & dword_mask(0, m, 2)) |
+                       (v.w & dword_mask(0, m, 3));
+        if (acc & 0x80808080u) return utf8_valid(s, n);
+    }
+    return true;
+}
+
+// 16-byte big-endian key prefix from the window's key dwords, zero past klen
+__device__ __forceinline__ void win_prefix(const uint32_t kd[7], uint64_t klen, uint64_t& hi, uint64_t& lo) {
+    uint32_t n = klen < 16 ? (uint32_t)klen : 16u;
+    uint32_t d0 = kd[0] & dword_mask(0, n, 0), d1 = kd[1] & dword_mask(0, n, 1);
+    uint32_t d2 = kd[2] & dword_mask(0, n, 2), d3 = kd[3] & dword_mask(0, n, 3);
+    hi = ((uint64_t)__builtin_bswap32(d0) << 32) | __builtin_bswap32(d1);
+    lo = ((uint64_t)__builtin_bswap32(d2) << 32) | __builtin_bswap32(d3);
+}
+
+struct RecHdr {
+    uint32_t marker;
+    uint32_t err;    // DERR_* | extra << 8
+    uint64_t klen;
+    uint64_t size;
+    uint64_t hi, lo; // key prefix
+};
+
+// One record of runs::read_run_stream (runs.rs:559-626) at p, checks in the reference's order,
+// from one 32-byte window plus (only for long keys / non-ASCII keys) further loads.
+template <bool PREFIX>
+__device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, uint64_t p) {
+    RecHdr h;
+    h.size = 0;
+    h.hi = h.lo = 0;
+    uint32_t w[8];
+    window32(run, len, p, w);
+    h.marker = w[0] & 0xFFu;
+    if (p + 5 > len) { h.err = DERR_IO; h.klen = 0; return h; }
+    h.klen = __builtin_bswap32(__builtin_amdgcn_alignbyte(w[1], w[0], 1));
+    const uint64_t kp = p + 5;
+    if (kp + h.klen > len) { h.err = DERR_KEY; return h; }
+    uint32_t kd[7];
+    win_key(w, kd);
+    bool ok = h.klen <= 27 && ascii_prefix(kd, (uint32_t)h.klen);
+    if (!ok) ok = utf8_valid_fast(run + kp, h.klen);
+    if (!ok) { h.err = DERR_UTF8; return h; }
+    if (PREFIX) win_prefix(kd, h.klen, h.hi, h.lo);
+    if (h.marker == 1) {
+        if (kp + h.klen + 4 > len) { h.err = DERR_IO; return h; }
+        uint64_t vo = 5 + h.klen;
+        uint64_t vlen;
+        if (vo + 4 <= 32) vlen = win_be32(w, (uint32_t)vo);
+        else {
+            uint4 v = load_window16(run + p + vo, 4);
+            vlen = __builtin_bswap32(v.x);
+        }
+        if (kp + h.klen + 4 + vlen > len) { h.err = DERR_VAL; return h; }
+        h.size = 9 + h.klen + vlen;
+    } else if (h.marker == 2) {
+        h.size = 5 + h.klen;
+    } else {
+        h.err = DERR_MARKER | (h.marker << 8);
+        return h;
+    }
+    h.err = DERR_NONE;
+    return h;
+}
+
+// walk_checked with vectorized headers: one dependent round trip per record
+__device__ inline WalkRes walk_fast(const uint8_t* run, uint64_t len, uint64_t p, uint64_t stop, uint32_t max_recs) {
+    uint32_t cnt = 0;
+    while (p < stop && cnt < max_recs) {
+        RecHdr h = parse_rec<false>(run, len, p);
+        if (h.err) return {p, cnt, h.err};
+        ++cnt;
+        p += h.size;
+    }
+    return {p, cnt, DERR_NONE};
+}
+
+__device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t k) {
+    uint32_t d = (k >> 2) == 0 ? v.x : ((k >> 2) == 1 ? v.y : ((k >> 2) == 2 ? v.z : v.w));
+    return (d >> (8 * (k & 3))) & 0xFFu;
 }
 
 #endif  // __HIPCC__

@@ -20,44 +20,7 @@
 #include "../../include/skv.h"
 #include "skv_dev.hpp"
 
-namespace skv {
-void launch_run_header(hipStream_t, const RunInfo*, uint32_t, uint32_t*);
-void launch_spec(hipStream_t, const RunInfo*, uint32_t, uint64_t, const uint32_t*, uint64_t*, uint64_t*, uint32_t*,
-                 uint32_t*);
-void launch_validate(hipStream_t, const RunInfo*, uint32_t, uint64_t, const uint32_t*, const uint64_t*, const uint64_t*,
-                     const uint32_t*, unsigned long long*, uint32_t*);
-void launch_fixup(hipStream_t, const RunInfo*, uint32_t, const uint32_t*, const uint32_t*, const unsigned long long*,
-                  uint64_t*, uint64_t*, uint32_t*, uint32_t*);
-void launch_err_chunk(hipStream_t, const RunInfo*, uint32_t, uint64_t, const uint32_t*, const uint32_t*, uint32_t*);
-void launch_mask(hipStream_t, const RunInfo*, uint32_t, uint64_t, const uint32_t*, const uint32_t*, const uint32_t*,
-                 uint64_t*);
-void launch_run_summary(hipStream_t, const RunInfo*, uint32_t, const uint32_t*, const uint32_t*, const uint32_t*,
-                        const uint64_t*, RunSummary*);
-void launch_emit(hipStream_t, const RunInfo*, uint32_t, uint64_t, const uint64_t*, const uint64_t*, uint64_t*, uint64_t*,
-                 uint64_t*, uint32_t*, uint32_t*, uint32_t*);
-void launch_order_check(hipStream_t, uint64_t, const uint64_t*, uint32_t, const uint64_t*, const uint64_t*,
-                        const uint64_t*, const uint32_t*, unsigned long long*, uint32_t*);
-void launch_sample(hipStream_t, bool, const uint64_t*, const uint64_t*, const uint64_t*, const uint32_t*, const uint64_t*,
-                   const uint64_t*, uint32_t, uint64_t, uint64_t, uint64_t*, uint64_t*, uint64_t*);
-void launch_bounds(hipStream_t, bool, const uint64_t*, const uint64_t*, const uint64_t*, const uint32_t*,
-                   const uint64_t*, uint32_t, const uint64_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t,
-                   const uint64_t*, uint64_t*);
-void launch_tile_n(hipStream_t, const uint64_t*, uint32_t, uint64_t, uint64_t*);
-
-hipError_t launch_tile(hipStream_t, bool, const uint64_t*, const uint64_t*, const uint64_t*, const uint32_t*,
-                       const uint64_t*, uint32_t, uint64_t, const uint64_t*, const uint32_t*, const uint64_t*, uint32_t,
-                       TileOut);
-void launch_finalize(hipStream_t, uint64_t, const uint64_t*, const uint64_t*, const uint64_t*, const uint64_t*,
-                     const uint64_t*, const uint32_t*, const uint32_t*, const uint64_t*, uint32_t*, uint64_t*, uint64_t*,
-                     uint64_t*, uint32_t*);
-void launch_chain(hipStream_t, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
-void launch_run_stats(hipStream_t, const uint64_t*, const uint64_t*, const uint64_t*, const uint64_t*, const uint32_t*,
-                      const uint32_t*, DevRunDesc*, uint64_t);
-void launch_gather(hipStream_t, const uint64_t*, const uint64_t*, const uint64_t*, const uint64_t*, const uint64_t*,
-                   uint8_t*, uint64_t);
-uint64_t scan_tmp_words(uint64_t);
-void launch_scan(hipStream_t, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
-}  // namespace skv
+#include "skv_launch.hpp"
 
 using namespace skv;
 
@@ -242,14 +205,18 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     HIPCHK(hipMemsetAsync(bad_bits, 0, (n_chunks / 64 + 1) * 8, st));
     HIPCHK(hipMemsetAsync(first_bad, 0xFF, n_runs * 4, st));
     HIPCHK(hipMemsetAsync(err_chunk, 0xFF, n_runs * 4, st));
-    launch_run_header(st, d_runs, n_runs, d_hdr);
-    launch_spec(st, d_runs, n_runs, n_chunks, d_hdr, ch_start, ch_end, ch_cnt, ch_err);
+    RunFmt* d_fmt = dbuf<RunFmt>(ctx, "run_fmt", n_runs);
+    uint32_t* d_broken = dbuf<uint32_t>(ctx, "run_broken", n_runs);
+    uint64_t* d_recb = dbuf<uint64_t>(ctx, "run_recb", n_runs + 1);
+    HIPCHK(hipMemsetAsync(d_broken, 0, (size_t)n_runs * 4, st));
+    launch_run_header(st, d_runs, n_runs, d_hdr, d_fmt);
+    launch_spec(st, d_runs, n_runs, n_chunks, d_hdr, d_fmt, d_broken, ch_start, ch_end, ch_cnt, ch_err);
     launch_validate(st, d_runs, n_runs, n_chunks, d_hdr, ch_start, ch_end, ch_err, bad_bits, first_bad);
     launch_fixup(st, d_runs, n_runs, d_hdr, first_bad, bad_bits, ch_start, ch_end, ch_cnt, ch_err);
     launch_err_chunk(st, d_runs, n_runs, n_chunks, d_hdr, ch_err, err_chunk);
     launch_mask(st, d_runs, n_runs, n_chunks, d_hdr, err_chunk, ch_cnt, cnt64);
     launch_scan(st, cnt64, n_chunks, ch_rec_base, scan_tmp);
-    launch_run_summary(st, d_runs, n_runs, d_hdr, err_chunk, ch_err, ch_rec_base, d_sum);
+    launch_run_summary(st, d_runs, n_runs, d_hdr, err_chunk, ch_err, ch_rec_base, d_sum, d_recb);
     HIPCHK(hipGetLastError());
 
     std::vector<RunSummary> sum(n_runs);
@@ -300,7 +267,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     HIPCHK(hipMemsetAsync(d_flags, 0, 16, st));
     HIPCHK(hipMemsetAsync(d_first_dec, 0xFF, (size_t)k * 8, st));
     h2d(ctx, d_stream_base, stream_base.data(), (k + 1) * 8);
-    launch_emit(st, d_runs, n_runs, n_chunks, ch_start, ch_rec_base, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
+    launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
                 d_flags);
     mark(ctx, PH_PARSE);
     launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
@@ -499,7 +466,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     uint64_t* run_b = dbuf<uint64_t>(ctx, "run_b", R + 2);
     uint64_t* d_nruns = dbuf<uint64_t>(ctx, "n_runs", 2);
     DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", R + 1);
-    launch_chain(st, d_K, m_P, job.max_run_size, run_b, d_nruns);
+    launch_chain(st, d_K, m_P, job.max_run_size, max_rec, run_b, d_nruns);
     launch_run_stats(st, d_nruns, run_b, m_P, m_Dp, m_rec, rec_klen, d_desc, R);
     mark(ctx, PH_CHAIN);
     // ---- gather -----------------------------------------------------------------------------

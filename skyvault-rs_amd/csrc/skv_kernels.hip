@@ -13,7 +13,7 @@
 //
 // Everything is integer/byte work: no MFMA. The HBM-bound kernel is k_gather (reads the
 // surviving input records once, writes the output once, 16-byte vector stores).
-#include "skv_dev.hpp"
+#include "skv_launch.hpp"
 
 namespace skv {
 
@@ -82,47 +82,67 @@ __device__ __forceinline__ uint32_t find_run(const RunInfo* runs, uint32_t n_run
 // ---------------------------------------------------------------------------------------
 // parse: run headers (runs.rs:537-556)
 
-__global__ void k_run_header(const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err) {
+// Header checks (runs.rs:537-556) and the run's fixed-stride hypothesis: when the first record is
+// a Put of size S and the body is a whole number of S-byte records, every chunk can verify its
+// records at their predicted positions with independent loads (k_spec), and the records can be
+// emitted one thread per record (k_emit_fixed). The hypothesis is verified record by record.
+__global__ void k_run_header(const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err, RunFmt* fmt) {
     uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_runs) return;
     RunInfo R = runs[r];
     uint32_t e = 0;
+    RunFmt f{0, 0, 0};
+    const uint8_t* run = (const uint8_t*)R.ptr;
     if (R.len == 0) e = DERR_EMPTY;
     else {
-        uint32_t v = ((const uint8_t*)R.ptr)[0];
+        uint32_t v = run[0];
         if (v != 1) e = DERR_VERSION | (v << 8);
-    }
-    hdr_err[r] = e;
-}
-
-// Speculative start of chunk `local` (> 0): a record start must lie in [cs, ce). Try the
-// position a fixed record stride predicts, then scan for the first position whose next three
-// records decode cleanly. Wrong guesses are caught by k_validate and repaired by k_fixup.
-__device__ uint64_t spec_start(const uint8_t* run, uint64_t len, uint64_t cs, uint64_t ce) {
-    WalkRes f = walk_checked(run, len, 1, len, 1);
-    if (f.err == DERR_NONE && f.cnt == 1) {
-        uint64_t S = f.end - 1;
-        uint64_t p0 = 1 + ((cs - 1 + S - 1) / S) * S;
-        if (p0 < ce) {
-            uint32_t m = run[p0];
-            if (m == 1 || m == 2) {
-                WalkRes w = walk_checked(run, len, p0, len, 3);
-                if (w.err == DERR_NONE) return p0;
+        else if (R.len >= 2) {
+            RecHdr h = parse_rec<false>(run, R.len, 1);
+            if (!h.err && h.marker == 1 && (R.len - 1) % h.size == 0 && h.klen <= 0xFFFFFFFFu) {
+                f.S = h.size;
+                f.K = (uint32_t)h.klen;
+                f.V = (uint32_t)(h.size - 9 - h.klen);
             }
         }
     }
+    hdr_err[r] = e;
+    fmt[r] = f;
+}
+
+// Speculative start of chunk `local` (> 0): a record start must lie in [cs, ce). Scan for the
+// first position whose next three records decode cleanly. Wrong guesses are caught by
+// k_validate and repaired by k_fixup.
+__device__ uint64_t spec_start(const uint8_t* run, uint64_t len, uint64_t cs, uint64_t ce) {
     for (uint64_t p = cs; p < ce; ++p) {
         uint32_t m = run[p];
         if (m != 1 && m != 2) continue;
-        WalkRes w = walk_checked(run, len, p, len, 3);
+        WalkRes w = walk_fast(run, len, p, len, 3);
         if (w.err == DERR_NONE) return p;
     }
     return NO_POS;
 }
 
+__device__ __forceinline__ bool fixed_rec_ok(const uint8_t* run, uint64_t len, uint64_t q, const RunFmt& f) {
+    uint32_t w[8];
+    window32(run, len, q, w);
+    if ((w[0] & 0xFFu) != 1u) return false;
+    uint32_t klen = __builtin_bswap32(__builtin_amdgcn_alignbyte(w[1], w[0], 1));
+    if (klen != f.K) return false;
+    uint32_t kd[7];
+    win_key(w, kd);
+    bool ok = f.K <= 27 ? ascii_prefix(kd, f.K) : false;
+    if (!ok && !utf8_valid_fast(run + q + 5, f.K)) return false;
+    uint32_t vo = 5 + f.K;
+    uint32_t vlen;
+    if (vo + 4 <= 32) vlen = win_be32(w, vo);
+    else vlen = __builtin_bswap32(load_window16(run + q + vo, 4).x);
+    return vlen == f.V;
+}
+
 __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
-                       const uint32_t* __restrict__ hdr_err, uint64_t* ch_start, uint64_t* ch_end,
-                       uint32_t* ch_cnt, uint32_t* ch_err) {
+                       const uint32_t* __restrict__ hdr_err, const RunFmt* __restrict__ fmt, uint32_t* run_broken,
+                       uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err) {
     uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
     uint32_t r = find_run(runs, n_runs, c);
@@ -138,7 +158,41 @@ __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         ch_err[c] = 0;
         return;
     }
-    uint64_t start = local == 0 ? 1 : spec_start(run, R.len, cs, ce);
+    uint64_t start;
+    const RunFmt f = fmt[r];
+    if (f.S) {
+        // fixed stride: the records starting in this chunk sit at p0, p0+S, ...; verify each with
+        // independent loads (no dependent walk)
+        const uint64_t S = f.S;
+        const uint64_t p0 = 1 + ((cs - 1 + S - 1) / S) * S;
+        if (p0 >= ce) {
+            ch_start[c] = p0;
+            ch_end[c] = p0;
+            ch_cnt[c] = 0;
+            ch_err[c] = 0;
+            return;
+        }
+        const uint64_t n = (ce - p0 + S - 1) / S;
+        bool ok = true;
+        for (uint64_t i = 0; i < n; i += 4) {
+            bool o0 = fixed_rec_ok(run, R.len, p0 + i * S, f);
+            bool o1 = i + 1 < n ? fixed_rec_ok(run, R.len, p0 + (i + 1) * S, f) : true;
+            bool o2 = i + 2 < n ? fixed_rec_ok(run, R.len, p0 + (i + 2) * S, f) : true;
+            bool o3 = i + 3 < n ? fixed_rec_ok(run, R.len, p0 + (i + 3) * S, f) : true;
+            ok = ok && o0 && o1 && o2 && o3;
+        }
+        if (ok) {
+            ch_start[c] = p0;
+            ch_end[c] = p0 + n * S;
+            ch_cnt[c] = (uint32_t)n;
+            ch_err[c] = 0;
+            return;
+        }
+        atomicOr(&run_broken[r], 1u);  // hypothesis broken: this run takes the general path
+        start = p0;
+    } else {
+        start = local == 0 ? 1 : spec_start(run, R.len, cs, ce);
+    }
     if (start == NO_POS) {
         ch_start[c] = NO_POS;
         ch_end[c] = NO_POS;
@@ -146,7 +200,7 @@ __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         ch_err[c] = 0;
         return;
     }
-    WalkRes w = walk_checked(run, R.len, start, ce, 0xFFFFFFFFu);
+    WalkRes w = walk_fast(run, R.len, start, ce, 0xFFFFFFFFu);
     ch_start[c] = start;
     ch_end[c] = w.end;
     ch_cnt[c] = w.cnt;
@@ -205,7 +259,7 @@ __global__ void k_fixup(const RunInfo* __restrict__ runs, uint32_t n_runs, const
         uint64_t end = E;
         uint32_t cnt = 0, err = 0;
         if (E < ce) {
-            WalkRes w = walk_checked(run, R.len, E, ce, 0xFFFFFFFFu);
+            WalkRes w = walk_fast(run, R.len, E, ce, 0xFFFFFFFFu);
             end = w.end;
             cnt = w.cnt;
             err = w.err;
@@ -245,7 +299,7 @@ __global__ void k_mask(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
 
 __global__ void k_run_summary(const RunInfo* __restrict__ runs, uint32_t n_runs, const uint32_t* __restrict__ hdr_err,
                               const uint32_t* __restrict__ run_err_chunk, const uint32_t* __restrict__ ch_err,
-                              const uint64_t* __restrict__ ch_rec_base, RunSummary* out) {
+                              const uint64_t* __restrict__ ch_rec_base, RunSummary* out, uint64_t* run_recb) {
     uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_runs) return;
     RunInfo R = runs[r];
@@ -255,10 +309,25 @@ __global__ void k_run_summary(const RunInfo* __restrict__ runs, uint32_t n_runs,
     s.err = hdr_err[r] ? hdr_err[r] : (ec != NO_POS32 ? ch_err[R.chunk_base + ec] : 0u);
     s.pad = 0;
     out[r] = s;
+    run_recb[r] = ch_rec_base[R.chunk_base];
+    if (r == n_runs - 1) run_recb[n_runs] = ch_rec_base[R.chunk_base + R.n_chunks];
 }
 
-// Emit the record arrays for every validated chunk: address, 16 B key prefix, key length, meta.
+__device__ __forceinline__ void put_rec(uint64_t o, const uint8_t* rp, const RecHdr& h, uint64_t* rec_addr,
+                                        uint64_t* rec_hi, uint64_t* rec_lo, uint32_t* rec_klen, uint32_t* rec_meta,
+                                        uint32_t* flags) {
+    rec_addr[o] = (uint64_t)rp;
+    rec_hi[o] = h.hi;
+    rec_lo[o] = h.lo;
+    rec_klen[o] = (uint32_t)h.klen;
+    if (h.size >= (1ull << 31)) atomicOr(flags, 1u);  // record too large for this build
+    rec_meta[o] = (uint32_t)h.size | (h.marker == 2 ? 0x80000000u : 0u);
+}
+
+// Emit the record arrays (address, 16 B key prefix, key length, meta) of every validated chunk of
+// the runs that are not fixed-stride: walk from the chunk's validated start.
 __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
+                       const RunFmt* __restrict__ fmt, const uint32_t* __restrict__ run_broken,
                        const uint64_t* __restrict__ ch_start, const uint64_t* __restrict__ ch_rec_base,
                        uint64_t* __restrict__ rec_addr, uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
                        uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags) {
@@ -267,24 +336,37 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
     uint64_t b0 = ch_rec_base[c], cnt = ch_rec_base[c + 1] - b0;
     if (!cnt) return;
     uint32_t r = find_run(runs, n_runs, c);
+    if (fmt[r].S && !run_broken[r]) return;  // k_emit_fixed
     const uint8_t* run = (const uint8_t*)runs[r].ptr;
+    const uint64_t len = runs[r].len;
     uint64_t p = ch_start[c];
     for (uint64_t i = 0; i < cnt; ++i) {
-        const uint8_t* rp = run + p;
-        uint32_t marker = rp[0];
-        uint64_t klen = ld_be32(rp + 1);
-        uint64_t size = marker == 1 ? 9 + klen + ld_be32(rp + 5 + klen) : 5 + klen;
-        uint64_t hi, lo;
-        key_prefix(rp + 5, klen, hi, lo);
-        uint64_t o = b0 + i;
-        rec_addr[o] = (uint64_t)rp;
-        rec_hi[o] = hi;
-        rec_lo[o] = lo;
-        rec_klen[o] = (uint32_t)klen;
-        if (size >= (1ull << 31)) atomicOr(flags, 1u);  // record too large for this build
-        rec_meta[o] = (uint32_t)size | (marker == 2 ? 0x80000000u : 0u);
-        p += size;
+        RecHdr h = parse_rec<true>(run, len, p);
+        put_rec(b0 + i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
+        p += h.size;
     }
+}
+
+// Fixed-stride runs: one thread per record at 1 + i*S (coalesced stores, independent loads).
+__global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t R_total,
+                             const RunFmt* __restrict__ fmt, const uint32_t* __restrict__ run_broken,
+                             const uint64_t* __restrict__ run_recb, uint64_t* __restrict__ rec_addr,
+                             uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
+                             uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R_total) return;
+    uint32_t lo = 0, hi = n_runs;  // last run with run_recb <= i
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (run_recb[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    const RunFmt f = fmt[lo];
+    if (!f.S || run_broken[lo]) return;
+    const uint8_t* run = (const uint8_t*)runs[lo].ptr;
+    uint64_t p = 1 + (i - run_recb[lo]) * f.S;
+    RecHdr h = parse_rec<true>(run, runs[lo].len, p);
+    put_rec(i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -701,12 +783,16 @@ __global__ void __launch_bounds__(1024) k_finalize(uint64_t T, const uint64_t* _
             m_Dp[g + i] = pd + ed;
             mx = (uint32_t)sz > mx ? (uint32_t)sz : mx;
         }
-        g += 0;
         pb += tb;
         pd += td;
-        (void)0;
     }
-    if (mx) atomicMax(max_rec, mx);
+    // largest surviving record: one atomic per workgroup, not per thread
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        uint32_t o = __shfl_xor(mx, d, 64);
+        mx = o > mx ? o : mx;
+    }
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(max_rec, mx);
     if (t == T - 1 && threadIdx.x == 0) {
         m_P[kept_base[t] + n] = pb;
         m_Dp[kept_base[t] + n] = pd;
@@ -727,80 +813,115 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     return v;
 }
 
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        uint64_t o = __shfl_xor(v, d, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+// largest e in [lo, hi] with P[e] <= v, given P[lo] <= v (64-ary search, exact)
+__device__ uint64_t chain_search(const uint64_t* P, uint64_t lo, uint64_t hi, uint64_t v, int lane) {
+    while (lo < hi) {
+        uint64_t span = hi - lo;
+        uint64_t step = (span + 63) / 64;
+        uint64_t pos = lo + (uint64_t)(lane + 1) * step;
+        if (pos > hi) pos = hi;
+        bool f = P[pos] <= v;
+        uint64_t nlo = wave_max_u64(f ? pos : lo);
+        uint64_t gtpos = wave_min_u64(f ? ~0ull : pos);
+        lo = nlo;
+        if (gtpos != ~0ull) hi = gtpos - 1;
+        if (step == 1) break;
+    }
+    return lo;
+}
+
+constexpr int CH_D = 8;  // predicted windows in flight
+constexpr int CH_Q = 4;  // entries per lane per window (256 per window)
+
 __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ P,
-                                              uint64_t max_size, uint64_t* run_b, uint64_t* n_runs_out) {
+                                              uint64_t max_size, const uint32_t* __restrict__ max_rec,
+                                              uint64_t* run_b, uint64_t* n_runs_out) {
     const uint64_t K = *Kp;
     const int lane = threadIdx.x;
     if (K == 0) {
         if (lane == 0) { run_b[0] = 0; *n_runs_out = 0; }
         return;
     }
+    // every record fits a run on its own when 1 + largest record <= max: no oversize probe
+    const bool all_fit = max_size >= 1 && (uint64_t)(*max_rec) + 1 <= max_size;
     uint64_t b = 0, m = 0;
     uint64_t Pb = P[0];
-    const uint64_t total = P[K];
     uint64_t L = 1;
     if (max_size > 1) {
-        uint64_t avg = total / K;
+        uint64_t avg = P[K] / K;
         if (avg == 0) avg = 1;
         L = (max_size - 1) / avg;
         if (L == 0) L = 1;
+        if (L > K) L = K;
     }
     while (b < K) {
-        uint64_t e;
-        if (max_size == 0 || P[b + 1] - Pb + 1 > max_size) {
-            e = b + 1;  // the first record never splits: a run of one oversized record
-        } else {
-            const uint64_t v = Pb + max_size - 1;  // record j fits iff P[j+1] <= v
-            // window of 256 positions around b + L
-            uint64_t ws = b + L > 128 ? b + L - 128 : 0;
-            if (ws < b + 1) ws = b + 1;
-            uint64_t best = 0;
-            bool any_gt = false;
-            for (int q = 0; q < 4; ++q) {
-                uint64_t pos = ws + (uint64_t)lane * 4 + q;
-                if (pos <= K) {
-                    uint64_t pv = P[pos];
-                    if (pv <= v) best = pos > best ? pos : best;
-                    else any_gt = true;
-                }
-            }
-            best = wave_max_u64(best);
-            bool gt = __any(any_gt);
-            uint64_t wend = ws + 256;  // exclusive
-            bool ok = best >= ws && (best == K || (gt && best + 1 < wend));
-            if (ok) {
-                e = best;
-            } else {
-                // 64-ary search on [lo, hi]: P[lo] <= v holds for lo = b+1
-                uint64_t lo = b + 1, hi = K;
-                while (lo < hi) {
-                    uint64_t span = hi - lo;
-                    uint64_t step = (span + 63) / 64;
-                    uint64_t pos = lo + (uint64_t)(lane + 1) * step;
-                    if (pos > hi) pos = hi;
-                    bool f = P[pos] <= v;
-                    uint64_t cand = f ? pos : lo;
-                    uint64_t nlo = wave_max_u64(cand);
-                    // smallest probed position with P > v bounds hi
-                    uint64_t gtpos = f ? ~0ull : pos;
+        // prefetch CH_D windows of P around the predicted ends of the next CH_D runs
+        uint64_t wv[CH_D][CH_Q];
+        uint64_t wsd[CH_D];
 #pragma unroll
-                    for (int d = 32; d >= 1; d >>= 1) {
-                        uint64_t o = __shfl_xor(gtpos, d, 64);
-                        gtpos = o < gtpos ? o : gtpos;
-                    }
-                    lo = nlo;
-                    if (gtpos != ~0ull) hi = gtpos - 1;
-                    if (step == 1) break;
-                }
-                e = lo;
+        for (int d = 0; d < CH_D; ++d) {
+            uint64_t c = b + (uint64_t)(d + 1) * L;
+            uint64_t ws = c > 128 ? c - 128 : 0;
+            if (ws < b + 1) ws = b + 1;
+            wsd[d] = ws;
+#pragma unroll
+            for (int q = 0; q < CH_Q; ++q) {
+                uint64_t pos = ws + (uint64_t)lane * CH_Q + q;
+                wv[d][q] = pos <= K ? P[pos] : ~0ull;
             }
-            uint64_t len = e - b;
-            L = len;
         }
-        if (lane == 0) run_b[m] = b;
-        ++m;
-        b = e;
-        Pb = P[b];
+#pragma unroll
+        for (int d = 0; d < CH_D; ++d) {
+            if (b >= K) break;
+            uint64_t e, Pe;
+            if (max_size == 0 || (!all_fit && P[b + 1] - Pb + 1 > max_size)) {
+                e = b + 1;  // a run of one record that alone exceeds max (runs.rs:219 needs !first)
+                Pe = P[e];
+            } else {
+                const uint64_t v = Pb + max_size - 1;  // record j fits iff P[j+1] <= v
+                const uint64_t ws = wsd[d];
+                uint64_t best = 0;
+                bool any_le = false, any_gt = false;
+#pragma unroll
+                for (int q = 0; q < CH_Q; ++q) {
+                    uint64_t pos = ws + (uint64_t)lane * CH_Q + q;
+                    bool valid = pos >= b + 1 && pos <= K;
+                    if (valid && wv[d][q] <= v) { best = pos; any_le = true; }
+                    if (valid && wv[d][q] > v) any_gt = true;
+                }
+                best = wave_max_u64(any_le ? best : 0);
+                bool le = __any(any_le), gt = __any(any_gt);
+                if (le && (gt || best == K)) {
+                    e = best;
+                    uint64_t idx = e - ws;
+                    int src = (int)(idx / CH_Q);
+                    uint32_t qq = (uint32_t)(idx % CH_Q);
+                    uint64_t v0 = __shfl(wv[d][0], src, 64), v1 = __shfl(wv[d][1], src, 64);
+                    uint64_t v2 = __shfl(wv[d][2], src, 64), v3 = __shfl(wv[d][3], src, 64);
+                    Pe = qq == 0 ? v0 : (qq == 1 ? v1 : (qq == 2 ? v2 : v3));
+                } else {
+                    uint64_t lo = b + 1, hi = K;
+                    if (le) lo = best;            // window all <= v: answer at or past its end
+                    else if (ws > b + 1) hi = ws - 1;  // window all > v: answer before it
+                    e = chain_search(P, lo, hi, v, lane);
+                    Pe = P[e];
+                }
+            }
+            if (lane == 0) run_b[m] = b;
+            ++m;
+            L = e - b;
+            b = e;
+            Pb = Pe;
+        }
     }
     if (lane == 0) {
         run_b[m] = K;
@@ -924,20 +1045,29 @@ __global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __res
             *(uint4*)(out + B) = v;
             continue;
         }
-        uint32_t w[4] = {0, 0, 0, 0};
-        for (uint64_t x = x0; x < x1; ++x) {
-            while (s_dst[p] + s_len[p] <= x) ++p;
-            uint32_t byte = s_src[p] ? ((const uint8_t*)s_src[p])[x - s_dst[p]] : 1u;
-            uint32_t k = (uint32_t)(x - B);
-            if (full) {
-#pragma unroll
-                for (int wi = 0; wi < 4; ++wi)
-                    if ((k >> 2) == (uint32_t)wi) w[wi] |= byte << (8 * (k & 3));
-            } else {
-                out[x] = (uint8_t)byte;
-            }
+        // block spans several pieces: each contributes bytes [a, b) of the block, moved with at
+        // most two aligned 16-byte loads and merged under a byte mask
+        uint4 acc = make_uint4(0, 0, 0, 0);
+        uint64_t x = x0;
+        while (x < x1) {
+            const uint64_t d = s_dst[p];
+            const uint64_t src = s_src[p];
+            const uint64_t e = d + s_len[p] < x1 ? d + s_len[p] : x1;
+            const uint32_t a = (uint32_t)(x - B), b = (uint32_t)(e - B);
+            uint4 w = src ? load_window16((const uint8_t*)src + (x - d), b - a) : make_uint4(1u, 0, 0, 0);
+            w = shl_bytes(w, a);
+            acc.x |= w.x & dword_mask(a, b, 0);
+            acc.y |= w.y & dword_mask(a, b, 1);
+            acc.z |= w.z & dword_mask(a, b, 2);
+            acc.w |= w.w & dword_mask(a, b, 3);
+            x = e;
+            ++p;
         }
-        if (full) *(uint4*)(out + B) = make_uint4(w[0], w[1], w[2], w[3]);
+        if (full) {
+            *(uint4*)(out + B) = acc;
+        } else {  // block shared with a neighbouring workgroup: write only this segment's bytes
+            for (uint64_t y = x0; y < x1; ++y) out[y] = (uint8_t)byte_of(acc, (uint32_t)(y - B));
+        }
     }
 }
 
@@ -989,12 +1119,15 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(const uint64_t* in,
 
 static inline unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
-void launch_run_header(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err) {
-    if (n_runs) k_run_header<<<blocks_for(n_runs, 256), 256, 0, s>>>(runs, n_runs, hdr_err);
+void launch_run_header(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err, RunFmt* fmt) {
+    if (n_runs) k_run_header<<<blocks_for(n_runs, 256), 256, 0, s>>>(runs, n_runs, hdr_err, fmt);
 }
 void launch_spec(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
-                 uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err) {
-    if (n_chunks) k_spec<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, ch_start, ch_end, ch_cnt, ch_err);
+                 const RunFmt* fmt, uint32_t* run_broken, uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt,
+                 uint32_t* ch_err) {
+    if (n_chunks)
+        k_spec<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, fmt, run_broken, ch_start,
+                                                         ch_end, ch_cnt, ch_err);
 }
 void launch_validate(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                      const uint64_t* ch_start, const uint64_t* ch_end, const uint32_t* ch_err,
@@ -1020,16 +1153,21 @@ void launch_mask(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n
 }
 void launch_run_summary(hipStream_t s, const RunInfo* runs, uint32_t n_runs, const uint32_t* hdr_err,
                         const uint32_t* run_err_chunk, const uint32_t* ch_err, const uint64_t* ch_rec_base,
-                        RunSummary* out) {
+                        RunSummary* out, uint64_t* run_recb) {
     if (n_runs)
-        k_run_summary<<<blocks_for(n_runs, 256), 256, 0, s>>>(runs, n_runs, hdr_err, run_err_chunk, ch_err, ch_rec_base, out);
+        k_run_summary<<<blocks_for(n_runs, 256), 256, 0, s>>>(runs, n_runs, hdr_err, run_err_chunk, ch_err, ch_rec_base,
+                                                              out, run_recb);
 }
-void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint64_t* ch_start,
-                 const uint64_t* ch_rec_base, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
+void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const RunFmt* fmt,
+                 const uint32_t* run_broken, const uint64_t* ch_start, const uint64_t* ch_rec_base,
+                 const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                  uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags) {
     if (n_chunks)
-        k_emit<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, ch_start, ch_rec_base, rec_addr, rec_hi,
-                                                         rec_lo, rec_klen, rec_meta, flags);
+        k_emit<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, fmt, run_broken, ch_start, ch_rec_base,
+                                                         rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
+    if (R)
+        k_emit_fixed<<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, R, fmt, run_broken, run_recb, rec_addr, rec_hi,
+                                                        rec_lo, rec_klen, rec_meta, flags);
 }
 void launch_order_check(hipStream_t s, uint64_t R, const uint64_t* stream_base, uint32_t k, const uint64_t* rec_addr,
                         const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,
@@ -1085,9 +1223,9 @@ void launch_finalize(hipStream_t s, uint64_t T, const uint64_t* tile_base, const
     k_finalize<<<(unsigned)T, 1024, 0, s>>>(T, tile_base, tile_kept, kept_base, byte_base, del_base, t_rec, t_meta,
                                               rec_addr, m_rec, m_src, m_P, m_Dp, max_rec);
 }
-void launch_chain(hipStream_t s, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, uint64_t* run_b,
-                  uint64_t* n_runs) {
-    k_chain<<<1, 64, 0, s>>>(Kp, P, max_size, run_b, n_runs);
+void launch_chain(hipStream_t s, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, const uint32_t* max_rec,
+                  uint64_t* run_b, uint64_t* n_runs) {
+    k_chain<<<1, 64, 0, s>>>(Kp, P, max_size, max_rec, run_b, n_runs);
 }
 void launch_run_stats(hipStream_t s, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
                       const uint64_t* Dp, const uint32_t* m_rec, const uint32_t* rec_klen, DevRunDesc* descs,

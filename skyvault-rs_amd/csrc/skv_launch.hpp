@@ -1,0 +1,54 @@
+// skv_launch.hpp — host-side launch wrappers of skv_kernels.hip (declarations shared by both TUs)
+#pragma once
+#include "skv_dev.hpp"
+
+namespace skv {
+void launch_run_header(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err, RunFmt* fmt);
+void launch_spec(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
+                 const RunFmt* fmt, uint32_t* run_broken, uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt,
+                 uint32_t* ch_err);
+void launch_validate(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
+                     const uint64_t* ch_start, const uint64_t* ch_end, const uint32_t* ch_err,
+                     unsigned long long* bad_bits, uint32_t* run_first_bad);
+void launch_fixup(hipStream_t, const RunInfo* runs, uint32_t n_runs, const uint32_t* hdr_err,
+                  const uint32_t* run_first_bad, const unsigned long long* bad_bits, uint64_t* ch_start,
+                  uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err);
+void launch_err_chunk(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
+                      const uint32_t* ch_err, uint32_t* run_err_chunk);
+void launch_mask(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
+                 const uint32_t* run_err_chunk, const uint32_t* ch_cnt, uint64_t* cnt64);
+void launch_run_summary(hipStream_t, const RunInfo* runs, uint32_t n_runs, const uint32_t* hdr_err,
+                        const uint32_t* run_err_chunk, const uint32_t* ch_err, const uint64_t* ch_rec_base,
+                        RunSummary* out, uint64_t* run_recb);
+void launch_emit(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const RunFmt* fmt,
+                 const uint32_t* run_broken, const uint64_t* ch_start, const uint64_t* ch_rec_base,
+                 const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
+                 uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags);
+void launch_order_check(hipStream_t, uint64_t R, const uint64_t* stream_base, uint32_t k, const uint64_t* rec_addr,
+                        const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,
+                        unsigned long long* first_dec, uint32_t* any_dec);
+void launch_sample(hipStream_t, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
+                   const uint32_t* klen, const uint64_t* off_src, const uint64_t* off_dst, uint32_t k, uint64_t S,
+                   uint64_t n_dst, uint64_t* dhi, uint64_t* dlo, uint64_t* dc);
+void launch_bounds(hipStream_t, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
+                   const uint32_t* klen, const uint64_t* off, uint32_t k, const uint64_t* shi, const uint64_t* slo,
+                   const uint64_t* sc, uint64_t m, uint64_t T, const uint64_t* rec_addr, uint64_t* bounds);
+void launch_tile_n(hipStream_t, const uint64_t* bounds, uint32_t k, uint64_t T, uint64_t* tile_n);
+size_t tile_lds_bytes(uint32_t k);
+hipError_t launch_tile(hipStream_t, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
+                       const uint32_t* klen, const uint64_t* bounds, uint32_t k, uint64_t T, const uint64_t* tile_base,
+                       const uint32_t* rec_meta, const uint64_t* rec_addr, uint32_t drop, TileOut O);
+void launch_finalize(hipStream_t, uint64_t T, const uint64_t* tile_base, const uint64_t* tile_kept,
+                     const uint64_t* kept_base, const uint64_t* byte_base, const uint64_t* del_base, const uint32_t* t_rec,
+                     const uint32_t* t_meta, const uint64_t* rec_addr, uint32_t* m_rec, uint64_t* m_src, uint64_t* m_P,
+                     uint64_t* m_Dp, uint32_t* max_rec);
+void launch_chain(hipStream_t, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, const uint32_t* max_rec,
+                  uint64_t* run_b, uint64_t* n_runs);
+void launch_run_stats(hipStream_t, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
+                      const uint64_t* Dp, const uint32_t* m_rec, const uint32_t* rec_klen, DevRunDesc* descs,
+                      uint64_t max_runs);
+void launch_gather(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
+                   const uint64_t* m_src, uint8_t* out, uint64_t max_K);
+uint64_t scan_tmp_words(uint64_t n);
+void launch_scan(hipStream_t, const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tmp);
+}  // namespace skv
