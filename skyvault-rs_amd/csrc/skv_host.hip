@@ -452,13 +452,9 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     uint64_t* m_src = dbuf<uint64_t>(ctx, "m_src", R + 1);
     uint64_t* m_P = dbuf<uint64_t>(ctx, "m_P", R + 1);
     uint64_t* m_Dp = dbuf<uint64_t>(ctx, "m_Dp", R + 1);
-    uint32_t* max_rec = d_flags + 2;
-    if (R == 0) {
-        HIPCHK(hipMemsetAsync(m_P, 0, 8, st));
-        HIPCHK(hipMemsetAsync(m_Dp, 0, 8, st));
-    }
+    uint32_t* tile_max = dbuf<uint32_t>(ctx, "tile_max", T0);
     launch_finalize(st, T0, d_tile_base0, O0.tile_kept, kept_base, byte_base, del_base, O0.t_rec, O0.t_meta, rec_addr,
-                    m_rec, m_src, m_P, m_Dp, max_rec);
+                    m_rec, m_src, m_P, m_Dp, tile_max);
     HIPCHK(hipGetLastError());
     mark(ctx, PH_MERGE);
     // ---- chain + stats ----------------------------------------------------------------------
@@ -466,15 +462,16 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     uint64_t* run_b = dbuf<uint64_t>(ctx, "run_b", R + 2);
     uint64_t* d_nruns = dbuf<uint64_t>(ctx, "n_runs", 2);
     DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", R + 1);
-    launch_chain(st, d_K, m_P, job.max_run_size, max_rec, run_b, d_nruns);
-    launch_run_stats(st, d_nruns, run_b, m_P, m_Dp, m_rec, rec_klen, d_desc, R);
+    uint64_t* seg_r0 = dbuf<uint64_t>(ctx, "seg_r0", R / GATHER_SEG + 2);
+    launch_chain(st, d_K, m_P, job.max_run_size, tile_max, T0, run_b, d_nruns);
+    launch_run_stats(st, d_nruns, run_b, m_P, m_Dp, m_rec, rec_klen, d_desc, seg_r0, R);
     mark(ctx, PH_CHAIN);
     // ---- gather -----------------------------------------------------------------------------
     uint64_t total_rec_bytes = 0;
     for (const InStream& S : job.ranked)
         for (uint64_t l : S.lens) total_rec_bytes += l;
     uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + R + 16);
-    launch_gather(st, d_K, d_nruns, run_b, m_P, m_src, d_out, R);
+    launch_gather(st, d_K, d_nruns, run_b, m_P, m_src, seg_r0, d_out, R);
     HIPCHK(hipGetLastError());
     mark(ctx, PH_GATHER);
     // ---- readback ---------------------------------------------------------------------------

@@ -786,13 +786,19 @@ __global__ void __launch_bounds__(1024) k_finalize(uint64_t T, const uint64_t* _
         pb += tb;
         pd += td;
     }
-    // largest surviving record: one atomic per workgroup, not per thread
+    // largest surviving record of the tile (no global atomics: k_chain reduces the tiles)
+    __shared__ uint32_t wmax[16];
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         uint32_t o = __shfl_xor(mx, d, 64);
         mx = o > mx ? o : mx;
     }
-    if ((threadIdx.x & 63) == 0 && mx) atomicMax(max_rec, mx);
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) mx = wmax[w] > mx ? wmax[w] : mx;
+        max_rec[t] = mx;
+    }
     if (t == T - 1 && threadIdx.x == 0) {
         m_P[kept_base[t] + n] = pb;
         m_Dp[kept_base[t] + n] = pd;
@@ -839,20 +845,34 @@ __device__ uint64_t chain_search(const uint64_t* P, uint64_t lo, uint64_t hi, ui
     return lo;
 }
 
-constexpr int CH_D = 8;  // predicted windows in flight
-constexpr int CH_Q = 4;  // entries per lane per window (256 per window)
+constexpr int CH_D = 16;  // predicted windows in flight
+constexpr int CH_Q = 4;   // entries per lane per window (256 per window)
+
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
+    uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+    uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
 
 __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ P,
-                                              uint64_t max_size, const uint32_t* __restrict__ max_rec,
-                                              uint64_t* run_b, uint64_t* n_runs_out) {
+                                              uint64_t max_size, const uint32_t* __restrict__ tile_max,
+                                              uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs_out) {
     const uint64_t K = *Kp;
     const int lane = threadIdx.x;
     if (K == 0) {
         if (lane == 0) { run_b[0] = 0; *n_runs_out = 0; }
         return;
     }
+    // largest surviving record (per-tile maxima from k_finalize)
+    uint32_t mr = 0;
+    for (uint64_t t = lane; t < n_tiles; t += 64) mr = tile_max[t] > mr ? tile_max[t] : mr;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        uint32_t o = __shfl_xor(mr, d, 64);
+        mr = o > mr ? o : mr;
+    }
     // every record fits a run on its own when 1 + largest record <= max: no oversize probe
-    const bool all_fit = max_size >= 1 && (uint64_t)(*max_rec) + 1 <= max_size;
+    const bool all_fit = max_size >= 1 && (uint64_t)mr + 1 <= max_size;
     uint64_t b = 0, m = 0;
     uint64_t Pb = P[0];
     uint64_t L = 1;
@@ -881,36 +901,35 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
         }
 #pragma unroll
         for (int d = 0; d < CH_D; ++d) {
-            if (b >= K) break;
-            uint64_t e, Pe;
+            if (b < K) {  // (no break: keeps the loop fully unrolled, windows in registers)
+            uint64_t e, Pe = 0;
             if (max_size == 0 || (!all_fit && P[b + 1] - Pb + 1 > max_size)) {
                 e = b + 1;  // a run of one record that alone exceeds max (runs.rs:219 needs !first)
                 Pe = P[e];
             } else {
                 const uint64_t v = Pb + max_size - 1;  // record j fits iff P[j+1] <= v
                 const uint64_t ws = wsd[d];
+                // predicate P[pos] <= v is monotone in pos = ws + 4*lane + q: the last true
+                // position is found from four wave ballots with scalar bit ops
+                const uint64_t m0 = __ballot(wv[d][0] <= v), m1 = __ballot(wv[d][1] <= v);
+                const uint64_t m2 = __ballot(wv[d][2] <= v), m3 = __ballot(wv[d][3] <= v);
+                bool found = false;
                 uint64_t best = 0;
-                bool any_le = false, any_gt = false;
-#pragma unroll
-                for (int q = 0; q < CH_Q; ++q) {
-                    uint64_t pos = ws + (uint64_t)lane * CH_Q + q;
-                    bool valid = pos >= b + 1 && pos <= K;
-                    if (valid && wv[d][q] <= v) { best = pos; any_le = true; }
-                    if (valid && wv[d][q] > v) any_gt = true;
+                if (m0) {
+                    const int ls = 63 - __builtin_clzll(m0);
+                    const uint32_t qs = (uint32_t)((m1 >> ls) & 1) + (uint32_t)((m2 >> ls) & 1) + (uint32_t)((m3 >> ls) & 1);
+                    best = ws + (uint64_t)ls * CH_Q + qs;
+                    found = best == K || best < ws + CH_Q * 64 - 1;
+                    if (found) {
+                        uint64_t x = qs == 0 ? wv[d][0] : (qs == 1 ? wv[d][1] : (qs == 2 ? wv[d][2] : wv[d][3]));
+                        Pe = readlane_u64(x, ls);
+                    }
                 }
-                best = wave_max_u64(any_le ? best : 0);
-                bool le = __any(any_le), gt = __any(any_gt);
-                if (le && (gt || best == K)) {
+                if (found) {
                     e = best;
-                    uint64_t idx = e - ws;
-                    int src = (int)(idx / CH_Q);
-                    uint32_t qq = (uint32_t)(idx % CH_Q);
-                    uint64_t v0 = __shfl(wv[d][0], src, 64), v1 = __shfl(wv[d][1], src, 64);
-                    uint64_t v2 = __shfl(wv[d][2], src, 64), v3 = __shfl(wv[d][3], src, 64);
-                    Pe = qq == 0 ? v0 : (qq == 1 ? v1 : (qq == 2 ? v2 : v3));
                 } else {
                     uint64_t lo = b + 1, hi = K;
-                    if (le) lo = best;            // window all <= v: answer at or past its end
+                    if (m0) lo = best;                 // window all <= v: answer at or past its end
                     else if (ws > b + 1) hi = ws - 1;  // window all > v: answer before it
                     e = chain_search(P, lo, hi, v, lane);
                     Pe = P[e];
@@ -921,6 +940,7 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
             L = e - b;
             b = e;
             Pb = Pe;
+            }
         }
     }
     if (lane == 0) {
@@ -932,10 +952,12 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
 __global__ void k_run_stats(const uint64_t* __restrict__ n_runs_p, const uint64_t* __restrict__ run_b,
                             const uint64_t* __restrict__ P, const uint64_t* __restrict__ Dp,
                             const uint32_t* __restrict__ m_rec, const uint32_t* __restrict__ rec_klen,
-                            DevRunDesc* descs) {
+                            DevRunDesc* descs, uint64_t* seg_r0) {
     const uint64_t n_runs = *n_runs_p;
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_runs; r += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t b = run_b[r], e = run_b[r + 1];
+        // gather segments whose first record lies in this run
+        for (uint64_t sg = (b + GATHER_SEG - 1) / GATHER_SEG; sg * GATHER_SEG < e; ++sg) seg_r0[sg] = r;
         DevRunDesc d;
         d.off = P[b] + r;
         d.len = 1 + P[e] - P[b];
@@ -958,33 +980,63 @@ __global__ void k_run_stats(const uint64_t* __restrict__ n_runs_p, const uint64_
 // 16-byte aligned output blocks with one vector store; blocks shared with a neighbouring
 // workgroup (segment edges) are written bytewise.
 
+// last piece whose destination starts at or before x
+__device__ __forceinline__ uint32_t gather_piece(const uint64_t* s_dst, uint32_t npieces, uint64_t x) {
+    uint32_t lo = 0, hi = npieces;
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (s_dst[mid] <= x) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// An output block covering several pieces: each piece contributes bytes [a, b) of the block,
+// moved with at most two aligned 16-byte loads and merged under a byte mask. Blocks shared
+// with a neighbouring workgroup (segment edges) are written bytewise, only this segment's bytes.
+__device__ __noinline__ void gather_block_slow(uint64_t B, uint64_t x0, uint64_t x1, uint32_t p,
+                                               const uint64_t* s_dst, const uint64_t* s_src, const uint32_t* s_len,
+                                               uint8_t* out) {
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    uint64_t x = x0;
+    while (x < x1) {
+        const uint64_t d = s_dst[p];
+        const uint64_t src = s_src[p];
+        const uint64_t e = d + s_len[p] < x1 ? d + s_len[p] : x1;
+        const uint32_t a = (uint32_t)(x - B), b = (uint32_t)(e - B);
+        uint4 w = src ? load_window16((const uint8_t*)src + (x - d), b - a) : make_uint4(1u, 0, 0, 0);
+        w = shl_bytes(w, a);
+        acc.x |= w.x & dword_mask(a, b, 0);
+        acc.y |= w.y & dword_mask(a, b, 1);
+        acc.z |= w.z & dword_mask(a, b, 2);
+        acc.w |= w.w & dword_mask(a, b, 3);
+        x = e;
+        ++p;
+    }
+    if (x0 == B && x1 == B + 16) {
+        *(uint4*)(out + B) = acc;
+    } else {
+        for (uint64_t y = x0; y < x1; ++y) out[y] = (uint8_t)byte_of(acc, (uint32_t)(y - B));
+    }
+}
+
 __global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __restrict__ Kp,
                                                            const uint64_t* __restrict__ n_runs_p,
                                                            const uint64_t* __restrict__ run_b,
                                                            const uint64_t* __restrict__ P,
-                                                           const uint64_t* __restrict__ m_src, uint8_t* __restrict__ out) {
+                                                           const uint64_t* __restrict__ m_src,
+                                                           const uint64_t* __restrict__ seg_r0, uint8_t* __restrict__ out) {
     __shared__ uint64_t s_dst[2 * GATHER_SEG];
     __shared__ uint64_t s_src[2 * GATHER_SEG];  // 0 => version byte
     __shared__ uint32_t s_len[2 * GATHER_SEG];
     __shared__ uint64_t s_rb[GATHER_SEG + 2];
     __shared__ uint64_t ws[16];
-    __shared__ uint64_t s_r0;
     const uint64_t K = *Kp;
     const uint64_t j0 = (uint64_t)blockIdx.x * GATHER_SEG;
     if (j0 >= K) return;
     const uint64_t j1 = j0 + GATHER_SEG < K ? j0 + GATHER_SEG : K;
     const uint64_t n_runs = *n_runs_p;
-    if (threadIdx.x == 0) {
-        uint64_t lo = 0, hi = n_runs;  // last run with run_b <= j0
-        while (hi - lo > 1) {
-            uint64_t mid = (lo + hi) >> 1;
-            if (run_b[mid] <= j0) lo = mid;
-            else hi = mid;
-        }
-        s_r0 = lo;
-    }
-    __syncthreads();
-    const uint64_t r0 = s_r0;
+    const uint64_t r0 = seg_r0[blockIdx.x];  // run holding record j0 (k_run_stats)
     // run starts r0 .. r0+nrb-1 that are <= j1-1
     for (uint32_t i = threadIdx.x; i < GATHER_SEG + 1; i += blockDim.x) {
         uint64_t r = r0 + i;
@@ -1022,51 +1074,27 @@ __global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __res
     const uint64_t lo_b = s_dst[0];
     const uint64_t hi_b = s_dst[npieces - 1] + s_len[npieces - 1];
     const uint64_t q0 = lo_b >> 4, q1 = (hi_b + 15) >> 4;
-    uint32_t hint = 0;
-    for (uint64_t q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
-        const uint64_t B = q << 4;
-        const uint64_t x0 = B > lo_b ? B : lo_b;
-        const uint64_t x1 = B + 16 < hi_b ? B + 16 : hi_b;
-        // piece containing x0
-        uint32_t p;
-        {
-            uint32_t lo = 0, hi = npieces;
-            while (hi - lo > 1) {
-                uint32_t mid = (lo + hi) >> 1;
-                if (s_dst[mid] <= x0) lo = mid;
-                else hi = mid;
-            }
-            p = lo;
-        }
-        (void)hint;
-        const bool full = x0 == B && x1 == B + 16;
-        if (full && s_src[p] != 0 && s_dst[p] + s_len[p] >= B + 16) {
-            uint4 v = load16_unaligned((const uint8_t*)s_src[p] + (B - s_dst[p]));
-            *(uint4*)(out + B) = v;
-            continue;
-        }
-        // block spans several pieces: each contributes bytes [a, b) of the block, moved with at
-        // most two aligned 16-byte loads and merged under a byte mask
-        uint4 acc = make_uint4(0, 0, 0, 0);
-        uint64_t x = x0;
-        while (x < x1) {
-            const uint64_t d = s_dst[p];
-            const uint64_t src = s_src[p];
-            const uint64_t e = d + s_len[p] < x1 ? d + s_len[p] : x1;
-            const uint32_t a = (uint32_t)(x - B), b = (uint32_t)(e - B);
-            uint4 w = src ? load_window16((const uint8_t*)src + (x - d), b - a) : make_uint4(1u, 0, 0, 0);
-            w = shl_bytes(w, a);
-            acc.x |= w.x & dword_mask(a, b, 0);
-            acc.y |= w.y & dword_mask(a, b, 1);
-            acc.z |= w.z & dword_mask(a, b, 2);
-            acc.w |= w.w & dword_mask(a, b, 3);
-            x = e;
-            ++p;
-        }
-        if (full) {
-            *(uint4*)(out + B) = acc;
-        } else {  // block shared with a neighbouring workgroup: write only this segment's bytes
-            for (uint64_t y = x0; y < x1; ++y) out[y] = (uint8_t)byte_of(acc, (uint32_t)(y - B));
+    const uint32_t step = blockDim.x;
+    for (uint64_t qa = q0 + threadIdx.x; qa < q1; qa += 2 * step) {
+        // two output blocks per lane per iteration: both locate their piece and issue their
+        // loads before either stores
+        const uint64_t qb = qa + step;
+        const bool hb = qb < q1;
+        const uint64_t Ba = qa << 4, Bb = qb << 4;
+        const uint64_t xa0 = Ba > lo_b ? Ba : lo_b, xa1 = Ba + 16 < hi_b ? Ba + 16 : hi_b;
+        const uint64_t xb0 = Bb > lo_b ? Bb : lo_b, xb1 = Bb + 16 < hi_b ? Bb + 16 : hi_b;
+        const uint32_t pa = gather_piece(s_dst, npieces, xa0);
+        const uint32_t pb = hb ? gather_piece(s_dst, npieces, xb0) : 0;
+        const bool fa = xa0 == Ba && xa1 == Ba + 16 && s_src[pa] != 0 && s_dst[pa] + s_len[pa] >= Ba + 16;
+        const bool fb = hb && xb0 == Bb && xb1 == Bb + 16 && s_src[pb] != 0 && s_dst[pb] + s_len[pb] >= Bb + 16;
+        uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
+        if (fa) va = load16_unaligned((const uint8_t*)s_src[pa] + (Ba - s_dst[pa]));
+        if (fb) vb = load16_unaligned((const uint8_t*)s_src[pb] + (Bb - s_dst[pb]));
+        if (fa) *(uint4*)(out + Ba) = va;
+        else gather_block_slow(Ba, xa0, xa1, pa, s_dst, s_src, s_len, out);
+        if (hb) {
+            if (fb) *(uint4*)(out + Bb) = vb;
+            else gather_block_slow(Bb, xb0, xb1, pb, s_dst, s_src, s_len, out);
         }
     }
 }
@@ -1223,21 +1251,21 @@ void launch_finalize(hipStream_t s, uint64_t T, const uint64_t* tile_base, const
     k_finalize<<<(unsigned)T, 1024, 0, s>>>(T, tile_base, tile_kept, kept_base, byte_base, del_base, t_rec, t_meta,
                                               rec_addr, m_rec, m_src, m_P, m_Dp, max_rec);
 }
-void launch_chain(hipStream_t s, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, const uint32_t* max_rec,
-                  uint64_t* run_b, uint64_t* n_runs) {
-    k_chain<<<1, 64, 0, s>>>(Kp, P, max_size, max_rec, run_b, n_runs);
+void launch_chain(hipStream_t s, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, const uint32_t* tile_max,
+                  uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs) {
+    k_chain<<<1, 64, 0, s>>>(Kp, P, max_size, tile_max, n_tiles, run_b, n_runs);
 }
 void launch_run_stats(hipStream_t s, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
                       const uint64_t* Dp, const uint32_t* m_rec, const uint32_t* rec_klen, DevRunDesc* descs,
-                      uint64_t max_runs) {
+                      uint64_t* seg_r0, uint64_t max_runs) {
     unsigned blocks = blocks_for(max_runs ? max_runs : 1, 256);
     if (blocks > 4096) blocks = 4096;
-    k_run_stats<<<blocks, 256, 0, s>>>(n_runs, run_b, P, Dp, m_rec, rec_klen, descs);
+    k_run_stats<<<blocks, 256, 0, s>>>(n_runs, run_b, P, Dp, m_rec, rec_klen, descs, seg_r0);
 }
 void launch_gather(hipStream_t s, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
-                   const uint64_t* m_src, uint8_t* out, uint64_t max_K) {
+                   const uint64_t* m_src, const uint64_t* seg_r0, uint8_t* out, uint64_t max_K) {
     if (!max_K) return;
-    k_gather<<<blocks_for(max_K, GATHER_SEG), GATHER_THREADS, 0, s>>>(Kp, n_runs, run_b, P, m_src, out);
+    k_gather<<<blocks_for(max_K, GATHER_SEG), GATHER_THREADS, 0, s>>>(Kp, n_runs, run_b, P, m_src, seg_r0, out);
 }
 // exclusive scan of n u64 values into out[0..n] (out[n] = total); tmp needs scan_tmp_words(n)
 uint64_t scan_tmp_words(uint64_t n) {

@@ -42,13 +42,13 @@ void launch_finalize(hipStream_t, uint64_t T, const uint64_t* tile_base, const u
                      const uint64_t* kept_base, const uint64_t* byte_base, const uint64_t* del_base, const uint32_t* t_rec,
                      const uint32_t* t_meta, const uint64_t* rec_addr, uint32_t* m_rec, uint64_t* m_src, uint64_t* m_P,
                      uint64_t* m_Dp, uint32_t* max_rec);
-void launch_chain(hipStream_t, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, const uint32_t* max_rec,
-                  uint64_t* run_b, uint64_t* n_runs);
+void launch_chain(hipStream_t, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, const uint32_t* tile_max,
+                  uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs);
 void launch_run_stats(hipStream_t, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
                       const uint64_t* Dp, const uint32_t* m_rec, const uint32_t* rec_klen, DevRunDesc* descs,
-                      uint64_t max_runs);
+                      uint64_t* seg_r0, uint64_t max_runs);
 void launch_gather(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
-                   const uint64_t* m_src, uint8_t* out, uint64_t max_K);
+                   const uint64_t* m_src, const uint64_t* seg_r0, uint8_t* out, uint64_t max_K);
 uint64_t scan_tmp_words(uint64_t n);
 void launch_scan(hipStream_t, const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tmp);
 }  // namespace skv
