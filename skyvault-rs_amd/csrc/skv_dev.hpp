@@ -22,6 +22,7 @@ constexpr int TILE_TARGET = 2048;         // target elements per merge tile
 constexpr int TILE_THREADS = 1024;
 constexpr int GATHER_SEG = 256;           // surviving records per gather workgroup
 constexpr int GATHER_THREADS = 256;
+constexpr int GATHER_TBL = 6144;         // output 16-byte blocks per gather workgroup with a direct piece table
 constexpr uint32_t NO_POS32 = 0xFFFFFFFFu;
 constexpr uint64_t NO_POS = ~0ull;
 

@@ -1031,12 +1031,18 @@ __global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __res
     __shared__ uint32_t s_len[2 * GATHER_SEG];
     __shared__ uint64_t s_rb[GATHER_SEG + 2];
     __shared__ uint64_t ws[16];
+    __shared__ uint16_t s_tbl[GATHER_TBL];      // output block -> piece covering its first byte
+    // XCD-aware segment order: workgroups are dealt round-robin over the 8 XCDs, so give each XCD
+    // a contiguous range of segments (neighbouring segments share input lines and one L2)
+    const uint32_t nb = gridDim.x, bid = blockIdx.x;
+    const uint32_t xcd = bid & 7, qn = nb >> 3, rn = nb & 7;
+    const uint32_t seg = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
     const uint64_t K = *Kp;
-    const uint64_t j0 = (uint64_t)blockIdx.x * GATHER_SEG;
+    const uint64_t j0 = (uint64_t)seg * GATHER_SEG;
     if (j0 >= K) return;
     const uint64_t j1 = j0 + GATHER_SEG < K ? j0 + GATHER_SEG : K;
     const uint64_t n_runs = *n_runs_p;
-    const uint64_t r0 = seg_r0[blockIdx.x];  // run holding record j0 (k_run_stats)
+    const uint64_t r0 = seg_r0[seg];  // run holding record j0 (k_run_stats)
     // run starts r0 .. r0+nrb-1 that are <= j1-1
     for (uint32_t i = threadIdx.x; i < GATHER_SEG + 1; i += blockDim.x) {
         uint64_t r = r0 + i;
@@ -1074,6 +1080,18 @@ __global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __res
     const uint64_t lo_b = s_dst[0];
     const uint64_t hi_b = s_dst[npieces - 1] + s_len[npieces - 1];
     const uint64_t q0 = lo_b >> 4, q1 = (hi_b + 15) >> 4;
+    const bool use_tbl = q1 - q0 <= GATHER_TBL;
+    if (use_tbl) {
+        // piece p covers the blocks whose first byte (lo_b for the first block, else 16q) it holds
+        for (uint32_t p = threadIdx.x; p < npieces; p += blockDim.x) {
+            const uint64_t d = s_dst[p], e = d + s_len[p];
+            uint64_t qs = (d + 15) >> 4, qe = (e + 15) >> 4;  // blocks q with 16q in [d, e)
+            if (d == lo_b) s_tbl[0] = (uint16_t)p;
+            if (qs <= q0) qs = q0 + 1;
+            for (uint64_t q = qs; q < qe; ++q) s_tbl[q - q0] = (uint16_t)p;
+        }
+        __syncthreads();
+    }
     const uint32_t step = blockDim.x;
     for (uint64_t qa = q0 + threadIdx.x; qa < q1; qa += 2 * step) {
         // two output blocks per lane per iteration: both locate their piece and issue their
@@ -1083,8 +1101,8 @@ __global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __res
         const uint64_t Ba = qa << 4, Bb = qb << 4;
         const uint64_t xa0 = Ba > lo_b ? Ba : lo_b, xa1 = Ba + 16 < hi_b ? Ba + 16 : hi_b;
         const uint64_t xb0 = Bb > lo_b ? Bb : lo_b, xb1 = Bb + 16 < hi_b ? Bb + 16 : hi_b;
-        const uint32_t pa = gather_piece(s_dst, npieces, xa0);
-        const uint32_t pb = hb ? gather_piece(s_dst, npieces, xb0) : 0;
+        const uint32_t pa = use_tbl ? s_tbl[qa - q0] : gather_piece(s_dst, npieces, xa0);
+        const uint32_t pb = hb ? (use_tbl ? s_tbl[qb - q0] : gather_piece(s_dst, npieces, xb0)) : 0;
         const bool fa = xa0 == Ba && xa1 == Ba + 16 && s_src[pa] != 0 && s_dst[pa] + s_len[pa] >= Ba + 16;
         const bool fb = hb && xb0 == Bb && xb1 == Bb + 16 && s_src[pb] != 0 && s_dst[pb] + s_len[pb] >= Bb + 16;
         uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
