@@ -1092,27 +1092,59 @@ __global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __res
         }
         __syncthreads();
     }
+    // Per output block, three cases (gfx950 serves unaligned 16-byte global loads at full rate):
+    //  (1) inside one record: one unaligned 16-byte load + one aligned store;
+    //  (2) straddling two records of >= 16 bytes: the first one's last 16 bytes and the second's
+    //      first 16 bytes (both loads stay inside their records) merged by one funnel shift;
+    //  (3) anything else (version bytes, records < 16 B, segment edges): gather_block_slow.
+    constexpr int U = 4;  // blocks per lane per iteration, loads issued before stores
     const uint32_t step = blockDim.x;
-    for (uint64_t qa = q0 + threadIdx.x; qa < q1; qa += 2 * step) {
-        // two output blocks per lane per iteration: both locate their piece and issue their
-        // loads before either stores
-        const uint64_t qb = qa + step;
-        const bool hb = qb < q1;
-        const uint64_t Ba = qa << 4, Bb = qb << 4;
-        const uint64_t xa0 = Ba > lo_b ? Ba : lo_b, xa1 = Ba + 16 < hi_b ? Ba + 16 : hi_b;
-        const uint64_t xb0 = Bb > lo_b ? Bb : lo_b, xb1 = Bb + 16 < hi_b ? Bb + 16 : hi_b;
-        const uint32_t pa = use_tbl ? s_tbl[qa - q0] : gather_piece(s_dst, npieces, xa0);
-        const uint32_t pb = hb ? (use_tbl ? s_tbl[qb - q0] : gather_piece(s_dst, npieces, xb0)) : 0;
-        const bool fa = xa0 == Ba && xa1 == Ba + 16 && s_src[pa] != 0 && s_dst[pa] + s_len[pa] >= Ba + 16;
-        const bool fb = hb && xb0 == Bb && xb1 == Bb + 16 && s_src[pb] != 0 && s_dst[pb] + s_len[pb] >= Bb + 16;
-        uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
-        if (fa) va = load16_unaligned((const uint8_t*)s_src[pa] + (Ba - s_dst[pa]));
-        if (fb) vb = load16_unaligned((const uint8_t*)s_src[pb] + (Bb - s_dst[pb]));
-        if (fa) *(uint4*)(out + Ba) = va;
-        else gather_block_slow(Ba, xa0, xa1, pa, s_dst, s_src, s_len, out);
-        if (hb) {
-            if (fb) *(uint4*)(out + Bb) = vb;
-            else gather_block_slow(Bb, xb0, xb1, pb, s_dst, s_src, s_len, out);
+    for (uint64_t q = q0 + threadIdx.x; q < q1; q += U * step) {
+        uint4 v[U];
+        uint32_t kind[U];  // 0: none, 1: store v, 2: slow
+        uint32_t pp[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t qq = q + (uint64_t)u * step;
+            kind[u] = 0;
+            pp[u] = 0;
+            v[u] = make_uint4(0, 0, 0, 0);
+            if (qq < q1) {
+                const uint64_t B = qq << 4;
+                const bool full = B >= lo_b && B + 16 <= hi_b;
+                const uint32_t p = use_tbl ? s_tbl[qq - q0] : gather_piece(s_dst, npieces, B > lo_b ? B : lo_b);
+                pp[u] = p;
+                const uint64_t d = s_dst[p], src = s_src[p];
+                const uint32_t len = s_len[p];
+                kind[u] = 2;
+                if (full && src) {
+                    if (d + len >= B + 16) {
+                        v[u] = *(const uint4*)((const uint8_t*)src + (B - d));
+                        kind[u] = 1;
+                    } else if (p + 1 < npieces && len >= 16) {
+                        const uint64_t src2 = s_src[p + 1];
+                        const uint32_t len2 = s_len[p + 1];
+                        if (src2 && len2 >= 16 && s_dst[p + 1] + len2 >= B + 16) {
+                            const uint32_t k = (uint32_t)(d + len - B);  // bytes from the first record
+                            const uint4 L = *(const uint4*)((const uint8_t*)src + len - 16);
+                            const uint4 F = *(const uint4*)((const uint8_t*)src2);
+                            v[u] = funnel16(L, F, 16 - k);
+                            kind[u] = 1;
+                        }
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t qq = q + (uint64_t)u * step;
+            if (kind[u] == 1) {
+                *(uint4*)(out + (qq << 4)) = v[u];
+            } else if (kind[u] == 2) {
+                const uint64_t B = qq << 4;
+                gather_block_slow(B, B > lo_b ? B : lo_b, B + 16 < hi_b ? B + 16 : hi_b, pp[u], s_dst, s_src, s_len,
+                                  out);
+            }
         }
     }
 }
