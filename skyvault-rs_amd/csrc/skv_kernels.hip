@@ -502,8 +502,8 @@ __global__ void k_tile_n(const uint64_t* __restrict__ bounds, uint32_t k, uint64
 
 
 
-// LDS layout of k_tile (dynamic): hi[CAP] lo[CAP] c[CAP] u64 | meta[CAP] u32 | pA[CAP] pB[CAP] u16
-// | cbA[k+1] cbB[k+1] u32 | ws[16] u64
+// LDS layout of k_tile (dynamic): el_lo[CAP] el_c[CAP] mhA[CAP] mhB[CAP] u64 | miA[CAP] miB[CAP] u16
+// | cbA[k+1] cbB[k+1] u32 | ws[16] u64 | flag
 __device__ __forceinline__ uint32_t seg_of(const uint32_t* cb, uint32_t m, uint32_t i) {
     uint32_t lo = 0, hi = m;  // last s in [0, m) with cb[s] <= i
     while (hi - lo > 1) {
@@ -514,16 +514,18 @@ __device__ __forceinline__ uint32_t seg_of(const uint32_t* cb, uint32_t m, uint3
     return lo;
 }
 
+// Output stage of an LDS tile. Position i of the merged tile: hi = mh[i], element mi[i] (its lo and
+// c in el_lo / el_c); level 0 also has meta by position in pmeta.
 template <bool L0>
-__device__ void tile_output(uint32_t n, const uint64_t* hi, const uint64_t* lo, const uint64_t* c, const uint32_t* meta,
-                            const uint16_t* perm, uint64_t base, uint64_t t, bool drop_deletes,
+__device__ void tile_output(uint32_t n, const uint64_t* mh, const uint16_t* mi, const uint64_t* el_lo,
+                            const uint64_t* el_c, const uint32_t* pmeta, uint64_t base, uint64_t t, bool drop_deletes,
                             const uint64_t* rec_addr, const TileOut& O, uint64_t* ws) {
     if (!L0) {
         for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-            uint32_t e = perm[i];
-            O.ohi[base + i] = hi[e];
-            O.olo[base + i] = lo[e];
-            O.oc[base + i] = c[e];
+            uint32_t e = mi[i];
+            O.ohi[base + i] = mh[i];
+            O.olo[base + i] = el_lo[e];
+            O.oc[base + i] = el_c[e];
         }
         return;
     }
@@ -532,22 +534,32 @@ __device__ void tile_output(uint32_t n, const uint64_t* hi, const uint64_t* lo, 
     uint32_t i0 = threadIdx.x * PER;
     uint32_t keep_mask = 0, nk = 0;
     uint64_t bytes = 0, dels = 0;
+    uint32_t idx[PER], mt[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         uint32_t i = i0 + q;
+        idx[q] = 0;
+        mt[q] = 0;
         if (i < n) {
-            uint32_t e = perm[i];
+            uint32_t e = mi[i];
+            uint64_t h = mh[i], l = el_lo[e], c = el_c[e];
             bool first = true;
             if (i > 0) {
-                uint32_t p = perm[i - 1];
-                first = ekey_cmp(rec_addr, hi[p], lo[p], c[p], hi[e], lo[e], c[e]) != 0;
+                uint64_t ph = mh[i - 1];
+                if (ph == h) {
+                    uint32_t p = mi[i - 1];
+                    first = ekey_cmp(rec_addr, ph, el_lo[p], el_c[p], h, l, c) != 0;
+                }
             }
-            bool del = (meta[e] >> 31) != 0;
+            uint32_t meta = pmeta[i];
+            bool del = (meta >> 31) != 0;
             bool keep = first && !(drop_deletes && del);
+            idx[q] = (uint32_t)c;
+            mt[q] = meta;
             if (keep) {
                 keep_mask |= 1u << q;
                 ++nk;
-                bytes += meta[e] & 0x7FFFFFFFu;
+                bytes += meta & 0x7FFFFFFFu;
                 dels += del ? 1 : 0;
             }
         }
@@ -557,9 +569,8 @@ __device__ void tile_output(uint32_t n, const uint64_t* hi, const uint64_t* lo, 
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         if (keep_mask & (1u << q)) {
-            uint32_t e = perm[i0 + q];
-            O.t_rec[base + rank] = (uint32_t)c[e];
-            O.t_meta[base + rank] = meta[e];
+            O.t_rec[base + rank] = idx[q];
+            O.t_meta[base + rank] = mt[q];
             ++rank;
         }
     }
@@ -666,13 +677,13 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                                                       const uint64_t* __restrict__ rec_addr, uint32_t drop_deletes,
                                                       TileOut O) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint64_t* s_hi = (uint64_t*)smem;
-    uint64_t* s_lo = s_hi + TILE_CAP;
-    uint64_t* s_c = s_lo + TILE_CAP;
-    uint32_t* s_meta = (uint32_t*)(s_c + TILE_CAP);
-    uint16_t* pA = (uint16_t*)(s_meta + TILE_CAP);
-    uint16_t* pB = pA + TILE_CAP;
-    uint32_t* cbA = (uint32_t*)(pB + TILE_CAP);
+    uint64_t* el_lo = (uint64_t*)smem;  // by element id (= load position)
+    uint64_t* el_c = el_lo + TILE_CAP;
+    uint64_t* mhA = el_c + TILE_CAP;  // key-hi by merged position (ping-pong)
+    uint64_t* mhB = mhA + TILE_CAP;
+    uint16_t* miA = (uint16_t*)(mhB + TILE_CAP);  // element id by merged position (ping-pong)
+    uint16_t* miB = miA + TILE_CAP;
+    uint32_t* cbA = (uint32_t*)(miB + TILE_CAP);
     uint32_t* cbB = cbA + (k + 1);
     uint64_t* ws = (uint64_t*)(((uintptr_t)(cbB + (k + 1)) + 15) & ~(uintptr_t)15);
     uint32_t* s_flag = (uint32_t*)(ws + 16);
@@ -705,53 +716,90 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         }
         return;
     }
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        uint32_t j = seg_of(cbA, k + 1, i);
-        uint64_t pos = bounds[t * k + j] + (i - cbA[j]);
-        uint64_t h, l, c;
-        load_elem<L0>(E, pos, h, l, c);
-        s_hi[i] = h;
-        s_lo[i] = l;
-        s_c[i] = c;
-        s_meta[i] = L0 ? rec_meta[pos] : 0u;
-        pA[i] = (uint16_t)i;
+    // Thread owns elements e = threadIdx.x + u*TILE_THREADS; key, position and segment stay in
+    // registers across the merge rounds, so each round is one binary search + one LDS write.
+    constexpr int PER = TILE_CAP / TILE_THREADS;
+    uint64_t rh[PER], rl[PER], rc[PER];
+    uint32_t rpos[PER], rseg[PER], rmeta[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        uint32_t e = threadIdx.x + u * TILE_THREADS;
+        rh[u] = rl[u] = rc[u] = 0;
+        rpos[u] = e;
+        rseg[u] = 0;
+        rmeta[u] = 0;
+        if (e < n) {
+            uint32_t j = seg_of(cbA, k + 1, e);
+            uint64_t pos = bounds[t * k + j] + (e - cbA[j]);
+            load_elem<L0>(E, pos, rh[u], rl[u], rc[u]);
+            if (L0) rmeta[u] = rec_meta[pos];
+            rseg[u] = j;
+            el_lo[e] = rl[u];
+            el_c[e] = rc[u];
+            mhA[e] = rh[u];
+            miA[e] = (uint16_t)e;
+        }
     }
     __syncthreads();
     // pairwise merge rounds: each element finds its rank in the partner segment
     uint32_t m = k;
     uint32_t* cb = cbA;
     uint32_t* cbn = cbB;
+    uint64_t* mh = mhA;
+    uint64_t* mhn = mhB;
+    uint16_t* mi = miA;
+    uint16_t* min_ = miB;
     while (m > 1) {
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-            uint32_t s = seg_of(cb, m + 1, i);
-            uint32_t e = pA[i];
-            uint32_t local = i - cb[s];
-            uint32_t ps = s ^ 1u;
-            uint32_t newpos;
-            if (ps >= m) {
-                newpos = i;
-            } else {
-                uint32_t a = cb[ps], b = cb[ps + 1];
-                uint64_t eh = s_hi[e], el = s_lo[e], ec = s_c[e];
-                while (a < b) {  // count partner elements < e
-                    uint32_t mid = (a + b) >> 1;
-                    uint32_t x = pA[mid];
-                    if (elem_less(rec_addr, s_hi[x], s_lo[x], s_c[x], eh, el, ec)) a = mid + 1;
-                    else b = mid;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            uint32_t e = threadIdx.x + u * TILE_THREADS;
+            if (e < n) {
+                uint32_t s = rseg[u];
+                uint32_t ps = s ^ 1u;
+                uint32_t newpos = rpos[u];
+                if (ps < m) {
+                    const uint64_t h = rh[u];
+                    uint32_t a = cb[ps], b = cb[ps + 1];
+                    const uint32_t a0 = a;
+                    while (a < b) {  // count partner elements < e
+                        uint32_t mid = (a + b) >> 1;
+                        uint64_t xh = mh[mid];
+                        bool less = xh < h;
+                        if (xh == h) {
+                            uint32_t x = mi[mid];
+                            less = elem_less(rec_addr, xh, el_lo[x], el_c[x], h, rl[u], rc[u]);
+                        }
+                        if (less) a = mid + 1;
+                        else b = mid;
+                    }
+                    newpos = cb[s & ~1u] + (rpos[u] - cb[s]) + (a - a0);
                 }
-                newpos = cb[s & ~1u] + local + (a - cb[ps]);
+                mhn[newpos] = rh[u];
+                min_[newpos] = (uint16_t)e;
+                rpos[u] = newpos;
+                rseg[u] = s >> 1;
             }
-            pB[newpos] = (uint16_t)e;
         }
         __syncthreads();
         uint32_t mn = (m + 1) >> 1;
         for (uint32_t p = threadIdx.x; p <= mn; p += blockDim.x) cbn[p] = p < mn ? cb[2 * p] : cb[m];
         __syncthreads();
-        uint16_t* tp = pA; pA = pB; pB = tp;
-        uint32_t* tc = cb; cb = cbn; cbn = tc;
+        { uint64_t* tp = mh; mh = mhn; mhn = tp; }
+        { uint16_t* tp = mi; mi = min_; min_ = tp; }
+        { uint32_t* tp = cb; cb = cbn; cbn = tp; }
         m = mn;
     }
-    tile_output<L0>(n, s_hi, s_lo, s_c, s_meta, pA, base, t, drop_deletes != 0, rec_addr, O, ws);
+    // level 0: meta by final position, in the free ping-pong buffer
+    uint32_t* pmeta = (uint32_t*)mhn;
+    if (L0) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            uint32_t e = threadIdx.x + u * TILE_THREADS;
+            if (e < n) pmeta[rpos[u]] = rmeta[u];
+        }
+        __syncthreads();
+    }
+    tile_output<L0>(n, mh, mi, el_lo, el_c, pmeta, base, t, drop_deletes != 0, rec_addr, O, ws);
 }
 
 // dense merged arrays: rec_idx, source address, output-byte prefix P, delete-count prefix
@@ -1276,7 +1324,7 @@ void launch_tile_n(hipStream_t s, const uint64_t* bounds, uint32_t k, uint64_t T
     k_tile_n<<<blocks_for(T, 256), 256, 0, s>>>(bounds, k, T, tile_n);
 }
 size_t tile_lds_bytes(uint32_t k) {
-    size_t b = (size_t)TILE_CAP * (3 * 8 + 4 + 2 + 2) + 2 * (size_t)(k + 1) * 4;
+    size_t b = (size_t)TILE_CAP * (4 * 8 + 2 + 2) + 2 * (size_t)(k + 1) * 4;
     b = (b + 15) & ~(size_t)15;
     return b + 16 * 8 + 16;
 }
