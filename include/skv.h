@@ -10,8 +10,8 @@
  *  -> runs::build_runs        (src/runs.rs:166-282)     greedy split into <= max-byte runs
  *
  * One skv_compact() call replaces that whole composition as it appears in the three
- * compaction jobs (table_buffer_compaction.rs:224-279, table_tree_compaction.rs:81-147,
- * wal_compaction.rs:207-347). The jobs keep doing everything around it (forest
+ * compaction jobs (table_buffer_compaction.rs:48-121, table_tree_compaction.rs:81-167,
+ * wal_compaction.rs:34-174). The jobs keep doing everything around it (forest
  * snapshot, get_run/put_run, metadata commit), so the Rust side binds this header through
  * a thin `extern "C"` block called from `tokio::task::spawn_blocking`.
  *
@@ -43,7 +43,7 @@ typedef struct skv_ctx skv_ctx;
  * One input stream of k_way::merge: a (SeqNo, stream) pair (k_way.rs:113). The stream is
  * the flattened concatenation of its member runs, each decoded separately by
  * read_run_stream — exactly how the jobs build their inputs (table_buffer_compaction.rs
- * :243-275 concatenates all L0 runs into one stream at SeqNo 0; table_tree_compaction.rs
+ * :67-100 concatenates all L0 runs into one stream at SeqNo 0; table_tree_compaction.rs
  * :105-135 does the same for the overlapping next-level runs). A stream with n_runs == 0
  * yields nothing (k_way.rs:138); a member run of 0 bytes yields RunError::EmptyInput.
  * seq_no values must be pairwise distinct (k_way.rs:121 keys streams by SeqNo).
@@ -69,7 +69,7 @@ typedef struct {
     uint64_t min_key_len;
     uint64_t max_key_off;  /* StatsV1.max_key = bytes[max_key_off .. +max_key_len] */
     uint64_t max_key_len;
-    int64_t table_id;      /* SKV_SPLIT_BY_TABLE: owning table (wal_compaction.rs:248-252); else 0 */
+    int64_t table_id;      /* SKV_SPLIT_BY_TABLE: owning table (wal_compaction.rs:75-79); else 0 */
     uint64_t reserved;
 } skv_run_desc;
 
@@ -83,7 +83,7 @@ typedef struct {
     uint64_t in_records;     /* records decoded from the inputs */
     uint64_t out_records;    /* records written to the output runs */
     uint64_t dropped_tables; /* SKV_SPLIT_BY_TABLE: tables whose build the reference discards
-                                (wal_compaction.rs:276, :341 swallow a failed table task) */
+                                (wal_compaction.rs:103, :168 swallow a failed table task) */
 } skv_result;
 
 /* Status codes. The first five mirror the reference's error variants. */
@@ -93,7 +93,7 @@ enum {
     SKV_E_UNSUPPORTED_VERSION = 2, /* RunError::UnsupportedVersion  (runs.rs:91, :553-556) */
     SKV_E_IO = 3,                  /* RunError::Io, UnexpectedEof   (runs.rs:85, :570-576, :598-604) */
     SKV_E_FORMAT = 4,              /* RunError::Format(..)          (runs.rs:87; :194, :581, :588, :609, :622) */
-    SKV_E_INVALID_INPUT = 5,       /* JobError::InvalidInput, WAL key (jobs/mod.rs:26; wal_compaction.rs:244-251) */
+    SKV_E_INVALID_INPUT = 5,       /* JobError::InvalidInput, WAL key (jobs/mod.rs:26; wal_compaction.rs:71-79) */
     SKV_E_INVALID_ARG = 6,         /* API misuse: NULL pointers, duplicate seq_no, bad device */
     SKV_E_DEVICE = 7,              /* HIP runtime failure or device capacity exceeded */
     SKV_E_UNSUPPORTED = 8          /* input shape outside what this build supports (message says which) */
@@ -105,7 +105,7 @@ enum {
                                 (table_tree_compaction.rs:139-145, metadata.rs:117-126) */
     SKV_SPLIT_BY_TABLE = 2   /* WAL compaction: split merged ops by "{table_id}." key prefix, strip
                                 it, one build_runs per table with the reference's exactly-one-run
-                                rule and error swallowing (wal_compaction.rs:239-347) */
+                                rule and error swallowing (wal_compaction.rs:66-174) */
 };
 
 /* Per-phase device timings of the last call (HIP events on the ctx stream), when enabled. */

@@ -181,7 +181,7 @@ static int dec_next(dec_t* d, oop* o, char* eb, size_t en) {
 
 /* ------------------------------------------------------------------------------------ */
 /* One merge input: a (SeqNo, stream) pair whose stream is the flatten of its member runs'
- * read_run_stream (table_buffer_compaction.rs:247-272, table_tree_compaction.rs:105-128).
+ * read_run_stream (table_buffer_compaction.rs:67-100, table_tree_compaction.rs:105-135).
  * The merge aborts on the first Err it pulls, so nothing past a member's error is read. */
 typedef struct {
     const skv_stream* s;
@@ -425,7 +425,7 @@ static int parse_i64(const uint8_t* s, uint64_t n, int64_t* out, const char** er
     return 1;
 }
 
-/* WAL split consumer (wal_compaction.rs:239-347). One builder per table in order of
+/* WAL split consumer (wal_compaction.rs:66-174). One builder per table in order of
  * appearance; a failing build (order error, or != 1 run) is swallowed by `if let Ok`
  * (:276, :341) and that table's data is dropped. */
 typedef struct {

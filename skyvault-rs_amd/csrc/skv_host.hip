@@ -1,7 +1,7 @@
 // skv_host.hip — C ABI (include/skv.h) and host orchestration of the MI355X compaction path.
 //
 // One skv_compact call = the decode -> merge -> [filter] -> build_runs composition of the
-// compaction jobs (table_buffer_compaction.rs:224-279, table_tree_compaction.rs:81-147). The
+// compaction jobs (table_buffer_compaction.rs:48-121, table_tree_compaction.rs:81-167). The
 // device does all per-record work; the host only sequences kernels, sizes buffers and turns
 // per-run / per-stream summaries into the reference's error (which error surfaces first is a
 // property of k_way::merge's pull order, resolved here from a handful of candidate records).
@@ -14,6 +14,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -32,8 +34,40 @@ struct DevBuf {
 
 enum Phase { PH_START = 0, PH_PARSE, PH_CHECK, PH_MERGE, PH_CHAIN, PH_GATHER, PH_N };
 
+// Pinned host buffers for skv_compact outputs. Shared by the ctx and its live results, so a
+// result may outlive its ctx; a freed result's buffer is kept for the next call.
+struct PinnedPool {
+    std::mutex mu;
+    std::vector<std::pair<void*, size_t>> free_list;
+    ~PinnedPool() {
+        for (auto& b : free_list) (void)hipHostFree(b.first);
+    }
+    void* take(size_t bytes, size_t& cap) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            for (size_t i = 0; i < free_list.size(); ++i) {
+                if (free_list[i].second >= bytes) {
+                    void* p = free_list[i].first;
+                    cap = free_list[i].second;
+                    free_list.erase(free_list.begin() + i);
+                    return p;
+                }
+            }
+        }
+        void* p = nullptr;
+        cap = std::max<size_t>(bytes, 1 << 20);
+        if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+        return p;
+    }
+    void give(void* p, size_t cap) {
+        std::lock_guard<std::mutex> g(mu);
+        free_list.emplace_back(p, cap);
+    }
+};
+
 struct skv_ctx {
     int device = 0;
+    std::shared_ptr<PinnedPool> out_pool = std::make_shared<PinnedPool>();
     hipStream_t stream = nullptr;
     std::string err;
     bool profiling = false;
@@ -47,7 +81,8 @@ struct skv_ctx {
 
 struct ResultBox {  // skv_result + how to free it
     skv_result pub;
-    int host_bytes;  // 1: bytes malloc'd by us
+    std::shared_ptr<PinnedPool> pool;  // set: bytes is a pinned host buffer of pool_cap bytes
+    size_t pool_cap = 0;
 };
 
 static int set_err(skv_ctx* ctx, int code, const char* fmt, ...) {
@@ -334,7 +369,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     }
     if (hflags[0]) throw ApiError{SKV_E_UNSUPPORTED, "record of 2 GiB or more: unsupported by this build"};
     if (R == 0) {  // nothing survives: build_runs yields no run (runs.rs:270-271)
-        ResultBox* box = (ResultBox*)calloc(1, sizeof(ResultBox));
+        ResultBox* box = new ResultBox();
         box->pub.runs = (skv_run_desc*)malloc(sizeof(skv_run_desc));
         box->pub.bytes = dbuf<uint8_t>(ctx, "out", 16);
         box->pub.in_bytes = job.in_bytes;
@@ -486,7 +521,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     const uint64_t n_out_runs = h3[0], K = h3[1];
     uint64_t kept_bytes = 0;
     HIPCHK(hipMemcpy(&kept_bytes, m_P + K, 8, hipMemcpyDeviceToHost));
-    ResultBox* box = (ResultBox*)calloc(1, sizeof(ResultBox));
+    ResultBox* box = new ResultBox();
     skv_result* res = &box->pub;
     res->runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, n_out_runs) * sizeof(skv_run_desc));
     static_assert(sizeof(skv_run_desc) == sizeof(DevRunDesc), "desc layout");
@@ -498,7 +533,6 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     res->in_records = R;
     res->out_records = K;
     res->dropped_tables = 0;
-    box->host_bytes = 0;
     if (ctx->profiling) {
         HIPCHK(hipEventSynchronize(ctx->ev[PH_GATHER]));
         float ms[PH_N] = {};
@@ -662,14 +696,21 @@ int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uin
     rc = run_guarded(ctx, job, &dres);
     if (rc) return rc;
     ResultBox* box = (ResultBox*)dres;
-    uint8_t* hb = (uint8_t*)malloc(std::max<uint64_t>(1, dres->n_bytes));
-    if (dres->n_bytes && hipMemcpy(hb, dres->bytes, dres->n_bytes, hipMemcpyDeviceToHost) != hipSuccess) {
-        free(hb);
+    size_t cap = 0;
+    uint8_t* hb = (uint8_t*)ctx->out_pool->take(std::max<uint64_t>(1, dres->n_bytes), cap);
+    if (!hb) {
+        skv_result_free(dres);
+        return set_err(ctx, SKV_E_DEVICE, "pinned host allocation of %" PRIu64 " output bytes failed", dres->n_bytes);
+    }
+    if (dres->n_bytes && (hipMemcpyAsync(hb, dres->bytes, dres->n_bytes, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+                          hipStreamSynchronize(ctx->stream) != hipSuccess)) {
+        ctx->out_pool->give(hb, cap);
         skv_result_free(dres);
         return set_err(ctx, SKV_E_DEVICE, "device-to-host copy of the output failed");
     }
     dres->bytes = hb;
-    box->host_bytes = 1;
+    box->pool = ctx->out_pool;
+    box->pool_cap = cap;
     *out = dres;
     return SKV_OK;
 }
@@ -677,9 +718,9 @@ int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uin
 void skv_result_free(skv_result* r) {
     if (!r) return;
     ResultBox* box = (ResultBox*)r;
-    if (box->host_bytes) free(r->bytes);
+    if (box->pool) box->pool->give(r->bytes, box->pool_cap);
     free(r->runs);
-    free(box);
+    delete box;
 }
 
 }  // extern "C"

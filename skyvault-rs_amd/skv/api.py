@@ -25,7 +25,7 @@ from ._abi import (
     result_to_runs,
 )
 
-MAX_RUN_SIZE = 4 * 1024 * 1024  # the jobs' build_runs limit (table_buffer_compaction.rs:279)
+MAX_RUN_SIZE = 4 * 1024 * 1024  # the jobs' build_runs limit (table_buffer_compaction.rs:103)
 
 _lib = None
 
@@ -146,6 +146,19 @@ class Compactor:
         if rc != SKV_OK:
             raise self._err(rc)
         return DeviceResult(self.lib, res)
+
+    def compact_host_ptrs(self, streams: Sequence[Tuple[int, Sequence[Tuple[int, int]]]],
+                          max_run_size: int = MAX_RUN_SIZE, flags: int = 0) -> Tuple[int, int]:
+        """skv_compact on raw host buffers (e.g. pinned tensors): [(seq_no, [(host_ptr, length)])].
+        Returns (output bytes, output runs); the pinned output is released immediately."""
+        sa = StreamArgs(streams, device=True)
+        res = C.POINTER(SkvResult)()
+        rc = self.lib.skv_compact(self.ctx, C.cast(sa.arr, C.c_void_p), sa.n, max_run_size, flags, C.byref(res))
+        if rc != SKV_OK:
+            raise self._err(rc)
+        n = (int(res.contents.n_bytes), int(res.contents.n_runs))
+        self.lib.skv_result_free(res)
+        return n
 
     def timings(self) -> dict:
         t = SkvTimings()

@@ -11,13 +11,13 @@ from typing import Dict, List, Sequence
 from ._abi import SKV_DROP_TOMBSTONES, SKV_SPLIT_BY_TABLE, OutRun
 from .api import MAX_RUN_SIZE, Compactor
 
-FAN_IN_CAP = 16  # table_buffer_compaction.rs:208, wal_compaction.rs:191
+FAN_IN_CAP = 16  # table_buffer_compaction.rs:32, wal_compaction.rs:18
 LEVEL_MAX = 6    # metadata.rs:117-126
 
 
 def table_buffer_compaction(c: Compactor, buffer: Dict[int, bytes], level0: Sequence[bytes],
                             max_run_size: int = MAX_RUN_SIZE) -> List[OutRun]:
-    """table_buffer_compaction.rs:208-279: the oldest min(16, n) buffer runs, each at its own
+    """table_buffer_compaction.rs:32-103: the oldest min(16, n) buffer runs, each at its own
     SeqNo (BTreeMap order), plus every L0 run concatenated (min_key order) as ONE stream at
     SeqNo 0 when the table has a level 0 (:243-276). Output runs belong to L0."""
     streams = [(seq, [data]) for seq, data in sorted(buffer.items())[:FAN_IN_CAP]]
@@ -38,7 +38,7 @@ def table_tree_compaction(c: Compactor, level_run: bytes, next_level_runs: Seque
 
 
 def wal_compaction(c: Compactor, wal: Dict[int, bytes], max_run_size: int = MAX_RUN_SIZE) -> List[OutRun]:
-    """wal_compaction.rs:191-347: the oldest min(16, n) WAL runs at their own SeqNos, merged,
+    """wal_compaction.rs:18-174: the oldest min(16, n) WAL runs at their own SeqNos, merged,
     split by "{table_id}." key prefix into one run per table (OutRun.table_id)."""
     streams = [(seq, [data]) for seq, data in sorted(wal.items())[:FAN_IN_CAP]]
     return c.compact(streams, max_run_size, SKV_SPLIT_BY_TABLE)

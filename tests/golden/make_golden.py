@@ -220,10 +220,10 @@ def compact_cases():
     add("wal_two_tables", [(1, [enc([P("1.a", b"x"), P("1.b", b"y"), P("2.a", b"z")])]),
                            (2, [enc([D("1.a"), P("2.c", b"w")])])], 4 * MiB, 2)
     add("wal_negative_and_prefix_quirks", [(1, [enc([P("+5.a", b"1"), P("-0.b", b"2"), P("007.c", b"3"), P("7.d", b"4")])])],
-        4 * MiB, 2, "format!(\"{id}.\").len() strip quirk (wal_compaction.rs:254)")
+        4 * MiB, 2, "format!(\"{id}.\").len() strip quirk (wal_compaction.rs:81)")
     add("wal_table_too_big_dropped", [(1, [enc([P(f"3.k{i:02d}", b"v" * 30) for i in range(10)] +
                                                [P("4.a", b"1")])])], 200, 2,
-        "table 3 needs > 1 run -> its task errors and is swallowed (wal_compaction.rs:304-310, :276)")
+        "table 3 needs > 1 run -> its task errors and is swallowed (wal_compaction.rs:131-137, :103)")
     add("wal_bad_key", [(1, [enc([P("1.a", b"x"), P("nodot", b"y")])])], 4 * MiB, 2)
     add("wal_bad_table_id", [(1, [enc([P("1.a", b"x"), P("1x.b", b"y")])])], 4 * MiB, 2)
     add("wal_table_overflow", [(1, [enc([P("99999999999999999999.a", b"x")])])], 4 * MiB, 2)

@@ -7,7 +7,7 @@ restatements check each other (tests/test_oracle_vs_pyref.py). Test infrastructu
   merge    : k_way::merge + HeapItem::cmp src/k_way.rs:14-33, :113-179
   filter   : Delete drop at Level::max    src/jobs/table_tree_compaction.rs:139-145
   encode   : runs::build_runs             src/runs.rs:166-282
-  wal      : table split + prefix strip   src/jobs/wal_compaction.rs:239-347
+  wal      : table split + prefix strip   src/jobs/wal_compaction.rs:66-174
 """
 from __future__ import annotations
 

@@ -133,7 +133,7 @@ def test_generated_configs_match_oracle(dev, name, streams, max_size, flags):
 
 
 def test_l0_concatenation_many_members(dev):
-    """buffer runs + a 40-member L0 stream at SeqNo 0 (table_buffer_compaction.rs:243-276)."""
+    """buffer runs + a 40-member L0 stream at SeqNo 0 (table_buffer_compaction.rs:67-100)."""
     r = random.Random(7)
     l0 = []
     for i in range(40):
