@@ -17,12 +17,29 @@
 namespace skv {
 
 constexpr uint64_t CHUNK = 4096;          // bytes of run body per speculative walk lane
-constexpr int TILE_CAP = 4096;            // max elements a merge tile sorts in LDS
-constexpr int TILE_TARGET = 2048;         // target elements per merge tile
-constexpr int TILE_THREADS = 1024;
-constexpr int GATHER_SEG = 256;           // surviving records per gather workgroup
-constexpr int GATHER_THREADS = 256;
-constexpr int GATHER_TBL = 6144;         // output 16-byte blocks per gather workgroup with a direct piece table
+#ifndef SKV_TILE_CAP
+#define SKV_TILE_CAP 4096
+#define SKV_TILE_TARGET 2048
+#define SKV_TILE_THREADS 1024
+#endif
+constexpr int TILE_CAP = SKV_TILE_CAP;          // max elements a merge tile sorts in LDS
+constexpr int TILE_TARGET = SKV_TILE_TARGET;    // target elements per merge tile
+constexpr int TILE_THREADS = SKV_TILE_THREADS;
+#ifndef SKV_GATHER_SEG
+#define SKV_GATHER_SEG 256
+#endif
+constexpr int GATHER_SEG = SKV_GATHER_SEG;      // surviving records per gather workgroup
+constexpr int GATHER_THREADS = SKV_GATHER_SEG;  // one lane per record in the setup phase
+constexpr int GATHER_TBL = 23 * SKV_GATHER_SEG; // output 16-byte blocks per gather workgroup with a direct piece table
+#ifndef SKV_GATHER_U
+#define SKV_GATHER_U 2                   // output blocks per lane in flight in k_gather
+#endif
+#ifndef SKV_GATHER_WAVES
+#define SKV_GATHER_WAVES 8               // k_gather register budget: waves per SIMD (64 VGPRs at 8)
+#endif
+#ifndef SKV_GATHER_NT
+#define SKV_GATHER_NT 1                  // 1: non-temporal output stores (written once, never re-read)
+#endif
 constexpr uint32_t NO_POS32 = 0xFFFFFFFFu;
 constexpr uint64_t NO_POS = ~0ull;
 

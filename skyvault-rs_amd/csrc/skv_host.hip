@@ -245,30 +245,24 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     uint64_t* d_recb = dbuf<uint64_t>(ctx, "run_recb", n_runs + 1);
     HIPCHK(hipMemsetAsync(d_broken, 0, (size_t)n_runs * 4, st));
     launch_run_header(st, d_runs, n_runs, d_hdr, d_fmt);
-    launch_spec(st, d_runs, n_runs, n_chunks, d_hdr, d_fmt, d_broken, ch_start, ch_end, ch_cnt, ch_err);
-    launch_validate(st, d_runs, n_runs, n_chunks, d_hdr, ch_start, ch_end, ch_err, bad_bits, first_bad);
-    launch_fixup(st, d_runs, n_runs, d_hdr, first_bad, bad_bits, ch_start, ch_end, ch_cnt, ch_err);
-    launch_err_chunk(st, d_runs, n_runs, n_chunks, d_hdr, ch_err, err_chunk);
-    launch_mask(st, d_runs, n_runs, n_chunks, d_hdr, err_chunk, ch_cnt, cnt64);
-    launch_scan(st, cnt64, n_chunks, ch_rec_base, scan_tmp);
-    launch_run_summary(st, d_runs, n_runs, d_hdr, err_chunk, ch_err, ch_rec_base, d_sum, d_recb);
-    HIPCHK(hipGetLastError());
 
     std::vector<RunSummary> sum(n_runs);
-    uint64_t R = 0;
-    {
-        RunSummary* hs = (RunSummary*)pinned(ctx, n_runs * sizeof(RunSummary) + 16);
-        d2h(ctx, hs, d_sum, n_runs * sizeof(RunSummary));
-        d2h(ctx, (uint8_t*)hs + n_runs * sizeof(RunSummary), ch_rec_base + n_chunks, 8);
-        sync(ctx);
-        memcpy(sum.data(), hs, n_runs * sizeof(RunSummary));
-        memcpy(&R, (uint8_t*)hs + n_runs * sizeof(RunSummary), 8);
-    }
-    // per stream (rank order): valid record count n_s and the first error
     std::vector<uint64_t> stream_base(k + 1, 0), stream_valid(k, 0);
     std::vector<uint32_t> stream_err(k, 0);
     bool any_err = false;
-    {
+    uint64_t R = 0;
+    uint64_t* rec_addr = nullptr;
+    uint64_t* rec_hi = nullptr;
+    uint64_t* rec_lo = nullptr;
+    uint32_t* rec_klen = nullptr;
+    uint32_t* rec_meta = nullptr;
+    uint32_t* d_flags = dbuf<uint32_t>(ctx, "flags", 4);
+    uint64_t* d_stream_base = dbuf<uint64_t>(ctx, "stream_base", k + 1);
+    unsigned long long* d_first_dec = dbuf<unsigned long long>(ctx, "first_dec", k);
+    std::vector<uint64_t> first_dec(k);
+    uint32_t hflags[4];
+    // per stream (rank order): base index, valid record count n_s and the first error
+    auto stream_tables = [&]() {
         uint64_t acc = 0;
         for (uint32_t s = 0; s < k; ++s) {
             stream_base[s] = acc;
@@ -289,33 +283,91 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
         }
         stream_base[k] = acc;
         if (acc != R) throw DevError("internal: record count mismatch");
-    }
-    // ---- record arrays ---------------------------------------------------------------------
-    uint64_t* rec_addr = dbuf<uint64_t>(ctx, "rec_addr", R);
-    uint64_t* rec_hi = dbuf<uint64_t>(ctx, "rec_hi", R);
-    uint64_t* rec_lo = dbuf<uint64_t>(ctx, "rec_lo", R);
-    uint32_t* rec_klen = dbuf<uint32_t>(ctx, "rec_klen", R);
-    uint32_t* rec_meta = dbuf<uint32_t>(ctx, "rec_meta", R);
-    uint32_t* d_flags = dbuf<uint32_t>(ctx, "flags", 4);
-    uint64_t* d_stream_base = dbuf<uint64_t>(ctx, "stream_base", k + 1);
-    unsigned long long* d_first_dec = dbuf<unsigned long long>(ctx, "first_dec", k);
-    HIPCHK(hipMemsetAsync(d_flags, 0, 16, st));
-    HIPCHK(hipMemsetAsync(d_first_dec, 0xFF, (size_t)k * 8, st));
-    h2d(ctx, d_stream_base, stream_base.data(), (k + 1) * 8);
-    launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
-                d_flags);
-    mark(ctx, PH_PARSE);
-    launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
-    HIPCHK(hipGetLastError());
-    std::vector<uint64_t> first_dec(k);
-    uint32_t hflags[4];
-    {
-        uint8_t* hp = (uint8_t*)pinned(ctx, k * 8 + 16);
+    };
+    auto alloc_records = [&]() {
+        rec_addr = dbuf<uint64_t>(ctx, "rec_addr", R);
+        rec_hi = dbuf<uint64_t>(ctx, "rec_hi", R);
+        rec_lo = dbuf<uint64_t>(ctx, "rec_lo", R);
+        rec_klen = dbuf<uint32_t>(ctx, "rec_klen", R);
+        rec_meta = dbuf<uint32_t>(ctx, "rec_meta", R);
+        HIPCHK(hipMemsetAsync(d_flags, 0, 16, st));
+        HIPCHK(hipMemsetAsync(d_first_dec, 0xFF, (size_t)k * 8, st));
+        h2d(ctx, d_stream_base, stream_base.data(), (k + 1) * 8);
+    };
+    // order check + readback of its result, the record flags and (fast path) the broken-run flags
+    auto check_and_read = [&](bool read_broken) -> bool {
+        launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
+        HIPCHK(hipGetLastError());
+        uint8_t* hp = (uint8_t*)pinned(ctx, k * 8 + 16 + (read_broken ? n_runs * 4 : 0));
         d2h(ctx, hp, d_first_dec, (size_t)k * 8);
         d2h(ctx, hp + (size_t)k * 8, d_flags, 16);
+        if (read_broken) d2h(ctx, hp + (size_t)k * 8 + 16, d_broken, (size_t)n_runs * 4);
         sync(ctx);
         memcpy(first_dec.data(), hp, (size_t)k * 8);
         memcpy(hflags, hp + (size_t)k * 8, 16);
+        bool broken = false;
+        if (read_broken) {
+            const uint32_t* b = (const uint32_t*)(hp + (size_t)k * 8 + 16);
+            for (uint32_t r = 0; r < n_runs && !broken; ++r) broken = b[r] != 0;
+        }
+        return broken;
+    };
+
+    // ---- fast path: every run fixed-stride (one record size per run) -> one verifying pass ------
+    bool parsed = false;
+    {
+        RunFmt* hf = (RunFmt*)pinned(ctx, (size_t)n_runs * sizeof(RunFmt) + 16);
+        d2h(ctx, hf, d_fmt, (size_t)n_runs * sizeof(RunFmt));
+        sync(ctx);
+        bool all_fixed = n_runs > 0;
+        for (uint32_t r = 0; r < n_runs && all_fixed; ++r) all_fixed = hf[r].S != 0;
+        if (all_fixed) {
+            std::vector<uint64_t> recb(n_runs + 1, 0);
+            for (uint32_t r = 0; r < n_runs; ++r) {
+                sum[r].records = (runs[r].len - 1) / hf[r].S;
+                sum[r].err = 0;
+                sum[r].pad = 0;
+                recb[r + 1] = recb[r] + sum[r].records;
+            }
+            R = recb[n_runs];
+            stream_tables();
+            alloc_records();
+            h2d(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
+            launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
+                               rec_meta, d_flags);
+            mark(ctx, PH_PARSE);
+            parsed = !check_and_read(true);
+            if (!parsed) {  // a run is not what its first record promised: general parse
+                R = 0;
+                any_err = false;
+                std::fill(stream_err.begin(), stream_err.end(), 0u);
+            }
+        }
+    }
+    // ---- general path: speculative chunk walks ----------------------------------------------
+    if (!parsed) {
+        launch_spec(st, d_runs, n_runs, n_chunks, d_hdr, d_fmt, d_broken, ch_start, ch_end, ch_cnt, ch_err);
+        launch_validate(st, d_runs, n_runs, n_chunks, d_hdr, ch_start, ch_end, ch_err, bad_bits, first_bad);
+        launch_fixup(st, d_runs, n_runs, d_hdr, first_bad, bad_bits, ch_start, ch_end, ch_cnt, ch_err);
+        launch_err_chunk(st, d_runs, n_runs, n_chunks, d_hdr, ch_err, err_chunk);
+        launch_mask(st, d_runs, n_runs, n_chunks, d_hdr, err_chunk, ch_cnt, cnt64);
+        launch_scan(st, cnt64, n_chunks, ch_rec_base, scan_tmp);
+        launch_run_summary(st, d_runs, n_runs, d_hdr, err_chunk, ch_err, ch_rec_base, d_sum, d_recb);
+        HIPCHK(hipGetLastError());
+        {
+            RunSummary* hs = (RunSummary*)pinned(ctx, n_runs * sizeof(RunSummary) + 16);
+            d2h(ctx, hs, d_sum, n_runs * sizeof(RunSummary));
+            d2h(ctx, (uint8_t*)hs + n_runs * sizeof(RunSummary), ch_rec_base + n_chunks, 8);
+            sync(ctx);
+            memcpy(sum.data(), hs, n_runs * sizeof(RunSummary));
+            memcpy(&R, (uint8_t*)hs + n_runs * sizeof(RunSummary), 8);
+        }
+        stream_tables();
+        alloc_records();
+        launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, R, rec_addr, rec_hi,
+                    rec_lo, rec_klen, rec_meta, d_flags);
+        mark(ctx, PH_PARSE);
+        check_and_read(false);
     }
     mark(ctx, PH_CHECK);
     bool any_dec = false;

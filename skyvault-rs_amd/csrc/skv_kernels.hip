@@ -348,8 +348,13 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
 }
 
 // Fixed-stride runs: one thread per record at 1 + i*S (coalesced stores, independent loads).
+// VERIFY: the single-pass parse of a job whose runs are all fixed-stride — each record is parsed
+// exactly as read_run_stream would (runs.rs:559-626) and must have size S, which by induction
+// proves the whole run decodes to these records; any other outcome marks the run broken and
+// the host reruns the general parse.
+template <bool VERIFY>
 __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t R_total,
-                             const RunFmt* __restrict__ fmt, const uint32_t* __restrict__ run_broken,
+                             const RunFmt* __restrict__ fmt, uint32_t* run_broken,
                              const uint64_t* __restrict__ run_recb, uint64_t* __restrict__ rec_addr,
                              uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
                              uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags) {
@@ -362,10 +367,14 @@ __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, 
         else hi = mid;
     }
     const RunFmt f = fmt[lo];
-    if (!f.S || run_broken[lo]) return;
+    if (!VERIFY && (!f.S || run_broken[lo])) return;
     const uint8_t* run = (const uint8_t*)runs[lo].ptr;
     uint64_t p = 1 + (i - run_recb[lo]) * f.S;
     RecHdr h = parse_rec<true>(run, runs[lo].len, p);
+    if (VERIFY && (h.err || h.size != f.S)) {
+        atomicOr(&run_broken[lo], 1u);
+        return;
+    }
     put_rec(i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
 }
 
@@ -1043,14 +1052,14 @@ __device__ __forceinline__ uint32_t gather_piece(const uint64_t* s_dst, uint32_t
 // moved with at most two aligned 16-byte loads and merged under a byte mask. Blocks shared
 // with a neighbouring workgroup (segment edges) are written bytewise, only this segment's bytes.
 __device__ __noinline__ void gather_block_slow(uint64_t B, uint64_t x0, uint64_t x1, uint32_t p,
-                                               const uint64_t* s_dst, const uint64_t* s_src, const uint32_t* s_len,
+                                               const uint64_t* s_dst, const uint64_t* s_src,
                                                uint8_t* out) {
     uint4 acc = make_uint4(0, 0, 0, 0);
     uint64_t x = x0;
     while (x < x1) {
         const uint64_t d = s_dst[p];
         const uint64_t src = s_src[p];
-        const uint64_t e = d + s_len[p] < x1 ? d + s_len[p] : x1;
+        const uint64_t e = s_dst[p + 1] < x1 ? s_dst[p + 1] : x1;  // pieces tile the output densely
         const uint32_t a = (uint32_t)(x - B), b = (uint32_t)(e - B);
         uint4 w = src ? load_window16((const uint8_t*)src + (x - d), b - a) : make_uint4(1u, 0, 0, 0);
         w = shl_bytes(w, a);
@@ -1068,18 +1077,20 @@ __device__ __noinline__ void gather_block_slow(uint64_t B, uint64_t x0, uint64_t
     }
 }
 
-__global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __restrict__ Kp,
+__global__ void __launch_bounds__(GATHER_THREADS, SKV_GATHER_WAVES) k_gather(const uint64_t* __restrict__ Kp,
                                                            const uint64_t* __restrict__ n_runs_p,
                                                            const uint64_t* __restrict__ run_b,
                                                            const uint64_t* __restrict__ P,
                                                            const uint64_t* __restrict__ m_src,
                                                            const uint64_t* __restrict__ seg_r0, uint8_t* __restrict__ out) {
-    __shared__ uint64_t s_dst[2 * GATHER_SEG];
-    __shared__ uint64_t s_src[2 * GATHER_SEG];  // 0 => version byte
-    __shared__ uint32_t s_len[2 * GATHER_SEG];
-    __shared__ uint64_t s_rb[GATHER_SEG + 2];
+    // 20 KB of LDS at 256 records: 8 workgroups (32 waves) per CU
+    __shared__ uint64_t s_dst[2 * GATHER_SEG + 1];  // piece p = output bytes [s_dst[p], s_dst[p+1])
+    __shared__ uint64_t s_src[2 * GATHER_SEG];      // 0 => version byte
     __shared__ uint64_t ws[16];
-    __shared__ uint16_t s_tbl[GATHER_TBL];      // output block -> piece covering its first byte
+    __shared__ uint64_t s_tbl64[GATHER_TBL / 4];
+    uint16_t* s_tbl = (uint16_t*)s_tbl64;  // output block -> piece covering its first byte
+    uint64_t* s_rb = s_tbl64;              // run starts (setup only; dead before the table is built)
+    static_assert(GATHER_TBL / 4 >= GATHER_SEG + 2, "s_rb alias");
     // XCD-aware segment order: workgroups are dealt round-robin over the 8 XCDs, so give each XCD
     // a contiguous range of segments (neighbouring segments share input lines and one L2)
     const uint32_t nb = gridDim.x, bid = blockIdx.x;
@@ -1089,6 +1100,15 @@ __global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __res
     const uint64_t j0 = (uint64_t)seg * GATHER_SEG;
     if (j0 >= K) return;
     const uint64_t j1 = j0 + GATHER_SEG < K ? j0 + GATHER_SEG : K;
+    const uint32_t nrec = (uint32_t)(j1 - j0);
+    // independent loads first: this lane's record (P, size, source) and the segment's first run
+    const uint64_t j = j0 + threadIdx.x;
+    uint64_t Pj = 0, Pj1 = 0, srcj = 0;
+    if (threadIdx.x < nrec) {
+        Pj = P[j];
+        Pj1 = P[j + 1];
+        srcj = m_src[j];
+    }
     const uint64_t n_runs = *n_runs_p;
     const uint64_t r0 = seg_r0[seg];  // run holding record j0 (k_run_stats)
     // run starts r0 .. r0+nrb-1 that are <= j1-1
@@ -1098,9 +1118,7 @@ __global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __res
     }
     __syncthreads();
     // pieces: per record 1 or 2
-    const uint32_t nrec = (uint32_t)(j1 - j0);
     uint32_t cntp = 0;
-    uint64_t j = j0 + threadIdx.x;
     uint64_t rr = 0;
     bool start = false;
     if (threadIdx.x < nrec) {
@@ -1113,26 +1131,25 @@ __global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __res
     uint32_t pi = (uint32_t)block_excl_scan<uint64_t>(cntp, ws, tot);
     const uint32_t npieces = (uint32_t)tot;
     if (threadIdx.x < nrec) {
-        uint64_t dst = P[j] + rr + 1;
+        uint64_t dst = Pj + rr + 1;
         if (start) {
             s_dst[pi] = dst - 1;
             s_src[pi] = 0;
-            s_len[pi] = 1;
             ++pi;
         }
         s_dst[pi] = dst;
-        s_src[pi] = m_src[j];
-        s_len[pi] = (uint32_t)(P[j + 1] - P[j]);
+        s_src[pi] = srcj;
+        if (threadIdx.x == nrec - 1) s_dst[pi + 1] = dst + (Pj1 - Pj);  // end sentinel
     }
     __syncthreads();
     const uint64_t lo_b = s_dst[0];
-    const uint64_t hi_b = s_dst[npieces - 1] + s_len[npieces - 1];
+    const uint64_t hi_b = s_dst[npieces];
     const uint64_t q0 = lo_b >> 4, q1 = (hi_b + 15) >> 4;
     const bool use_tbl = q1 - q0 <= GATHER_TBL;
     if (use_tbl) {
         // piece p covers the blocks whose first byte (lo_b for the first block, else 16q) it holds
         for (uint32_t p = threadIdx.x; p < npieces; p += blockDim.x) {
-            const uint64_t d = s_dst[p], e = d + s_len[p];
+            const uint64_t d = s_dst[p], e = s_dst[p + 1];
             uint64_t qs = (d + 15) >> 4, qe = (e + 15) >> 4;  // blocks q with 16q in [d, e)
             if (d == lo_b) s_tbl[0] = (uint16_t)p;
             if (qs <= q0) qs = q0 + 1;
@@ -1145,54 +1162,82 @@ __global__ void __launch_bounds__(GATHER_THREADS) k_gather(const uint64_t* __res
     //  (2) straddling two records of >= 16 bytes: the first one's last 16 bytes and the second's
     //      first 16 bytes (both loads stay inside their records) merged by one funnel shift;
     //  (3) anything else (version bytes, records < 16 B, segment edges): gather_block_slow.
-    constexpr int U = 4;  // blocks per lane per iteration, loads issued before stores
+    constexpr int U = SKV_GATHER_U;  // blocks per lane per iteration, loads issued before stores
     const uint32_t step = blockDim.x;
-    for (uint64_t q = q0 + threadIdx.x; q < q1; q += U * step) {
+    const uint32_t nq = (uint32_t)(q1 - q0);
+    // Fast pass: cases (1) and (2) only. Slow blocks are remembered in a per-lane bit mask (block
+    // it*step + lane <-> bit it) and done after the loop, so the main loop carries no call.
+    const bool use_mask = nq <= 32u * step;
+    uint32_t slow = 0;
+    auto fast_block = [&](uint32_t qi, uint4& v) -> bool {
+        const uint64_t B = (q0 + qi) << 4;
+        if (!(B >= lo_b && B + 16 <= hi_b)) return false;
+        const uint32_t p = use_tbl ? s_tbl[qi] : gather_piece(s_dst, npieces, B);
+        const uint64_t d = s_dst[p], src = s_src[p];
+        const uint64_t len = s_dst[p + 1] - d;
+        if (!src) return false;
+        if (d + len >= B + 16) {
+            v = *(const uint4*)((const uint8_t*)src + (B - d));
+            return true;
+        }
+        if (p + 1 < npieces && len >= 16) {
+            const uint64_t src2 = s_src[p + 1];
+            const uint64_t len2 = s_dst[p + 2] - s_dst[p + 1];
+            if (src2 && len2 >= 16 && s_dst[p + 1] + len2 >= B + 16) {
+                const uint32_t k = (uint32_t)(d + len - B);  // bytes from the first record
+                const uint4 L = *(const uint4*)((const uint8_t*)src + len - 16);
+                const uint4 F = *(const uint4*)((const uint8_t*)src2);
+                v = funnel16(L, F, 16 - k);
+                return true;
+            }
+        }
+        return false;
+    };
+    uint32_t it = 0;
+    for (uint32_t qi = threadIdx.x; qi < nq; qi += U * step, it += U) {
         uint4 v[U];
-        uint32_t kind[U];  // 0: none, 1: store v, 2: slow
-        uint32_t pp[U];
+        bool ok[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t qq = q + (uint64_t)u * step;
-            kind[u] = 0;
-            pp[u] = 0;
+            const uint32_t qq = qi + u * step;
+            ok[u] = false;
             v[u] = make_uint4(0, 0, 0, 0);
-            if (qq < q1) {
-                const uint64_t B = qq << 4;
-                const bool full = B >= lo_b && B + 16 <= hi_b;
-                const uint32_t p = use_tbl ? s_tbl[qq - q0] : gather_piece(s_dst, npieces, B > lo_b ? B : lo_b);
-                pp[u] = p;
-                const uint64_t d = s_dst[p], src = s_src[p];
-                const uint32_t len = s_len[p];
-                kind[u] = 2;
-                if (full && src) {
-                    if (d + len >= B + 16) {
-                        v[u] = *(const uint4*)((const uint8_t*)src + (B - d));
-                        kind[u] = 1;
-                    } else if (p + 1 < npieces && len >= 16) {
-                        const uint64_t src2 = s_src[p + 1];
-                        const uint32_t len2 = s_len[p + 1];
-                        if (src2 && len2 >= 16 && s_dst[p + 1] + len2 >= B + 16) {
-                            const uint32_t k = (uint32_t)(d + len - B);  // bytes from the first record
-                            const uint4 L = *(const uint4*)((const uint8_t*)src + len - 16);
-                            const uint4 F = *(const uint4*)((const uint8_t*)src2);
-                            v[u] = funnel16(L, F, 16 - k);
-                            kind[u] = 1;
-                        }
-                    }
-                }
+            if (qq < nq) {
+                ok[u] = fast_block(qq, v[u]);
+                if (!ok[u] && use_mask) slow |= 1u << (it + u);
             }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t qq = q + (uint64_t)u * step;
-            if (kind[u] == 1) {
-                *(uint4*)(out + (qq << 4)) = v[u];
-            } else if (kind[u] == 2) {
-                const uint64_t B = qq << 4;
-                gather_block_slow(B, B > lo_b ? B : lo_b, B + 16 < hi_b ? B + 16 : hi_b, pp[u], s_dst, s_src, s_len,
-                                  out);
+            if (ok[u]) {
+                uint8_t* o = out + ((q0 + qi + u * step) << 4);
+#if SKV_GATHER_NT
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                u32x4 vv = {v[u].x, v[u].y, v[u].z, v[u].w};
+                __builtin_nontemporal_store(vv, (u32x4*)o);
+#else
+                *(uint4*)o = v[u];
+#endif
             }
+        }
+    }
+    // Slow pass: case (3) — version bytes, records < 16 B, segment-edge blocks.
+    auto slow_block = [&](uint32_t qi) {
+        const uint64_t B = (q0 + qi) << 4;
+        const uint64_t x0 = B > lo_b ? B : lo_b;
+        const uint32_t p = use_tbl ? s_tbl[qi] : gather_piece(s_dst, npieces, x0);
+        gather_block_slow(B, x0, B + 16 < hi_b ? B + 16 : hi_b, p, s_dst, s_src, out);
+    };
+    if (use_mask) {
+        while (slow) {
+            const uint32_t b = __builtin_ctz(slow);
+            slow &= slow - 1;
+            slow_block(threadIdx.x + b * step);
+        }
+    } else {
+        for (uint32_t qi = threadIdx.x; qi < nq; qi += step) {
+            uint4 v;
+            if (!fast_block(qi, v)) slow_block(qi);
         }
     }
 }
@@ -1292,8 +1337,15 @@ void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n
         k_emit<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, fmt, run_broken, ch_start, ch_rec_base,
                                                          rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
     if (R)
-        k_emit_fixed<<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, R, fmt, run_broken, run_recb, rec_addr, rec_hi,
-                                                        rec_lo, rec_klen, rec_meta, flags);
+        k_emit_fixed<false><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, R, fmt, (uint32_t*)run_broken, run_recb, rec_addr,
+                                                               rec_hi, rec_lo, rec_klen, rec_meta, flags);
+}
+void launch_parse_fixed(hipStream_t s, const RunInfo* runs, uint32_t n_runs, const RunFmt* fmt, uint32_t* run_broken,
+                        const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
+                        uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags) {
+    if (R)
+        k_emit_fixed<true><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, R, fmt, run_broken, run_recb, rec_addr,
+                                                              rec_hi, rec_lo, rec_klen, rec_meta, flags);
 }
 void launch_order_check(hipStream_t s, uint64_t R, const uint64_t* stream_base, uint32_t k, const uint64_t* rec_addr,
                         const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,
@@ -1365,6 +1417,32 @@ void launch_gather(hipStream_t s, const uint64_t* Kp, const uint64_t* n_runs, co
     if (!max_K) return;
     k_gather<<<blocks_for(max_K, GATHER_SEG), GATHER_THREADS, 0, s>>>(Kp, n_runs, run_b, P, m_src, seg_r0, out);
 }
+// small n: one workgroup walks the input in SCAN_BLOCK pieces with a running carry (one launch)
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_single(const uint64_t* in, uint64_t n, uint64_t* out) {
+    __shared__ uint64_t ws[16];
+    uint64_t carry = 0;
+    for (uint64_t b0 = 0; b0 < n; b0 += SCAN_BLOCK) {
+        uint64_t v[SCAN_PER];
+        uint64_t s = 0;
+#pragma unroll
+        for (int q = 0; q < SCAN_PER; ++q) {
+            uint64_t i = b0 + (uint64_t)threadIdx.x * SCAN_PER + q;
+            v[q] = i < n ? in[i] : 0;
+            s += v[q];
+        }
+        uint64_t tot;
+        uint64_t ex = block_excl_scan<uint64_t>(s, ws, tot) + carry;
+#pragma unroll
+        for (int q = 0; q < SCAN_PER; ++q) {
+            uint64_t i = b0 + (uint64_t)threadIdx.x * SCAN_PER + q;
+            if (i < n) out[i] = ex;
+            ex += v[q];
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0) out[n] = carry;
+}
+
 // exclusive scan of n u64 values into out[0..n] (out[n] = total); tmp needs scan_tmp_words(n)
 uint64_t scan_tmp_words(uint64_t n) {
     uint64_t w = 0;
@@ -1380,6 +1458,10 @@ void launch_scan(hipStream_t s, const uint64_t* in, uint64_t n, uint64_t* out, u
     uint64_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
     if (nb == 0) {
         (void)hipMemsetAsync(out, 0, 8, s);
+        return;
+    }
+    if (nb <= 16) {
+        k_scan_single<<<1, SCAN_THREADS, 0, s>>>(in, n, out);
         return;
     }
     uint64_t* partial = tmp;

@@ -13,7 +13,8 @@ from typing import List, Optional, Sequence
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT_DIR = os.path.dirname(os.path.dirname(PKG_DIR))
-LIB_PATH = os.path.join(PKG_DIR, "libskv.so")
+# SKV_LIB selects an alternative build of the same library (tuning variants, tools/variants.sh)
+LIB_PATH = os.environ.get("SKV_LIB") or os.path.join(PKG_DIR, "libskv.so")
 
 SKV_OK = 0
 SKV_E_EMPTY_INPUT = 1

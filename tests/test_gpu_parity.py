@@ -217,3 +217,42 @@ def test_device_resident_entry_point(dev):
     t = dev.timings()
     assert t["gather_ms"] > 0 and t["total_ms"] >= t["gather_ms"]
     res.free()
+
+
+def test_fixed_stride_fast_path_and_fallback(dev):
+    """The single-pass parse taken when every run's first record predicts a fixed stride, and
+    its fallback to the general parse when a run breaks the prediction."""
+    r = random.Random(21)
+
+    def fixed_run(s, n, corrupt=None):
+        keys = sorted({f"{s:02d}{r.randrange(10**12):012d}xy" for _ in range(n)})
+        data = bytearray(fmt.encode_run([fmt.put(k, bytes(r.randrange(256) for _ in range(30))) for k in keys]))
+        if corrupt is not None:
+            data[corrupt] = 0xFF
+        return bytes(data)
+
+    cases = []
+    # all fixed, clean (fast path end to end)
+    cases.append([(s, [fixed_run(s, 500)]) for s in range(1, 9)])
+    # all fixed, one run corrupt deep inside (fast path -> fallback -> the reference's error)
+    for pos in (1 + 55 * 300 + 0, 1 + 55 * 300 + 7, 1 + 55 * 410 + 21, 1 + 55 * 499 + 30):  # marker, key, val_len, value
+        cases.append([(s, [fixed_run(s, 500, corrupt=pos if s == 3 else None)]) for s in range(1, 9)])
+    # first record predicts stride 25 and the body is a multiple of it, but sizes vary
+    odd = fmt.encode_run([fmt.put("a" * 16, b""), fmt.put("b" * 15, b""), fmt.put("c" * 17, b""), fmt.put("d" * 16, b"")])
+    cases.append([(2, [odd]), (1, [fixed_run(1, 100)])])
+    # Puts and Deletes of one size (9 + 16 + 0 == 5 + 20): a valid fixed stride with both markers
+    mixed = fmt.encode_run(sorted([fmt.put(f"m{i:015d}", b"") for i in range(0, 400, 2)] +
+                                  [fmt.delete(f"m{i:019d}") for i in range(1, 400, 2)], key=lambda o: o[1]))
+    cases.append([(2, [mixed]), (1, [fixed_run(1, 100)])])
+    # fixed stride, key order violated inside a run (order error from the fast path's check)
+    keys = [f"k{i:015d}" for i in range(200)]
+    keys[120], keys[121] = keys[121], keys[120]
+    cases.append([(1, [fmt.encode_run([fmt.put(k, b"v") for k in keys])]), (2, [fixed_run(2, 50)])])
+    # L0-style stream of several fixed members + a variable-size stream (general path)
+    cases.append([(0, [fixed_run(7, 80), fixed_run(8, 80)]), (5, [odd])])
+    bad = []
+    for i, streams in enumerate(cases):
+        exp, got = _run_both(dev, streams, 8 * KiB, 0)
+        if exp != got:
+            bad.append((i, _diff(exp, got)))
+    assert not bad, bad
