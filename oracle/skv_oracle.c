@@ -427,7 +427,7 @@ static int parse_i64(const uint8_t* s, uint64_t n, int64_t* out, const char** er
 
 /* WAL split consumer (wal_compaction.rs:66-174). One builder per table in order of
  * appearance; a failing build (order error, or != 1 run) is swallowed by `if let Ok`
- * (:276, :341) and that table's data is dropped. */
+ * (:103, :168) and that table's data is dropped. */
 typedef struct {
     outbuf* out;
     uint64_t max;
@@ -442,7 +442,7 @@ static void wal_finish(walc* w) {
     if (!w->have_table) return;
     builder* b = &w->cur;
     if (!w->cur_failed) bld_end(b, w->table);
-    /* build_runs(...).try_collect() then results.len() != 1 -> Err (:299-310) */
+    /* build_runs(...).try_collect() then results.len() != 1 -> Err (:126-137) */
     if (w->cur_failed || b->local.n_runs != 1) {
         w->dropped++;
     } else {
@@ -465,17 +465,17 @@ static void wal_finish(walc* w) {
 static int wal_push(walc* w, oop* op, char* eb, size_t en) {
     uint64_t dot = 0;
     while (dot < op->klen && op->key[dot] != '.') dot++;
-    if (dot == op->klen) /* :244-246 */
+    if (dot == op->klen) /* :71-73 */
         return fail(eb, en, SKV_E_INVALID_INPUT, "Invalid input: Key does not follow 'table_id.key' format: %.*s",
                     (int)op->klen, (const char*)op->key);
     int64_t id = 0;
     const char* perr = NULL;
-    if (!parse_i64(op->key, dot, &id, &perr)) /* :248-252 */
+    if (!parse_i64(op->key, dot, &id, &perr)) /* :75-79 */
         return fail(eb, en, SKV_E_INVALID_INPUT, "Invalid input: Invalid table ID '%.*s': %s", (int)dot,
                     (const char*)op->key, perr);
     char tmp[32];
-    uint64_t strip = (uint64_t)snprintf(tmp, sizeof tmp, "%" PRId64 ".", id); /* :254 */
-    if (!w->have_table || w->table != id) { /* :255-259, :269-327 */
+    uint64_t strip = (uint64_t)snprintf(tmp, sizeof tmp, "%" PRId64 ".", id); /* :81 */
+    if (!w->have_table || w->table != id) { /* :82-86, :96-123 */
         wal_finish(w);
         w->have_table = 1;
         w->table = id;
@@ -484,7 +484,7 @@ static int wal_push(walc* w, oop* op, char* eb, size_t en) {
         w->cur.use_local = 1;
     }
     if (w->cur_failed) return SKV_OK;
-    oop s = *op; /* key.split_off(table_prefix_len) (:264-267) */
+    oop s = *op; /* key.split_off(table_prefix_len) (:91-94) */
     s.key = op->key + strip;
     s.klen = op->klen - (uint32_t)strip;
     char e2[256];

@@ -19,7 +19,7 @@ namespace skv {
 constexpr uint64_t CHUNK = 4096;          // bytes of run body per speculative walk lane
 #ifndef SKV_TILE_CAP
 #define SKV_TILE_CAP 4096
-#define SKV_TILE_TARGET 2048
+#define SKV_TILE_TARGET 3072
 #define SKV_TILE_THREADS 1024
 #endif
 constexpr int TILE_CAP = SKV_TILE_CAP;          // max elements a merge tile sorts in LDS
@@ -92,6 +92,9 @@ struct TileOut {
     uint64_t* xc;
     uint32_t* xmeta;
 };
+
+// WAL key errors (wal_compaction.rs:71-79): no '.', or Rust's ParseIntError kinds
+enum : uint32_t { WERR_NONE = 0, WERR_NODOT, WERR_EMPTY, WERR_DIGIT, WERR_POS, WERR_NEG };
 
 struct DevRunDesc {       // == skv_run_desc layout
     uint64_t off, len, put_count, delete_count;

@@ -196,6 +196,137 @@ static std::string fetch_key(skv_ctx* ctx, const uint64_t* d_rec_addr, const uin
     return k;
 }
 
+// JobError::InvalidInput text of a bad WAL key (wal_compaction.rs:71-79; Rust ParseIntError Display)
+static std::string wal_key_error(const std::string& key) {
+    size_t dot = key.find('.');
+    if (dot == std::string::npos) return "Invalid input: Key does not follow 'table_id.key' format: " + key;
+    const std::string pre = key.substr(0, dot);
+    const char* why = nullptr;
+    if (pre.empty()) why = "cannot parse integer from empty string";
+    else {
+        size_t i = 0;
+        bool neg = false;
+        if (pre[0] == '+' || pre[0] == '-') {
+            neg = pre[0] == '-';
+            i = 1;
+            if (pre.size() == 1) why = "invalid digit found in string";
+        }
+        int64_t r = 0;
+        for (; !why && i < pre.size(); ++i) {
+            if (pre[i] < '0' || pre[i] > '9') { why = "invalid digit found in string"; break; }
+            int64_t m, d = pre[i] - '0';
+            if (__builtin_mul_overflow(r, (int64_t)10, &m) ||
+                (neg ? __builtin_sub_overflow(m, d, &r) : __builtin_add_overflow(m, d, &r)))
+                why = neg ? "number too small to fit in target type" : "number too large to fit in target type";
+        }
+    }
+    if (!why) return "internal: WAL key flagged but parses: " + key;
+    return "Invalid input: Invalid table ID '" + pre + "': " + why;
+}
+
+// SKV_SPLIT_BY_TABLE after the merge: table split, prefix strip, one run per kept table
+// (skv_wal.hip). One extra host sync reads the surviving record count first.
+static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, const uint32_t* m_rec,
+                     const uint64_t* m_src, const uint64_t* m_P, const uint64_t* m_Dp, const uint64_t* rec_addr,
+                     const uint32_t* rec_klen, skv_result** out) {
+    hipStream_t st = ctx->stream;
+    uint64_t K = 0;
+    {
+        uint64_t* hp = (uint64_t*)pinned(ctx, 64);
+        d2h(ctx, hp, d_K, 8);
+        sync(ctx);
+        K = hp[0];
+    }
+    (void)R;
+    int64_t* tid = dbuf<int64_t>(ctx, "w_tid", K + 1);
+    uint32_t* strip = dbuf<uint32_t>(ctx, "w_strip", K + 1);
+    uint64_t* wsize = dbuf<uint64_t>(ctx, "w_size", K + 1);
+    uint64_t* is_new = dbuf<uint64_t>(ctx, "w_new", K + 1);
+    uint64_t* new_ex = dbuf<uint64_t>(ctx, "w_new_ex", K + 1);
+    uint32_t* bad = dbuf<uint32_t>(ctx, "w_bad", K + 1);
+    uint32_t* tix = dbuf<uint32_t>(ctx, "w_tix", K + 1);
+    uint64_t* tstart = dbuf<uint64_t>(ctx, "w_tstart", K + 2);
+    uint32_t* tbad = dbuf<uint32_t>(ctx, "w_tbad", K + 1);
+    uint64_t* Pw = dbuf<uint64_t>(ctx, "w_P", K + 1);
+    uint64_t* run_len = dbuf<uint64_t>(ctx, "w_run_len", K + 1);
+    uint64_t* keep = dbuf<uint64_t>(ctx, "w_keep", K + 1);
+    uint64_t* run_off = dbuf<uint64_t>(ctx, "w_run_off", K + 1);
+    uint64_t* keep_ex = dbuf<uint64_t>(ctx, "w_keep_ex", K + 1);
+    unsigned long long* first_err = dbuf<unsigned long long>(ctx, "w_first_err", 1);
+    uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "w_scan_tmp", scan_tmp_words(K + 1) + 64);
+    DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", K + 1);
+    uint64_t total_rec_bytes = 0;
+    for (const InStream& S : job.ranked)
+        for (uint64_t l : S.lens) total_rec_bytes += l;
+    uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + K + 16);
+    HIPCHK(hipMemsetAsync(first_err, 0xFF, 8, st));
+    HIPCHK(hipMemsetAsync(tbad, 0, (K + 1) * 4, st));
+    HIPCHK(hipMemsetAsync(run_len, 0, (K + 1) * 8, st));
+    HIPCHK(hipMemsetAsync(keep, 0, (K + 1) * 8, st));
+    launch_wal_keys(st, d_K, K, m_src, m_rec, rec_klen, m_P, tid, strip, wsize, first_err);
+    launch_wal_flags(st, d_K, K, tid, strip, m_src, m_rec, rec_klen, is_new, bad);
+    launch_scan(st, is_new, K, new_ex, scan_tmp);  // new_ex[K] = number of tables
+    launch_wal_index(st, d_K, K, is_new, new_ex, bad, tix, tstart, tbad);
+    launch_scan(st, wsize, K, Pw, scan_tmp);       // stripped record offsets
+    const uint64_t* d_NT = new_ex + K;
+    launch_wal_tables(st, d_NT, K, tstart, Pw, tbad, job.max_run_size, run_len, keep);
+    launch_scan(st, run_len, K, run_off, scan_tmp);  // output offset per table, total at [K]
+    launch_scan(st, keep, K, keep_ex, scan_tmp);     // run index per kept table, count at [K]
+    launch_wal_desc(st, d_NT, K, tstart, Pw, m_Dp, keep, keep_ex, run_off, tid, strip, m_rec, rec_klen, d_desc);
+    mark(ctx, PH_CHAIN);
+    launch_wal_gather(st, d_K, K, tix, tstart, keep, run_off, Pw, strip, m_src, m_rec, rec_klen, d_out);
+    HIPCHK(hipGetLastError());
+    mark(ctx, PH_GATHER);
+    uint64_t h[4];
+    {
+        uint64_t* hp = (uint64_t*)pinned(ctx, 64);
+        d2h(ctx, hp, first_err, 8);
+        d2h(ctx, hp + 1, d_NT, 8);
+        d2h(ctx, hp + 2, keep_ex + K, 8);
+        d2h(ctx, hp + 3, run_off + K, 8);
+        sync(ctx);
+        memcpy(h, hp, 32);
+    }
+    if (h[0] != ~0ull) {  // the first bad key in merged order fails the job (:67-79 `?`)
+        uint32_t rec = 0;
+        HIPCHK(hipMemcpy(&rec, m_rec + h[0], 4, hipMemcpyDeviceToHost));
+        throw ApiError{SKV_E_INVALID_INPUT, wal_key_error(fetch_key(ctx, rec_addr, rec_klen, rec))};
+    }
+    const uint64_t n_tables = h[1], n_kept = h[2], n_bytes = h[3];
+    ResultBox* box = new ResultBox();
+    skv_result* res = &box->pub;
+    res->runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, n_kept) * sizeof(skv_run_desc));
+    if (n_kept) HIPCHK(hipMemcpy(res->runs, d_desc, n_kept * sizeof(DevRunDesc), hipMemcpyDeviceToHost));
+    uint64_t out_records = 0;
+    for (uint64_t i = 0; i < n_kept; ++i) out_records += res->runs[i].put_count + res->runs[i].delete_count;
+    res->n_runs = n_kept;
+    res->bytes = d_out;
+    res->n_bytes = n_bytes;
+    res->in_bytes = job.in_bytes;
+    res->in_records = R;
+    res->out_records = out_records;
+    res->dropped_tables = n_tables - n_kept;
+    if (ctx->profiling) {
+        HIPCHK(hipEventSynchronize(ctx->ev[PH_GATHER]));
+        float ms[PH_N] = {};
+        for (int p = PH_PARSE; p < PH_N; ++p) HIPCHK(hipEventElapsedTime(&ms[p], ctx->ev[p - 1], ctx->ev[p]));
+        float tot = 0;
+        HIPCHK(hipEventElapsedTime(&tot, ctx->ev[PH_START], ctx->ev[PH_GATHER]));
+        skv_timings& t = ctx->timings;
+        t.total_ms = tot;
+        t.parse_ms = ms[PH_PARSE];
+        t.check_ms = ms[PH_CHECK];
+        t.merge_ms = ms[PH_MERGE];
+        t.chain_ms = ms[PH_CHAIN];
+        t.gather_ms = ms[PH_GATHER];
+        t.gather_read_bytes = n_bytes - n_kept;
+        t.gather_write_bytes = n_bytes;
+    }
+    ctx->timings.host_syncs = ctx->syncs;
+    *out = res;
+    return SKV_OK;
+}
+
 static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     hipStream_t st = ctx->stream;
     ctx->syncs = 0;
@@ -375,6 +506,10 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
         if (first_dec[s] != ~0ull && first_dec[s] + 1 < stream_valid[s]) any_dec = true;
 
     // ---- errors: which one k_way::merge surfaces first --------------------------------------
+    if ((any_err || any_dec) && (job.flags & SKV_SPLIT_BY_TABLE))
+        throw ApiError{SKV_E_UNSUPPORTED,
+                       "SKV_SPLIT_BY_TABLE with an undecodable or unsorted input stream: which of the run error and "
+                       "the WAL key / table outcome surfaces first is not resolved on device in this build"};
     if (any_err || any_dec) {
         // (1) first items are pulled in the caller's vector order (k_way.rs:126-140)
         std::vector<uint32_t> by_vec(k);
@@ -539,13 +674,14 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     uint64_t* m_src = dbuf<uint64_t>(ctx, "m_src", R + 1);
     uint64_t* m_P = dbuf<uint64_t>(ctx, "m_P", R + 1);
     uint64_t* m_Dp = dbuf<uint64_t>(ctx, "m_Dp", R + 1);
-    uint32_t* tile_max = dbuf<uint32_t>(ctx, "tile_max", T0);
+    uint32_t* tile_max = dbuf<uint32_t>(ctx, "tile_max", 2 * T0);  // (min, max) record size per tile
     launch_finalize(st, T0, d_tile_base0, O0.tile_kept, kept_base, byte_base, del_base, O0.t_rec, O0.t_meta, rec_addr,
                     m_rec, m_src, m_P, m_Dp, tile_max);
     HIPCHK(hipGetLastError());
     mark(ctx, PH_MERGE);
-    // ---- chain + stats ----------------------------------------------------------------------
     const uint64_t* d_K = kept_base + T0;
+    if (job.flags & SKV_SPLIT_BY_TABLE) return wal_stage(ctx, job, R, d_K, m_rec, m_src, m_P, m_Dp, rec_addr, rec_klen, out);
+    // ---- chain + stats ----------------------------------------------------------------------
     uint64_t* run_b = dbuf<uint64_t>(ctx, "run_b", R + 2);
     uint64_t* d_nruns = dbuf<uint64_t>(ctx, "n_runs", 2);
     DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", R + 1);
@@ -635,8 +771,6 @@ static int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64
     for (size_t i = 1; i < job.ranked.size(); ++i)
         if (job.ranked[i].seq == job.ranked[i - 1].seq)
             return set_err(ctx, SKV_E_INVALID_ARG, "duplicate seq_no %" PRId64, job.ranked[i].seq);
-    if (flags & SKV_SPLIT_BY_TABLE)
-        return set_err(ctx, SKV_E_UNSUPPORTED, "SKV_SPLIT_BY_TABLE (WAL compaction) is not on the device path in this build");
     return SKV_OK;
 }
 

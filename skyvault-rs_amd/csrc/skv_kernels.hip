@@ -824,7 +824,7 @@ __global__ void __launch_bounds__(1024) k_finalize(uint64_t T, const uint64_t* _
     const uint64_t t = blockIdx.x;
     const uint64_t n = tile_kept[t], src = tile_base[t];
     uint64_t g = kept_base[t], pb = byte_base[t], pd = del_base[t];
-    uint32_t mx = 0;
+    uint32_t mx = 0, mn = 0xFFFFFFFFu;
     for (uint64_t b0 = 0; b0 < n; b0 += blockDim.x) {
         uint64_t i = b0 + threadIdx.x;
         uint32_t meta = i < n ? t_meta[src + i] : 0u;
@@ -839,22 +839,32 @@ __global__ void __launch_bounds__(1024) k_finalize(uint64_t T, const uint64_t* _
             m_P[g + i] = pb + eb;
             m_Dp[g + i] = pd + ed;
             mx = (uint32_t)sz > mx ? (uint32_t)sz : mx;
+            mn = (uint32_t)sz < mn ? (uint32_t)sz : mn;
         }
         pb += tb;
         pd += td;
     }
-    // largest surviving record of the tile (no global atomics: k_chain reduces the tiles)
-    __shared__ uint32_t wmax[16];
+    // smallest / largest surviving record of the tile (no global atomics: k_chain reduces them)
+    __shared__ uint32_t wmax[16], wmin[16];
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         uint32_t o = __shfl_xor(mx, d, 64);
         mx = o > mx ? o : mx;
+        o = __shfl_xor(mn, d, 64);
+        mn = o < mn ? o : mn;
     }
-    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
+    if ((threadIdx.x & 63) == 0) {
+        wmax[threadIdx.x >> 6] = mx;
+        wmin[threadIdx.x >> 6] = mn;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) mx = wmax[w] > mx ? wmax[w] : mx;
-        max_rec[t] = mx;
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            mx = wmax[w] > mx ? wmax[w] : mx;
+            mn = wmin[w] < mn ? wmin[w] : mn;
+        }
+        max_rec[2 * t] = mn;
+        max_rec[2 * t + 1] = mx;
     }
     if (t == T - 1 && threadIdx.x == 0) {
         m_P[kept_base[t] + n] = pb;
@@ -920,16 +930,30 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
         if (lane == 0) { run_b[0] = 0; *n_runs_out = 0; }
         return;
     }
-    // largest surviving record (per-tile maxima from k_finalize)
-    uint32_t mr = 0;
-    for (uint64_t t = lane; t < n_tiles; t += 64) mr = tile_max[t] > mr ? tile_max[t] : mr;
+    // smallest / largest surviving record (per-tile pairs from k_finalize)
+    uint32_t mr = 0, mn = 0xFFFFFFFFu;
+    for (uint64_t t = lane; t < n_tiles; t += 64) {
+        mn = tile_max[2 * t] < mn ? tile_max[2 * t] : mn;
+        mr = tile_max[2 * t + 1] > mr ? tile_max[2 * t + 1] : mr;
+    }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         uint32_t o = __shfl_xor(mr, d, 64);
         mr = o > mr ? o : mr;
+        o = __shfl_xor(mn, d, 64);
+        mn = o < mn ? o : mn;
     }
     // every record fits a run on its own when 1 + largest record <= max: no oversize probe
     const bool all_fit = max_size >= 1 && (uint64_t)mr + 1 <= max_size;
+    if (all_fit && mn == mr) {
+        // one record size S: the greedy split (runs.rs:211-238) closes every run after exactly
+        // n = (max - 1) / S records, so the chain is arithmetic
+        const uint64_t n = (max_size - 1) / mr;
+        const uint64_t runs = (K + n - 1) / n;
+        for (uint64_t i = lane; i <= runs; i += 64) run_b[i] = i * n < K ? i * n : K;
+        if (lane == 0) *n_runs_out = runs;
+        return;
+    }
     uint64_t b = 0, m = 0;
     uint64_t Pb = P[0];
     uint64_t L = 1;

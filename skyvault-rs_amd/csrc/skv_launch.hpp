@@ -52,6 +52,24 @@ void launch_run_stats(hipStream_t, const uint64_t* n_runs, const uint64_t* run_b
                       uint64_t* seg_r0, uint64_t max_runs);
 void launch_gather(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
                    const uint64_t* m_src, const uint64_t* seg_r0, uint8_t* out, uint64_t max_K);
+// skv_wal.hip — SKV_SPLIT_BY_TABLE (wal_compaction.rs:66-174)
+void launch_wal_keys(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint32_t* m_rec,
+                     const uint32_t* rec_klen, const uint64_t* P, int64_t* tid, uint32_t* strip, uint64_t* wsize,
+                     unsigned long long* first_err);
+void launch_wal_flags(hipStream_t, const uint64_t* Kp, uint64_t max_K, const int64_t* tid, const uint32_t* strip,
+                      const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen, uint64_t* is_new,
+                      uint32_t* bad);
+void launch_wal_index(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint64_t* is_new, const uint64_t* new_ex,
+                      const uint32_t* bad, uint32_t* tix, uint64_t* tstart, uint32_t* tbad);
+void launch_wal_tables(hipStream_t, const uint64_t* NTp, uint64_t max_NT, const uint64_t* tstart, const uint64_t* Pw,
+                       const uint32_t* tbad, uint64_t max_size, uint64_t* run_len, uint64_t* keep);
+void launch_wal_desc(hipStream_t, const uint64_t* NTp, uint64_t max_NT, const uint64_t* tstart, const uint64_t* Pw,
+                     const uint64_t* Dp, const uint64_t* keep, const uint64_t* keep_ex, const uint64_t* run_off,
+                     const int64_t* tid, const uint32_t* strip, const uint32_t* m_rec, const uint32_t* rec_klen,
+                     DevRunDesc* descs);
+void launch_wal_gather(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint32_t* tix, const uint64_t* tstart,
+                       const uint64_t* keep, const uint64_t* run_off, const uint64_t* Pw, const uint32_t* strip,
+                       const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen, uint8_t* out);
 uint64_t scan_tmp_words(uint64_t n);
 void launch_scan(hipStream_t, const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tmp);
 }  // namespace skv

@@ -1,0 +1,228 @@
+// skv_wal.hip — WAL compaction's table split on the device (SKV_SPLIT_BY_TABLE).
+//
+// After the merge (k_finalize's dense arrays: K surviving records in key order), the reference's
+// WAL loop (src/jobs/wal_compaction.rs:66-174) does, per merged op:
+//   split_once('.') -> InvalidInput if missing (:71-73); prefix.parse::<i64>() -> InvalidInput
+//   (:75-79); strip format!("{id}.").len() bytes (:81, :91-94); a change of table id closes the
+//   table's build_runs task and opens a new one (:82-86, :96-123). Each task must produce exactly
+//   one run (:126-137); a failing task (that check, or build_runs' order error) is swallowed by
+//   `if let Ok(..)` (:103, :168) and the table's data is dropped.
+// Here: one thread per merged record parses its key prefix; tables are the maximal runs of equal
+// table id in merged order; per table the stripped sizes, order check and one-run rule decide
+// keep/drop; kept tables become one output run each (version byte + rewritten records).
+#include "skv_launch.hpp"
+
+namespace skv {
+
+static inline unsigned wal_blocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+// Rust `str::parse::<i64>` (core::num, radix 10): returns 0 ok, else WERR_*.
+__device__ __forceinline__ uint32_t parse_i64_dev(const uint8_t* s, uint64_t n, int64_t& out) {
+    if (n == 0) return WERR_EMPTY;
+    uint64_t i = 0;
+    bool neg = false;
+    uint8_t c0 = s[0];
+    if (c0 == '+' || c0 == '-') {
+        if (n == 1) return WERR_DIGIT;
+        neg = c0 == '-';
+        i = 1;
+    }
+    int64_t r = 0;
+    for (; i < n; ++i) {
+        uint32_t c = s[i];
+        if (c < '0' || c > '9') return WERR_DIGIT;  // to_digit before the overflow checks
+        int64_t m;
+        if (__builtin_mul_overflow(r, (int64_t)10, &m)) return neg ? WERR_NEG : WERR_POS;
+        int64_t d = (int64_t)(c - '0');
+        if (neg ? __builtin_sub_overflow(m, d, &r) : __builtin_add_overflow(m, d, &r)) return neg ? WERR_NEG : WERR_POS;
+    }
+    out = r;
+    return 0;
+}
+
+// byte length of format!("{id}.")
+__device__ __forceinline__ uint32_t id_prefix_len(int64_t id) {
+    uint64_t u = id < 0 ? (uint64_t)0 - (uint64_t)id : (uint64_t)id;
+    uint32_t d = 1;
+    while (u >= 10) {
+        u /= 10;
+        ++d;
+    }
+    return d + (id < 0 ? 1u : 0u) + 1u;
+}
+
+// per merged record: table id, strip length, stripped record size; the first bad key (merged
+// order) is the job's InvalidInput error
+__global__ void k_wal_keys(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ m_src,
+                           const uint32_t* __restrict__ m_rec, const uint32_t* __restrict__ rec_klen,
+                           const uint64_t* __restrict__ P, int64_t* tid, uint32_t* strip, uint64_t* wsize,
+                           unsigned long long* first_err) {
+    const uint64_t K = *Kp;
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= K) return;
+    const uint8_t* key = (const uint8_t*)m_src[j] + 5;
+    const uint64_t klen = rec_klen[m_rec[j]];
+    uint64_t dot = 0;
+    while (dot < klen && key[dot] != '.') ++dot;
+    int64_t id = 0;
+    uint32_t e = dot == klen ? WERR_NODOT : parse_i64_dev(key, dot, id);
+    uint32_t st = 0;
+    if (e) atomicMin(first_err, (unsigned long long)j);
+    else st = id_prefix_len(id);
+    tid[j] = id;
+    strip[j] = st;
+    wsize[j] = (P[j + 1] - P[j]) - st;
+}
+
+// stripped key of record j: bytes [src+5+strip, src+5+klen)
+__device__ __forceinline__ int stripped_cmp(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
+    const uint64_t n = la < lb ? la : lb;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint32_t x = a[i], y = b[i];
+        if (x != y) return x < y ? -1 : 1;
+    }
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+// table starts (a change of table id, :82-86) and build_runs' order check between neighbours of
+// one table on the stripped keys (runs.rs:190-198)
+__global__ void k_wal_flags(const uint64_t* __restrict__ Kp, const int64_t* __restrict__ tid,
+                            const uint32_t* __restrict__ strip, const uint64_t* __restrict__ m_src,
+                            const uint32_t* __restrict__ m_rec, const uint32_t* __restrict__ rec_klen,
+                            uint64_t* is_new, uint32_t* bad) {
+    const uint64_t K = *Kp;
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= K) return;
+    const bool nw = j == 0 || tid[j] != tid[j - 1];
+    is_new[j] = nw ? 1 : 0;
+    uint32_t b = 0;
+    if (!nw) {
+        const uint64_t sa = strip[j - 1], sb = strip[j];
+        const uint8_t* ka = (const uint8_t*)m_src[j - 1] + 5 + sa;
+        const uint8_t* kb = (const uint8_t*)m_src[j] + 5 + sb;
+        const uint64_t la = rec_klen[m_rec[j - 1]] - sa, lb = rec_klen[m_rec[j]] - sb;
+        b = stripped_cmp(ka, la, kb, lb) >= 0 ? 1u : 0u;
+    }
+    bad[j] = b;
+}
+
+// table index per record, table start table, failing tables
+__global__ void k_wal_index(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ is_new,
+                            const uint64_t* __restrict__ new_ex, const uint32_t* __restrict__ bad, uint32_t* tix,
+                            uint64_t* tstart, uint32_t* tbad) {
+    const uint64_t K = *Kp;
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= K) return;
+    const uint64_t t = new_ex[j] + is_new[j] - 1;
+    tix[j] = (uint32_t)t;
+    if (is_new[j]) tstart[t] = j;
+    if (j == K - 1) tstart[t + 1] = K;
+    if (bad[j]) tbad[t] = 1;
+}
+
+// keep/drop per table: no order error and exactly one run (count == 1, or 1 + bytes <= max)
+__global__ void k_wal_tables(const uint64_t* __restrict__ NTp, const uint64_t* __restrict__ tstart,
+                             const uint64_t* __restrict__ Pw, const uint32_t* __restrict__ tbad, uint64_t max_size,
+                             uint64_t* run_len, uint64_t* keep) {
+    const uint64_t NT = *NTp;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= NT) return;
+    const uint64_t b = tstart[t], e = tstart[t + 1];
+    const uint64_t bytes = Pw[e] - Pw[b];
+    const bool ok = !tbad[t] && (e - b == 1 || 1 + bytes <= max_size);
+    run_len[t] = ok ? 1 + bytes : 0;
+    keep[t] = ok ? 1 : 0;
+}
+
+__global__ void k_wal_desc(const uint64_t* __restrict__ NTp, const uint64_t* __restrict__ tstart,
+                           const uint64_t* __restrict__ Pw, const uint64_t* __restrict__ Dp,
+                           const uint64_t* __restrict__ keep, const uint64_t* __restrict__ keep_ex,
+                           const uint64_t* __restrict__ run_off, const int64_t* __restrict__ tid,
+                           const uint32_t* __restrict__ strip, const uint32_t* __restrict__ m_rec,
+                           const uint32_t* __restrict__ rec_klen, DevRunDesc* descs) {
+    const uint64_t NT = *NTp;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= NT || !keep[t]) return;
+    const uint64_t b = tstart[t], e = tstart[t + 1];
+    DevRunDesc d;
+    d.off = run_off[t];
+    d.len = 1 + Pw[e] - Pw[b];
+    d.delete_count = Dp[e] - Dp[b];
+    d.put_count = (e - b) - d.delete_count;
+    d.min_key_off = d.off + 1 + 5;
+    d.min_key_len = rec_klen[m_rec[b]] - strip[b];
+    d.max_key_off = d.off + 1 + (Pw[e - 1] - Pw[b]) + 5;
+    d.max_key_len = rec_klen[m_rec[e - 1]] - strip[e - 1];
+    d.table_id = tid[b];
+    d.reserved = 0;
+    descs[keep_ex[t]] = d;
+}
+
+// output bytes of kept tables: version byte per run, then every record with its key_len rewritten
+// and the table prefix removed (WriteOperation::Put(key.split_off(..), value), :91-94). One
+// thread per record; records are small in WAL workloads (config 5: 49 bytes).
+__global__ void k_wal_gather(const uint64_t* __restrict__ Kp, const uint32_t* __restrict__ tix,
+                             const uint64_t* __restrict__ tstart, const uint64_t* __restrict__ keep,
+                             const uint64_t* __restrict__ run_off, const uint64_t* __restrict__ Pw,
+                             const uint32_t* __restrict__ strip, const uint64_t* __restrict__ m_src,
+                             const uint32_t* __restrict__ m_rec, const uint32_t* __restrict__ rec_klen,
+                             uint8_t* out) {
+    const uint64_t K = *Kp;
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= K) return;
+    const uint32_t t = tix[j];
+    if (!keep[t]) return;
+    const uint64_t b = tstart[t];
+    uint8_t* o = out + run_off[t];
+    if (j == b) o[0] = 1;  // CURRENT_VERSION (runs.rs:241-246)
+    o += 1 + (Pw[j] - Pw[b]);
+    const uint8_t* src = (const uint8_t*)m_src[j];
+    const uint32_t st = strip[j];
+    const uint32_t nk = rec_klen[m_rec[j]] - st;
+    o[0] = src[0];
+    o[1] = (uint8_t)(nk >> 24);
+    o[2] = (uint8_t)(nk >> 16);
+    o[3] = (uint8_t)(nk >> 8);
+    o[4] = (uint8_t)nk;
+    const uint64_t rest = (Pw[j + 1] - Pw[j]) - 5;  // stripped key + value part
+    const uint8_t* s = src + 5 + st;
+    for (uint64_t i = 0; i < rest; ++i) o[5 + i] = s[i];
+}
+
+void launch_wal_keys(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint32_t* m_rec,
+                     const uint32_t* rec_klen, const uint64_t* P, int64_t* tid, uint32_t* strip, uint64_t* wsize,
+                     unsigned long long* first_err) {
+    if (max_K)
+        k_wal_keys<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, m_src, m_rec, rec_klen, P, tid, strip, wsize, first_err);
+}
+void launch_wal_flags(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const int64_t* tid, const uint32_t* strip,
+                      const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen, uint64_t* is_new,
+                      uint32_t* bad) {
+    if (max_K)
+        k_wal_flags<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, tid, strip, m_src, m_rec, rec_klen, is_new, bad);
+}
+void launch_wal_index(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* is_new, const uint64_t* new_ex,
+                      const uint32_t* bad, uint32_t* tix, uint64_t* tstart, uint32_t* tbad) {
+    if (max_K) k_wal_index<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, is_new, new_ex, bad, tix, tstart, tbad);
+}
+void launch_wal_tables(hipStream_t s, const uint64_t* NTp, uint64_t max_NT, const uint64_t* tstart, const uint64_t* Pw,
+                       const uint32_t* tbad, uint64_t max_size, uint64_t* run_len, uint64_t* keep) {
+    if (max_NT) k_wal_tables<<<wal_blocks(max_NT, 256), 256, 0, s>>>(NTp, tstart, Pw, tbad, max_size, run_len, keep);
+}
+void launch_wal_desc(hipStream_t s, const uint64_t* NTp, uint64_t max_NT, const uint64_t* tstart, const uint64_t* Pw,
+                     const uint64_t* Dp, const uint64_t* keep, const uint64_t* keep_ex, const uint64_t* run_off,
+                     const int64_t* tid, const uint32_t* strip, const uint32_t* m_rec, const uint32_t* rec_klen,
+                     DevRunDesc* descs) {
+    if (max_NT)
+        k_wal_desc<<<wal_blocks(max_NT, 256), 256, 0, s>>>(NTp, tstart, Pw, Dp, keep, keep_ex, run_off, tid, strip,
+                                                           m_rec, rec_klen, descs);
+}
+void launch_wal_gather(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint32_t* tix, const uint64_t* tstart,
+                       const uint64_t* keep, const uint64_t* run_off, const uint64_t* Pw, const uint32_t* strip,
+                       const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen, uint8_t* out) {
+    if (max_K)
+        k_wal_gather<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, tix, tstart, keep, run_off, Pw, strip, m_src, m_rec,
+                                                            rec_klen, out);
+}
+
+}  // namespace skv

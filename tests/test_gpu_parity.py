@@ -41,12 +41,15 @@ def _norm(runs):
 
 
 def _run_both(dev, streams, max_size, flags):
+    """(oracle outcome, device outcome): ("ok", runs, dropped_tables) or ("err", code, text)."""
     try:
-        exp = ("ok", _norm(pyoracle.compact(streams, max_size, flags)))
+        runs, info = pyoracle.compact(streams, max_size, flags, with_result=True)
+        exp = ("ok", _norm(runs), info["dropped_tables"])
     except _abi.RunError as e:
         exp = ("err", e.code, e.message)
     try:
-        got = ("ok", _norm(dev.compact(streams, max_size, flags)))
+        runs, info = dev.compact(streams, max_size, flags, with_info=True)
+        got = ("ok", _norm(runs), info["dropped_tables"])
     except _abi.RunError as e:
         got = ("err", e.code, e.message)
     return exp, got
@@ -56,6 +59,8 @@ def _diff(exp, got):
     if exp[0] != got[0] or exp[0] == "err":
         return f"expected {exp[:3] if exp[0] == 'err' else 'ok'} got {got[:3] if got[0] == 'err' else 'ok'}"
     a, b = exp[1], got[1]
+    if exp[2] != got[2]:
+        return f"dropped tables {exp[2]} vs {got[2]}"
     if len(a) != len(b):
         return f"run count {len(a)} vs {len(b)}"
     for i, (x, y) in enumerate(zip(a, b)):
@@ -65,11 +70,7 @@ def _diff(exp, got):
     return "?"
 
 
-WAL = [c for c in CASES if c["flags"] & _abi.SKV_SPLIT_BY_TABLE]
-
-
-@pytest.mark.parametrize("case", [c for c in CASES if not (c["flags"] & _abi.SKV_SPLIT_BY_TABLE)],
-                         ids=lambda c: c["name"])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c["name"])
 def test_golden_fixture(dev, case):
     streams = [(s, [bytes.fromhex(r) for r in runs]) for s, runs in case["streams"]]
     exp = case["expect"]
@@ -78,7 +79,10 @@ def test_golden_fixture(dev, case):
             dev.compact(streams, case["max"], case["flags"])
         assert (ei.value.code, ei.value.message) == (exp["error_code"], exp["message"])
         return
-    runs = dev.compact(streams, case["max"], case["flags"])
+    runs, info = dev.compact(streams, case["max"], case["flags"], with_info=True)
+    if "dropped_tables" in exp:
+        assert info["dropped_tables"] == exp["dropped_tables"]
+    assert [r.table_id for r in runs] == [e.get("table_id", 0) for e in exp["runs"]]
     assert [r.data.hex() for r in runs] == [e["hex"] for e in exp["runs"]]
     assert [(r.stats.size_bytes, r.stats.put_count, r.stats.delete_count) for r in runs] == \
         [(e["size_bytes"], e["put_count"], e["delete_count"]) for e in exp["runs"]]
@@ -87,24 +91,57 @@ def test_golden_fixture(dev, case):
     assert hashlib.sha256(b"".join(r.data for r in runs)).hexdigest() == case["sha256"]
 
 
-@pytest.mark.parametrize("case", WAL, ids=lambda c: c["name"])
-def test_wal_mode_is_loudly_unsupported(dev, case):
-    """WAL split is not on the device path yet: it must fail loudly."""
-    streams = [(s, [bytes.fromhex(r) for r in runs]) for s, runs in case["streams"]]
+def test_wal_with_corrupt_stream_is_loudly_unsupported(dev):
+    """Documented gap: WAL split + an undecodable stream fails loudly."""
+    good = fmt.encode_run([fmt.put("1.a", b"x"), fmt.put("2.b", b"y")])
     with pytest.raises(_abi.RunError) as ei:
-        dev.compact(streams, case["max"], case["flags"])
+        dev.compact([(2, [good]), (1, [good[:-1]])], 4 * MiB, _abi.SKV_SPLIT_BY_TABLE)
     assert ei.value.code == _abi.SKV_E_UNSUPPORTED
+
+
+def test_wal_split_matches_oracle(dev):
+    """WAL compaction (wal_compaction.rs:66-174) on device: table split, prefix strip (incl. the
+    format!("{id}.") length quirk), one run per table, swallowed failing tables, bad keys."""
+    r = random.Random(17)
+    bad = []
+    n = 0
+    for trial in range(120):
+        n_streams = r.randint(1, 16)
+        tables = [r.choice(["7", "-3", "12", "007", "+5", "0", "9223372036854775807", "-9223372036854775808"])
+                  for _ in range(r.randint(1, 5))]
+        streams = []
+        for s in range(n_streams):
+            keys = sorted({f"{r.choice(tables)}.{r.randrange(10**4):04d}" for _ in range(r.randint(0, 60))})
+            if r.random() < 0.05:
+                keys = sorted(set(keys) | {r.choice(["nodot", "x.1", ".5", "99999999999999999999.z", "-.q"])})
+            ops = [fmt.put(k, bytes(r.randrange(256) for _ in range(r.randrange(0, 12)))) if r.random() < .85
+                   else fmt.delete(k) for k in keys]
+            streams.append((s + 1, [fmt.encode_run(ops)] if ops else []))
+        max_size = r.choice([40, 200, 1000, 4 * MiB])
+        exp, got = _run_both(dev, streams, max_size, _abi.SKV_SPLIT_BY_TABLE)
+        n += 1
+        if exp != got:
+            bad.append((trial, _diff(exp, got)))
+    assert not bad, bad[:5]
+
+
+def test_wal_config5_shape(dev):
+    """Config-5 record shape (32 B keys "{table}.{suffix}", 8 B values) at a 16-run fan-in like
+    the reference job (wal_compaction.rs:18), and at 1000 runs."""
+    for n_streams in (16, 1000):
+        streams = gen.config5(n_streams=n_streams)
+        exp, got = _run_both(dev, streams, 4 * MiB, _abi.SKV_SPLIT_BY_TABLE)
+        assert exp == got, _diff(exp, got)
 
 
 def test_random_cases_match_oracle(dev):
     """The oracle-vs-pyref domain (corrupt runs, unsorted streams, dups, tombstones, tiny
-    max sizes) through the GPU path; WAL and filter+unsorted cases are excluded here."""
+    max sizes, WAL splits) through the GPU path; the documented SKV_E_UNSUPPORTED gaps
+    (filter + unsorted input, WAL + undecodable/unsorted input) are skipped."""
     bad = []
     n = 0
     for seed in range(600):
         streams, max_size, flags = _case(seed)
-        if flags & _abi.SKV_SPLIT_BY_TABLE:
-            continue
         exp, got = _run_both(dev, streams, max_size, flags)
         if got[0] == "err" and got[1] == _abi.SKV_E_UNSUPPORTED:
             continue
