@@ -427,7 +427,8 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     };
     // order check + readback of its result, the record flags and (fast path) the broken-run flags
     auto check_and_read = [&](bool read_broken) -> bool {
-        launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
+        // the fast path's parse kernel already did the order check
+        if (!read_broken) launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
         HIPCHK(hipGetLastError());
         uint8_t* hp = (uint8_t*)pinned(ctx, k * 8 + 16 + (read_broken ? n_runs * 4 : 0));
         d2h(ctx, hp, d_first_dec, (size_t)k * 8);
@@ -465,7 +466,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
             alloc_records();
             h2d(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
             launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
-                               rec_meta, d_flags);
+                               rec_meta, d_flags, d_stream_base, d_first_dec);
             mark(ctx, PH_PARSE);
             parsed = !check_and_read(true);
             if (!parsed) {  // a run is not what its first record promised: general parse

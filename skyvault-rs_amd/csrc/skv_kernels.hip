@@ -357,25 +357,73 @@ __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, 
                              const RunFmt* __restrict__ fmt, uint32_t* run_broken,
                              const uint64_t* __restrict__ run_recb, uint64_t* __restrict__ rec_addr,
                              uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
-                             uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= R_total) return;
-    uint32_t lo = 0, hi = n_runs;  // last run with run_recb <= i
-    while (hi - lo > 1) {
-        uint32_t mid = (lo + hi) >> 1;
-        if (run_recb[mid] <= i) lo = mid;
-        else hi = mid;
+                             uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags,
+                             const uint64_t* __restrict__ stream_base, unsigned long long* first_dec) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool act = i < R_total;
+    uint32_t lo = 0;
+    RunFmt f{0, 0, 0};
+    const uint8_t* run = nullptr;
+    uint64_t p = 0, len = 0;
+    RecHdr h{};
+    if (act) {
+        uint32_t hi = n_runs;  // last run with run_recb <= i
+        while (hi - lo > 1) {
+            uint32_t mid = (lo + hi) >> 1;
+            if (run_recb[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        f = fmt[lo];
+        if (!VERIFY && (!f.S || run_broken[lo])) act = false;
     }
-    const RunFmt f = fmt[lo];
-    if (!VERIFY && (!f.S || run_broken[lo])) return;
-    const uint8_t* run = (const uint8_t*)runs[lo].ptr;
-    uint64_t p = 1 + (i - run_recb[lo]) * f.S;
-    RecHdr h = parse_rec<true>(run, runs[lo].len, p);
-    if (VERIFY && (h.err || h.size != f.S)) {
-        atomicOr(&run_broken[lo], 1u);
-        return;
+    if (act) {
+        run = (const uint8_t*)runs[lo].ptr;
+        len = runs[lo].len;
+        p = 1 + (i - run_recb[lo]) * f.S;
+        h = parse_rec<true>(run, len, p);
+        if (VERIFY && (h.err || h.size != f.S)) {
+            atomicOr(&run_broken[lo], 1u);
+            act = false;
+        }
+        if (act) put_rec(i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
     }
-    put_rec(i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
+    if (!VERIFY) return;
+    // fused order check (runs.rs:190-198 as k_order_check does it): compare with the previous
+    // record of the same stream — the neighbouring lane's, or parsed here at a run / wave edge
+    const int lane = threadIdx.x & 63;
+    uint64_t phi = __shfl_up(h.hi, 1, 64), plo = __shfl_up(h.lo, 1, 64);
+    uint64_t paddr = __shfl_up((uint64_t)(uintptr_t)(run + p), 1, 64);
+    uint32_t pkl = __shfl_up((uint32_t)h.klen, 1, 64);
+    uint32_t prun = __shfl_up(lo, 1, 64);
+    int pact = __shfl_up(act ? 1 : 0, 1, 64);
+    if (!act) return;
+    const uint64_t local = i - run_recb[lo];
+    if (lane == 0 || prun != lo || !pact) {
+        const uint8_t* prev = nullptr;
+        uint64_t pl = 0, pp = 0;
+        if (local > 0) {
+            prev = run;
+            pl = len;
+            pp = p - f.S;
+        } else if (lo > 0 && runs[lo - 1].stream == runs[lo].stream) {  // L0-style concatenation
+            const RunFmt pf = fmt[lo - 1];
+            prev = (const uint8_t*)runs[lo - 1].ptr;
+            pl = runs[lo - 1].len;
+            pp = 1 + (run_recb[lo] - 1 - run_recb[lo - 1]) * pf.S;
+        }
+        if (!prev) return;  // first record of its stream
+        RecHdr ph = parse_rec<true>(prev, pl, pp);
+        phi = ph.hi;
+        plo = ph.lo;
+        pkl = (uint32_t)ph.klen;
+        paddr = (uint64_t)(uintptr_t)(prev + pp);
+    }
+    const int c = key_cmp(phi, plo, pkl, (const uint8_t*)paddr + 5, h.hi, h.lo, (uint32_t)h.klen, run + p + 5);
+    if (c > 0) {
+        const uint32_t sidx = runs[lo].stream;
+        atomicMin(&first_dec[sidx], (unsigned long long)(i - 1 - stream_base[sidx]));
+        atomicOr(flags + 1, 1u);
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1361,15 +1409,18 @@ void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n
         k_emit<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, fmt, run_broken, ch_start, ch_rec_base,
                                                          rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
     if (R)
-        k_emit_fixed<false><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, R, fmt, (uint32_t*)run_broken, run_recb, rec_addr,
-                                                               rec_hi, rec_lo, rec_klen, rec_meta, flags);
+        k_emit_fixed<false><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, R, fmt, (uint32_t*)run_broken, run_recb,
+                                                               rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags,
+                                                               nullptr, nullptr);
 }
 void launch_parse_fixed(hipStream_t s, const RunInfo* runs, uint32_t n_runs, const RunFmt* fmt, uint32_t* run_broken,
                         const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
-                        uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags) {
+                        uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, const uint64_t* stream_base,
+                        unsigned long long* first_dec) {
     if (R)
         k_emit_fixed<true><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, R, fmt, run_broken, run_recb, rec_addr,
-                                                              rec_hi, rec_lo, rec_klen, rec_meta, flags);
+                                                              rec_hi, rec_lo, rec_klen, rec_meta, flags, stream_base,
+                                                              first_dec);
 }
 void launch_order_check(hipStream_t s, uint64_t R, const uint64_t* stream_base, uint32_t k, const uint64_t* rec_addr,
                         const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,

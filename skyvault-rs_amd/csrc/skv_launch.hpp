@@ -26,7 +26,8 @@ void launch_emit(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_c
                  uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags);
 void launch_parse_fixed(hipStream_t, const RunInfo* runs, uint32_t n_runs, const RunFmt* fmt, uint32_t* run_broken,
                         const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
-                        uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags);
+                        uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, const uint64_t* stream_base,
+                        unsigned long long* first_dec);
 void launch_order_check(hipStream_t, uint64_t R, const uint64_t* stream_base, uint32_t k, const uint64_t* rec_addr,
                         const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,
                         unsigned long long* first_dec, uint32_t* any_dec);
