@@ -29,7 +29,11 @@ constexpr int TILE_THREADS = SKV_TILE_THREADS;
 #define SKV_GATHER_SEG 256
 #endif
 constexpr int GATHER_SEG = SKV_GATHER_SEG;      // surviving records per gather workgroup
-constexpr int GATHER_THREADS = SKV_GATHER_SEG;  // one lane per record in the setup phase
+#ifndef SKV_GATHER_THREADS
+#define SKV_GATHER_THREADS SKV_GATHER_SEG
+#endif
+constexpr int GATHER_THREADS = SKV_GATHER_THREADS;  // >= GATHER_SEG: one lane per record in the setup
+static_assert(SKV_GATHER_THREADS >= SKV_GATHER_SEG && SKV_GATHER_THREADS % 64 == 0, "gather block shape");
 constexpr int GATHER_TBL = 23 * SKV_GATHER_SEG; // output 16-byte blocks per gather workgroup with a direct piece table
 #ifndef SKV_GATHER_U
 #define SKV_GATHER_U 2                   // output blocks per lane in flight in k_gather
@@ -37,6 +41,17 @@ constexpr int GATHER_TBL = 23 * SKV_GATHER_SEG; // output 16-byte blocks per gat
 #ifndef SKV_GATHER_WAVES
 #define SKV_GATHER_WAVES 8               // k_gather register budget: waves per SIMD (64 VGPRs at 8)
 #endif
+#ifndef SKV_PAGE_U
+#define SKV_PAGE_U 4                     // page gather: 16-byte output blocks per lane
+#endif
+#ifndef SKV_PAGE_WAVES
+#define SKV_PAGE_WAVES 5                 // k_gather_pages register budget (waves per SIMD)
+#endif
+#ifndef SKV_PAGE_GATHER
+#define SKV_PAGE_GATHER 0                // 1: page gather (k_page_prep + k_gather_pages), 0: segment gather
+#endif
+constexpr int PAGE_U = SKV_PAGE_U;
+constexpr uint64_t PAGE_BYTES = 16ull * 256 * SKV_PAGE_U;
 #ifndef SKV_GATHER_NT
 #define SKV_GATHER_NT 1                  // 1: non-temporal output stores (written once, never re-read)
 #endif

@@ -695,7 +695,18 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     for (const InStream& S : job.ranked)
         for (uint64_t l : S.lens) total_rec_bytes += l;
     uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + R + 16);
+#if SKV_PAGE_GATHER
+    {
+        const uint64_t max_out = total_rec_bytes + R + 16;
+        uint64_t* Dst = dbuf<uint64_t>(ctx, "g_dst", R + 1);
+        uint32_t* page_first = dbuf<uint32_t>(ctx, "g_page_first", max_out / PAGE_BYTES + 2);
+        launch_page_prep(st, d_K, d_nruns, run_b, m_P, seg_r0, Dst, page_first, R);
+        mark(ctx, PH_CHAIN);
+        launch_gather_pages(st, d_K, d_nruns, m_P, Dst, m_src, page_first, d_out, max_out);
+    }
+#else
     launch_gather(st, d_K, d_nruns, run_b, m_P, m_src, seg_r0, d_out, R);
+#endif
     HIPCHK(hipGetLastError());
     mark(ctx, PH_GATHER);
     // ---- readback ---------------------------------------------------------------------------

@@ -71,6 +71,10 @@ void launch_wal_desc(hipStream_t, const uint64_t* NTp, uint64_t max_NT, const ui
 void launch_wal_gather(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint32_t* tix, const uint64_t* tstart,
                        const uint64_t* keep, const uint64_t* run_off, const uint64_t* Pw, const uint32_t* strip,
                        const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen, uint8_t* out);
+void launch_page_prep(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
+                      const uint64_t* seg_r0, uint64_t* Dst, uint32_t* page_first, uint64_t max_K);
+void launch_gather_pages(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* P, const uint64_t* Dst,
+                         const uint64_t* m_src, const uint32_t* page_first, uint8_t* out, uint64_t max_out_bytes);
 uint64_t scan_tmp_words(uint64_t n);
 void launch_scan(hipStream_t, const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tmp);
 }  // namespace skv
