@@ -95,12 +95,16 @@ struct TileOut {
     uint64_t* ohi;
     uint64_t* olo;
     uint64_t* oc;
-    // level 0: surviving records of the tile, in merged order, at tile_base + rank
-    uint32_t* t_rec;
-    uint32_t* t_meta;
-    uint64_t* tile_kept;
-    uint64_t* tile_bytes;
-    uint64_t* tile_dels;
+    // level 0: the dense merged arrays (k_tile emits them directly, decoupled look-back)
+    uint32_t* m_rec;      // rec index of the g-th surviving record
+    uint64_t* m_src;      // its source address
+    uint64_t* m_P;        // output-byte prefix (m_P[K] = total)
+    uint64_t* m_Dp;       // delete-count prefix
+    uint32_t* tile_mm;    // (min, max) surviving record size per tile
+    uint64_t* tstate;     // look-back words, 3 per tile (zeroed per call)
+    uint32_t* tcounter;   // tile ticket (zeroed per call)
+    uint64_t* Kout;       // K = surviving records
+    uint64_t T;           // level-0 tile count
     // global scratch for tiles larger than TILE_CAP
     uint64_t* xhi;
     uint64_t* xlo;

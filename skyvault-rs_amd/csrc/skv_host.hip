@@ -76,6 +76,11 @@ struct skv_ctx {
     hipEvent_t ev[PH_N] = {};
     void* pinned = nullptr;  // small readback staging
     size_t pinned_cap = 0;
+    // pinned upload arena: small host tables are staged here so their H2D copies are truly async
+    // (a copy from pageable memory stalls the host); chunks live until the ctx is destroyed and
+    // are reused from the start on every call (each call ends with a stream sync)
+    std::vector<std::pair<uint8_t*, size_t>> up_chunks;
+    size_t up_chunk = 0, up_off = 0;
     uint64_t syncs = 0;
 };
 
@@ -137,6 +142,28 @@ static void* pinned(skv_ctx* ctx, size_t bytes) {
         ctx->pinned_cap = cap;
     }
     return ctx->pinned;
+}
+
+// async H2D of a host table through the pinned upload arena
+static void h2d_up(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!bytes) return;
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    while (ctx->up_chunk < ctx->up_chunks.size() &&
+           ctx->up_off + need > ctx->up_chunks[ctx->up_chunk].second) {
+        ++ctx->up_chunk;
+        ctx->up_off = 0;
+    }
+    if (ctx->up_chunk == ctx->up_chunks.size()) {
+        const size_t cap = std::max<size_t>(need, 1 << 20);
+        void* p = nullptr;
+        HIPCHK(hipHostMalloc(&p, cap, hipHostMallocDefault));
+        ctx->up_chunks.emplace_back((uint8_t*)p, cap);
+        ctx->up_off = 0;
+    }
+    uint8_t* stage = ctx->up_chunks[ctx->up_chunk].first + ctx->up_off;
+    ctx->up_off += need;
+    memcpy(stage, src, bytes);
+    HIPCHK(hipMemcpyAsync(dst, stage, bytes, hipMemcpyHostToDevice, ctx->stream));
 }
 
 static void d2h(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
@@ -330,6 +357,8 @@ static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
 static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     hipStream_t st = ctx->stream;
     ctx->syncs = 0;
+    ctx->up_chunk = 0;
+    ctx->up_off = 0;
     mark(ctx, PH_START);
     const uint32_t k = (uint32_t)job.ranked.size();
     // ---- run table ------------------------------------------------------------------------
@@ -367,10 +396,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "scan_tmp", scan_tmp_words(std::max<uint64_t>(n_chunks, 1 << 20)) + 64);
     RunSummary* d_sum = dbuf<RunSummary>(ctx, "run_sum", n_runs);
 
-    h2d(ctx, d_runs, runs.data(), n_runs * sizeof(RunInfo));
-    HIPCHK(hipMemsetAsync(bad_bits, 0, (n_chunks / 64 + 1) * 8, st));
-    HIPCHK(hipMemsetAsync(first_bad, 0xFF, n_runs * 4, st));
-    HIPCHK(hipMemsetAsync(err_chunk, 0xFF, n_runs * 4, st));
+    h2d_up(ctx, d_runs, runs.data(), n_runs * sizeof(RunInfo));
     RunFmt* d_fmt = dbuf<RunFmt>(ctx, "run_fmt", n_runs);
     uint32_t* d_broken = dbuf<uint32_t>(ctx, "run_broken", n_runs);
     uint64_t* d_recb = dbuf<uint64_t>(ctx, "run_recb", n_runs + 1);
@@ -423,7 +449,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
         rec_meta = dbuf<uint32_t>(ctx, "rec_meta", R);
         HIPCHK(hipMemsetAsync(d_flags, 0, 16, st));
         HIPCHK(hipMemsetAsync(d_first_dec, 0xFF, (size_t)k * 8, st));
-        h2d(ctx, d_stream_base, stream_base.data(), (k + 1) * 8);
+        h2d_up(ctx, d_stream_base, stream_base.data(), (k + 1) * 8);
     };
     // order check + readback of its result, the record flags and (fast path) the broken-run flags
     auto check_and_read = [&](bool read_broken) -> bool {
@@ -464,7 +490,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
             R = recb[n_runs];
             stream_tables();
             alloc_records();
-            h2d(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
+            h2d_up(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
             launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
                                rec_meta, d_flags, d_stream_base, d_first_dec);
             mark(ctx, PH_PARSE);
@@ -478,6 +504,9 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     }
     // ---- general path: speculative chunk walks ----------------------------------------------
     if (!parsed) {
+        HIPCHK(hipMemsetAsync(bad_bits, 0, (n_chunks / 64 + 1) * 8, st));
+        HIPCHK(hipMemsetAsync(first_bad, 0xFF, n_runs * 4, st));
+        HIPCHK(hipMemsetAsync(err_chunk, 0xFF, n_runs * 4, st));
         launch_spec(st, d_runs, n_runs, n_chunks, d_hdr, d_fmt, d_broken, ch_start, ch_end, ch_cnt, ch_err);
         launch_validate(st, d_runs, n_runs, n_chunks, d_hdr, ch_start, ch_end, ch_err, bad_bits, first_bad);
         launch_fixup(st, d_runs, n_runs, d_hdr, first_bad, bad_bits, ch_start, ch_end, ch_cnt, ch_err);
@@ -612,14 +641,18 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
         snprintf(nm, sizeof nm, "lv%d_lo", li); L.lo = dbuf<uint64_t>(ctx, nm, L.N);
         snprintf(nm, sizeof nm, "lv%d_c", li); L.c = dbuf<uint64_t>(ctx, nm, L.N);
         snprintf(nm, sizeof nm, "lv%d_off", li); L.d_off = dbuf<uint64_t>(ctx, nm, k + 1);
-        h2d(ctx, L.d_off, L.off.data(), (k + 1) * 8);
+        h2d_up(ctx, L.d_off, L.off.data(), (k + 1) * 8);
         launch_sample(st, li == 1, P.hi, P.lo, P.c, rec_klen, P.d_off, L.d_off, k, L.S, L.N, L.hi, L.lo, L.c);
         lv.push_back(L);
     }
     // top-down: sort each sample level, derive splitters for the level below
     uint64_t T0 = 1;
-    uint64_t* d_tile_base0 = nullptr;
-    TileOut O0{};
+    uint32_t* m_rec = dbuf<uint32_t>(ctx, "m_rec", R + 1);
+    uint64_t* m_src = dbuf<uint64_t>(ctx, "m_src", R + 1);
+    uint64_t* m_P = dbuf<uint64_t>(ctx, "m_P", R + 1);
+    uint64_t* m_Dp = dbuf<uint64_t>(ctx, "m_Dp", R + 1);
+    uint64_t* d_Kout = dbuf<uint64_t>(ctx, "K_out", 1);
+    uint32_t* tile_max = nullptr;
     for (int li = (int)lv.size() - 1; li >= 0; --li) {
         Level& L = lv[li];
         const bool l0 = li == 0;
@@ -646,11 +679,17 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
         snprintf(nm, sizeof nm, "x%d_c", li); O.xc = dbuf<uint64_t>(ctx, nm, L.N);
         if (l0) {
             O.xmeta = dbuf<uint32_t>(ctx, "x0_meta", L.N);
-            O.t_rec = dbuf<uint32_t>(ctx, "t_rec", L.N);
-            O.t_meta = dbuf<uint32_t>(ctx, "t_meta", L.N);
-            O.tile_kept = dbuf<uint64_t>(ctx, "tile_kept", T);
-            O.tile_bytes = dbuf<uint64_t>(ctx, "tile_bytes", T);
-            O.tile_dels = dbuf<uint64_t>(ctx, "tile_dels", T);
+            O.m_rec = m_rec;
+            O.m_src = m_src;
+            O.m_P = m_P;
+            O.m_Dp = m_Dp;
+            O.Kout = d_Kout;
+            O.T = T;
+            tile_max = O.tile_mm = dbuf<uint32_t>(ctx, "tile_mm", 2 * T);  // (min, max) record size per tile
+            O.tstate = dbuf<uint64_t>(ctx, "tile_state", 3 * T);
+            O.tcounter = dbuf<uint32_t>(ctx, "tile_ticket", 1);
+            HIPCHK(hipMemsetAsync(O.tstate, 0, 3 * T * 8, st));
+            HIPCHK(hipMemsetAsync(O.tcounter, 0, 4, st));
         } else {
             snprintf(nm, sizeof nm, "s%d_hi", li); L.shi = O.ohi = dbuf<uint64_t>(ctx, nm, L.N);
             snprintf(nm, sizeof nm, "s%d_lo", li); L.slo = O.olo = dbuf<uint64_t>(ctx, nm, L.N);
@@ -658,33 +697,15 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
         }
         HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, rec_klen, bounds, k, T, tile_base, rec_meta, rec_addr,
                            (job.flags & SKV_DROP_TOMBSTONES) ? 1u : 0u, O));
-        if (l0) {
-            T0 = T;
-            d_tile_base0 = tile_base;
-            O0 = O;
-        }
+        if (l0) T0 = T;
     }
-    // dense merged arrays
-    uint64_t* kept_base = dbuf<uint64_t>(ctx, "kept_base", T0 + 1);
-    uint64_t* byte_base = dbuf<uint64_t>(ctx, "byte_base", T0 + 1);
-    uint64_t* del_base = dbuf<uint64_t>(ctx, "del_base", T0 + 1);
-    launch_scan(st, O0.tile_kept, T0, kept_base, scan_tmp);
-    launch_scan(st, O0.tile_bytes, T0, byte_base, scan_tmp);
-    launch_scan(st, O0.tile_dels, T0, del_base, scan_tmp);
-    uint32_t* m_rec = dbuf<uint32_t>(ctx, "m_rec", R + 1);
-    uint64_t* m_src = dbuf<uint64_t>(ctx, "m_src", R + 1);
-    uint64_t* m_P = dbuf<uint64_t>(ctx, "m_P", R + 1);
-    uint64_t* m_Dp = dbuf<uint64_t>(ctx, "m_Dp", R + 1);
-    uint32_t* tile_max = dbuf<uint32_t>(ctx, "tile_max", 2 * T0);  // (min, max) record size per tile
-    launch_finalize(st, T0, d_tile_base0, O0.tile_kept, kept_base, byte_base, del_base, O0.t_rec, O0.t_meta, rec_addr,
-                    m_rec, m_src, m_P, m_Dp, tile_max);
     HIPCHK(hipGetLastError());
     mark(ctx, PH_MERGE);
-    const uint64_t* d_K = kept_base + T0;
+    const uint64_t* d_K = d_Kout;
     if (job.flags & SKV_SPLIT_BY_TABLE) return wal_stage(ctx, job, R, d_K, m_rec, m_src, m_P, m_Dp, rec_addr, rec_klen, out);
     // ---- chain + stats ----------------------------------------------------------------------
     uint64_t* run_b = dbuf<uint64_t>(ctx, "run_b", R + 2);
-    uint64_t* d_nruns = dbuf<uint64_t>(ctx, "n_runs", 2);
+    uint64_t* d_nruns = dbuf<uint64_t>(ctx, "n_runs", 4);  // {runs, K, P[K]} (k_chain)
     DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", R + 1);
     uint64_t* seg_r0 = dbuf<uint64_t>(ctx, "seg_r0", R / GATHER_SEG + 2);
     launch_chain(st, d_K, m_P, job.max_run_size, tile_max, T0, run_b, d_nruns);
@@ -709,23 +730,26 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
 #endif
     HIPCHK(hipGetLastError());
     mark(ctx, PH_GATHER);
-    // ---- readback ---------------------------------------------------------------------------
+    // ---- readback: summary + descriptors in one sync (descriptor count guessed from sizes) -------
+    static_assert(sizeof(skv_run_desc) == sizeof(DevRunDesc), "desc layout");
+    const uint64_t guess = std::min<uint64_t>(
+        R + 1, job.max_run_size > 1 ? 2 * (total_rec_bytes / (job.max_run_size - 1)) + 64 : R + 1);
     uint64_t h3[4];
-    {
-        uint64_t* hp = (uint64_t*)pinned(ctx, 64);
-        d2h(ctx, hp, d_nruns, 8);
-        d2h(ctx, hp + 1, d_K, 8);
-        sync(ctx);
-        memcpy(h3, hp, 16);
-    }
-    const uint64_t n_out_runs = h3[0], K = h3[1];
-    uint64_t kept_bytes = 0;
-    HIPCHK(hipMemcpy(&kept_bytes, m_P + K, 8, hipMemcpyDeviceToHost));
     ResultBox* box = new ResultBox();
     skv_result* res = &box->pub;
-    res->runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, n_out_runs) * sizeof(skv_run_desc));
-    static_assert(sizeof(skv_run_desc) == sizeof(DevRunDesc), "desc layout");
-    if (n_out_runs) HIPCHK(hipMemcpy(res->runs, d_desc, n_out_runs * sizeof(DevRunDesc), hipMemcpyDeviceToHost));
+    {
+        uint8_t* hp = (uint8_t*)pinned(ctx, 64 + guess * sizeof(DevRunDesc));
+        d2h(ctx, hp, d_nruns, 24);
+        d2h(ctx, hp + 64, d_desc, guess * sizeof(DevRunDesc));
+        sync(ctx);
+        memcpy(h3, hp, 24);
+        const uint64_t n = h3[0];
+        res->runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, n) * sizeof(skv_run_desc));
+        memcpy(res->runs, hp + 64, std::min(n, guess) * sizeof(DevRunDesc));
+        if (n > guess)
+            HIPCHK(hipMemcpy(res->runs + guess, d_desc + guess, (n - guess) * sizeof(DevRunDesc), hipMemcpyDeviceToHost));
+    }
+    const uint64_t n_out_runs = h3[0], K = h3[1], kept_bytes = h3[2];
     res->n_runs = n_out_runs;
     res->bytes = d_out;
     res->n_bytes = kept_bytes + n_out_runs;
@@ -834,6 +858,7 @@ void skv_ctx_destroy(skv_ctx* ctx) {
     for (auto& kv : ctx->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    for (auto& c : ctx->up_chunks) (void)hipHostFree(c.first);
     for (int i = 0; i < PH_N; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
     (void)hipStreamDestroy(ctx->stream);

@@ -4,7 +4,7 @@
 //   parse   k_run_header, k_spec, k_validate, k_fixup, k_err_chunk, k_mask, scan, k_run_summary,
 //           k_emit           — runs::read_run_stream (runs.rs:517-628) for every input run at once
 //   check   k_order_check    — first in-stream key decrease (what build_runs rejects, runs.rs:190-198)
-//   merge   k_sample, k_bounds, k_tile_n, k_tile<L0>, k_finalize
+//   merge   k_sample, k_bounds, k_tile_n, k_tile<L0> (level 0 emits the merged arrays)
 //                            — k_way::merge (k_way.rs:113-179): order by (key asc, seq_no desc),
 //                              keep the first record per key, drop Deletes at Level::max
 //                              (table_tree_compaction.rs:139-145)
@@ -571,73 +571,92 @@ __device__ __forceinline__ uint32_t seg_of(const uint32_t* cb, uint32_t m, uint3
     return lo;
 }
 
-// Output stage of an LDS tile. Position i of the merged tile: hi = mh[i], element mi[i] (its lo and
-// c in el_lo / el_c); level 0 also has meta by position in pmeta.
-template <bool L0>
-__device__ void tile_output(uint32_t n, const uint64_t* mh, const uint16_t* mi, const uint64_t* el_lo,
-                            const uint64_t* el_c, const uint32_t* pmeta, uint64_t base, uint64_t t, bool drop_deletes,
-                            const uint64_t* rec_addr, const TileOut& O, uint64_t* ws) {
-    if (!L0) {
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-            uint32_t e = mi[i];
-            O.ohi[base + i] = mh[i];
-            O.olo[base + i] = el_lo[e];
-            O.oc[base + i] = el_c[e];
-        }
-        return;
+// Output stage of a level > 0 LDS tile (sorted samples): position i has hi = mh[i] and element
+// mi[i] (its lo and c in el_lo / el_c).
+__device__ void tile_output_samples(uint32_t n, const uint64_t* mh, const uint16_t* mi, const uint64_t* el_lo,
+                                    const uint64_t* el_c, uint64_t base, const TileOut& O) {
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        uint32_t e = mi[i];
+        O.ohi[base + i] = mh[i];
+        O.olo[base + i] = el_lo[e];
+        O.oc[base + i] = el_c[e];
     }
-    // dedup (first per key survives: k_way.rs:146-151) + Delete filter, order-preserving compaction
-    constexpr int PER = TILE_CAP / TILE_THREADS;
-    uint32_t i0 = threadIdx.x * PER;
-    uint32_t keep_mask = 0, nk = 0;
-    uint64_t bytes = 0, dels = 0;
-    uint32_t idx[PER], mt[PER];
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        uint32_t i = i0 + q;
-        idx[q] = 0;
-        mt[q] = 0;
-        if (i < n) {
-            uint32_t e = mi[i];
-            uint64_t h = mh[i], l = el_lo[e], c = el_c[e];
-            bool first = true;
-            if (i > 0) {
-                uint64_t ph = mh[i - 1];
-                if (ph == h) {
-                    uint32_t p = mi[i - 1];
-                    first = ekey_cmp(rec_addr, ph, el_lo[p], el_c[p], h, l, c) != 0;
+}
+
+// Decoupled look-back over tiles (single pass, no separate scan kernel): tile t publishes its
+// (kept, bytes, deletes) aggregate, adds up its predecessors' until one with an inclusive prefix,
+// then publishes its own inclusive prefix. Each counter is one 64-bit word (flag in bits 62-63),
+// stored and polled with 8-byte agent-scope atomics — no payload rides on the flag. Tile ids come
+// from an atomic ticket, so every predecessor of a waiting tile is resident or done.
+__device__ void tile_lookback(uint64_t* st, uint64_t t, uint64_t a0, uint64_t a1, uint64_t a2, uint64_t* s_ex) {
+    if (threadIdx.x < 3) {
+        const uint32_t q = threadIdx.x;
+        const uint64_t agg = q == 0 ? a0 : (q == 1 ? a1 : a2);
+        constexpr uint64_t FA = 1ull << 62, FI = 2ull << 62, VM = FA - 1;
+        uint64_t acc = 0;
+        if (t == 0) {
+            __hip_atomic_store(&st[q], FI | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&st[3 * t + q], FA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t p = t - 1;
+            for (;;) {
+                const uint64_t v = __hip_atomic_load(&st[3 * p + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t f = v >> 62;
+                if (f == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
                 }
+                acc += v & VM;
+                if (f == 2) break;
+                --p;
             }
-            uint32_t meta = pmeta[i];
-            bool del = (meta >> 31) != 0;
-            bool keep = first && !(drop_deletes && del);
-            idx[q] = (uint32_t)c;
-            mt[q] = meta;
-            if (keep) {
-                keep_mask |= 1u << q;
-                ++nk;
-                bytes += meta & 0x7FFFFFFFu;
-                dels += del ? 1 : 0;
-            }
+            __hip_atomic_store(&st[3 * t + q], FI | (acc + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        s_ex[q] = acc;
     }
-    uint64_t tot;
-    uint64_t rank = block_excl_scan<uint64_t>(nk, ws, tot);
+    __syncthreads();
+}
+
+// block-wide min / max of a record size (for k_chain's uniform-size and all-fit tests)
+__device__ void tile_minmax(uint32_t mn, uint32_t mx, uint32_t* s_mm, uint32_t* out) {
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        if (keep_mask & (1u << q)) {
-            O.t_rec[base + rank] = idx[q];
-            O.t_meta[base + rank] = mt[q];
-            ++rank;
-        }
+    for (int d = 32; d >= 1; d >>= 1) {
+        uint32_t o = __shfl_xor(mx, d, 64);
+        mx = o > mx ? o : mx;
+        o = __shfl_xor(mn, d, 64);
+        mn = o < mn ? o : mn;
     }
-    uint64_t tb = block_reduce_sum<uint64_t>(bytes, ws);
-    uint64_t td = block_reduce_sum<uint64_t>(dels, ws);
+    if ((threadIdx.x & 63) == 0) {
+        s_mm[2 * (threadIdx.x >> 6)] = mn;
+        s_mm[2 * (threadIdx.x >> 6) + 1] = mx;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        O.tile_kept[t] = tot;
-        O.tile_bytes[t] = tb;
-        O.tile_dels[t] = td;
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            mn = s_mm[2 * w] < mn ? s_mm[2 * w] : mn;
+            mx = s_mm[2 * w + 1] > mx ? s_mm[2 * w + 1] : mx;
+        }
+        out[0] = mn;
+        out[1] = mx;
     }
+}
+
+// the dense merged arrays of k_way::merge's output (k_way.rs:146-151: first record per key; the
+// Delete filter of table_tree_compaction.rs:139-145 when asked) at global record g:
+// rec index, source address, output-byte prefix P, delete-count prefix
+__device__ __forceinline__ void emit_merged(const TileOut& O, uint64_t g, uint32_t idx, uint64_t addr, uint64_t pb,
+                                            uint64_t pd) {
+    O.m_rec[g] = idx;
+    O.m_src[g] = addr;
+    O.m_P[g] = pb;
+    O.m_Dp[g] = pd;
+}
+
+// after the last tile: K, P[K], Dp[K]
+__device__ __forceinline__ void emit_totals(const TileOut& O, uint64_t K, uint64_t B, uint64_t D) {
+    O.Kout[0] = K;
+    O.m_P[K] = B;
+    O.m_Dp[K] = D;
 }
 
 // Tiles larger than TILE_CAP: bitonic sort in global scratch (ascending-comparator form, so
@@ -697,34 +716,45 @@ __device__ void tile_big(Elems E, const uint64_t* bounds, uint32_t k, uint64_t t
         }
         return;
     }
-    uint64_t kept = 0, bytes = 0, dels = 0;
+    // pass 1: this tile's totals (dedup + filter), then its global prefix
+    auto keep_at = [&](uint32_t i, uint32_t& m) -> bool {
+        const bool first = i == 0 || ekey_cmp(rec_addr, xh[i - 1], xl[i - 1], xc[i - 1], xh[i], xl[i], xc[i]) != 0;
+        m = xm[i];
+        return first && !(drop_deletes && (m >> 31));
+    };
+    uint64_t kd = 0, bytes = 0;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        uint32_t m;
+        if (keep_at(i, m)) {
+            kd += 1 | ((uint64_t)(m >> 31) << 32);
+            bytes += m & 0x7FFFFFFFu;
+            mn = (m & 0x7FFFFFFFu) < mn ? (m & 0x7FFFFFFFu) : mn;
+            mx = (m & 0x7FFFFFFFu) > mx ? (m & 0x7FFFFFFFu) : mx;
+        }
+    }
+    const uint64_t kd_tot = block_reduce_sum<uint64_t>(kd, ws);
+    const uint64_t b_tot = block_reduce_sum<uint64_t>(bytes, ws);
+    tile_minmax(mn, mx, s_flag, O.tile_mm + 2 * t);
+    tile_lookback(O.tstate, t, kd_tot & 0xFFFFFFFFull, b_tot, kd_tot >> 32, ws + 8);
+    uint64_t g = ws[8], pb = ws[9], pd = ws[10];
+    __syncthreads();
+    if (t == O.T - 1 && threadIdx.x == 0) emit_totals(O, g + (kd_tot & 0xFFFFFFFFull), pb + b_tot, pd + (kd_tot >> 32));
+    // pass 2: write the survivors in order
     for (uint32_t b0 = 0; b0 < n; b0 += blockDim.x) {
-        uint32_t i = b0 + threadIdx.x;
-        bool keep = false;
+        const uint32_t i = b0 + threadIdx.x;
         uint32_t m = 0;
-        if (i < n) {
-            bool first = i == 0 || ekey_cmp(rec_addr, xh[i - 1], xl[i - 1], xc[i - 1], xh[i], xl[i], xc[i]) != 0;
-            m = xm[i];
-            keep = first && !(drop_deletes && (m >> 31));
-        }
-        uint64_t tot;
-        uint64_t r = block_excl_scan<uint64_t>(keep ? 1 : 0, ws, tot);
-        // all reads of this block are done before any writes of it (output region == base..)
-        __syncthreads();
-        if (keep) {
-            O.t_rec[base + kept + r] = (uint32_t)xc[i];
-            O.t_meta[base + kept + r] = m;
-        }
-        kept += tot;
-        bytes += block_reduce_sum<uint64_t>(keep ? (m & 0x7FFFFFFFu) : 0, ws);
-        dels += block_reduce_sum<uint64_t>(keep && (m >> 31) ? 1 : 0, ws);
+        const bool keep = i < n && keep_at(i, m);
+        const uint64_t sz = keep ? (m & 0x7FFFFFFFu) : 0, dl = keep ? (m >> 31) : 0;
+        uint64_t ck, cb_, cd;
+        const uint64_t rk = block_excl_scan<uint64_t>(keep ? 1 : 0, ws, ck);
+        const uint64_t rb = block_excl_scan<uint64_t>(sz, ws, cb_);
+        const uint64_t rd = block_excl_scan<uint64_t>(dl, ws, cd);
+        if (keep) emit_merged(O, g + rk, (uint32_t)xc[i], rec_addr[(uint32_t)xc[i]], pb + rb, pd + rd);
+        g += ck;
+        pb += cb_;
+        pd += cd;
     }
-    if (threadIdx.x == 0) {
-        O.tile_kept[t] = kept;
-        O.tile_bytes[t] = bytes;
-        O.tile_dels[t] = dels;
-    }
-    (void)s_flag;
 }
 
 template <bool L0>
@@ -745,7 +775,13 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     uint64_t* ws = (uint64_t*)(((uintptr_t)(cbB + (k + 1)) + 15) & ~(uintptr_t)15);
     uint32_t* s_flag = (uint32_t*)(ws + 16);
 
-    const uint64_t t = blockIdx.x;
+    __shared__ uint64_t s_tk;
+    uint64_t t = blockIdx.x;
+    if (L0) {  // level 0 tiles take tickets in start order (tile_lookback's progress guarantee)
+        if (threadIdx.x == 0) s_tk = atomicAdd(O.tcounter, 1u);
+        __syncthreads();
+        t = s_tk;
+    }
     const uint64_t base = tile_base[t];
     const uint64_t n64 = tile_base[t + 1] - base;
     // segment starts
@@ -766,22 +802,22 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         return;
     }
     if (n == 0) {
-        if (L0 && threadIdx.x == 0) {
-            O.tile_kept[t] = 0;
-            O.tile_bytes[t] = 0;
-            O.tile_dels[t] = 0;
+        if (L0) {
+            tile_minmax(0xFFFFFFFFu, 0, s_flag, O.tile_mm + 2 * t);
+            tile_lookback(O.tstate, t, 0, 0, 0, ws + 8);
+            if (t == O.T - 1 && threadIdx.x == 0) emit_totals(O, ws[8], ws[9], ws[10]);
         }
         return;
     }
     // Thread owns elements e = threadIdx.x + u*TILE_THREADS; key, position and segment stay in
     // registers across the merge rounds, so each round is one binary search + one LDS write.
     constexpr int PER = TILE_CAP / TILE_THREADS;
-    uint64_t rh[PER], rl[PER], rc[PER];
+    uint64_t rh[PER], rl[PER], rc[PER], raddr[PER];
     uint32_t rpos[PER], rseg[PER], rmeta[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         uint32_t e = threadIdx.x + u * TILE_THREADS;
-        rh[u] = rl[u] = rc[u] = 0;
+        rh[u] = rl[u] = rc[u] = raddr[u] = 0;
         rpos[u] = e;
         rseg[u] = 0;
         rmeta[u] = 0;
@@ -789,7 +825,10 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
             uint32_t j = seg_of(cbA, k + 1, e);
             uint64_t pos = bounds[t * k + j] + (e - cbA[j]);
             load_elem<L0>(E, pos, rh[u], rl[u], rc[u]);
-            if (L0) rmeta[u] = rec_meta[pos];
+            if (L0) {
+                rmeta[u] = rec_meta[pos];
+                raddr[u] = rec_addr[pos];  // coalesced here, instead of a random gather later
+            }
             rseg[u] = j;
             el_lo[e] = rl[u];
             el_c[e] = rc[u];
@@ -846,77 +885,86 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         { uint32_t* tp = cb; cb = cbn; cbn = tp; }
         m = mn;
     }
-    // level 0: meta by final position, in the free ping-pong buffer
-    uint32_t* pmeta = (uint32_t*)mhn;
-    if (L0) {
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            uint32_t e = threadIdx.x + u * TILE_THREADS;
-            if (e < n) pmeta[rpos[u]] = rmeta[u];
-        }
-        __syncthreads();
+    if (!L0) {
+        tile_output_samples(n, mh, mi, el_lo, el_c, base, O);
+        return;
     }
-    tile_output<L0>(n, mh, mi, el_lo, el_c, pmeta, base, t, drop_deletes != 0, rec_addr, O, ws);
-}
-
-// dense merged arrays: rec_idx, source address, output-byte prefix P, delete-count prefix
-__global__ void __launch_bounds__(1024) k_finalize(uint64_t T, const uint64_t* __restrict__ tile_base,
-                                                   const uint64_t* __restrict__ tile_kept,
-                                                   const uint64_t* __restrict__ kept_base,
-                                                   const uint64_t* __restrict__ byte_base,
-                                                   const uint64_t* __restrict__ del_base,
-                                                   const uint32_t* __restrict__ t_rec, const uint32_t* __restrict__ t_meta,
-                                                   const uint64_t* __restrict__ rec_addr, uint32_t* m_rec,
-                                                   uint64_t* m_src, uint64_t* m_P, uint64_t* m_Dp, uint32_t* max_rec) {
-    __shared__ uint64_t ws[16];
-    const uint64_t t = blockIdx.x;
-    const uint64_t n = tile_kept[t], src = tile_base[t];
-    uint64_t g = kept_base[t], pb = byte_base[t], pd = del_base[t];
-    uint32_t mx = 0, mn = 0xFFFFFFFFu;
-    for (uint64_t b0 = 0; b0 < n; b0 += blockDim.x) {
-        uint64_t i = b0 + threadIdx.x;
-        uint32_t meta = i < n ? t_meta[src + i] : 0u;
-        uint64_t sz = meta & 0x7FFFFFFFu, dl = meta >> 31;
-        uint64_t tb, td;
-        uint64_t eb = block_excl_scan<uint64_t>(sz, ws, tb);
-        uint64_t ed = block_excl_scan<uint64_t>(dl, ws, td);
+    // level 0 output: (a) first-per-key flags by merged position (k_way.rs:146-151)
+    const uint32_t i0 = threadIdx.x * PER;
+    uint32_t keep_mask = 0;
+    uint32_t idx[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = i0 + q;
+        idx[q] = 0;
         if (i < n) {
-            uint32_t r = t_rec[src + i];
-            m_rec[g + i] = r;
-            m_src[g + i] = rec_addr[r];
-            m_P[g + i] = pb + eb;
-            m_Dp[g + i] = pd + ed;
-            mx = (uint32_t)sz > mx ? (uint32_t)sz : mx;
-            mn = (uint32_t)sz < mn ? (uint32_t)sz : mn;
+            const uint32_t e = mi[i];
+            const uint64_t h = mh[i], c = el_c[e];
+            bool first = true;
+            if (i > 0 && mh[i - 1] == h) {
+                const uint32_t p = mi[i - 1];
+                first = ekey_cmp(rec_addr, h, el_lo[p], el_c[p], h, el_lo[e], c) != 0;
+            }
+            idx[q] = (uint32_t)c;
+            if (first) keep_mask |= 1u << q;
         }
-        pb += tb;
-        pd += td;
-    }
-    // smallest / largest surviving record of the tile (no global atomics: k_chain reduces them)
-    __shared__ uint32_t wmax[16], wmin[16];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        uint32_t o = __shfl_xor(mx, d, 64);
-        mx = o > mx ? o : mx;
-        o = __shfl_xor(mn, d, 64);
-        mn = o < mn ? o : mn;
-    }
-    if ((threadIdx.x & 63) == 0) {
-        wmax[threadIdx.x >> 6] = mx;
-        wmin[threadIdx.x >> 6] = mn;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
-            mx = wmax[w] > mx ? wmax[w] : mx;
-            mn = wmin[w] < mn ? wmin[w] : mn;
+    // (b) meta and source address by final position (el_lo and the free ping-pong buffer)
+    uint32_t* pmeta = (uint32_t*)el_lo;
+    uint64_t* paddr = mhn;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const uint32_t e = threadIdx.x + u * TILE_THREADS;
+        if (e < n) {
+            pmeta[rpos[u]] = rmeta[u];
+            paddr[rpos[u]] = raddr[u];
         }
-        max_rec[2 * t] = mn;
-        max_rec[2 * t + 1] = mx;
     }
-    if (t == T - 1 && threadIdx.x == 0) {
-        m_P[kept_base[t] + n] = pb;
-        m_Dp[kept_base[t] + n] = pd;
+    __syncthreads();
+    // (c) Delete filter, tile totals
+    uint32_t mt[PER];
+    uint64_t ad[PER];
+    uint64_t kd = 0, bytes = 0;
+    uint32_t smin = 0xFFFFFFFFu, smax = 0;
+    const bool drop = drop_deletes != 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        mt[q] = 0;
+        ad[q] = 0;
+        if (keep_mask & (1u << q)) {
+            const uint32_t i = i0 + q;
+            mt[q] = pmeta[i];
+            ad[q] = paddr[i];
+            if (drop && (mt[q] >> 31)) {
+                keep_mask &= ~(1u << q);
+            } else {
+                const uint32_t sz = mt[q] & 0x7FFFFFFFu;
+                kd += 1 | ((uint64_t)(mt[q] >> 31) << 32);
+                bytes += sz;
+                smin = sz < smin ? sz : smin;
+                smax = sz > smax ? sz : smax;
+            }
+        }
+    }
+    uint64_t kd_tot, b_tot;
+    const uint64_t kd_ex = block_excl_scan<uint64_t>(kd, ws, kd_tot);
+    const uint64_t b_ex = block_excl_scan<uint64_t>(bytes, ws, b_tot);
+    tile_minmax(smin, smax, s_flag, O.tile_mm + 2 * t);
+    // (d) global position of this tile's survivors
+    tile_lookback(O.tstate, t, kd_tot & 0xFFFFFFFFull, b_tot, kd_tot >> 32, ws + 8);
+    const uint64_t K0 = ws[8], B0 = ws[9], D0 = ws[10];
+    if (t == O.T - 1 && threadIdx.x == 0)
+        emit_totals(O, K0 + (kd_tot & 0xFFFFFFFFull), B0 + b_tot, D0 + (kd_tot >> 32));
+    uint64_t g = K0 + (kd_ex & 0xFFFFFFFFull), pb = B0 + b_ex, pd = D0 + (kd_ex >> 32);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (keep_mask & (1u << q)) {
+            emit_merged(O, g, idx[q], ad[q], pb, pd);
+            ++g;
+            pb += mt[q] & 0x7FFFFFFFu;
+            pd += mt[q] >> 31;
+        }
     }
 }
 
@@ -974,11 +1022,16 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
                                               uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs_out) {
     const uint64_t K = *Kp;
     const int lane = threadIdx.x;
+    // n_runs_out = {runs, K, output record bytes P[K]}: the host's single readback
     if (K == 0) {
-        if (lane == 0) { run_b[0] = 0; *n_runs_out = 0; }
+        if (lane == 0) { run_b[0] = 0; n_runs_out[0] = 0; n_runs_out[1] = 0; n_runs_out[2] = 0; }
         return;
     }
-    // smallest / largest surviving record (per-tile pairs from k_finalize)
+    if (lane == 0) {
+        n_runs_out[1] = K;
+        n_runs_out[2] = P[K];
+    }
+    // smallest / largest surviving record (per-tile pairs from k_tile<true>)
     uint32_t mr = 0, mn = 0xFFFFFFFFu;
     for (uint64_t t = lane; t < n_tiles; t += 64) {
         mn = tile_max[2 * t] < mn ? tile_max[2 * t] : mn;
@@ -1658,7 +1711,7 @@ void launch_tile_n(hipStream_t s, const uint64_t* bounds, uint32_t k, uint64_t T
 size_t tile_lds_bytes(uint32_t k) {
     size_t b = (size_t)TILE_CAP * (4 * 8 + 2 + 2) + 2 * (size_t)(k + 1) * 4;
     b = (b + 15) & ~(size_t)15;
-    return b + 16 * 8 + 16;
+    return b + 16 * 8 + 32 * 4;  // ws[16] u64, then 32 u32 (tile_minmax)
 }
 hipError_t launch_tile(hipStream_t s, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
                        const uint32_t* klen, const uint64_t* bounds, uint32_t k, uint64_t T, const uint64_t* tile_base,
@@ -1673,13 +1726,6 @@ hipError_t launch_tile(hipStream_t s, bool l0, const uint64_t* hi, const uint64_
         k_tile<false><<<(unsigned)T, TILE_THREADS, lds, s>>>(E, bounds, k, tile_base, rec_meta, rec_addr, drop, O);
     }
     return hipGetLastError();
-}
-void launch_finalize(hipStream_t s, uint64_t T, const uint64_t* tile_base, const uint64_t* tile_kept,
-                     const uint64_t* kept_base, const uint64_t* byte_base, const uint64_t* del_base, const uint32_t* t_rec,
-                     const uint32_t* t_meta, const uint64_t* rec_addr, uint32_t* m_rec, uint64_t* m_src, uint64_t* m_P,
-                     uint64_t* m_Dp, uint32_t* max_rec) {
-    k_finalize<<<(unsigned)T, 1024, 0, s>>>(T, tile_base, tile_kept, kept_base, byte_base, del_base, t_rec, t_meta,
-                                              rec_addr, m_rec, m_src, m_P, m_Dp, max_rec);
 }
 void launch_chain(hipStream_t s, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, const uint32_t* tile_max,
                   uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs) {

@@ -42,10 +42,6 @@ size_t tile_lds_bytes(uint32_t k);
 hipError_t launch_tile(hipStream_t, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
                        const uint32_t* klen, const uint64_t* bounds, uint32_t k, uint64_t T, const uint64_t* tile_base,
                        const uint32_t* rec_meta, const uint64_t* rec_addr, uint32_t drop, TileOut O);
-void launch_finalize(hipStream_t, uint64_t T, const uint64_t* tile_base, const uint64_t* tile_kept,
-                     const uint64_t* kept_base, const uint64_t* byte_base, const uint64_t* del_base, const uint32_t* t_rec,
-                     const uint32_t* t_meta, const uint64_t* rec_addr, uint32_t* m_rec, uint64_t* m_src, uint64_t* m_P,
-                     uint64_t* m_Dp, uint32_t* max_rec);
 void launch_chain(hipStream_t, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, const uint32_t* tile_max,
                   uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs);
 void launch_run_stats(hipStream_t, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,

@@ -293,3 +293,20 @@ def test_fixed_stride_fast_path_and_fallback(dev):
         if exp != got:
             bad.append((i, _diff(exp, got)))
     assert not bad, bad
+
+
+def test_oversized_tile_fallback(dev):
+    """Splitter sampling bounds a tile at m*S + k*S records; this input puts 4,606 records in
+    one tile (> TILE_CAP 4096), so the global-memory sort path (tile_big) runs, with duplicates
+    across streams and Deletes (also under SKV_DROP_TOMBSTONES)."""
+    a_keys = [f"k{10 * i + 5:09d}" for i in range(20000)]
+    b_keys = ([f"k{0:09d}"] + [f"k{76801 + 20 * i:09d}" for i in range(1535)] +
+              [f"k{10 ** 8 + i:09d}" for i in range(1000)])
+    b_dup = sorted(set(b_keys) | {f"k{10 * i + 5:09d}" for i in range(7700, 10700, 3)})
+    r = random.Random(9)
+    for keys_b in (b_keys, b_dup):
+        a = fmt.encode_run([fmt.put(k, bytes([r.randrange(256)]) * r.randrange(0, 9)) for k in a_keys])
+        b = fmt.encode_run([fmt.delete(k) if r.random() < 0.3 else fmt.put(k, b"new") for k in keys_b])
+        for flags in (0, _abi.SKV_DROP_TOMBSTONES):
+            exp, got = _run_both(dev, [(1, [a]), (2, [b])], 64 * KiB, flags)
+            assert exp == got, _diff(exp, got)

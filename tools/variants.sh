@@ -6,6 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/variants
 export TMPDIR=/tmp
 for lib in skyvault-rs_amd/skv/libskv.so skyvault-rs_amd/skv/variants/libskv_*.so; do
+  [ -f "$lib" ] || continue
   tag=$(basename "$lib" .so)
   SKV_LIB="$PWD/$lib" timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-host-path \
     ${BENCH_ARGS:-} > "gpurun_out/variants/$tag.log" 2>&1
