@@ -354,7 +354,10 @@ static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
     return SKV_OK;
 }
 
-static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
+// allow_deferred: on the fixed-stride fast path, launch the merge without waiting for the parse's
+// verdict (broken runs / order errors / oversized records) and check it with the final readback;
+// a bad verdict discards the result and reruns the call on the exact general path.
+static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_deferred = true) {
     hipStream_t st = ctx->stream;
     ctx->syncs = 0;
     ctx->up_chunk = 0;
@@ -472,7 +475,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     };
 
     // ---- fast path: every run fixed-stride (one record size per run) -> one verifying pass ------
-    bool parsed = false;
+    bool parsed = false, deferred = false;
     {
         RunFmt* hf = (RunFmt*)pinned(ctx, (size_t)n_runs * sizeof(RunFmt) + 16);
         d2h(ctx, hf, d_fmt, (size_t)n_runs * sizeof(RunFmt));
@@ -494,7 +497,14 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
             launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
                                rec_meta, d_flags, d_stream_base, d_first_dec);
             mark(ctx, PH_PARSE);
-            parsed = !check_and_read(true);
+            if (allow_deferred && !(job.flags & SKV_SPLIT_BY_TABLE)) {
+                deferred = true;  // verdict read with the result
+                parsed = true;
+                std::fill(first_dec.begin(), first_dec.end(), ~0ull);
+                memset(hflags, 0, sizeof hflags);
+            } else {
+                parsed = !check_and_read(true);
+            }
             if (!parsed) {  // a run is not what its first record promised: general parse
                 R = 0;
                 any_err = false;
@@ -666,7 +676,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
         uint64_t* bounds = dbuf<uint64_t>(ctx, nm, (T + 1) * k);
         const Level* U = li + 1 < (int)lv.size() ? &lv[li + 1] : nullptr;
         launch_bounds(st, l0, L.hi, L.lo, L.c, rec_klen, L.d_off, k, U ? U->shi : nullptr, U ? U->slo : nullptr,
-                      U ? U->sc : nullptr, m, T, rec_addr, bounds);
+                      U ? U->sc : nullptr, m, T, rec_addr, bounds, d_flags + 2);
         snprintf(nm, sizeof nm, "tile_n%d", li);
         uint64_t* tile_n = dbuf<uint64_t>(ctx, nm, T);
         snprintf(nm, sizeof nm, "tile_base%d", li);
@@ -696,7 +706,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
             snprintf(nm, sizeof nm, "s%d_c", li); L.sc = O.oc = dbuf<uint64_t>(ctx, nm, L.N);
         }
         HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, rec_klen, bounds, k, T, tile_base, rec_meta, rec_addr,
-                           (job.flags & SKV_DROP_TOMBSTONES) ? 1u : 0u, O));
+                           (job.flags & SKV_DROP_TOMBSTONES) ? 1u : 0u, O, d_flags + 2));
         if (l0) T0 = T;
     }
     HIPCHK(hipGetLastError());
@@ -738,10 +748,25 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out) {
     ResultBox* box = new ResultBox();
     skv_result* res = &box->pub;
     {
-        uint8_t* hp = (uint8_t*)pinned(ctx, 64 + guess * sizeof(DevRunDesc));
+        const size_t vbytes = deferred ? 16 + (size_t)n_runs * 4 : 0;  // flags + broken runs
+        uint8_t* hp = (uint8_t*)pinned(ctx, 64 + guess * sizeof(DevRunDesc) + vbytes);
+        uint8_t* hv = hp + 64 + guess * sizeof(DevRunDesc);
         d2h(ctx, hp, d_nruns, 24);
         d2h(ctx, hp + 64, d_desc, guess * sizeof(DevRunDesc));
+        if (deferred) {
+            d2h(ctx, hv, d_flags, 16);
+            d2h(ctx, hv + 16, d_broken, (size_t)n_runs * 4);
+        }
         sync(ctx);
+        if (deferred) {
+            const uint32_t* f = (const uint32_t*)hv;  // >= 2 GiB record, key decrease, poison
+            bool bad = f[0] || f[1] || f[2];
+            for (uint32_t r = 0; r < n_runs && !bad; ++r) bad = ((const uint32_t*)(hv + 16))[r] != 0;
+            if (bad) {
+                delete box;
+                return compact_device(ctx, job, out, false);
+            }
+        }
         memcpy(h3, hp, 24);
         const uint64_t n = h3[0];
         res->runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, n) * sizeof(skv_run_desc));

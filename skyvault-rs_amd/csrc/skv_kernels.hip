@@ -381,9 +381,15 @@ __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, 
         len = runs[lo].len;
         p = 1 + (i - run_recb[lo]) * f.S;
         h = parse_rec<true>(run, len, p);
-        if (VERIFY && (h.err || h.size != f.S)) {
+        if (VERIFY && (h.err || h.size != f.S || h.size >= (1ull << 31))) {
             atomicOr(&run_broken[lo], 1u);
+            atomicOr(flags + 2, 1u);  // poison the speculative merge
             act = false;
+            // a harmless stand-in (empty key, zero size) so that the speculatively launched merge
+            // never follows a garbage address; the host reruns the general parse
+            RecHdr z{};
+            z.marker = 1;
+            put_rec(i, run, z, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
         }
         if (act) put_rec(i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
     }
@@ -423,6 +429,7 @@ __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, 
         const uint32_t sidx = runs[lo].stream;
         atomicMin(&first_dec[sidx], (unsigned long long)(i - 1 - stream_base[sidx]));
         atomicOr(flags + 1, 1u);
+        atomicOr(flags + 2, 1u);  // unsorted segment: poison the speculative merge
     }
 }
 
@@ -462,6 +469,8 @@ struct Elems {
     const uint64_t* lo;
     const uint64_t* c;       // null at level 0 (c = klen << 32 | position)
     const uint32_t* klen;    // level 0 only
+    const uint32_t* poison;  // set: the speculatively parsed records are invalid (unsorted or
+                             // stand-ins) -> splitter / merge kernels do nothing (see k_emit_fixed)
 };
 
 template <bool L0>
@@ -531,7 +540,7 @@ __global__ void k_bounds(Elems E, const uint64_t* __restrict__ off, uint32_t k, 
                          const uint64_t* __restrict__ slo, const uint64_t* __restrict__ sc, uint64_t m, uint64_t T,
                          const uint64_t* __restrict__ rec_addr, uint64_t* bounds) {
     uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= (T + 1) * k) return;
+    if (g >= (T + 1) * k || *E.poison) return;
     uint64_t t = g / k;
     uint32_t j = (uint32_t)(g - t * k);
     uint64_t a = off[j], b = off[j + 1];
@@ -776,6 +785,10 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     uint32_t* s_flag = (uint32_t*)(ws + 16);
 
     __shared__ uint64_t s_tk;
+    if (*E.poison) {  // a merge of unsorted segments is not a permutation: touch nothing
+        if (L0 && blockIdx.x == 0 && threadIdx.x == 0) O.Kout[0] = 0;
+        return;
+    }
     uint64_t t = blockIdx.x;
     if (L0) {  // level 0 tiles take tickets in start order (tile_lookback's progress guarantee)
         if (threadIdx.x == 0) s_tk = atomicAdd(O.tcounter, 1u);
@@ -846,30 +859,49 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     uint16_t* mi = miA;
     uint16_t* min_ = miB;
     while (m > 1) {
+        // count, for each element, the partner segment's elements that order before it: the PER
+        // binary searches of a thread run in lockstep (one LDS read of each per step -> ILP)
+        uint32_t sb[PER], sn[PER];
+        uint32_t maxn = 0;
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            uint32_t e = threadIdx.x + u * TILE_THREADS;
-            if (e < n) {
-                uint32_t s = rseg[u];
-                uint32_t ps = s ^ 1u;
-                uint32_t newpos = rpos[u];
-                if (ps < m) {
-                    const uint64_t h = rh[u];
-                    uint32_t a = cb[ps], b = cb[ps + 1];
-                    const uint32_t a0 = a;
-                    while (a < b) {  // count partner elements < e
-                        uint32_t mid = (a + b) >> 1;
-                        uint64_t xh = mh[mid];
-                        bool less = xh < h;
-                        if (xh == h) {
-                            uint32_t x = mi[mid];
-                            less = elem_less(rec_addr, xh, el_lo[x], el_c[x], h, rl[u], rc[u]);
-                        }
-                        if (less) a = mid + 1;
-                        else b = mid;
+            const uint32_t e = threadIdx.x + u * TILE_THREADS;
+            const uint32_t ps = rseg[u] ^ 1u;
+            sb[u] = 0;
+            sn[u] = 0;
+            if (e < n && ps < m) {
+                sb[u] = cb[ps];
+                sn[u] = cb[ps + 1] - sb[u];
+                maxn = sn[u] > maxn ? sn[u] : maxn;
+            }
+        }
+        for (; maxn; maxn >>= 1) {  // every step at least halves each remaining range
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                if (sn[u]) {
+                    const uint32_t half = sn[u] >> 1, mid = sb[u] + half;
+                    const uint64_t xh = mh[mid];
+                    bool less = xh < rh[u];
+                    if (xh == rh[u]) {
+                        const uint32_t x = mi[mid];
+                        less = elem_less(rec_addr, xh, el_lo[x], el_c[x], rh[u], rl[u], rc[u]);
                     }
-                    newpos = cb[s & ~1u] + (rpos[u] - cb[s]) + (a - a0);
+                    if (less) {
+                        sb[u] = mid + 1;
+                        sn[u] -= half + 1;
+                    } else {
+                        sn[u] = half;
+                    }
                 }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const uint32_t e = threadIdx.x + u * TILE_THREADS;
+            if (e < n) {
+                const uint32_t s = rseg[u], ps = s ^ 1u;
+                uint32_t newpos = rpos[u];
+                if (ps < m) newpos = cb[s & ~1u] + (rpos[u] - cb[s]) + (sb[u] - cb[ps]);
                 mhn[newpos] = rh[u];
                 min_[newpos] = (uint16_t)e;
                 rpos[u] = newpos;
@@ -1691,14 +1723,15 @@ void launch_sample(hipStream_t s, bool l0, const uint64_t* hi, const uint64_t* l
                    const uint32_t* klen, const uint64_t* off_src, const uint64_t* off_dst, uint32_t k, uint64_t S,
                    uint64_t n_dst, uint64_t* dhi, uint64_t* dlo, uint64_t* dc) {
     if (!n_dst) return;
-    Elems E{hi, lo, c, klen};
+    Elems E{hi, lo, c, klen, nullptr};
     if (l0) k_sample<true><<<blocks_for(n_dst, 256), 256, 0, s>>>(E, off_src, off_dst, k, S, n_dst, dhi, dlo, dc);
     else k_sample<false><<<blocks_for(n_dst, 256), 256, 0, s>>>(E, off_src, off_dst, k, S, n_dst, dhi, dlo, dc);
 }
 void launch_bounds(hipStream_t s, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
                    const uint32_t* klen, const uint64_t* off, uint32_t k, const uint64_t* shi, const uint64_t* slo,
-                   const uint64_t* sc, uint64_t m, uint64_t T, const uint64_t* rec_addr, uint64_t* bounds) {
-    Elems E{hi, lo, c, klen};
+                   const uint64_t* sc, uint64_t m, uint64_t T, const uint64_t* rec_addr, uint64_t* bounds,
+                   const uint32_t* poison) {
+    Elems E{hi, lo, c, klen, poison};
     uint64_t n = (T + 1) * k;
     if (!n) return;
     if (l0) k_bounds<true><<<blocks_for(n, 256), 256, 0, s>>>(E, off, k, shi, slo, sc, m, T, rec_addr, bounds);
@@ -1715,14 +1748,23 @@ size_t tile_lds_bytes(uint32_t k) {
 }
 hipError_t launch_tile(hipStream_t s, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
                        const uint32_t* klen, const uint64_t* bounds, uint32_t k, uint64_t T, const uint64_t* tile_base,
-                       const uint32_t* rec_meta, const uint64_t* rec_addr, uint32_t drop, TileOut O) {
-    Elems E{hi, lo, c, klen};
+                       const uint32_t* rec_meta, const uint64_t* rec_addr, uint32_t drop, TileOut O,
+                       const uint32_t* poison) {
+    Elems E{hi, lo, c, klen, poison};
     size_t lds = tile_lds_bytes(k);
+    // raise the dynamic LDS limit once per device and size, not per call
+    static size_t lds_set[64][2] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    size_t& done = lds_set[dev & 63][l0 ? 1 : 0];
+    if (lds > done) {
+        (void)hipFuncSetAttribute(l0 ? (const void*)k_tile<true> : (const void*)k_tile<false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        done = lds;
+    }
     if (l0) {
-        (void)hipFuncSetAttribute((const void*)k_tile<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         k_tile<true><<<(unsigned)T, TILE_THREADS, lds, s>>>(E, bounds, k, tile_base, rec_meta, rec_addr, drop, O);
     } else {
-        (void)hipFuncSetAttribute((const void*)k_tile<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         k_tile<false><<<(unsigned)T, TILE_THREADS, lds, s>>>(E, bounds, k, tile_base, rec_meta, rec_addr, drop, O);
     }
     return hipGetLastError();

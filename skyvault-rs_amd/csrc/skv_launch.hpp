@@ -36,12 +36,14 @@ void launch_sample(hipStream_t, bool l0, const uint64_t* hi, const uint64_t* lo,
                    uint64_t n_dst, uint64_t* dhi, uint64_t* dlo, uint64_t* dc);
 void launch_bounds(hipStream_t, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
                    const uint32_t* klen, const uint64_t* off, uint32_t k, const uint64_t* shi, const uint64_t* slo,
-                   const uint64_t* sc, uint64_t m, uint64_t T, const uint64_t* rec_addr, uint64_t* bounds);
+                   const uint64_t* sc, uint64_t m, uint64_t T, const uint64_t* rec_addr, uint64_t* bounds,
+                   const uint32_t* poison);
 void launch_tile_n(hipStream_t, const uint64_t* bounds, uint32_t k, uint64_t T, uint64_t* tile_n);
 size_t tile_lds_bytes(uint32_t k);
 hipError_t launch_tile(hipStream_t, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
                        const uint32_t* klen, const uint64_t* bounds, uint32_t k, uint64_t T, const uint64_t* tile_base,
-                       const uint32_t* rec_meta, const uint64_t* rec_addr, uint32_t drop, TileOut O);
+                       const uint32_t* rec_meta, const uint64_t* rec_addr, uint32_t drop, TileOut O,
+                       const uint32_t* poison);
 void launch_chain(hipStream_t, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, const uint32_t* tile_max,
                   uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs);
 void launch_run_stats(hipStream_t, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
