@@ -41,6 +41,9 @@ constexpr int GATHER_TBL = 23 * SKV_GATHER_SEG; // output 16-byte blocks per gat
 #ifndef SKV_GATHER_WAVES
 #define SKV_GATHER_WAVES 8               // k_gather register budget: waves per SIMD (64 VGPRs at 8)
 #endif
+#ifndef SKV_TILE_PROF
+#define SKV_TILE_PROF 0                  // 1: k_tile<true> accumulates per-phase times (diagnostic builds)
+#endif
 #ifndef SKV_PAGE_U
 #define SKV_PAGE_U 4                     // page gather: 16-byte output blocks per lane
 #endif
@@ -105,6 +108,7 @@ struct TileOut {
     uint32_t* tcounter;   // tile ticket (zeroed per call)
     uint64_t* Kout;       // K = surviving records
     uint64_t T;           // level-0 tile count
+    uint64_t* prof;       // SKV_TILE_PROF builds: per-phase time of level-0 tiles (8 counters)
     // global scratch for tiles larger than TILE_CAP
     uint64_t* xhi;
     uint64_t* xlo;

@@ -68,6 +68,7 @@ struct PinnedPool {
 struct skv_ctx {
     int device = 0;
     std::shared_ptr<PinnedPool> out_pool = std::make_shared<PinnedPool>();
+    bool prof_init = false;  // SKV_TILE_PROF builds
     hipStream_t stream = nullptr;
     std::string err;
     bool profiling = false;
@@ -700,6 +701,13 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             O.tcounter = dbuf<uint32_t>(ctx, "tile_ticket", 1);
             HIPCHK(hipMemsetAsync(O.tstate, 0, 3 * T * 8, st));
             HIPCHK(hipMemsetAsync(O.tcounter, 0, 4, st));
+#if SKV_TILE_PROF
+            O.prof = dbuf<uint64_t>(ctx, "tile_prof", 8);
+            if (!ctx->prof_init) {
+                HIPCHK(hipMemsetAsync(O.prof, 0, 64, st));
+                ctx->prof_init = true;
+            }
+#endif
         } else {
             snprintf(nm, sizeof nm, "s%d_hi", li); L.shi = O.ohi = dbuf<uint64_t>(ctx, nm, L.N);
             snprintf(nm, sizeof nm, "s%d_lo", li); L.slo = O.olo = dbuf<uint64_t>(ctx, nm, L.N);
@@ -880,6 +888,16 @@ void skv_ctx_destroy(skv_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+#if SKV_TILE_PROF
+    if (ctx->bufs.count("tile_prof")) {
+        uint64_t pr[8];
+        if (hipMemcpy(pr, ctx->bufs["tile_prof"].p, 64, hipMemcpyDeviceToHost) == hipSuccess) {
+            fprintf(stderr, "tile phase time (100 MHz ticks summed over tiles):");
+            for (int i = 0; i < 8; ++i) fprintf(stderr, " %d:%llu", i, (unsigned long long)pr[i]);
+            fprintf(stderr, "\n");
+        }
+    }
+#endif
     for (auto& kv : ctx->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);

@@ -766,6 +766,19 @@ __device__ void tile_big(Elems E, const uint64_t* bounds, uint32_t k, uint64_t t
     }
 }
 
+#if SKV_TILE_PROF
+#define TPROF(i)                                                                 \
+    do {                                                                         \
+        if (L0 && threadIdx.x == 0) {                                            \
+            const uint64_t now_ = __builtin_amdgcn_s_memrealtime();              \
+            atomicAdd((unsigned long long*)&O.prof[i], (unsigned long long)(now_ - tp_last)); \
+            tp_last = now_;                                                      \
+        }                                                                        \
+    } while (0)
+#else
+#define TPROF(i) do {} while (0)
+#endif
+
 template <bool L0>
 __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* __restrict__ bounds, uint32_t k,
                                                       const uint64_t* __restrict__ tile_base,
@@ -785,6 +798,9 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     uint32_t* s_flag = (uint32_t*)(ws + 16);
 
     __shared__ uint64_t s_tk;
+#if SKV_TILE_PROF
+    uint64_t tp_last = __builtin_amdgcn_s_memrealtime();
+#endif
     if (*E.poison) {  // a merge of unsorted segments is not a permutation: touch nothing
         if (L0 && blockIdx.x == 0 && threadIdx.x == 0) O.Kout[0] = 0;
         return;
@@ -809,6 +825,7 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     }
     if (threadIdx.x == 0) cbA[k] = (uint32_t)segtot;
     __syncthreads();
+    TPROF(0);
     const uint32_t n = (uint32_t)n64;
     if (n64 > TILE_CAP) {
         tile_big<L0>(E, bounds, k, t, base, n, cbA, rec_meta, rec_addr, drop_deletes != 0, O, ws, s_flag);
@@ -850,6 +867,7 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         }
     }
     __syncthreads();
+    TPROF(1);
     // pairwise merge rounds: each element finds its rank in the partner segment
     uint32_t m = k;
     uint32_t* cb = cbA;
@@ -921,6 +939,7 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         tile_output_samples(n, mh, mi, el_lo, el_c, base, O);
         return;
     }
+    TPROF(2);
     // level 0 output: (a) first-per-key flags by merged position (k_way.rs:146-151)
     const uint32_t i0 = threadIdx.x * PER;
     uint32_t keep_mask = 0;
@@ -942,6 +961,7 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         }
     }
     __syncthreads();
+    TPROF(3);
     // (b) meta and source address by final position (el_lo and the free ping-pong buffer)
     uint32_t* pmeta = (uint32_t*)el_lo;
     uint64_t* paddr = mhn;
@@ -954,6 +974,7 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         }
     }
     __syncthreads();
+    TPROF(4);
     // (c) Delete filter, tile totals
     uint32_t mt[PER];
     uint64_t ad[PER];
@@ -984,8 +1005,10 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     const uint64_t b_ex = block_excl_scan<uint64_t>(bytes, ws, b_tot);
     tile_minmax(smin, smax, s_flag, O.tile_mm + 2 * t);
     // (d) global position of this tile's survivors
+    TPROF(5);
     tile_lookback(O.tstate, t, kd_tot & 0xFFFFFFFFull, b_tot, kd_tot >> 32, ws + 8);
     const uint64_t K0 = ws[8], B0 = ws[9], D0 = ws[10];
+    TPROF(6);
     if (t == O.T - 1 && threadIdx.x == 0)
         emit_totals(O, K0 + (kd_tot & 0xFFFFFFFFull), B0 + b_tot, D0 + (kd_tot >> 32));
     uint64_t g = K0 + (kd_ex & 0xFFFFFFFFull), pb = B0 + b_ex, pd = D0 + (kd_ex >> 32);
@@ -998,6 +1021,7 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
             pd += mt[q] >> 31;
         }
     }
+    TPROF(7);
 }
 
 // ---------------------------------------------------------------------------------------
