@@ -151,12 +151,16 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(device)
 
-    gather_ms, total_ms, phases = [], [], []
+    gather_ms, total_ms, phases, host_ms, sync_ms, call_ms = [], [], [], [], [], []
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        tc = time.perf_counter()
         res = comp.compact_dev(streams, MAX_RUN, 0)
+        call_ms.append((time.perf_counter() - tc) * 1e3)
         t = comp.timings()
+        host_ms.append(t["host_total_ms"])
+        sync_ms.append(t["host_sync_ms"])
         gather_ms.append(t["gather_ms"])
         total_ms.append(t["total_ms"])
         phases.append([t[k] for k in ("parse_ms", "check_ms", "merge_ms", "chain_ms", "gather_ms")])
@@ -220,6 +224,9 @@ def main():
                 "parallelism": f"{world} independent compactions (one per GPU), no collective",
             },
             "device_ms_per_compaction": round(float(np.mean(total_ms)), 4),
+            "host_ms": {"python_call": round(float(np.mean(call_ms)), 4),
+                        "library": round(float(np.mean(host_ms)), 4),
+                        "in_syncs": round(float(np.mean(sync_ms)), 4)},
             "phases_ms": dict(zip(("parse", "check", "merge", "chain", "gather"),
                                   [round(float(x), 4) for x in np.mean(np.array(phases), axis=0)])),
             "roofline": {

@@ -119,6 +119,8 @@ typedef struct {
     uint64_t gather_read_bytes;  /* algorithmic bytes read by the gather (surviving input records) */
     uint64_t gather_write_bytes; /* algorithmic bytes written by the gather (== output bytes) */
     uint64_t host_syncs;
+    double host_total_ms;  /* wall time inside the skv_compact* call */
+    double host_sync_ms;   /* of which: waiting in stream synchronisations */
 } skv_timings;
 
 int skv_abi_version(void);

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cinttypes>
 #include <cstdarg>
 #include <cstdio>
@@ -83,6 +84,7 @@ struct skv_ctx {
     std::vector<std::pair<uint8_t*, size_t>> up_chunks;
     size_t up_chunk = 0, up_off = 0;
     uint64_t syncs = 0;
+    double sync_ms = 0;
 };
 
 struct ResultBox {  // skv_result + how to free it
@@ -175,8 +177,13 @@ static void h2d(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
     if (!bytes) return;
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
 }
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 static void sync(skv_ctx* ctx) {
+    const double t0 = now_ms();
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->sync_ms += now_ms() - t0;
     ctx->syncs++;
 }
 static void mark(skv_ctx* ctx, Phase p) {
@@ -843,9 +850,13 @@ static int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64
     return SKV_OK;
 }
 
-static int run_guarded(skv_ctx* ctx, const Job& job, skv_result** out) {
+static int run_guarded(skv_ctx* ctx, const Job& job, skv_result** out, double t_entry) {
     try {
-        return compact_device(ctx, job, out);
+        ctx->sync_ms = 0;
+        const int rc = compact_device(ctx, job, out);
+        ctx->timings.host_total_ms = now_ms() - t_entry;
+        ctx->timings.host_sync_ms = ctx->sync_ms;
+        return rc;
     } catch (const ApiError& e) {
         (void)hipStreamSynchronize(ctx->stream);
         return set_err(ctx, e.code, "%s", e.msg.c_str());
@@ -924,17 +935,19 @@ int skv_ctx_get_timings(const skv_ctx* ctx, skv_timings* out) {
 
 int skv_compact_dev(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uint64_t max_run_size, uint32_t flags,
                     skv_result** out) {
+    const double t_entry = now_ms();
     if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
     *out = nullptr;
     if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
     Job job;
     int rc = build_job(ctx, streams, n_streams, max_run_size, flags, job);
     if (rc) return rc;
-    return run_guarded(ctx, job, out);
+    return run_guarded(ctx, job, out, t_entry);
 }
 
 int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uint64_t max_run_size, uint32_t flags,
                 skv_result** out) {
+    const double t_entry = now_ms();
     if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
     *out = nullptr;
     if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
@@ -959,7 +972,7 @@ int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uin
         return set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());
     }
     skv_result* dres = nullptr;
-    rc = run_guarded(ctx, job, &dres);
+    rc = run_guarded(ctx, job, &dres, t_entry);
     if (rc) return rc;
     ResultBox* box = (ResultBox*)dres;
     size_t cap = 0;

@@ -89,6 +89,8 @@ class SkvTimings(C.Structure):
         ("gather_read_bytes", C.c_uint64),
         ("gather_write_bytes", C.c_uint64),
         ("host_syncs", C.c_uint64),
+        ("host_total_ms", C.c_double),
+        ("host_sync_ms", C.c_double),
     ]
 
 

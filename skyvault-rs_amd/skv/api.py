@@ -81,8 +81,17 @@ class DeviceResult:
         self.in_bytes = int(r.in_bytes)
         self.in_records = int(r.in_records)
         self.out_records = int(r.out_records)
-        self.descs = [(d.off, d.len, d.put_count, d.delete_count, d.min_key_off, d.min_key_len, d.max_key_off,
-                       d.max_key_len, d.table_id) for d in (r.runs[i] for i in range(r.n_runs))]
+        self._descs = None
+
+    @property
+    def descs(self):
+        """Run descriptors as tuples (built on first use: a hot loop that only needs the byte
+        counts does not pay for 1000+ ctypes reads)."""
+        if self._descs is None:
+            r = self._res.contents
+            self._descs = [(d.off, d.len, d.put_count, d.delete_count, d.min_key_off, d.min_key_len, d.max_key_off,
+                            d.max_key_len, d.table_id) for d in (r.runs[i] for i in range(r.n_runs))]
+        return self._descs
 
     def free(self):
         if self._res:
