@@ -112,7 +112,7 @@ def compact(streams: Sequence[tuple], max_run_size: int, flags: int = 0, with_re
     sa = StreamArgs(streams)
     res = C.POINTER(SkvResult)()
     eb = C.create_string_buffer(512)
-    rc = lib().skvo_compact(C.cast(sa.arr, C.c_void_p), sa.n, max_run_size, flags, C.byref(res), eb, 512)
+    rc = lib().skvo_compact(sa.ptr, sa.n, max_run_size, flags, C.byref(res), eb, 512)
     if rc != SKV_OK:
         raise RunError(rc, eb.value.decode("utf-8", "replace"))
     try:
@@ -129,7 +129,7 @@ def compact_bytes(streams: Sequence[tuple], max_run_size: int, flags: int = 0):
     sa = StreamArgs(streams)
     res = C.POINTER(SkvResult)()
     eb = C.create_string_buffer(512)
-    rc = lib().skvo_compact(C.cast(sa.arr, C.c_void_p), sa.n, max_run_size, flags, C.byref(res), eb, 512)
+    rc = lib().skvo_compact(sa.ptr, sa.n, max_run_size, flags, C.byref(res), eb, 512)
     if rc != SKV_OK:
         raise RunError(rc, eb.value.decode("utf-8", "replace"))
     try:

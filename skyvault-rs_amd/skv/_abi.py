@@ -138,14 +138,43 @@ class RunError(Exception):
         self.message = message
 
 
+def _stream_dtype():
+    import numpy as np
+
+    return np.dtype({"names": ["runs", "run_lens", "n_runs", "seq_no"],
+                     "formats": [np.uint64, np.uint64, np.uint32, np.int64],
+                     "offsets": [SkvStream.runs.offset, SkvStream.run_lens.offset, SkvStream.n_runs.offset,
+                                 SkvStream.seq_no.offset],
+                     "itemsize": C.sizeof(SkvStream)})
+
+
 class StreamArgs:
     """Keeps the ctypes arrays of one skv_stream[] alive for a call."""
 
     def __init__(self, streams: Sequence[tuple], device: bool = False):
         # streams: [(seq_no, [run_ptr_or_bytes, ...], [len, ...]?)]
         self._keep: List[object] = []
-        self.arr = (SkvStream * max(1, len(streams)))()
         self.n = len(streams)
+        if device:  # numpy-built tables: one flat pointer / length array + the stream structs
+            import numpy as np
+
+            counts = np.fromiter((len(st[1]) for st in streams), dtype=np.int64, count=len(streams))
+            flat = [r for st in streams for r in st[1]]
+            ptrs = np.array([int(p) for p, _ in flat] or [0], dtype=np.uint64)
+            lens = np.array([int(l) for _, l in flat] or [0], dtype=np.uint64)
+            offs = np.zeros(len(streams), dtype=np.uint64)
+            if len(streams) > 1:
+                offs[1:] = np.cumsum(counts[:-1]) * 8
+            tbl = np.zeros(max(1, len(streams)), dtype=_STREAM_DT)
+            tbl["runs"][: len(streams)] = ptrs.ctypes.data + offs
+            tbl["run_lens"][: len(streams)] = lens.ctypes.data + offs
+            tbl["n_runs"][: len(streams)] = counts
+            tbl["seq_no"][: len(streams)] = [int(st[0]) for st in streams]
+            self._keep += [ptrs, lens, tbl]
+            self.ptr = C.c_void_p(tbl.ctypes.data)
+            return
+        self.arr = (SkvStream * max(1, len(streams)))()
+        self.ptr = C.cast(self.arr, C.c_void_p)
         for i, st in enumerate(streams):
             seq, runs = st[0], st[1]
             n = len(runs)
@@ -167,6 +196,9 @@ class StreamArgs:
             self.arr[i].run_lens = C.cast(lens, C.POINTER(C.c_uint64))
             self.arr[i].n_runs = n
             self.arr[i].seq_no = int(seq)
+
+
+_STREAM_DT = _stream_dtype()
 
 
 def result_to_runs(res: SkvResult, host_bytes: Optional[bytes] = None) -> List[OutRun]:

@@ -134,7 +134,7 @@ class Compactor:
         """streams: [(seq_no, [run_bytes, ...])] (host memory). Returns [OutRun]."""
         sa = StreamArgs(streams)
         res = C.POINTER(SkvResult)()
-        rc = self.lib.skv_compact(self.ctx, C.cast(sa.arr, C.c_void_p), sa.n, max_run_size, flags, C.byref(res))
+        rc = self.lib.skv_compact(self.ctx, sa.ptr, sa.n, max_run_size, flags, C.byref(res))
         if rc != SKV_OK:
             raise self._err(rc)
         try:
@@ -151,7 +151,7 @@ class Compactor:
         """streams: [(seq_no, [(device_ptr, length), ...])] with inputs resident in HBM."""
         sa = StreamArgs(streams, device=True)
         res = C.POINTER(SkvResult)()
-        rc = self.lib.skv_compact_dev(self.ctx, C.cast(sa.arr, C.c_void_p), sa.n, max_run_size, flags, C.byref(res))
+        rc = self.lib.skv_compact_dev(self.ctx, sa.ptr, sa.n, max_run_size, flags, C.byref(res))
         if rc != SKV_OK:
             raise self._err(rc)
         return DeviceResult(self.lib, res)
@@ -162,7 +162,7 @@ class Compactor:
         Returns (output bytes, output runs); the pinned output is released immediately."""
         sa = StreamArgs(streams, device=True)
         res = C.POINTER(SkvResult)()
-        rc = self.lib.skv_compact(self.ctx, C.cast(sa.arr, C.c_void_p), sa.n, max_run_size, flags, C.byref(res))
+        rc = self.lib.skv_compact(self.ctx, sa.ptr, sa.n, max_run_size, flags, C.byref(res))
         if rc != SKV_OK:
             raise self._err(rc)
         n = (int(res.contents.n_bytes), int(res.contents.n_runs))
