@@ -28,6 +28,9 @@ import torch  # noqa: E402
 METRIC = "compaction GiB/s of input run bytes merged (device-resident), 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MAX_RUN = 4 * 1024 * 1024
+# the dominant kernel of each device path (skv_timings.path) and what its bytes count
+HOT_KERNEL = {1: "k_gather", 2: "k_gather", 3: "k_fx_tile"}
+PATH_NAMES = {1: "general", 2: "fixed", 3: "fused"}
 GiB = float(1 << 30)
 
 
@@ -117,7 +120,7 @@ def main():
     ap.add_argument("--cpu-sample-records", type=int, default=238821 // 16)
     ap.add_argument("--cpu-repeats", type=int, default=3)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
-                    help="per-launch HBM bytes of the gather kernel measured with rocprofv3 --pmc")
+                    help="per-launch HBM bytes of each kernel measured with rocprofv3 --pmc (tools/traffic.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -161,10 +164,11 @@ def main():
         t = comp.timings()
         host_ms.append(t["host_total_ms"])
         sync_ms.append(t["host_sync_ms"])
-        gather_ms.append(t["gather_ms"])
+        gather_ms.append(t["hot_ms"])
         total_ms.append(t["total_ms"])
         phases.append([t[k] for k in ("parse_ms", "check_ms", "merge_ms", "chain_ms", "gather_ms")])
-        gread, gwrite = t["gather_read_bytes"], t["gather_write_bytes"]
+        gread, gwrite = t["hot_read_bytes"], t["hot_write_bytes"]
+        path = t["path"]
         out_bytes, n_out_runs = res.n_bytes, res.n_runs
         res.free()
     barrier()
@@ -197,7 +201,8 @@ def main():
         traffic = None
         try:
             with open(args.traffic_json) as f:
-                traffic = json.load(f).get("gather_hbm_bytes_per_launch")
+                kt = json.load(f).get("kernels", {}).get("skv::" + HOT_KERNEL.get(path, "?"))
+                traffic = kt["hbm_bytes"] if kt else None
         except (OSError, ValueError):
             traffic = None
         line = {
@@ -231,7 +236,8 @@ def main():
                                   [round(float(x), 4) for x in np.mean(np.array(phases), axis=0)])),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_gather",
+                "kernel": HOT_KERNEL.get(path, "?"),
+                "path": PATH_NAMES.get(path, "?"),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

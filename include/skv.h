@@ -121,7 +121,21 @@ typedef struct {
     uint64_t host_syncs;
     double host_total_ms;  /* wall time inside the skv_compact* call */
     double host_sync_ms;   /* of which: waiting in stream synchronisations */
+    /* which device path produced the result (SKV_PATH_*) and its dominant kernel: HIP-event
+       time of that one launch and its algorithmic bytes */
+    uint32_t path;
+    uint32_t fused_reject;   /* SKV_PATH_FUSED attempted but poisoned: reason bits, else 0 */
+    double hot_ms;
+    uint64_t hot_read_bytes;
+    uint64_t hot_write_bytes;
 } skv_timings;
+
+/* skv_timings.path */
+enum {
+    SKV_PATH_GENERAL = 1, /* chunk-walk parse, record arrays, merge, chain, gather */
+    SKV_PATH_FIXED = 2,   /* fixed-stride verifying parse, record arrays, merge, chain, gather */
+    SKV_PATH_FUSED = 3    /* one record size and key length <= 16: fused verify/merge/copy tiles */
+};
 
 int skv_abi_version(void);
 int skv_device_count(int* out);

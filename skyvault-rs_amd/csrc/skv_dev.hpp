@@ -116,6 +116,51 @@ struct TileOut {
     uint32_t* xmeta;
 };
 
+// Fused stride path (skv_stride.hip): every input record is a Put of one size S with one key
+// length K <= 16, so record addresses, output offsets and the greedy split are arithmetic.
+#ifndef SKV_FX_THREADS
+#define SKV_FX_THREADS 512
+#endif
+#ifndef SKV_FX_U
+#define SKV_FX_U 8                       // output blocks per lane in flight in the fused copy
+#endif
+constexpr int FX_CAP = 4096;             // records per fused tile (same splitters as TILE_CAP)
+constexpr int FX_THREADS = SKV_FX_THREADS;
+constexpr uint64_t FX_MIN_S = 32;        // a 16-byte output block touches at most two records
+constexpr uint64_t FX_MAX_S = 1u << 19;  // tile output spans stay below 2^31 bytes (u32 offsets)
+constexpr uint32_t FX_MAX_K = 16;        // the whole key is the 16-byte compare prefix
+
+struct FxBound {                  // per (tile boundary t, stream j), written by k_fx_bounds
+    uint64_t pos;                 // first record of stream j whose key >= splitter t
+    uint64_t addr;                // its address (pos < stream end)
+    uint64_t rem;                 // records of its member run from pos on
+    uint64_t has_prev;            // pos > stream start: ph/pl = key of record pos - 1
+    uint64_t ph, pl;
+};
+
+struct FxArgs {
+    const RunInfo* runs;
+    const uint64_t* run_recb;     // records before run r, rank order (n_runs + 1)
+    const uint32_t* stream_run;   // first run of stream j (k + 1)
+    const uint64_t* stream_base;  // first record of stream j (k + 1)
+    FxBound* bnd;                 // level-0 tile bounds, (T + 1) x k
+    uint32_t k;
+    uint32_t K, V;                // key / value length of every record
+    uint32_t pad;
+    uint64_t S;                   // record size
+    uint64_t n;                   // records per output run (build_runs' greedy split, arithmetic)
+    double inv_S, inv_W, inv_n;   // reciprocals for fx_divmod (W = n * S + 1 bytes per output run)
+    uint64_t T;                   // level-0 tiles
+    uint8_t* out;
+    uint32_t* flags;              // [2] poison (result discarded, general path reruns), [3] reason bits
+    uint64_t* tstate;             // look-back word per tile (zeroed per call)
+    uint32_t* tcounter;           // tile ticket (zeroed per call)
+    uint64_t* Kout;               // surviving records
+    uint64_t* prof;               // SKV_TILE_PROF builds: per-phase ticks of the fused tiles (16 counters)
+};
+// flags[3] reason bits of a poisoned fused call
+enum : uint32_t { FXR_RECORD = 1, FXR_OVERSIZE = 2, FXR_SPLIT = 4, FXR_ORDER = 8, FXR_SAMPLE = 16 };
+
 // WAL key errors (wal_compaction.rs:71-79): no '.', or Rust's ParseIntError kinds
 enum : uint32_t { WERR_NONE = 0, WERR_NODOT, WERR_EMPTY, WERR_DIGIT, WERR_POS, WERR_NEG };
 

@@ -362,6 +362,207 @@ static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
     return SKV_OK;
 }
 
+// The fused stride path (skv_stride.hip): every run is fixed-stride with one record size S and one
+// key length K <= 16. Splitters, then one fused verify/merge/copy kernel, then the descriptors;
+// one host sync reads the descriptors together with the verdict. Returns false when the device
+// poisoned the call (a record or key order the run's first record did not promise, or splitter
+// skew): the caller then reruns the exact path, which produces the reference's outcome.
+static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInfo>& runs, const RunInfo* d_runs,
+                          const std::vector<uint32_t>& stream_first_run, const RunFmt& f,
+                          const std::vector<uint64_t>& recb, skv_result** out) {
+    hipStream_t st = ctx->stream;
+    const uint32_t k = (uint32_t)job.ranked.size();
+    const uint32_t n_runs = (uint32_t)runs.size();
+    const uint64_t R = recb[n_runs];
+    std::vector<uint64_t> stream_base(k + 1);
+    for (uint32_t s = 0; s <= k; ++s) stream_base[s] = recb[stream_first_run[s]];
+    uint64_t* d_recb = dbuf<uint64_t>(ctx, "run_recb", n_runs + 1);
+    uint32_t* d_srun = dbuf<uint32_t>(ctx, "fx_stream_run", k + 1);
+    uint64_t* d_sbase = dbuf<uint64_t>(ctx, "stream_base", k + 1);
+    uint32_t* d_flags = dbuf<uint32_t>(ctx, "flags", 4);
+    uint64_t* d_K = dbuf<uint64_t>(ctx, "K_out", 1);
+    h2d_up(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
+    h2d_up(ctx, d_srun, stream_first_run.data(), (k + 1) * 4);
+    h2d_up(ctx, d_sbase, stream_base.data(), (k + 1) * 8);
+    HIPCHK(hipMemsetAsync(d_flags, 0, 16, st));
+    HIPCHK(hipMemsetAsync(d_K, 0, 8, st));
+    mark(ctx, PH_PARSE);
+
+    FxArgs A{};
+    A.runs = d_runs;
+    A.run_recb = d_recb;
+    A.stream_run = d_srun;
+    A.stream_base = d_sbase;
+    A.k = k;
+    A.K = f.K;
+    A.V = f.V;
+    A.S = f.S;
+    uint64_t n = job.max_run_size >= 1 ? (job.max_run_size - 1) / f.S : 0;  // runs.rs:211-238
+    if (n < 1) n = 1;  // a record that alone exceeds max still forms its own run (runs.rs:219)
+    if (n > R) n = R;
+    A.n = n;
+    A.inv_S = 1.0 / (double)f.S;
+    A.inv_W = 1.0 / (double)(n * f.S + 1);
+    A.inv_n = 1.0 / (double)n;
+    A.flags = d_flags;
+    A.Kout = d_K;
+#if SKV_TILE_PROF
+    A.prof = dbuf<uint64_t>(ctx, "tile_prof", 16);
+    if (!ctx->prof_init) {
+        HIPCHK(hipMemsetAsync(A.prof, 0, 128, st));
+        ctx->prof_init = true;
+    }
+#endif
+
+    // ---- splitters: level 1 sampled from the run bytes, higher levels as in the general path
+    struct Level {
+        uint64_t N = 0, S = 1;
+        std::vector<uint64_t> off;
+        uint64_t *hi = nullptr, *lo = nullptr, *c = nullptr, *d_off = nullptr;
+        uint64_t *shi = nullptr, *slo = nullptr, *sc = nullptr;
+    };
+    std::vector<Level> lv(1);
+    lv[0].N = R;
+    lv[0].off = stream_base;
+    lv[0].d_off = d_sbase;
+    const uint64_t S_step = std::max<uint64_t>(2, (uint64_t)TILE_TARGET / std::max<uint32_t>(k, 1));
+    uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "scan_tmp", scan_tmp_words(std::max<uint64_t>(R / S_step + 1, 1 << 20)) + 64);
+    while (lv.back().N > (uint64_t)FX_CAP) {
+        const Level& P = lv.back();
+        Level L;
+        L.S = S_step;
+        L.off.resize(k + 1);
+        uint64_t acc = 0;
+        for (uint32_t j = 0; j < k; ++j) {
+            L.off[j] = acc;
+            acc += (P.off[j + 1] - P.off[j] + L.S - 1) / L.S;
+        }
+        L.off[k] = acc;
+        L.N = acc;
+        const int li = (int)lv.size();
+        char nm[64];
+        snprintf(nm, sizeof nm, "lv%d_hi", li); L.hi = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "lv%d_lo", li); L.lo = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "lv%d_c", li); L.c = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "lv%d_off", li); L.d_off = dbuf<uint64_t>(ctx, nm, k + 1);
+        h2d_up(ctx, L.d_off, L.off.data(), (k + 1) * 8);
+        if (li == 1) launch_fx_sample(st, A, L.d_off, L.S, L.N, L.hi, L.lo, L.c);
+        else launch_sample(st, false, P.hi, P.lo, P.c, nullptr, P.d_off, L.d_off, k, L.S, L.N, L.hi, L.lo, L.c);
+        lv.push_back(L);
+    }
+    uint64_t T0 = 1, m0 = 1;
+    for (int li = (int)lv.size() - 1; li >= 0; --li) {
+        Level& L = lv[li];
+        uint64_t T = 1, m = 1;
+        if (li + 1 < (int)lv.size()) {
+            m = std::max<uint64_t>(1, (uint64_t)TILE_TARGET / lv[li + 1].S);
+            T = std::max<uint64_t>(1, (lv[li + 1].N + m - 1) / m);
+        }
+        if (li == 0) {
+            T0 = T;
+            m0 = m;
+            break;
+        }
+        char nm[64];
+        snprintf(nm, sizeof nm, "bounds%d", li);
+        uint64_t* bounds = dbuf<uint64_t>(ctx, nm, (T + 1) * k);
+        const Level* U = li + 1 < (int)lv.size() ? &lv[li + 1] : nullptr;
+        launch_bounds(st, false, L.hi, L.lo, L.c, nullptr, L.d_off, k, U ? U->shi : nullptr, U ? U->slo : nullptr,
+                      U ? U->sc : nullptr, m, T, nullptr, bounds, d_flags + 2);
+        snprintf(nm, sizeof nm, "tile_n%d", li);
+        uint64_t* tile_n = dbuf<uint64_t>(ctx, nm, T);
+        snprintf(nm, sizeof nm, "tile_base%d", li);
+        uint64_t* tile_base = dbuf<uint64_t>(ctx, nm, T + 1);
+        launch_tile_n(st, bounds, k, T, tile_n);
+        launch_scan(st, tile_n, T, tile_base, scan_tmp);
+        TileOut O{};
+        snprintf(nm, sizeof nm, "x%d_hi", li); O.xhi = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "x%d_lo", li); O.xlo = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "x%d_c", li); O.xc = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "s%d_hi", li); L.shi = O.ohi = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "s%d_lo", li); L.slo = O.olo = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "s%d_c", li); L.sc = O.oc = dbuf<uint64_t>(ctx, nm, L.N);
+        HIPCHK(launch_tile(st, false, L.hi, L.lo, L.c, nullptr, bounds, k, T, tile_base, nullptr, nullptr, 0u, O,
+                           d_flags + 2));
+    }
+    A.T = T0;
+    A.bnd = dbuf<FxBound>(ctx, "fx_bnd", (T0 + 1) * k);
+    launch_fx_bounds(st, A, lv.size() > 1 ? lv[1].shi : nullptr, lv.size() > 1 ? lv[1].slo : nullptr, m0);
+    A.tstate = dbuf<uint64_t>(ctx, "fx_tstate", T0);
+    A.tcounter = dbuf<uint32_t>(ctx, "tile_ticket", 1);
+    HIPCHK(hipMemsetAsync(A.tstate, 0, T0 * 8, st));
+    HIPCHK(hipMemsetAsync(A.tcounter, 0, 4, st));
+    uint64_t total_rec_bytes = 0;
+    for (const RunInfo& r : runs) total_rec_bytes += r.len;
+    uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + R + 16);
+    A.out = d_out;
+    mark(ctx, PH_CHECK);
+    // ---- the fused tiles
+    HIPCHK(launch_fx_tile(st, A));
+    mark(ctx, PH_MERGE);
+    const uint64_t max_runs = (R + n - 1) / n;
+    DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", max_runs + 1);
+    uint64_t* d_nruns = dbuf<uint64_t>(ctx, "n_runs", 4);
+    launch_fx_desc(st, A, d_desc, d_nruns, max_runs);
+    HIPCHK(hipGetLastError());
+    mark(ctx, PH_CHAIN);
+    mark(ctx, PH_GATHER);
+    // ---- one readback: {runs, K, record bytes}, descriptors (count guessed from sizes), verdict
+    const uint64_t guess = std::min<uint64_t>(max_runs, 64 + total_rec_bytes / (n * f.S));
+    uint8_t* hp = (uint8_t*)pinned(ctx, 64 + guess * sizeof(DevRunDesc) + 16);
+    uint8_t* hv = hp + 64 + guess * sizeof(DevRunDesc);
+    d2h(ctx, hp, d_nruns, 24);
+    d2h(ctx, hp + 64, d_desc, guess * sizeof(DevRunDesc));
+    d2h(ctx, hv, d_flags, 16);
+    sync(ctx);
+    uint32_t hf[4];
+    memcpy(hf, hv, 16);
+    if (hf[2]) {
+        ctx->timings.fused_reject = hf[3] ? hf[3] : 0x80000000u;
+        return false;
+    }
+    uint64_t h3[3];
+    memcpy(h3, hp, 24);
+    const uint64_t n_out = h3[0], K = h3[1];
+    ResultBox* box = new ResultBox();
+    skv_result* res = &box->pub;
+    res->runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, n_out) * sizeof(skv_run_desc));
+    memcpy(res->runs, hp + 64, std::min(n_out, guess) * sizeof(DevRunDesc));
+    if (n_out > guess)
+        HIPCHK(hipMemcpy(res->runs + guess, d_desc + guess, (n_out - guess) * sizeof(DevRunDesc), hipMemcpyDeviceToHost));
+    res->n_runs = n_out;
+    res->bytes = d_out;
+    res->n_bytes = h3[2] + n_out;
+    res->in_bytes = job.in_bytes;
+    res->in_records = R;
+    res->out_records = K;
+    res->dropped_tables = 0;
+    skv_timings& t = ctx->timings;
+    const uint32_t reject = t.fused_reject;
+    t = skv_timings{};
+    t.path = SKV_PATH_FUSED;
+    t.fused_reject = reject;
+    t.hot_read_bytes = K * f.S + (R - K) * (9 + (uint64_t)f.K);  // survivors whole, superseded: header + key
+    t.hot_write_bytes = h3[2] + n_out;
+    if (ctx->profiling) {
+        HIPCHK(hipEventSynchronize(ctx->ev[PH_GATHER]));
+        float ms[PH_N] = {};
+        for (int p = PH_PARSE; p < PH_N; ++p) HIPCHK(hipEventElapsedTime(&ms[p], ctx->ev[p - 1], ctx->ev[p]));
+        float tot = 0;
+        HIPCHK(hipEventElapsedTime(&tot, ctx->ev[PH_START], ctx->ev[PH_GATHER]));
+        t.total_ms = tot;
+        t.parse_ms = ms[PH_PARSE];
+        t.check_ms = ms[PH_CHECK];  // splitters
+        t.merge_ms = ms[PH_MERGE];  // k_fx_tile: verify + merge + output bytes
+        t.chain_ms = ms[PH_CHAIN];
+        t.gather_ms = ms[PH_GATHER];
+        t.hot_ms = ms[PH_MERGE];
+    }
+    t.host_syncs = ctx->syncs;
+    *out = res;
+    return true;
+}
+
 // allow_deferred: on the fixed-stride fast path, launch the merge without waiting for the parse's
 // verdict (broken runs / order errors / oversized records) and check it with the final readback;
 // a bad verdict discards the result and reruns the call on the exact general path.
@@ -499,6 +700,17 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
                 recb[r + 1] = recb[r] + sum[r].records;
             }
             R = recb[n_runs];
+            // one record size and one key length <= 16 everywhere: the fused stride path
+            bool uniform = true;
+            for (uint32_t r = 1; r < n_runs && uniform; ++r) uniform = hf[r].S == hf[0].S && hf[r].K == hf[0].K;
+            const RunFmt f0 = hf[0];
+            const char* fenv = getenv("SKV_FUSED");
+            if (allow_deferred && uniform && !(job.flags & SKV_SPLIT_BY_TABLE) && !(fenv && fenv[0] == '0') &&
+                f0.K <= FX_MAX_K && f0.S >= FX_MIN_S && f0.S <= FX_MAX_S && k <= (uint32_t)TILE_TARGET / 2 &&
+                R < 0xFFFFFFFFull) {
+                if (compact_fused(ctx, job, runs, d_runs, stream_first_run, f0, recb, out)) return SKV_OK;
+                return compact_device(ctx, job, out, false);
+            }
             stream_tables();
             alloc_records();
             h2d_up(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
@@ -709,9 +921,9 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             HIPCHK(hipMemsetAsync(O.tstate, 0, 3 * T * 8, st));
             HIPCHK(hipMemsetAsync(O.tcounter, 0, 4, st));
 #if SKV_TILE_PROF
-            O.prof = dbuf<uint64_t>(ctx, "tile_prof", 8);
+            O.prof = dbuf<uint64_t>(ctx, "tile_prof", 16);
             if (!ctx->prof_init) {
-                HIPCHK(hipMemsetAsync(O.prof, 0, 64, st));
+                HIPCHK(hipMemsetAsync(O.prof, 0, 128, st));
                 ctx->prof_init = true;
             }
 #endif
@@ -812,7 +1024,11 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         t.gather_ms = ms[PH_GATHER];
         t.gather_read_bytes = kept_bytes;
         t.gather_write_bytes = kept_bytes + n_out_runs;
+        t.hot_ms = ms[PH_GATHER];
     }
+    ctx->timings.path = parsed ? SKV_PATH_FIXED : SKV_PATH_GENERAL;
+    ctx->timings.hot_read_bytes = kept_bytes;
+    ctx->timings.hot_write_bytes = kept_bytes + n_out_runs;
     ctx->timings.host_syncs = ctx->syncs;
     *out = res;
     return SKV_OK;
@@ -853,6 +1069,7 @@ static int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64
 static int run_guarded(skv_ctx* ctx, const Job& job, skv_result** out, double t_entry) {
     try {
         ctx->sync_ms = 0;
+        ctx->timings = skv_timings{};
         const int rc = compact_device(ctx, job, out);
         ctx->timings.host_total_ms = now_ms() - t_entry;
         ctx->timings.host_sync_ms = ctx->sync_ms;
@@ -901,10 +1118,11 @@ void skv_ctx_destroy(skv_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
 #if SKV_TILE_PROF
     if (ctx->bufs.count("tile_prof")) {
-        uint64_t pr[8];
-        if (hipMemcpy(pr, ctx->bufs["tile_prof"].p, 64, hipMemcpyDeviceToHost) == hipSuccess) {
-            fprintf(stderr, "tile phase time (100 MHz ticks summed over tiles):");
-            for (int i = 0; i < 8; ++i) fprintf(stderr, " %d:%llu", i, (unsigned long long)pr[i]);
+        uint64_t pr[16] = {};
+        const size_t nb = ctx->bufs["tile_prof"].cap >= 128 ? 128 : 64;
+        if (hipMemcpy(pr, ctx->bufs["tile_prof"].p, nb, hipMemcpyDeviceToHost) == hipSuccess) {
+            fprintf(stderr, "tile phase time (100 MHz ticks summed over tiles; [15] = tiles):");
+            for (int i = 0; i < (int)(nb / 8); ++i) fprintf(stderr, " %d:%llu", i, (unsigned long long)pr[i]);
             fprintf(stderr, "\n");
         }
     }

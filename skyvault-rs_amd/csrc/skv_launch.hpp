@@ -73,6 +73,13 @@ void launch_page_prep(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, c
                       const uint64_t* seg_r0, uint64_t* Dst, uint32_t* page_first, uint64_t max_K);
 void launch_gather_pages(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* P, const uint64_t* Dst,
                          const uint64_t* m_src, const uint32_t* page_first, uint8_t* out, uint64_t max_out_bytes);
+// skv_stride.hip — fused stride path
+void launch_fx_sample(hipStream_t, const FxArgs& A, const uint64_t* off_dst, uint64_t Sstep, uint64_t n_dst,
+                      uint64_t* dhi, uint64_t* dlo, uint64_t* dc);
+void launch_fx_bounds(hipStream_t, const FxArgs& A, const uint64_t* shi, const uint64_t* slo, uint64_t m);
+size_t fx_tile_lds_bytes(uint32_t k);
+hipError_t launch_fx_tile(hipStream_t, const FxArgs& A);
+void launch_fx_desc(hipStream_t, const FxArgs& A, DevRunDesc* descs, uint64_t* n_runs_out, uint64_t max_runs);
 uint64_t scan_tmp_words(uint64_t n);
 void launch_scan(hipStream_t, const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tmp);
 }  // namespace skv

@@ -1,0 +1,844 @@
+// skv_stride.hip — the fused stride path of the compaction (gfx950).
+//
+// When every input record is a Put of one size S whose key has one length K <= 16 (the shape
+// of BASELINE configs 1, 2 and 4), everything between the run bytes and the output bytes is
+// arithmetic except the merge itself:
+//   - record i of a run sits at run + 1 + i * S, so no parse pass writes record arrays: the
+//     merge tiles read the 16-byte keys straight from the run bytes and verify each record
+//     exactly as runs::read_run_stream would decode it (runs.rs:559-626);
+//   - every survivor has size S, so build_runs' greedy split (runs.rs:211-238) closes a run
+//     after n = (max - 1) / S records and survivor g lands at (g / n) * (n S + 1) + 1 + (g % n) S;
+//   - hence a tile that knows its first survivor's global index (decoupled look-back) writes its
+//     output bytes itself: one kernel reads every input byte once and writes every output byte
+//     once, and the LDS-bound merge of one tile overlaps the HBM-bound copy of another.
+// Kernels:
+//   k_fx_sample  level-1 splitter samples read from the runs (+ per-stream sample order check)
+//   k_fx_bounds  level-0 tile bounds: per (tile, stream) lower_bound over the run bytes
+//   k_fx_tile    verify + in-stream order check + k_way::merge (k_way.rs:113-179: key asc,
+//                seq_no desc, first per key) + look-back + output bytes
+//   k_fx_desc    output run descriptors and StatsV1 (runs.rs:102-109, :221-228, :271-280)
+// A record that is not what the run's first record promised, a key decrease inside a stream or
+// a splitter tile above FX_CAP sets the poison flag; the host then discards the result and
+// reruns the call on the general path, which reproduces the reference's exact outcome.
+#include "skv_launch.hpp"
+
+namespace skv {
+
+typedef unsigned int fx_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void fx_store16(uint8_t* p, uint4 v) {
+    fx_u32x4 vv = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(vv, (fx_u32x4*)p);  // written once, never re-read here
+}
+
+// q = z / d, r = z % d from a double reciprocal and one correction step (z < 2^52)
+__device__ __forceinline__ uint64_t fx_divmod(uint64_t z, uint64_t d, double inv, uint64_t& r) {
+    uint64_t q = (uint64_t)((double)z * inv);
+    int64_t rem = (int64_t)(z - q * d);
+    if (rem < 0) {
+        --q;
+        rem += (int64_t)d;
+    } else if ((uint64_t)rem >= d) {
+        ++q;
+        rem -= (int64_t)d;
+    }
+    r = (uint64_t)rem;
+    return q;
+}
+
+template <typename T>
+__device__ __forceinline__ T fx_wave_incl(T v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+
+// exclusive block scan; ws >= 16 entries of LDS
+template <typename T>
+__device__ T fx_block_excl(T v, T* ws, T& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    T inc = fx_wave_incl(v);
+    if (lane == 63) ws[wid] = inc;
+    __syncthreads();
+    if (wid == 0) {
+        T w = lane < nw ? ws[lane] : (T)0;
+        w = fx_wave_incl(w);
+        if (lane < nw) ws[lane] = w;
+    }
+    __syncthreads();
+    T off = wid ? ws[wid - 1] : (T)0;
+    total = ws[nw - 1];
+    __syncthreads();
+    return off + inc - v;
+}
+
+// last s in [0, m) with cb[s] <= i
+__device__ __forceinline__ uint32_t fx_seg(const uint32_t* cb, uint32_t m, uint32_t i) {
+    uint32_t lo = 0, hi = m;
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (cb[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// address of record `pos` (rank-order record index) of stream j
+__device__ __forceinline__ uint64_t fx_addr(const FxArgs& A, uint32_t j, uint64_t pos) {
+    uint32_t lo = A.stream_run[j], hi = A.stream_run[j + 1];
+    while (hi - lo > 1) {  // member runs of an L0-style concatenated stream
+        uint32_t mid = (lo + hi) >> 1;
+        if (A.run_recb[mid] <= pos) lo = mid;
+        else hi = mid;
+    }
+    return A.runs[lo].ptr + 1 + (pos - A.run_recb[lo]) * A.S;
+}
+
+// Loads through the global address space (an integer address would otherwise become a flat
+// access, which also counts against lgkmcnt and so serialises with every LDS wait).
+typedef unsigned int fx_v4 __attribute__((ext_vector_type(4)));
+typedef unsigned int fx_v2 __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(1))) fx_v4 fx_g16;
+typedef const __attribute__((address_space(1))) fx_v2 fx_g8;
+typedef const __attribute__((address_space(1))) uint32_t fx_g4;
+__device__ __forceinline__ uint4 fx_ld16(uint64_t a) {  // unaligned: full rate on gfx950
+    const fx_v4 v = *(fx_g16*)a;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// One record's header pieces: marker + key_len (bytes 0..7), the 16 bytes from the key start,
+// val_len (at 5 + K). All inside the record (S >= 32), issued as three independent loads.
+struct FxRec {
+    uint2 h;
+    uint4 k;
+    uint32_t v;
+};
+__device__ __forceinline__ void fx_issue(uint64_t a, uint32_t K, FxRec& r) {
+    const fx_v2 h = *(fx_g8*)a;
+    r.h = make_uint2(h.x, h.y);
+    r.k = fx_ld16(a + 5);
+    r.v = *(fx_g4*)(a + 5 + K);
+}
+
+// The record at a, decoded as read_run_stream does (runs.rs:559-626): marker 1 (Put), key_len
+// == K, UTF-8 key (runs.rs:585-591), val_len == V, so its size is S. Returns false otherwise.
+// Key -> (hi, lo) big-endian, zero padded past K.
+__device__ __forceinline__ bool fx_check(const FxArgs& A, const FxRec& r, uint64_t a, uint64_t& hi, uint64_t& lo) {
+    const uint32_t marker = r.h.x & 0xFFu;
+    const uint32_t klen = __builtin_bswap32(__builtin_amdgcn_alignbyte(r.h.y, r.h.x, 1));
+    const uint32_t vlen = __builtin_bswap32(r.v);
+    const uint32_t d0 = r.k.x & dword_mask(0, A.K, 0), d1 = r.k.y & dword_mask(0, A.K, 1);
+    const uint32_t d2 = r.k.z & dword_mask(0, A.K, 2), d3 = r.k.w & dword_mask(0, A.K, 3);
+    hi = ((uint64_t)__builtin_bswap32(d0) << 32) | __builtin_bswap32(d1);
+    lo = ((uint64_t)__builtin_bswap32(d2) << 32) | __builtin_bswap32(d3);
+    bool ok = marker == 1u && klen == A.K && vlen == A.V;
+    if (ok && ((d0 | d1 | d2 | d3) & 0x80808080u)) ok = utf8_valid((const uint8_t*)a + 5, A.K);
+    return ok;
+}
+
+__device__ __forceinline__ bool fx_key(const FxArgs& A, uint64_t a, uint64_t& hi, uint64_t& lo) {
+    FxRec r;
+    fx_issue(a, A.K, r);
+    return fx_check(A, r, a, hi, lo);
+}
+
+__device__ __forceinline__ bool fx_gt(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
+    return ah > bh || (ah == bh && al > bl);
+}
+
+__device__ __forceinline__ void fx_poison(const FxArgs& A, uint32_t why) {
+    atomicOr(A.flags + 3, why);
+    atomicOr(A.flags + 2, 1u);
+}
+
+// ---------------------------------------------------------------------------------------------
+// splitters
+
+// level-1 samples: every Sstep-th record of each stream, c = K << 32 | pos (the element form of
+// k_tile<false>). Samples out of order inside a stream poison the call before any sample tile
+// merges them (a merge of unsorted lists is not a permutation).
+__global__ void k_fx_sample(FxArgs A, const uint64_t* __restrict__ off_dst, uint64_t Sstep, uint64_t n_dst,
+                            uint64_t* dhi, uint64_t* dlo, uint64_t* dc) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_dst) return;
+    uint32_t lo = 0, hi = A.k;
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (off_dst[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    const uint64_t pos = A.stream_base[lo] + (i - off_dst[lo]) * Sstep;
+    uint64_t h, l;
+    fx_key(A, fx_addr(A, lo, pos), h, l);
+    dhi[i] = h;
+    dlo[i] = l;
+    dc[i] = ((uint64_t)A.K << 32) | pos;
+    if (i > off_dst[lo]) {
+        uint64_t ph, pl;
+        fx_key(A, fx_addr(A, lo, pos - Sstep), ph, pl);
+        if (fx_gt(ph, pl, h, l)) fx_poison(A, FXR_SAMPLE);
+    }
+}
+
+// member run of stream j holding record pos
+__device__ __forceinline__ uint32_t fx_run(const FxArgs& A, uint32_t j, uint64_t pos) {
+    uint32_t lo = A.stream_run[j], hi = A.stream_run[j + 1];
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (A.run_recb[mid] <= pos) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// bnd[t*k + j].pos = first record of stream j whose key >= splitter t (sorted level-1 samples,
+// every m-th one), plus what tile t needs to start its segment without further searches: the
+// record's address, the records left in its member run, and the key of the record before it
+// (the in-stream order check across tile edges, runs.rs:190-198)
+__global__ void k_fx_bounds(FxArgs A, const uint64_t* __restrict__ shi, const uint64_t* __restrict__ slo, uint64_t m) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t k = A.k;
+    if (g >= (A.T + 1) * k) return;
+    const uint64_t t = g / k;
+    const uint32_t j = (uint32_t)(g - t * k);
+    const uint64_t s0 = A.stream_base[j], s1 = A.stream_base[j + 1];
+    uint64_t a = s0, b = s1;
+    FxBound o{};
+    if (t == A.T) {
+        a = s1;
+    } else if (t > 0) {
+        if (__hip_atomic_load(A.flags + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            o.pos = s0;
+            A.bnd[g] = o;
+            return;
+        }
+        const uint64_t h = shi[t * m], l = slo[t * m];
+        while (a < b) {
+            const uint64_t mid = (a + b) >> 1;
+            uint64_t eh, el;
+            fx_key(A, fx_addr(A, j, mid), eh, el);
+            if (eh < h || (eh == h && el < l)) a = mid + 1;
+            else b = mid;
+        }
+    }
+    o.pos = a;
+    if (a < s1) {
+        const uint32_t r = fx_run(A, j, a);
+        o.addr = A.runs[r].ptr + 1 + (a - A.run_recb[r]) * A.S;
+        o.rem = A.run_recb[r + 1] - a;
+    }
+    if (a > s0 && t < A.T) {
+        o.has_prev = 1;
+        fx_key(A, fx_addr(A, j, a - 1), o.ph, o.pl);
+    }
+    A.bnd[g] = o;
+}
+
+// ---------------------------------------------------------------------------------------------
+// the fused tile
+
+// decoupled look-back over tiles with one wave (64 predecessors per probe), one 62-bit counter
+// per tile (flag in bits 62-63: 1 aggregate, 2 inclusive prefix). Tiles take tickets in start
+// order, so every predecessor of a waiting tile is resident or done. Called by wave 0.
+__device__ uint64_t fx_lookback(uint64_t* st, uint64_t t, uint64_t agg) {
+    constexpr uint64_t FA = 1ull << 62, FI = 2ull << 62, VM = FA - 1;
+    const int lane = threadIdx.x & 63;
+    if (t == 0) {
+        if (lane == 0) __hip_atomic_store(&st[0], FI | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    if (lane == 0) __hip_atomic_store(&st[t], FA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t acc = 0;
+    int64_t top = (int64_t)t - 1;  // window: predecessors top, top-1, ..., top-63
+    for (;;) {
+        const int64_t p = top - lane;
+        const uint64_t v = p >= 0 ? __hip_atomic_load(&st[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : FI;
+        const uint64_t f = v >> 62;
+        const uint64_t incl = __ballot(f == 2), none = __ballot(f == 0);
+        const int first = incl ? __builtin_ctzll(incl) : 64;       // nearest inclusive prefix
+        const uint64_t upto = first == 64 ? ~0ull : (first == 63 ? ~0ull : ((2ull << first) - 1));
+        if (none & upto) {  // a predecessor before it has not published yet
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint64_t x = (uint64_t)lane <= (uint64_t)first ? (v & VM) : 0;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+        acc += x;
+        if (first < 64) break;
+        top -= 64;
+    }
+    if (lane == 0) __hip_atomic_store(&st[t], FI | (acc + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return acc;
+}
+
+// Output bytes [x0, x1) (inside one 16-byte block B) that start at byte o of local survivor j
+// (o == -1: the version byte before it; qj = j's index inside its output run). Pieces are taken
+// in output order: record tail, version byte of the next run, next record, ...
+__device__ uint4 fx_compose(const FxArgs& A, const uint64_t* src, uint64_t B, uint64_t x0, uint64_t x1, uint32_t j,
+                            int64_t o, uint64_t qj) {
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    uint64_t x = x0;
+    while (x < x1) {
+        const uint32_t a = (uint32_t)(x - B);
+        if (o < 0) {  // version byte (runs.rs:241-246)
+            const uint32_t sh = 8 * (a & 3), q = a >> 2;
+            if (q == 0) acc.x |= 1u << sh;
+            else if (q == 1) acc.y |= 1u << sh;
+            else if (q == 2) acc.z |= 1u << sh;
+            else acc.w |= 1u << sh;
+            ++x;
+            o = 0;
+            continue;
+        }
+        const uint64_t m = (A.S - (uint64_t)o) < (x1 - x) ? (A.S - (uint64_t)o) : (x1 - x);
+        const uint32_t b = a + (uint32_t)m;
+        uint4 w = load_window16((const uint8_t*)src[j] + o, (uint32_t)m);
+        w = shl_bytes(w, a);
+        acc.x |= w.x & dword_mask(a, b, 0);
+        acc.y |= w.y & dword_mask(a, b, 1);
+        acc.z |= w.z & dword_mask(a, b, 2);
+        acc.w |= w.w & dword_mask(a, b, 3);
+        x += m;
+        o += (int64_t)m;
+        if ((uint64_t)o == A.S) {
+            ++j;
+            ++qj;
+            o = 0;
+            if (qj == A.n) {
+                qj = 0;
+                o = -1;
+            }
+        }
+    }
+    return acc;
+}
+
+__device__ __forceinline__ void fx_store_bytes(uint8_t* out, uint64_t B, uint64_t x0, uint64_t x1, uint4 v) {
+    for (uint64_t y = x0; y < x1; ++y) out[y] = (uint8_t)byte_of(v, (uint32_t)(y - B));
+}
+
+// key order with the left (newer seq_no) side winning ties
+__device__ __forceinline__ bool fx_le(const ulong2& a, const ulong2& b) {
+    return a.x < b.x || (a.x == b.x && a.y <= b.y);
+}
+
+__device__ __forceinline__ uint4 fx_vbyte_then(uint4 head) {  // version byte, then 15 record bytes
+    uint4 v = shl_bytes(head, 1);
+    v.x |= 1u;
+    return v;
+}
+
+// x / d and x % d for x < 2^31 (double reciprocal, one correction)
+__device__ __forceinline__ uint32_t fx_div32(uint32_t x, uint32_t d, double inv, uint32_t& r) {
+    uint32_t q = (uint32_t)((double)x * inv);
+    int32_t rem = (int32_t)(x - q * d);
+    if (rem < 0) {
+        --q;
+        rem += (int32_t)d;
+    } else if ((uint32_t)rem >= d) {
+        ++q;
+        rem -= (int32_t)d;
+    }
+    r = (uint32_t)rem;
+    return q;
+}
+
+#if SKV_TILE_PROF
+#define FXPROF(i)                                                                               \
+    do {                                                                                        \
+        if (threadIdx.x == 0) {                                                                 \
+            const uint64_t now_ = __builtin_amdgcn_s_memrealtime();                             \
+            atomicAdd((unsigned long long*)&A.prof[i], (unsigned long long)(now_ - tp_last));  \
+            tp_last = now_;                                                                     \
+        }                                                                                       \
+    } while (0)
+#else
+#define FXPROF(i) do {} while (0)
+#endif
+
+// LDS: key[FX_CAP] 16 B (by position; after the merge: source addresses by survivor, u64)
+//      | prevk[k] 16 B | segaddr[k] sbase[k] u64 | cb0[k+1] cbA[k+1] cbB[k+1] u32 | id[FX_CAP] u16
+//      | prevok[k] u8
+__global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
+    constexpr int PER = FX_CAP / FX_THREADS;
+    extern __shared__ __attribute__((aligned(16))) uint64_t fx_smem[];
+    const uint32_t k = A.k;
+    ulong2* key = (ulong2*)fx_smem;
+    ulong2* prevk = key + FX_CAP;
+    uint64_t* segaddr = (uint64_t*)(prevk + k);
+    uint64_t* sbase = segaddr + k;
+    uint32_t* cb0 = (uint32_t*)(sbase + k);
+    uint32_t* cbA = cb0 + (k + 1);
+    uint32_t* cbB = cbA + (k + 1);
+    uint16_t* id = (uint16_t*)(cbB + (k + 1));
+    uint8_t* prevok = (uint8_t*)(id + FX_CAP);
+    __shared__ uint64_t ws[16];
+    __shared__ uint64_t s_t, s_g0;
+    __shared__ uint32_t s_dead, s_bad;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t S = A.S;
+#if SKV_TILE_PROF
+    uint64_t tp_last = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) atomicAdd((unsigned long long*)&A.prof[15], 1ull);
+#endif
+    if (tid == 0) {
+        s_t = atomicAdd(A.tcounter, 1u);
+        s_dead = __hip_atomic_load(A.flags + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_bad = 0;
+    }
+    __syncthreads();
+    const uint64_t t = s_t;
+    // ---- segments: stream j contributes its records [bnd[t][j].pos, bnd[t+1][j].pos)
+    uint64_t tot = 0;
+    if (!s_dead) {
+        for (uint32_t j0 = 0; j0 < k; j0 += FX_THREADS) {
+            const uint32_t j = j0 + tid;
+            uint64_t len = 0;
+            if (j < k) {
+                const FxBound b = A.bnd[t * k + j];
+                uint64_t b1 = A.bnd[(t + 1) * k + j].pos;
+                if (b1 < b.pos) {  // splitters over unsorted input
+                    atomicOr(&s_bad, FXR_SPLIT);
+                    b1 = b.pos;
+                }
+                len = b1 - b.pos;
+                sbase[j] = b.pos;
+                segaddr[j] = len <= b.rem ? b.addr : 0;  // 0: the segment spans member runs
+                prevk[j] = make_ulong2(b.ph, b.pl);
+                prevok[j] = (uint8_t)b.has_prev;
+                if (len > FX_CAP) len = FX_CAP + 1;
+            }
+            uint64_t part;
+            const uint64_t ex = fx_block_excl<uint64_t>(len, ws, part);
+            if (j < k) cb0[j] = (uint32_t)(tot + ex < FX_CAP + 1 ? tot + ex : FX_CAP + 1);
+            tot += part;
+        }
+        if (tid == 0) {
+            cb0[k] = (uint32_t)(tot < FX_CAP + 1 ? tot : FX_CAP + 1);
+            if (tot > FX_CAP) s_bad |= FXR_OVERSIZE;
+        }
+    }
+    __syncthreads();
+    FXPROF(0);
+    const uint32_t n = (uint32_t)(tot <= FX_CAP ? tot : 0);
+    const bool live = !s_dead && !s_bad;
+    // ---- load + verify every record of the tile: addresses from LDS, all loads issued first
+    uint32_t bad = 0;
+    {
+        uint64_t ad[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const uint32_t e = tid + u * FX_THREADS;
+            ad[u] = 0;
+            if (live && e < n) {
+                const uint32_t j = fx_seg(cb0, k + 1, e);
+                const uint64_t sa = segaddr[j];
+                ad[u] = sa ? sa + (uint64_t)(e - cb0[j]) * S : fx_addr(A, j, sbase[j] + (e - cb0[j]));
+            }
+        }
+        FxRec rec[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u)
+            if (ad[u]) fx_issue(ad[u], A.K, rec[u]);
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            if (ad[u]) {
+                const uint32_t e = tid + u * FX_THREADS;
+                uint64_t h, l;
+                if (!fx_check(A, rec[u], ad[u], h, l)) bad |= FXR_RECORD;
+                key[e] = make_ulong2(h, l);
+                id[e] = (uint16_t)e;
+            }
+        }
+    }
+    __syncthreads();
+    FXPROF(1);
+    // ---- order check inside each stream (runs.rs:190-198): against the previous record of the
+    // same stream (the previous element of the segment, or the record before the segment)
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const uint32_t e = tid + u * FX_THREADS;
+        if (live && e < n) {
+            const uint32_t j = fx_seg(cb0, k + 1, e);
+            const ulong2 c = key[e];
+            bool has = true;
+            ulong2 pv;
+            if (e > cb0[j]) pv = key[e - 1];
+            else {
+                pv = prevk[j];
+                has = prevok[j] != 0;
+            }
+            if (has && !fx_le(pv, c)) bad |= FXR_ORDER;  // a strict decrease
+        }
+    }
+    if (bad) atomicOr(&s_bad, bad);
+    __syncthreads();
+    FXPROF(2);
+    if (s_dead || s_bad) {  // publish an empty aggregate so later tiles never wait on this one
+        if (tid == 0) {
+            if (s_bad) fx_poison(A, s_bad);
+            __hip_atomic_store(&A.tstate[t], (t == 0 ? 2ull : 1ull) << 62, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    // ---- k_way::merge order (k_way.rs:20-27, :113-179): pairwise merge-path rounds over the k
+    // stream segments (segment s pairs with s ^ 1, the left one holds newer seq_nos and wins ties,
+    // so equal keys end up seq_no-descending, and in stream order within a stream). Each thread
+    // produces PER consecutive outputs of a round: one merge-path search, then a sequential merge.
+    const uint32_t i0 = tid * PER;
+    {
+        uint32_t m = k;
+        const uint32_t* cb = cb0;
+        uint32_t* cbn = cbA;
+        while (m > 1) {
+            const uint32_t mp = (m + 1) >> 1;
+            ulong2 ok_[PER];
+            uint32_t oi[PER];
+            uint32_t pos = i0, ia = 0, a1 = 0, ib = 0, b1 = 0;
+            ulong2 hA = make_ulong2(0, 0), hB = make_ulong2(0, 0);
+            bool setup = true;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                ok_[q] = make_ulong2(0, 0);
+                oi[q] = 0;
+                if (pos < n) {
+                    if (setup || pos >= b1) {
+                        uint32_t lo = 0, hi = mp;  // pair p with cb[2p] <= pos
+                        while (hi - lo > 1) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (cb[2 * mid] <= pos) lo = mid;
+                            else hi = mid;
+                        }
+                        const uint32_t a0 = cb[2 * lo];
+                        a1 = cb[2 * lo + 1 < m ? 2 * lo + 1 : m];
+                        b1 = cb[2 * lo + 2 < m ? 2 * lo + 2 : m];
+                        const uint32_t lenA = a1 - a0, lenB = b1 - a1, d = pos - a0;
+                        uint32_t l = d > lenB ? d - lenB : 0, h = d < lenA ? d : lenA;
+                        while (l < h) {  // how many of the first d outputs come from A
+                            const uint32_t mid = (l + h) >> 1;
+                            if (fx_le(key[a0 + mid], key[a1 + d - mid - 1])) l = mid + 1;
+                            else h = mid;
+                        }
+                        ia = a0 + l;
+                        ib = a1 + (d - l);
+                        if (ia < a1) hA = key[ia];
+                        if (ib < b1) hB = key[ib];
+                        setup = false;
+                    }
+                    const bool takeA = ia < a1 && (ib >= b1 || fx_le(hA, hB));
+                    if (takeA) {
+                        ok_[q] = hA;
+                        oi[q] = id[ia];
+                        if (++ia < a1) hA = key[ia];
+                    } else {
+                        ok_[q] = hB;
+                        oi[q] = id[ib];
+                        if (++ib < b1) hB = key[ib];
+                    }
+                    ++pos;
+                }
+            }
+            __syncthreads();  // every thread has read its inputs of this round
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                if (i0 + q < n) {
+                    key[i0 + q] = ok_[q];
+                    id[i0 + q] = (uint16_t)oi[q];
+                }
+            }
+            for (uint32_t p = tid; p <= mp; p += FX_THREADS) cbn[p] = p < mp ? cb[2 * p] : cb[m];
+            __syncthreads();
+            cb = cbn;
+            cbn = cbn == cbA ? cbB : cbA;
+            m = mp;
+        }
+    }
+    FXPROF(3);
+    // ---- first record per key survives (k_way.rs:146-151); source address of each survivor
+    uint32_t keep = 0;
+    uint64_t sad[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = i0 + q;
+        sad[q] = 0;
+        if (i < n) {
+            const ulong2 c = key[i];
+            bool first = i == 0;
+            if (!first) {
+                const ulong2 p = key[i - 1];
+                first = p.x != c.x || p.y != c.y;
+            }
+            if (first) {
+                keep |= 1u << q;
+                const uint32_t e = id[i];
+                const uint32_t j = fx_seg(cb0, k + 1, e);
+                const uint64_t sa = segaddr[j];
+                sad[q] = sa ? sa + (uint64_t)(e - cb0[j]) * S : fx_addr(A, j, sbase[j] + (e - cb0[j]));
+            }
+        }
+    }
+    uint32_t total;
+    uint32_t c = fx_block_excl<uint32_t>((uint32_t)__builtin_popcount(keep), (uint32_t*)ws, total);  // barriers
+    uint64_t* src = (uint64_t*)key;  // source address by survivor
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+        if (keep & (1u << q)) src[c++] = sad[q];
+    const uint32_t cnt = total;
+    FXPROF(4);
+    if (tid < 64) {
+        const uint64_t g0 = fx_lookback(A.tstate, t, cnt);
+        if (tid == 0) {
+            s_g0 = g0;
+            if (t == A.T - 1) *A.Kout = g0 + cnt;
+            s_dead = __hip_atomic_load(A.flags + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    FXPROF(5);
+    if (!cnt || s_dead) return;
+    // ---- output bytes of survivors g0 .. g0+cnt-1 (build_runs' bytes, runs.rs:241-267). The
+    // tile's survivors form "pieces": runs of consecutive survivors inside one output run; piece 0
+    // starts at survivor 0, piece i >= 1 at survivor jb1 + (i-1) n behind its run's version byte.
+    const uint64_t nr = A.n, W = nr * S + 1;
+    const uint64_t g0 = s_g0;
+    uint64_t q0;
+    const uint64_t r0 = fx_divmod(g0, nr, A.inv_n, q0);
+    const uint64_t a0 = r0 * W + 1 + q0 * S;  // first survivor's record
+    const uint64_t start = q0 == 0 ? a0 - 1 : a0;
+    const uint64_t jb1 = nr - q0;             // first survivor (local) opening a new run
+    const uint64_t V1 = a0 + jb1 * S;         // its version byte (when jb1 < cnt)
+    const uint64_t jL = cnt - 1;
+    uint64_t nbL = 0;
+    if (jL >= jb1) {
+        uint64_t rr;
+        nbL = 1 + fx_divmod(jL - jb1, nr, A.inv_n, rr);
+    }
+    const uint64_t aL = a0 + jL * S + nbL;
+    const uint64_t end = aL + S;
+    uint8_t* out = A.out;
+    const uint32_t S32 = (uint32_t)S;
+    const uint64_t Blo = (start + 15) & ~15ull, Bhi = end & ~15ull;
+    const uint32_t nb = Bhi > Blo ? (uint32_t)((Bhi - Blo) >> 4) : 0u;
+    constexpr int U = SKV_FX_U;
+    // At most one run boundary inside the tile (n >= cnt, e.g. 4 MiB runs): each lane walks its
+    // blocks with incremental (record, offset) coordinates. Every block, including those that
+    // straddle a record end or start at a version byte, is written by the wave instruction that
+    // writes its neighbours, so each 128-B output line is completed at once and each input line
+    // is read while the neighbouring lanes read it (no partial-line writes, no re-reads).
+    // Tiles crossing several runs (small max sizes) take the generic loop.
+#ifndef SKV_FX_GENERIC_COPY
+#define SKV_FX_GENERIC_COPY 0            // 1: every tile takes the generic copy loop (A/B diagnostics)
+#endif
+    const bool multi = SKV_FX_GENERIC_COPY || (jb1 < cnt && cnt - jb1 > nr);
+    if (!multi) {
+        const uint64_t V0 = q0 == 0 ? a0 - 1 : ~0ull;       // version byte before survivor 0
+        const uint64_t Vb = jb1 < cnt ? V1 : ~0ull;          // version byte before survivor jb1
+        constexpr uint32_t D = 16u * FX_THREADS;              // bytes between a lane's blocks
+        const uint32_t dq = D / S32, dr = D % S32;
+        uint64_t B = Blo + 16ull * tid;
+        uint32_t j = 0, o = 0;
+        bool past = B > Vb;
+        {
+            const int64_t y = (int64_t)(B - a0) - (past ? 1 : 0);
+            if (y < 0) {  // B is the version byte before survivor 0: y == -1
+                j = 0xFFFFFFFFu;
+                o = S32 - 1;
+            } else if (B < Bhi) {
+                j = fx_div32((uint32_t)y, S32, A.inv_S, o);
+            }
+        }
+        for (uint32_t b = tid; b < nb; b += U * FX_THREADS) {
+            uint64_t aL[U], aX[U];
+            uint32_t mode[U], sh[U];  // 0: one record, 1: record tail + next, 2: version byte + record, 3: tail + version + next
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                aL[u] = aX[u] = 0;
+                mode[u] = 0;
+                sh[u] = 0;
+                if (b + u * FX_THREADS < nb) {
+                    if (B == V0 || B == Vb) {
+                        aL[u] = src[B == V0 ? 0 : (uint32_t)jb1];
+                        mode[u] = 2;
+                    } else if (o + 16 <= S32) {
+                        aL[u] = src[j] + o;
+                    } else {  // straddles record j's end: its last 16 bytes + what follows it
+                        aL[u] = src[j] + S - 16;
+                        aX[u] = src[j + 1];
+                        mode[u] = j + 1 == jb1 ? 3 : 1;
+                        sh[u] = 16 - (S32 - o);
+                    }
+                }
+                B += D;  // this lane's next block
+                o += dr;
+                j += dq;
+                if (o >= S32) {
+                    o -= S32;
+                    ++j;
+                }
+                if (!past && B > Vb) {  // crossed the run boundary: one version byte earlier
+                    past = true;
+                    if (o == 0) {
+                        o = S32 - 1;
+                        --j;
+                    } else {
+                        --o;
+                    }
+                }
+            }
+            uint4 L[U], X[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                L[u] = aL[u] ? fx_ld16(aL[u]) : make_uint4(0, 0, 0, 0);
+                X[u] = aX[u] ? fx_ld16(aX[u]) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!aL[u]) continue;
+                uint4 v = L[u];
+                if (mode[u] == 2) v = fx_vbyte_then(L[u]);
+                else if (mode[u] != 0) v = funnel16(L[u], mode[u] == 3 ? fx_vbyte_then(X[u]) : X[u], sh[u]);
+                fx_store16(out + Blo + 16ull * (b + u * FX_THREADS), v);
+            }
+        }
+    }
+    // Per block: addresses and mode first, then every load of the U blocks, then the merges and
+    // stores, so that a lane keeps U (or 2U) loads in flight instead of waiting on each.
+    if (multi) for (uint32_t b = tid; b < nb; b += U * FX_THREADS) {
+        uint64_t aL[U], aX[U];
+        uint32_t mode[U], sh[U];  // mode 0: one record, 1: record tail + next, 2: version byte + record
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t bb = b + u * FX_THREADS;
+            aL[u] = 0;
+            aX[u] = 0;
+            mode[u] = 0;
+            sh[u] = 0;
+            if (bb < nb) {
+                const uint64_t B = Blo + 16ull * bb;
+                uint64_t pj = 0, pend = jb1;
+                int64_t rel;
+                if (jb1 >= cnt || B < V1) {
+                    rel = (int64_t)(B - a0);
+                } else {
+                    const uint64_t d = B - V1;
+                    uint64_t i = 0, dr = d;
+                    if (d >= W) i = fx_divmod(d, W, A.inv_W, dr);
+                    pj = jb1 + i * nr;
+                    pend = pj + nr;
+                    rel = (int64_t)dr - 1;
+                }
+                if (rel < 0) {  // the block starts at a version byte
+                    if (pj < cnt) {
+                        aL[u] = src[pj];
+                        mode[u] = 2;
+                    }
+                } else {
+                    uint32_t o;
+                    const uint32_t j = (uint32_t)pj + fx_div32((uint32_t)rel, S32, A.inv_S, o);
+                    if (o + 16 <= S32) {
+                        if (j < cnt) aL[u] = src[j] + o;
+                    } else if (j + 1 < cnt) {  // straddles record j's end: its last 16 bytes + what follows
+                        aL[u] = src[j] + S - 16;
+                        aX[u] = src[j + 1];
+                        mode[u] = (j + 1 == pend) ? 3 : 1;  // 3: a version byte sits between the records
+                        sh[u] = 16 - (S32 - o);
+                    }
+                }
+            }
+        }
+        uint4 L[U], X[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            L[u] = aL[u] ? fx_ld16(aL[u]) : make_uint4(0, 0, 0, 0);
+            X[u] = aX[u] ? fx_ld16(aX[u]) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!aL[u]) continue;
+            uint4 v = L[u];
+            if (mode[u] == 2) v = fx_vbyte_then(L[u]);
+            else if (mode[u] != 0) v = funnel16(L[u], mode[u] == 3 ? fx_vbyte_then(X[u]) : X[u], sh[u]);
+            fx_store16(out + Blo + 16ull * (b + u * FX_THREADS), v);
+        }
+    }
+    FXPROF(6);
+    // tile edges: blocks shared with the neighbouring tiles get this tile's bytes only
+    if (tid == 0 && (start & 15)) {
+        const uint64_t B = start & ~15ull, x1 = B + 16 < end ? B + 16 : end;
+        fx_store_bytes(out, B, start, x1, fx_compose(A, src, B, start, x1, 0, q0 == 0 ? -1 : 0, q0));
+    }
+    if (tid == FX_THREADS - 1 && (end & 15)) {
+        const uint64_t B = end & ~15ull;
+        uint64_t qL;
+        fx_divmod(q0 + jL, nr, A.inv_n, qL);
+        fx_store_bytes(out, B, B, end, fx_compose(A, src, B, B, end, (uint32_t)jL, (int64_t)(B - aL), qL));
+    }
+    FXPROF(7);
+}
+
+// descriptors + StatsV1 of the output runs: run r holds survivors [r n, min((r+1) n, K))
+__global__ void k_fx_desc(FxArgs A, DevRunDesc* descs, uint64_t* n_runs_out, uint64_t max_runs) {
+    const uint64_t K = *A.Kout, nr = A.n, S = A.S, W = nr * S + 1;
+    uint64_t runs = (K + nr - 1) / nr;
+    if (runs > max_runs) runs = max_runs;  // poisoned call: Kout is meaningless, stay in bounds
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        n_runs_out[0] = runs;
+        n_runs_out[1] = K;
+        n_runs_out[2] = K * S;
+    }
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < runs; r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = K - r * nr < nr ? K - r * nr : nr;
+        DevRunDesc d;
+        d.off = r * W;
+        d.len = 1 + c * S;
+        d.put_count = c;
+        d.delete_count = 0;
+        d.min_key_off = d.off + 1 + 5;
+        d.min_key_len = A.K;
+        d.max_key_off = d.off + 1 + (c - 1) * S + 5;
+        d.max_key_len = A.K;
+        d.table_id = 0;
+        d.reserved = 0;
+        descs[r] = d;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+static inline unsigned fx_blocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+void launch_fx_sample(hipStream_t s, const FxArgs& A, const uint64_t* off_dst, uint64_t Sstep, uint64_t n_dst,
+                      uint64_t* dhi, uint64_t* dlo, uint64_t* dc) {
+    if (n_dst) k_fx_sample<<<fx_blocks(n_dst, 256), 256, 0, s>>>(A, off_dst, Sstep, n_dst, dhi, dlo, dc);
+}
+void launch_fx_bounds(hipStream_t s, const FxArgs& A, const uint64_t* shi, const uint64_t* slo, uint64_t m) {
+    const uint64_t n = (A.T + 1) * A.k;
+    if (n) k_fx_bounds<<<fx_blocks(n, 256), 256, 0, s>>>(A, shi, slo, m);
+}
+size_t fx_tile_lds_bytes(uint32_t k) {
+    return (size_t)FX_CAP * 16 + (size_t)k * 16 + 2 * (size_t)k * 8 + 3 * (size_t)(k + 1) * 4 + (size_t)FX_CAP * 2 + k + 16;
+}
+hipError_t launch_fx_tile(hipStream_t s, const FxArgs& A) {
+    const size_t lds = fx_tile_lds_bytes(A.k);
+    static size_t lds_set[64] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (lds > lds_set[dev & 63]) {
+        (void)hipFuncSetAttribute((const void*)k_fx_tile, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        lds_set[dev & 63] = lds;
+    }
+    k_fx_tile<<<(unsigned)A.T, FX_THREADS, lds, s>>>(A);
+    return hipGetLastError();
+}
+void launch_fx_desc(hipStream_t s, const FxArgs& A, DevRunDesc* descs, uint64_t* n_runs_out, uint64_t max_runs) {
+    unsigned blocks = fx_blocks(max_runs ? max_runs : 1, 256);
+    if (blocks > 4096) blocks = 4096;
+    k_fx_desc<<<blocks, 256, 0, s>>>(A, descs, n_runs_out, max_runs);
+}
+
+}  // namespace skv

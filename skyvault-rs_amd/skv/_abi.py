@@ -91,7 +91,17 @@ class SkvTimings(C.Structure):
         ("host_syncs", C.c_uint64),
         ("host_total_ms", C.c_double),
         ("host_sync_ms", C.c_double),
+        ("path", C.c_uint32),
+        ("fused_reject", C.c_uint32),
+        ("hot_ms", C.c_double),
+        ("hot_read_bytes", C.c_uint64),
+        ("hot_write_bytes", C.c_uint64),
     ]
+
+
+# skv_timings.path (include/skv.h)
+PATH_GENERAL, PATH_FIXED, PATH_FUSED = 1, 2, 3
+PATH_NAMES = {PATH_GENERAL: "general", PATH_FIXED: "fixed", PATH_FUSED: "fused"}
 
 
 # Every symbol include/skv.h declares (tests/test_abi.py checks the built library exports them).
