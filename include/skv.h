@@ -128,6 +128,8 @@ typedef struct {
     double hot_ms;
     uint64_t hot_read_bytes;
     uint64_t hot_write_bytes;
+    uint32_t sorted;         /* 1: merge fan-in above 1536 streams took the record sort (one list) */
+    uint32_t reserved;
 } skv_timings;
 
 /* skv_timings.path */

@@ -122,9 +122,16 @@ struct TileOut {
 #define SKV_FX_THREADS 512
 #endif
 #ifndef SKV_FX_U
-#define SKV_FX_U 8                       // output blocks per lane in flight in the fused copy
+#define SKV_FX_U 2                       // output blocks per lane per batch in the fused copy (two batches in flight)
 #endif
-constexpr int FX_CAP = 4096;             // records per fused tile (same splitters as TILE_CAP)
+#ifndef SKV_FX_CAP
+#define SKV_FX_CAP 4096
+#endif
+#ifndef SKV_FX_NT
+#define SKV_FX_NT 1                      // 1: non-temporal output stores in the fused copy
+#endif
+constexpr int FX_CAP = SKV_FX_CAP;       // max records per fused tile
+constexpr int FX_TARGET = FX_CAP / 4 * 3;  // target records per fused tile (splitter spacing)
 constexpr int FX_THREADS = SKV_FX_THREADS;
 constexpr uint64_t FX_MIN_S = 32;        // a 16-byte output block touches at most two records
 constexpr uint64_t FX_MAX_S = 1u << 19;  // tile output spans stay below 2^31 bytes (u32 offsets)
@@ -160,6 +167,17 @@ struct FxArgs {
 };
 // flags[3] reason bits of a poisoned fused call
 enum : uint32_t { FXR_RECORD = 1, FXR_OVERSIZE = 2, FXR_SPLIT = 4, FXR_ORDER = 8, FXR_SAMPLE = 16 };
+
+// Record sort for merges of more than TILE_TARGET / 2 streams (skv_sort.hip)
+struct SElem {
+    uint64_t hi, lo;              // 16-byte key prefix (big-endian, zero padded)
+    uint64_t addr;                // record address (key at addr + 5)
+    uint32_t pos, klen;           // record index (rank order), key length
+};
+constexpr int SORT_CAP = 2048;           // elements a bucket sorts in LDS
+constexpr int SORT_THREADS = 256;
+constexpr uint64_t SORT_EVERY = 48;      // one sample per SORT_EVERY elements
+constexpr uint64_t SORT_OV = 16;         // samples per bucket (bucket target SORT_EVERY * SORT_OV = 768)
 
 // WAL key errors (wal_compaction.rs:71-79): no '.', or Rust's ParseIntError kinds
 enum : uint32_t { WERR_NONE = 0, WERR_NODOT, WERR_EMPTY, WERR_DIGIT, WERR_POS, WERR_NEG };

@@ -425,8 +425,7 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
     lv[0].N = R;
     lv[0].off = stream_base;
     lv[0].d_off = d_sbase;
-    const uint64_t S_step = std::max<uint64_t>(2, (uint64_t)TILE_TARGET / std::max<uint32_t>(k, 1));
-    uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "scan_tmp", scan_tmp_words(std::max<uint64_t>(R / S_step + 1, 1 << 20)) + 64);
+    const uint64_t S_step = std::max<uint64_t>(2, (uint64_t)FX_TARGET / std::max<uint32_t>(k, 1));
     while (lv.back().N > (uint64_t)FX_CAP) {
         const Level& P = lv.back();
         Level L;
@@ -455,7 +454,7 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
         Level& L = lv[li];
         uint64_t T = 1, m = 1;
         if (li + 1 < (int)lv.size()) {
-            m = std::max<uint64_t>(1, (uint64_t)TILE_TARGET / lv[li + 1].S);
+            m = std::max<uint64_t>(1, (uint64_t)(li == 0 ? FX_TARGET : TILE_TARGET) / lv[li + 1].S);
             T = std::max<uint64_t>(1, (lv[li + 1].N + m - 1) / m);
         }
         if (li == 0) {
@@ -469,25 +468,21 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
         const Level* U = li + 1 < (int)lv.size() ? &lv[li + 1] : nullptr;
         launch_bounds(st, false, L.hi, L.lo, L.c, nullptr, L.d_off, k, U ? U->shi : nullptr, U ? U->slo : nullptr,
                       U ? U->sc : nullptr, m, T, nullptr, bounds, d_flags + 2);
-        snprintf(nm, sizeof nm, "tile_n%d", li);
-        uint64_t* tile_n = dbuf<uint64_t>(ctx, nm, T);
-        snprintf(nm, sizeof nm, "tile_base%d", li);
-        uint64_t* tile_base = dbuf<uint64_t>(ctx, nm, T + 1);
-        launch_tile_n(st, bounds, k, T, tile_n);
-        launch_scan(st, tile_n, T, tile_base, scan_tmp);
-        TileOut O{};
+        TileOut O{};  // sample tiles find their output base from the bounds (no tile_base table)
         snprintf(nm, sizeof nm, "x%d_hi", li); O.xhi = dbuf<uint64_t>(ctx, nm, L.N);
         snprintf(nm, sizeof nm, "x%d_lo", li); O.xlo = dbuf<uint64_t>(ctx, nm, L.N);
         snprintf(nm, sizeof nm, "x%d_c", li); O.xc = dbuf<uint64_t>(ctx, nm, L.N);
         snprintf(nm, sizeof nm, "s%d_hi", li); L.shi = O.ohi = dbuf<uint64_t>(ctx, nm, L.N);
         snprintf(nm, sizeof nm, "s%d_lo", li); L.slo = O.olo = dbuf<uint64_t>(ctx, nm, L.N);
         snprintf(nm, sizeof nm, "s%d_c", li); L.sc = O.oc = dbuf<uint64_t>(ctx, nm, L.N);
-        HIPCHK(launch_tile(st, false, L.hi, L.lo, L.c, nullptr, bounds, k, T, tile_base, nullptr, nullptr, 0u, O,
+        HIPCHK(launch_tile(st, false, L.hi, L.lo, L.c, nullptr, bounds, k, T, nullptr, nullptr, nullptr, 0u, O,
                            d_flags + 2));
     }
     A.T = T0;
     A.bnd = dbuf<FxBound>(ctx, "fx_bnd", (T0 + 1) * k);
-    launch_fx_bounds(st, A, lv.size() > 1 ? lv[1].shi : nullptr, lv.size() > 1 ? lv[1].slo : nullptr, m0);
+    const bool l1 = lv.size() > 1;
+    launch_fx_bounds(st, A, l1 ? lv[1].shi : nullptr, l1 ? lv[1].slo : nullptr, m0, l1 ? lv[1].hi : nullptr,
+                     l1 ? lv[1].lo : nullptr, l1 ? lv[1].d_off : nullptr, S_step);
     A.tstate = dbuf<uint64_t>(ctx, "fx_tstate", T0);
     A.tcounter = dbuf<uint32_t>(ctx, "tile_ticket", 1);
     HIPCHK(hipMemsetAsync(A.tstate, 0, T0 * 8, st));
@@ -561,6 +556,70 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
     t.host_syncs = ctx->syncs;
     *out = res;
     return true;
+}
+
+// Sorts n SElems by (key, record index) (skv_sort.hip); E and T are n-element buffers, the
+// result is in the returned one of the two. Samples recurse with their own buffers (depth).
+static SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth) {
+    hipStream_t st = ctx->stream;
+    char nm[64];
+    if (n <= (uint64_t)SORT_CAP) {  // one bucket
+        snprintf(nm, sizeof nm, "sort_one%d", depth);
+        uint64_t* start = dbuf<uint64_t>(ctx, nm, 2);
+        const uint64_t h[2] = {0, n};
+        h2d_up(ctx, start, h, 16);
+        launch_sort_tile(st, E, start, nullptr, 1, T);
+        return T;
+    }
+    const uint64_t Ns = (n + SORT_EVERY - 1) / SORT_EVERY;
+    snprintf(nm, sizeof nm, "sort_s%d", depth);
+    SElem* S = dbuf<SElem>(ctx, nm, Ns);
+    snprintf(nm, sizeof nm, "sort_sT%d", depth);
+    SElem* S2 = dbuf<SElem>(ctx, nm, Ns);
+    launch_sort_sample(st, E, n, Ns, S);
+    const SElem* Ss = sort_elems(ctx, S, S2, Ns, depth + 1);
+    const uint64_t Tb = (Ns + SORT_OV - 1) / SORT_OV;  // buckets; Tb - 1 splitters
+    snprintf(nm, sizeof nm, "sort_L%d", depth);
+    uint32_t* L = dbuf<uint32_t>(ctx, nm, Tb);
+    snprintf(nm, sizeof nm, "sort_cnt%d", depth);
+    uint64_t* cnt = dbuf<uint64_t>(ctx, nm, Tb + 1);
+    snprintf(nm, sizeof nm, "sort_bs%d", depth);
+    uint64_t* bs = dbuf<uint64_t>(ctx, nm, n);
+    snprintf(nm, sizeof nm, "sort_start%d", depth);
+    uint64_t* start = dbuf<uint64_t>(ctx, nm, Tb + 1);
+    snprintf(nm, sizeof nm, "sort_scan%d", depth);
+    uint64_t* scan_tmp = dbuf<uint64_t>(ctx, nm, scan_tmp_words(Tb) + 64);
+    launch_sort_prefix(st, Ss, SORT_OV, Tb, L);
+    HIPCHK(hipMemsetAsync(cnt, 0, (Tb + 1) * 8, st));
+    launch_sort_bucket(st, E, n, Ss, SORT_OV, Tb - 1, cnt, bs);
+    launch_scan(st, cnt, Tb, start, scan_tmp);
+    launch_sort_scatter(st, E, n, bs, start, T);
+    launch_sort_tile(st, T, start, L, Tb, E);
+    return E;
+}
+
+// The merged order of R records as one sorted list: the record arrays are replaced by sorted
+// copies (merges of more than TILE_TARGET / 2 streams, whose splitter bounds table would be
+// tiles x streams).
+static void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo, uint64_t*& addr, uint32_t*& klen,
+                         uint32_t*& meta) {
+    hipStream_t st = ctx->stream;
+    SElem* E = dbuf<SElem>(ctx, "sort_e", R);
+    SElem* T = dbuf<SElem>(ctx, "sort_t", R);
+    launch_sort_load(st, R, hi, lo, addr, klen, E);
+    const SElem* S = sort_elems(ctx, E, T, R, 0);
+    uint64_t* nhi = dbuf<uint64_t>(ctx, "srt_hi", R);
+    uint64_t* nlo = dbuf<uint64_t>(ctx, "srt_lo", R);
+    uint64_t* naddr = dbuf<uint64_t>(ctx, "srt_addr", R);
+    uint32_t* nklen = dbuf<uint32_t>(ctx, "srt_klen", R);
+    uint32_t* nmeta = dbuf<uint32_t>(ctx, "srt_meta", R);
+    launch_sort_store(st, R, S, meta, nhi, nlo, naddr, nklen, nmeta);
+    HIPCHK(hipGetLastError());
+    hi = nhi;
+    lo = nlo;
+    addr = naddr;
+    klen = nklen;
+    meta = nmeta;
 }
 
 // allow_deferred: on the fixed-stride fast path, launch the merge without waiting for the parse's
@@ -843,36 +902,50 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         uint64_t* slo = nullptr;
         uint64_t* sc = nullptr;
     };
+    // Past TILE_TARGET / 2 streams the records are sorted into one list first (skv_sort.hip);
+    // SKV_SORT=1 forces that path (tests).
+    uint32_t km = k;  // lists the splitter merge sees
+    std::vector<uint64_t> list_off = stream_base;
+    uint64_t* d_list_off = d_stream_base;
+    {
+        const char* se = getenv("SKV_SORT");
+        if ((k > (uint32_t)TILE_TARGET / 2 && R > (uint64_t)TILE_CAP) || (se && se[0] == '1')) {
+            sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta);
+            km = 1;
+            list_off = {0, R};
+            d_list_off = dbuf<uint64_t>(ctx, "sorted_off", 2);
+            h2d_up(ctx, d_list_off, list_off.data(), 16);
+            ctx->timings.sorted = 1;
+        }
+    }
     std::vector<Level> lv(1);
     lv[0].N = R;
-    lv[0].off = stream_base;
+    lv[0].off = list_off;
     lv[0].hi = rec_hi;
     lv[0].lo = rec_lo;
-    lv[0].d_off = d_stream_base;
-    const uint64_t S_step = std::max<uint64_t>(2, (uint64_t)TILE_TARGET / std::max<uint32_t>(k, 1));
-    if (k > (uint32_t)TILE_TARGET / 2 && R > (uint64_t)TILE_CAP)
-        throw ApiError{SKV_E_UNSUPPORTED, "merge fan-in above 1024 streams is not supported by this build yet"};
+    lv[0].d_off = d_list_off;
+    const uint64_t S_step = std::max<uint64_t>(2, (uint64_t)TILE_TARGET / std::max<uint32_t>(km, 1));
     while (lv.back().N > (uint64_t)TILE_CAP) {
         const Level& P = lv.back();
         Level L;
         L.S = S_step;
-        L.off.resize(k + 1);
+        L.off.resize(km + 1);
         uint64_t acc = 0;
-        for (uint32_t j = 0; j < k; ++j) {
+        for (uint32_t j = 0; j < km; ++j) {
             L.off[j] = acc;
             uint64_t nj = P.off[j + 1] - P.off[j];
             acc += (nj + L.S - 1) / L.S;
         }
-        L.off[k] = acc;
+        L.off[km] = acc;
         L.N = acc;
         char nm[64];
         int li = (int)lv.size();
         snprintf(nm, sizeof nm, "lv%d_hi", li); L.hi = dbuf<uint64_t>(ctx, nm, L.N);
         snprintf(nm, sizeof nm, "lv%d_lo", li); L.lo = dbuf<uint64_t>(ctx, nm, L.N);
         snprintf(nm, sizeof nm, "lv%d_c", li); L.c = dbuf<uint64_t>(ctx, nm, L.N);
-        snprintf(nm, sizeof nm, "lv%d_off", li); L.d_off = dbuf<uint64_t>(ctx, nm, k + 1);
-        h2d_up(ctx, L.d_off, L.off.data(), (k + 1) * 8);
-        launch_sample(st, li == 1, P.hi, P.lo, P.c, rec_klen, P.d_off, L.d_off, k, L.S, L.N, L.hi, L.lo, L.c);
+        snprintf(nm, sizeof nm, "lv%d_off", li); L.d_off = dbuf<uint64_t>(ctx, nm, km + 1);
+        h2d_up(ctx, L.d_off, L.off.data(), (km + 1) * 8);
+        launch_sample(st, li == 1, P.hi, P.lo, P.c, rec_klen, P.d_off, L.d_off, km, L.S, L.N, L.hi, L.lo, L.c);
         lv.push_back(L);
     }
     // top-down: sort each sample level, derive splitters for the level below
@@ -893,15 +966,15 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         }
         char nm[64];
         snprintf(nm, sizeof nm, "bounds%d", li);
-        uint64_t* bounds = dbuf<uint64_t>(ctx, nm, (T + 1) * k);
+        uint64_t* bounds = dbuf<uint64_t>(ctx, nm, (T + 1) * km);
         const Level* U = li + 1 < (int)lv.size() ? &lv[li + 1] : nullptr;
-        launch_bounds(st, l0, L.hi, L.lo, L.c, rec_klen, L.d_off, k, U ? U->shi : nullptr, U ? U->slo : nullptr,
+        launch_bounds(st, l0, L.hi, L.lo, L.c, rec_klen, L.d_off, km, U ? U->shi : nullptr, U ? U->slo : nullptr,
                       U ? U->sc : nullptr, m, T, rec_addr, bounds, d_flags + 2);
         snprintf(nm, sizeof nm, "tile_n%d", li);
         uint64_t* tile_n = dbuf<uint64_t>(ctx, nm, T);
         snprintf(nm, sizeof nm, "tile_base%d", li);
         uint64_t* tile_base = dbuf<uint64_t>(ctx, nm, T + 1);
-        launch_tile_n(st, bounds, k, T, tile_n);
+        launch_tile_n(st, bounds, km, T, tile_n);
         launch_scan(st, tile_n, T, tile_base, scan_tmp);
         TileOut O{};
         snprintf(nm, sizeof nm, "x%d_hi", li); O.xhi = dbuf<uint64_t>(ctx, nm, L.N);
@@ -932,7 +1005,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             snprintf(nm, sizeof nm, "s%d_lo", li); L.slo = O.olo = dbuf<uint64_t>(ctx, nm, L.N);
             snprintf(nm, sizeof nm, "s%d_c", li); L.sc = O.oc = dbuf<uint64_t>(ctx, nm, L.N);
         }
-        HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, rec_klen, bounds, k, T, tile_base, rec_meta, rec_addr,
+        HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, rec_klen, bounds, km, T, tile_base, rec_meta, rec_addr,
                            (job.flags & SKV_DROP_TOMBSTONES) ? 1u : 0u, O, d_flags + 2));
         if (l0) T0 = T;
     }

@@ -811,10 +811,9 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         __syncthreads();
         t = s_tk;
     }
-    const uint64_t base = tile_base[t];
-    const uint64_t n64 = tile_base[t + 1] - base;
-    // segment starts
-    uint64_t segtot = 0;
+    // segment starts (and, without a tile_base table, the tile's output base: the elements of all
+    // lists before bounds[t], as bounds[0] holds the list starts)
+    uint64_t segtot = 0, before = 0;
     for (uint32_t j0 = 0; j0 < k; j0 += blockDim.x) {
         uint32_t j = j0 + threadIdx.x;
         uint64_t len = j < k ? bounds[(t + 1) * k + j] - bounds[t * k + j] : 0;
@@ -822,7 +821,10 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         uint64_t ex = block_excl_scan<uint64_t>(len, ws, tot);
         if (j < k) cbA[j] = (uint32_t)(segtot + ex);
         segtot += tot;
+        if (!tile_base) before += block_reduce_sum<uint64_t>(j < k ? bounds[t * k + j] - bounds[j] : 0, ws);
     }
+    const uint64_t base = tile_base ? tile_base[t] : before;
+    const uint64_t n64 = tile_base ? tile_base[t + 1] - base : segtot;
     if (threadIdx.x == 0) cbA[k] = (uint32_t)segtot;
     __syncthreads();
     TPROF(0);

@@ -76,10 +76,23 @@ void launch_gather_pages(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs
 // skv_stride.hip — fused stride path
 void launch_fx_sample(hipStream_t, const FxArgs& A, const uint64_t* off_dst, uint64_t Sstep, uint64_t n_dst,
                       uint64_t* dhi, uint64_t* dlo, uint64_t* dc);
-void launch_fx_bounds(hipStream_t, const FxArgs& A, const uint64_t* shi, const uint64_t* slo, uint64_t m);
+void launch_fx_bounds(hipStream_t, const FxArgs& A, const uint64_t* shi, const uint64_t* slo, uint64_t m,
+                      const uint64_t* l1hi, const uint64_t* l1lo, const uint64_t* l1off, uint64_t Sstep);
 size_t fx_tile_lds_bytes(uint32_t k);
 hipError_t launch_fx_tile(hipStream_t, const FxArgs& A);
 void launch_fx_desc(hipStream_t, const FxArgs& A, DevRunDesc* descs, uint64_t* n_runs_out, uint64_t max_runs);
+// skv_sort.hip — record sort (fan-in above TILE_TARGET / 2)
+void launch_sort_load(hipStream_t, uint64_t R, const uint64_t* hi, const uint64_t* lo, const uint64_t* addr,
+                      const uint32_t* klen, SElem* E);
+void launch_sort_store(hipStream_t, uint64_t R, const SElem* E, const uint32_t* meta_in, uint64_t* hi, uint64_t* lo,
+                       uint64_t* addr, uint32_t* klen, uint32_t* meta);
+void launch_sort_sample(hipStream_t, const SElem* E, uint64_t n, uint64_t Ns, SElem* S);
+void launch_sort_prefix(hipStream_t, const SElem* Ss, uint64_t ov, uint64_t Tb, uint32_t* L);
+void launch_sort_bucket(hipStream_t, const SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
+                        uint64_t* cnt, uint64_t* bs);
+void launch_sort_scatter(hipStream_t, const SElem* E, uint64_t n, const uint64_t* bs, const uint64_t* start,
+                         SElem* out);
+void launch_sort_tile(hipStream_t, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out);
 uint64_t scan_tmp_words(uint64_t n);
 void launch_scan(hipStream_t, const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tmp);
 }  // namespace skv

@@ -1,0 +1,294 @@
+// skv_sort.hip — the record sort behind merges of more than TILE_TARGET / 2 streams (gfx950).
+//
+// k_way::merge pops records in (key ascending, seq_no descending) order (k_way.rs:14-33), and a
+// stream's own records come out in stream order (its order is checked first, runs.rs:190-198).
+// Records are numbered stream by stream in rank (seq_no descending) order, so the merged order is
+// the order of (key bytes, record index): a sort. For up to TILE_TARGET / 2 streams the splitter
+// merge of skv_kernels.hip produces it from the sorted streams; past that its (tiles x streams)
+// bounds table outgrows memory (config 5: 10^6 WAL runs of 83 records), and this sample sort
+// takes over:
+//   1. one SElem {prefix, address, index, key length} per record (coalesced)
+//   2. samples: every SORT_EVERY-th element, sorted by this same routine (recursion down to one
+//      workgroup)
+//   3. splitters: every SORT_OV-th sorted sample; bucket b holds the keys in (sp[b-1], sp[b]]
+//      (key-only order, so equal keys share a bucket), L[b] = common prefix length of its two
+//      splitters, which every key of the bucket shares
+//   4. bucket of each element (binary search over the splitters), slot by atomic count, exclusive
+//      scan, scatter
+//   5. one workgroup per bucket: bitonic sort in LDS on the 16 key bytes after the bucket's common
+//      prefix, then the key length and record index (the rest of a longer key from memory on a
+//      tie); buckets above SORT_CAP sort in global memory (same order, slower)
+// The sorted records then form ONE stream, and the level-0 merge machinery runs on them with
+// k = 1: first record per key, Delete filter, dense output arrays (skv_host.hip).
+#include "skv_launch.hpp"
+
+namespace skv {
+
+// bytewise order of the first n bytes at a and b (<0, 0, >0), 16 bytes per step
+__device__ inline int sk_bytes_cmp(const uint8_t* a, const uint8_t* b, uint64_t n) {
+    for (uint64_t i = 0; i < n; i += 16) {
+        const uint32_t m = (uint32_t)(n - i < 16 ? n - i : 16);
+        const uint4 x = load_window16(a + i, m), y = load_window16(b + i, m);
+        const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t mk = dword_mask(0, m, q);
+            const uint32_t xa = __builtin_bswap32(xs[q] & mk), ya = __builtin_bswap32(ys[q] & mk);
+            if (xa != ya) return xa < ya ? -1 : 1;
+        }
+    }
+    return 0;
+}
+
+// index of the first differing byte among the first n bytes (n if none)
+__device__ inline uint64_t sk_bytes_diff(const uint8_t* a, const uint8_t* b, uint64_t n) {
+    for (uint64_t i = 0; i < n; i += 16) {
+        const uint32_t m = (uint32_t)(n - i < 16 ? n - i : 16);
+        const uint4 x = load_window16(a + i, m), y = load_window16(b + i, m);
+        const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t d = (xs[q] ^ ys[q]) & dword_mask(0, m, q);
+            if (d) return i + 4 * q + (__builtin_ctz(d) >> 3);
+        }
+    }
+    return n;
+}
+
+__device__ __forceinline__ const uint8_t* sk_key(const SElem& e) { return (const uint8_t*)e.addr + 5; }
+
+// key-only order: Rust str Ord (bytewise, a proper prefix first), as HeapItem compares keys
+__device__ inline int sk_kcmp(const SElem& a, const SElem& b) {
+    if (a.hi != b.hi) return a.hi < b.hi ? -1 : 1;
+    if (a.lo != b.lo) return a.lo < b.lo ? -1 : 1;
+    if (a.klen > 16 && b.klen > 16) {
+        const uint32_t n = a.klen < b.klen ? a.klen : b.klen;
+        const int s = sk_bytes_cmp(sk_key(a) + 16, sk_key(b) + 16, n - 16);
+        if (s) return s;
+    }
+    return a.klen < b.klen ? -1 : (a.klen > b.klen ? 1 : 0);
+}
+
+// the merged order: key, then record index (== seq_no descending, then stream order)
+__device__ __forceinline__ bool sk_less(const SElem& a, const SElem& b) {
+    const int c = sk_kcmp(a, b);
+    return c ? c < 0 : a.pos < b.pos;
+}
+
+// common prefix length of two keys
+__device__ inline uint32_t sk_common(const SElem& a, const SElem& b) {
+    const uint32_t n = a.klen < b.klen ? a.klen : b.klen;
+    uint64_t c;
+    if (a.hi != b.hi) c = __builtin_clzll(a.hi ^ b.hi) >> 3;
+    else if (a.lo != b.lo) c = 8 + (__builtin_clzll(a.lo ^ b.lo) >> 3);
+    else if (n > 16) c = 16 + sk_bytes_diff(sk_key(a) + 16, sk_key(b) + 16, n - 16);
+    else c = 16;
+    return (uint32_t)(c < n ? c : n);
+}
+
+// the 16 key bytes from byte L on (big-endian, zero past the key's end)
+__device__ inline void sk_window(const SElem& e, uint32_t L, uint64_t& wh, uint64_t& wl) {
+    if (L == 0) {
+        wh = e.hi;
+        wl = e.lo;
+        return;
+    }
+    wh = wl = 0;
+    if (e.klen <= L) return;
+    const uint32_t m = e.klen - L < 16 ? e.klen - L : 16;
+    const uint4 v = load_window16(sk_key(e) + L, m);
+    const uint32_t d0 = v.x & dword_mask(0, m, 0), d1 = v.y & dword_mask(0, m, 1);
+    const uint32_t d2 = v.z & dword_mask(0, m, 2), d3 = v.w & dword_mask(0, m, 3);
+    wh = ((uint64_t)__builtin_bswap32(d0) << 32) | __builtin_bswap32(d1);
+    wl = ((uint64_t)__builtin_bswap32(d2) << 32) | __builtin_bswap32(d3);
+}
+
+// ---------------------------------------------------------------------------------------------
+
+__global__ void k_sort_load(uint64_t R, const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo,
+                            const uint64_t* __restrict__ addr, const uint32_t* __restrict__ klen, SElem* E) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R) return;
+    SElem e;
+    e.hi = hi[i];
+    e.lo = lo[i];
+    e.addr = addr[i];
+    e.pos = (uint32_t)i;
+    e.klen = klen[i];
+    E[i] = e;
+}
+
+// the record arrays in sorted order (meta follows its record)
+__global__ void k_sort_store(uint64_t R, const SElem* __restrict__ E, const uint32_t* __restrict__ meta_in,
+                             uint64_t* hi, uint64_t* lo, uint64_t* addr, uint32_t* klen, uint32_t* meta) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R) return;
+    const SElem e = E[i];
+    hi[i] = e.hi;
+    lo[i] = e.lo;
+    addr[i] = e.addr;
+    klen[i] = e.klen;
+    meta[i] = meta_in[e.pos];
+}
+
+// S[j] = E[j * n / Ns]  (n < 2^32)
+__global__ void k_sort_sample(const SElem* __restrict__ E, uint64_t n, uint64_t Ns, SElem* S) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= Ns) return;
+    S[j] = E[j * n / Ns];
+}
+
+// L[b] of the Tb buckets; splitter b (b < Tb - 1) is sorted sample (b + 1) * ov - 1
+__global__ void k_sort_prefix(const SElem* __restrict__ Ss, uint64_t ov, uint64_t Tb, uint32_t* L) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= Tb) return;
+    L[b] = (b == 0 || b + 1 == Tb) ? 0u : sk_common(Ss[b * ov - 1], Ss[(b + 1) * ov - 1]);
+}
+
+// bucket of each element = the splitters whose key orders strictly before its key; slot by an
+// atomic count (the bucket sort restores a deterministic order)
+__global__ void k_sort_bucket(const SElem* __restrict__ E, uint64_t n, const SElem* __restrict__ Ss, uint64_t ov,
+                              uint64_t nsp, unsigned long long* cnt, uint64_t* bs) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const SElem x = E[i];
+    uint64_t a = 0, b = nsp;
+    while (a < b) {
+        const uint64_t mid = (a + b) >> 1;
+        if (sk_kcmp(Ss[(mid + 1) * ov - 1], x) < 0) a = mid + 1;
+        else b = mid;
+    }
+    const uint64_t slot = atomicAdd(cnt + a, 1ull);
+    bs[i] = (a << 32) | slot;
+}
+
+__global__ void k_sort_scatter(const SElem* __restrict__ E, uint64_t n, const uint64_t* __restrict__ bs,
+                               const uint64_t* __restrict__ start, SElem* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t v = bs[i];
+    out[start[v >> 32] + (v & 0xFFFFFFFFull)] = E[i];
+}
+
+// Bucket order: window (wh, wl), then the key bytes past the window when both keys run past it,
+// then key length, then record index. Every key of the bucket shares its first L bytes.
+struct SKey {
+    uint64_t wh, wl;
+    uint32_t klen, pos;
+};
+__device__ __forceinline__ bool sk_wless(const SKey& a, const SKey& b, const SElem* bk, uint32_t ia, uint32_t ib,
+                                         uint32_t L) {
+    if (a.wh != b.wh) return a.wh < b.wh;
+    if (a.wl != b.wl) return a.wl < b.wl;
+    if (a.klen > L + 16 && b.klen > L + 16) {
+        const uint32_t nmin = a.klen < b.klen ? a.klen : b.klen;
+        const int s = sk_bytes_cmp(sk_key(bk[ia]) + L + 16, sk_key(bk[ib]) + L + 16, nmin - L - 16);
+        if (s) return s < 0;
+    }
+    if (a.klen != b.klen) return a.klen < b.klen;
+    return a.pos < b.pos;
+}
+
+// One workgroup per bucket: in[start[b], start[b+1]) sorted into out[...]. Bitonic network in
+// the ascending-comparator form (the second element of the first step of each merge is mirrored),
+// so padding past n acts as +inf and is never touched.
+__global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uint64_t* __restrict__ start,
+                                                            const uint32_t* __restrict__ Lb, uint64_t Tb,
+                                                            SElem* out) {
+    __shared__ SKey key[SORT_CAP];
+    __shared__ uint16_t id[SORT_CAP];
+    const uint64_t b = blockIdx.x;
+    if (b >= Tb) return;
+    const uint64_t s0 = start[b], n = start[b + 1] - s0;
+    const uint32_t L = Lb ? Lb[b] : 0u;
+    SElem* bk = in + s0;
+    if (n == 0) return;
+    if (n > (uint64_t)SORT_CAP) {  // global-memory bitonic sort on the full order, then copy
+        uint64_t P = 1;
+        while (P < n) P <<= 1;
+        for (uint64_t kk = 2; kk <= P; kk <<= 1) {
+            for (uint64_t jj = kk >> 1; jj >= 1; jj >>= 1) {
+                for (uint64_t i = threadIdx.x; i < P / 2; i += blockDim.x) {
+                    const uint64_t blk = i / jj, off = i % jj;
+                    const bool first = jj == (kk >> 1);
+                    const uint64_t a = first ? blk * kk + off : blk * 2 * jj + off;
+                    const uint64_t c = first ? blk * kk + kk - 1 - off : a + jj;
+                    if (c < n && sk_less(bk[c], bk[a])) {
+                        const SElem t = bk[a];
+                        bk[a] = bk[c];
+                        bk[c] = t;
+                    }
+                }
+                __threadfence_block();
+                __syncthreads();
+            }
+        }
+        for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) out[s0 + i] = bk[i];
+        return;
+    }
+    const uint32_t n32 = (uint32_t)n;
+    for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
+        const SElem e = bk[i];
+        SKey k;
+        sk_window(e, L, k.wh, k.wl);
+        k.klen = e.klen;
+        k.pos = e.pos;
+        key[i] = k;
+        id[i] = (uint16_t)i;
+    }
+    __syncthreads();
+    uint32_t P = 1;
+    while (P < n32) P <<= 1;
+    for (uint32_t kk = 2; kk <= P; kk <<= 1) {
+        for (uint32_t jj = kk >> 1; jj >= 1; jj >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P / 2; i += blockDim.x) {
+                const uint32_t blk = i / jj, off = i % jj;
+                const bool first = jj == (kk >> 1);
+                const uint32_t a = first ? blk * kk + off : blk * 2 * jj + off;
+                const uint32_t c = first ? blk * kk + kk - 1 - off : a + jj;
+                if (c < n32) {
+                    const SKey ka = key[a], kc = key[c];
+                    const uint32_t ia = id[a], ic = id[c];
+                    if (sk_wless(kc, ka, bk, ic, ia, L)) {
+                        key[a] = kc;
+                        key[c] = ka;
+                        id[a] = (uint16_t)ic;
+                        id[c] = (uint16_t)ia;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) out[s0 + i] = bk[id[i]];
+}
+
+static inline unsigned sk_blocks(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+void launch_sort_load(hipStream_t s, uint64_t R, const uint64_t* hi, const uint64_t* lo, const uint64_t* addr,
+                      const uint32_t* klen, SElem* E) {
+    if (R) k_sort_load<<<sk_blocks(R), 256, 0, s>>>(R, hi, lo, addr, klen, E);
+}
+void launch_sort_store(hipStream_t s, uint64_t R, const SElem* E, const uint32_t* meta_in, uint64_t* hi, uint64_t* lo,
+                       uint64_t* addr, uint32_t* klen, uint32_t* meta) {
+    if (R) k_sort_store<<<sk_blocks(R), 256, 0, s>>>(R, E, meta_in, hi, lo, addr, klen, meta);
+}
+void launch_sort_sample(hipStream_t s, const SElem* E, uint64_t n, uint64_t Ns, SElem* S) {
+    if (Ns) k_sort_sample<<<sk_blocks(Ns), 256, 0, s>>>(E, n, Ns, S);
+}
+void launch_sort_prefix(hipStream_t s, const SElem* Ss, uint64_t ov, uint64_t Tb, uint32_t* L) {
+    if (Tb) k_sort_prefix<<<sk_blocks(Tb), 256, 0, s>>>(Ss, ov, Tb, L);
+}
+void launch_sort_bucket(hipStream_t s, const SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
+                        uint64_t* cnt, uint64_t* bs) {
+    if (n) k_sort_bucket<<<sk_blocks(n), 256, 0, s>>>(E, n, Ss, ov, nsp, (unsigned long long*)cnt, bs);
+}
+void launch_sort_scatter(hipStream_t s, const SElem* E, uint64_t n, const uint64_t* bs, const uint64_t* start,
+                         SElem* out) {
+    if (n) k_sort_scatter<<<sk_blocks(n), 256, 0, s>>>(E, n, bs, start, out);
+}
+void launch_sort_tile(hipStream_t s, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out) {
+    if (Tb) k_sort_tile<<<(unsigned)Tb, SORT_THREADS, 0, s>>>(in, start, L, Tb, out);
+}
+
+}  // namespace skv

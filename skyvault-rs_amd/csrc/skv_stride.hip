@@ -22,13 +22,22 @@
 // reruns the call on the general path, which reproduces the reference's exact outcome.
 #include "skv_launch.hpp"
 
+#ifndef SKV_FX_DIAG
+#define SKV_FX_DIAG 0  // diagnostic builds only (output invalid): 1 skip the copy, 2 skip the merge
+                       // rounds, 3 copy only (no key loads, no merge: records in load order)
+#endif
+
 namespace skv {
 
 typedef unsigned int fx_u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void fx_store16(uint8_t* p, uint4 v) {
     fx_u32x4 vv = {v.x, v.y, v.z, v.w};
+#if SKV_FX_NT
     __builtin_nontemporal_store(vv, (fx_u32x4*)p);  // written once, never re-read here
+#else
+    *(fx_u32x4*)p = vv;
+#endif
 }
 
 // q = z / d, r = z % d from a double reciprocal and one correction step (z < 2^52)
@@ -195,36 +204,94 @@ __device__ __forceinline__ uint32_t fx_run(const FxArgs& A, uint32_t j, uint64_t
     return lo;
 }
 
+// first index in [lo, hi) whose element is not below the splitter (or hi), one thread: each round
+// issues 8 independent probes and keeps the gap where the predicate flips (9-ary search), so a
+// search of n elements costs ~log9(n) dependent round trips instead of log2(n)
+template <typename Below>
+__device__ __forceinline__ uint64_t fx_lower_bound8(uint64_t lo, uint64_t hi, Below below) {
+    while (lo < hi) {
+        const uint64_t n = hi - lo;
+        uint64_t idx[8];
+        bool p[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) idx[i] = n >= 9 ? lo + ((uint64_t)(i + 1) * n) / 9 : lo + (uint64_t)i;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) p[i] = idx[i] < hi && below(idx[i]);
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c += p[i] ? 1u : 0u;
+        if (n < 9) return lo + c;
+        if (c == 0) {
+            hi = idx[0];
+        } else {
+            uint64_t l2 = idx[0], h2 = hi;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (i + 1 == (int)c) l2 = idx[i] + 1;
+                if (i == (int)c) h2 = idx[i];
+            }
+            lo = l2;
+            hi = h2;
+        }
+    }
+    return lo;
+}
+
 // bnd[t*k + j].pos = first record of stream j whose key >= splitter t (sorted level-1 samples,
 // every m-th one), plus what tile t needs to start its segment without further searches: the
 // record's address, the records left in its member run, and the key of the record before it
-// (the in-stream order check across tile edges, runs.rs:190-198)
-__global__ void k_fx_bounds(FxArgs A, const uint64_t* __restrict__ shi, const uint64_t* __restrict__ slo, uint64_t m) {
+// (the in-stream order check across tile edges, runs.rs:190-198). One thread per (t, j): a 9-ary
+// search over stream j's own level-1 samples (every Sstep-th record, L2-resident) narrows the
+// bound to one sample gap, then a 9-ary search over the records of that gap.
+__global__ void k_fx_bounds(FxArgs A, const uint64_t* __restrict__ shi, const uint64_t* __restrict__ slo, uint64_t m,
+                            const uint64_t* __restrict__ l1hi, const uint64_t* __restrict__ l1lo,
+                            const uint64_t* __restrict__ l1off, uint64_t Sstep) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t k = A.k;
     if (g >= (A.T + 1) * k) return;
     const uint64_t t = g / k;
     const uint32_t j = (uint32_t)(g - t * k);
     const uint64_t s0 = A.stream_base[j], s1 = A.stream_base[j + 1];
-    uint64_t a = s0, b = s1;
-    FxBound o{};
+    uint64_t a = s0;
     if (t == A.T) {
         a = s1;
-    } else if (t > 0) {
+    } else if (t > 0 && s1 > s0) {
         if (__hip_atomic_load(A.flags + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            FxBound o{};
             o.pos = s0;
             A.bnd[g] = o;
             return;
         }
         const uint64_t h = shi[t * m], l = slo[t * m];
-        while (a < b) {
-            const uint64_t mid = (a + b) >> 1;
-            uint64_t eh, el;
-            fx_key(A, fx_addr(A, j, mid), eh, el);
-            if (eh < h || (eh == h && el < l)) a = mid + 1;
-            else b = mid;
+        const uint64_t q0 = l1off[j], q1 = l1off[j + 1];
+        const uint64_t c = fx_lower_bound8(q0, q1, [&](uint64_t i) {
+                               const uint64_t eh = l1hi[i], el = l1lo[i];
+                               return eh < h || (eh == h && el < l);
+                           }) - q0;
+        if (c > 0) {
+            const uint64_t lo = s0 + (c - 1) * Sstep + 1;
+            const uint64_t hi = s0 + c * Sstep < s1 ? s0 + c * Sstep : s1;
+            const uint32_t r0 = A.stream_run[j];
+            const bool one_run = A.stream_run[j + 1] - r0 == 1;
+            const uint64_t base = A.runs[r0].ptr + 1 - A.run_recb[r0] * A.S;  // record pos -> address (one run)
+            // inside the gap (< Sstep records, each probe a random HBM line): plain binary search,
+            // one line per round, log2(Sstep) rounds
+            uint64_t b2 = hi;
+            a = lo;
+            while (a < b2) {
+                const uint64_t i = (a + b2) >> 1;
+                const uint64_t ad = one_run ? base + i * A.S : fx_addr(A, j, i);
+                const uint4 kk = fx_ld16(ad + 5);
+                const uint64_t eh = ((uint64_t)__builtin_bswap32(kk.x & dword_mask(0, A.K, 0)) << 32) |
+                                    __builtin_bswap32(kk.y & dword_mask(0, A.K, 1));
+                const uint64_t el = ((uint64_t)__builtin_bswap32(kk.z & dword_mask(0, A.K, 2)) << 32) |
+                                    __builtin_bswap32(kk.w & dword_mask(0, A.K, 3));
+                if (eh < h || (eh == h && el < l)) a = i + 1;
+                else b2 = i;
+            }
         }
     }
+    FxBound o{};
     o.pos = a;
     if (a < s1) {
         const uint32_t r = fx_run(A, j, a);
@@ -348,6 +415,88 @@ __device__ __forceinline__ uint32_t fx_div32(uint32_t x, uint32_t d, double inv,
     return q;
 }
 
+// The copy walk of one lane over its output blocks B, B + 16 FX_THREADS, ... of a tile with at
+// most one run boundary: (record j, byte o) of the block's first byte, kept incrementally.
+struct FxWalk {
+    uint64_t B, V0, Vb;
+    uint32_t j, o, jb1, S32, dq, dr;
+    bool past;
+};
+template <int U>
+struct FxBatch {
+    uint64_t aL[U], aX[U];
+    uint32_t mode[U], sh[U];  // 0 one record, 1 record tail + next, 2 version byte + record,
+                              // 3 record tail + version byte + next
+    uint4 L[U], X[U];
+    uint32_t b;
+};
+// addresses of the batch's U blocks (b, b + FX_THREADS, ...) and their loads, issued together.
+// Branch-free where memory is touched: every block issues both loads (a block that does not
+// straddle a record end re-reads its own address, an L1 hit) and blocks past nb load `safe`, so
+// the waitcnt pass sees the same count on every path and can leave later batches in flight.
+template <int U>
+__device__ __forceinline__ void fx_plan(FxBatch<U>& t, FxWalk& w, const uint64_t* src, uint32_t b, uint32_t nb,
+                                        uint64_t safe) {
+    t.b = b;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const bool valid = b + u * FX_THREADS < nb;
+        const bool vb = w.B == w.V0 || w.B == w.Vb;
+        const bool st = !vb && w.o + 16 > w.S32;
+        uint32_t ja = vb ? (w.B == w.V0 ? 0u : w.jb1) : w.j;
+        ja = ja < (uint32_t)(FX_CAP - 1) ? ja : (uint32_t)(FX_CAP - 1);
+        const uint64_t s0 = src[ja], s1 = src[ja + 1];
+        uint64_t aL = vb ? s0 : s0 + (st ? w.S32 - 16 : w.o);
+        uint64_t aX = st ? s1 : aL;
+        t.aL[u] = valid ? aL : 0;
+        t.aX[u] = valid ? aX : safe;
+        if (!valid) aL = aX = safe;
+        t.mode[u] = vb ? 2u : (st ? (w.j + 1 == w.jb1 ? 3u : 1u) : 0u);
+        t.sh[u] = 16 - (w.S32 - w.o);
+        w.B += 16u * FX_THREADS;  // this lane's next block
+        w.o += w.dr;
+        w.j += w.dq;
+        const bool wrap = w.o >= w.S32;
+        w.o = wrap ? w.o - w.S32 : w.o;
+        w.j = wrap ? w.j + 1 : w.j;
+        if (!w.past && w.B > w.Vb) {  // crossed the run boundary: one version byte earlier
+            w.past = true;
+            const bool z = w.o == 0;
+            w.o = z ? w.S32 - 1 : w.o - 1;
+            w.j = z ? w.j - 1 : w.j;
+        }
+        t.L[u] = fx_ld16(aL);
+        t.X[u] = fx_ld16(aX);
+    }
+}
+__device__ __forceinline__ uint4 fx_sel4(bool c, uint4 a, uint4 b) {  // c ? a : b, per dword
+    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+// funnel16 without the sh == 0 early exit (alignbyte by 0 is the identity): straight-line code
+__device__ __forceinline__ uint4 fx_funnel16(uint4 x, uint4 y, uint32_t sh) {
+    const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+    const uint32_t q = sh >> 2, r = sh & 3;
+    uint32_t t[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t v3 = (i + 3 < 8) ? w[i + 3] : 0u;
+        t[i] = q == 0 ? w[i] : (q == 1 ? w[i + 1] : (q == 2 ? w[i + 2] : v3));
+    }
+    return make_uint4(__builtin_amdgcn_alignbyte(t[1], t[0], r), __builtin_amdgcn_alignbyte(t[2], t[1], r),
+                      __builtin_amdgcn_alignbyte(t[3], t[2], r), __builtin_amdgcn_alignbyte(t[4], t[3], r));
+}
+template <int U, bool FULL>
+__device__ __forceinline__ void fx_finish(const FxBatch<U>& t, uint8_t* ob) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t m = t.mode[u];
+        const uint4 xv = fx_sel4(m == 3, fx_vbyte_then(t.X[u]), t.X[u]);
+        const uint4 f = fx_funnel16(t.L[u], xv, t.sh[u] & 15);
+        const uint4 v = fx_sel4(m == 2, fx_vbyte_then(t.L[u]), fx_sel4(m != 0, f, t.L[u]));
+        if (FULL || t.aL[u]) fx_store16(ob + 16ull * (t.b + u * FX_THREADS), v);
+    }
+}
+
 #if SKV_TILE_PROF
 #define FXPROF(i)                                                                               \
     do {                                                                                        \
@@ -384,7 +533,6 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     const uint64_t S = A.S;
 #if SKV_TILE_PROF
     uint64_t tp_last = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0) atomicAdd((unsigned long long*)&A.prof[15], 1ull);
 #endif
     if (tid == 0) {
         s_t = atomicAdd(A.tcounter, 1u);
@@ -393,6 +541,10 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     }
     __syncthreads();
     const uint64_t t = s_t;
+#if SKV_TILE_PROF
+    if (tid == 0) atomicAdd((unsigned long long*)&A.prof[15], 1ull);
+#endif
+    do {
     // ---- segments: stream j contributes its records [bnd[t][j].pos, bnd[t+1][j].pos)
     uint64_t tot = 0;
     if (!s_dead) {
@@ -444,13 +596,13 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
         FxRec rec[PER];
 #pragma unroll
         for (int u = 0; u < PER; ++u)
-            if (ad[u]) fx_issue(ad[u], A.K, rec[u]);
+            if (ad[u] && SKV_FX_DIAG != 3) fx_issue(ad[u], A.K, rec[u]);
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             if (ad[u]) {
                 const uint32_t e = tid + u * FX_THREADS;
-                uint64_t h, l;
-                if (!fx_check(A, rec[u], ad[u], h, l)) bad |= FXR_RECORD;
+                uint64_t h = e + 1, l = 0;
+                if (SKV_FX_DIAG != 3 && !fx_check(A, rec[u], ad[u], h, l)) bad |= FXR_RECORD;
                 key[e] = make_ulong2(h, l);
                 id[e] = (uint16_t)e;
             }
@@ -473,7 +625,7 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
                 pv = prevk[j];
                 has = prevok[j] != 0;
             }
-            if (has && !fx_le(pv, c)) bad |= FXR_ORDER;  // a strict decrease
+            if (has && !fx_le(pv, c) && SKV_FX_DIAG != 3) bad |= FXR_ORDER;  // a strict decrease
         }
     }
     if (bad) atomicOr(&s_bad, bad);
@@ -485,7 +637,7 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
             __hip_atomic_store(&A.tstate[t], (t == 0 ? 2ull : 1ull) << 62, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
-        return;
+        break;
     }
     // ---- k_way::merge order (k_way.rs:20-27, :113-179): pairwise merge-path rounds over the k
     // stream segments (segment s pairs with s ^ 1, the left one holds newer seq_nos and wins ties,
@@ -493,7 +645,7 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     // produces PER consecutive outputs of a round: one merge-path search, then a sequential merge.
     const uint32_t i0 = tid * PER;
     {
-        uint32_t m = k;
+        uint32_t m = SKV_FX_DIAG >= 2 ? 1 : k;
         const uint32_t* cb = cb0;
         uint32_t* cbn = cbA;
         while (m > 1) {
@@ -601,7 +753,7 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     }
     __syncthreads();
     FXPROF(5);
-    if (!cnt || s_dead) return;
+    if (!cnt || s_dead || SKV_FX_DIAG == 1) break;
     // ---- output bytes of survivors g0 .. g0+cnt-1 (build_runs' bytes, runs.rs:241-267). The
     // tile's survivors form "pieces": runs of consecutive survivors inside one output run; piece 0
     // starts at survivor 0, piece i >= 1 at survivor jb1 + (i-1) n behind its run's version byte.
@@ -637,74 +789,57 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
 #endif
     const bool multi = SKV_FX_GENERIC_COPY || (jb1 < cnt && cnt - jb1 > nr);
     if (!multi) {
-        const uint64_t V0 = q0 == 0 ? a0 - 1 : ~0ull;       // version byte before survivor 0
-        const uint64_t Vb = jb1 < cnt ? V1 : ~0ull;          // version byte before survivor jb1
-        constexpr uint32_t D = 16u * FX_THREADS;              // bytes between a lane's blocks
-        const uint32_t dq = D / S32, dr = D % S32;
-        uint64_t B = Blo + 16ull * tid;
-        uint32_t j = 0, o = 0;
-        bool past = B > Vb;
+        FxWalk w;
+        w.V0 = q0 == 0 ? a0 - 1 : ~0ull;  // version byte before survivor 0
+        w.Vb = jb1 < cnt ? V1 : ~0ull;     // version byte before survivor jb1
+        w.jb1 = (uint32_t)jb1;
+        w.S32 = S32;
+        w.dq = (16u * FX_THREADS) / S32;
+        w.dr = (16u * FX_THREADS) % S32;
+        w.B = Blo + 16ull * tid;
+        w.j = 0;
+        w.o = 0;
+        w.past = w.B > w.Vb;
         {
-            const int64_t y = (int64_t)(B - a0) - (past ? 1 : 0);
+            const int64_t y = (int64_t)(w.B - a0) - (w.past ? 1 : 0);
             if (y < 0) {  // B is the version byte before survivor 0: y == -1
-                j = 0xFFFFFFFFu;
-                o = S32 - 1;
-            } else if (B < Bhi) {
-                j = fx_div32((uint32_t)y, S32, A.inv_S, o);
+                w.j = 0xFFFFFFFFu;
+                w.o = S32 - 1;
+            } else if (w.B < Bhi) {
+                uint32_t oo;
+                w.j = fx_div32((uint32_t)y, S32, A.inv_S, oo);
+                w.o = oo;
             }
         }
-        for (uint32_t b = tid; b < nb; b += U * FX_THREADS) {
-            uint64_t aL[U], aX[U];
-            uint32_t mode[U], sh[U];  // 0: one record, 1: record tail + next, 2: version byte + record, 3: tail + version + next
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                aL[u] = aX[u] = 0;
-                mode[u] = 0;
-                sh[u] = 0;
-                if (b + u * FX_THREADS < nb) {
-                    if (B == V0 || B == Vb) {
-                        aL[u] = src[B == V0 ? 0 : (uint32_t)jb1];
-                        mode[u] = 2;
-                    } else if (o + 16 <= S32) {
-                        aL[u] = src[j] + o;
-                    } else {  // straddles record j's end: its last 16 bytes + what follows it
-                        aL[u] = src[j] + S - 16;
-                        aX[u] = src[j + 1];
-                        mode[u] = j + 1 == jb1 ? 3 : 1;
-                        sh[u] = 16 - (S32 - o);
-                    }
-                }
-                B += D;  // this lane's next block
-                o += dr;
-                j += dq;
-                if (o >= S32) {
-                    o -= S32;
-                    ++j;
-                }
-                if (!past && B > Vb) {  // crossed the run boundary: one version byte earlier
-                    past = true;
-                    if (o == 0) {
-                        o = S32 - 1;
-                        --j;
-                    } else {
-                        --o;
-                    }
-                }
+        // Software-pipelined over batches of U blocks: batch i+1's loads are issued before batch
+        // i's stores, so waiting for a batch's loads never waits for the previous batch's stores
+        // (vmcnt counts loads and stores in issue order on gfx9-family CDNA).
+        FxBatch<U> P0, P1;
+        uint8_t* const ob = out + Blo;
+        const uint64_t safe = src[0];
+        const uint32_t nfull = nb / (U * FX_THREADS);  // batches whose blocks are all < nb, every lane
+        uint32_t i = 0;
+        if (nfull) {
+            fx_plan<U>(P0, w, src, tid, nb, safe);
+            for (; i + 2 < nfull; i += 2) {  // P0 = batch i in flight
+                fx_plan<U>(P1, w, src, tid + (i + 1) * U * FX_THREADS, nb, safe);
+                fx_finish<U, true>(P0, ob);
+                fx_plan<U>(P0, w, src, tid + (i + 2) * U * FX_THREADS, nb, safe);
+                fx_finish<U, true>(P1, ob);
             }
-            uint4 L[U], X[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                L[u] = aL[u] ? fx_ld16(aL[u]) : make_uint4(0, 0, 0, 0);
-                X[u] = aX[u] ? fx_ld16(aX[u]) : make_uint4(0, 0, 0, 0);
+            if (i + 1 < nfull) {
+                fx_plan<U>(P1, w, src, tid + (i + 1) * U * FX_THREADS, nb, safe);
+                fx_finish<U, true>(P0, ob);
+                fx_finish<U, true>(P1, ob);
+                i += 2;
+            } else {
+                fx_finish<U, true>(P0, ob);
+                i += 1;
             }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (!aL[u]) continue;
-                uint4 v = L[u];
-                if (mode[u] == 2) v = fx_vbyte_then(L[u]);
-                else if (mode[u] != 0) v = funnel16(L[u], mode[u] == 3 ? fx_vbyte_then(X[u]) : X[u], sh[u]);
-                fx_store16(out + Blo + 16ull * (b + u * FX_THREADS), v);
-            }
+        }
+        for (uint32_t bb = tid + i * U * FX_THREADS; bb < nb; bb += U * FX_THREADS) {  // the partial batch
+            fx_plan<U>(P0, w, src, bb, nb, safe);
+            fx_finish<U, false>(P0, ob);
         }
     }
     // Per block: addresses and mode first, then every load of the U blocks, then the merges and
@@ -780,6 +915,7 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
         fx_store_bytes(out, B, B, end, fx_compose(A, src, B, B, end, (uint32_t)jL, (int64_t)(B - aL), qL));
     }
     FXPROF(7);
+    } while (0);
 }
 
 // descriptors + StatsV1 of the output runs: run r holds survivors [r n, min((r+1) n, K))
@@ -816,9 +952,10 @@ void launch_fx_sample(hipStream_t s, const FxArgs& A, const uint64_t* off_dst, u
                       uint64_t* dhi, uint64_t* dlo, uint64_t* dc) {
     if (n_dst) k_fx_sample<<<fx_blocks(n_dst, 256), 256, 0, s>>>(A, off_dst, Sstep, n_dst, dhi, dlo, dc);
 }
-void launch_fx_bounds(hipStream_t s, const FxArgs& A, const uint64_t* shi, const uint64_t* slo, uint64_t m) {
+void launch_fx_bounds(hipStream_t s, const FxArgs& A, const uint64_t* shi, const uint64_t* slo, uint64_t m,
+                      const uint64_t* l1hi, const uint64_t* l1lo, const uint64_t* l1off, uint64_t Sstep) {
     const uint64_t n = (A.T + 1) * A.k;
-    if (n) k_fx_bounds<<<fx_blocks(n, 256), 256, 0, s>>>(A, shi, slo, m);
+    if (n) k_fx_bounds<<<fx_blocks(n, 256), 256, 0, s>>>(A, shi, slo, m, l1hi, l1lo, l1off, Sstep);
 }
 size_t fx_tile_lds_bytes(uint32_t k) {
     return (size_t)FX_CAP * 16 + (size_t)k * 16 + 2 * (size_t)k * 8 + 3 * (size_t)(k + 1) * 4 + (size_t)FX_CAP * 2 + k + 16;

@@ -96,6 +96,8 @@ class SkvTimings(C.Structure):
         ("hot_ms", C.c_double),
         ("hot_read_bytes", C.c_uint64),
         ("hot_write_bytes", C.c_uint64),
+        ("sorted", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 

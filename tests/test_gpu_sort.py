@@ -1,0 +1,143 @@
+"""GPU parity of the record sort (skv_sort.hip): merges of more than TILE_TARGET / 2 = 1536
+streams (config 5's 10^6 WAL runs) sort the records by (key, record index) into one list before
+the level-0 merge stage. Same bar as test_gpu_parity: output bytes, StatsV1, dropped tables and
+the first error, bit-exact against the CPU restatement (oracle/).
+
+SKV_SORT=1 forces the sort at any fan-in, so the reference-derived fixtures and the random
+domain run through it as well."""
+import json
+import os
+import random
+
+import pytest
+
+from skv import _abi, gen
+from skv import format as fmt
+from skv.api import Compactor
+
+from test_gpu_parity import _case, _diff, _run_both
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = json.load(open(os.path.join(GOLDEN, "compact_cases.json")))
+MiB = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def dev():
+    torch = pytest.importorskip("torch")
+    torch.cuda.init()
+    c = Compactor(0, profiling=True)
+    yield c
+    c.close()
+
+
+@pytest.fixture
+def forced_sort(monkeypatch):
+    monkeypatch.setenv("SKV_SORT", "1")
+    monkeypatch.setenv("SKV_FUSED", "0")
+
+
+def _check(dev, streams, max_size, flags, expect_sorted=True):
+    exp, got = _run_both(dev, streams, max_size, flags)
+    assert exp == got, _diff(exp, got)
+    if expect_sorted and got[0] == "ok" and got[1]:
+        assert dev.timings()["sorted"] == 1, "the record sort did not run"
+    return got
+
+
+def test_forced_sort_golden_fixtures(dev, forced_sort):
+    bad = []
+    for case in CASES:
+        streams = [(s, [bytes.fromhex(r) for r in runs]) for s, runs in case["streams"]]
+        exp, got = _run_both(dev, streams, case["max"], case["flags"])
+        if exp != got:
+            bad.append((case["name"], _diff(exp, got)))
+    assert not bad, bad[:5]
+
+
+def test_forced_sort_random_cases(dev, forced_sort):
+    bad, n = [], 0
+    for seed in range(400):
+        streams, max_size, flags = _case(seed)
+        exp, got = _run_both(dev, streams, max_size, flags)
+        if got[0] == "err" and got[1] == _abi.SKV_E_UNSUPPORTED:
+            continue
+        n += 1
+        if exp != got:
+            bad.append((seed, _diff(exp, got)))
+    assert n > 200
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:5]}"
+
+
+@pytest.mark.parametrize("name,streams,max_size,flags", [
+    ("cfg2B", lambda: gen.config2(n_streams=16, n_records=3000, vsize=40, variant="B"), 256 * 1024, 0),
+    ("cfg3_var_keys", lambda: gen.config3(n_streams=24, run_bytes=96 * 1024, vsize=32), 128 * 1024, 0),
+    ("cfg3_drop", lambda: gen.config3(n_streams=24, run_bytes=96 * 1024, vsize=32), 128 * 1024, 1),
+    ("cfg5_wal", lambda: gen.config5(n_streams=300), 4 * MiB, 2),
+])
+def test_forced_sort_generated(dev, forced_sort, name, streams, max_size, flags):
+    _check(dev, streams(), max_size, flags)
+
+
+def test_fan_in_2000_wal_runs(dev):
+    """Config-5 shape past the splitter merge's fan-in: 2000 WAL runs of 83 records (32-byte
+    "{table}.{suffix}" keys whose first 16 bytes mostly agree, so every bucket sorts on the bytes
+    after its splitters' common prefix)."""
+    _check(dev, gen.config5(n_streams=2000), 4 * MiB, _abi.SKV_SPLIT_BY_TABLE)
+
+
+def test_fan_in_1600_overlapping_streams(dev):
+    """1600 streams over a shared key universe: superseded records across streams (newest wins)."""
+    streams = gen.config2(n_streams=1600, n_records=60, vsize=12, variant="B")
+    _check(dev, streams, 64 * 1024, 0)
+
+
+def test_fan_in_var_keys_with_tombstones(dev):
+    streams = gen.config3(n_streams=1700, run_bytes=6000, vsize=16)
+    _check(dev, streams, 256 * 1024, 0)
+    _check(dev, streams, 256 * 1024, _abi.SKV_DROP_TOMBSTONES)
+
+
+def test_fan_in_equal_key_flood(dev):
+    """3000 streams holding the same few keys: one bucket far above SORT_CAP (the global-memory
+    bucket sort), the newest seq_no wins each key."""
+    r = random.Random(5)
+    streams = []
+    for s in range(3000):
+        keys = sorted({f"k{r.randrange(4)}" for _ in range(3)} | {f"u{s:05d}"})
+        ops = [fmt.put(k, s.to_bytes(4, "big")) if r.random() < 0.8 else fmt.delete(k) for k in keys]
+        streams.append((s * 7 - 9000, [fmt.encode_run(ops)]))
+    _check(dev, streams, 1 << 14, 0)
+    _check(dev, streams, 1 << 14, _abi.SKV_DROP_TOMBSTONES)
+
+
+def test_fan_in_long_shared_prefixes(dev):
+    """Keys of 40-90 bytes sharing a 35-byte prefix, plus keys that are prefixes of others."""
+    r = random.Random(9)
+    base = "tenant-0001/namespace/partition-000/"
+    streams = []
+    for s in range(1800):
+        ks = set()
+        for _ in range(r.randint(1, 8)):
+            tail = "".join(r.choice("ab") for _ in range(r.randint(0, 50)))
+            ks.add((base + tail).encode())
+        ops = [fmt.put(k, bytes([s & 255])) for k in sorted(ks)]
+        streams.append((s + 1, [fmt.encode_run(ops)]))
+    _check(dev, streams, 1 << 16, 0)
+
+
+def test_fan_in_errors_surface_like_the_reference(dev):
+    """A corrupt or unsorted stream among 1600: the error is resolved before the sort."""
+    r = random.Random(3)
+    streams = []
+    for s in range(1600):
+        ops = [fmt.put(f"{r.randrange(10**6):07d}", b"v") for _ in range(5)]
+        ops = sorted({o[1]: o for o in ops}.values(), key=lambda o: o[1])
+        streams.append((s + 1, [fmt.encode_run(ops)]))
+    bad = bytearray(streams[777][1][0])
+    bad[0] = 3  # unsupported version
+    streams[777] = (streams[777][0], [bytes(bad)])
+    exp, got = _run_both(dev, streams, 4 * MiB, 0)
+    assert exp == got, _diff(exp, got)
