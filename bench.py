@@ -9,9 +9,17 @@ record, 67,108,702 B per run, 4.0 GiB total), max run size 4 MiB, no tombstones.
 inputs already resident in HBM. At N GPUs every rank runs its own independent compaction
 (distinct seeds; BASELINE config 4 at N=8): weak scaling, no collective on the data path.
 
-Prints ONE JSON line on rank 0 with `roofline` (the gather kernel: algorithmic bytes / its
+Prints ONE JSON line on rank 0 with `roofline` (the dominant kernel: algorithmic bytes / its
 HIP-event-timed duration on the library stream) and `cpu_baseline` (the C restatement in
 oracle/, faithful shape, 1 core, on a bounded sample of the same workload).
+
+--config selects the other BASELINE shapes for measurement records (never the default line):
+  2B  config 2 with keys from a universe of |R| ids (~37 % superseded)
+  3   256 streams of variable-length keys (8-128 B alnum) + 10 % Deletes, runs of --run-mib MiB
+      (default 16: 1/16 of BASELINE's 256 MiB runs), built on the host, general path
+  5   10^6 WAL runs x 83 records (32 B "{table}.{suffix}" keys, 8 B values), SKV_SPLIT_BY_TABLE,
+      built in HBM; max run size 2^62 so every table keeps its one run (at the reference's 4 MiB
+      every table of this size would be dropped by the exactly-one-run rule)
 """
 import argparse
 import json
@@ -29,7 +37,7 @@ METRIC = "compaction GiB/s of input run bytes merged (device-resident), 1/2/4/8 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MAX_RUN = 4 * 1024 * 1024
 # the dominant kernel of each device path (skv_timings.path) and what its bytes count
-HOT_KERNEL = {1: "k_gather", 2: "k_gather", 3: "k_fx_tile"}
+HOT_KERNEL = {1: "k_gather", 2: "k_gather", 3: "k_fx_tile"}  # config 5 (WAL stage): k_wal_gather
 PATH_NAMES = {1: "general", 2: "fixed", 3: "fused"}
 GiB = float(1 << 30)
 
@@ -62,20 +70,84 @@ def make_cfg2_on_device(device, seed, n_streams, n_records, vsize, variant="A"):
     return runs
 
 
-def cpu_baseline(sample_records, n_streams, vsize, repeats):
+def make_cfg3_on_device(device, seed, n_streams, run_mib, vsize=256):
+    """Config 3 (scaled): gen.config3's runs (variable-length sorted alnum keys, 10 % Deletes)
+    built on the host, copied to HBM."""
+    from skv import gen
+
+    streams = gen.config3(seed=seed, n_streams=n_streams, run_bytes=run_mib << 20, vsize=vsize)
+    runs = [torch.frombuffer(bytearray(r[1][0]), dtype=torch.uint8).to(device) for r in streams]
+    torch.cuda.synchronize(device)
+    return runs
+
+
+def make_cfg5_on_device(device, seed, n_streams, n_records=83, n_tables=64):
+    """Config 5: n_streams WAL runs of n_records Puts, key "{t}." + zero-filled decimal suffix
+    (32 B, gen.wal_run's format), 8 B values, each run sorted bytewise; one HBM tensor."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    N = n_streams * n_records
+    t = torch.randint(0, n_tables, (N,), device=device, generator=g)
+    suf = torch.randint(0, 10 ** 12, (N,), device=device, generator=g, dtype=torch.int64)
+    keys = torch.full((N, 32), ord("0"), dtype=torch.int64, device=device)
+    two = t < 10
+    keys[:, 0] = torch.where(two, t, t // 10) + ord("0")
+    keys[:, 1] = torch.where(two, torch.full_like(t, ord(".")), t % 10 + ord("0"))
+    keys[:, 2] = torch.where(two, torch.full_like(t, ord("0")), torch.full_like(t, ord(".")))
+    x = suf.clone()
+    for i in range(31, 19, -1):
+        keys[:, i] = x % 10 + ord("0")
+        x //= 10
+    # bytewise order inside each run: stable LSD sorts over the four big-endian 8-byte words
+    w = (keys.view(N, 4, 8) << torch.tensor([56, 48, 40, 32, 24, 16, 8, 0], device=device)).sum(dim=2)
+    w = w.view(n_streams, n_records, 4)
+    order = torch.arange(n_records, device=device).expand(n_streams, n_records).contiguous()
+    for q in (3, 2, 1, 0):
+        vals = torch.gather(w[:, :, q], 1, order)
+        _, o = torch.sort(vals, dim=1, stable=True)
+        order = torch.gather(order, 1, o)
+    rows = torch.arange(n_streams, device=device).unsqueeze(1) * n_records
+    keys = keys.to(torch.uint8)[(rows + order).reshape(-1)]
+    rec = torch.empty((N, 49), dtype=torch.uint8, device=device)
+    rec[:, 0:5] = torch.tensor([1, 0, 0, 0, 32], dtype=torch.uint8, device=device)
+    rec[:, 5:37] = keys
+    rec[:, 37:41] = torch.tensor([0, 0, 0, 8], dtype=torch.uint8, device=device)
+    rec[:, 41:49] = torch.randint(0, 256, (N, 8), dtype=torch.uint8, device=device, generator=g)
+    run_len = 1 + n_records * 49
+    buf = torch.empty((n_streams, run_len), dtype=torch.uint8, device=device)
+    buf[:, 0] = 1
+    buf[:, 1:] = rec.view(n_streams, n_records * 49)
+    del rec, keys, w, order, t, suf, x
+    torch.cuda.synchronize(device)
+    return buf
+
+
+def cpu_baseline(config, sample_records, n_streams, vsize, repeats, run_mib=16):
     """oracle/ (C restatement of read_run_stream + k_way::merge + build_runs, faithful shape,
-    single thread) on a bounded sample: same shape, n_streams x sample_records records."""
+    single thread) on a bounded sample of the same shape."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     from skv import gen
 
-    streams = gen.config2(seed=0xC0FFEE, n_streams=n_streams, n_records=sample_records, vsize=vsize)
+    flags, max_run = 0, MAX_RUN
+    if config in ("2A", "2B"):
+        streams = gen.config2(seed=0xC0FFEE, n_streams=n_streams, n_records=sample_records, vsize=vsize,
+                              variant=config[1])
+        sample = (f"{n_streams} streams x {sample_records} records x {9 + 16 + vsize} B (config-{config} shape, "
+                  f"1/{round(238821 / sample_records)} of the records)")
+    elif config == "3":
+        streams = gen.config3(seed=0xC0FFEE, n_streams=n_streams, run_bytes=(run_mib << 20) // 16)
+        sample = f"{n_streams} streams x {run_mib / 16:.2f} MiB runs (config-3 shape, 1/16 of the bench's runs)"
+    else:
+        streams = gen.config5(seed=0xC0FFEE, n_streams=20000)
+        flags, max_run = 2, 1 << 62
+        sample = "20,000 WAL runs x 83 records (config-5 shape, 1/50 of the streams)"
     nbytes = gen.total_bytes(streams)
-    pyoracle.compact(streams, MAX_RUN)  # warm-up
+    pyoracle.compact(streams, max_run, flags)  # warm-up
     ts = []
     for _ in range(repeats):
         t0 = time.perf_counter()
-        pyoracle.compact(streams, MAX_RUN)
+        pyoracle.compact(streams, max_run, flags)
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
     return {
@@ -83,8 +155,7 @@ def cpu_baseline(sample_records, n_streams, vsize, repeats):
         "unit": "GiB/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{n_streams} streams x {sample_records} records x {9 + 16 + vsize} B = {nbytes / 2**20:.1f} MiB "
-                  f"(config-2 shape, 1/{round(238821 / sample_records)} of the records), median of {repeats} after 1 warm-up",
+        "sample": f"{sample} = {nbytes / 2**20:.1f} MiB, median of {repeats} after 1 warm-up",
         "seconds_per_run": round(t, 3),
     }
 
@@ -114,7 +185,10 @@ def main():
     ap.add_argument("--streams", type=int, default=64)
     ap.add_argument("--records", type=int, default=238821)
     ap.add_argument("--vsize", type=int, default=256)
-    ap.add_argument("--variant", default="A")
+    ap.add_argument("--variant", default="A", help="config 2 variant (same as --config 2A / 2B)")
+    ap.add_argument("--config", default=None, choices=["2A", "2B", "3", "5"])
+    ap.add_argument("--run-mib", type=int, default=16, help="config 3 run size")
+    ap.add_argument("--wal-runs", type=int, default=1_000_000, help="config 5 stream count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-memory figure")
     ap.add_argument("--cpu-sample-records", type=int, default=238821 // 16)
@@ -137,15 +211,48 @@ def main():
     from skv.api import Compactor
 
     seed = rank_seed(rank)
-    runs = make_cfg2_on_device(device, seed, args.streams, args.records, args.vsize, args.variant)
-    in_bytes = sum(r.numel() for r in runs)
-    streams = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(runs)]
+    config = args.config or "2" + args.variant
+    flags, max_run = 0, MAX_RUN
+    if config in ("2A", "2B"):
+        runs = make_cfg2_on_device(device, seed, args.streams, args.records, args.vsize, config[1])
+        workload = (f"config {config}: {args.streams}-way L0->L1 compaction, {args.streams} x 1 run x {args.records} "
+                    f"records ({9 + 16 + args.vsize} B: 16 B keys / {args.vsize} B values), max run 4 MiB, "
+                    f"one independent compaction per GPU")
+        data = "synthetic: splitmix64 sorted unique hex keys + device-RNG values, built in HBM"
+        n_streams = args.streams
+    elif config == "3":
+        n_streams = 256 if args.streams == 64 else args.streams
+        runs = make_cfg3_on_device(device, seed, n_streams, args.run_mib)
+        workload = (f"config 3 (scaled): {n_streams}-way compaction, {n_streams} x 1 run of ~{args.run_mib} MiB, "
+                    f"variable-length keys 8-128 B + 10 % Deletes, 256 B values, max run 4 MiB")
+        data = "synthetic: gen.config3 (splitmix64 ids, alnum keys sorted bytewise), host-built, copied to HBM"
+    else:
+        n_streams = args.wal_runs
+        buf = make_cfg5_on_device(device, seed, n_streams)
+        runs = [buf]
+        flags, max_run = 2, 1 << 62
+        workload = (f"config 5: WAL -> table-buffer flush, {n_streams} WAL runs x 83 records (32 B keys / 8 B values, "
+                    f"4,068 B runs), SKV_SPLIT_BY_TABLE over 64 tables, one run per table")
+        data = "synthetic: device-RNG table ids and suffixes, runs sorted in HBM"
+    if config == "5":
+        rl = buf.shape[1]
+        base = buf.data_ptr()
+        in_bytes = buf.numel()
+        streams = [(s + 1, [(base + s * rl, rl)]) for s in range(n_streams)]
+    else:
+        in_bytes = sum(r.numel() for r in runs)
+        streams = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(runs)]
     comp = Compactor(local_rank, profiling=True)
+    # the skv_stream[] table, built once like a caller's Vec (at 10^6 streams building it in Python
+    # costs more than the compaction)
+    from skv._abi import StreamArgs
+
+    table = StreamArgs(streams, device=True)
 
     out_bytes = 0
     n_out_runs = 0
     for _ in range(args.warmup):
-        res = comp.compact_dev(streams, MAX_RUN, 0)
+        res = comp.compact_dev(table, max_run, flags)
         out_bytes, n_out_runs = res.n_bytes, res.n_runs
         res.free()
 
@@ -159,7 +266,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tc = time.perf_counter()
-        res = comp.compact_dev(streams, MAX_RUN, 0)
+        res = comp.compact_dev(table, max_run, flags)
         call_ms.append((time.perf_counter() - tc) * 1e3)
         t = comp.timings()
         host_ms.append(t["host_total_ms"])
@@ -177,14 +284,14 @@ def main():
     # PCIe-inclusive figure (not `value`): the host entry point skv_compact with the inputs in
     # pinned host memory and the output runs returned in pinned host memory.
     host_path = None
-    if rank == 0 and world == 1 and not args.no_host_path:
+    if rank == 0 and world == 1 and not args.no_host_path and config in ("2A", "2B", "3"):
         host_runs = [r.cpu().pin_memory() for r in runs]
         hstreams = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(host_runs)]
-        comp.compact_host_ptrs(hstreams, MAX_RUN, 0)  # warm-up (allocates the staging buffers)
+        comp.compact_host_ptrs(hstreams, max_run, flags)  # warm-up (allocates the staging buffers)
         hts = []
         for _ in range(2):
             t1 = time.perf_counter()
-            hb, _ = comp.compact_host_ptrs(hstreams, MAX_RUN, 0)
+            hb, _ = comp.compact_host_ptrs(hstreams, max_run, flags)
             hts.append(time.perf_counter() - t1)
         ht = min(hts)
         host_path = {"value": round(in_bytes / ht / GiB, 3), "unit": "GiB/s", "ms": round(ht * 1e3, 3),
@@ -197,6 +304,8 @@ def main():
         ms_per_step = elapsed / args.steps * 1e3
         value = total_in * args.steps / elapsed / GiB
         g_ms = float(np.mean(gather_ms))
+        if g_ms <= 0:  # the WAL stage reports no single dominant launch: the whole device time
+            g_ms = float(np.mean(total_ms))
         achieved = (gread + gwrite) / (g_ms * 1e-3) / 1e9
         traffic = None
         try:
@@ -217,12 +326,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: splitmix64 sorted unique hex keys + device-RNG values, built in HBM",
+            "data": data,
             "config": {
-                "workload": f"config 2{args.variant}: {args.streams}-way L0->L1 compaction, {args.streams} x 1 run x "
-                            f"{args.records} records ({9 + 16 + args.vsize} B: 16 B keys / {args.vsize} B values), "
-                            f"max run 4 MiB, one independent compaction per GPU",
-                "streams": args.streams,
+                "workload": workload,
+                "streams": n_streams,
                 "input_bytes_per_gpu": in_bytes,
                 "output_bytes_per_gpu": out_bytes,
                 "output_runs_per_gpu": n_out_runs,
@@ -234,9 +341,10 @@ def main():
                         "in_syncs": round(float(np.mean(sync_ms)), 4)},
             "phases_ms": dict(zip(("parse", "check", "merge", "chain", "gather"),
                                   [round(float(x), 4) for x in np.mean(np.array(phases), axis=0)])),
+            "record_sort": bool(t["sorted"]),
             "roofline": {
                 "bound": "hbm",
-                "kernel": HOT_KERNEL.get(path, "?"),
+                "kernel": "k_wal_gather" if config == "5" else HOT_KERNEL.get(path, "?"),
                 "path": PATH_NAMES.get(path, "?"),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
@@ -253,7 +361,8 @@ def main():
         if host_path is not None:
             line["host_path"] = host_path
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_sample_records, args.streams, args.vsize, args.cpu_repeats)
+            line["cpu_baseline"] = cpu_baseline(config, args.cpu_sample_records, n_streams if config != "5" else 0,
+                                            args.vsize, args.cpu_repeats, args.run_mib)
         print(json.dumps(line), flush=True)
     comp.close()
     if dist is not None:

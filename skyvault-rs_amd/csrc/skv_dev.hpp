@@ -275,21 +275,6 @@ __device__ inline void key_prefix(const uint8_t* k, uint64_t klen, uint64_t& hi,
     lo = l;
 }
 
-// Ordering of two keys given their 16-byte prefixes, lengths and (for keys > 16 B) their bytes:
-// bytewise lexicographic, proper prefix first (Rust str Ord). Returns <0, 0, >0.
-__device__ inline int key_cmp(uint64_t ahi, uint64_t alo, uint32_t alen, const uint8_t* akey,
-                              uint64_t bhi, uint64_t blo, uint32_t blen, const uint8_t* bkey) {
-    if (ahi != bhi) return ahi < bhi ? -1 : 1;
-    if (alo != blo) return alo < blo ? -1 : 1;
-    if (alen > 16 && blen > 16) {
-        uint32_t n = (alen < blen ? alen : blen);
-        for (uint32_t i = 16; i < n; ++i) {
-            uint32_t x = akey[i], y = bkey[i];
-            if (x != y) return x < y ? -1 : 1;
-        }
-    }
-    return alen < blen ? -1 : (alen > blen ? 1 : 0);
-}
 
 // 16 bytes from an arbitrary (unaligned) address using two aligned 16-byte loads. The second
 // aligned block contains p+15, so it holds at least one byte the caller owns and never crosses
@@ -358,6 +343,37 @@ __device__ __forceinline__ uint32_t dword_mask(uint32_t a, uint32_t b, uint32_t 
     if (lo >= hi) return 0u;
     uint64_t m = ((1ull << (8 * (hi - lo))) - 1) << (8 * (lo - 4 * i));
     return (uint32_t)m;
+}
+
+// bytewise order of the first n bytes at a and b (<0, 0, >0), 16 bytes per step (only the
+// aligned 16-byte blocks holding requested bytes are read)
+__device__ inline int bytes_cmp16(const uint8_t* a, const uint8_t* b, uint64_t n) {
+    for (uint64_t i = 0; i < n; i += 16) {
+        const uint32_t m = (uint32_t)(n - i < 16 ? n - i : 16);
+        const uint4 x = load_window16(a + i, m), y = load_window16(b + i, m);
+        const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t mk = dword_mask(0, m, q);
+            const uint32_t xa = __builtin_bswap32(xs[q] & mk), ya = __builtin_bswap32(ys[q] & mk);
+            if (xa != ya) return xa < ya ? -1 : 1;
+        }
+    }
+    return 0;
+}
+
+// Ordering of two keys given their 16-byte prefixes, lengths and (for keys > 16 B) their bytes:
+// bytewise lexicographic, proper prefix first (Rust str Ord). Returns <0, 0, >0.
+__device__ inline int key_cmp(uint64_t ahi, uint64_t alo, uint32_t alen, const uint8_t* akey,
+                              uint64_t bhi, uint64_t blo, uint32_t blen, const uint8_t* bkey) {
+    if (ahi != bhi) return ahi < bhi ? -1 : 1;
+    if (alo != blo) return alo < blo ? -1 : 1;
+    if (alen > 16 && blen > 16) {
+        const uint32_t n = (alen < blen ? alen : blen);
+        const int c = bytes_cmp16(akey + 16, bkey + 16, n - 16);
+        if (c) return c;
+    }
+    return alen < blen ? -1 : (alen > blen ? 1 : 0);
 }
 
 // ---- vectorized record headers --------------------------------------------------------------

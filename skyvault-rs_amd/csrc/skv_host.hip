@@ -210,11 +210,13 @@ static int derr_to_api(uint32_t e, std::string& msg) {
 struct InStream {
     int64_t seq;
     uint32_t vec_idx;  // position in the caller's vector (merge pulls first items in this order)
-    std::vector<uint64_t> ptrs, lens;
+    uint32_t n_runs;
+    uint64_t first;    // its member runs: Job::run_ptr/run_len[first, first + n_runs)
 };
 
 struct Job {
     std::vector<InStream> ranked;  // streams sorted by seq_no descending
+    std::vector<uint64_t> run_ptr, run_len;  // member runs, caller order (flat: 10^6-stream jobs)
     uint64_t max_run_size = 0;
     uint32_t flags = 0;
     uint64_t in_bytes = 0;
@@ -275,6 +277,7 @@ static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
     (void)R;
     int64_t* tid = dbuf<int64_t>(ctx, "w_tid", K + 1);
     uint32_t* strip = dbuf<uint32_t>(ctx, "w_strip", K + 1);
+    uint8_t* canon = dbuf<uint8_t>(ctx, "w_canon", K + 1);
     uint64_t* wsize = dbuf<uint64_t>(ctx, "w_size", K + 1);
     uint64_t* is_new = dbuf<uint64_t>(ctx, "w_new", K + 1);
     uint64_t* new_ex = dbuf<uint64_t>(ctx, "w_new_ex", K + 1);
@@ -291,15 +294,14 @@ static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
     uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "w_scan_tmp", scan_tmp_words(K + 1) + 64);
     DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", K + 1);
     uint64_t total_rec_bytes = 0;
-    for (const InStream& S : job.ranked)
-        for (uint64_t l : S.lens) total_rec_bytes += l;
+    for (uint64_t l : job.run_len) total_rec_bytes += l;
     uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + K + 16);
     HIPCHK(hipMemsetAsync(first_err, 0xFF, 8, st));
     HIPCHK(hipMemsetAsync(tbad, 0, (K + 1) * 4, st));
     HIPCHK(hipMemsetAsync(run_len, 0, (K + 1) * 8, st));
     HIPCHK(hipMemsetAsync(keep, 0, (K + 1) * 8, st));
-    launch_wal_keys(st, d_K, K, m_src, m_rec, rec_klen, m_P, tid, strip, wsize, first_err);
-    launch_wal_flags(st, d_K, K, tid, strip, m_src, m_rec, rec_klen, is_new, bad);
+    launch_wal_keys(st, d_K, K, m_src, m_rec, rec_klen, m_P, tid, strip, wsize, canon, first_err);
+    launch_wal_flags(st, d_K, K, tid, strip, canon, m_src, m_rec, rec_klen, is_new, bad);
     launch_scan(st, is_new, K, new_ex, scan_tmp);  // new_ex[K] = number of tables
     launch_wal_index(st, d_K, K, is_new, new_ex, bad, tix, tstart, tbad);
     launch_scan(st, wsize, K, Pw, scan_tmp);       // stripped record offsets
@@ -356,7 +358,11 @@ static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
         t.gather_ms = ms[PH_GATHER];
         t.gather_read_bytes = n_bytes - n_kept;
         t.gather_write_bytes = n_bytes;
+        t.hot_ms = ms[PH_GATHER];
     }
+    ctx->timings.path = SKV_PATH_GENERAL;  // WAL stage: the dominant launch is k_wal_gather
+    ctx->timings.hot_read_bytes = n_bytes - n_kept;
+    ctx->timings.hot_write_bytes = n_bytes;
     ctx->timings.host_syncs = ctx->syncs;
     *out = res;
     return SKV_OK;
@@ -560,7 +566,7 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
 
 // Sorts n SElems by (key, record index) (skv_sort.hip); E and T are n-element buffers, the
 // result is in the returned one of the two. Samples recurse with their own buffers (depth).
-static SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth) {
+static SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth, uint64_t* newkey = nullptr) {
     hipStream_t st = ctx->stream;
     char nm[64];
     if (n <= (uint64_t)SORT_CAP) {  // one bucket
@@ -568,7 +574,7 @@ static SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth
         uint64_t* start = dbuf<uint64_t>(ctx, nm, 2);
         const uint64_t h[2] = {0, n};
         h2d_up(ctx, start, h, 16);
-        launch_sort_tile(st, E, start, nullptr, 1, T);
+        launch_sort_tile(st, E, start, nullptr, 1, T, newkey);
         return T;
     }
     const uint64_t Ns = (n + SORT_EVERY - 1) / SORT_EVERY;
@@ -591,35 +597,44 @@ static SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth
     uint64_t* scan_tmp = dbuf<uint64_t>(ctx, nm, scan_tmp_words(Tb) + 64);
     launch_sort_prefix(st, Ss, SORT_OV, Tb, L);
     HIPCHK(hipMemsetAsync(cnt, 0, (Tb + 1) * 8, st));
-    launch_sort_bucket(st, E, n, Ss, SORT_OV, Tb - 1, cnt, bs);
+    snprintf(nm, sizeof nm, "sort_split%d", depth);
+    uint8_t* split_buf = dbuf<uint8_t>(ctx, nm, sort_split_bytes(Tb - 1));
+    launch_sort_bucket(st, E, n, Ss, SORT_OV, Tb - 1, split_buf, cnt, bs);
     launch_scan(st, cnt, Tb, start, scan_tmp);
     launch_sort_scatter(st, E, n, bs, start, T);
-    launch_sort_tile(st, T, start, L, Tb, E);
+    launch_sort_tile(st, T, start, L, Tb, E, newkey);
     return E;
 }
 
 // The merged order of R records as one sorted list: the record arrays are replaced by sorted
 // copies (merges of more than TILE_TARGET / 2 streams, whose splitter bounds table would be
-// tiles x streams).
+// tiles x streams). hi/lo/cmp_klen become dense key ranks for the merge stage; klen stays the real
+// key length (descriptors, WAL split).
 static void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo, uint64_t*& addr, uint32_t*& klen,
-                         uint32_t*& meta) {
+                         uint32_t*& meta, const uint32_t*& cmp_klen) {
     hipStream_t st = ctx->stream;
     SElem* E = dbuf<SElem>(ctx, "sort_e", R);
     SElem* T = dbuf<SElem>(ctx, "sort_t", R);
+    uint64_t* newkey = dbuf<uint64_t>(ctx, "sort_newkey", R + 1);
+    uint64_t* newkey_ex = dbuf<uint64_t>(ctx, "sort_newkey_ex", R + 1);
+    uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "sort_rank_scan", scan_tmp_words(R) + 64);
     launch_sort_load(st, R, hi, lo, addr, klen, E);
-    const SElem* S = sort_elems(ctx, E, T, R, 0);
+    const SElem* S = sort_elems(ctx, E, T, R, 0, newkey);
+    launch_scan(st, newkey, R, newkey_ex, scan_tmp);
     uint64_t* nhi = dbuf<uint64_t>(ctx, "srt_hi", R);
     uint64_t* nlo = dbuf<uint64_t>(ctx, "srt_lo", R);
     uint64_t* naddr = dbuf<uint64_t>(ctx, "srt_addr", R);
     uint32_t* nklen = dbuf<uint32_t>(ctx, "srt_klen", R);
+    uint32_t* ncklen = dbuf<uint32_t>(ctx, "srt_cklen", R);
     uint32_t* nmeta = dbuf<uint32_t>(ctx, "srt_meta", R);
-    launch_sort_store(st, R, S, meta, nhi, nlo, naddr, nklen, nmeta);
+    launch_sort_store(st, R, S, meta, newkey, newkey_ex, nhi, nlo, naddr, nklen, ncklen, nmeta);
     HIPCHK(hipGetLastError());
     hi = nhi;
     lo = nlo;
     addr = naddr;
     klen = nklen;
     meta = nmeta;
+    cmp_klen = ncklen;
 }
 
 // allow_deferred: on the fixed-stride fast path, launch the merge without waiting for the parse's
@@ -639,10 +654,10 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     for (uint32_t s = 0; s < k; ++s) {
         stream_first_run[s] = (uint32_t)runs.size();
         const InStream& S = job.ranked[s];
-        for (size_t m = 0; m < S.ptrs.size(); ++m) {
+        for (uint32_t m = 0; m < S.n_runs; ++m) {
             RunInfo R;
-            R.ptr = S.ptrs[m];
-            R.len = S.lens[m];
+            R.ptr = job.run_ptr[S.first + m];
+            R.len = job.run_len[S.first + m];
             R.chunk_base = n_chunks;
             R.n_chunks = R.len >= 2 ? (uint32_t)((R.len - 1 + CHUNK - 1) / CHUNK) : 0;
             R.stream = s;
@@ -905,12 +920,13 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     // Past TILE_TARGET / 2 streams the records are sorted into one list first (skv_sort.hip);
     // SKV_SORT=1 forces that path (tests).
     uint32_t km = k;  // lists the splitter merge sees
+    const uint32_t* cmp_klen = rec_klen;  // key lengths the merge compares (dense ranks: 0)
     std::vector<uint64_t> list_off = stream_base;
     uint64_t* d_list_off = d_stream_base;
     {
         const char* se = getenv("SKV_SORT");
         if ((k > (uint32_t)TILE_TARGET / 2 && R > (uint64_t)TILE_CAP) || (se && se[0] == '1')) {
-            sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta);
+            sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen);
             km = 1;
             list_off = {0, R};
             d_list_off = dbuf<uint64_t>(ctx, "sorted_off", 2);
@@ -945,7 +961,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         snprintf(nm, sizeof nm, "lv%d_c", li); L.c = dbuf<uint64_t>(ctx, nm, L.N);
         snprintf(nm, sizeof nm, "lv%d_off", li); L.d_off = dbuf<uint64_t>(ctx, nm, km + 1);
         h2d_up(ctx, L.d_off, L.off.data(), (km + 1) * 8);
-        launch_sample(st, li == 1, P.hi, P.lo, P.c, rec_klen, P.d_off, L.d_off, km, L.S, L.N, L.hi, L.lo, L.c);
+        launch_sample(st, li == 1, P.hi, P.lo, P.c, cmp_klen, P.d_off, L.d_off, km, L.S, L.N, L.hi, L.lo, L.c);
         lv.push_back(L);
     }
     // top-down: sort each sample level, derive splitters for the level below
@@ -968,7 +984,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         snprintf(nm, sizeof nm, "bounds%d", li);
         uint64_t* bounds = dbuf<uint64_t>(ctx, nm, (T + 1) * km);
         const Level* U = li + 1 < (int)lv.size() ? &lv[li + 1] : nullptr;
-        launch_bounds(st, l0, L.hi, L.lo, L.c, rec_klen, L.d_off, km, U ? U->shi : nullptr, U ? U->slo : nullptr,
+        launch_bounds(st, l0, L.hi, L.lo, L.c, cmp_klen, L.d_off, km, U ? U->shi : nullptr, U ? U->slo : nullptr,
                       U ? U->sc : nullptr, m, T, rec_addr, bounds, d_flags + 2);
         snprintf(nm, sizeof nm, "tile_n%d", li);
         uint64_t* tile_n = dbuf<uint64_t>(ctx, nm, T);
@@ -1005,7 +1021,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             snprintf(nm, sizeof nm, "s%d_lo", li); L.slo = O.olo = dbuf<uint64_t>(ctx, nm, L.N);
             snprintf(nm, sizeof nm, "s%d_c", li); L.sc = O.oc = dbuf<uint64_t>(ctx, nm, L.N);
         }
-        HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, rec_klen, bounds, km, T, tile_base, rec_meta, rec_addr,
+        HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, cmp_klen, bounds, km, T, tile_base, rec_meta, rec_addr,
                            (job.flags & SKV_DROP_TOMBSTONES) ? 1u : 0u, O, d_flags + 2));
         if (l0) T0 = T;
     }
@@ -1023,8 +1039,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     mark(ctx, PH_CHAIN);
     // ---- gather -----------------------------------------------------------------------------
     uint64_t total_rec_bytes = 0;
-    for (const InStream& S : job.ranked)
-        for (uint64_t l : S.lens) total_rec_bytes += l;
+    for (uint64_t l : job.run_len) total_rec_bytes += l;
     uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + R + 16);
 #if SKV_PAGE_GATHER
     {
@@ -1124,15 +1139,26 @@ static int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64
         InStream S;
         S.seq = s.seq_no;
         S.vec_idx = i;
+        S.n_runs = s.n_runs;
+        S.first = job.run_ptr.size();
         for (uint32_t r = 0; r < s.n_runs; ++r) {
             if (s.run_lens[r] && !s.runs[r]) return set_err(ctx, SKV_E_INVALID_ARG, "stream %u run %u: NULL data", i, r);
-            S.ptrs.push_back((uint64_t)(uintptr_t)s.runs[r]);
-            S.lens.push_back(s.run_lens[r]);
+            job.run_ptr.push_back((uint64_t)(uintptr_t)s.runs[r]);
+            job.run_len.push_back(s.run_lens[r]);
             job.in_bytes += s.run_lens[r];
         }
-        job.ranked.push_back(std::move(S));
+        job.ranked.push_back(S);
     }
-    std::stable_sort(job.ranked.begin(), job.ranked.end(), [](const InStream& a, const InStream& b) { return a.seq > b.seq; });
+    // rank order = seq_no descending (callers usually hand streams in one of the two orders)
+    bool asc = true, desc = true;
+    for (size_t i = 1; i < job.ranked.size() && (asc || desc); ++i) {
+        asc = asc && job.ranked[i - 1].seq < job.ranked[i].seq;
+        desc = desc && job.ranked[i - 1].seq > job.ranked[i].seq;
+    }
+    if (asc) std::reverse(job.ranked.begin(), job.ranked.end());
+    else if (!desc)
+        std::stable_sort(job.ranked.begin(), job.ranked.end(),
+                         [](const InStream& a, const InStream& b) { return a.seq > b.seq; });
     for (size_t i = 1; i < job.ranked.size(); ++i)
         if (job.ranked[i].seq == job.ranked[i - 1].seq)
             return set_err(ctx, SKV_E_INVALID_ARG, "duplicate seq_no %" PRId64, job.ranked[i].seq);
@@ -1248,16 +1274,13 @@ int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uin
     try {
         // stage inputs into HBM (16-byte aligned per run)
         uint64_t total = 0;
-        for (const InStream& S : job.ranked)
-            for (uint64_t l : S.lens) total += (l + 15) & ~15ull;
+        for (uint64_t l : job.run_len) total += (l + 15) & ~15ull;
         uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", total + 16);
         uint64_t off = 0;
-        for (InStream& S : job.ranked) {
-            for (size_t m = 0; m < S.ptrs.size(); ++m) {
-                if (S.lens[m]) h2d(ctx, d_in + off, (const void*)S.ptrs[m], S.lens[m]);
-                S.ptrs[m] = (uint64_t)(uintptr_t)(d_in + off);
-                off += (S.lens[m] + 15) & ~15ull;
-            }
+        for (size_t m = 0; m < job.run_ptr.size(); ++m) {
+            if (job.run_len[m]) h2d(ctx, d_in + off, (const void*)job.run_ptr[m], job.run_len[m]);
+            job.run_ptr[m] = (uint64_t)(uintptr_t)(d_in + off);
+            off += (job.run_len[m] + 15) & ~15ull;
         }
     } catch (const DevError& e) {
         return set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());

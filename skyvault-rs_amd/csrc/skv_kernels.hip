@@ -485,11 +485,8 @@ __device__ __forceinline__ int suffix_cmp(const uint64_t* rec_addr, uint64_t ca,
     if (la > 16 && lb > 16) {
         const uint8_t* a = (const uint8_t*)rec_addr[(uint32_t)ca] + 5;
         const uint8_t* b = (const uint8_t*)rec_addr[(uint32_t)cb] + 5;
-        uint32_t n = la < lb ? la : lb;
-        for (uint32_t i = 16; i < n; ++i) {
-            uint32_t x = a[i], y = b[i];
-            if (x != y) return x < y ? -1 : 1;
-        }
+        const uint32_t n = la < lb ? la : lb;
+        return bytes_cmp16(a + 16, b + 16, n - 16);
     }
     return 0;
 }

@@ -54,10 +54,10 @@ void launch_gather(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, cons
 // skv_wal.hip — SKV_SPLIT_BY_TABLE (wal_compaction.rs:66-174)
 void launch_wal_keys(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint32_t* m_rec,
                      const uint32_t* rec_klen, const uint64_t* P, int64_t* tid, uint32_t* strip, uint64_t* wsize,
-                     unsigned long long* first_err);
+                     uint8_t* canon, unsigned long long* first_err);
 void launch_wal_flags(hipStream_t, const uint64_t* Kp, uint64_t max_K, const int64_t* tid, const uint32_t* strip,
-                      const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen, uint64_t* is_new,
-                      uint32_t* bad);
+                      const uint8_t* canon, const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen,
+                      uint64_t* is_new, uint32_t* bad);
 void launch_wal_index(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint64_t* is_new, const uint64_t* new_ex,
                       const uint32_t* bad, uint32_t* tix, uint64_t* tstart, uint32_t* tbad);
 void launch_wal_tables(hipStream_t, const uint64_t* NTp, uint64_t max_NT, const uint64_t* tstart, const uint64_t* Pw,
@@ -84,15 +84,18 @@ void launch_fx_desc(hipStream_t, const FxArgs& A, DevRunDesc* descs, uint64_t* n
 // skv_sort.hip — record sort (fan-in above TILE_TARGET / 2)
 void launch_sort_load(hipStream_t, uint64_t R, const uint64_t* hi, const uint64_t* lo, const uint64_t* addr,
                       const uint32_t* klen, SElem* E);
-void launch_sort_store(hipStream_t, uint64_t R, const SElem* E, const uint32_t* meta_in, uint64_t* hi, uint64_t* lo,
-                       uint64_t* addr, uint32_t* klen, uint32_t* meta);
+void launch_sort_store(hipStream_t, uint64_t R, const SElem* E, const uint32_t* meta_in, const uint64_t* newkey,
+                       const uint64_t* newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr, uint32_t* klen,
+                       uint32_t* cmp_klen, uint32_t* meta);
 void launch_sort_sample(hipStream_t, const SElem* E, uint64_t n, uint64_t Ns, SElem* S);
 void launch_sort_prefix(hipStream_t, const SElem* Ss, uint64_t ov, uint64_t Tb, uint32_t* L);
 void launch_sort_bucket(hipStream_t, const SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
-                        uint64_t* cnt, uint64_t* bs);
+                        void* split_buf, uint64_t* cnt, uint64_t* bs);
+size_t sort_split_bytes(uint64_t nsp);
 void launch_sort_scatter(hipStream_t, const SElem* E, uint64_t n, const uint64_t* bs, const uint64_t* start,
                          SElem* out);
-void launch_sort_tile(hipStream_t, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out);
+void launch_sort_tile(hipStream_t, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out,
+                      uint64_t* newkey);
 uint64_t scan_tmp_words(uint64_t n);
 void launch_scan(hipStream_t, const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tmp);
 }  // namespace skv

@@ -19,26 +19,11 @@
 //      prefix, then the key length and record index (the rest of a longer key from memory on a
 //      tie); buckets above SORT_CAP sort in global memory (same order, slower)
 // The sorted records then form ONE stream, and the level-0 merge machinery runs on them with
-// k = 1: first record per key, Delete filter, dense output arrays (skv_host.hip).
+// k = 1 on dense key ranks (one per distinct key, flagged by the bucket sort): first record per
+// key, Delete filter, dense output arrays (skv_host.hip).
 #include "skv_launch.hpp"
 
 namespace skv {
-
-// bytewise order of the first n bytes at a and b (<0, 0, >0), 16 bytes per step
-__device__ inline int sk_bytes_cmp(const uint8_t* a, const uint8_t* b, uint64_t n) {
-    for (uint64_t i = 0; i < n; i += 16) {
-        const uint32_t m = (uint32_t)(n - i < 16 ? n - i : 16);
-        const uint4 x = load_window16(a + i, m), y = load_window16(b + i, m);
-        const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w};
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            const uint32_t mk = dword_mask(0, m, q);
-            const uint32_t xa = __builtin_bswap32(xs[q] & mk), ya = __builtin_bswap32(ys[q] & mk);
-            if (xa != ya) return xa < ya ? -1 : 1;
-        }
-    }
-    return 0;
-}
 
 // index of the first differing byte among the first n bytes (n if none)
 __device__ inline uint64_t sk_bytes_diff(const uint8_t* a, const uint8_t* b, uint64_t n) {
@@ -63,7 +48,7 @@ __device__ inline int sk_kcmp(const SElem& a, const SElem& b) {
     if (a.lo != b.lo) return a.lo < b.lo ? -1 : 1;
     if (a.klen > 16 && b.klen > 16) {
         const uint32_t n = a.klen < b.klen ? a.klen : b.klen;
-        const int s = sk_bytes_cmp(sk_key(a) + 16, sk_key(b) + 16, n - 16);
+        const int s = bytes_cmp16(sk_key(a) + 16, sk_key(b) + 16, n - 16);
         if (s) return s;
     }
     return a.klen < b.klen ? -1 : (a.klen > b.klen ? 1 : 0);
@@ -118,16 +103,21 @@ __global__ void k_sort_load(uint64_t R, const uint64_t* __restrict__ hi, const u
     E[i] = e;
 }
 
-// the record arrays in sorted order (meta follows its record)
+// The record arrays in sorted order (meta follows its record). The merge stage then compares
+// dense key ranks (hi = rank of the key among the distinct keys, lo = 0, compare length 0): the
+// same order and the same equal-key groups as the key bytes, with no key bytes read again.
 __global__ void k_sort_store(uint64_t R, const SElem* __restrict__ E, const uint32_t* __restrict__ meta_in,
-                             uint64_t* hi, uint64_t* lo, uint64_t* addr, uint32_t* klen, uint32_t* meta) {
+                             const uint64_t* __restrict__ newkey, const uint64_t* __restrict__ newkey_ex,
+                             uint64_t* hi, uint64_t* lo, uint64_t* addr, uint32_t* klen, uint32_t* cmp_klen,
+                             uint32_t* meta) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= R) return;
     const SElem e = E[i];
-    hi[i] = e.hi;
-    lo[i] = e.lo;
+    hi[i] = newkey_ex[i] + newkey[i] - 1;
+    lo[i] = 0;
     addr[i] = e.addr;
     klen[i] = e.klen;
+    cmp_klen[i] = 0;
     meta[i] = meta_in[e.pos];
 }
 
@@ -145,17 +135,66 @@ __global__ void k_sort_prefix(const SElem* __restrict__ Ss, uint64_t ov, uint64_
     L[b] = (b == 0 || b + 1 == Tb) ? 0u : sk_common(Ss[b * ov - 1], Ss[(b + 1) * ov - 1]);
 }
 
+// A splitter for the bucket search: the 16-byte prefix plus key bytes 16..31 (big-endian, zero
+// padded), so keys of up to 32 bytes compare without touching the records again.
+struct SSplit {
+    uint64_t hi, lo, x0, x1;
+    uint64_t addr;
+    uint32_t klen, pad;
+};
+
+__device__ __forceinline__ void sk_ext(const uint8_t* key, uint32_t klen, uint64_t& x0, uint64_t& x1) {
+    x0 = x1 = 0;
+    if (klen <= 16) return;
+    const uint32_t m = klen - 16 < 16 ? klen - 16 : 16;
+    const uint4 v = load_window16(key + 16, m);
+    x0 = ((uint64_t)__builtin_bswap32(v.x & dword_mask(0, m, 0)) << 32) | __builtin_bswap32(v.y & dword_mask(0, m, 1));
+    x1 = ((uint64_t)__builtin_bswap32(v.z & dword_mask(0, m, 2)) << 32) | __builtin_bswap32(v.w & dword_mask(0, m, 3));
+}
+
+__global__ void k_sort_splitters(const SElem* __restrict__ Ss, uint64_t ov, uint64_t nsp, SSplit* sp) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nsp) return;
+    const SElem e = Ss[(b + 1) * ov - 1];
+    SSplit o;
+    o.hi = e.hi;
+    o.lo = e.lo;
+    sk_ext(sk_key(e), e.klen, o.x0, o.x1);
+    o.addr = e.addr;
+    o.klen = e.klen;
+    o.pad = 0;
+    sp[b] = o;
+}
+
+// splitter vs element key order (<0, 0, >0)
+__device__ __forceinline__ int sk_scmp(const SSplit& a, const SElem& b, uint64_t bx0, uint64_t bx1) {
+    if (a.hi != b.hi) return a.hi < b.hi ? -1 : 1;
+    if (a.lo != b.lo) return a.lo < b.lo ? -1 : 1;
+    if (a.klen > 16 && b.klen > 16) {
+        if (a.x0 != bx0) return a.x0 < bx0 ? -1 : 1;
+        if (a.x1 != bx1) return a.x1 < bx1 ? -1 : 1;
+        if (a.klen > 32 && b.klen > 32) {
+            const uint32_t n = a.klen < b.klen ? a.klen : b.klen;
+            const int s = bytes_cmp16((const uint8_t*)a.addr + 5 + 32, sk_key(b) + 32, n - 32);
+            if (s) return s;
+        }
+    }
+    return a.klen < b.klen ? -1 : (a.klen > b.klen ? 1 : 0);
+}
+
 // bucket of each element = the splitters whose key orders strictly before its key; slot by an
 // atomic count (the bucket sort restores a deterministic order)
-__global__ void k_sort_bucket(const SElem* __restrict__ E, uint64_t n, const SElem* __restrict__ Ss, uint64_t ov,
-                              uint64_t nsp, unsigned long long* cnt, uint64_t* bs) {
+__global__ void k_sort_bucket(const SElem* __restrict__ E, uint64_t n, const SSplit* __restrict__ sp, uint64_t nsp,
+                              unsigned long long* cnt, uint64_t* bs) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const SElem x = E[i];
+    uint64_t x0, x1;
+    sk_ext(sk_key(x), x.klen, x0, x1);
     uint64_t a = 0, b = nsp;
     while (a < b) {
         const uint64_t mid = (a + b) >> 1;
-        if (sk_kcmp(Ss[(mid + 1) * ov - 1], x) < 0) a = mid + 1;
+        if (sk_scmp(sp[mid], x, x0, x1) < 0) a = mid + 1;
         else b = mid;
     }
     const uint64_t slot = atomicAdd(cnt + a, 1ull);
@@ -182,7 +221,7 @@ __device__ __forceinline__ bool sk_wless(const SKey& a, const SKey& b, const SEl
     if (a.wl != b.wl) return a.wl < b.wl;
     if (a.klen > L + 16 && b.klen > L + 16) {
         const uint32_t nmin = a.klen < b.klen ? a.klen : b.klen;
-        const int s = sk_bytes_cmp(sk_key(bk[ia]) + L + 16, sk_key(bk[ib]) + L + 16, nmin - L - 16);
+        const int s = bytes_cmp16(sk_key(bk[ia]) + L + 16, sk_key(bk[ib]) + L + 16, nmin - L - 16);
         if (s) return s < 0;
     }
     if (a.klen != b.klen) return a.klen < b.klen;
@@ -194,7 +233,7 @@ __device__ __forceinline__ bool sk_wless(const SKey& a, const SKey& b, const SEl
 // so padding past n acts as +inf and is never touched.
 __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uint64_t* __restrict__ start,
                                                             const uint32_t* __restrict__ Lb, uint64_t Tb,
-                                                            SElem* out) {
+                                                            SElem* out, uint64_t* newkey) {
     __shared__ SKey key[SORT_CAP];
     __shared__ uint16_t id[SORT_CAP];
     const uint64_t b = blockIdx.x;
@@ -223,7 +262,10 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
                 __syncthreads();
             }
         }
-        for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) out[s0 + i] = bk[i];
+        for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+            out[s0 + i] = bk[i];
+            if (newkey) newkey[s0 + i] = (i == 0 || sk_kcmp(bk[i - 1], bk[i]) != 0) ? 1 : 0;
+        }
         return;
     }
     const uint32_t n32 = (uint32_t)n;
@@ -260,7 +302,19 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
             __syncthreads();
         }
     }
-    for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) out[s0 + i] = bk[id[i]];
+    for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
+        out[s0 + i] = bk[id[i]];
+        if (newkey) {  // a key differing from its predecessor's (buckets never share a key)
+            bool nk = i == 0;
+            if (!nk) {
+                const SKey a = key[i - 1], c = key[i];
+                nk = a.wh != c.wh || a.wl != c.wl || a.klen != c.klen;
+                if (!nk && c.klen > L + 16)
+                    nk = bytes_cmp16(sk_key(bk[id[i - 1]]) + L + 16, sk_key(bk[id[i]]) + L + 16, c.klen - L - 16) != 0;
+            }
+            newkey[s0 + i] = nk ? 1 : 0;
+        }
+    }
 }
 
 static inline unsigned sk_blocks(uint64_t n) { return (unsigned)((n + 255) / 256); }
@@ -269,9 +323,10 @@ void launch_sort_load(hipStream_t s, uint64_t R, const uint64_t* hi, const uint6
                       const uint32_t* klen, SElem* E) {
     if (R) k_sort_load<<<sk_blocks(R), 256, 0, s>>>(R, hi, lo, addr, klen, E);
 }
-void launch_sort_store(hipStream_t s, uint64_t R, const SElem* E, const uint32_t* meta_in, uint64_t* hi, uint64_t* lo,
-                       uint64_t* addr, uint32_t* klen, uint32_t* meta) {
-    if (R) k_sort_store<<<sk_blocks(R), 256, 0, s>>>(R, E, meta_in, hi, lo, addr, klen, meta);
+void launch_sort_store(hipStream_t s, uint64_t R, const SElem* E, const uint32_t* meta_in, const uint64_t* newkey,
+                       const uint64_t* newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr, uint32_t* klen,
+                       uint32_t* cmp_klen, uint32_t* meta) {
+    if (R) k_sort_store<<<sk_blocks(R), 256, 0, s>>>(R, E, meta_in, newkey, newkey_ex, hi, lo, addr, klen, cmp_klen, meta);
 }
 void launch_sort_sample(hipStream_t s, const SElem* E, uint64_t n, uint64_t Ns, SElem* S) {
     if (Ns) k_sort_sample<<<sk_blocks(Ns), 256, 0, s>>>(E, n, Ns, S);
@@ -280,15 +335,19 @@ void launch_sort_prefix(hipStream_t s, const SElem* Ss, uint64_t ov, uint64_t Tb
     if (Tb) k_sort_prefix<<<sk_blocks(Tb), 256, 0, s>>>(Ss, ov, Tb, L);
 }
 void launch_sort_bucket(hipStream_t s, const SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
-                        uint64_t* cnt, uint64_t* bs) {
-    if (n) k_sort_bucket<<<sk_blocks(n), 256, 0, s>>>(E, n, Ss, ov, nsp, (unsigned long long*)cnt, bs);
+                        void* split_buf, uint64_t* cnt, uint64_t* bs) {
+    SSplit* sp = (SSplit*)split_buf;
+    if (nsp) k_sort_splitters<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, sp);
+    if (n) k_sort_bucket<<<sk_blocks(n), 256, 0, s>>>(E, n, sp, nsp, (unsigned long long*)cnt, bs);
 }
+size_t sort_split_bytes(uint64_t nsp) { return (size_t)(nsp + 1) * sizeof(SSplit); }
 void launch_sort_scatter(hipStream_t s, const SElem* E, uint64_t n, const uint64_t* bs, const uint64_t* start,
                          SElem* out) {
     if (n) k_sort_scatter<<<sk_blocks(n), 256, 0, s>>>(E, n, bs, start, out);
 }
-void launch_sort_tile(hipStream_t s, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out) {
-    if (Tb) k_sort_tile<<<(unsigned)Tb, SORT_THREADS, 0, s>>>(in, start, L, Tb, out);
+void launch_sort_tile(hipStream_t s, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out,
+                      uint64_t* newkey) {
+    if (Tb) k_sort_tile<<<(unsigned)Tb, SORT_THREADS, 0, s>>>(in, start, L, Tb, out, newkey);
 }
 
 }  // namespace skv

@@ -56,7 +56,7 @@ __device__ __forceinline__ uint32_t id_prefix_len(int64_t id) {
 __global__ void k_wal_keys(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ m_src,
                            const uint32_t* __restrict__ m_rec, const uint32_t* __restrict__ rec_klen,
                            const uint64_t* __restrict__ P, int64_t* tid, uint32_t* strip, uint64_t* wsize,
-                           unsigned long long* first_err) {
+                           uint8_t* canon, unsigned long long* first_err) {
     const uint64_t K = *Kp;
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= K) return;
@@ -71,32 +71,33 @@ __global__ void k_wal_keys(const uint64_t* __restrict__ Kp, const uint64_t* __re
     else st = id_prefix_len(id);
     tid[j] = id;
     strip[j] = st;
+    canon[j] = (!e && dot + 1 == st) ? 1 : 0;  // the prefix is format!("{id}.") itself
     wsize[j] = (P[j + 1] - P[j]) - st;
 }
 
 // stripped key of record j: bytes [src+5+strip, src+5+klen)
 __device__ __forceinline__ int stripped_cmp(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
     const uint64_t n = la < lb ? la : lb;
-    for (uint64_t i = 0; i < n; ++i) {
-        uint32_t x = a[i], y = b[i];
-        if (x != y) return x < y ? -1 : 1;
-    }
+    const int c = bytes_cmp16(a, b, n);
+    if (c) return c;
     return la < lb ? -1 : (la > lb ? 1 : 0);
 }
 
 // table starts (a change of table id, :82-86) and build_runs' order check between neighbours of
-// one table on the stripped keys (runs.rs:190-198)
+// one table on the stripped keys (runs.rs:190-198). Two neighbours whose prefixes are both the
+// canonical "{id}." text of the same id share that prefix, so their stripped keys order like the
+// merged keys (strictly ascending): only non-canonical prefixes ("007.", "+5.") compare bytes.
 __global__ void k_wal_flags(const uint64_t* __restrict__ Kp, const int64_t* __restrict__ tid,
-                            const uint32_t* __restrict__ strip, const uint64_t* __restrict__ m_src,
-                            const uint32_t* __restrict__ m_rec, const uint32_t* __restrict__ rec_klen,
-                            uint64_t* is_new, uint32_t* bad) {
+                            const uint32_t* __restrict__ strip, const uint8_t* __restrict__ canon,
+                            const uint64_t* __restrict__ m_src, const uint32_t* __restrict__ m_rec,
+                            const uint32_t* __restrict__ rec_klen, uint64_t* is_new, uint32_t* bad) {
     const uint64_t K = *Kp;
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= K) return;
     const bool nw = j == 0 || tid[j] != tid[j - 1];
     is_new[j] = nw ? 1 : 0;
     uint32_t b = 0;
-    if (!nw) {
+    if (!nw && !(canon[j - 1] && canon[j])) {
         const uint64_t sa = strip[j - 1], sb = strip[j];
         const uint8_t* ka = (const uint8_t*)m_src[j - 1] + 5 + sa;
         const uint8_t* kb = (const uint8_t*)m_src[j] + 5 + sb;
@@ -158,48 +159,142 @@ __global__ void k_wal_desc(const uint64_t* __restrict__ NTp, const uint64_t* __r
     descs[keep_ex[t]] = d;
 }
 
-// output bytes of kept tables: version byte per run, then every record with its key_len rewritten
-// and the table prefix removed (WriteOperation::Put(key.split_off(..), value), :91-94). One
-// thread per record; records are small in WAL workloads (config 5: 49 bytes).
-__global__ void k_wal_gather(const uint64_t* __restrict__ Kp, const uint32_t* __restrict__ tix,
-                             const uint64_t* __restrict__ tstart, const uint64_t* __restrict__ keep,
-                             const uint64_t* __restrict__ run_off, const uint64_t* __restrict__ Pw,
-                             const uint32_t* __restrict__ strip, const uint64_t* __restrict__ m_src,
-                             const uint32_t* __restrict__ m_rec, const uint32_t* __restrict__ rec_klen,
-                             uint8_t* out) {
+// Output bytes of kept tables: a version byte per run, then every record with its key_len
+// rewritten and the table prefix removed (WriteOperation::Put(key.split_off(..), value), :91-94).
+// One workgroup per WAL_G merged records: the kept ones' output pieces (a synthesized head of
+// [version byte,] marker, key_len and the source body after the prefix) go to LDS; the
+// workgroup's output span is contiguous (kept tables are), and each lane then composes whole
+// 16-byte output blocks from the pieces (bytewise only at the span's two edges).
+constexpr int WAL_G = 256;
+
+__device__ __forceinline__ void or_byte(uint4& v, uint32_t pos, uint32_t byte) {
+    const uint32_t w = byte << (8 * (pos & 3));
+    const uint32_t q = pos >> 2;
+    if (q == 0) v.x |= w;
+    else if (q == 1) v.y |= w;
+    else if (q == 2) v.z |= w;
+    else v.w |= w;
+}
+
+// bytes [x0, x1) of output block B, starting inside kept record r
+__device__ uint4 wal_compose(uint64_t B, uint64_t x0, uint64_t x1, uint32_t r, const uint64_t* os,
+                             const uint64_t* src, const uint64_t* head, const uint32_t* hl) {
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    uint64_t x = x0;
+    while (x < x1) {
+        const uint64_t rel = x - os[r];
+        const uint64_t rlen = os[r + 1] - os[r];
+        uint64_t m;
+        if (rel < hl[r]) {  // synthesized head bytes
+            m = hl[r] - rel;
+            if (m > x1 - x) m = x1 - x;
+            for (uint64_t k = 0; k < m; ++k)
+                or_byte(acc, (uint32_t)(x - B + k), (uint32_t)(head[r] >> (8 * (rel + k))) & 0xFFu);
+        } else {
+            m = rlen - rel;
+            if (m > x1 - x) m = x1 - x;
+            const uint32_t a = (uint32_t)(x - B), e = a + (uint32_t)m;
+            uint4 w = load_window16((const uint8_t*)src[r] + (rel - hl[r]), (uint32_t)m);
+            w = shl_bytes(w, a);
+            acc.x |= w.x & dword_mask(a, e, 0);
+            acc.y |= w.y & dword_mask(a, e, 1);
+            acc.z |= w.z & dword_mask(a, e, 2);
+            acc.w |= w.w & dword_mask(a, e, 3);
+        }
+        x += m;
+        if (x - os[r] == rlen) ++r;
+    }
+    return acc;
+}
+
+__global__ void __launch_bounds__(WAL_G) k_wal_gather(const uint64_t* __restrict__ Kp, const uint32_t* __restrict__ tix,
+                                                      const uint64_t* __restrict__ tstart,
+                                                      const uint64_t* __restrict__ keep,
+                                                      const uint64_t* __restrict__ run_off,
+                                                      const uint64_t* __restrict__ Pw,
+                                                      const uint32_t* __restrict__ strip,
+                                                      const uint64_t* __restrict__ m_src,
+                                                      const uint32_t* __restrict__ m_rec,
+                                                      const uint32_t* __restrict__ rec_klen, uint8_t* out) {
+    __shared__ uint64_t os[WAL_G + 1], src[WAL_G], head[WAL_G];
+    __shared__ uint32_t hl[WAL_G];
+    __shared__ uint32_t s_cnt[WAL_G / 64 + 1];
     const uint64_t K = *Kp;
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= K) return;
-    const uint32_t t = tix[j];
-    if (!keep[t]) return;
-    const uint64_t b = tstart[t];
-    uint8_t* o = out + run_off[t];
-    if (j == b) o[0] = 1;  // CURRENT_VERSION (runs.rs:241-246)
-    o += 1 + (Pw[j] - Pw[b]);
-    const uint8_t* src = (const uint8_t*)m_src[j];
-    const uint32_t st = strip[j];
-    const uint32_t nk = rec_klen[m_rec[j]] - st;
-    o[0] = src[0];
-    o[1] = (uint8_t)(nk >> 24);
-    o[2] = (uint8_t)(nk >> 16);
-    o[3] = (uint8_t)(nk >> 8);
-    o[4] = (uint8_t)nk;
-    const uint64_t rest = (Pw[j + 1] - Pw[j]) - 5;  // stripped key + value part
-    const uint8_t* s = src + 5 + st;
-    for (uint64_t i = 0; i < rest; ++i) o[5 + i] = s[i];
+    const uint64_t j0 = (uint64_t)blockIdx.x * WAL_G;
+    if (j0 >= K) return;
+    const uint64_t j = j0 + threadIdx.x;
+    bool kept = false;
+    uint64_t ostart = 0, olen = 0, body = 0, hd = 0;
+    uint32_t hlen = 0;
+    if (j < K) {
+        const uint32_t t = tix[j];
+        kept = keep[t] != 0;
+        if (kept) {
+            const uint64_t b = tstart[t];
+            const uint8_t* sp = (const uint8_t*)m_src[j];
+            const uint32_t st = strip[j];
+            const uint32_t nk = rec_klen[m_rec[j]] - st;
+            const bool first = j == b;
+            ostart = run_off[t] + 1 + (Pw[j] - Pw[b]) - (first ? 1 : 0);
+            olen = (Pw[j + 1] - Pw[j]) + (first ? 1 : 0);
+            body = (uint64_t)sp + 5 + st;
+            const uint64_t h5 = (uint64_t)sp[0] | ((uint64_t)(nk >> 24) << 8) | ((uint64_t)((nk >> 16) & 0xFF) << 16) |
+                                ((uint64_t)((nk >> 8) & 0xFF) << 24) | ((uint64_t)(nk & 0xFF) << 32);
+            hd = first ? (1ull | (h5 << 8)) : h5;  // CURRENT_VERSION (runs.rs:241-246), marker, key_len
+            hlen = first ? 6u : 5u;
+        }
+    }
+    // compact the kept records (merged order) into the piece table
+    const uint64_t bal = __ballot(kept);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) s_cnt[wv] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t before = 0, c = 0;
+    for (int w = 0; w < WAL_G / 64; ++w) {
+        if (w < wv) before += s_cnt[w];
+        c += s_cnt[w];
+    }
+    if (kept) {
+        const uint32_t i = before + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+        os[i] = ostart;
+        src[i] = body;
+        head[i] = hd;
+        hl[i] = hlen;
+        if (i + 1 == c) os[c] = ostart + olen;
+    }
+    __syncthreads();
+    if (c == 0) return;
+    const uint64_t lo = os[0], hi = os[c];
+    const uint64_t Blo = lo & ~15ull, Bhi = (hi + 15) & ~15ull;
+    for (uint64_t B = Blo + 16ull * threadIdx.x; B < Bhi; B += 16ull * WAL_G) {
+        const uint64_t x0 = B > lo ? B : lo, x1 = B + 16 < hi ? B + 16 : hi;
+        uint32_t a = 0, bb = c;  // last record with os <= x0
+        while (bb - a > 1) {
+            const uint32_t mid = (a + bb) >> 1;
+            if (os[mid] <= x0) a = mid;
+            else bb = mid;
+        }
+        const uint4 v = wal_compose(B, x0, x1, a, os, src, head, hl);
+        if (x0 == B && x1 == B + 16) {
+            *(uint4*)(out + B) = v;
+        } else {  // span edge: this workgroup's bytes only
+            for (uint64_t y = x0; y < x1; ++y) out[y] = (uint8_t)byte_of(v, (uint32_t)(y - B));
+        }
+    }
 }
 
 void launch_wal_keys(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint32_t* m_rec,
                      const uint32_t* rec_klen, const uint64_t* P, int64_t* tid, uint32_t* strip, uint64_t* wsize,
-                     unsigned long long* first_err) {
+                     uint8_t* canon, unsigned long long* first_err) {
     if (max_K)
-        k_wal_keys<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, m_src, m_rec, rec_klen, P, tid, strip, wsize, first_err);
+        k_wal_keys<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, m_src, m_rec, rec_klen, P, tid, strip, wsize, canon,
+                                                          first_err);
 }
 void launch_wal_flags(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const int64_t* tid, const uint32_t* strip,
-                      const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen, uint64_t* is_new,
-                      uint32_t* bad) {
+                      const uint8_t* canon, const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen,
+                      uint64_t* is_new, uint32_t* bad) {
     if (max_K)
-        k_wal_flags<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, tid, strip, m_src, m_rec, rec_klen, is_new, bad);
+        k_wal_flags<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, tid, strip, canon, m_src, m_rec, rec_klen, is_new, bad);
 }
 void launch_wal_index(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* is_new, const uint64_t* new_ex,
                       const uint32_t* bad, uint32_t* tix, uint64_t* tstart, uint32_t* tbad) {
@@ -221,8 +316,8 @@ void launch_wal_gather(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const 
                        const uint64_t* keep, const uint64_t* run_off, const uint64_t* Pw, const uint32_t* strip,
                        const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen, uint8_t* out) {
     if (max_K)
-        k_wal_gather<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, tix, tstart, keep, run_off, Pw, strip, m_src, m_rec,
-                                                            rec_klen, out);
+        k_wal_gather<<<wal_blocks(max_K, WAL_G), WAL_G, 0, s>>>(Kp, tix, tstart, keep, run_off, Pw, strip, m_src,
+                                                                m_rec, rec_klen, out);
 }
 
 }  // namespace skv

@@ -146,10 +146,10 @@ class Compactor:
             self.lib.skv_result_free(res)
         return (runs, info) if with_info else runs
 
-    def compact_dev(self, streams: Sequence[Tuple[int, Sequence[Tuple[int, int]]]],
-                    max_run_size: int = MAX_RUN_SIZE, flags: int = 0) -> DeviceResult:
-        """streams: [(seq_no, [(device_ptr, length), ...])] with inputs resident in HBM."""
-        sa = StreamArgs(streams, device=True)
+    def compact_dev(self, streams, max_run_size: int = MAX_RUN_SIZE, flags: int = 0) -> DeviceResult:
+        """streams: [(seq_no, [(device_ptr, length), ...])] with inputs resident in HBM, or a
+        StreamArgs(..., device=True) built once and reused (the caller's skv_stream[] table)."""
+        sa = streams if isinstance(streams, StreamArgs) else StreamArgs(streams, device=True)
         res = C.POINTER(SkvResult)()
         rc = self.lib.skv_compact_dev(self.ctx, sa.ptr, sa.n, max_run_size, flags, C.byref(res))
         if rc != SKV_OK:
