@@ -129,7 +129,8 @@ typedef struct {
     uint64_t hot_read_bytes;
     uint64_t hot_write_bytes;
     uint32_t sorted;         /* 1: merge fan-in above 1536 streams took the record sort (one list) */
-    uint32_t reserved;
+    uint32_t fp_rerun;       /* 1: the merge's key-fingerprint shortcut misordered a tile and the
+                                call was rerun with exact key compares (a 64-bit collision) */
 } skv_timings;
 
 /* skv_timings.path */

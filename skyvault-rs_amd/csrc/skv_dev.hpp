@@ -109,6 +109,11 @@ struct TileOut {
     uint64_t* Kout;       // K = surviving records
     uint64_t T;           // level-0 tile count
     uint64_t* prof;       // SKV_TILE_PROF builds: per-phase time of level-0 tiles (8 counters)
+    // level 0: fingerprints of the key bytes past 16 (k_key_fp); equal prefix, length and
+    // fingerprint count as equal inside the merge rounds, every adjacent pair of the result is then
+    // compared exactly and a misorder sets *fp_bad (the host reruns with exact compares)
+    const uint64_t* key_fp;
+    uint32_t* fp_bad;
     // global scratch for tiles larger than TILE_CAP
     uint64_t* xhi;
     uint64_t* xlo;
@@ -427,13 +432,27 @@ __device__ __forceinline__ bool ascii_prefix(const uint32_t kd[7], uint32_t n /*
     return (acc & 0x80808080u) == 0;
 }
 
-// UTF-8 validity with an all-ASCII vector fast path (16 bytes per step)
+// UTF-8 validity with an all-ASCII vector fast path: the aligned 16-byte blocks of the key are
+// loaded 4 at a time with no dependence between them (one memory round trip per 64 bytes), their
+// bytes past the key masked off; any high bit falls back to the exact scalar check.
 __device__ inline bool utf8_valid_fast(const uint8_t* s, uint64_t n) {
-    for (uint64_t i = 0; i < n; i += 16) {
-        uint32_t m = (uint32_t)(n - i < 16 ? n - i : 16);
-        uint4 v = load_window16(s + i, m);
-        uint32_t acc = (v.x & dword_mask(0, m, 0)) | (v.y & dword_mask(0, m, 1)) | (v.z & dword_mask(0, m, 2)) |
-                       (v.w & dword_mask(0, m, 3));
+    if (n == 0) return true;
+    const uintptr_t a0 = (uintptr_t)s, a1 = a0 + n;  // bytes [a0, a1)
+    const uintptr_t b0 = a0 & ~(uintptr_t)15, b1 = (a1 + 15) & ~(uintptr_t)15;
+    for (uintptr_t b = b0; b < b1; b += 64) {
+        uint4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = b + 16 * q < b1 ? *(const uint4*)(b + 16 * q) : make_uint4(0, 0, 0, 0);
+        uint32_t acc = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uintptr_t blk = b + 16 * q;
+            const uint32_t lo = a0 > blk ? (uint32_t)(a0 - blk) : 0u;
+            const uint32_t hi = a1 < blk + 16 ? (uint32_t)(a1 - blk) : 16u;
+            if (blk < b1 && lo < hi)
+                acc |= (v[q].x & dword_mask(lo, hi, 0)) | (v[q].y & dword_mask(lo, hi, 1)) |
+                       (v[q].z & dword_mask(lo, hi, 2)) | (v[q].w & dword_mask(lo, hi, 3));
+        }
         if (acc & 0x80808080u) return utf8_valid(s, n);
     }
     return true;

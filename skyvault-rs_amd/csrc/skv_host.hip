@@ -85,6 +85,7 @@ struct skv_ctx {
     size_t up_chunk = 0, up_off = 0;
     uint64_t syncs = 0;
     double sync_ms = 0;
+    bool exact_keys = false;  // rerun after a fingerprint shortcut misordered a tile (never in practice)
 };
 
 struct ResultBox {  // skv_result + how to free it
@@ -261,18 +262,37 @@ static std::string wal_key_error(const std::string& key) {
     return "Invalid input: Invalid table ID '" + pre + "': " + why;
 }
 
+constexpr int RC_RETRY_EXACT = -100;  // internal: the merge's fingerprint shortcut misordered a tile
+static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_deferred);
+// the whole call again with exact key compares in the merge rounds
+static int rerun_exact(skv_ctx* ctx, const Job& job, skv_result** out) {
+    ctx->exact_keys = true;
+    int rc;
+    try {
+        rc = compact_device(ctx, job, out, false);
+    } catch (...) {
+        ctx->exact_keys = false;
+        throw;
+    }
+    ctx->exact_keys = false;
+    ctx->timings.fp_rerun = 1;
+    return rc;
+}
+
 // SKV_SPLIT_BY_TABLE after the merge: table split, prefix strip, one run per kept table
 // (skv_wal.hip). One extra host sync reads the surviving record count first.
 static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, const uint32_t* m_rec,
                      const uint64_t* m_src, const uint64_t* m_P, const uint64_t* m_Dp, const uint64_t* rec_addr,
-                     const uint32_t* rec_klen, skv_result** out) {
+                     const uint32_t* rec_klen, const uint32_t* fp_bad, skv_result** out) {
     hipStream_t st = ctx->stream;
     uint64_t K = 0;
     {
         uint64_t* hp = (uint64_t*)pinned(ctx, 64);
         d2h(ctx, hp, d_K, 8);
+        d2h(ctx, hp + 1, fp_bad, 4);
         sync(ctx);
         K = hp[0];
+        if ((uint32_t)hp[1]) return RC_RETRY_EXACT;
     }
     (void)R;
     int64_t* tid = dbuf<int64_t>(ctx, "w_tid", K + 1);
@@ -640,7 +660,7 @@ static void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo,
 // allow_deferred: on the fixed-stride fast path, launch the merge without waiting for the parse's
 // verdict (broken runs / order errors / oversized records) and check it with the final readback;
 // a bad verdict discards the result and reruns the call on the exact general path.
-static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_deferred = true) {
+static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_deferred) {
     hipStream_t st = ctx->stream;
     ctx->syncs = 0;
     ctx->up_chunk = 0;
@@ -972,6 +992,18 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     uint64_t* m_Dp = dbuf<uint64_t>(ctx, "m_Dp", R + 1);
     uint64_t* d_Kout = dbuf<uint64_t>(ctx, "K_out", 1);
     uint32_t* tile_max = nullptr;
+    // fingerprints of the key bytes past 16 for the level-0 merge rounds (SKV_FP_TEST=1: all zero,
+    // so every same-length key pair with one prefix is taken as equal and the exact check must catch it)
+    const uint64_t* key_fp = nullptr;
+    uint32_t* fp_bad = dbuf<uint32_t>(ctx, "fp_bad", 1);
+    HIPCHK(hipMemsetAsync(fp_bad, 0, 4, st));
+    if (km > 1 && !ctx->exact_keys) {
+        uint64_t* f = dbuf<uint64_t>(ctx, "rec_fp", R);
+        const char* te = getenv("SKV_FP_TEST");
+        if (te && te[0] == '1') HIPCHK(hipMemsetAsync(f, 0, R * 8, st));
+        else launch_key_fp(st, R, rec_addr, rec_klen, f);
+        key_fp = f;
+    }
     for (int li = (int)lv.size() - 1; li >= 0; --li) {
         Level& L = lv[li];
         const bool l0 = li == 0;
@@ -1005,6 +1037,8 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             O.Kout = d_Kout;
             O.T = T;
             tile_max = O.tile_mm = dbuf<uint32_t>(ctx, "tile_mm", 2 * T);  // (min, max) record size per tile
+            O.key_fp = key_fp;
+            O.fp_bad = fp_bad;
             O.tstate = dbuf<uint64_t>(ctx, "tile_state", 3 * T);
             O.tcounter = dbuf<uint32_t>(ctx, "tile_ticket", 1);
             HIPCHK(hipMemsetAsync(O.tstate, 0, 3 * T * 8, st));
@@ -1028,7 +1062,11 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     HIPCHK(hipGetLastError());
     mark(ctx, PH_MERGE);
     const uint64_t* d_K = d_Kout;
-    if (job.flags & SKV_SPLIT_BY_TABLE) return wal_stage(ctx, job, R, d_K, m_rec, m_src, m_P, m_Dp, rec_addr, rec_klen, out);
+    if (job.flags & SKV_SPLIT_BY_TABLE) {
+        const int rc = wal_stage(ctx, job, R, d_K, m_rec, m_src, m_P, m_Dp, rec_addr, rec_klen, fp_bad, out);
+        if (rc == RC_RETRY_EXACT) return rerun_exact(ctx, job, out);
+        return rc;
+    }
     // ---- chain + stats ----------------------------------------------------------------------
     uint64_t* run_b = dbuf<uint64_t>(ctx, "run_b", R + 2);
     uint64_t* d_nruns = dbuf<uint64_t>(ctx, "n_runs", 4);  // {runs, K, P[K]} (k_chain)
@@ -1067,6 +1105,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         uint8_t* hp = (uint8_t*)pinned(ctx, 64 + guess * sizeof(DevRunDesc) + vbytes);
         uint8_t* hv = hp + 64 + guess * sizeof(DevRunDesc);
         d2h(ctx, hp, d_nruns, 24);
+        d2h(ctx, hp + 32, fp_bad, 4);
         d2h(ctx, hp + 64, d_desc, guess * sizeof(DevRunDesc));
         if (deferred) {
             d2h(ctx, hv, d_flags, 16);
@@ -1081,6 +1120,12 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
                 delete box;
                 return compact_device(ctx, job, out, false);
             }
+        }
+        uint32_t fpb = 0;
+        memcpy(&fpb, hp + 32, 4);
+        if (fpb) {
+            delete box;
+            return rerun_exact(ctx, job, out);
         }
         memcpy(h3, hp, 24);
         const uint64_t n = h3[0];
@@ -1169,7 +1214,7 @@ static int run_guarded(skv_ctx* ctx, const Job& job, skv_result** out, double t_
     try {
         ctx->sync_ms = 0;
         ctx->timings = skv_timings{};
-        const int rc = compact_device(ctx, job, out);
+        const int rc = compact_device(ctx, job, out, true);
         ctx->timings.host_total_ms = now_ms() - t_entry;
         ctx->timings.host_sync_ms = ctx->sync_ms;
         return rc;

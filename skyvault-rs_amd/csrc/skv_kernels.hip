@@ -114,11 +114,22 @@ __global__ void k_run_header(const RunInfo* runs, uint32_t n_runs, uint32_t* hdr
 // first position whose next three records decode cleanly. Wrong guesses are caught by
 // k_validate and repaired by k_fixup.
 __device__ uint64_t spec_start(const uint8_t* run, uint64_t len, uint64_t cs, uint64_t ce) {
-    for (uint64_t p = cs; p < ce; ++p) {
-        uint32_t m = run[p];
-        if (m != 1 && m != 2) continue;
-        WalkRes w = walk_fast(run, len, p, len, 3);
-        if (w.err == DERR_NONE) return p;
+    for (uint64_t p0 = cs; p0 < ce; p0 += 16) {  // 16 bytes per load; marker candidates as a mask
+        const uint32_t m = (uint32_t)(ce - p0 < 16 ? ce - p0 : 16);
+        const uint4 v = load_window16(run + p0, m);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t cand = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t b = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+            if ((b == 1u || b == 2u) && (uint32_t)i < m) cand |= 1u << i;
+        }
+        while (cand) {
+            const uint32_t i = __builtin_ctz(cand);
+            cand &= cand - 1;
+            WalkRes r = walk_fast(run, len, p0 + i, len, 3);
+            if (r.err == DERR_NONE) return p0 + i;
+        }
     }
     return NO_POS;
 }
@@ -480,7 +491,11 @@ __device__ __forceinline__ void load_elem(const Elems& E, uint64_t pos, uint64_t
     c = L0 ? (((uint64_t)E.klen[pos] << 32) | pos) : E.c[pos];
 }
 
+#ifndef SKV_DIAG_NOSUFFIX
+#define SKV_DIAG_NOSUFFIX 0  // diagnostic builds only (wrong order): skip key bytes past 16
+#endif
 __device__ __forceinline__ int suffix_cmp(const uint64_t* rec_addr, uint64_t ca, uint64_t cb) {
+    if (SKV_DIAG_NOSUFFIX) return 0;
     uint32_t la = (uint32_t)(ca >> 32), lb = (uint32_t)(cb >> 32);
     if (la > 16 && lb > 16) {
         const uint8_t* a = (const uint8_t*)rec_addr[(uint32_t)ca] + 5;
@@ -508,6 +523,55 @@ __device__ __forceinline__ bool elem_less(const uint64_t* rec_addr, uint64_t ha,
     int k = ekey_cmp(rec_addr, ha, la_, ca, hb, lb_, cb);
     if (k) return k < 0;
     return (uint32_t)ca < (uint32_t)cb;
+}
+
+// elem_less with a fingerprint shortcut (level-0 merge rounds): keys with equal prefix, length
+// and fingerprint of the bytes past 16 are taken as equal (no record bytes read); b's fingerprint
+// is in a register, a's read on demand. The tile verifies its result exactly afterwards.
+__device__ __forceinline__ bool elem_less_fp(const uint64_t* fp, const uint64_t* rec_addr, uint64_t ha, uint64_t la_,
+                                             uint64_t ca, uint64_t hb, uint64_t lb_, uint64_t cb, uint64_t fpb) {
+    if (ha != hb) return ha < hb;
+    if (la_ != lb_) return la_ < lb_;
+    const uint32_t la = (uint32_t)(ca >> 32), lb = (uint32_t)(cb >> 32);
+    if (la > 16 && lb > 16) {
+        if (!(fp && la == lb && fp[(uint32_t)ca] == fpb)) {
+            const int s = suffix_cmp(rec_addr, ca, cb);
+            if (s) return s < 0;
+        }
+    }
+    if (la != lb) return la < lb;
+    return (uint32_t)ca < (uint32_t)cb;
+}
+
+// 64-bit fingerprint of the key bytes past the 16-byte prefix (0 for keys of at most 16 bytes)
+__device__ inline uint64_t fp_mix(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+__global__ void k_key_fp(uint64_t R, const uint64_t* __restrict__ rec_addr, const uint32_t* __restrict__ rec_klen,
+                         uint64_t* fp) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R) return;
+    const uint32_t kl = rec_klen[i];
+    uint64_t h = 0;
+    if (kl > 16) {
+        const uint8_t* k = (const uint8_t*)rec_addr[i] + 5 + 16;
+        const uint32_t n = kl - 16;
+        h = 0x9E3779B97F4A7C15ull ^ n;
+        for (uint32_t o = 0; o < n; o += 16) {
+            const uint32_t m = n - o < 16 ? n - o : 16;
+            const uint4 v = load_window16(k + o, m);
+            const uint64_t w0 = ((uint64_t)(v.y & dword_mask(0, m, 1)) << 32) | (v.x & dword_mask(0, m, 0));
+            const uint64_t w1 = ((uint64_t)(v.w & dword_mask(0, m, 3)) << 32) | (v.z & dword_mask(0, m, 2));
+            h = fp_mix(h ^ w0);
+            h = fp_mix(h ^ w1 ^ 0x2545F4914F6CDD1Dull);
+        }
+    }
+    fp[i] = h;
 }
 
 // samples: every S-th element of each list
@@ -841,12 +905,13 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     // Thread owns elements e = threadIdx.x + u*TILE_THREADS; key, position and segment stay in
     // registers across the merge rounds, so each round is one binary search + one LDS write.
     constexpr int PER = TILE_CAP / TILE_THREADS;
-    uint64_t rh[PER], rl[PER], rc[PER], raddr[PER];
+    uint64_t rh[PER], rl[PER], rc[PER], raddr[PER], rfp[PER];
     uint32_t rpos[PER], rseg[PER], rmeta[PER];
+    const uint64_t* kfp = L0 ? O.key_fp : nullptr;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         uint32_t e = threadIdx.x + u * TILE_THREADS;
-        rh[u] = rl[u] = rc[u] = raddr[u] = 0;
+        rh[u] = rl[u] = rc[u] = raddr[u] = rfp[u] = 0;
         rpos[u] = e;
         rseg[u] = 0;
         rmeta[u] = 0;
@@ -857,6 +922,7 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
             if (L0) {
                 rmeta[u] = rec_meta[pos];
                 raddr[u] = rec_addr[pos];  // coalesced here, instead of a random gather later
+                if (kfp) rfp[u] = kfp[pos];
             }
             rseg[u] = j;
             el_lo[e] = rl[u];
@@ -901,7 +967,8 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                     bool less = xh < rh[u];
                     if (xh == rh[u]) {
                         const uint32_t x = mi[mid];
-                        less = elem_less(rec_addr, xh, el_lo[x], el_c[x], rh[u], rl[u], rc[u]);
+                        less = L0 ? elem_less_fp(kfp, rec_addr, xh, el_lo[x], el_c[x], rh[u], rl[u], rc[u], rfp[u])
+                                  : elem_less(rec_addr, xh, el_lo[x], el_c[x], rh[u], rl[u], rc[u]);
                     }
                     if (less) {
                         sb[u] = mid + 1;
@@ -951,9 +1018,11 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
             const uint32_t e = mi[i];
             const uint64_t h = mh[i], c = el_c[e];
             bool first = true;
-            if (i > 0 && mh[i - 1] == h) {
+            if (i > 0 && mh[i - 1] == h) {  // exact: first-per-key and the check of the fp shortcut
                 const uint32_t p = mi[i - 1];
-                first = ekey_cmp(rec_addr, h, el_lo[p], el_c[p], h, el_lo[e], c) != 0;
+                const int kc = ekey_cmp(rec_addr, h, el_lo[p], el_c[p], h, el_lo[e], c);
+                first = kc != 0;
+                if (O.fp_bad && (kc > 0 || (kc == 0 && (uint32_t)el_c[p] > (uint32_t)c))) atomicOr(O.fp_bad, 1u);
             }
             idx[q] = (uint32_t)c;
             if (first) keep_mask |= 1u << q;
@@ -1759,6 +1828,9 @@ void launch_bounds(hipStream_t s, bool l0, const uint64_t* hi, const uint64_t* l
     if (!n) return;
     if (l0) k_bounds<true><<<blocks_for(n, 256), 256, 0, s>>>(E, off, k, shi, slo, sc, m, T, rec_addr, bounds);
     else k_bounds<false><<<blocks_for(n, 256), 256, 0, s>>>(E, off, k, shi, slo, sc, m, T, rec_addr, bounds);
+}
+void launch_key_fp(hipStream_t s, uint64_t R, const uint64_t* rec_addr, const uint32_t* rec_klen, uint64_t* fp) {
+    if (R) k_key_fp<<<blocks_for(R, 256), 256, 0, s>>>(R, rec_addr, rec_klen, fp);
 }
 void launch_tile_n(hipStream_t s, const uint64_t* bounds, uint32_t k, uint64_t T, uint64_t* tile_n) {
     if (!T) return;

@@ -39,6 +39,7 @@ void launch_bounds(hipStream_t, bool l0, const uint64_t* hi, const uint64_t* lo,
                    const uint64_t* sc, uint64_t m, uint64_t T, const uint64_t* rec_addr, uint64_t* bounds,
                    const uint32_t* poison);
 void launch_tile_n(hipStream_t, const uint64_t* bounds, uint32_t k, uint64_t T, uint64_t* tile_n);
+void launch_key_fp(hipStream_t, uint64_t R, const uint64_t* rec_addr, const uint32_t* rec_klen, uint64_t* fp);
 size_t tile_lds_bytes(uint32_t k);
 hipError_t launch_tile(hipStream_t, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
                        const uint32_t* klen, const uint64_t* bounds, uint32_t k, uint64_t T, const uint64_t* tile_base,

@@ -97,7 +97,7 @@ class SkvTimings(C.Structure):
         ("hot_read_bytes", C.c_uint64),
         ("hot_write_bytes", C.c_uint64),
         ("sorted", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("fp_rerun", C.c_uint32),
     ]
 
 

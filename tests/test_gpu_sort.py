@@ -141,3 +141,45 @@ def test_fan_in_errors_surface_like_the_reference(dev):
     streams[777] = (streams[777][0], [bytes(bad)])
     exp, got = _run_both(dev, streams, 4 * MiB, 0)
     assert exp == got, _diff(exp, got)
+
+
+# ---- the level-0 merge's key-fingerprint shortcut (skv_kernels.hip elem_less_fp) -----------------
+
+def _prefix_keys_streams(n_streams=12, per=300, seed=11):
+    """Keys sharing their first 16 bytes, same length, distinct tails, spread over many streams:
+    under SKV_FP_TEST=1 (all fingerprints 0) the merge rounds take them as equal and misorder
+    them, which the exact adjacency check must catch."""
+    r = random.Random(seed)
+    streams = []
+    for s in range(n_streams):
+        ks = sorted({f"shared-prefix-16/{r.randrange(10**6):06d}" for _ in range(per)})
+        ops = [fmt.put(k, bytes([s])) for k in ks]
+        streams.append((s + 1, [fmt.encode_run(ops)]))
+    return streams
+
+
+def test_fp_shortcut_collisions_are_caught(dev, monkeypatch):
+    monkeypatch.setenv("SKV_FUSED", "0")
+    monkeypatch.setenv("SKV_FP_TEST", "1")
+    streams = _prefix_keys_streams()
+    _check(dev, streams, 1 << 16, 0, expect_sorted=False)
+    assert dev.timings()["fp_rerun"] == 1, "forced collisions were not detected"
+    _check(dev, streams, 1 << 16, _abi.SKV_DROP_TOMBSTONES, expect_sorted=False)
+
+
+def test_fp_shortcut_no_rerun_on_real_fingerprints(dev, monkeypatch):
+    monkeypatch.setenv("SKV_FUSED", "0")
+    for streams, mx, fl in ((_prefix_keys_streams(), 1 << 16, 0),
+                            (gen.config3(n_streams=32, run_bytes=64 * 1024, vsize=16), 1 << 18, 0),
+                            (gen.config3(n_streams=32, run_bytes=64 * 1024, vsize=16), 1 << 18, 1),
+                            (gen.config5(n_streams=64), 4 * MiB, 2)):
+        _check(dev, streams, mx, fl, expect_sorted=False)
+        assert dev.timings()["fp_rerun"] == 0
+
+
+def test_fp_shortcut_wal_collisions(dev, monkeypatch):
+    """WAL split after a merge whose fingerprints all collide (config-5 keys: one 16-byte prefix
+    per table): the WAL stage must see the rerun's exact merge."""
+    monkeypatch.setenv("SKV_FP_TEST", "1")
+    _check(dev, gen.config5(n_streams=40), 4 * MiB, _abi.SKV_SPLIT_BY_TABLE, expect_sorted=False)
+    assert dev.timings()["fp_rerun"] == 1
