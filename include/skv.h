@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SKV_ABI_VERSION 1
+#define SKV_ABI_VERSION 2  /* 2: skv_timings gained sorted, fp_rerun */
 
 typedef struct skv_ctx skv_ctx;
 
