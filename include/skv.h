@@ -167,6 +167,18 @@ int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams,
 int skv_compact_dev(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams,
                     uint64_t max_run_size, uint32_t flags, skv_result** out);
 
+/*
+ * Writer-side batch encode (replaces writer_service.rs:148-162 process_batch's BTreeMap + build_runs):
+ * ops_run holds the batch's WriteOperations in request order, serialized as one v1 run (unsorted,
+ * duplicates allowed). The result is build_runs(max_run_size) over the ops sorted by key with
+ * the LAST op of each key kept, exactly as the BTreeMap collection does. Decode errors of ops_run
+ * are reported like skv_compact's. skv_encode_batch_dev takes a device pointer.
+ */
+int skv_encode_batch(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_t max_run_size,
+                     skv_result** out);
+int skv_encode_batch_dev(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_t max_run_size,
+                         skv_result** out);
+
 void skv_result_free(skv_result* r);
 
 #ifdef __cplusplus

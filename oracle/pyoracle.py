@@ -193,3 +193,17 @@ def merge_ops(streams: Sequence[Tuple[int, Sequence[Op]]]):
             lib().skvo_op_list_free(out)
     err = None if rc == SKV_OK else RunError(rc, eb.value.decode("utf-8", "replace"))
     return ops, err
+
+
+def encode_batch(ops_run: bytes, max_run_size: int):
+    """writer_service.rs:148-162 (process_batch), restated: the batch's ops (decoded with the
+    oracle's read_run_stream, oracle/skv_oracle.c) collected into a BTreeMap keyed by key — a
+    later op replaces an earlier one of the same key — then build_runs over the map's values in
+    key order. Returns (runs) or raises like compact()."""
+    ops, err = decode_run(ops_run)
+    if err is not None:  # one stream: its decode error always surfaces (k_way.rs:134-137, :154-171)
+        raise err
+    latest = {}
+    for op in ops:
+        latest[op[1]] = op
+    return build_runs([latest[k] for k in sorted(latest)], max_run_size)

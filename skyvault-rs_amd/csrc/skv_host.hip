@@ -221,6 +221,7 @@ struct Job {
     uint64_t max_run_size = 0;
     uint32_t flags = 0;
     uint64_t in_bytes = 0;
+    bool batch = false;  // writer batch encode (skv_encode_batch): one unsorted run, last op per key wins
 };
 
 // a record's key bytes (host copy) for error-trigger comparisons
@@ -631,14 +632,14 @@ static SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth
 // tiles x streams). hi/lo/cmp_klen become dense key ranks for the merge stage; klen stays the real
 // key length (descriptors, WAL split).
 static void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo, uint64_t*& addr, uint32_t*& klen,
-                         uint32_t*& meta, const uint32_t*& cmp_klen) {
+                         uint32_t*& meta, const uint32_t*& cmp_klen, bool last_wins) {
     hipStream_t st = ctx->stream;
     SElem* E = dbuf<SElem>(ctx, "sort_e", R);
     SElem* T = dbuf<SElem>(ctx, "sort_t", R);
     uint64_t* newkey = dbuf<uint64_t>(ctx, "sort_newkey", R + 1);
     uint64_t* newkey_ex = dbuf<uint64_t>(ctx, "sort_newkey_ex", R + 1);
     uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "sort_rank_scan", scan_tmp_words(R) + 64);
-    launch_sort_load(st, R, hi, lo, addr, klen, E);
+    launch_sort_load(st, R, hi, lo, addr, klen, E, last_wins);
     const SElem* S = sort_elems(ctx, E, T, R, 0, newkey);
     launch_scan(st, newkey, R, newkey_ex, scan_tmp);
     uint64_t* nhi = dbuf<uint64_t>(ctx, "srt_hi", R);
@@ -647,7 +648,7 @@ static void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo,
     uint32_t* nklen = dbuf<uint32_t>(ctx, "srt_klen", R);
     uint32_t* ncklen = dbuf<uint32_t>(ctx, "srt_cklen", R);
     uint32_t* nmeta = dbuf<uint32_t>(ctx, "srt_meta", R);
-    launch_sort_store(st, R, S, meta, newkey, newkey_ex, nhi, nlo, naddr, nklen, ncklen, nmeta);
+    launch_sort_store(st, R, S, meta, newkey, newkey_ex, nhi, nlo, naddr, nklen, ncklen, nmeta, last_wins);
     HIPCHK(hipGetLastError());
     hi = nhi;
     lo = nlo;
@@ -760,7 +761,8 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     // order check + readback of its result, the record flags and (fast path) the broken-run flags
     auto check_and_read = [&](bool read_broken) -> bool {
         // the fast path's parse kernel already did the order check
-        if (!read_broken) launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
+        if (!read_broken && !job.batch)  // a writer batch is unsorted by definition
+            launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
         HIPCHK(hipGetLastError());
         uint8_t* hp = (uint8_t*)pinned(ctx, k * 8 + 16 + (read_broken ? n_runs * 4 : 0));
         d2h(ctx, hp, d_first_dec, (size_t)k * 8);
@@ -799,7 +801,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             for (uint32_t r = 1; r < n_runs && uniform; ++r) uniform = hf[r].S == hf[0].S && hf[r].K == hf[0].K;
             const RunFmt f0 = hf[0];
             const char* fenv = getenv("SKV_FUSED");
-            if (allow_deferred && uniform && !(job.flags & SKV_SPLIT_BY_TABLE) && !(fenv && fenv[0] == '0') &&
+            if (allow_deferred && uniform && !job.batch && !(job.flags & SKV_SPLIT_BY_TABLE) && !(fenv && fenv[0] == '0') &&
                 f0.K <= FX_MAX_K && f0.S >= FX_MIN_S && f0.S <= FX_MAX_S && k <= (uint32_t)TILE_TARGET / 2 &&
                 R < 0xFFFFFFFFull) {
                 if (compact_fused(ctx, job, runs, d_runs, stream_first_run, f0, recb, out)) return SKV_OK;
@@ -809,7 +811,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             alloc_records();
             h2d_up(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
             launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
-                               rec_meta, d_flags, d_stream_base, d_first_dec);
+                               rec_meta, d_flags, d_stream_base, job.batch ? nullptr : d_first_dec);
             mark(ctx, PH_PARSE);
             if (allow_deferred && !(job.flags & SKV_SPLIT_BY_TABLE)) {
                 deferred = true;  // verdict read with the result
@@ -945,8 +947,8 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     uint64_t* d_list_off = d_stream_base;
     {
         const char* se = getenv("SKV_SORT");
-        if ((k > (uint32_t)TILE_TARGET / 2 && R > (uint64_t)TILE_CAP) || (se && se[0] == '1')) {
-            sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen);
+        if ((k > (uint32_t)TILE_TARGET / 2 && R > (uint64_t)TILE_CAP) || (se && se[0] == '1') || job.batch) {
+            sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen, job.batch);
             km = 1;
             list_off = {0, R};
             d_list_off = dbuf<uint64_t>(ctx, "sorted_off", 2);
@@ -1307,15 +1309,11 @@ int skv_compact_dev(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams,
     return run_guarded(ctx, job, out, t_entry);
 }
 
-int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uint64_t max_run_size, uint32_t flags,
-                skv_result** out) {
-    const double t_entry = now_ms();
-    if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
-    *out = nullptr;
-    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
-    Job job;
-    int rc = build_job(ctx, streams, n_streams, max_run_size, flags, job);
-    if (rc) return rc;
+}  // extern "C"
+
+// host inputs: stage them into HBM, compact, return the output bytes in pinned host memory
+static int compact_host_job(skv_ctx* ctx, Job& job, skv_result** out, double t_entry) {
+    int rc;
     try {
         // stage inputs into HBM (16-byte aligned per run)
         uint64_t total = 0;
@@ -1351,6 +1349,54 @@ int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uin
     box->pool_cap = cap;
     *out = dres;
     return SKV_OK;
+}
+
+// the one-run job of a writer batch (writer_service.rs:148-162)
+static int batch_job(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_t max_run_size, Job& job) {
+    if (len && !ops_run) return set_err(ctx, SKV_E_INVALID_ARG, "ops_run is NULL");
+    const uint8_t* runs[1] = {ops_run};
+    const uint64_t lens[1] = {len};
+    skv_stream st{runs, lens, 1u, 0};
+    const int rc = build_job(ctx, &st, 1, max_run_size, 0, job);
+    job.batch = true;
+    return rc;
+}
+
+extern "C" {
+
+int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uint64_t max_run_size, uint32_t flags,
+                skv_result** out) {
+    const double t_entry = now_ms();
+    if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
+    *out = nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    Job job;
+    int rc = build_job(ctx, streams, n_streams, max_run_size, flags, job);
+    if (rc) return rc;
+    return compact_host_job(ctx, job, out, t_entry);
+}
+
+int skv_encode_batch(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_t max_run_size, skv_result** out) {
+    const double t_entry = now_ms();
+    if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
+    *out = nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    Job job;
+    int rc = batch_job(ctx, ops_run, len, max_run_size, job);
+    if (rc) return rc;
+    return compact_host_job(ctx, job, out, t_entry);
+}
+
+int skv_encode_batch_dev(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_t max_run_size,
+                         skv_result** out) {
+    const double t_entry = now_ms();
+    if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
+    *out = nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    Job job;
+    int rc = batch_job(ctx, ops_run, len, max_run_size, job);
+    if (rc) return rc;
+    return run_guarded(ctx, job, out, t_entry);
 }
 
 void skv_result_free(skv_result* r) {

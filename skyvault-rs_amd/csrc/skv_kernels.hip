@@ -404,7 +404,7 @@ __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, 
         }
         if (act) put_rec(i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
     }
-    if (!VERIFY) return;
+    if (!VERIFY || !first_dec) return;  // (no order check for a writer batch)
     // fused order check (runs.rs:190-198 as k_order_check does it): compare with the previous
     // record of the same stream — the neighbouring lane's, or parsed here at a run / wave edge
     const int lane = threadIdx.x & 63;

@@ -84,10 +84,10 @@ hipError_t launch_fx_tile(hipStream_t, const FxArgs& A);
 void launch_fx_desc(hipStream_t, const FxArgs& A, DevRunDesc* descs, uint64_t* n_runs_out, uint64_t max_runs);
 // skv_sort.hip — record sort (fan-in above TILE_TARGET / 2)
 void launch_sort_load(hipStream_t, uint64_t R, const uint64_t* hi, const uint64_t* lo, const uint64_t* addr,
-                      const uint32_t* klen, SElem* E);
+                      const uint32_t* klen, SElem* E, bool last_wins);
 void launch_sort_store(hipStream_t, uint64_t R, const SElem* E, const uint32_t* meta_in, const uint64_t* newkey,
                        const uint64_t* newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr, uint32_t* klen,
-                       uint32_t* cmp_klen, uint32_t* meta);
+                       uint32_t* cmp_klen, uint32_t* meta, bool last_wins);
 void launch_sort_sample(hipStream_t, const SElem* E, uint64_t n, uint64_t Ns, SElem* S);
 void launch_sort_prefix(hipStream_t, const SElem* Ss, uint64_t ov, uint64_t Tb, uint32_t* L);
 void launch_sort_bucket(hipStream_t, const SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,

@@ -90,15 +90,18 @@ __device__ inline void sk_window(const SElem& e, uint32_t L, uint64_t& wh, uint6
 
 // ---------------------------------------------------------------------------------------------
 
+// pos is the tie-break: the record index (newer stream first), or for a writer batch the index
+// from the end (the last op of a key wins, BTreeMap insertion in writer_service.rs:153-157)
 __global__ void k_sort_load(uint64_t R, const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo,
-                            const uint64_t* __restrict__ addr, const uint32_t* __restrict__ klen, SElem* E) {
+                            const uint64_t* __restrict__ addr, const uint32_t* __restrict__ klen, SElem* E,
+                            bool last_wins) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= R) return;
     SElem e;
     e.hi = hi[i];
     e.lo = lo[i];
     e.addr = addr[i];
-    e.pos = (uint32_t)i;
+    e.pos = (uint32_t)(last_wins ? R - 1 - i : i);
     e.klen = klen[i];
     E[i] = e;
 }
@@ -109,16 +112,17 @@ __global__ void k_sort_load(uint64_t R, const uint64_t* __restrict__ hi, const u
 __global__ void k_sort_store(uint64_t R, const SElem* __restrict__ E, const uint32_t* __restrict__ meta_in,
                              const uint64_t* __restrict__ newkey, const uint64_t* __restrict__ newkey_ex,
                              uint64_t* hi, uint64_t* lo, uint64_t* addr, uint32_t* klen, uint32_t* cmp_klen,
-                             uint32_t* meta) {
+                             uint32_t* meta, bool last_wins) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= R) return;
     const SElem e = E[i];
+    const uint64_t src = last_wins ? R - 1 - e.pos : e.pos;
     hi[i] = newkey_ex[i] + newkey[i] - 1;
     lo[i] = 0;
     addr[i] = e.addr;
     klen[i] = e.klen;
     cmp_klen[i] = 0;
-    meta[i] = meta_in[e.pos];
+    meta[i] = meta_in[src];
 }
 
 // S[j] = E[j * n / Ns]  (n < 2^32)
@@ -320,13 +324,15 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
 static inline unsigned sk_blocks(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
 void launch_sort_load(hipStream_t s, uint64_t R, const uint64_t* hi, const uint64_t* lo, const uint64_t* addr,
-                      const uint32_t* klen, SElem* E) {
-    if (R) k_sort_load<<<sk_blocks(R), 256, 0, s>>>(R, hi, lo, addr, klen, E);
+                      const uint32_t* klen, SElem* E, bool last_wins) {
+    if (R) k_sort_load<<<sk_blocks(R), 256, 0, s>>>(R, hi, lo, addr, klen, E, last_wins);
 }
 void launch_sort_store(hipStream_t s, uint64_t R, const SElem* E, const uint32_t* meta_in, const uint64_t* newkey,
                        const uint64_t* newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr, uint32_t* klen,
-                       uint32_t* cmp_klen, uint32_t* meta) {
-    if (R) k_sort_store<<<sk_blocks(R), 256, 0, s>>>(R, E, meta_in, newkey, newkey_ex, hi, lo, addr, klen, cmp_klen, meta);
+                       uint32_t* cmp_klen, uint32_t* meta, bool last_wins) {
+    if (R)
+        k_sort_store<<<sk_blocks(R), 256, 0, s>>>(R, E, meta_in, newkey, newkey_ex, hi, lo, addr, klen, cmp_klen, meta,
+                                                  last_wins);
 }
 void launch_sort_sample(hipStream_t s, const SElem* E, uint64_t n, uint64_t Ns, SElem* S) {
     if (Ns) k_sort_sample<<<sk_blocks(Ns), 256, 0, s>>>(E, n, Ns, S);

@@ -117,6 +117,8 @@ EXPORTED_SYMBOLS = [
     "skv_ctx_get_timings",
     "skv_compact",
     "skv_compact_dev",
+    "skv_encode_batch",
+    "skv_encode_batch_dev",
     "skv_result_free",
 ]
 

@@ -57,6 +57,9 @@ def load():
     for fn in (l.skv_compact, l.skv_compact_dev):
         fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.POINTER(C.POINTER(SkvResult))]
         fn.restype = C.c_int
+    for fn in (l.skv_encode_batch, l.skv_encode_batch_dev):
+        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.POINTER(SkvResult))]
+        fn.restype = C.c_int
     l.skv_result_free.argtypes = [C.POINTER(SkvResult)]
     l.skv_result_free.restype = None
     _lib = l
@@ -168,6 +171,30 @@ class Compactor:
         n = (int(res.contents.n_bytes), int(res.contents.n_runs))
         self.lib.skv_result_free(res)
         return n
+
+    def encode_batch(self, ops_run: bytes, max_run_size: int = MAX_RUN_SIZE, with_info: bool = False):
+        """Writer batch encode (writer_service.rs:148-162): ops_run = the batch's ops in request
+        order as one v1 run; returns build_runs over the ops sorted by key, last op per key kept."""
+        buf = C.create_string_buffer(bytes(ops_run), max(1, len(ops_run)))
+        res = C.POINTER(SkvResult)()
+        rc = self.lib.skv_encode_batch(self.ctx, C.cast(buf, C.c_void_p), len(ops_run), max_run_size, C.byref(res))
+        if rc != SKV_OK:
+            raise self._err(rc)
+        try:
+            runs = result_to_runs(res.contents)
+            info = dict(in_bytes=res.contents.in_bytes, in_records=res.contents.in_records,
+                        out_records=res.contents.out_records)
+        finally:
+            self.lib.skv_result_free(res)
+        return (runs, info) if with_info else runs
+
+    def encode_batch_dev(self, ptr: int, length: int, max_run_size: int = MAX_RUN_SIZE) -> DeviceResult:
+        """skv_encode_batch_dev: the ops run already in HBM."""
+        res = C.POINTER(SkvResult)()
+        rc = self.lib.skv_encode_batch_dev(self.ctx, C.c_void_p(ptr), length, max_run_size, C.byref(res))
+        if rc != SKV_OK:
+            raise self._err(rc)
+        return DeviceResult(self.lib, res)
 
     def timings(self) -> dict:
         t = SkvTimings()
