@@ -179,6 +179,36 @@ int skv_encode_batch(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_
 int skv_encode_batch_dev(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_t max_run_size,
                          skv_result** out);
 
+/*
+ * Batched point lookups in one run: runs::search_run (runs.rs:285-398) for n_keys keys at once,
+ * the cache service's per-key scan (cache_service.rs:52-151). keys = the keys' bytes
+ * concatenated, key i = keys[key_offs[i] .. key_offs[i+1]). out[i] gets the key's outcome; a
+ * value is at run + val_off. Where search_run would panic for a key, out[i].kind =
+ * SKV_LOOKUP_PANIC and the call returns SKV_E_FORMAT with the panic text of the lowest such key
+ * ("Invalid marker byte: 7", "Incomplete key data", "Empty run data", ...); the other keys'
+ * outcomes are still filled in. run and keys are host memory.
+ */
+typedef struct {
+    uint32_t kind;     /* SKV_LOOKUP_* */
+    uint32_t panic;    /* SKV_LOOKUP_PANIC: which check (SKV_PANIC_*) | offending byte << 8 */
+    uint64_t val_off;  /* SKV_LOOKUP_FOUND: value bytes at run + val_off, val_len of them */
+    uint64_t val_len;
+} skv_lookup;
+enum { SKV_LOOKUP_NOT_FOUND = 0, SKV_LOOKUP_FOUND = 1, SKV_LOOKUP_TOMBSTONE = 2, SKV_LOOKUP_PANIC = 3 };
+enum {
+    SKV_PANIC_EMPTY = 1,           /* "Empty run data" */
+    SKV_PANIC_VERSION = 2,         /* "Unsupported version: {v}" */
+    SKV_PANIC_MARKER = 3,          /* "Invalid marker byte: {m}" */
+    SKV_PANIC_KEYLEN = 4,          /* "Incomplete key length data" */
+    SKV_PANIC_KEY = 5,             /* "Incomplete key data" */
+    SKV_PANIC_VALLEN = 6,          /* "Incomplete value length data" */
+    SKV_PANIC_VAL = 7,             /* "Incomplete value data" */
+    SKV_PANIC_VALLEN_FOUND = 8,    /* "Incomplete value length data for found key" */
+    SKV_PANIC_VAL_FOUND = 9        /* "Incomplete value data for found key" */
+};
+int skv_search_run(skv_ctx* ctx, const uint8_t* run, uint64_t len, const uint8_t* keys, const uint64_t* key_offs,
+                   uint32_t n_keys, skv_lookup* out);
+
 void skv_result_free(skv_result* r);
 
 #ifdef __cplusplus

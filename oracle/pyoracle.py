@@ -207,3 +207,50 @@ def encode_batch(ops_run: bytes, max_run_size: int):
     for op in ops:
         latest[op[1]] = op
     return build_runs([latest[k] for k in sorted(latest)], max_run_size)
+
+
+def search_run(run: bytes, key: bytes):
+    """runs::search_run (runs.rs:285-398), restated literally (test infrastructure): scan from the
+    first record; stop at the first key not below `key`. Returns ("found", value) |
+    ("tombstone", None) | ("not_found", None) | ("panic", the reference's panic text)."""
+    n = len(run)
+    if n == 0:
+        return ("panic", "Empty run data")  # :289-291
+    if run[0] != 1:
+        return ("panic", f"Unsupported version: {run[0]}")  # :294-297
+    p = 1
+    while p < n:  # :300
+        m = run[p]
+        p += 1
+        if m not in (1, 2):
+            return ("panic", f"Invalid marker byte: {m}")  # :307-310
+        if p + 4 > n:
+            return ("panic", "Incomplete key length data")  # :313-315
+        klen = int.from_bytes(run[p:p + 4], "big")
+        p += 4
+        if p + klen > n:
+            return ("panic", "Incomplete key data")  # :324-326
+        k = run[p:p + klen]
+        p += klen
+        if k < key:  # :331-356
+            if m == 1:
+                if p + 4 > n:
+                    return ("panic", "Incomplete value length data")
+                vlen = int.from_bytes(run[p:p + 4], "big")
+                p += 4
+                if p + vlen > n:
+                    return ("panic", "Incomplete value data")
+                p += vlen
+            continue
+        if k == key:  # :357-386
+            if m == 2:
+                return ("tombstone", None)
+            if p + 4 > n:
+                return ("panic", "Incomplete value length data for found key")
+            vlen = int.from_bytes(run[p:p + 4], "big")
+            p += 4
+            if p + vlen > n:
+                return ("panic", "Incomplete value data for found key")
+            return ("found", run[p:p + vlen])
+        return ("not_found", None)  # :387-391
+    return ("not_found", None)  # :395-396

@@ -184,6 +184,18 @@ constexpr int SORT_THREADS = 256;
 constexpr uint64_t SORT_EVERY = 48;      // one sample per SORT_EVERY elements
 constexpr uint64_t SORT_OV = 16;         // samples per bucket (bucket target SORT_EVERY * SORT_OV = 768)
 
+// Batched run lookups (skv_search.hip): same layout and codes as skv_lookup / SKV_LOOKUP_* /
+// SKV_PANIC_* in include/skv.h
+struct SrResult {
+    uint32_t kind, panic;
+    uint64_t val_off, val_len;
+};
+enum : uint32_t { SR_NOT_FOUND = 0, SR_FOUND = 1, SR_TOMBSTONE = 2, SR_PANIC = 3 };
+enum : uint32_t {
+    SRP_EMPTY = 1, SRP_VERSION = 2, SRP_MARKER = 3, SRP_KEYLEN = 4, SRP_KEY = 5, SRP_VALLEN = 6, SRP_VAL = 7,
+    SRP_VALLEN_FOUND = 8, SRP_VAL_FOUND = 9
+};
+
 // WAL key errors (wal_compaction.rs:71-79): no '.', or Rust's ParseIntError kinds
 enum : uint32_t { WERR_NONE = 0, WERR_NODOT, WERR_EMPTY, WERR_DIGIT, WERR_POS, WERR_NEG };
 

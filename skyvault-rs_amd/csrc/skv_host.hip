@@ -222,6 +222,12 @@ struct Job {
     uint32_t flags = 0;
     uint64_t in_bytes = 0;
     bool batch = false;  // writer batch encode (skv_encode_batch): one unsorted run, last op per key wins
+    // skv_search_run: one run, the keys (host), the outcomes (host)
+    const uint8_t* sr_keys = nullptr;
+    const uint64_t* sr_offs = nullptr;
+    uint32_t sr_n = 0;
+    skv_lookup* sr_out = nullptr;
+    bool search = false;
 };
 
 // a record's key bytes (host copy) for error-trigger comparisons
@@ -658,6 +664,33 @@ static void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo,
     cmp_klen = ncklen;
 }
 
+// skv_search_run after the parse: a run that parsed clean with no key decrease takes one binary
+// search per key over its record arrays; any other run the reference's scan (skv_search.hip).
+static int search_stage(skv_ctx* ctx, const Job& job, const RunInfo& run, uint64_t R, uint32_t run_err,
+                        uint64_t first_dec, const uint64_t* rec_addr, const uint64_t* rec_hi, const uint64_t* rec_lo,
+                        const uint32_t* rec_klen, const uint32_t* rec_meta) {
+    hipStream_t st = ctx->stream;
+    const uint32_t n = job.sr_n;
+    const uint64_t qbytes = job.sr_offs[n];
+    uint8_t* d_q = dbuf<uint8_t>(ctx, "sr_keys", qbytes + 16);
+    uint64_t* d_off = dbuf<uint64_t>(ctx, "sr_offs", n + 1);
+    SrResult* d_out = dbuf<SrResult>(ctx, "sr_out", n);
+    if (qbytes) h2d(ctx, d_q, job.sr_keys, qbytes);
+    h2d(ctx, d_off, job.sr_offs, (n + 1) * 8);
+    const bool clean = run_err == 0 && first_dec == ~0ull;
+    if (clean)
+        launch_search_bsearch(st, (const uint8_t*)run.ptr, run.len, R, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
+                              d_q, d_off, n, d_out);
+    else
+        launch_search_scan(st, (const uint8_t*)run.ptr, run.len, d_q, d_off, n, d_out);
+    HIPCHK(hipGetLastError());
+    static_assert(sizeof(SrResult) == sizeof(skv_lookup), "lookup layout");
+    if (n) HIPCHK(hipMemcpyAsync(job.sr_out, d_out, (size_t)n * sizeof(SrResult), hipMemcpyDeviceToHost, st));
+    sync(ctx);
+    ctx->timings.path = clean ? SKV_PATH_FIXED : SKV_PATH_GENERAL;
+    return SKV_OK;
+}
+
 // allow_deferred: on the fixed-stride fast path, launch the merge without waiting for the parse's
 // verdict (broken runs / order errors / oversized records) and check it with the final readback;
 // a bad verdict discards the result and reruns the call on the exact general path.
@@ -801,7 +834,8 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             for (uint32_t r = 1; r < n_runs && uniform; ++r) uniform = hf[r].S == hf[0].S && hf[r].K == hf[0].K;
             const RunFmt f0 = hf[0];
             const char* fenv = getenv("SKV_FUSED");
-            if (allow_deferred && uniform && !job.batch && !(job.flags & SKV_SPLIT_BY_TABLE) && !(fenv && fenv[0] == '0') &&
+            if (allow_deferred && uniform && !job.batch && !job.search && !(job.flags & SKV_SPLIT_BY_TABLE) &&
+                !(fenv && fenv[0] == '0') &&
                 f0.K <= FX_MAX_K && f0.S >= FX_MIN_S && f0.S <= FX_MAX_S && k <= (uint32_t)TILE_TARGET / 2 &&
                 R < 0xFFFFFFFFull) {
                 if (compact_fused(ctx, job, runs, d_runs, stream_first_run, f0, recb, out)) return SKV_OK;
@@ -813,7 +847,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
                                rec_meta, d_flags, d_stream_base, job.batch ? nullptr : d_first_dec);
             mark(ctx, PH_PARSE);
-            if (allow_deferred && !(job.flags & SKV_SPLIT_BY_TABLE)) {
+            if (allow_deferred && !(job.flags & SKV_SPLIT_BY_TABLE) && !job.search) {
                 deferred = true;  // verdict read with the result
                 parsed = true;
                 std::fill(first_dec.begin(), first_dec.end(), ~0ull);
@@ -857,6 +891,8 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         check_and_read(false);
     }
     mark(ctx, PH_CHECK);
+    if (job.search) return search_stage(ctx, job, runs[0], R, stream_err[0], first_dec[0], rec_addr, rec_hi, rec_lo,
+                                        rec_klen, rec_meta);
     bool any_dec = false;
     for (uint32_t s = 0; s < k; ++s)
         if (first_dec[s] != ~0ull && first_dec[s] + 1 < stream_valid[s]) any_dec = true;
@@ -1385,6 +1421,67 @@ int skv_encode_batch(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_
     int rc = batch_job(ctx, ops_run, len, max_run_size, job);
     if (rc) return rc;
     return compact_host_job(ctx, job, out, t_entry);
+}
+
+}  // extern "C"
+
+// runs::search_run's panic text (runs.rs:288-386)
+static std::string search_panic_text(uint32_t p) {
+    char buf[64];
+    switch (p & 0xFF) {
+        case SKV_PANIC_EMPTY: return "Empty run data";
+        case SKV_PANIC_VERSION: snprintf(buf, sizeof buf, "Unsupported version: %u", p >> 8); return buf;
+        case SKV_PANIC_MARKER: snprintf(buf, sizeof buf, "Invalid marker byte: %u", p >> 8); return buf;
+        case SKV_PANIC_KEYLEN: return "Incomplete key length data";
+        case SKV_PANIC_KEY: return "Incomplete key data";
+        case SKV_PANIC_VALLEN: return "Incomplete value length data";
+        case SKV_PANIC_VAL: return "Incomplete value data";
+        case SKV_PANIC_VALLEN_FOUND: return "Incomplete value length data for found key";
+        case SKV_PANIC_VAL_FOUND: return "Incomplete value data for found key";
+        default: return "internal: unknown search panic";
+    }
+}
+
+extern "C" {
+
+int skv_search_run(skv_ctx* ctx, const uint8_t* run, uint64_t len, const uint8_t* keys, const uint64_t* key_offs,
+                   uint32_t n_keys, skv_lookup* out) {
+    const double t_entry = now_ms();
+    if (!ctx) return SKV_E_INVALID_ARG;
+    if (n_keys && (!out || !key_offs)) return set_err(ctx, SKV_E_INVALID_ARG, "out/key_offs is NULL");
+    if (len && !run) return set_err(ctx, SKV_E_INVALID_ARG, "run is NULL");
+    if (n_keys && key_offs[n_keys] && !keys) return set_err(ctx, SKV_E_INVALID_ARG, "keys is NULL");
+    for (uint32_t i = 0; i < n_keys; ++i)
+        if (key_offs[i + 1] < key_offs[i]) return set_err(ctx, SKV_E_INVALID_ARG, "key_offs not ascending at %u", i);
+    if (n_keys == 0) return SKV_OK;
+    if (len == 0 || run[0] != 1) {  // the panics before the scan loop (runs.rs:288-297)
+        const uint32_t pc = len == 0 ? (uint32_t)SKV_PANIC_EMPTY : (SKV_PANIC_VERSION | ((uint32_t)run[0] << 8));
+        for (uint32_t i = 0; i < n_keys; ++i) out[i] = skv_lookup{SKV_LOOKUP_PANIC, pc, 0, 0};
+        return set_err(ctx, SKV_E_FORMAT, "%s", search_panic_text(pc).c_str());
+    }
+    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    Job job;
+    int rc = batch_job(ctx, run, len, 1ull << 62, job);
+    if (rc) return rc;
+    job.batch = false;
+    job.search = true;
+    job.sr_keys = keys;
+    job.sr_offs = key_offs;
+    job.sr_n = n_keys;
+    job.sr_out = out;
+    try {
+        uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", len + 16);
+        h2d(ctx, d_in, run, len);
+        job.run_ptr[0] = (uint64_t)(uintptr_t)d_in;
+    } catch (const DevError& e) {
+        return set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());
+    }
+    skv_result* none = nullptr;
+    rc = run_guarded(ctx, job, &none, t_entry);
+    if (rc) return rc;
+    for (uint32_t i = 0; i < n_keys; ++i)
+        if (out[i].kind == SKV_LOOKUP_PANIC) return set_err(ctx, SKV_E_FORMAT, "%s", search_panic_text(out[i].panic).c_str());
+    return SKV_OK;
 }
 
 int skv_encode_batch_dev(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_t max_run_size,

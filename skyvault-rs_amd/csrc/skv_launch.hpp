@@ -97,6 +97,13 @@ void launch_sort_scatter(hipStream_t, const SElem* E, uint64_t n, const uint64_t
                          SElem* out);
 void launch_sort_tile(hipStream_t, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out,
                       uint64_t* newkey);
+// skv_search.hip — batched run lookups
+void launch_search_bsearch(hipStream_t, const uint8_t* run, uint64_t len, uint64_t R, const uint64_t* rec_addr,
+                           const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,
+                           const uint32_t* rec_meta, const uint8_t* qbytes, const uint64_t* qoff, uint32_t n_q,
+                           SrResult* out);
+void launch_search_scan(hipStream_t, const uint8_t* run, uint64_t len, const uint8_t* qbytes, const uint64_t* qoff,
+                        uint32_t n_q, SrResult* out);
 uint64_t scan_tmp_words(uint64_t n);
 void launch_scan(hipStream_t, const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tmp);
 }  // namespace skv

@@ -78,6 +78,17 @@ class SkvResult(C.Structure):
     ]
 
 
+class SkvLookup(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("panic", C.c_uint32), ("val_off", C.c_uint64), ("val_len", C.c_uint64)]
+
+
+LOOKUP_NOT_FOUND, LOOKUP_FOUND, LOOKUP_TOMBSTONE, LOOKUP_PANIC = 0, 1, 2, 3
+PANIC_TEXT = {1: "Empty run data", 2: "Unsupported version: {}", 3: "Invalid marker byte: {}",
+              4: "Incomplete key length data", 5: "Incomplete key data", 6: "Incomplete value length data",
+              7: "Incomplete value data", 8: "Incomplete value length data for found key",
+              9: "Incomplete value data for found key"}
+
+
 class SkvTimings(C.Structure):
     _fields_ = [
         ("total_ms", C.c_double),
@@ -119,6 +130,7 @@ EXPORTED_SYMBOLS = [
     "skv_compact_dev",
     "skv_encode_batch",
     "skv_encode_batch_dev",
+    "skv_search_run",
     "skv_result_free",
 ]
 

@@ -57,6 +57,9 @@ def load():
     for fn in (l.skv_compact, l.skv_compact_dev):
         fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.POINTER(C.POINTER(SkvResult))]
         fn.restype = C.c_int
+    l.skv_search_run.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32,
+                                 C.c_void_p]
+    l.skv_search_run.restype = C.c_int
     for fn in (l.skv_encode_batch, l.skv_encode_batch_dev):
         fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.POINTER(SkvResult))]
         fn.restype = C.c_int
@@ -195,6 +198,41 @@ class Compactor:
         if rc != SKV_OK:
             raise self._err(rc)
         return DeviceResult(self.lib, res)
+
+    def search_run(self, run: bytes, keys: Sequence[bytes]):
+        """runs::search_run (runs.rs:285-398) for every key at once on the device. Returns one
+        outcome per key: ("found", value) | ("tombstone", None) | ("not_found", None) |
+        ("panic", reference panic text)."""
+        import numpy as np
+
+        from ._abi import (LOOKUP_FOUND, LOOKUP_NOT_FOUND, LOOKUP_PANIC, LOOKUP_TOMBSTONE, PANIC_TEXT,
+                           SkvLookup)
+
+        run = bytes(run)
+        kb = b"".join(bytes(k) for k in keys)
+        offs = np.zeros(len(keys) + 1, dtype=np.uint64)
+        if keys:
+            offs[1:] = np.cumsum([len(k) for k in keys])
+        rbuf = C.create_string_buffer(run, max(1, len(run)))
+        qbuf = C.create_string_buffer(kb, max(1, len(kb)))
+        out = (SkvLookup * max(1, len(keys)))()
+        rc = self.lib.skv_search_run(self.ctx, C.cast(rbuf, C.c_void_p), len(run), C.cast(qbuf, C.c_void_p),
+                                     C.c_void_p(offs.ctypes.data), len(keys), C.cast(out, C.c_void_p))
+        if rc not in (SKV_OK, 4):  # 4 = SKV_E_FORMAT: some key panicked, outcomes filled in
+            raise self._err(rc)
+        res = []
+        for i in range(len(keys)):
+            o = out[i]
+            if o.kind == LOOKUP_FOUND:
+                res.append(("found", run[o.val_off:o.val_off + o.val_len]))
+            elif o.kind == LOOKUP_TOMBSTONE:
+                res.append(("tombstone", None))
+            elif o.kind == LOOKUP_NOT_FOUND:
+                res.append(("not_found", None))
+            else:
+                assert o.kind == LOOKUP_PANIC
+                res.append(("panic", PANIC_TEXT[o.panic & 0xFF].format(o.panic >> 8)))
+        return res
 
     def timings(self) -> dict:
         t = SkvTimings()
