@@ -489,7 +489,9 @@ struct RecHdr {
 
 // One record of runs::read_run_stream (runs.rs:559-626) at p, checks in the reference's order,
 // from one 32-byte window plus (only for long keys / non-ASCII keys) further loads.
-template <bool PREFIX>
+// UTF8 = false: the record was already validated by a walk (k_emit re-reads records that
+// k_spec / k_fixup walked with every check)
+template <bool PREFIX, bool UTF8 = true>
 __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, uint64_t p) {
     RecHdr h;
     h.size = 0;
@@ -503,7 +505,7 @@ __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, ui
     if (kp + h.klen > len) { h.err = DERR_KEY; return h; }
     uint32_t kd[7];
     win_key(w, kd);
-    bool ok = h.klen <= 27 && ascii_prefix(kd, (uint32_t)h.klen);
+    bool ok = !UTF8 || (h.klen <= 27 && ascii_prefix(kd, (uint32_t)h.klen));
     if (!ok) ok = utf8_valid_fast(run + kp, h.klen);
     if (!ok) { h.err = DERR_UTF8; return h; }
     if (PREFIX) win_prefix(kd, h.klen, h.hi, h.lo);

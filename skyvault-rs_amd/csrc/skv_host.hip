@@ -181,6 +181,19 @@ static void h2d(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
 static double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
+// SKV_HOST_TRACE=1: host-side milestones of a call on stderr (ms since the call's first one)
+static void htrace(const char* what) {
+    static int on = -1;
+    static double t0 = 0;
+    if (on < 0) {
+        const char* e = getenv("SKV_HOST_TRACE");
+        on = e && e[0] == '1';
+    }
+    if (!on) return;
+    const double t = now_ms();
+    if (!strcmp(what, "start")) t0 = t;
+    fprintf(stderr, "[skv host] %8.3f ms %s\n", t - t0, what);
+}
 static void sync(skv_ctx* ctx) {
     const double t0 = now_ms();
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -301,6 +314,7 @@ static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
         K = hp[0];
         if ((uint32_t)hp[1]) return RC_RETRY_EXACT;
     }
+    htrace("wal K read");
     (void)R;
     int64_t* tid = dbuf<int64_t>(ctx, "w_tid", K + 1);
     uint32_t* strip = dbuf<uint32_t>(ctx, "w_strip", K + 1);
@@ -351,6 +365,7 @@ static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
         sync(ctx);
         memcpy(h, hp, 32);
     }
+    htrace("wal outcome read");
     if (h[0] != ~0ull) {  // the first bad key in merged order fails the job (:67-79 `?`)
         uint32_t rec = 0;
         HIPCHK(hipMemcpy(&rec, m_rec + h[0], 4, hipMemcpyDeviceToHost));
@@ -700,9 +715,11 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     ctx->up_chunk = 0;
     ctx->up_off = 0;
     mark(ctx, PH_START);
+    htrace("start");
     const uint32_t k = (uint32_t)job.ranked.size();
     // ---- run table ------------------------------------------------------------------------
     std::vector<RunInfo> runs;
+    runs.reserve(job.run_ptr.size());
     std::vector<uint32_t> stream_first_run(k + 1, 0);
     uint64_t n_chunks = 0;
     for (uint32_t s = 0; s < k; ++s) {
@@ -737,6 +754,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     RunSummary* d_sum = dbuf<RunSummary>(ctx, "run_sum", n_runs);
 
     h2d_up(ctx, d_runs, runs.data(), n_runs * sizeof(RunInfo));
+    htrace("runs uploaded");
     RunFmt* d_fmt = dbuf<RunFmt>(ctx, "run_fmt", n_runs);
     uint32_t* d_broken = dbuf<uint32_t>(ctx, "run_broken", n_runs);
     uint64_t* d_recb = dbuf<uint64_t>(ctx, "run_recb", n_runs + 1);
@@ -818,6 +836,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         RunFmt* hf = (RunFmt*)pinned(ctx, (size_t)n_runs * sizeof(RunFmt) + 16);
         d2h(ctx, hf, d_fmt, (size_t)n_runs * sizeof(RunFmt));
         sync(ctx);
+        htrace("run formats read");
         bool all_fixed = n_runs > 0;
         for (uint32_t r = 0; r < n_runs && all_fixed; ++r) all_fixed = hf[r].S != 0;
         if (all_fixed) {
@@ -843,6 +862,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             }
             stream_tables();
             alloc_records();
+            htrace("record tables");
             h2d_up(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
             launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
                                rec_meta, d_flags, d_stream_base, job.batch ? nullptr : d_first_dec);
@@ -854,6 +874,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
                 memset(hflags, 0, sizeof hflags);
             } else {
                 parsed = !check_and_read(true);
+                htrace("parse verdict read");
             }
             if (!parsed) {  // a run is not what its first record promised: general parse
                 R = 0;
@@ -891,6 +912,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         check_and_read(false);
     }
     mark(ctx, PH_CHECK);
+    htrace("check done");
     if (job.search) return search_stage(ctx, job, runs[0], R, stream_err[0], first_dec[0], rec_addr, rec_hi, rec_lo,
                                         rec_klen, rec_meta);
     bool any_dec = false;
@@ -985,6 +1007,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         const char* se = getenv("SKV_SORT");
         if ((k > (uint32_t)TILE_TARGET / 2 && R > (uint64_t)TILE_CAP) || (se && se[0] == '1') || job.batch) {
             sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen, job.batch);
+            htrace("sort launched");
             km = 1;
             list_off = {0, R};
             d_list_off = dbuf<uint64_t>(ctx, "sorted_off", 2);
@@ -1101,7 +1124,9 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     mark(ctx, PH_MERGE);
     const uint64_t* d_K = d_Kout;
     if (job.flags & SKV_SPLIT_BY_TABLE) {
+        htrace("merge launched");
         const int rc = wal_stage(ctx, job, R, d_K, m_rec, m_src, m_P, m_Dp, rec_addr, rec_klen, fp_bad, out);
+        htrace("wal stage done");
         if (rc == RC_RETRY_EXACT) return rerun_exact(ctx, job, out);
         return rc;
     }

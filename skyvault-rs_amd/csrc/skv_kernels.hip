@@ -352,7 +352,7 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
     const uint64_t len = runs[r].len;
     uint64_t p = ch_start[c];
     for (uint64_t i = 0; i < cnt; ++i) {
-        RecHdr h = parse_rec<true>(run, len, p);
+        RecHdr h = parse_rec<true, false>(run, len, p);  // validated by k_spec / k_fixup's walk
         put_rec(b0 + i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
         p += h.size;
     }

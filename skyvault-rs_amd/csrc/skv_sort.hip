@@ -186,23 +186,40 @@ __device__ __forceinline__ int sk_scmp(const SSplit& a, const SElem& b, uint64_t
     return a.klen < b.klen ? -1 : (a.klen > b.klen ? 1 : 0);
 }
 
-// bucket of each element = the splitters whose key orders strictly before its key; slot by an
-// atomic count (the bucket sort restores a deterministic order)
-__global__ void k_sort_bucket(const SElem* __restrict__ E, uint64_t n, const SSplit* __restrict__ sp, uint64_t nsp,
-                              unsigned long long* cnt, uint64_t* bs) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const SElem x = E[i];
-    uint64_t x0, x1;
-    sk_ext(sk_key(x), x.klen, x0, x1);
-    uint64_t a = 0, b = nsp;
-    while (a < b) {
-        const uint64_t mid = (a + b) >> 1;
-        if (sk_scmp(sp[mid], x, x0, x1) < 0) a = mid + 1;
-        else b = mid;
+// Bucket of each element = the splitters whose key orders strictly before its key; slot by an
+// atomic count (the bucket sort restores a deterministic order). Two-level search: every
+// top-th splitter sits in LDS (one table per workgroup of SB_PER elements per thread), the
+// final <= top splitters are searched in global memory.
+constexpr int SB_THREADS = 256, SB_PER = 16, SB_TOP = 1024;
+__global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restrict__ E, uint64_t n,
+                                                            const SSplit* __restrict__ sp, uint64_t nsp, uint64_t top,
+                                                            unsigned long long* cnt, uint64_t* bs) {
+    __shared__ SSplit tt[SB_TOP];
+    const uint64_t nt = nsp / top;  // top entry j = splitter (j + 1) * top - 1
+    for (uint64_t j = threadIdx.x; j < nt; j += SB_THREADS) tt[j] = sp[(j + 1) * top - 1];
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * SB_THREADS * SB_PER;
+    for (int u = 0; u < SB_PER; ++u) {
+        const uint64_t i = base + (uint64_t)u * SB_THREADS + threadIdx.x;
+        if (i >= n) break;
+        const SElem x = E[i];
+        uint64_t x0, x1;
+        sk_ext(sk_key(x), x.klen, x0, x1);
+        uint64_t a = 0, b = nt;  // top entries ordered strictly before x
+        while (a < b) {
+            const uint64_t mid = (a + b) >> 1;
+            if (sk_scmp(tt[mid], x, x0, x1) < 0) a = mid + 1;
+            else b = mid;
+        }
+        uint64_t lo = a * top, hi = a * top + top - 1 < nsp ? a * top + top - 1 : nsp;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (sk_scmp(sp[mid], x, x0, x1) < 0) lo = mid + 1;
+            else hi = mid;
+        }
+        const uint64_t slot = atomicAdd(cnt + lo, 1ull);
+        bs[i] = (lo << 32) | slot;
     }
-    const uint64_t slot = atomicAdd(cnt + a, 1ull);
-    bs[i] = (a << 32) | slot;
 }
 
 __global__ void k_sort_scatter(const SElem* __restrict__ E, uint64_t n, const uint64_t* __restrict__ bs,
@@ -344,7 +361,11 @@ void launch_sort_bucket(hipStream_t s, const SElem* E, uint64_t n, const SElem* 
                         void* split_buf, uint64_t* cnt, uint64_t* bs) {
     SSplit* sp = (SSplit*)split_buf;
     if (nsp) k_sort_splitters<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, sp);
-    if (n) k_sort_bucket<<<sk_blocks(n), 256, 0, s>>>(E, n, sp, nsp, (unsigned long long*)cnt, bs);
+    uint64_t top = 1;
+    while (nsp / top > (uint64_t)SB_TOP) top <<= 1;
+    const uint64_t per_wg = (uint64_t)SB_THREADS * SB_PER;
+    if (n) k_sort_bucket<<<(unsigned)((n + per_wg - 1) / per_wg), SB_THREADS, 0, s>>>(E, n, sp, nsp, top,
+                                                                                     (unsigned long long*)cnt, bs);
 }
 size_t sort_split_bytes(uint64_t nsp) { return (size_t)(nsp + 1) * sizeof(SSplit); }
 void launch_sort_scatter(hipStream_t s, const SElem* E, uint64_t n, const uint64_t* bs, const uint64_t* start,
