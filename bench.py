@@ -81,6 +81,59 @@ def make_cfg3_on_device(device, seed, n_streams, run_mib, vsize=256):
     return runs
 
 
+def make_cfg3_full_on_device(device, seed, n_streams, run_mib, vsize=256):
+    """Config 3 at BASELINE size, built in HBM: per stream ~run_mib MiB of records whose keys are
+    an order-preserving 11-character base-62 rendering of a sorted unique id (ids drawn from a
+    universe shared by all streams, so streams overlap and equal ids give equal keys) plus a
+    deterministic alnum tail, 11-128 B in all; 10 % Deletes; 256 B random values."""
+    n = (run_mib << 20) // 333
+    universe = n * n_streams * 2
+    M = 0x7FFFFFFFFFFFFFFF
+
+    def h(x):  # a 63-bit integer mix (deterministic, non-negative)
+        x = (x * 0x5851F42D4C957F2D + 0x14057B7EF767814F) & M
+        x = x ^ (x >> 29)
+        x = (x * 0x2545F4914F6CDD1D) & M
+        return x ^ (x >> 32)
+
+    alnum = torch.tensor(list(b"0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz"), dtype=torch.int64,
+                         device=device)
+    pow62 = torch.tensor([62 ** (10 - i) for i in range(11)], dtype=torch.int64, device=device)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    runs = []
+    for s in range(n_streams):
+        ids = torch.unique(torch.randint(0, universe, (n + n // 20,), generator=g, device=device))[:n]
+        m = ids.numel()
+        klen = 11 + h(ids) % 118
+        is_put = h(ids ^ (seed + 7919 * s)) % 1000 >= 100
+        size = 5 + klen + torch.where(is_put, 4 + vsize, 0)
+        off = torch.cumsum(size, 0) - size + 1
+        total = int(off[-1] + size[-1])
+        buf = torch.empty(total, dtype=torch.uint8, device=device)
+        buf[0] = 1
+        buf[off] = torch.where(is_put, 1, 2).to(torch.uint8)
+        for b in range(4):
+            buf[off + 1 + b] = ((klen >> (8 * (3 - b))) & 0xFF).to(torch.uint8)
+        kidx = torch.repeat_interleave(torch.arange(m, device=device), klen)
+        kpos = torch.arange(kidx.numel(), device=device) - torch.repeat_interleave(torch.cumsum(klen, 0) - klen, klen)
+        kid = ids[kidx]
+        digit = torch.where(kpos < 11, (kid // pow62[kpos.clamp(max=10)]) % 62, h(kid * 131 + kpos) % 62)
+        buf[off[kidx] + 5 + kpos] = alnum[digit].to(torch.uint8)
+        del kidx, kpos, kid, digit
+        pidx = torch.nonzero(is_put).squeeze(1)
+        vo = off[pidx] + 5 + klen[pidx]
+        for b in range(4):
+            buf[vo + b] = (vsize >> (8 * (3 - b))) & 0xFF
+        vpos = (vo + 4).unsqueeze(1) + torch.arange(vsize, device=device)
+        buf[vpos.reshape(-1)] = torch.randint(0, 256, (pidx.numel() * vsize,), dtype=torch.uint8, device=device,
+                                              generator=g)
+        del vpos, pidx, vo
+        runs.append(buf)
+    torch.cuda.synchronize(device)
+    return runs
+
+
 def make_cfg5_on_device(device, seed, n_streams, n_records=83, n_tables=64):
     """Config 5: n_streams WAL runs of n_records Puts, key "{t}." + zero-filled decimal suffix
     (32 B, gen.wal_run's format), 8 B values, each run sorted bytewise; one HBM tensor."""
@@ -135,8 +188,8 @@ def cpu_baseline(config, sample_records, n_streams, vsize, repeats, run_mib=16):
                               variant=config[1])
         sample = (f"{n_streams} streams x {sample_records} records x {9 + 16 + vsize} B (config-{config} shape, "
                   f"1/{round(238821 / sample_records)} of the records)")
-    elif config == "3":
-        streams = gen.config3(seed=0xC0FFEE, n_streams=n_streams, run_bytes=(run_mib << 20) // 16)
+    elif config in ("3", "3F"):
+        streams = gen.config3(seed=0xC0FFEE, n_streams=n_streams, run_bytes=(min(run_mib, 16) << 20) // 16)
         sample = f"{n_streams} streams x {run_mib / 16:.2f} MiB runs (config-3 shape, 1/16 of the bench's runs)"
     else:
         streams = gen.config5(seed=0xC0FFEE, n_streams=20000)
@@ -186,7 +239,7 @@ def main():
     ap.add_argument("--records", type=int, default=238821)
     ap.add_argument("--vsize", type=int, default=256)
     ap.add_argument("--variant", default="A", help="config 2 variant (same as --config 2A / 2B)")
-    ap.add_argument("--config", default=None, choices=["2A", "2B", "3", "5"])
+    ap.add_argument("--config", default=None, choices=["2A", "2B", "3", "3F", "5"])
     ap.add_argument("--run-mib", type=int, default=16, help="config 3 run size")
     ap.add_argument("--wal-runs", type=int, default=1_000_000, help="config 5 stream count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -220,6 +273,13 @@ def main():
                     f"one independent compaction per GPU")
         data = "synthetic: splitmix64 sorted unique hex keys + device-RNG values, built in HBM"
         n_streams = args.streams
+    elif config == "3F":
+        n_streams = 256 if args.streams == 64 else args.streams
+        run_mib = 256 if args.run_mib == 16 else args.run_mib
+        runs = make_cfg3_full_on_device(device, seed, n_streams, run_mib)
+        workload = (f"config 3: {n_streams}-way compaction, {n_streams} x 1 run of ~{run_mib} MiB, variable-length "
+                    f"keys 11-128 B + 10 % Deletes, 256 B values, max run 4 MiB")
+        data = "synthetic: sorted unique ids rendered as order-preserving alnum keys + alnum tails, built in HBM"
     elif config == "3":
         n_streams = 256 if args.streams == 64 else args.streams
         runs = make_cfg3_on_device(device, seed, n_streams, args.run_mib)
@@ -284,7 +344,7 @@ def main():
     # PCIe-inclusive figure (not `value`): the host entry point skv_compact with the inputs in
     # pinned host memory and the output runs returned in pinned host memory.
     host_path = None
-    if rank == 0 and world == 1 and not args.no_host_path and config in ("2A", "2B", "3"):
+    if rank == 0 and world == 1 and not args.no_host_path and config in ("2A", "2B", "3"):  # not 3F / 5
         host_runs = [r.cpu().pin_memory() for r in runs]
         hstreams = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(host_runs)]
         comp.compact_host_ptrs(hstreams, max_run, flags)  # warm-up (allocates the staging buffers)
