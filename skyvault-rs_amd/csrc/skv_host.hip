@@ -1135,7 +1135,10 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     uint64_t* d_nruns = dbuf<uint64_t>(ctx, "n_runs", 4);  // {runs, K, P[K]} (k_chain)
     DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", R + 1);
     uint64_t* seg_r0 = dbuf<uint64_t>(ctx, "seg_r0", R / GATHER_SEG + 2);
-    launch_chain(st, d_K, m_P, job.max_run_size, tile_max, T0, run_b, d_nruns);
+    uint64_t in_rec_bytes = 0;  // bounds P[K]
+    for (uint64_t l : job.run_len) in_rec_bytes += l;
+    uint32_t* chain_tbl = dbuf<uint32_t>(ctx, "chain_tbl", chain_table_entries(in_rec_bytes));
+    launch_chain(st, d_K, m_P, job.max_run_size, tile_max, T0, run_b, d_nruns, chain_tbl, R, in_rec_bytes);
     launch_run_stats(st, d_nruns, run_b, m_P, m_Dp, m_rec, rec_klen, d_desc, seg_r0, R);
     mark(ctx, PH_CHAIN);
     // ---- gather -----------------------------------------------------------------------------

@@ -1132,8 +1132,22 @@ __device__ uint64_t chain_search(const uint64_t* P, uint64_t lo, uint64_t hi, ui
     return lo;
 }
 
-constexpr int CH_D = 16;  // predicted windows in flight
-constexpr int CH_Q = 4;   // entries per lane per window (256 per window)
+constexpr int CH_D = 8;   // predicted windows in flight
+constexpr int CH_Q = 8;   // entries per lane per window (512 per window)
+constexpr uint32_t CH_SHIFT = 10;  // byte -> record table granularity (1 KiB)
+
+// tbl[t] = the surviving record j with P[j] <= t * 2^CH_SHIFT < P[j+1] (K past the end): lets the
+// chain turn a byte position into a record index with one load
+__global__ void k_chain_table(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ P, uint32_t* tbl,
+                              uint64_t n_tbl) {
+    const uint64_t K = *Kp;
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > K) return;
+    const uint64_t G = 1ull << CH_SHIFT;
+    const uint64_t lo = P[j];
+    const uint64_t hi = j < K ? P[j + 1] : lo + 1;  // past P[K] the chain clamps to K itself
+    for (uint64_t t = (lo + G - 1) >> CH_SHIFT; t < ((hi + G - 1) >> CH_SHIFT) && t < n_tbl; ++t) tbl[t] = (uint32_t)j;
+}
 
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
     uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane);
@@ -1143,7 +1157,8 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
 
 __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ P,
                                               uint64_t max_size, const uint32_t* __restrict__ tile_max,
-                                              uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs_out) {
+                                              uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs_out,
+                                              const uint32_t* __restrict__ tbl, uint64_t n_tbl) {
     const uint64_t K = *Kp;
     const int lane = threadIdx.x;
     // n_runs_out = {runs, K, output record bytes P[K]}: the host's single readback
@@ -1181,6 +1196,7 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
     }
     uint64_t b = 0, m = 0;
     uint64_t Pb = P[0];
+    const uint64_t PK = P[K];
     uint64_t L = 1;
     if (max_size > 1) {
         uint64_t avg = P[K] / K;
@@ -1193,10 +1209,23 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
         // prefetch CH_D windows of P around the predicted ends of the next CH_D runs
         uint64_t wv[CH_D][CH_Q];
         uint64_t wsd[CH_D];
+        // window starts: with every record fitting a run, run d+1 from here ends at a record
+        // starting in (Pb + (d+1)(max-1-mr), Pb + (d+1)(max-1)] bytes: the byte table gives the
+        // record at the low end with one load (all CH_D loads independent); else by count
 #pragma unroll
         for (int d = 0; d < CH_D; ++d) {
-            uint64_t c = b + (uint64_t)(d + 1) * L;
-            uint64_t ws = c > 128 ? c - 128 : 0;
+            if (tbl && all_fit) {
+                const uint64_t low = Pb + (uint64_t)(d + 1) * (max_size - 1 - mr);
+                const uint64_t t = low >> CH_SHIFT;
+                wsd[d] = low >= PK ? K : tbl[t];
+            } else {
+                const uint64_t c = b + (uint64_t)(d + 1) * L;
+                wsd[d] = c > 128 ? c - 128 : 0;
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < CH_D; ++d) {
+            uint64_t ws = wsd[d];
             if (ws < b + 1) ws = b + 1;
             wsd[d] = ws;
 #pragma unroll
@@ -1217,17 +1246,23 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
                 const uint64_t ws = wsd[d];
                 // predicate P[pos] <= v is monotone in pos = ws + 4*lane + q: the last true
                 // position is found from four wave ballots with scalar bit ops
-                const uint64_t m0 = __ballot(wv[d][0] <= v), m1 = __ballot(wv[d][1] <= v);
-                const uint64_t m2 = __ballot(wv[d][2] <= v), m3 = __ballot(wv[d][3] <= v);
+                uint64_t mq[CH_Q];
+#pragma unroll
+                for (int q = 0; q < CH_Q; ++q) mq[q] = __ballot(wv[d][q] <= v);
+                const uint64_t m0 = mq[0];
                 bool found = false;
                 uint64_t best = 0;
                 if (m0) {
                     const int ls = 63 - __builtin_clzll(m0);
-                    const uint32_t qs = (uint32_t)((m1 >> ls) & 1) + (uint32_t)((m2 >> ls) & 1) + (uint32_t)((m3 >> ls) & 1);
+                    uint32_t qs = 0;  // true entries of lane ls past its first
+#pragma unroll
+                    for (int q = 1; q < CH_Q; ++q) qs += (uint32_t)((mq[q] >> ls) & 1);
                     best = ws + (uint64_t)ls * CH_Q + qs;
                     found = best == K || best < ws + CH_Q * 64 - 1;
                     if (found) {
-                        uint64_t x = qs == 0 ? wv[d][0] : (qs == 1 ? wv[d][1] : (qs == 2 ? wv[d][2] : wv[d][3]));
+                        uint64_t x = wv[d][0];
+#pragma unroll
+                        for (int q = 1; q < CH_Q; ++q) x = qs == (uint32_t)q ? wv[d][q] : x;
                         Pe = readlane_u64(x, ls);
                     }
                 }
@@ -1865,9 +1900,13 @@ hipError_t launch_tile(hipStream_t s, bool l0, const uint64_t* hi, const uint64_
     return hipGetLastError();
 }
 void launch_chain(hipStream_t s, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, const uint32_t* tile_max,
-                  uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs) {
-    k_chain<<<1, 64, 0, s>>>(Kp, P, max_size, tile_max, n_tiles, run_b, n_runs);
+                  uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs, uint32_t* tbl, uint64_t max_K,
+                  uint64_t max_bytes) {
+    const uint64_t n_tbl = tbl ? (max_bytes >> CH_SHIFT) + 2 : 0;
+    if (tbl) k_chain_table<<<blocks_for(max_K + 1, 256), 256, 0, s>>>(Kp, P, tbl, n_tbl);
+    k_chain<<<1, 64, 0, s>>>(Kp, P, max_size, tile_max, n_tiles, run_b, n_runs, tbl, n_tbl);
 }
+uint64_t chain_table_entries(uint64_t max_bytes) { return (max_bytes >> CH_SHIFT) + 2; }
 void launch_run_stats(hipStream_t s, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
                       const uint64_t* Dp, const uint32_t* m_rec, const uint32_t* rec_klen, DevRunDesc* descs,
                       uint64_t* seg_r0, uint64_t max_runs) {
