@@ -530,16 +530,48 @@ __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, ui
     return h;
 }
 
-// walk_checked with vectorized headers: one dependent round trip per record
+// walk_checked with vectorized headers: one dependent round trip per record. UTF8 = false: the
+// structure only (k_spec's fast mode; k_emit checks the keys and flags a bad one for an exact rerun)
+template <bool UTF8 = true>
 __device__ inline WalkRes walk_fast(const uint8_t* run, uint64_t len, uint64_t p, uint64_t stop, uint32_t max_recs) {
     uint32_t cnt = 0;
     while (p < stop && cnt < max_recs) {
-        RecHdr h = parse_rec<false>(run, len, p);
+        RecHdr h = parse_rec<false, UTF8>(run, len, p);
         if (h.err) return {p, cnt, h.err};
         ++cnt;
         p += h.size;
     }
     return {p, cnt, DERR_NONE};
+}
+
+// 64-bit fingerprint of the key bytes past the 16-byte prefix (0 for keys of at most 16 bytes),
+// a function of the bytes alone; ascii: those bytes have no high bit
+__device__ __forceinline__ uint64_t fp_mix(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+__device__ inline uint64_t key_tail_fp(const uint8_t* key, uint32_t klen, bool& ascii) {
+    ascii = true;
+    if (klen <= 16) return 0;
+    const uint8_t* k = key + 16;
+    const uint32_t n = klen - 16;
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+    uint32_t acc = 0;
+    for (uint32_t o = 0; o < n; o += 16) {
+        const uint32_t m = n - o < 16 ? n - o : 16;
+        const uint4 v = load_window16(k + o, m);
+        const uint32_t a0 = v.x & dword_mask(0, m, 0), a1 = v.y & dword_mask(0, m, 1);
+        const uint32_t a2 = v.z & dword_mask(0, m, 2), a3 = v.w & dword_mask(0, m, 3);
+        acc |= a0 | a1 | a2 | a3;
+        h = fp_mix(h ^ (((uint64_t)a1 << 32) | a0));
+        h = fp_mix(h ^ (((uint64_t)a3 << 32) | a2) ^ 0x2545F4914F6CDD1Dull);
+    }
+    ascii = (acc & 0x80808080u) == 0;
+    return h;
 }
 
 __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t k) {

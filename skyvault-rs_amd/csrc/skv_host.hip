@@ -86,6 +86,7 @@ struct skv_ctx {
     uint64_t syncs = 0;
     double sync_ms = 0;
     bool exact_keys = false;  // rerun after a fingerprint shortcut misordered a tile (never in practice)
+    bool exact_utf8 = false;  // rerun with UTF-8 checked in the chunk walks (a run holds a bad key)
 };
 
 struct ResultBox {  // skv_result + how to free it
@@ -771,6 +772,8 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     uint64_t* rec_lo = nullptr;
     uint32_t* rec_klen = nullptr;
     uint32_t* rec_meta = nullptr;
+    uint64_t* rec_fp = nullptr;  // fingerprints of the key bytes past 16 (written by the emit kernels)
+    uint32_t* utf8_bad = dbuf<uint32_t>(ctx, "utf8_bad", 1);
     uint32_t* d_flags = dbuf<uint32_t>(ctx, "flags", 4);
     uint64_t* d_stream_base = dbuf<uint64_t>(ctx, "stream_base", k + 1);
     unsigned long long* d_first_dec = dbuf<unsigned long long>(ctx, "first_dec", k);
@@ -805,23 +808,29 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         rec_lo = dbuf<uint64_t>(ctx, "rec_lo", R);
         rec_klen = dbuf<uint32_t>(ctx, "rec_klen", R);
         rec_meta = dbuf<uint32_t>(ctx, "rec_meta", R);
+        rec_fp = dbuf<uint64_t>(ctx, "rec_fp", R);
         HIPCHK(hipMemsetAsync(d_flags, 0, 16, st));
+        HIPCHK(hipMemsetAsync(utf8_bad, 0, 4, st));
         HIPCHK(hipMemsetAsync(d_first_dec, 0xFF, (size_t)k * 8, st));
         h2d_up(ctx, d_stream_base, stream_base.data(), (k + 1) * 8);
     };
+    uint32_t utf8_flag = 0;
     // order check + readback of its result, the record flags and (fast path) the broken-run flags
     auto check_and_read = [&](bool read_broken) -> bool {
         // the fast path's parse kernel already did the order check
         if (!read_broken && !job.batch)  // a writer batch is unsorted by definition
             launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
         HIPCHK(hipGetLastError());
-        uint8_t* hp = (uint8_t*)pinned(ctx, k * 8 + 16 + (read_broken ? n_runs * 4 : 0));
+        uint8_t* hp = (uint8_t*)pinned(ctx, k * 8 + 16 + (read_broken ? n_runs * 4 : 0) + 16);
         d2h(ctx, hp, d_first_dec, (size_t)k * 8);
         d2h(ctx, hp + (size_t)k * 8, d_flags, 16);
+        uint8_t* hu = hp + k * 8 + 16 + (read_broken ? n_runs * 4 : 0);
+        d2h(ctx, hu, utf8_bad, 4);
         if (read_broken) d2h(ctx, hp + (size_t)k * 8 + 16, d_broken, (size_t)n_runs * 4);
         sync(ctx);
         memcpy(first_dec.data(), hp, (size_t)k * 8);
         memcpy(hflags, hp + (size_t)k * 8, 16);
+        memcpy(&utf8_flag, hu, 4);
         bool broken = false;
         if (read_broken) {
             const uint32_t* b = (const uint32_t*)(hp + (size_t)k * 8 + 16);
@@ -865,7 +874,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             htrace("record tables");
             h2d_up(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
             launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
-                               rec_meta, d_flags, d_stream_base, job.batch ? nullptr : d_first_dec);
+                               rec_meta, d_flags, d_stream_base, job.batch ? nullptr : d_first_dec, rec_fp);
             mark(ctx, PH_PARSE);
             if (allow_deferred && !(job.flags & SKV_SPLIT_BY_TABLE) && !job.search) {
                 deferred = true;  // verdict read with the result
@@ -888,9 +897,11 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         HIPCHK(hipMemsetAsync(bad_bits, 0, (n_chunks / 64 + 1) * 8, st));
         HIPCHK(hipMemsetAsync(first_bad, 0xFF, n_runs * 4, st));
         HIPCHK(hipMemsetAsync(err_chunk, 0xFF, n_runs * 4, st));
-        launch_spec(st, d_runs, n_runs, n_chunks, d_hdr, d_fmt, d_broken, ch_start, ch_end, ch_cnt, ch_err);
+        launch_spec(st, d_runs, n_runs, n_chunks, d_hdr, d_fmt, d_broken, ch_start, ch_end, ch_cnt, ch_err,
+                    ctx->exact_utf8);
         launch_validate(st, d_runs, n_runs, n_chunks, d_hdr, ch_start, ch_end, ch_err, bad_bits, first_bad);
-        launch_fixup(st, d_runs, n_runs, d_hdr, first_bad, bad_bits, ch_start, ch_end, ch_cnt, ch_err);
+        launch_fixup(st, d_runs, n_runs, d_hdr, first_bad, bad_bits, ch_start, ch_end, ch_cnt, ch_err,
+                     ctx->exact_utf8);
         launch_err_chunk(st, d_runs, n_runs, n_chunks, d_hdr, ch_err, err_chunk);
         launch_mask(st, d_runs, n_runs, n_chunks, d_hdr, err_chunk, ch_cnt, cnt64);
         launch_scan(st, cnt64, n_chunks, ch_rec_base, scan_tmp);
@@ -907,9 +918,21 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         stream_tables();
         alloc_records();
         launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, R, rec_addr, rec_hi,
-                    rec_lo, rec_klen, rec_meta, d_flags);
+                    rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad);
         mark(ctx, PH_PARSE);
         check_and_read(false);
+        if (utf8_flag && !ctx->exact_utf8) {  // a key the chunk walks did not check: exact walks
+            ctx->exact_utf8 = true;
+            int rc;
+            try {
+                rc = compact_device(ctx, job, out, false);
+            } catch (...) {
+                ctx->exact_utf8 = false;
+                throw;
+            }
+            ctx->exact_utf8 = false;
+            return rc;
+        }
     }
     mark(ctx, PH_CHECK);
     htrace("check done");
@@ -1059,11 +1082,14 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     uint32_t* fp_bad = dbuf<uint32_t>(ctx, "fp_bad", 1);
     HIPCHK(hipMemsetAsync(fp_bad, 0, 4, st));
     if (km > 1 && !ctx->exact_keys) {
-        uint64_t* f = dbuf<uint64_t>(ctx, "rec_fp", R);
         const char* te = getenv("SKV_FP_TEST");
-        if (te && te[0] == '1') HIPCHK(hipMemsetAsync(f, 0, R * 8, st));
-        else launch_key_fp(st, R, rec_addr, rec_klen, f);
-        key_fp = f;
+        if (te && te[0] == '1') {
+            uint64_t* f = dbuf<uint64_t>(ctx, "rec_fp_test", R);
+            HIPCHK(hipMemsetAsync(f, 0, R * 8, st));
+            key_fp = f;
+        } else {
+            key_fp = rec_fp;  // written by the emit kernels with the record arrays
+        }
     }
     for (int li = (int)lv.size() - 1; li >= 0; --li) {
         Level& L = lv[li];

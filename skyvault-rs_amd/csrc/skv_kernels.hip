@@ -113,7 +113,7 @@ __global__ void k_run_header(const RunInfo* runs, uint32_t n_runs, uint32_t* hdr
 // Speculative start of chunk `local` (> 0): a record start must lie in [cs, ce). Scan for the
 // first position whose next three records decode cleanly. Wrong guesses are caught by
 // k_validate and repaired by k_fixup.
-__device__ uint64_t spec_start(const uint8_t* run, uint64_t len, uint64_t cs, uint64_t ce) {
+__device__ uint64_t spec_start(const uint8_t* run, uint64_t len, uint64_t cs, uint64_t ce, bool utf8) {
     for (uint64_t p0 = cs; p0 < ce; p0 += 16) {  // 16 bytes per load; marker candidates as a mask
         const uint32_t m = (uint32_t)(ce - p0 < 16 ? ce - p0 : 16);
         const uint4 v = load_window16(run + p0, m);
@@ -127,7 +127,7 @@ __device__ uint64_t spec_start(const uint8_t* run, uint64_t len, uint64_t cs, ui
         while (cand) {
             const uint32_t i = __builtin_ctz(cand);
             cand &= cand - 1;
-            WalkRes r = walk_fast(run, len, p0 + i, len, 3);
+            WalkRes r = utf8 ? walk_fast<true>(run, len, p0 + i, len, 3) : walk_fast<false>(run, len, p0 + i, len, 3);
             if (r.err == DERR_NONE) return p0 + i;
         }
     }
@@ -153,7 +153,7 @@ __device__ __forceinline__ bool fixed_rec_ok(const uint8_t* run, uint64_t len, u
 
 __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
                        const uint32_t* __restrict__ hdr_err, const RunFmt* __restrict__ fmt, uint32_t* run_broken,
-                       uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err) {
+                       uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, bool utf8) {
     uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
     uint32_t r = find_run(runs, n_runs, c);
@@ -202,7 +202,7 @@ __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         atomicOr(&run_broken[r], 1u);  // hypothesis broken: this run takes the general path
         start = p0;
     } else {
-        start = local == 0 ? 1 : spec_start(run, R.len, cs, ce);
+        start = local == 0 ? 1 : spec_start(run, R.len, cs, ce, utf8);
     }
     if (start == NO_POS) {
         ch_start[c] = NO_POS;
@@ -211,7 +211,8 @@ __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         ch_err[c] = 0;
         return;
     }
-    WalkRes w = walk_fast(run, R.len, start, ce, 0xFFFFFFFFu);
+    WalkRes w = utf8 ? walk_fast<true>(run, R.len, start, ce, 0xFFFFFFFFu)
+                     : walk_fast<false>(run, R.len, start, ce, 0xFFFFFFFFu);
     ch_start[c] = start;
     ch_end[c] = w.end;
     ch_cnt[c] = w.cnt;
@@ -252,7 +253,7 @@ __device__ uint64_t next_bad(const unsigned long long* bits, uint64_t from, uint
 // Sequential repair of each run's bad chunks from the true chain (exact; rare on real data).
 __global__ void k_fixup(const RunInfo* __restrict__ runs, uint32_t n_runs, const uint32_t* __restrict__ hdr_err,
                         const uint32_t* __restrict__ run_first_bad, const unsigned long long* __restrict__ bad_bits,
-                        uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err) {
+                        uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, bool utf8) {
     uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_runs) return;
     uint32_t fb = run_first_bad[r];
@@ -270,7 +271,8 @@ __global__ void k_fixup(const RunInfo* __restrict__ runs, uint32_t n_runs, const
         uint64_t end = E;
         uint32_t cnt = 0, err = 0;
         if (E < ce) {
-            WalkRes w = walk_fast(run, R.len, E, ce, 0xFFFFFFFFu);
+            WalkRes w = utf8 ? walk_fast<true>(run, R.len, E, ce, 0xFFFFFFFFu)
+                             : walk_fast<false>(run, R.len, E, ce, 0xFFFFFFFFu);
             end = w.end;
             cnt = w.cnt;
             err = w.err;
@@ -326,8 +328,9 @@ __global__ void k_run_summary(const RunInfo* __restrict__ runs, uint32_t n_runs,
 
 __device__ __forceinline__ void put_rec(uint64_t o, const uint8_t* rp, const RecHdr& h, uint64_t* rec_addr,
                                         uint64_t* rec_hi, uint64_t* rec_lo, uint32_t* rec_klen, uint32_t* rec_meta,
-                                        uint32_t* flags) {
+                                        uint32_t* flags, uint64_t* rec_fp, uint64_t fpv) {
     rec_addr[o] = (uint64_t)rp;
+    rec_fp[o] = fpv;
     rec_hi[o] = h.hi;
     rec_lo[o] = h.lo;
     rec_klen[o] = (uint32_t)h.klen;
@@ -341,7 +344,8 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
                        const RunFmt* __restrict__ fmt, const uint32_t* __restrict__ run_broken,
                        const uint64_t* __restrict__ ch_start, const uint64_t* __restrict__ ch_rec_base,
                        uint64_t* __restrict__ rec_addr, uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
-                       uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags) {
+                       uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags,
+                       uint64_t* __restrict__ rec_fp, uint32_t* utf8_bad) {
     uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
     uint64_t b0 = ch_rec_base[c], cnt = ch_rec_base[c + 1] - b0;
@@ -352,8 +356,14 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
     const uint64_t len = runs[r].len;
     uint64_t p = ch_start[c];
     for (uint64_t i = 0; i < cnt; ++i) {
-        RecHdr h = parse_rec<true, false>(run, len, p);  // validated by k_spec / k_fixup's walk
-        put_rec(b0 + i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
+        // structure validated by k_spec / k_fixup's walk; the key's UTF-8 is checked here with the
+        // same loads that fingerprint it (a bad key flags the call for an exact rerun)
+        RecHdr h = parse_rec<true, false>(run, len, p);
+        bool ascii;
+        const uint64_t fpv = key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii);
+        if (!(ascii && ((h.hi | h.lo) & 0x8080808080808080ull) == 0) && !utf8_valid(run + p + 5, h.klen))
+            atomicOr(utf8_bad, 1u);
+        put_rec(b0 + i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp, fpv);
         p += h.size;
     }
 }
@@ -369,7 +379,8 @@ __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, 
                              const uint64_t* __restrict__ run_recb, uint64_t* __restrict__ rec_addr,
                              uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
                              uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags,
-                             const uint64_t* __restrict__ stream_base, unsigned long long* first_dec) {
+                             const uint64_t* __restrict__ stream_base, unsigned long long* first_dec,
+                             uint64_t* __restrict__ rec_fp) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool act = i < R_total;
     uint32_t lo = 0;
@@ -400,9 +411,13 @@ __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, 
             // never follows a garbage address; the host reruns the general parse
             RecHdr z{};
             z.marker = 1;
-            put_rec(i, run, z, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
+            put_rec(i, run, z, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp, 0);
         }
-        if (act) put_rec(i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
+        if (act) {
+            bool ascii;
+            put_rec(i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp,
+                    key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii));
+        }
     }
     if (!VERIFY || !first_dec) return;  // (no order check for a writer batch)
     // fused order check (runs.rs:190-198 as k_order_check does it): compare with the previous
@@ -543,35 +558,14 @@ __device__ __forceinline__ bool elem_less_fp(const uint64_t* fp, const uint64_t*
     return (uint32_t)ca < (uint32_t)cb;
 }
 
-// 64-bit fingerprint of the key bytes past the 16-byte prefix (0 for keys of at most 16 bytes)
-__device__ inline uint64_t fp_mix(uint64_t x) {
-    x ^= x >> 33;
-    x *= 0xff51afd7ed558ccdull;
-    x ^= x >> 33;
-    x *= 0xc4ceb9fe1a85ec53ull;
-    x ^= x >> 33;
-    return x;
-}
+// fingerprints of the key bytes past 16 of the record arrays (records the emit kernels did not
+// fingerprint themselves)
 __global__ void k_key_fp(uint64_t R, const uint64_t* __restrict__ rec_addr, const uint32_t* __restrict__ rec_klen,
                          uint64_t* fp) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= R) return;
-    const uint32_t kl = rec_klen[i];
-    uint64_t h = 0;
-    if (kl > 16) {
-        const uint8_t* k = (const uint8_t*)rec_addr[i] + 5 + 16;
-        const uint32_t n = kl - 16;
-        h = 0x9E3779B97F4A7C15ull ^ n;
-        for (uint32_t o = 0; o < n; o += 16) {
-            const uint32_t m = n - o < 16 ? n - o : 16;
-            const uint4 v = load_window16(k + o, m);
-            const uint64_t w0 = ((uint64_t)(v.y & dword_mask(0, m, 1)) << 32) | (v.x & dword_mask(0, m, 0));
-            const uint64_t w1 = ((uint64_t)(v.w & dword_mask(0, m, 3)) << 32) | (v.z & dword_mask(0, m, 2));
-            h = fp_mix(h ^ w0);
-            h = fp_mix(h ^ w1 ^ 0x2545F4914F6CDD1Dull);
-        }
-    }
-    fp[i] = h;
+    bool ascii;
+    fp[i] = key_tail_fp((const uint8_t*)rec_addr[i] + 5, rec_klen[i], ascii);
 }
 
 // samples: every S-th element of each list
@@ -1784,10 +1778,10 @@ void launch_run_header(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint
 }
 void launch_spec(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                  const RunFmt* fmt, uint32_t* run_broken, uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt,
-                 uint32_t* ch_err) {
+                 uint32_t* ch_err, bool utf8) {
     if (n_chunks)
         k_spec<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, fmt, run_broken, ch_start,
-                                                         ch_end, ch_cnt, ch_err);
+                                                         ch_end, ch_cnt, ch_err, utf8);
 }
 void launch_validate(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                      const uint64_t* ch_start, const uint64_t* ch_end, const uint32_t* ch_err,
@@ -1798,10 +1792,10 @@ void launch_validate(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64
 }
 void launch_fixup(hipStream_t s, const RunInfo* runs, uint32_t n_runs, const uint32_t* hdr_err,
                   const uint32_t* run_first_bad, const unsigned long long* bad_bits, uint64_t* ch_start,
-                  uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err) {
+                  uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, bool utf8) {
     if (n_runs)
         k_fixup<<<blocks_for(n_runs, 64), 64, 0, s>>>(runs, n_runs, hdr_err, run_first_bad, bad_bits, ch_start, ch_end,
-                                                       ch_cnt, ch_err);
+                                                       ch_cnt, ch_err, utf8);
 }
 void launch_err_chunk(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                       const uint32_t* ch_err, uint32_t* run_err_chunk) {
@@ -1821,23 +1815,24 @@ void launch_run_summary(hipStream_t s, const RunInfo* runs, uint32_t n_runs, con
 void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const RunFmt* fmt,
                  const uint32_t* run_broken, const uint64_t* ch_start, const uint64_t* ch_rec_base,
                  const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
-                 uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags) {
+                 uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, uint64_t* rec_fp, uint32_t* utf8_bad) {
     if (n_chunks)
         k_emit<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, fmt, run_broken, ch_start, ch_rec_base,
-                                                         rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags);
+                                                         rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp,
+                                                         utf8_bad);
     if (R)
         k_emit_fixed<false><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, R, fmt, (uint32_t*)run_broken, run_recb,
                                                                rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags,
-                                                               nullptr, nullptr);
+                                                               nullptr, nullptr, rec_fp);
 }
 void launch_parse_fixed(hipStream_t s, const RunInfo* runs, uint32_t n_runs, const RunFmt* fmt, uint32_t* run_broken,
                         const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                         uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, const uint64_t* stream_base,
-                        unsigned long long* first_dec) {
+                        unsigned long long* first_dec, uint64_t* rec_fp) {
     if (R)
         k_emit_fixed<true><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, R, fmt, run_broken, run_recb, rec_addr,
                                                               rec_hi, rec_lo, rec_klen, rec_meta, flags, stream_base,
-                                                              first_dec);
+                                                              first_dec, rec_fp);
 }
 void launch_order_check(hipStream_t s, uint64_t R, const uint64_t* stream_base, uint32_t k, const uint64_t* rec_addr,
                         const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,

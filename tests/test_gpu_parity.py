@@ -310,3 +310,27 @@ def test_oversized_tile_fallback(dev):
         for flags in (0, _abi.SKV_DROP_TOMBSTONES):
             exp, got = _run_both(dev, [(1, [a]), (2, [b])], 64 * KiB, flags)
             assert exp == got, _diff(exp, got)
+
+
+def test_invalid_utf8_key_in_variable_runs(dev):
+    """Variable-size runs: the chunk walks check structure only, the emit pass checks each key's
+    UTF-8 with the loads that fingerprint it; a bad key reruns the exact walks, whose decode stops
+    there (runs.rs:585-591). Valid non-ASCII keys take no rerun."""
+    r = random.Random(21)
+    for trial in range(6):
+        streams = []
+        for s in range(5):
+            keys = sorted({("k%05d" % r.randrange(10**5)) + "é" * r.randint(0, 3) + "x" * r.randint(0, 40)
+                           for _ in range(300)})
+            ops = [fmt.put(k, bytes(r.randrange(256) for _ in range(r.randint(0, 30)))) for k in keys]
+            run = bytearray(fmt.encode_run(ops))
+            if s == trial % 5 and trial < 5:  # corrupt one key byte into an invalid UTF-8 byte
+                p = 1
+                for _ in range(r.randrange(len(ops))):
+                    kl = int.from_bytes(run[p + 1:p + 5], "big")
+                    vl = int.from_bytes(run[p + 5 + kl:p + 9 + kl], "big")
+                    p += 9 + kl + vl
+                run[p + 5 + 1] = 0xFF
+            streams.append((s + 1, [bytes(run)]))
+        exp, got = _run_both(dev, streams, 1 << 16, 0)
+        assert exp == got, _diff(exp, got)
