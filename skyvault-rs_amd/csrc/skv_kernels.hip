@@ -1000,7 +1000,16 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         return;
     }
     TPROF(2);
-    // level 0 output: (a) first-per-key flags by merged position (k_way.rs:146-151)
+    // level 0 output: source addresses by final position first (the free ping-pong buffer), so
+    // that the exact neighbour compares below read the key bytes without a rec_addr lookup
+    uint64_t* paddr = mhn;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const uint32_t e = threadIdx.x + u * TILE_THREADS;
+        if (e < n) paddr[rpos[u]] = raddr[u];
+    }
+    __syncthreads();
+    // (a) first-per-key flags by merged position (k_way.rs:146-151)
     const uint32_t i0 = threadIdx.x * PER;
     uint32_t keep_mask = 0;
     uint32_t idx[PER];
@@ -1014,9 +1023,15 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
             bool first = true;
             if (i > 0 && mh[i - 1] == h) {  // exact: first-per-key and the check of the fp shortcut
                 const uint32_t p = mi[i - 1];
-                const int kc = ekey_cmp(rec_addr, h, el_lo[p], el_c[p], h, el_lo[e], c);
+                const uint64_t lp = el_lo[p], le = el_lo[e], cp = el_c[p];
+                int kc = lp != le ? (lp < le ? -1 : 1) : 0;
+                const uint32_t kp = (uint32_t)(cp >> 32), ke = (uint32_t)(c >> 32);
+                if (!kc && kp > 16 && ke > 16)
+                    kc = bytes_cmp16((const uint8_t*)paddr[i - 1] + 5 + 16, (const uint8_t*)paddr[i] + 5 + 16,
+                                     (kp < ke ? kp : ke) - 16);
+                if (!kc) kc = kp < ke ? -1 : (kp > ke ? 1 : 0);
                 first = kc != 0;
-                if (O.fp_bad && (kc > 0 || (kc == 0 && (uint32_t)el_c[p] > (uint32_t)c))) atomicOr(O.fp_bad, 1u);
+                if (O.fp_bad && (kc > 0 || (kc == 0 && (uint32_t)cp > (uint32_t)c))) atomicOr(O.fp_bad, 1u);
             }
             idx[q] = (uint32_t)c;
             if (first) keep_mask |= 1u << q;
@@ -1024,16 +1039,12 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     }
     __syncthreads();
     TPROF(3);
-    // (b) meta and source address by final position (el_lo and the free ping-pong buffer)
+    // (b) meta by final position (el_lo is free now)
     uint32_t* pmeta = (uint32_t*)el_lo;
-    uint64_t* paddr = mhn;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const uint32_t e = threadIdx.x + u * TILE_THREADS;
-        if (e < n) {
-            pmeta[rpos[u]] = rmeta[u];
-            paddr[rpos[u]] = raddr[u];
-        }
+        if (e < n) pmeta[rpos[u]] = rmeta[u];
     }
     __syncthreads();
     TPROF(4);
