@@ -130,7 +130,7 @@ struct TileOut {
 #define SKV_FX_U 2                       // output blocks per lane per batch in the fused copy (two batches in flight)
 #endif
 #ifndef SKV_FX_CAP
-#define SKV_FX_CAP 4096
+#define SKV_FX_CAP 2048                  // 2048: 63 VGPRs, 4 workgroups per CU (4096: 91 VGPRs, 2 per CU; 3 % slower end to end)
 #endif
 #ifndef SKV_FX_NT
 #define SKV_FX_NT 1                      // 1: non-temporal output stores in the fused copy
@@ -169,6 +169,12 @@ struct FxArgs {
     uint32_t* tcounter;           // tile ticket (zeroed per call)
     uint64_t* Kout;               // surviving records
     uint64_t* prof;               // SKV_TILE_PROF builds: per-phase ticks of the fused tiles (16 counters)
+    // in-tile bounds (inb != 0): each tile searches its own segment bounds (k_fx_bounds' search)
+    // instead of reading bnd[]; the sorted level-1 samples (every m-th is a splitter) and each
+    // stream's own level-1 samples (every Sstep-th record, offsets l1off)
+    const uint64_t *shi, *slo, *l1hi, *l1lo, *l1off;
+    uint64_t m, Sstep;
+    uint32_t inb, pad2;
 };
 // flags[3] reason bits of a poisoned fused call
 enum : uint32_t { FXR_RECORD = 1, FXR_OVERSIZE = 2, FXR_SPLIT = 4, FXR_ORDER = 8, FXR_SAMPLE = 16 };

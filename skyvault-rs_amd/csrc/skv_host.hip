@@ -474,7 +474,12 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
     lv[0].N = R;
     lv[0].off = stream_base;
     lv[0].d_off = d_sbase;
-    const uint64_t S_step = std::max<uint64_t>(2, (uint64_t)FX_TARGET / std::max<uint32_t>(k, 1));
+    // level-1 sample spacing: FX_TARGET/k records gives ~k samples between splitters, whose
+    // sampling noise spreads tile sizes by ~1/sqrt(k) (a few streams of a few thousand records
+    // reached 1.5x the target, above FX_CAP); small inputs sample densely (>= 256 per tile),
+    // where the extra samples cost nothing
+    const uint64_t S_step = std::max<uint64_t>(
+        2, (uint64_t)FX_TARGET / std::max<uint32_t>(R >= (1ull << 22) ? k : std::max<uint32_t>(k, 256), 1));
     while (lv.back().N > (uint64_t)FX_CAP) {
         const Level& P = lv.back();
         Level L;
@@ -528,10 +533,24 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
                            d_flags + 2));
     }
     A.T = T0;
-    A.bnd = dbuf<FxBound>(ctx, "fx_bnd", (T0 + 1) * k);
     const bool l1 = lv.size() > 1;
-    launch_fx_bounds(st, A, l1 ? lv[1].shi : nullptr, l1 ? lv[1].slo : nullptr, m0, l1 ? lv[1].hi : nullptr,
-                     l1 ? lv[1].lo : nullptr, l1 ? lv[1].d_off : nullptr, S_step);
+    A.shi = l1 ? lv[1].shi : nullptr;
+    A.slo = l1 ? lv[1].slo : nullptr;
+    A.l1hi = l1 ? lv[1].hi : nullptr;
+    A.l1lo = l1 ? lv[1].lo : nullptr;
+    A.l1off = l1 ? lv[1].d_off : nullptr;
+    A.m = m0;
+    A.Sstep = S_step;
+    // k_fx_bounds searches every tile's bounds up front; SKV_FX_INB=1 lets each tile search its
+    // own instead (measured slower: the tile's dependent searches are not hidden by the other
+    // workgroups of its CU, +0.23 ms of tile time for -0.09 ms of k_fx_bounds at config 2A)
+    const char* inb_e = getenv("SKV_FX_INB");
+    const int inb_env = inb_e ? atoi(inb_e) : 0;
+    A.inb = (inb_env != 0 && k <= (uint32_t)FX_CAP) ? 1u : 0u;
+    if (!A.inb) {
+        A.bnd = dbuf<FxBound>(ctx, "fx_bnd", (T0 + 1) * k);
+        launch_fx_bounds(st, A, A.shi, A.slo, m0, A.l1hi, A.l1lo, A.l1off, S_step);
+    }
     A.tstate = dbuf<uint64_t>(ctx, "fx_tstate", T0);
     A.tcounter = dbuf<uint32_t>(ctx, "tile_ticket", 1);
     HIPCHK(hipMemsetAsync(A.tstate, 0, T0 * 8, st));

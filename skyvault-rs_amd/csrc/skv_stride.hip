@@ -119,6 +119,21 @@ __device__ __forceinline__ uint4 fx_ld16(uint64_t a) {  // unaligned: full rate 
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+#ifndef SKV_FX_XMASK
+#define SKV_FX_XMASK 1  // 1: the copy's second load only on straddling lanes (exec mask)
+#endif
+#ifndef SKV_FX_NTL
+#define SKV_FX_NTL 0  // 1: non-temporal loads in the copy (the bytes are read once there)
+#endif
+__device__ __forceinline__ uint4 fx_cld16(uint64_t a) {  // the copy's loads
+#if SKV_FX_NTL
+    const fx_v4 v = __builtin_nontemporal_load((fx_g16*)a);
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return fx_ld16(a);
+#endif
+}
+
 // One record's header pieces: marker + key_len (bytes 0..7), the 16 bytes from the key start,
 // val_len (at 5 + K). All inside the record (S >= 32), issued as three independent loads.
 struct FxRec {
@@ -237,20 +252,11 @@ __device__ __forceinline__ uint64_t fx_lower_bound8(uint64_t lo, uint64_t hi, Be
     return lo;
 }
 
-// bnd[t*k + j].pos = first record of stream j whose key >= splitter t (sorted level-1 samples,
-// every m-th one), plus what tile t needs to start its segment without further searches: the
-// record's address, the records left in its member run, and the key of the record before it
-// (the in-stream order check across tile edges, runs.rs:190-198). One thread per (t, j): a 9-ary
-// search over stream j's own level-1 samples (every Sstep-th record, L2-resident) narrows the
-// bound to one sample gap, then a 9-ary search over the records of that gap.
-__global__ void k_fx_bounds(FxArgs A, const uint64_t* __restrict__ shi, const uint64_t* __restrict__ slo, uint64_t m,
-                            const uint64_t* __restrict__ l1hi, const uint64_t* __restrict__ l1lo,
-                            const uint64_t* __restrict__ l1off, uint64_t Sstep) {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t k = A.k;
-    if (g >= (A.T + 1) * k) return;
-    const uint64_t t = g / k;
-    const uint32_t j = (uint32_t)(g - t * k);
+template <bool FULL>
+__device__ __forceinline__ FxBound fx_bound(const FxArgs& A, const uint64_t* __restrict__ shi,
+                                            const uint64_t* __restrict__ slo, uint64_t m,
+                                            const uint64_t* __restrict__ l1hi, const uint64_t* __restrict__ l1lo,
+                                            const uint64_t* __restrict__ l1off, uint64_t Sstep, uint64_t t, uint32_t j) {
     const uint64_t s0 = A.stream_base[j], s1 = A.stream_base[j + 1];
     uint64_t a = s0;
     if (t == A.T) {
@@ -259,8 +265,7 @@ __global__ void k_fx_bounds(FxArgs A, const uint64_t* __restrict__ shi, const ui
         if (__hip_atomic_load(A.flags + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
             FxBound o{};
             o.pos = s0;
-            A.bnd[g] = o;
-            return;
+            return o;
         }
         const uint64_t h = shi[t * m], l = slo[t * m];
         const uint64_t q0 = l1off[j], q1 = l1off[j + 1];
@@ -293,6 +298,7 @@ __global__ void k_fx_bounds(FxArgs A, const uint64_t* __restrict__ shi, const ui
     }
     FxBound o{};
     o.pos = a;
+    if (!FULL) return o;
     if (a < s1) {
         const uint32_t r = fx_run(A, j, a);
         o.addr = A.runs[r].ptr + 1 + (a - A.run_recb[r]) * A.S;
@@ -302,7 +308,24 @@ __global__ void k_fx_bounds(FxArgs A, const uint64_t* __restrict__ shi, const ui
         o.has_prev = 1;
         fx_key(A, fx_addr(A, j, a - 1), o.ph, o.pl);
     }
-    A.bnd[g] = o;
+    return o;
+}
+
+// bnd[t*k + j].pos = first record of stream j whose key >= splitter t (sorted level-1 samples,
+// every m-th one), plus what tile t needs to start its segment without further searches: the
+// record's address, the records left in its member run, and the key of the record before it
+// (the in-stream order check across tile edges, runs.rs:190-198). One thread per (t, j): a 9-ary
+// search over stream j's own level-1 samples (every Sstep-th record, L2-resident) narrows the
+// bound to one sample gap, then a binary search over the records of that gap.
+__global__ void k_fx_bounds(FxArgs A, const uint64_t* __restrict__ shi, const uint64_t* __restrict__ slo, uint64_t m,
+                            const uint64_t* __restrict__ l1hi, const uint64_t* __restrict__ l1lo,
+                            const uint64_t* __restrict__ l1off, uint64_t Sstep) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t k = A.k;
+    if (g >= (A.T + 1) * k) return;
+    const uint64_t t = g / k;
+    const uint32_t j = (uint32_t)(g - t * k);
+    A.bnd[g] = fx_bound<true>(A, shi, slo, m, l1hi, l1lo, l1off, Sstep, t, j);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -431,9 +454,10 @@ struct FxBatch {
     uint32_t b;
 };
 // addresses of the batch's U blocks (b, b + FX_THREADS, ...) and their loads, issued together.
-// Branch-free where memory is touched: every block issues both loads (a block that does not
-// straddle a record end re-reads its own address, an L1 hit) and blocks past nb load `safe`, so
-// the waitcnt pass sees the same count on every path and can leave later batches in flight.
+// No branches where memory is touched: blocks past nb load `safe`, and the second load (X, the
+// next record's head) is exec-masked to the lanes whose block straddles a record end (~6 % at
+// 281-byte records), so the waitcnt pass sees the same count on every path and can leave later
+// batches in flight. Issuing X on every lane (re-reading its own address) cost 9 % of the tile.
 template <int U>
 __device__ __forceinline__ void fx_plan(FxBatch<U>& t, FxWalk& w, const uint64_t* src, uint32_t b, uint32_t nb,
                                         uint64_t safe) {
@@ -447,7 +471,7 @@ __device__ __forceinline__ void fx_plan(FxBatch<U>& t, FxWalk& w, const uint64_t
         ja = ja < (uint32_t)(FX_CAP - 1) ? ja : (uint32_t)(FX_CAP - 1);
         const uint64_t s0 = src[ja], s1 = src[ja + 1];
         uint64_t aL = vb ? s0 : s0 + (st ? w.S32 - 16 : w.o);
-        uint64_t aX = st ? s1 : aL;
+        uint64_t aX = st ? s1 : aL;  // only a block that straddles a record end needs X
         t.aL[u] = valid ? aL : 0;
         t.aX[u] = valid ? aX : safe;
         if (!valid) aL = aX = safe;
@@ -465,8 +489,17 @@ __device__ __forceinline__ void fx_plan(FxBatch<U>& t, FxWalk& w, const uint64_t
             w.o = z ? w.S32 - 1 : w.o - 1;
             w.j = z ? w.j - 1 : w.j;
         }
-        t.L[u] = fx_ld16(aL);
-        t.X[u] = fx_ld16(aX);
+        t.L[u] = fx_cld16(aL);
+#if SKV_FX_DIAG_1LD  // diagnostic (output invalid at record ends): no second load
+        t.X[u] = t.L[u];
+        (void)aX;
+#elif SKV_FX_XMASK  // second load only on the lanes that straddle (exec-masked)
+        uint4 xv = make_uint4(0, 0, 0, 0);
+        if (st && valid) xv = fx_cld16(aX);
+        t.X[u] = xv;
+#else
+        t.X[u] = fx_cld16(aX);
+#endif
     }
 }
 __device__ __forceinline__ uint4 fx_sel4(bool c, uint4 a, uint4 b) {  // c ? a : b, per dword
@@ -547,13 +580,42 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     do {
     // ---- segments: stream j contributes its records [bnd[t][j].pos, bnd[t+1][j].pos)
     uint64_t tot = 0;
+    uint64_t* ib_end = (uint64_t*)key;  // in-tile bounds: end pos, then rem, per stream (key is free here)
+    uint64_t* ib_rem = ib_end + k;
+    if (A.inb && !s_dead) {
+        // both bounds of every stream, searched by 2k lanes at once (latency only: the other
+        // workgroups of the CU keep streaming meanwhile)
+        for (uint32_t x = tid; x < 2 * k; x += FX_THREADS) {
+            if (x < k) {
+                const FxBound b = fx_bound<true>(A, A.shi, A.slo, A.m, A.l1hi, A.l1lo, A.l1off, A.Sstep, t, x);
+                sbase[x] = b.pos;
+                segaddr[x] = b.addr;
+                ib_rem[x] = b.rem;
+                prevk[x] = make_ulong2(b.ph, b.pl);
+                prevok[x] = (uint8_t)b.has_prev;
+            } else {
+                const uint32_t j = x - k;
+                ib_end[j] = fx_bound<false>(A, A.shi, A.slo, A.m, A.l1hi, A.l1lo, A.l1off, A.Sstep, t + 1, j).pos;
+            }
+        }
+        __syncthreads();
+    }
     if (!s_dead) {
         for (uint32_t j0 = 0; j0 < k; j0 += FX_THREADS) {
             const uint32_t j = j0 + tid;
             uint64_t len = 0;
             if (j < k) {
-                const FxBound b = A.bnd[t * k + j];
-                uint64_t b1 = A.bnd[(t + 1) * k + j].pos;
+                FxBound b;
+                uint64_t b1;
+                if (A.inb) {
+                    b.pos = sbase[j];
+                    b.addr = segaddr[j];
+                    b.rem = ib_rem[j];
+                    b1 = ib_end[j];
+                } else {
+                    b = A.bnd[t * k + j];
+                    b1 = A.bnd[(t + 1) * k + j].pos;
+                }
                 if (b1 < b.pos) {  // splitters over unsorted input
                     atomicOr(&s_bad, FXR_SPLIT);
                     b1 = b.pos;
@@ -561,8 +623,10 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
                 len = b1 - b.pos;
                 sbase[j] = b.pos;
                 segaddr[j] = len <= b.rem ? b.addr : 0;  // 0: the segment spans member runs
-                prevk[j] = make_ulong2(b.ph, b.pl);
-                prevok[j] = (uint8_t)b.has_prev;
+                if (!A.inb) {
+                    prevk[j] = make_ulong2(b.ph, b.pl);
+                    prevok[j] = (uint8_t)b.has_prev;
+                }
                 if (len > FX_CAP) len = FX_CAP + 1;
             }
             uint64_t part;
@@ -890,8 +954,8 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
         uint4 L[U], X[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            L[u] = aL[u] ? fx_ld16(aL[u]) : make_uint4(0, 0, 0, 0);
-            X[u] = aX[u] ? fx_ld16(aX[u]) : make_uint4(0, 0, 0, 0);
+            L[u] = aL[u] ? fx_cld16(aL[u]) : make_uint4(0, 0, 0, 0);
+            X[u] = aX[u] ? fx_cld16(aX[u]) : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
