@@ -175,6 +175,8 @@ struct FxArgs {
     const uint64_t *shi, *slo, *l1hi, *l1lo, *l1off;
     uint64_t m, Sstep;
     uint32_t inb, pad2;
+    const uint32_t* l1cnt;        // (T + 1) x k: stream j's level-1 samples sorted before splitter t
+                                  // (k_fx_l1cnt), or null: k_fx_bounds searches them
 };
 // flags[3] reason bits of a poisoned fused call
 enum : uint32_t { FXR_RECORD = 1, FXR_OVERSIZE = 2, FXR_SPLIT = 4, FXR_ORDER = 8, FXR_SAMPLE = 16 };

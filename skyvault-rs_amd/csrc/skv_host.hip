@@ -547,6 +547,12 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
     const char* inb_e = getenv("SKV_FX_INB");
     const int inb_env = inb_e ? atoi(inb_e) : 0;
     A.inb = (inb_env != 0 && k <= (uint32_t)FX_CAP) ? 1u : 0u;
+    if (l1 && T0 > 1) {  // per (splitter, stream) sample counts: k_fx_bounds skips its sample search
+        uint32_t* posof = dbuf<uint32_t>(ctx, "fx_posof", lv[1].N);
+        uint32_t* cnt = dbuf<uint32_t>(ctx, "fx_l1cnt", (T0 + 1) * k);
+        launch_fx_l1cnt(st, A, lv[1].sc, lv[1].N, posof, cnt);
+        A.l1cnt = cnt;
+    }
     if (!A.inb) {
         A.bnd = dbuf<FxBound>(ctx, "fx_bnd", (T0 + 1) * k);
         launch_fx_bounds(st, A, A.shi, A.slo, m0, A.l1hi, A.l1lo, A.l1off, S_step);

@@ -269,10 +269,18 @@ __device__ __forceinline__ FxBound fx_bound(const FxArgs& A, const uint64_t* __r
         }
         const uint64_t h = shi[t * m], l = slo[t * m];
         const uint64_t q0 = l1off[j], q1 = l1off[j + 1];
-        const uint64_t c = fx_lower_bound8(q0, q1, [&](uint64_t i) {
-                               const uint64_t eh = l1hi[i], el = l1lo[i];
-                               return eh < h || (eh == h && el < l);
-                           }) - q0;
+        uint64_t c;
+        if (A.l1cnt) {
+            // the samples of stream j sorted before the splitter, minus those equal to it (they
+            // sort on either side of it; lower_bound counts only the smaller ones)
+            c = A.l1cnt[t * A.k + j];
+            while (c > 0 && l1hi[q0 + c - 1] == h && l1lo[q0 + c - 1] == l) --c;
+        } else {
+            c = fx_lower_bound8(q0, q1, [&](uint64_t i) {
+                    const uint64_t eh = l1hi[i], el = l1lo[i];
+                    return eh < h || (eh == h && el < l);
+                }) - q0;
+        }
         if (c > 0) {
             const uint64_t lo = s0 + (c - 1) * Sstep + 1;
             const uint64_t hi = s0 + c * Sstep < s1 ? s0 + c * Sstep : s1;
@@ -309,6 +317,45 @@ __device__ __forceinline__ FxBound fx_bound(const FxArgs& A, const uint64_t* __r
         fx_key(A, fx_addr(A, j, a - 1), o.ph, o.pl);
     }
     return o;
+}
+
+// Level-1 sample counts per (splitter, stream) from the sorted samples' positions: sorted sample
+// p is stream j's c-th sample (record pos = the low half of sc[p]); posof[l1off[j] + c] = p.
+__global__ void k_fx_posof(FxArgs A, const uint64_t* __restrict__ sc, uint64_t N1, uint32_t* posof) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N1) return;
+    const uint64_t pos = sc[p] & 0xFFFFFFFFull;
+    uint32_t lo = 0, hi = A.k;  // stream j: stream_base[j] <= pos < stream_base[j + 1]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (A.stream_base[mid] <= pos) lo = mid;
+        else hi = mid;
+    }
+    const uint64_t q = A.l1off[lo] + (pos - A.stream_base[lo]) / A.Sstep;
+    if (q < A.l1off[lo + 1]) posof[q] = (uint32_t)p;
+}
+// cnt[t*k + j] = stream j's samples at sorted positions < t*m (splitter t is sample t*m): sample c
+// at position p, next one at pn, is the last one before splitters t with p < t*m <= pn; every
+// (t, j) with t in [1, T) is written exactly once (c = 0 also covers the splitters before it).
+__global__ void k_fx_l1cnt(FxArgs A, const uint32_t* __restrict__ posof, uint64_t N1, uint32_t* cnt) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= N1) return;
+    uint32_t lo = 0, hi = A.k;  // stream j: l1off[j] <= q < l1off[j + 1]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (A.l1off[mid] <= q) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t j = lo, k = A.k;
+    const uint64_t c = q - A.l1off[j], m = A.m, T = A.T;
+    const uint64_t p = posof[q];
+    const uint64_t tmax = T - 1;
+    const uint64_t t_hi0 = p / m < tmax ? p / m : tmax;  // splitters at or before p: nothing of j's below
+    if (c == 0)
+        for (uint64_t t = 1; t <= t_hi0; ++t) cnt[t * k + j] = 0;
+    const uint64_t pn = q + 1 < A.l1off[j + 1] ? posof[q + 1] : ~0ull;
+    const uint64_t t_hi = pn == ~0ull ? tmax : (pn / m < tmax ? pn / m : tmax);
+    for (uint64_t t = p / m + 1; t <= t_hi; ++t) cnt[t * k + j] = (uint32_t)(c + 1);
 }
 
 // bnd[t*k + j].pos = first record of stream j whose key >= splitter t (sorted level-1 samples,
@@ -546,7 +593,14 @@ __device__ __forceinline__ void fx_finish(const FxBatch<U>& t, uint8_t* ob) {
 // LDS: key[FX_CAP] 16 B (by position; after the merge: source addresses by survivor, u64)
 //      | prevk[k] 16 B | segaddr[k] sbase[k] u64 | cb0[k+1] cbA[k+1] cbB[k+1] u32 | id[FX_CAP] u16
 //      | prevok[k] u8
+#ifndef SKV_FX_WAVES
+#define SKV_FX_WAVES 0  // >0: amdgpu_waves_per_eu floor for k_fx_tile (8 caps it at 64 VGPRs)
+#endif
+#if SKV_FX_WAVES
+__global__ void __launch_bounds__(FX_THREADS) __attribute__((amdgpu_waves_per_eu(SKV_FX_WAVES))) k_fx_tile(FxArgs A) {
+#else
 __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
+#endif
     constexpr int PER = FX_CAP / FX_THREADS;
     extern __shared__ __attribute__((aligned(16))) uint64_t fx_smem[];
     const uint32_t k = A.k;
@@ -1015,6 +1069,11 @@ static inline unsigned fx_blocks(uint64_t n, unsigned t) { return (unsigned)((n 
 void launch_fx_sample(hipStream_t s, const FxArgs& A, const uint64_t* off_dst, uint64_t Sstep, uint64_t n_dst,
                       uint64_t* dhi, uint64_t* dlo, uint64_t* dc) {
     if (n_dst) k_fx_sample<<<fx_blocks(n_dst, 256), 256, 0, s>>>(A, off_dst, Sstep, n_dst, dhi, dlo, dc);
+}
+void launch_fx_l1cnt(hipStream_t s, const FxArgs& A, const uint64_t* sc, uint64_t N1, uint32_t* posof, uint32_t* cnt) {
+    if (!N1) return;
+    k_fx_posof<<<fx_blocks(N1, 256), 256, 0, s>>>(A, sc, N1, posof);
+    k_fx_l1cnt<<<fx_blocks(N1, 256), 256, 0, s>>>(A, posof, N1, cnt);
 }
 void launch_fx_bounds(hipStream_t s, const FxArgs& A, const uint64_t* shi, const uint64_t* slo, uint64_t m,
                       const uint64_t* l1hi, const uint64_t* l1lo, const uint64_t* l1off, uint64_t Sstep) {
