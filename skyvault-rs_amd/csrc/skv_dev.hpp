@@ -499,7 +499,10 @@ struct RecHdr {
 // from one 32-byte window plus (only for long keys / non-ASCII keys) further loads.
 // UTF8 = false: the record was already validated by a walk (k_emit re-reads records that
 // k_spec / k_fixup walked with every check)
-template <bool PREFIX, bool UTF8 = true>
+// UTF8: 0 no key check (structure only), 1 the exact check, 2 a heuristic for speculative chunk
+// starts (a key whose in-window bytes are ASCII passes unchecked; any other key gets the exact
+// check): random bytes taken for a record fail it, real keys cost no extra loads
+template <bool PREFIX, int UTF8 = 1>
 __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, uint64_t p) {
     RecHdr h;
     h.size = 0;
@@ -513,7 +516,8 @@ __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, ui
     if (kp + h.klen > len) { h.err = DERR_KEY; return h; }
     uint32_t kd[7];
     win_key(w, kd);
-    bool ok = !UTF8 || (h.klen <= 27 && ascii_prefix(kd, (uint32_t)h.klen));
+    bool ok = UTF8 == 0 || (UTF8 == 2 ? ascii_prefix(kd, h.klen < 27 ? (uint32_t)h.klen : 27u)
+                                      : (h.klen <= 27 && ascii_prefix(kd, (uint32_t)h.klen)));
     if (!ok) ok = utf8_valid_fast(run + kp, h.klen);
     if (!ok) { h.err = DERR_UTF8; return h; }
     if (PREFIX) win_prefix(kd, h.klen, h.hi, h.lo);
@@ -540,7 +544,7 @@ __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, ui
 
 // walk_checked with vectorized headers: one dependent round trip per record. UTF8 = false: the
 // structure only (k_spec's fast mode; k_emit checks the keys and flags a bad one for an exact rerun)
-template <bool UTF8 = true>
+template <int UTF8 = 1>
 __device__ inline WalkRes walk_fast(const uint8_t* run, uint64_t len, uint64_t p, uint64_t stop, uint32_t max_recs) {
     uint32_t cnt = 0;
     while (p < stop && cnt < max_recs) {
@@ -551,6 +555,7 @@ __device__ inline WalkRes walk_fast(const uint8_t* run, uint64_t len, uint64_t p
     }
     return {p, cnt, DERR_NONE};
 }
+
 
 // 64-bit fingerprint of the key bytes past the 16-byte prefix (0 for keys of at most 16 bytes),
 // a function of the bytes alone; ascii: those bytes have no high bit
@@ -569,14 +574,29 @@ __device__ inline uint64_t key_tail_fp(const uint8_t* key, uint32_t klen, bool& 
     const uint32_t n = klen - 16;
     uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
     uint32_t acc = 0;
-    for (uint32_t o = 0; o < n; o += 16) {
-        const uint32_t m = n - o < 16 ? n - o : 16;
-        const uint4 v = load_window16(k + o, m);
-        const uint32_t a0 = v.x & dword_mask(0, m, 0), a1 = v.y & dword_mask(0, m, 1);
-        const uint32_t a2 = v.z & dword_mask(0, m, 2), a3 = v.w & dword_mask(0, m, 3);
-        acc |= a0 | a1 | a2 | a3;
-        h = fp_mix(h ^ (((uint64_t)a1 << 32) | a0));
-        h = fp_mix(h ^ (((uint64_t)a3 << 32) | a2) ^ 0x2545F4914F6CDD1Dull);
+    // 16-byte windows at k + o, assembled from aligned blocks (an aligned block holding a key byte
+    // never leaves the run's pages): five block loads per four windows, issued together
+    const uintptr_t a = (uintptr_t)k;
+    const uint4* base = (const uint4*)(a & ~(uintptr_t)15);
+    const uint32_t sh = (uint32_t)(a & 15);
+    const uint32_t nblk = (sh + n + 15) >> 4;
+    for (uint32_t o = 0; o < n; o += 64) {
+        const uint32_t q0 = o >> 4;
+        uint4 B[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) B[i] = q0 + i < nblk ? base[q0 + i] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            if (o + 16 * w < n) {
+                const uint32_t m = n - o - 16 * w < 16 ? n - o - 16 * w : 16;
+                const uint4 v = funnel16(B[w], B[w + 1], sh);
+                const uint32_t a0 = v.x & dword_mask(0, m, 0), a1 = v.y & dword_mask(0, m, 1);
+                const uint32_t a2 = v.z & dword_mask(0, m, 2), a3 = v.w & dword_mask(0, m, 3);
+                acc |= a0 | a1 | a2 | a3;
+                h = fp_mix(h ^ (((uint64_t)a1 << 32) | a0));
+                h = fp_mix(h ^ (((uint64_t)a3 << 32) | a2) ^ 0x2545F4914F6CDD1Dull);
+            }
+        }
     }
     ascii = (acc & 0x80808080u) == 0;
     return h;

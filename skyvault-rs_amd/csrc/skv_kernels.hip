@@ -113,7 +113,8 @@ __global__ void k_run_header(const RunInfo* runs, uint32_t n_runs, uint32_t* hdr
 // Speculative start of chunk `local` (> 0): a record start must lie in [cs, ce). Scan for the
 // first position whose next three records decode cleanly. Wrong guesses are caught by
 // k_validate and repaired by k_fixup.
-__device__ uint64_t spec_start(const uint8_t* run, uint64_t len, uint64_t cs, uint64_t ce, bool utf8) {
+template <int UTF8>
+__device__ uint64_t spec_start(const uint8_t* run, uint64_t len, uint64_t cs, uint64_t ce) {
     for (uint64_t p0 = cs; p0 < ce; p0 += 16) {  // 16 bytes per load; marker candidates as a mask
         const uint32_t m = (uint32_t)(ce - p0 < 16 ? ce - p0 : 16);
         const uint4 v = load_window16(run + p0, m);
@@ -127,7 +128,9 @@ __device__ uint64_t spec_start(const uint8_t* run, uint64_t len, uint64_t cs, ui
         while (cand) {
             const uint32_t i = __builtin_ctz(cand);
             cand &= cand - 1;
-            WalkRes r = utf8 ? walk_fast<true>(run, len, p0 + i, len, 3) : walk_fast<false>(run, len, p0 + i, len, 3);
+            // candidates are checked with the keys (the heuristic form in the structure-only mode),
+            // which rejects random bytes taken for a record far more often than structure alone
+            const WalkRes r = walk_fast<UTF8 ? 1 : 2>(run, len, p0 + i, len, 3);
             if (r.err == DERR_NONE) return p0 + i;
         }
     }
@@ -151,9 +154,10 @@ __device__ __forceinline__ bool fixed_rec_ok(const uint8_t* run, uint64_t len, u
     return vlen == f.V;
 }
 
+template <int UTF8>
 __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
                        const uint32_t* __restrict__ hdr_err, const RunFmt* __restrict__ fmt, uint32_t* run_broken,
-                       uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, bool utf8) {
+                       uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err) {
     uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
     uint32_t r = find_run(runs, n_runs, c);
@@ -202,7 +206,7 @@ __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         atomicOr(&run_broken[r], 1u);  // hypothesis broken: this run takes the general path
         start = p0;
     } else {
-        start = local == 0 ? 1 : spec_start(run, R.len, cs, ce, utf8);
+        start = local == 0 ? 1 : spec_start<UTF8>(run, R.len, cs, ce);
     }
     if (start == NO_POS) {
         ch_start[c] = NO_POS;
@@ -211,8 +215,7 @@ __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         ch_err[c] = 0;
         return;
     }
-    WalkRes w = utf8 ? walk_fast<true>(run, R.len, start, ce, 0xFFFFFFFFu)
-                     : walk_fast<false>(run, R.len, start, ce, 0xFFFFFFFFu);
+    const WalkRes w = walk_fast<UTF8>(run, R.len, start, ce, 0xFFFFFFFFu);
     ch_start[c] = start;
     ch_end[c] = w.end;
     ch_cnt[c] = w.cnt;
@@ -271,8 +274,7 @@ __global__ void k_fixup(const RunInfo* __restrict__ runs, uint32_t n_runs, const
         uint64_t end = E;
         uint32_t cnt = 0, err = 0;
         if (E < ce) {
-            WalkRes w = utf8 ? walk_fast<true>(run, R.len, E, ce, 0xFFFFFFFFu)
-                             : walk_fast<false>(run, R.len, E, ce, 0xFFFFFFFFu);
+            WalkRes w = utf8 ? walk_fast<1>(run, R.len, E, ce, 0xFFFFFFFFu) : walk_fast<0>(run, R.len, E, ce, 0xFFFFFFFFu);
             end = w.end;
             cnt = w.cnt;
             err = w.err;
@@ -1790,9 +1792,13 @@ void launch_run_header(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint
 void launch_spec(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                  const RunFmt* fmt, uint32_t* run_broken, uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt,
                  uint32_t* ch_err, bool utf8) {
-    if (n_chunks)
-        k_spec<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, fmt, run_broken, ch_start,
-                                                         ch_end, ch_cnt, ch_err, utf8);
+    if (!n_chunks) return;
+    if (utf8)
+        k_spec<1><<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, fmt, run_broken, ch_start,
+                                                            ch_end, ch_cnt, ch_err);
+    else
+        k_spec<0><<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, fmt, run_broken, ch_start,
+                                                            ch_end, ch_cnt, ch_err);
 }
 void launch_validate(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                      const uint64_t* ch_start, const uint64_t* ch_end, const uint32_t* ch_err,
