@@ -169,12 +169,10 @@ struct FxArgs {
     uint32_t* tcounter;           // tile ticket (zeroed per call)
     uint64_t* Kout;               // surviving records
     uint64_t* prof;               // SKV_TILE_PROF builds: per-phase ticks of the fused tiles (16 counters)
-    // in-tile bounds (inb != 0): each tile searches its own segment bounds (k_fx_bounds' search)
-    // instead of reading bnd[]; the sorted level-1 samples (every m-th is a splitter) and each
-    // stream's own level-1 samples (every Sstep-th record, offsets l1off)
+    // k_fx_bounds' inputs: the sorted level-1 samples (every m-th is a splitter) and each stream's
+    // own level-1 samples (every Sstep-th record, offsets l1off)
     const uint64_t *shi, *slo, *l1hi, *l1lo, *l1off;
     uint64_t m, Sstep;
-    uint32_t inb, pad2;
     const uint32_t* l1cnt;        // (T + 1) x k: stream j's level-1 samples sorted before splitter t
                                   // (k_fx_l1cnt), or null: k_fx_bounds searches them
 };

@@ -541,22 +541,14 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
     A.l1off = l1 ? lv[1].d_off : nullptr;
     A.m = m0;
     A.Sstep = S_step;
-    // k_fx_bounds searches every tile's bounds up front; SKV_FX_INB=1 lets each tile search its
-    // own instead (measured slower: the tile's dependent searches are not hidden by the other
-    // workgroups of its CU, +0.23 ms of tile time for -0.09 ms of k_fx_bounds at config 2A)
-    const char* inb_e = getenv("SKV_FX_INB");
-    const int inb_env = inb_e ? atoi(inb_e) : 0;
-    A.inb = (inb_env != 0 && k <= (uint32_t)FX_CAP) ? 1u : 0u;
     if (l1 && T0 > 1) {  // per (splitter, stream) sample counts: k_fx_bounds skips its sample search
         uint32_t* posof = dbuf<uint32_t>(ctx, "fx_posof", lv[1].N);
         uint32_t* cnt = dbuf<uint32_t>(ctx, "fx_l1cnt", (T0 + 1) * k);
         launch_fx_l1cnt(st, A, lv[1].sc, lv[1].N, posof, cnt);
         A.l1cnt = cnt;
     }
-    if (!A.inb) {
-        A.bnd = dbuf<FxBound>(ctx, "fx_bnd", (T0 + 1) * k);
-        launch_fx_bounds(st, A, A.shi, A.slo, m0, A.l1hi, A.l1lo, A.l1off, S_step);
-    }
+    A.bnd = dbuf<FxBound>(ctx, "fx_bnd", (T0 + 1) * k);
+    launch_fx_bounds(st, A, A.shi, A.slo, m0, A.l1hi, A.l1lo, A.l1off, S_step);
     A.tstate = dbuf<uint64_t>(ctx, "fx_tstate", T0);
     A.tcounter = dbuf<uint32_t>(ctx, "tile_ticket", 1);
     HIPCHK(hipMemsetAsync(A.tstate, 0, T0 * 8, st));

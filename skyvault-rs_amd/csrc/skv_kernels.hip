@@ -1339,6 +1339,14 @@ __device__ __forceinline__ uint32_t gather_piece(const uint64_t* s_dst, uint32_t
     return lo;
 }
 
+// 16 bytes at a global address given as an integer, through the global address space (a flat
+// load would also count against lgkmcnt and serialise with every LDS read)
+typedef unsigned int g_v4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gld16(uint64_t a) {
+    const g_v4 v = *(const __attribute__((address_space(1))) g_v4*)a;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // An output block covering several pieces: each piece contributes bytes [a, b) of the block,
 // moved with at most two aligned 16-byte loads and merged under a byte mask. Blocks shared
 // with a neighbouring workgroup (segment edges) are written bytewise, only this segment's bytes.
@@ -1484,30 +1492,54 @@ __global__ void __launch_bounds__(GATHER_THREADS, SKV_GATHER_WAVES) k_gather(con
         }
         return false;
     };
+    // Per batch of U blocks: addresses from LDS first, then every load, then the stores — no
+    // branch around a load (the second load, the next record's head, is exec-masked to the lanes
+    // of case 2), so the waitcnt pass does not drain between blocks.
+    const uint64_t safe = (uint64_t)run_b;  // a readable address for lanes with nothing to load
     uint32_t it = 0;
     for (uint32_t qi = threadIdx.x; qi < nq; qi += U * step, it += U) {
-        uint4 v[U];
-        bool ok[U];
+        uint64_t aL[U], aX[U];
+        uint32_t sh[U];
+        bool ok[U], two[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t qq = qi + u * step;
-            ok[u] = false;
-            v[u] = make_uint4(0, 0, 0, 0);
-            if (qq < nq) {
-                ok[u] = fast_block(qq, v[u]);
-                if (!ok[u] && use_mask) slow |= 1u << (it + u);
-            }
+            const bool inq = qq < nq;
+            const uint32_t qc = inq ? qq : nq - 1;
+            const uint64_t B = (q0 + qc) << 4;
+            const bool inr = inq && B >= lo_b && B + 16 <= hi_b;
+            const uint32_t p = use_tbl ? s_tbl[qc] : gather_piece(s_dst, npieces, B);
+            const uint64_t d = s_dst[p], src = s_src[p], e = s_dst[p + 1];
+            const uint64_t len = e - d;
+            const bool c1 = src && e >= B + 16;  // (1) inside one record
+            const uint32_t pn = p + 1 < npieces ? p + 1 : p;
+            const uint64_t src2 = s_src[pn], len2 = s_dst[pn + 1] - s_dst[pn];
+            const bool c2 = !c1 && src && p + 1 < npieces && len >= 16 && src2 && len2 >= 16 && e + len2 >= B + 16;
+            ok[u] = inr && (c1 || c2);
+            two[u] = ok[u] && c2;
+            aL[u] = ok[u] ? (c1 ? src + (B - d) : src + len - 16) : safe;
+            aX[u] = src2;
+            sh[u] = 16u - (uint32_t)(e - B);  // case 2: bytes taken from the first record = e - B
+            if (inq && !ok[u] && use_mask) slow |= 1u << (it + u);
+        }
+        uint4 L[U], X[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            L[u] = gld16(aL[u]);
+            X[u] = make_uint4(0, 0, 0, 0);
+            if (two[u]) X[u] = gld16(aX[u]);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            const uint4 v = two[u] ? funnel16(L[u], X[u], sh[u] & 15u) : L[u];
             if (ok[u]) {
                 uint8_t* o = out + ((q0 + qi + u * step) << 4);
 #if SKV_GATHER_NT
                 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                u32x4 vv = {v[u].x, v[u].y, v[u].z, v[u].w};
+                u32x4 vv = {v.x, v.y, v.z, v.w};
                 __builtin_nontemporal_store(vv, (u32x4*)o);
 #else
-                *(uint4*)o = v[u];
+                *(uint4*)o = v;
 #endif
             }
         }

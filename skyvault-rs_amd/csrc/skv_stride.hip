@@ -634,42 +634,13 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     do {
     // ---- segments: stream j contributes its records [bnd[t][j].pos, bnd[t+1][j].pos)
     uint64_t tot = 0;
-    uint64_t* ib_end = (uint64_t*)key;  // in-tile bounds: end pos, then rem, per stream (key is free here)
-    uint64_t* ib_rem = ib_end + k;
-    if (A.inb && !s_dead) {
-        // both bounds of every stream, searched by 2k lanes at once (latency only: the other
-        // workgroups of the CU keep streaming meanwhile)
-        for (uint32_t x = tid; x < 2 * k; x += FX_THREADS) {
-            if (x < k) {
-                const FxBound b = fx_bound<true>(A, A.shi, A.slo, A.m, A.l1hi, A.l1lo, A.l1off, A.Sstep, t, x);
-                sbase[x] = b.pos;
-                segaddr[x] = b.addr;
-                ib_rem[x] = b.rem;
-                prevk[x] = make_ulong2(b.ph, b.pl);
-                prevok[x] = (uint8_t)b.has_prev;
-            } else {
-                const uint32_t j = x - k;
-                ib_end[j] = fx_bound<false>(A, A.shi, A.slo, A.m, A.l1hi, A.l1lo, A.l1off, A.Sstep, t + 1, j).pos;
-            }
-        }
-        __syncthreads();
-    }
     if (!s_dead) {
         for (uint32_t j0 = 0; j0 < k; j0 += FX_THREADS) {
             const uint32_t j = j0 + tid;
             uint64_t len = 0;
             if (j < k) {
-                FxBound b;
-                uint64_t b1;
-                if (A.inb) {
-                    b.pos = sbase[j];
-                    b.addr = segaddr[j];
-                    b.rem = ib_rem[j];
-                    b1 = ib_end[j];
-                } else {
-                    b = A.bnd[t * k + j];
-                    b1 = A.bnd[(t + 1) * k + j].pos;
-                }
+                const FxBound b = A.bnd[t * k + j];
+                uint64_t b1 = A.bnd[(t + 1) * k + j].pos;
                 if (b1 < b.pos) {  // splitters over unsorted input
                     atomicOr(&s_bad, FXR_SPLIT);
                     b1 = b.pos;
@@ -677,10 +648,8 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
                 len = b1 - b.pos;
                 sbase[j] = b.pos;
                 segaddr[j] = len <= b.rem ? b.addr : 0;  // 0: the segment spans member runs
-                if (!A.inb) {
-                    prevk[j] = make_ulong2(b.ph, b.pl);
-                    prevok[j] = (uint8_t)b.has_prev;
-                }
+                prevk[j] = make_ulong2(b.ph, b.pl);
+                prevok[j] = (uint8_t)b.has_prev;
                 if (len > FX_CAP) len = FX_CAP + 1;
             }
             uint64_t part;
