@@ -299,16 +299,26 @@ __device__ inline void key_prefix(const uint8_t* k, uint64_t klen, uint64_t& hi,
 }
 
 
+// The aligned 16-byte block at global address a. Run bytes and every device buffer these helpers
+// read live in global memory: loading through the global address space keeps the loads off
+// lgkmcnt (a flat load counts against both counters and serialises with every LDS wait of the
+// kernels that merge in LDS).
+typedef unsigned int gblk_v4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gblk(uintptr_t a) {
+    const gblk_v4 v = *(const __attribute__((address_space(1))) gblk_v4*)a;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // 16 bytes from an arbitrary (unaligned) address using two aligned 16-byte loads. The second
 // aligned block contains p+15, so it holds at least one byte the caller owns and never crosses
 // into an unmapped page.
 __device__ __forceinline__ uint4 load16_unaligned(const uint8_t* p) {
     uintptr_t a = (uintptr_t)p;
-    const uint4* base = (const uint4*)(a & ~(uintptr_t)15);
+    const uintptr_t base = a & ~(uintptr_t)15;
     uint32_t sh = (uint32_t)(a & 15);
-    uint4 x = base[0];
+    uint4 x = gblk(base);
     if (sh == 0) return x;
-    uint4 y = base[1];
+    uint4 y = gblk(base + 16);
     uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
     uint32_t q = sh >> 2, r = sh & 3;
     uint32_t s[5];
@@ -348,11 +358,11 @@ __device__ __forceinline__ uint4 funnel16(uint4 x, uint4 y, uint32_t sh) {
 // aligned 16-byte blocks holding a requested byte are read, so no page beyond them is touched.
 __device__ __forceinline__ uint4 load_window16(const uint8_t* p, uint32_t n) {
     uintptr_t a = (uintptr_t)p;
-    const uint4* b0 = (const uint4*)(a & ~(uintptr_t)15);
+    const uintptr_t b0 = a & ~(uintptr_t)15;
     uint32_t sh = (uint32_t)(a & 15);
-    uint4 x = b0[0];
+    uint4 x = gblk(b0);
     uint4 y = make_uint4(0, 0, 0, 0);
-    if (sh + n > 16) y = b0[1];
+    if (sh + n > 16) y = gblk(b0 + 16);
     return funnel16(x, y, sh);
 }
 
@@ -408,11 +418,10 @@ __device__ __forceinline__ void window32(const uint8_t* run, uint64_t len, uint6
     uintptr_t end = (uintptr_t)(run + len);
     uintptr_t base = a & ~(uintptr_t)15;
     uint32_t sh = (uint32_t)(a & 15);
-    const uint4* b = (const uint4*)base;
     uint4 z = make_uint4(0, 0, 0, 0);
-    uint4 b0 = b[0];
-    uint4 b1 = base + 16 < end ? b[1] : z;
-    uint4 b2 = (sh && base + 32 < end) ? b[2] : z;
+    uint4 b0 = gblk(base);
+    uint4 b1 = base + 16 < end ? gblk(base + 16) : z;
+    uint4 b2 = (sh && base + 32 < end) ? gblk(base + 32) : z;
     uint4 lo = funnel16(b0, b1, sh), hi = funnel16(b1, b2, sh);
     w[0] = lo.x; w[1] = lo.y; w[2] = lo.z; w[3] = lo.w;
     w[4] = hi.x; w[5] = hi.y; w[6] = hi.z; w[7] = hi.w;
@@ -460,7 +469,7 @@ __device__ inline bool utf8_valid_fast(const uint8_t* s, uint64_t n) {
     for (uintptr_t b = b0; b < b1; b += 64) {
         uint4 v[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = b + 16 * q < b1 ? *(const uint4*)(b + 16 * q) : make_uint4(0, 0, 0, 0);
+        for (int q = 0; q < 4; ++q) v[q] = b + 16 * q < b1 ? gblk(b + 16 * q) : make_uint4(0, 0, 0, 0);
         uint32_t acc = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -575,14 +584,14 @@ __device__ inline uint64_t key_tail_fp(const uint8_t* key, uint32_t klen, bool& 
     // 16-byte windows at k + o, assembled from aligned blocks (an aligned block holding a key byte
     // never leaves the run's pages): five block loads per four windows, issued together
     const uintptr_t a = (uintptr_t)k;
-    const uint4* base = (const uint4*)(a & ~(uintptr_t)15);
+    const uintptr_t base = a & ~(uintptr_t)15;
     const uint32_t sh = (uint32_t)(a & 15);
     const uint32_t nblk = (sh + n + 15) >> 4;
     for (uint32_t o = 0; o < n; o += 64) {
         const uint32_t q0 = o >> 4;
         uint4 B[5];
 #pragma unroll
-        for (int i = 0; i < 5; ++i) B[i] = q0 + i < nblk ? base[q0 + i] : make_uint4(0, 0, 0, 0);
+        for (int i = 0; i < 5; ++i) B[i] = q0 + i < nblk ? gblk(base + 16ull * (q0 + i)) : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
             if (o + 16 * w < n) {
