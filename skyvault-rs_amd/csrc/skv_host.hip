@@ -83,6 +83,7 @@ struct skv_ctx {
     // are reused from the start on every call (each call ends with a stream sync)
     std::vector<std::pair<uint8_t*, size_t>> up_chunks;
     size_t up_chunk = 0, up_off = 0;
+    std::vector<uint8_t> fx_blob;  // fused path: host image of its one table upload
     uint64_t syncs = 0;
     double sync_ms = 0;
     bool exact_keys = false;  // rerun after a fingerprint shortcut misordered a tile (never in practice)
@@ -425,23 +426,8 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
     const uint64_t R = recb[n_runs];
     std::vector<uint64_t> stream_base(k + 1);
     for (uint32_t s = 0; s <= k; ++s) stream_base[s] = recb[stream_first_run[s]];
-    uint64_t* d_recb = dbuf<uint64_t>(ctx, "run_recb", n_runs + 1);
-    uint32_t* d_srun = dbuf<uint32_t>(ctx, "fx_stream_run", k + 1);
-    uint64_t* d_sbase = dbuf<uint64_t>(ctx, "stream_base", k + 1);
-    uint32_t* d_flags = dbuf<uint32_t>(ctx, "flags", 4);
-    uint64_t* d_K = dbuf<uint64_t>(ctx, "K_out", 1);
-    h2d_up(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
-    h2d_up(ctx, d_srun, stream_first_run.data(), (k + 1) * 4);
-    h2d_up(ctx, d_sbase, stream_base.data(), (k + 1) * 8);
-    HIPCHK(hipMemsetAsync(d_flags, 0, 16, st));
-    HIPCHK(hipMemsetAsync(d_K, 0, 8, st));
-    mark(ctx, PH_PARSE);
 
     FxArgs A{};
-    A.runs = d_runs;
-    A.run_recb = d_recb;
-    A.stream_run = d_srun;
-    A.stream_base = d_sbase;
     A.k = k;
     A.K = f.K;
     A.V = f.V;
@@ -453,8 +439,6 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
     A.inv_S = 1.0 / (double)f.S;
     A.inv_W = 1.0 / (double)(n * f.S + 1);
     A.inv_n = 1.0 / (double)n;
-    A.flags = d_flags;
-    A.Kout = d_K;
 #if SKV_TILE_PROF
     A.prof = dbuf<uint64_t>(ctx, "tile_prof", 16);
     if (!ctx->prof_init) {
@@ -463,7 +447,10 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
     }
 #endif
 
-    // ---- splitters: level 1 sampled from the run bytes, higher levels as in the general path
+    // ---- splitters: level 1 sampled from the run bytes, higher levels as in the general path.
+    // The level sizes, the tile count and every host table are known before the first launch, so
+    // all tables and the zeroed state (flags, tile states, ticket) go up as ONE blob: one H2D
+    // copy in place of six copies and four fills.
     struct Level {
         uint64_t N = 0, S = 1;
         std::vector<uint64_t> off;
@@ -473,7 +460,6 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
     std::vector<Level> lv(1);
     lv[0].N = R;
     lv[0].off = stream_base;
-    lv[0].d_off = d_sbase;
     // level-1 sample spacing: FX_TARGET/k records gives ~k samples between splitters, whose
     // sampling noise spreads tile sizes by ~1/sqrt(k) (a few streams of a few thousand records
     // reached 1.5x the target, above FX_CAP); small inputs sample densely (>= 256 per tile),
@@ -492,29 +478,61 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
         }
         L.off[k] = acc;
         L.N = acc;
-        const int li = (int)lv.size();
-        char nm[64];
-        snprintf(nm, sizeof nm, "lv%d_hi", li); L.hi = dbuf<uint64_t>(ctx, nm, L.N);
-        snprintf(nm, sizeof nm, "lv%d_lo", li); L.lo = dbuf<uint64_t>(ctx, nm, L.N);
-        snprintf(nm, sizeof nm, "lv%d_c", li); L.c = dbuf<uint64_t>(ctx, nm, L.N);
-        snprintf(nm, sizeof nm, "lv%d_off", li); L.d_off = dbuf<uint64_t>(ctx, nm, k + 1);
-        h2d_up(ctx, L.d_off, L.off.data(), (k + 1) * 8);
-        if (li == 1) launch_fx_sample(st, A, L.d_off, L.S, L.N, L.hi, L.lo, L.c);
-        else launch_sample(st, false, P.hi, P.lo, P.c, nullptr, P.d_off, L.d_off, k, L.S, L.N, L.hi, L.lo, L.c);
         lv.push_back(L);
     }
     uint64_t T0 = 1, m0 = 1;
-    for (int li = (int)lv.size() - 1; li >= 0; --li) {
+    if (lv.size() > 1) {
+        m0 = std::max<uint64_t>(1, (uint64_t)FX_TARGET / lv[1].S);
+        T0 = std::max<uint64_t>(1, (lv[1].N + m0 - 1) / m0);
+    }
+    // blob layout (256-byte aligned pieces): readback words {runs, K, bytes} + flags[4] | K_out |
+    // ticket | recb | stream_run | stream_base | level offsets | tile states
+    std::vector<size_t> lv_off(lv.size(), 0);
+    size_t blob_n = 0;
+    auto piece = [&](size_t bytes) {
+        const size_t at = blob_n;
+        blob_n += (bytes + 255) & ~(size_t)255;
+        return at;
+    };
+    const size_t o_rb = piece(64), o_K = piece(8), o_tick = piece(4), o_recb = piece((n_runs + 1) * 8),
+                 o_srun = piece((k + 1) * 4), o_sbase = piece((k + 1) * 8);
+    for (size_t li = 1; li < lv.size(); ++li) lv_off[li] = piece((k + 1) * 8);
+    const size_t o_tstate = piece(T0 * 8);
+    std::vector<uint8_t>& blob = ctx->fx_blob;
+    blob.assign(blob_n, 0);
+    memcpy(blob.data() + o_recb, recb.data(), (n_runs + 1) * 8);
+    memcpy(blob.data() + o_srun, stream_first_run.data(), (k + 1) * 4);
+    memcpy(blob.data() + o_sbase, stream_base.data(), (k + 1) * 8);
+    for (size_t li = 1; li < lv.size(); ++li) memcpy(blob.data() + lv_off[li], lv[li].off.data(), (k + 1) * 8);
+    uint8_t* d_blob = dbuf<uint8_t>(ctx, "fx_blob", blob_n);
+    h2d_up(ctx, d_blob, blob.data(), blob_n);
+    uint64_t* d_rb = (uint64_t*)(d_blob + o_rb);        // k_fx_desc: {runs, K, record bytes}
+    uint32_t* d_flags = (uint32_t*)(d_blob + o_rb + 32);  // verdict flags, read back with d_rb
+    A.runs = d_runs;
+    A.run_recb = (uint64_t*)(d_blob + o_recb);
+    A.stream_run = (uint32_t*)(d_blob + o_srun);
+    A.stream_base = (uint64_t*)(d_blob + o_sbase);
+    A.flags = d_flags;
+    A.Kout = (uint64_t*)(d_blob + o_K);
+    lv[0].d_off = (uint64_t*)(d_blob + o_sbase);
+    mark(ctx, PH_PARSE);
+    for (size_t li = 1; li < lv.size(); ++li) {
+        Level& L = lv[li];
+        const Level& P = lv[li - 1];
+        char nm[64];
+        snprintf(nm, sizeof nm, "lv%d_hi", (int)li); L.hi = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "lv%d_lo", (int)li); L.lo = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "lv%d_c", (int)li); L.c = dbuf<uint64_t>(ctx, nm, L.N);
+        L.d_off = (uint64_t*)(d_blob + lv_off[li]);
+        if (li == 1) launch_fx_sample(st, A, L.d_off, L.S, L.N, L.hi, L.lo, L.c);
+        else launch_sample(st, false, P.hi, P.lo, P.c, nullptr, P.d_off, L.d_off, k, L.S, L.N, L.hi, L.lo, L.c);
+    }
+    for (int li = (int)lv.size() - 1; li >= 1; --li) {
         Level& L = lv[li];
         uint64_t T = 1, m = 1;
         if (li + 1 < (int)lv.size()) {
-            m = std::max<uint64_t>(1, (uint64_t)(li == 0 ? FX_TARGET : TILE_TARGET) / lv[li + 1].S);
+            m = std::max<uint64_t>(1, (uint64_t)TILE_TARGET / lv[li + 1].S);
             T = std::max<uint64_t>(1, (lv[li + 1].N + m - 1) / m);
-        }
-        if (li == 0) {
-            T0 = T;
-            m0 = m;
-            break;
         }
         char nm[64];
         snprintf(nm, sizeof nm, "bounds%d", li);
@@ -549,10 +567,8 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
     }
     A.bnd = dbuf<FxBound>(ctx, "fx_bnd", (T0 + 1) * k);
     launch_fx_bounds(st, A, A.shi, A.slo, m0, A.l1hi, A.l1lo, A.l1off, S_step);
-    A.tstate = dbuf<uint64_t>(ctx, "fx_tstate", T0);
-    A.tcounter = dbuf<uint32_t>(ctx, "tile_ticket", 1);
-    HIPCHK(hipMemsetAsync(A.tstate, 0, T0 * 8, st));
-    HIPCHK(hipMemsetAsync(A.tcounter, 0, 4, st));
+    A.tstate = (uint64_t*)(d_blob + o_tstate);  // zeroed by the blob upload
+    A.tcounter = (uint32_t*)(d_blob + o_tick);
     uint64_t total_rec_bytes = 0;
     for (const RunInfo& r : runs) total_rec_bytes += r.len;
     uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + R + 16);
@@ -563,18 +579,16 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
     mark(ctx, PH_MERGE);
     const uint64_t max_runs = (R + n - 1) / n;
     DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", max_runs + 1);
-    uint64_t* d_nruns = dbuf<uint64_t>(ctx, "n_runs", 4);
-    launch_fx_desc(st, A, d_desc, d_nruns, max_runs);
+    launch_fx_desc(st, A, d_desc, d_rb, max_runs);
     HIPCHK(hipGetLastError());
     mark(ctx, PH_CHAIN);
     mark(ctx, PH_GATHER);
     // ---- one readback: {runs, K, record bytes}, descriptors (count guessed from sizes), verdict
     const uint64_t guess = std::min<uint64_t>(max_runs, 64 + total_rec_bytes / (n * f.S));
-    uint8_t* hp = (uint8_t*)pinned(ctx, 64 + guess * sizeof(DevRunDesc) + 16);
-    uint8_t* hv = hp + 64 + guess * sizeof(DevRunDesc);
-    d2h(ctx, hp, d_nruns, 24);
+    uint8_t* hp = (uint8_t*)pinned(ctx, 64 + guess * sizeof(DevRunDesc));
+    uint8_t* hv = hp + 32;
+    d2h(ctx, hp, d_rb, 48);  // {runs, K, bytes} and the flags
     d2h(ctx, hp + 64, d_desc, guess * sizeof(DevRunDesc));
-    d2h(ctx, hv, d_flags, 16);
     sync(ctx);
     uint32_t hf[4];
     memcpy(hf, hv, 16);
