@@ -187,23 +187,30 @@ __device__ __forceinline__ void fx_poison(const FxArgs& A, uint32_t why) {
 // merges them (a merge of unsorted lists is not a permutation).
 __global__ void k_fx_sample(FxArgs A, const uint64_t* __restrict__ off_dst, uint64_t Sstep, uint64_t n_dst,
                             uint64_t* dhi, uint64_t* dlo, uint64_t* dc) {
+    extern __shared__ uint64_t fx_offs[];  // off_dst[0..k], staged once per workgroup
+    for (uint32_t x = threadIdx.x; x <= A.k; x += blockDim.x) fx_offs[x] = off_dst[x];
+    __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_dst) return;
+    const bool act = i < n_dst;
     uint32_t lo = 0, hi = A.k;
-    while (hi - lo > 1) {
+    while (act && hi - lo > 1) {
         uint32_t mid = (lo + hi) >> 1;
-        if (off_dst[mid] <= i) lo = mid;
+        if (fx_offs[mid] <= i) lo = mid;
         else hi = mid;
     }
-    const uint64_t pos = A.stream_base[lo] + (i - off_dst[lo]) * Sstep;
-    uint64_t h, l;
-    fx_key(A, fx_addr(A, lo, pos), h, l);
-    dhi[i] = h;
-    dlo[i] = l;
-    dc[i] = ((uint64_t)A.K << 32) | pos;
-    if (i > off_dst[lo]) {
-        uint64_t ph, pl;
-        fx_key(A, fx_addr(A, lo, pos - Sstep), ph, pl);
+    const uint64_t pos = A.stream_base[lo] + (i - fx_offs[lo]) * Sstep;
+    uint64_t h = 0, l = 0;
+    if (act) {
+        fx_key(A, fx_addr(A, lo, pos), h, l);
+        dhi[i] = h;
+        dlo[i] = l;
+        dc[i] = ((uint64_t)A.K << 32) | pos;
+    }
+    // per-stream sample order: sample i-1 of the same stream is the previous lane's key (one load
+    // per sample; the first lane of each wave loads its predecessor itself)
+    uint64_t ph = __shfl_up(h, 1, 64), pl = __shfl_up(l, 1, 64);
+    if (act && i > fx_offs[lo]) {
+        if ((threadIdx.x & 63) == 0) fx_key(A, fx_addr(A, lo, pos - Sstep), ph, pl);
         if (fx_gt(ph, pl, h, l)) fx_poison(A, FXR_SAMPLE);
     }
 }
@@ -259,6 +266,8 @@ __device__ __forceinline__ FxBound fx_bound(const FxArgs& A, const uint64_t* __r
                                             const uint64_t* __restrict__ l1off, uint64_t Sstep, uint64_t t, uint32_t j) {
     const uint64_t s0 = A.stream_base[j], s1 = A.stream_base[j + 1];
     uint64_t a = s0;
+    uint64_t pvh = 0, pvl = 0;  // key of record a - 1 when pv
+    bool pv = false;
     if (t == A.T) {
         a = s1;
     } else if (t > 0 && s1 > s0) {
@@ -282,6 +291,11 @@ __device__ __forceinline__ FxBound fx_bound(const FxArgs& A, const uint64_t* __r
                 }) - q0;
         }
         if (c > 0) {
+            // record lo - 1 is stream j's sample c - 1: its key is the previous key until the
+            // search moves past it (then the last probe below the splitter is)
+            pvh = l1hi[q0 + c - 1];
+            pvl = l1lo[q0 + c - 1];
+            pv = true;
             const uint64_t lo = s0 + (c - 1) * Sstep + 1;
             const uint64_t hi = s0 + c * Sstep < s1 ? s0 + c * Sstep : s1;
             const uint32_t r0 = A.stream_run[j];
@@ -299,8 +313,13 @@ __device__ __forceinline__ FxBound fx_bound(const FxArgs& A, const uint64_t* __r
                                     __builtin_bswap32(kk.y & dword_mask(0, A.K, 1));
                 const uint64_t el = ((uint64_t)__builtin_bswap32(kk.z & dword_mask(0, A.K, 2)) << 32) |
                                     __builtin_bswap32(kk.w & dword_mask(0, A.K, 3));
-                if (eh < h || (eh == h && el < l)) a = i + 1;
-                else b2 = i;
+                if (eh < h || (eh == h && el < l)) {
+                    a = i + 1;
+                    pvh = eh;
+                    pvl = el;
+                } else {
+                    b2 = i;
+                }
             }
         }
     }
@@ -314,7 +333,12 @@ __device__ __forceinline__ FxBound fx_bound(const FxArgs& A, const uint64_t* __r
     }
     if (a > s0 && t < A.T) {
         o.has_prev = 1;
-        fx_key(A, fx_addr(A, j, a - 1), o.ph, o.pl);
+        if (pv) {
+            o.ph = pvh;
+            o.pl = pvl;
+        } else {
+            fx_key(A, fx_addr(A, j, a - 1), o.ph, o.pl);
+        }
     }
     return o;
 }
@@ -322,38 +346,47 @@ __device__ __forceinline__ FxBound fx_bound(const FxArgs& A, const uint64_t* __r
 // Level-1 sample counts per (splitter, stream) from the sorted samples' positions: sorted sample
 // p is stream j's c-th sample (record pos = the low half of sc[p]); posof[l1off[j] + c] = p.
 __global__ void k_fx_posof(FxArgs A, const uint64_t* __restrict__ sc, uint64_t N1, uint32_t* posof) {
+    extern __shared__ uint64_t fx_tab[];  // stream_base[0..k] | l1off[0..k]
+    for (uint32_t x = threadIdx.x; x <= A.k; x += blockDim.x) {
+        fx_tab[x] = A.stream_base[x];
+        fx_tab[A.k + 1 + x] = A.l1off[x];
+    }
+    __syncthreads();
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= N1) return;
     const uint64_t pos = sc[p] & 0xFFFFFFFFull;
     uint32_t lo = 0, hi = A.k;  // stream j: stream_base[j] <= pos < stream_base[j + 1]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (A.stream_base[mid] <= pos) lo = mid;
+        if (fx_tab[mid] <= pos) lo = mid;
         else hi = mid;
     }
-    const uint64_t q = A.l1off[lo] + (pos - A.stream_base[lo]) / A.Sstep;
-    if (q < A.l1off[lo + 1]) posof[q] = (uint32_t)p;
+    const uint64_t q = fx_tab[A.k + 1 + lo] + (pos - fx_tab[lo]) / A.Sstep;
+    if (q < fx_tab[A.k + 2 + lo]) posof[q] = (uint32_t)p;
 }
 // cnt[t*k + j] = stream j's samples at sorted positions < t*m (splitter t is sample t*m): sample c
 // at position p, next one at pn, is the last one before splitters t with p < t*m <= pn; every
 // (t, j) with t in [1, T) is written exactly once (c = 0 also covers the splitters before it).
 __global__ void k_fx_l1cnt(FxArgs A, const uint32_t* __restrict__ posof, uint64_t N1, uint32_t* cnt) {
+    extern __shared__ uint64_t fx_l1o[];  // l1off[0..k]
+    for (uint32_t x = threadIdx.x; x <= A.k; x += blockDim.x) fx_l1o[x] = A.l1off[x];
+    __syncthreads();
     const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= N1) return;
     uint32_t lo = 0, hi = A.k;  // stream j: l1off[j] <= q < l1off[j + 1]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (A.l1off[mid] <= q) lo = mid;
+        if (fx_l1o[mid] <= q) lo = mid;
         else hi = mid;
     }
     const uint32_t j = lo, k = A.k;
-    const uint64_t c = q - A.l1off[j], m = A.m, T = A.T;
+    const uint64_t c = q - fx_l1o[j], m = A.m, T = A.T;
     const uint64_t p = posof[q];
     const uint64_t tmax = T - 1;
     const uint64_t t_hi0 = p / m < tmax ? p / m : tmax;  // splitters at or before p: nothing of j's below
     if (c == 0)
         for (uint64_t t = 1; t <= t_hi0; ++t) cnt[t * k + j] = 0;
-    const uint64_t pn = q + 1 < A.l1off[j + 1] ? posof[q + 1] : ~0ull;
+    const uint64_t pn = q + 1 < fx_l1o[j + 1] ? posof[q + 1] : ~0ull;
     const uint64_t t_hi = pn == ~0ull ? tmax : (pn / m < tmax ? pn / m : tmax);
     for (uint64_t t = p / m + 1; t <= t_hi; ++t) cnt[t * k + j] = (uint32_t)(c + 1);
 }
@@ -1037,12 +1070,12 @@ static inline unsigned fx_blocks(uint64_t n, unsigned t) { return (unsigned)((n 
 
 void launch_fx_sample(hipStream_t s, const FxArgs& A, const uint64_t* off_dst, uint64_t Sstep, uint64_t n_dst,
                       uint64_t* dhi, uint64_t* dlo, uint64_t* dc) {
-    if (n_dst) k_fx_sample<<<fx_blocks(n_dst, 256), 256, 0, s>>>(A, off_dst, Sstep, n_dst, dhi, dlo, dc);
+    if (n_dst) k_fx_sample<<<fx_blocks(n_dst, 256), 256, (A.k + 1) * 8, s>>>(A, off_dst, Sstep, n_dst, dhi, dlo, dc);
 }
 void launch_fx_l1cnt(hipStream_t s, const FxArgs& A, const uint64_t* sc, uint64_t N1, uint32_t* posof, uint32_t* cnt) {
     if (!N1) return;
-    k_fx_posof<<<fx_blocks(N1, 256), 256, 0, s>>>(A, sc, N1, posof);
-    k_fx_l1cnt<<<fx_blocks(N1, 256), 256, 0, s>>>(A, posof, N1, cnt);
+    k_fx_posof<<<fx_blocks(N1, 256), 256, 2 * (A.k + 1) * 8, s>>>(A, sc, N1, posof);
+    k_fx_l1cnt<<<fx_blocks(N1, 256), 256, (A.k + 1) * 8, s>>>(A, posof, N1, cnt);
 }
 void launch_fx_bounds(hipStream_t s, const FxArgs& A, const uint64_t* shi, const uint64_t* slo, uint64_t m,
                       const uint64_t* l1hi, const uint64_t* l1lo, const uint64_t* l1off, uint64_t Sstep) {
