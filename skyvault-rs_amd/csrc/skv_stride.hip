@@ -1086,7 +1086,9 @@ size_t fx_tile_lds_bytes(uint32_t k) {
     return (size_t)FX_CAP * 16 + (size_t)k * 16 + 2 * (size_t)k * 8 + 3 * (size_t)(k + 1) * 4 + (size_t)FX_CAP * 2 + k + 16;
 }
 hipError_t launch_fx_tile(hipStream_t s, const FxArgs& A) {
-    const size_t lds = fx_tile_lds_bytes(A.k);
+    // SKV_FX_LDS=<bytes>: pad the tile's LDS request (caps workgroups per CU; occupancy studies)
+    static const size_t lds_pad = getenv("SKV_FX_LDS") ? (size_t)atol(getenv("SKV_FX_LDS")) : 0;
+    const size_t lds = std::max(fx_tile_lds_bytes(A.k), std::min<size_t>(lds_pad, 160 * 1024));
     static size_t lds_set[64] = {};
     int dev = 0;
     (void)hipGetDevice(&dev);

@@ -211,3 +211,26 @@ def test_fused_random_shapes(dev):
         if exp != got or path != _abi.PATH_FUSED:
             bad.append((trial, K, V, k, n, path, _diff(exp, got) if exp != got else "path"))
     assert not bad, bad[:5]
+
+
+def test_fused_key_decrease_positions(dev):
+    """A key decrease at many positions of one stream (run start and end, sample spacings, random
+    places, so some land on tile edges): every one is caught on the device by the sample check, a
+    tile's neighbour check or the tile-edge check against the previous record (whose key the
+    bounds search carries, k_fx_bounds), and the exact path reproduces the reference's outcome."""
+    n, K, V = 3000, 16, 30
+    base = [(s + 1, [_run(500 + s, n, K, V)]) for s in range(16)]
+    r = random.Random(99)
+    positions = [0, 1, 5, 6, 7, n // 2, n - 2] + r.sample(range(n - 1), 9)
+    bad = []
+    for p in positions:
+        keys = _keys(505, n, K)
+        keys[[p, p + 1]] = keys[[p + 1, p]]
+        vals = gen.random_bytes(505 ^ 0x5A5A, n * V).reshape(n, V)
+        streams = list(base)
+        streams[5] = (6, [gen.assemble_run(keys, vals, np.ones(n, dtype=bool)).tobytes()])
+        exp, got = _run_both(dev, streams, 64 * KiB, 0)
+        t = dev.timings()
+        if exp != got or t["path"] == _abi.PATH_FUSED or not t["fused_reject"] & (FXR_ORDER | FXR_SAMPLE | FXR_SPLIT):
+            bad.append((p, t["path"], t["fused_reject"], exp == got))
+    assert not bad, bad
