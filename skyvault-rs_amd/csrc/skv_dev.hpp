@@ -173,6 +173,9 @@ struct FxArgs {
     // own level-1 samples (every Sstep-th record, offsets l1off)
     const uint64_t *shi, *slo, *l1hi, *l1lo, *l1off;
     uint64_t m, Sstep;
+    // splitter t is sorted sample t*m for t <= T1, then T1*m + (t - T1)*m2: the last generation of
+    // tiles is shorter (m2 < m) so the grid drains sooner (T1 = T, m2 = m: uniform tiles)
+    uint64_t T1, m2;
     const uint32_t* l1cnt;        // (T + 1) x k: stream j's level-1 samples sorted before splitter t
                                   // (k_fx_l1cnt), or null: k_fx_bounds searches them
 };

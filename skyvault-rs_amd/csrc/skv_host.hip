@@ -485,6 +485,22 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
         m0 = std::max<uint64_t>(1, (uint64_t)FX_TARGET / lv[1].S);
         T0 = std::max<uint64_t>(1, (lv[1].N + m0 - 1) / m0);
     }
+    // the last generation of tiles (as many as are resident at once) at half size, so the grid
+    // drains in half a tile time (SKV_FX_TAIL=0: uniform tiles)
+    uint64_t T1 = T0, m2 = m0;
+    {
+        const char* te = getenv("SKV_FX_TAIL");
+        if (lv.size() > 1 && m0 >= 4 && !(te && te[0] == '0')) {
+            const char* se = getenv("SKV_FX_TAIL_SLOTS");  // tests: a small grid's worth of slots
+            const uint64_t slots = se ? std::max<uint64_t>(1, strtoull(se, nullptr, 10)) : fx_tile_slots(k);
+            const uint64_t h = m0 / 2;
+            if (T0 > 3 * slots) {
+                m2 = h;
+                T1 = (lv[1].N - slots * h) / m0;
+                T0 = T1 + (lv[1].N - T1 * m0 + h - 1) / h;
+            }
+        }
+    }
     // blob layout (256-byte aligned pieces): readback words {runs, K, bytes} + flags[4] | K_out |
     // ticket | recb | stream_run | stream_base | level offsets | tile states
     std::vector<size_t> lv_off(lv.size(), 0);
@@ -558,6 +574,8 @@ static bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInf
     A.l1lo = l1 ? lv[1].lo : nullptr;
     A.l1off = l1 ? lv[1].d_off : nullptr;
     A.m = m0;
+    A.T1 = T1;
+    A.m2 = m2;
     A.Sstep = S_step;
     if (l1 && T0 > 1) {  // per (splitter, stream) sample counts: k_fx_bounds skips its sample search
         uint32_t* posof = dbuf<uint32_t>(ctx, "fx_posof", lv[1].N);

@@ -84,6 +84,7 @@ void launch_fx_bounds(hipStream_t, const FxArgs& A, const uint64_t* shi, const u
                       const uint64_t* l1hi, const uint64_t* l1lo, const uint64_t* l1off, uint64_t Sstep);
 size_t fx_tile_lds_bytes(uint32_t k);
 hipError_t launch_fx_tile(hipStream_t, const FxArgs& A);
+uint64_t fx_tile_slots(uint32_t k);
 void launch_fx_desc(hipStream_t, const FxArgs& A, DevRunDesc* descs, uint64_t* n_runs_out, uint64_t max_runs);
 // skv_sort.hip — record sort (fan-in above TILE_TARGET / 2)
 void launch_sort_load(hipStream_t, uint64_t R, const uint64_t* hi, const uint64_t* lo, const uint64_t* addr,

@@ -215,6 +215,16 @@ __global__ void k_fx_sample(FxArgs A, const uint64_t* __restrict__ off_dst, uint
     }
 }
 
+// sorted level-1 sample index of splitter t, and its inverse (the last splitter at or before
+// sorted position p)
+__device__ __forceinline__ uint64_t fx_srank(const FxArgs& A, uint64_t t) {
+    return t <= A.T1 ? t * A.m : A.T1 * A.m + (t - A.T1) * A.m2;
+}
+__device__ __forceinline__ uint64_t fx_sinv(const FxArgs& A, uint64_t p) {
+    const uint64_t b = A.T1 * A.m;
+    return p < b ? p / A.m : A.T1 + (p - b) / A.m2;
+}
+
 // member run of stream j holding record pos
 __device__ __forceinline__ uint32_t fx_run(const FxArgs& A, uint32_t j, uint64_t pos) {
     uint32_t lo = A.stream_run[j], hi = A.stream_run[j + 1];
@@ -276,7 +286,8 @@ __device__ __forceinline__ FxBound fx_bound(const FxArgs& A, const uint64_t* __r
             o.pos = s0;
             return o;
         }
-        const uint64_t h = shi[t * m], l = slo[t * m];
+        const uint64_t sr = fx_srank(A, t);
+        const uint64_t h = shi[sr], l = slo[sr];
         const uint64_t q0 = l1off[j], q1 = l1off[j + 1];
         uint64_t c;
         if (A.l1cnt) {
@@ -380,15 +391,17 @@ __global__ void k_fx_l1cnt(FxArgs A, const uint32_t* __restrict__ posof, uint64_
         else hi = mid;
     }
     const uint32_t j = lo, k = A.k;
-    const uint64_t c = q - fx_l1o[j], m = A.m, T = A.T;
+    const uint64_t c = q - fx_l1o[j], T = A.T;
     const uint64_t p = posof[q];
     const uint64_t tmax = T - 1;
-    const uint64_t t_hi0 = p / m < tmax ? p / m : tmax;  // splitters at or before p: nothing of j's below
+    const uint64_t sp = fx_sinv(A, p);
+    const uint64_t t_hi0 = sp < tmax ? sp : tmax;  // splitters at or before p: nothing of j's below
     if (c == 0)
         for (uint64_t t = 1; t <= t_hi0; ++t) cnt[t * k + j] = 0;
     const uint64_t pn = q + 1 < fx_l1o[j + 1] ? posof[q + 1] : ~0ull;
-    const uint64_t t_hi = pn == ~0ull ? tmax : (pn / m < tmax ? pn / m : tmax);
-    for (uint64_t t = p / m + 1; t <= t_hi; ++t) cnt[t * k + j] = (uint32_t)(c + 1);
+    const uint64_t spn = pn == ~0ull ? tmax : fx_sinv(A, pn);
+    const uint64_t t_hi = spn < tmax ? spn : tmax;
+    for (uint64_t t = sp + 1; t <= t_hi; ++t) cnt[t * k + j] = (uint32_t)(c + 1);
 }
 
 // bnd[t*k + j].pos = first record of stream j whose key >= splitter t (sorted level-1 samples,
@@ -1098,6 +1111,16 @@ hipError_t launch_fx_tile(hipStream_t s, const FxArgs& A) {
     }
     k_fx_tile<<<(unsigned)A.T, FX_THREADS, lds, s>>>(A);
     return hipGetLastError();
+}
+uint64_t fx_tile_slots(uint32_t k) {  // fused tiles resident at once on the current device
+    static uint64_t cached[64] = {}, cached_k[64] = {};
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    if (cached[dev & 63] && cached_k[dev & 63] == k) return cached[dev & 63];
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_fx_tile, FX_THREADS, fx_tile_lds_bytes(k));
+    cached_k[dev & 63] = k;
+    return cached[dev & 63] = (uint64_t)(cus > 0 ? cus : 256) * (uint64_t)(per > 0 ? per : 1);
 }
 void launch_fx_desc(hipStream_t s, const FxArgs& A, DevRunDesc* descs, uint64_t* n_runs_out, uint64_t max_runs) {
     unsigned blocks = fx_blocks(max_runs ? max_runs : 1, 256);

@@ -234,3 +234,21 @@ def test_fused_key_decrease_positions(dev):
         if exp != got or t["path"] == _abi.PATH_FUSED or not t["fused_reject"] & (FXR_ORDER | FXR_SAMPLE | FXR_SPLIT):
             bad.append((p, t["path"], t["fused_reject"], exp == got))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("slots", ["1", "2", "5"])
+def test_fused_short_tail_tiles(dev, slots):
+    """The last generation of tiles at half size (splitter t at sorted sample t*m up to T1, then
+    T1*m + (t - T1)*m/2): forced on small inputs by pretending only `slots` tiles fit the GPU at
+    once; same bytes as the oracle, and the fused path is still the one taken."""
+    os.environ["SKV_FX_TAIL_SLOTS"] = slots
+    try:
+        r = random.Random(int(slots))
+        for trial in range(6):
+            k = r.choice([2, 7, 16, 64])
+            n = r.randint(2000, 6000)
+            uni = r.choice([0, k * n // 2])
+            streams = [(s + 1, [_run(7000 + 100 * trial + s, n, 16, 40, uni)]) for s in range(k)]
+            _check(dev, streams, r.choice([4 * MiB, 5000, 64 * KiB]))
+    finally:
+        del os.environ["SKV_FX_TAIL_SLOTS"]
