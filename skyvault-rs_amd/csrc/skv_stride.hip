@@ -119,6 +119,9 @@ __device__ __forceinline__ uint4 fx_ld16(uint64_t a) {  // unaligned: full rate 
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+#ifndef SKV_FX_NTSEL
+#define SKV_FX_NTSEL 0  // 1: the fused copy loads lines that hold no record head non-temporally
+#endif
 #ifndef SKV_FX_INTERP
 #define SKV_FX_INTERP 0  // 1: k_fx_bounds' first probe pair interpolated from the gap's end keys (measured slower: 0.283 vs 0.264 ms splitters; the search is bound by its line fetches, not their latency)
 #endif
@@ -625,7 +628,20 @@ __device__ __forceinline__ void fx_plan(FxBatch<U>& t, FxWalk& w, const uint64_t
             w.o = z ? w.S32 - 1 : w.o - 1;
             w.j = z ? w.j - 1 : w.j;
         }
+#if SKV_FX_NTSEL  // non-temporal loads for the lines no record head shares (read once here)
+        {
+            const uint64_t hEnd = ((s0 + 24) | 127ull) + 1, nHead = (s0 + w.S32) & ~127ull;
+            const bool nt = !vb && !st && aL >= hEnd && aL + 16 <= nHead;
+            if (nt) {
+                const fx_v4 v = __builtin_nontemporal_load((fx_g16*)aL);
+                t.L[u] = make_uint4(v.x, v.y, v.z, v.w);
+            } else {
+                t.L[u] = fx_ld16(aL);
+            }
+        }
+#else
         t.L[u] = fx_cld16(aL);
+#endif
 #if SKV_FX_DIAG_1LD  // diagnostic (output invalid at record ends): no second load
         t.X[u] = t.L[u];
         (void)aX;
