@@ -160,6 +160,8 @@ def test_random_cases_match_oracle(dev):
     ("cfg3_scaled", lambda: gen.config3(n_streams=32, run_bytes=192 * KiB), 256 * KiB, 0),
     ("cfg3_scaled_drop", lambda: gen.config3(n_streams=32, run_bytes=192 * KiB), 256 * KiB, 1),
     ("cfg3_256way", lambda: gen.config3(n_streams=256, run_bytes=24 * KiB, vsize=64), 1 * MiB, 0),
+    # 256 streams x ~295 records: two sample levels
+    ("cfg3_256way_levels", lambda: gen.config3(n_streams=256, run_bytes=96 * KiB, vsize=64), 1 * MiB, 0),
     ("two_streams_big", lambda: gen.config2(n_streams=2, n_records=40000, vsize=100, variant="B"), 4 * MiB, 0),
     ("one_stream", lambda: gen.config2(n_streams=1, n_records=50000, vsize=20), 1 * MiB, 0),
 ])
@@ -334,3 +336,17 @@ def test_invalid_utf8_key_in_variable_runs(dev):
             streams.append((s + 1, [bytes(run)]))
         exp, got = _run_both(dev, streams, 1 << 16, 0)
         assert exp == got, _diff(exp, got)
+
+
+def test_coarse_sample_levels_same_bytes(dev):
+    """The sample levels above the first only pick splitters: with a 2x or 4x coarser step there
+    (SKV_HI_STEP; tiles past TILE_CAP take the oversized-tile path) the output is the same."""
+    streams = gen.config3(seed=77, n_streams=300, run_bytes=160 * KiB, vsize=32)
+    ref = dev.compact(streams, 1 * MiB, 0)
+    for f in ("2", "4"):
+        os.environ["SKV_HI_STEP"] = f
+        try:
+            got = dev.compact(streams, 1 * MiB, 0)
+        finally:
+            del os.environ["SKV_HI_STEP"]
+        assert [r.data for r in got] == [r.data for r in ref], f
