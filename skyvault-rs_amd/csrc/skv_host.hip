@@ -193,7 +193,7 @@ static void htrace(const char* what) {
     }
     if (!on) return;
     const double t = now_ms();
-    if (!strcmp(what, "start")) t0 = t;
+    if (!strcmp(what, "entry")) t0 = t;  // each API call starts the clock
     fprintf(stderr, "[skv host] %8.3f ms %s\n", t - t0, what);
 }
 static void sync(skv_ctx* ctx) {
@@ -1323,6 +1323,13 @@ static int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64
         return set_err(ctx, SKV_E_INVALID_ARG, "SKV_SPLIT_BY_TABLE and SKV_DROP_TOMBSTONES are exclusive");
     job.max_run_size = max_run_size;
     job.flags = flags;
+    {  // one allocation per table (10^6 WAL runs: no regrowth copies)
+        uint64_t total_runs = 0;
+        for (uint32_t i = 0; i < n; ++i) total_runs += streams[i].n_runs;
+        job.run_ptr.reserve(total_runs);
+        job.run_len.reserve(total_runs);
+        job.ranked.reserve(n);
+    }
     for (uint32_t i = 0; i < n; ++i) {
         const skv_stream& s = streams[i];
         if (s.n_runs && (!s.runs || !s.run_lens))
@@ -1444,12 +1451,14 @@ int skv_ctx_get_timings(const skv_ctx* ctx, skv_timings* out) {
 int skv_compact_dev(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uint64_t max_run_size, uint32_t flags,
                     skv_result** out) {
     const double t_entry = now_ms();
+    htrace("entry");
     if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
     *out = nullptr;
     if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
     Job job;
     int rc = build_job(ctx, streams, n_streams, max_run_size, flags, job);
     if (rc) return rc;
+    htrace("job built");
     return run_guarded(ctx, job, out, t_entry);
 }
 
@@ -1511,6 +1520,7 @@ extern "C" {
 int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uint64_t max_run_size, uint32_t flags,
                 skv_result** out) {
     const double t_entry = now_ms();
+    htrace("entry");
     if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
     *out = nullptr;
     if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
