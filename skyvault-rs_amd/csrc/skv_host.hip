@@ -18,6 +18,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/skv.h"
@@ -84,6 +85,12 @@ struct skv_ctx {
     std::vector<std::pair<uint8_t*, size_t>> up_chunks;
     size_t up_chunk = 0, up_off = 0;
     std::vector<uint8_t> fx_blob;  // fused path: host image of its one table upload
+    // per-call host tables kept across calls: at 10^6 runs, fresh vectors cost their page faults
+    // (~15 ms per call) every time; reused ones keep their touched pages
+    std::vector<RunInfo> s_runs;
+    std::vector<RunSummary> s_sum;
+    std::vector<uint64_t> s_sbase, s_svalid, s_first_dec;
+    std::vector<uint32_t> s_sfr, s_serr;
     uint64_t syncs = 0;
     double sync_ms = 0;
     bool exact_keys = false;  // rerun after a fingerprint shortcut misordered a tile (never in practice)
@@ -150,6 +157,24 @@ static void* pinned(skv_ctx* ctx, size_t bytes) {
     return ctx->pinned;
 }
 
+// host copy into pinned staging; large tables (10^6-run calls: tens of MB) on several threads
+static void stage_copy(void* dst, const void* src, size_t bytes) {
+    const char* pe = getenv("SKV_PAR_COPY_MIN");  // tests: split small tables too
+    const size_t kPar = pe ? (size_t)strtoull(pe, nullptr, 10) : (8u << 20);
+    const unsigned hw = std::thread::hardware_concurrency();
+    const unsigned nt = std::min<unsigned>(8, hw ? hw : 1);
+    if (bytes < kPar || nt < 2) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t part = ((bytes + nt - 1) / nt + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    for (unsigned i = 1; i < nt && i * part < bytes; ++i)
+        th.emplace_back([=] { memcpy((uint8_t*)dst + i * part, (const uint8_t*)src + i * part, std::min(part, bytes - i * part)); });
+    memcpy(dst, src, std::min(part, bytes));
+    for (auto& t : th) t.join();
+}
+
 // async H2D of a host table through the pinned upload arena
 static void h2d_up(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
     if (!bytes) return;
@@ -168,7 +193,7 @@ static void h2d_up(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
     }
     uint8_t* stage = ctx->up_chunks[ctx->up_chunk].first + ctx->up_off;
     ctx->up_off += need;
-    memcpy(stage, src, bytes);
+    stage_copy(stage, src, bytes);
     HIPCHK(hipMemcpyAsync(dst, stage, bytes, hipMemcpyHostToDevice, ctx->stream));
 }
 
@@ -768,9 +793,11 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     htrace("start");
     const uint32_t k = (uint32_t)job.ranked.size();
     // ---- run table ------------------------------------------------------------------------
-    std::vector<RunInfo> runs;
+    std::vector<RunInfo>& runs = ctx->s_runs;  // (a rerun returns right after its nested call)
+    runs.clear();
     runs.reserve(job.run_ptr.size());
-    std::vector<uint32_t> stream_first_run(k + 1, 0);
+    std::vector<uint32_t>& stream_first_run = ctx->s_sfr;
+    stream_first_run.assign(k + 1, 0);
     uint64_t n_chunks = 0;
     for (uint32_t s = 0; s < k; ++s) {
         stream_first_run[s] = (uint32_t)runs.size();
@@ -788,6 +815,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     }
     stream_first_run[k] = (uint32_t)runs.size();
     const uint32_t n_runs = (uint32_t)runs.size();
+    htrace("run table built");
 
     RunInfo* d_runs = dbuf<RunInfo>(ctx, "runs", n_runs);
     uint32_t* d_hdr = dbuf<uint32_t>(ctx, "hdr_err", n_runs);
@@ -802,6 +830,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     uint64_t* ch_rec_base = dbuf<uint64_t>(ctx, "ch_rec_base", n_chunks + 1);
     uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "scan_tmp", scan_tmp_words(std::max<uint64_t>(n_chunks, 1 << 20)) + 64);
     RunSummary* d_sum = dbuf<RunSummary>(ctx, "run_sum", n_runs);
+    htrace("buffers");
 
     h2d_up(ctx, d_runs, runs.data(), n_runs * sizeof(RunInfo));
     htrace("runs uploaded");
@@ -811,9 +840,14 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     HIPCHK(hipMemsetAsync(d_broken, 0, (size_t)n_runs * 4, st));
     launch_run_header(st, d_runs, n_runs, d_hdr, d_fmt);
 
-    std::vector<RunSummary> sum(n_runs);
-    std::vector<uint64_t> stream_base(k + 1, 0), stream_valid(k, 0);
-    std::vector<uint32_t> stream_err(k, 0);
+    std::vector<RunSummary>& sum = ctx->s_sum;
+    sum.assign(n_runs, RunSummary{});
+    std::vector<uint64_t>& stream_base = ctx->s_sbase;
+    std::vector<uint64_t>& stream_valid = ctx->s_svalid;
+    std::vector<uint32_t>& stream_err = ctx->s_serr;
+    stream_base.assign(k + 1, 0);
+    stream_valid.assign(k, 0);
+    stream_err.assign(k, 0);
     bool any_err = false;
     uint64_t R = 0;
     uint64_t* rec_addr = nullptr;
@@ -826,7 +860,8 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     uint32_t* d_flags = dbuf<uint32_t>(ctx, "flags", 4);
     uint64_t* d_stream_base = dbuf<uint64_t>(ctx, "stream_base", k + 1);
     unsigned long long* d_first_dec = dbuf<unsigned long long>(ctx, "first_dec", k);
-    std::vector<uint64_t> first_dec(k);
+    std::vector<uint64_t>& first_dec = ctx->s_first_dec;
+    first_dec.assign(k, 0);
     uint32_t hflags[4];
     // per stream (rank order): base index, valid record count n_s and the first error
     auto stream_tables = [&]() {
@@ -893,7 +928,9 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     {
         RunFmt* hf = (RunFmt*)pinned(ctx, (size_t)n_runs * sizeof(RunFmt) + 16);
         d2h(ctx, hf, d_fmt, (size_t)n_runs * sizeof(RunFmt));
+        htrace("header launched");
         sync(ctx);
+        htrace("header synced");
         htrace("run formats read");
         bool all_fixed = n_runs > 0;
         for (uint32_t r = 0; r < n_runs && all_fixed; ++r) all_fixed = hf[r].S != 0;

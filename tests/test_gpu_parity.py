@@ -350,3 +350,17 @@ def test_coarse_sample_levels_same_bytes(dev):
         finally:
             del os.environ["SKV_HI_STEP"]
         assert [r.data for r in got] == [r.data for r in ref], f
+
+
+def test_threaded_table_staging(dev):
+    """Host tables above SKV_PAR_COPY_MIN bytes are copied into the pinned upload arena by
+    several threads (10^6-run calls); forced down to 4 KiB here, a 1000-run WAL call and a
+    256-way call still match the oracle."""
+    os.environ["SKV_PAR_COPY_MIN"] = "4096"
+    try:
+        for streams, flags in ((gen.config5(n_streams=1000), _abi.SKV_SPLIT_BY_TABLE),
+                               (gen.config3(n_streams=256, run_bytes=24 * KiB, vsize=64), 0)):
+            exp, got = _run_both(dev, streams, 4 * MiB, flags)
+            assert exp == got, _diff(exp, got)
+    finally:
+        del os.environ["SKV_PAR_COPY_MIN"]
