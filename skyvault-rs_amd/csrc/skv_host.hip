@@ -67,6 +67,13 @@ struct PinnedPool {
     }
 };
 
+struct InStream {
+    int64_t seq;
+    uint32_t vec_idx;  // position in the caller's vector (merge pulls first items in this order)
+    uint32_t n_runs;
+    uint64_t first;    // its member runs: Job::run_ptr/run_len[first, first + n_runs)
+};
+
 struct skv_ctx {
     int device = 0;
     std::shared_ptr<PinnedPool> out_pool = std::make_shared<PinnedPool>();
@@ -91,6 +98,8 @@ struct skv_ctx {
     std::vector<RunSummary> s_sum;
     std::vector<uint64_t> s_sbase, s_svalid, s_first_dec;
     std::vector<uint32_t> s_sfr, s_serr;
+    std::vector<InStream> j_ranked;  // skv_compact_dev's job tables, lent to each call
+    std::vector<uint64_t> j_ptr, j_len;
     uint64_t syncs = 0;
     double sync_ms = 0;
     bool exact_keys = false;  // rerun after a fingerprint shortcut misordered a tile (never in practice)
@@ -248,13 +257,6 @@ static int derr_to_api(uint32_t e, std::string& msg) {
 }
 
 // ------------------------------------------------------------------------------------------
-struct InStream {
-    int64_t seq;
-    uint32_t vec_idx;  // position in the caller's vector (merge pulls first items in this order)
-    uint32_t n_runs;
-    uint64_t first;    // its member runs: Job::run_ptr/run_len[first, first + n_runs)
-};
-
 struct Job {
     std::vector<InStream> ranked;  // streams sorted by seq_no descending
     std::vector<uint64_t> run_ptr, run_len;  // member runs, caller order (flat: 10^6-stream jobs)
@@ -1492,11 +1494,20 @@ int skv_compact_dev(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams,
     if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
     *out = nullptr;
     if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
-    Job job;
+    Job job;  // its tables borrow the ctx's storage for the call (no fresh 10^6-entry vectors)
+    job.ranked.swap(ctx->j_ranked);
+    job.run_ptr.swap(ctx->j_ptr);
+    job.run_len.swap(ctx->j_len);
+    job.ranked.clear();
+    job.run_ptr.clear();
+    job.run_len.clear();
     int rc = build_job(ctx, streams, n_streams, max_run_size, flags, job);
-    if (rc) return rc;
     htrace("job built");
-    return run_guarded(ctx, job, out, t_entry);
+    if (!rc) rc = run_guarded(ctx, job, out, t_entry);
+    job.ranked.swap(ctx->j_ranked);
+    job.run_ptr.swap(ctx->j_ptr);
+    job.run_len.swap(ctx->j_len);
+    return rc;
 }
 
 }  // extern "C"
