@@ -96,7 +96,7 @@ struct skv_ctx {
     // (~15 ms per call) every time; reused ones keep their touched pages
     std::vector<RunInfo> s_runs;
     std::vector<RunSummary> s_sum;
-    std::vector<uint64_t> s_sbase, s_svalid, s_first_dec;
+    std::vector<uint64_t> s_sbase, s_svalid, s_first_dec, s_recb;
     std::vector<uint32_t> s_sfr, s_serr;
     std::vector<InStream> j_ranked;  // skv_compact_dev's job tables, lent to each call
     std::vector<uint64_t> j_ptr, j_len;
@@ -937,7 +937,8 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         bool all_fixed = n_runs > 0;
         for (uint32_t r = 0; r < n_runs && all_fixed; ++r) all_fixed = hf[r].S != 0;
         if (all_fixed) {
-            std::vector<uint64_t> recb(n_runs + 1, 0);
+            std::vector<uint64_t>& recb = ctx->s_recb;
+            recb.assign(n_runs + 1, 0);
             for (uint32_t r = 0; r < n_runs; ++r) {
                 sum[r].records = (runs[r].len - 1) / hf[r].S;
                 sum[r].err = 0;
