@@ -96,7 +96,9 @@ enum {
     SKV_E_INVALID_INPUT = 5,       /* JobError::InvalidInput, WAL key (jobs/mod.rs:26; wal_compaction.rs:71-79) */
     SKV_E_INVALID_ARG = 6,         /* API misuse: NULL pointers, duplicate seq_no, bad device */
     SKV_E_DEVICE = 7,              /* HIP runtime failure or device capacity exceeded */
-    SKV_E_UNSUPPORTED = 8          /* input shape outside what this build supports (message says which) */
+    SKV_E_UNSUPPORTED = 8,         /* input shape outside what this build supports (message says which) */
+    SKV_E_INTERNAL = 9             /* JobError::Internal (jobs/mod.rs:29-30): a WAL table channel send that
+                                      cannot succeed (wal_compaction.rs:157-161) */
 };
 
 /* skv_compact flags */

@@ -68,6 +68,18 @@ def lib():
         l.skvo_merge_ops.restype = C.c_int
         l.skvo_result_free.argtypes = [C.POINTER(SkvResult)]
         l.skvo_op_list_free.argtypes = [C.POINTER(SkvoOpList)]
+        l.skvo_sb_new.argtypes = [C.c_uint64]
+        l.skvo_sb_new.restype = C.c_void_p
+        l.skvo_sb_feed_run.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_char_p, C.c_size_t]
+        l.skvo_sb_feed_run.restype = C.c_int
+        l.skvo_sb_pending.argtypes = [C.c_void_p]
+        l.skvo_sb_pending.restype = C.c_uint64
+        l.skvo_sb_drain.argtypes = [C.c_void_p, C.c_void_p]
+        l.skvo_sb_drain.restype = None
+        l.skvo_sb_finish.argtypes = [C.c_void_p, C.POINTER(C.POINTER(SkvResult))]
+        l.skvo_sb_finish.restype = C.c_int
+        l.skvo_sb_free.argtypes = [C.c_void_p]
+        l.skvo_sb_free.restype = None
         _lib = l
     return _lib
 
@@ -254,3 +266,76 @@ def search_run(run: bytes, key: bytes):
             return ("found", run[p:p + vlen])
         return ("not_found", None)  # :387-391
     return ("not_found", None)  # :395-396
+
+
+class StreamBuilder:
+    """Streaming runs::build_runs (runs.rs:166-282) over a merged op sequence that arrives as
+    consecutive v1 runs (skvo_sb_* in skv_oracle.c): feed(run) -> the output bytes it
+    completed; finish() -> (tail bytes, [descriptor tuples]) with absolute offsets. Used by the
+    full-size tests, which merge key ranges separately with an unbounded max and split here."""
+
+    def __init__(self, max_run_size: int):
+        self._l = lib()
+        self._s = self._l.skvo_sb_new(max_run_size)
+
+    def feed(self, run, length: int = None) -> "np.ndarray":
+        import numpy as np
+
+        if isinstance(run, int):
+            ptr, n = run, length
+        else:
+            a = np.frombuffer(run, dtype=np.uint8) if not isinstance(run, np.ndarray) else run
+            ptr, n = a.ctypes.data, a.size
+        eb = C.create_string_buffer(512)
+        rc = self._l.skvo_sb_feed_run(self._s, C.c_void_p(ptr), n, eb, 512)
+        if rc != SKV_OK:
+            raise RunError(rc, eb.value.decode("utf-8", "replace"))
+        out = np.empty(self._l.skvo_sb_pending(self._s), dtype=np.uint8)
+        self._l.skvo_sb_drain(self._s, C.c_void_p(out.ctypes.data))
+        return out
+
+    def finish(self):
+        res = C.POINTER(SkvResult)()
+        rc = self._l.skvo_sb_finish(self._s, C.byref(res))
+        if rc != SKV_OK:
+            raise RunError(rc, "stream builder failed earlier")
+        try:
+            r = res.contents
+            tail = C.string_at(r.bytes, r.n_bytes) if r.n_bytes else b""
+            descs = [(d.off, d.len, d.put_count, d.delete_count, d.min_key_off, d.min_key_len,
+                      d.max_key_off, d.max_key_len, d.table_id) for d in (r.runs[i] for i in range(r.n_runs))]
+        finally:
+            self._l.skvo_result_free(res)
+        return tail, descs
+
+    def __del__(self):
+        try:
+            if self._s:
+                self._l.skvo_sb_free(self._s)
+                self._s = None
+        except Exception:
+            pass
+
+
+def compact_np(sa, max_run_size: int, flags: int = 0):
+    """skvo_compact over a prebuilt skv_stream[] (skv._abi.StreamArgs / stream_table, host
+    pointers). Returns (output bytes as a numpy array, [descriptor tuples], info dict) or
+    raises RunError. For GiB-scale checks: no Python object per record or per stream."""
+    import numpy as np
+
+    res = C.POINTER(SkvResult)()
+    eb = C.create_string_buffer(512)
+    rc = lib().skvo_compact(sa.ptr, sa.n, max_run_size, flags, C.byref(res), eb, 512)
+    if rc != SKV_OK:
+        raise RunError(rc, eb.value.decode("utf-8", "replace"))
+    try:
+        r = res.contents
+        data = np.empty(r.n_bytes, dtype=np.uint8)
+        if r.n_bytes:
+            C.memmove(data.ctypes.data, r.bytes, r.n_bytes)
+        descs = [(d.off, d.len, d.put_count, d.delete_count, d.min_key_off, d.min_key_len,
+                  d.max_key_off, d.max_key_len, d.table_id) for d in (r.runs[i] for i in range(r.n_runs))]
+        info = dict(in_bytes=r.in_bytes, out_records=r.out_records, dropped_tables=r.dropped_tables)
+    finally:
+        lib().skvo_result_free(res)
+    return data, descs, info

@@ -303,6 +303,7 @@ typedef struct {
     uint64_t cur_size, put_count, delete_count;
     uint64_t run_off, max_key_off, max_klen, min_key_off, min_klen;
     uint64_t records;
+    uint64_t base;      /* bytes already drained from the output (skvo_sb_*); 0 otherwise */
 } builder;
 
 static void bld_init(builder* b, outbuf* out, uint64_t max) {
@@ -355,17 +356,17 @@ static int bld_push(builder* b, const oop* op, char* eb, size_t en) {
     outbuf* o = bld_buf(b);
     if (b->first_op_in_run) { /* :241-246 */
         ob_reserve(o, 1);
-        b->run_off = o->n;
+        b->run_off = b->base + o->n;
         o->b[o->n++] = 1; /* CURRENT_VERSION */
         b->cur_size += 1;
         b->min_key = dup_bytes(current_key, op->klen);
-        b->min_key_off = o->n + 5;
+        b->min_key_off = b->base + o->n + 5;
         b->min_klen = op->klen;
         b->first_op_in_run = 0;
     }
     free(b->max_key);
     b->max_key = dup_bytes(current_key, op->klen); /* :248 */
-    b->max_key_off = o->n + 5;
+    b->max_key_off = b->base + o->n + 5;
     b->max_klen = op->klen;
     b->cur_size += op_size; /* :249 */
     ob_reserve(o, op_size); /* :252-267 */
@@ -435,8 +436,15 @@ typedef struct {
     int64_t table;
     builder cur;
     int cur_failed;
+    uint64_t after_fail; /* ops sent to the table after its build_runs failed */
     uint64_t dropped;
 } walc;
+
+/* mpsc::channel(100) per table task (wal_compaction.rs:113). A task whose build_runs fails on an
+ * order error drops its receiver; the job's 101st send after the failing op cannot be buffered
+ * and fails with "Failed to send operation to table channel" (:157-161). Sends 1..100 after it
+ * race with the task's exit; they are modelled as buffered (the task is slow). */
+#define WAL_SENDS_AFTER_FAIL 101
 
 static void wal_finish(walc* w) {
     if (!w->have_table) return;
@@ -480,10 +488,15 @@ static int wal_push(walc* w, oop* op, char* eb, size_t en) {
         w->have_table = 1;
         w->table = id;
         w->cur_failed = 0;
+        w->after_fail = 0;
         bld_init(&w->cur, w->out, w->max);
         w->cur.use_local = 1;
     }
-    if (w->cur_failed) return SKV_OK;
+    if (w->cur_failed) {
+        if (++w->after_fail == WAL_SENDS_AFTER_FAIL)
+            return fail(eb, en, SKV_E_INTERNAL, "Internal error: Failed to send operation to table channel");
+        return SKV_OK;
+    }
     oop s = *op; /* key.split_off(table_prefix_len) (:91-94) */
     s.key = op->key + strip;
     s.klen = op->klen - (uint32_t)strip;
@@ -589,6 +602,20 @@ static int run_merge(sit_t* its, const int64_t* seqs, uint32_t n, consumer* c, c
     return rc;
 }
 
+typedef struct {
+    int64_t seq;
+    uint32_t idx;
+} seq_idx;
+static int seq_idx_cmp(const void* a, const void* b) {
+    const seq_idx* x = (const seq_idx*)a;
+    const seq_idx* y = (const seq_idx*)b;
+    if (x->seq != y->seq) return x->seq < y->seq ? -1 : 1;
+    return x->idx < y->idx ? -1 : (x->idx > y->idx ? 1 : 0);
+}
+
+/* API checks. Duplicate seq_nos (k_way.rs:121 keys streams by SeqNo) are found by sorting
+ * (seq, index): the reported pair is the first stream i with an earlier duplicate, and that
+ * duplicate's first occurrence j. */
 static int check_streams(const skv_stream* streams, uint32_t n, char* eb, size_t en) {
     if (n && !streams) return fail(eb, en, SKV_E_INVALID_ARG, "streams is NULL");
     for (uint32_t i = 0; i < n; i++) {
@@ -597,11 +624,24 @@ static int check_streams(const skv_stream* streams, uint32_t n, char* eb, size_t
         for (uint32_t r = 0; r < streams[i].n_runs; r++)
             if (streams[i].run_lens[r] && !streams[i].runs[r])
                 return fail(eb, en, SKV_E_INVALID_ARG, "stream %u run %u: NULL data", i, r);
-        for (uint32_t j = 0; j < i; j++)
-            if (streams[j].seq_no == streams[i].seq_no)
-                return fail(eb, en, SKV_E_INVALID_ARG, "duplicate seq_no %" PRId64 " (streams %u and %u)",
-                            streams[i].seq_no, j, i);
     }
+    if (n < 2) return SKV_OK;
+    seq_idx* v = (seq_idx*)xmalloc((size_t)n * sizeof(seq_idx));
+    for (uint32_t i = 0; i < n; i++) {
+        v[i].seq = streams[i].seq_no;
+        v[i].idx = i;
+    }
+    qsort(v, n, sizeof(seq_idx), seq_idx_cmp);
+    uint32_t best_i = UINT32_MAX, best_j = 0;
+    for (uint32_t a = 1; a < n; a++)
+        if (v[a].seq == v[a - 1].seq && (a < 2 || v[a - 2].seq != v[a].seq) && v[a].idx < best_i) {
+            best_i = v[a].idx;     /* the group's second occurrence */
+            best_j = v[a - 1].idx; /* its first */
+        }
+    free(v);
+    if (best_i != UINT32_MAX)
+        return fail(eb, en, SKV_E_INVALID_ARG, "duplicate seq_no %" PRId64 " (streams %u and %u)",
+                    streams[best_i].seq_no, best_j, best_i);
     return SKV_OK;
 }
 
@@ -786,4 +826,72 @@ void skvo_result_free(skv_result* r) {
     free(r->bytes);
     free(r->runs);
     free(r);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Streaming build_runs (runs.rs:166-282) for full-size checks: the merged op sequence arrives
+ * as a series of v1 runs (e.g. the per-key-range outputs of skvo_compact with an unbounded
+ * max), each decoded with read_run_stream (runs.rs:517-628) and pushed through ONE builder,
+ * so the greedy split and the order check carry across the pieces. Output bytes are drained
+ * as they are produced; descriptor offsets stay absolute. */
+struct skvo_sb {
+    outbuf ob;
+    builder b;
+    int failed;
+    int finished;
+};
+
+skvo_sb* skvo_sb_new(uint64_t max_run_size) {
+    skvo_sb* s = (skvo_sb*)calloc(1, sizeof(skvo_sb));
+    bld_init(&s->b, &s->ob, max_run_size);
+    return s;
+}
+
+int skvo_sb_feed_run(skvo_sb* s, const uint8_t* run, uint64_t len, char* eb, size_t en) {
+    if (s->failed) return fail(eb, en, SKV_E_INVALID_ARG, "builder already failed");
+    dec_t d;
+    dec_init(&d, run, len);
+    for (;;) {
+        oop o;
+        int r = dec_next(&d, &o, eb, en);
+        if (r == 0) return SKV_OK;
+        if (r < 0) { s->failed = 1; return -r; }
+        int rc = bld_push(&s->b, &o, eb, en);
+        oop_free(&o);
+        if (rc != SKV_OK) { s->failed = 1; return rc; }
+    }
+}
+
+uint64_t skvo_sb_pending(const skvo_sb* s) { return s->ob.n; }
+
+void skvo_sb_drain(skvo_sb* s, uint8_t* dst) {
+    if (s->ob.n && dst) memcpy(dst, s->ob.b, (size_t)s->ob.n);
+    s->b.base += s->ob.n;
+    s->ob.n = 0;
+}
+
+int skvo_sb_finish(skvo_sb* s, skv_result** out) {
+    if (s->failed) return SKV_E_INVALID_ARG;
+    bld_end(&s->b, 0);
+    bld_free(&s->b);
+    s->finished = 1;
+    skv_result* r = (skv_result*)calloc(1, sizeof(skv_result));
+    r->bytes = s->ob.b;           /* the undrained tail */
+    r->n_bytes = s->ob.n;
+    r->runs = s->ob.runs;
+    r->n_runs = s->ob.n_runs;
+    r->out_records = s->ob.out_records;
+    r->in_bytes = s->b.base;      /* bytes drained before the tail */
+    s->ob.b = NULL;
+    s->ob.runs = NULL;
+    *out = r;
+    return SKV_OK;
+}
+
+void skvo_sb_free(skvo_sb* s) {
+    if (!s) return;
+    if (!s->finished) bld_free(&s->b);
+    free(s->ob.b);
+    free(s->ob.runs);
+    free(s);
 }

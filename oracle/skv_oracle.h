@@ -57,6 +57,19 @@ int skvo_compact(const skv_stream* streams, uint32_t n_streams, uint64_t max_run
 
 void skvo_result_free(skv_result* r);
 
+/* Streaming build_runs for full-size checks (test infrastructure): feed the merged op sequence
+ * as consecutive v1 runs; the greedy split and order check carry across feeds. skvo_sb_drain
+ * moves the output bytes produced so far out (skvo_sb_pending of them); skvo_sb_finish ends
+ * the stream (runs.rs:270-280) and returns the undrained tail bytes and every run descriptor
+ * (absolute offsets; result->in_bytes = bytes drained before the tail). */
+typedef struct skvo_sb skvo_sb;
+skvo_sb* skvo_sb_new(uint64_t max_run_size);
+int skvo_sb_feed_run(skvo_sb* s, const uint8_t* run, uint64_t len, char* errbuf, size_t errlen);
+uint64_t skvo_sb_pending(const skvo_sb* s);
+void skvo_sb_drain(skvo_sb* s, uint8_t* dst);
+int skvo_sb_finish(skvo_sb* s, skv_result** out);
+void skvo_sb_free(skvo_sb* s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -119,6 +119,16 @@ struct TileOut {
     uint64_t* xlo;
     uint64_t* xc;
     uint32_t* xmeta;
+    // heap-order mode (skv_heap.hip; unsorted input streams under the Delete filter or the WAL
+    // split): the merge compares each record's stream-prefix-maximum key (which is how
+    // k_way::merge's heap pops unsorted streams), while first-per-key compares the records' own
+    // keys (act_*), the payload is the record itself (pay_addr) and pop_pos[rec] records every
+    // record's position in the pop sequence. All null otherwise.
+    const uint64_t* pay_addr;
+    const uint64_t* act_hi;
+    const uint64_t* act_lo;
+    const uint32_t* act_klen;
+    uint64_t* pop_pos;
 };
 
 // Fused stride path (skv_stride.hip): every input record is a Put of one size S with one key

@@ -312,6 +312,44 @@ static std::string wal_key_error(const std::string& key) {
 }
 
 constexpr int RC_RETRY_EXACT = -100;  // internal: the merge's fingerprint shortcut misordered a tile
+
+template <typename T>
+static T read_dev(const T* p) {
+    T v{};
+    HIPCHK(hipMemcpy(&v, p, sizeof(T), hipMemcpyDeviceToHost));
+    return v;
+}
+
+// Heap-order mode (skv_heap.hip): the merge reproduced k_way::merge's pop sequence for unsorted
+// streams; pop_pos[r] is record r's pop position (r in the merge's numbering; inv maps original
+// record indices to it after the record sort). Decode errors surface right after their stream's
+// last decodable record is popped (k_way.rs:154-171).
+struct HeapRes {
+    const uint64_t* pop_pos = nullptr;
+    const uint32_t* inv = nullptr;
+    struct Dec { uint64_t rec; uint32_t err; };
+    std::vector<Dec> dec;
+    uint64_t pos_of_original(uint64_t rec) const {
+        const uint64_t r = inv ? read_dev(inv + rec) : rec;
+        return read_dev(pop_pos + r);
+    }
+};
+
+// the job's first failure among events at pop positions: (position, order at one position, error)
+struct JobEvent {
+    uint64_t pos;
+    int sub;  // 0: the op itself fails (key / order / send), 1: a send after the op, 2: the stream's
+              // decode error, raised after the op at pos was handled
+    int code;
+    std::string msg;
+};
+static void throw_first(std::vector<JobEvent>& ev) {
+    if (ev.empty()) return;
+    std::sort(ev.begin(), ev.end(), [](const JobEvent& a, const JobEvent& b) {
+        return a.pos != b.pos ? a.pos < b.pos : a.sub < b.sub;
+    });
+    throw ApiError{ev[0].code, ev[0].msg};
+}
 static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_deferred);
 // the whole call again with exact key compares in the merge rounds
 static int rerun_exact(skv_ctx* ctx, const Job& job, skv_result** out) {
@@ -332,7 +370,7 @@ static int rerun_exact(skv_ctx* ctx, const Job& job, skv_result** out) {
 // (skv_wal.hip). One extra host sync reads the surviving record count first.
 static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, const uint32_t* m_rec,
                      const uint64_t* m_src, const uint64_t* m_P, const uint64_t* m_Dp, const uint64_t* rec_addr,
-                     const uint32_t* rec_klen, const uint32_t* fp_bad, skv_result** out) {
+                     const uint32_t* rec_klen, const uint32_t* fp_bad, const HeapRes* heap, skv_result** out) {
     hipStream_t st = ctx->stream;
     uint64_t K = 0;
     {
@@ -360,20 +398,23 @@ static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
     uint64_t* keep = dbuf<uint64_t>(ctx, "w_keep", K + 1);
     uint64_t* run_off = dbuf<uint64_t>(ctx, "w_run_off", K + 1);
     uint64_t* keep_ex = dbuf<uint64_t>(ctx, "w_keep_ex", K + 1);
-    unsigned long long* first_err = dbuf<unsigned long long>(ctx, "w_first_err", 1);
+    unsigned long long* first_err = dbuf<unsigned long long>(ctx, "w_first_err", 2);  // bad key, failed send
+    unsigned long long* tfirst = dbuf<unsigned long long>(ctx, "w_tfirst", K + 1);
     uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "w_scan_tmp", scan_tmp_words(K + 1) + 64);
     DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", K + 1);
     uint64_t total_rec_bytes = 0;
     for (uint64_t l : job.run_len) total_rec_bytes += l;
     uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + K + 16);
-    HIPCHK(hipMemsetAsync(first_err, 0xFF, 8, st));
+    HIPCHK(hipMemsetAsync(first_err, 0xFF, 16, st));
+    HIPCHK(hipMemsetAsync(tfirst, 0xFF, (K + 1) * 8, st));
     HIPCHK(hipMemsetAsync(tbad, 0, (K + 1) * 4, st));
     HIPCHK(hipMemsetAsync(run_len, 0, (K + 1) * 8, st));
     HIPCHK(hipMemsetAsync(keep, 0, (K + 1) * 8, st));
     launch_wal_keys(st, d_K, K, m_src, m_rec, rec_klen, m_P, tid, strip, wsize, canon, first_err);
-    launch_wal_flags(st, d_K, K, tid, strip, canon, m_src, m_rec, rec_klen, is_new, bad);
+    launch_wal_flags(st, d_K, K, tid, strip, canon, m_src, m_rec, rec_klen, is_new, bad, heap != nullptr);
     launch_scan(st, is_new, K, new_ex, scan_tmp);  // new_ex[K] = number of tables
-    launch_wal_index(st, d_K, K, is_new, new_ex, bad, tix, tstart, tbad);
+    launch_wal_index(st, d_K, K, is_new, new_ex, bad, tix, tstart, tbad, tfirst);
+    launch_wal_sendfail(st, new_ex + K, K, tstart, tfirst, first_err + 1);
     launch_scan(st, wsize, K, Pw, scan_tmp);       // stripped record offsets
     const uint64_t* d_NT = new_ex + K;
     launch_wal_tables(st, d_NT, K, tstart, Pw, tbad, job.max_run_size, run_len, keep);
@@ -384,22 +425,45 @@ static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
     launch_wal_gather(st, d_K, K, tix, tstart, keep, run_off, Pw, strip, m_src, m_rec, rec_klen, d_out);
     HIPCHK(hipGetLastError());
     mark(ctx, PH_GATHER);
-    uint64_t h[4];
+    uint64_t h[5];
     {
         uint64_t* hp = (uint64_t*)pinned(ctx, 64);
         d2h(ctx, hp, first_err, 8);
         d2h(ctx, hp + 1, d_NT, 8);
         d2h(ctx, hp + 2, keep_ex + K, 8);
         d2h(ctx, hp + 3, run_off + K, 8);
+        d2h(ctx, hp + 4, first_err + 1, 8);
         sync(ctx);
-        memcpy(h, hp, 32);
+        memcpy(h, hp, 40);
     }
     htrace("wal outcome read");
-    if (h[0] != ~0ull) {  // the first bad key in merged order fails the job (:67-79 `?`)
-        uint32_t rec = 0;
-        HIPCHK(hipMemcpy(&rec, m_rec + h[0], 4, hipMemcpyDeviceToHost));
-        throw ApiError{SKV_E_INVALID_INPUT, wal_key_error(fetch_key(ctx, rec_addr, rec_klen, rec))};
+    // The job's first failure in merged order: a bad key (:67-79 `?`), a send to a table whose task
+    // has failed (:157-161), or (heap-order mode) a stream's decode error (:66-67 `result?`).
+    // Sorted inputs without decode errors: survivor indices are the merged order.
+    std::vector<JobEvent> ev;
+    auto pos_of_survivor = [&](uint64_t j) -> uint64_t {
+        return heap ? read_dev(heap->pop_pos + read_dev(m_rec + j)) : j;
+    };
+    if (h[0] != ~0ull)
+        ev.push_back({pos_of_survivor(h[0]), 0, SKV_E_INVALID_INPUT,
+                      wal_key_error(fetch_key(ctx, rec_addr, rec_klen, read_dev(m_rec + h[0])))});
+    if (h[4] != ~0ull)
+        ev.push_back({pos_of_survivor(h[4]), 1, SKV_E_INTERNAL, "Internal error: Failed to send operation to table channel"});
+    if (heap)
+        for (const HeapRes::Dec& d : heap->dec) {
+            std::string msg;
+            const int code = derr_to_api(d.err, msg);
+            ev.push_back({heap->pos_of_original(d.rec), 2, code, msg});
+        }
+    if (getenv("SKV_HEAP_DEBUG")) {
+        fprintf(stderr, "[wal] K=%llu heap=%d badkey=%lld sendfail=%lld\n", (unsigned long long)K, heap ? 1 : 0,
+                (long long)h[0], (long long)h[4]);
+        for (const JobEvent& e : ev) fprintf(stderr, "  event pos=%llu sub=%d code=%d %s\n", (unsigned long long)e.pos, e.sub, e.code, e.msg.c_str());
+        if (heap)
+            for (uint64_t r = 0; r < R && r < 64; ++r)
+                fprintf(stderr, "  rec %llu pop=%llu\n", (unsigned long long)r, (unsigned long long)read_dev(heap->pop_pos + r));
     }
+    throw_first(ev);
     const uint64_t n_tables = h[1], n_kept = h[2], n_bytes = h[3];
     ResultBox* box = new ResultBox();
     skv_result* res = &box->pub;
@@ -730,7 +794,7 @@ static SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth
 // tiles x streams). hi/lo/cmp_klen become dense key ranks for the merge stage; klen stays the real
 // key length (descriptors, WAL split).
 static void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo, uint64_t*& addr, uint32_t*& klen,
-                         uint32_t*& meta, const uint32_t*& cmp_klen, bool last_wins) {
+                         uint32_t*& meta, const uint32_t*& cmp_klen, bool last_wins, const SElem** sorted = nullptr) {
     hipStream_t st = ctx->stream;
     SElem* E = dbuf<SElem>(ctx, "sort_e", R);
     SElem* T = dbuf<SElem>(ctx, "sort_t", R);
@@ -748,6 +812,7 @@ static void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo,
     uint32_t* nmeta = dbuf<uint32_t>(ctx, "srt_meta", R);
     launch_sort_store(st, R, S, meta, newkey, newkey_ex, nhi, nlo, naddr, nklen, ncklen, nmeta, last_wins);
     HIPCHK(hipGetLastError());
+    if (sorted) *sorted = S;
     hi = nhi;
     lo = nlo;
     addr = naddr;
@@ -1032,10 +1097,12 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         if (first_dec[s] != ~0ull && first_dec[s] + 1 < stream_valid[s]) any_dec = true;
 
     // ---- errors: which one k_way::merge surfaces first --------------------------------------
-    if ((any_err || any_dec) && (job.flags & SKV_SPLIT_BY_TABLE))
-        throw ApiError{SKV_E_UNSUPPORTED,
-                       "SKV_SPLIT_BY_TABLE with an undecodable or unsorted input stream: which of the run error and "
-                       "the WAL key / table outcome surfaces first is not resolved on device in this build"};
+    // Heap-order mode (skv_heap.hip) where the outcome depends on the merge's exact pop sequence
+    // past a stream's first key decrease or decode error: the WAL split with either, and the Delete
+    // filter with a decrease. Everywhere else the first trigger record decides (below).
+    const bool wal = (job.flags & SKV_SPLIT_BY_TABLE) != 0;
+    const bool heap = !job.batch && ((wal && (any_err || any_dec)) || ((job.flags & SKV_DROP_TOMBSTONES) && any_dec));
+    HeapRes hres;
     if (any_err || any_dec) {
         // (1) first items are pulled in the caller's vector order (k_way.rs:126-140)
         std::vector<uint32_t> by_vec(k);
@@ -1048,6 +1115,12 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
                 throw ApiError{code, msg};
             }
         }
+        if (heap) {
+            for (uint32_t s = 0; s < k; ++s)
+                if (stream_err[s]) hres.dec.push_back({stream_base[s] + stream_valid[s] - 1, stream_err[s]});
+        }
+    }
+    if ((any_err || any_dec) && !heap) {
         // (2) each stream's earliest trigger item; the one popped first wins
         struct Cand { uint32_t s; uint64_t idx; bool order; std::string key; };
         std::vector<Cand> cands;
@@ -1071,10 +1144,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             return a.s < b.s;
         });
         const Cand& w = cands[0];
-        if (any_order && (job.flags & SKV_DROP_TOMBSTONES))
-            throw ApiError{SKV_E_UNSUPPORTED,
-                           "unsorted input stream with SKV_DROP_TOMBSTONES: the reference's outcome depends on the "
-                           "Delete filter's interleaving; not resolved on device in this build"};
+        (void)any_order;
         if (w.order) throw ApiError{SKV_E_FORMAT, "Data format error: Operations must be sorted by key"};
         std::string msg;
         int code = derr_to_api(stream_err[w.s], msg);
@@ -1113,12 +1183,71 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     // SKV_SORT=1 forces that path (tests).
     uint32_t km = k;  // lists the splitter merge sees
     const uint32_t* cmp_klen = rec_klen;  // key lengths the merge compares (dense ranks: 0)
+    // the keys the merge orders by: the records' own, or (heap-order mode with a key decrease) each
+    // record's stream-prefix-maximum record's (skv_heap.hip)
+    uint64_t* cmp_hi = rec_hi;
+    uint64_t* cmp_lo = rec_lo;
+    const uint64_t* cmp_addr = rec_addr;
+    uint64_t* pop_pos = nullptr;
+    if (heap) {
+        // the fixed-stride parse poisons the merge on a key decrease (k_emit_fixed); here the
+        // decrease is what this mode merges exactly (broken runs never get this far: they reparse)
+        HIPCHK(hipMemsetAsync(d_flags + 2, 0, 4, st));
+        pop_pos = dbuf<uint64_t>(ctx, "heap_pop_pos", R);
+        // always the prefix-maximum keys: a stream may be unsorted past its decode error (records of
+        // later member runs), which any_dec does not see, and those records are merged too
+        {
+            uint32_t* eff = dbuf<uint32_t>(ctx, "heap_eff", R);
+            uint64_t* blk = dbuf<uint64_t>(ctx, "heap_blk", heap_key_blocks(R));
+            uint32_t* carry = dbuf<uint32_t>(ctx, "heap_carry", heap_key_blocks(R));
+            uint64_t* ehi = dbuf<uint64_t>(ctx, "heap_hi", R);
+            uint64_t* elo = dbuf<uint64_t>(ctx, "heap_lo", R);
+            uint32_t* ekl = dbuf<uint32_t>(ctx, "heap_klen", R);
+            uint64_t* ead = dbuf<uint64_t>(ctx, "heap_addr", R);
+            launch_heap_keys(st, R, d_stream_base, k, rec_hi, rec_lo, rec_klen, rec_addr, eff, blk, carry, ehi, elo, ekl,
+                             ead);
+            cmp_hi = ehi;
+            cmp_lo = elo;
+            cmp_klen = ekl;
+            cmp_addr = ead;
+        }
+    }
     std::vector<uint64_t> list_off = stream_base;
     uint64_t* d_list_off = d_stream_base;
     {
         const char* se = getenv("SKV_SORT");
         if ((k > (uint32_t)TILE_TARGET / 2 && R > (uint64_t)TILE_CAP) || (se && se[0] == '1') || job.batch) {
-            sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen, job.batch);
+            if (heap) {
+                // sort on the merge keys; the records' own keys, payload and meta follow in sorted
+                // order, and inv maps an original record index to its sorted position
+                uint64_t *h2 = cmp_hi, *l2 = cmp_lo, *a2 = (uint64_t*)cmp_addr;
+                uint32_t* k2 = (uint32_t*)cmp_klen;
+                uint32_t* m2 = rec_meta;
+                const uint32_t* ck = nullptr;
+                const SElem* S = nullptr;
+                sort_records(ctx, R, h2, l2, a2, k2, m2, ck, false, &S);
+                uint64_t* shi = dbuf<uint64_t>(ctx, "heap_s_hi", R);
+                uint64_t* slo = dbuf<uint64_t>(ctx, "heap_s_lo", R);
+                uint32_t* skl = dbuf<uint32_t>(ctx, "heap_s_klen", R);
+                uint64_t* sad = dbuf<uint64_t>(ctx, "heap_s_addr", R);
+                uint32_t* inv = dbuf<uint32_t>(ctx, "heap_inv", R);
+                launch_heap_sorted(st, R, S, rec_hi, rec_lo, rec_klen, rec_addr, shi, slo, skl, sad, inv);
+                rec_hi = shi;
+                rec_lo = slo;
+                rec_klen = skl;
+                rec_addr = sad;
+                rec_meta = m2;
+                cmp_hi = h2;
+                cmp_lo = l2;
+                cmp_addr = a2;
+                cmp_klen = ck;
+                hres.inv = inv;
+            } else {
+                sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen, job.batch);
+                cmp_hi = rec_hi;
+                cmp_lo = rec_lo;
+                cmp_addr = rec_addr;
+            }
             htrace("sort launched");
             km = 1;
             list_off = {0, R};
@@ -1130,8 +1259,8 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     std::vector<Level> lv(1);
     lv[0].N = R;
     lv[0].off = list_off;
-    lv[0].hi = rec_hi;
-    lv[0].lo = rec_lo;
+    lv[0].hi = cmp_hi;
+    lv[0].lo = cmp_lo;
     lv[0].d_off = d_list_off;
     const uint64_t S_step = std::max<uint64_t>(2, (uint64_t)TILE_TARGET / std::max<uint32_t>(km, 1));
     // SKV_HI_STEP=f: levels >= 2 (they only pick splitters for the sample sorts) at an f times
@@ -1175,7 +1304,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     const uint64_t* key_fp = nullptr;
     uint32_t* fp_bad = dbuf<uint32_t>(ctx, "fp_bad", 1);
     HIPCHK(hipMemsetAsync(fp_bad, 0, 4, st));
-    if (km > 1 && !ctx->exact_keys) {
+    if (km > 1 && !ctx->exact_keys && !heap) {
         const char* te = getenv("SKV_FP_TEST");
         if (te && te[0] == '1') {
             uint64_t* f = dbuf<uint64_t>(ctx, "rec_fp_test", R);
@@ -1198,7 +1327,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         uint64_t* bounds = dbuf<uint64_t>(ctx, nm, (T + 1) * km);
         const Level* U = li + 1 < (int)lv.size() ? &lv[li + 1] : nullptr;
         launch_bounds(st, l0, L.hi, L.lo, L.c, cmp_klen, L.d_off, km, U ? U->shi : nullptr, U ? U->slo : nullptr,
-                      U ? U->sc : nullptr, m, T, rec_addr, bounds, d_flags + 2);
+                      U ? U->sc : nullptr, m, T, cmp_addr, bounds, d_flags + 2);
         snprintf(nm, sizeof nm, "tile_n%d", li);
         uint64_t* tile_n = dbuf<uint64_t>(ctx, nm, T);
         snprintf(nm, sizeof nm, "tile_base%d", li);
@@ -1222,6 +1351,13 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             O.fp_bad = fp_bad;
             O.tstate = dbuf<uint64_t>(ctx, "tile_state", 3 * T);
             O.tcounter = dbuf<uint32_t>(ctx, "tile_ticket", 1);
+            if (heap) {
+                O.pay_addr = rec_addr;
+                O.act_hi = rec_hi;
+                O.act_lo = rec_lo;
+                O.act_klen = rec_klen;
+                O.pop_pos = pop_pos;
+            }
             HIPCHK(hipMemsetAsync(O.tstate, 0, 3 * T * 8, st));
             HIPCHK(hipMemsetAsync(O.tcounter, 0, 4, st));
 #if SKV_TILE_PROF
@@ -1236,19 +1372,57 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             snprintf(nm, sizeof nm, "s%d_lo", li); L.slo = O.olo = dbuf<uint64_t>(ctx, nm, L.N);
             snprintf(nm, sizeof nm, "s%d_c", li); L.sc = O.oc = dbuf<uint64_t>(ctx, nm, L.N);
         }
-        HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, cmp_klen, bounds, km, T, tile_base, rec_meta, rec_addr,
+        HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, cmp_klen, bounds, km, T, tile_base, rec_meta, cmp_addr,
                            (job.flags & SKV_DROP_TOMBSTONES) ? 1u : 0u, O, d_flags + 2));
         if (l0) T0 = T;
     }
     HIPCHK(hipGetLastError());
     mark(ctx, PH_MERGE);
     const uint64_t* d_K = d_Kout;
+    hres.pop_pos = pop_pos;
     if (job.flags & SKV_SPLIT_BY_TABLE) {
         htrace("merge launched");
-        const int rc = wal_stage(ctx, job, R, d_K, m_rec, m_src, m_P, m_Dp, rec_addr, rec_klen, fp_bad, out);
+        const int rc =
+            wal_stage(ctx, job, R, d_K, m_rec, m_src, m_P, m_Dp, rec_addr, rec_klen, fp_bad, heap ? &hres : nullptr, out);
         htrace("wal stage done");
         if (rc == RC_RETRY_EXACT) return rerun_exact(ctx, job, out);
         return rc;
+    }
+    if (heap) {
+        // Delete filter + unsorted input: build_runs' order check on what the filter let through
+        // (runs.rs:190-198, table_tree_compaction.rs:139-147), against the streams' decode errors
+        unsigned long long* first_bad = dbuf<unsigned long long>(ctx, "heap_first_bad", 1);
+        HIPCHK(hipMemsetAsync(first_bad, 0xFF, 8, st));
+        launch_merged_order(st, d_K, R, m_rec, rec_hi, rec_lo, rec_klen, rec_addr, first_bad);
+        HIPCHK(hipGetLastError());
+        sync(ctx);  // (read_dev copies on the null stream, which does not wait for the ctx stream)
+        const uint64_t v = read_dev((const uint64_t*)first_bad);
+        if (getenv("SKV_HEAP_DEBUG")) {  // diagnostic: the merged sequence of heap-order mode
+            const uint64_t K = read_dev(d_K);
+            fprintf(stderr, "[heap] R=%llu K=%llu first_bad=%lld\n", (unsigned long long)R, (unsigned long long)K,
+                    (long long)v);
+            const uint32_t* effp = (const uint32_t*)ctx->bufs["heap_eff"].p;
+            for (uint64_t i = 0; i < R && i < 40; ++i)
+                fprintf(stderr, "  rec %llu hi=%016llx lo=%016llx klen=%u eff=%u key=%s\n", (unsigned long long)i,
+                        (unsigned long long)read_dev(rec_hi + i), (unsigned long long)read_dev(rec_lo + i),
+                        read_dev(rec_klen + i), effp ? read_dev(effp + i) : 0u, fetch_key(ctx, rec_addr, rec_klen, i).c_str());
+            for (uint64_t g = 0; g < K && g < 200; ++g) {
+                const uint32_t r = read_dev(m_rec + g);
+                fprintf(stderr, "  g=%llu rec=%u pop=%llu key=%s cmpkey=%s\n", (unsigned long long)g, r,
+                        (unsigned long long)read_dev(pop_pos + r), fetch_key(ctx, rec_addr, rec_klen, r).c_str(),
+                        fetch_key(ctx, cmp_addr, cmp_klen, r).c_str());
+            }
+        }
+        std::vector<JobEvent> ev;
+        if (v != ~0ull)
+            ev.push_back({read_dev(pop_pos + read_dev(m_rec + v)), 0, SKV_E_FORMAT,
+                          "Data format error: Operations must be sorted by key"});
+        for (const HeapRes::Dec& d : hres.dec) {
+            std::string msg;
+            const int code = derr_to_api(d.err, msg);
+            ev.push_back({hres.pos_of_original(d.rec), 2, code, msg});
+        }
+        throw_first(ev);
     }
     // ---- chain + stats ----------------------------------------------------------------------
     uint64_t* run_b = dbuf<uint64_t>(ctx, "run_b", R + 2);

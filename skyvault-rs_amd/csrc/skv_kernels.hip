@@ -718,6 +718,12 @@ __device__ __forceinline__ void emit_merged(const TileOut& O, uint64_t g, uint32
     O.m_Dp[g] = pd;
 }
 
+// heap-order mode: the records' own keys (first-per-key compares them, not the merge keys)
+__device__ __forceinline__ int act_key_cmp(const TileOut& O, uint32_t a, uint32_t b) {
+    return key_cmp(O.act_hi[a], O.act_lo[a], O.act_klen[a], (const uint8_t*)O.pay_addr[a] + 5, O.act_hi[b],
+                   O.act_lo[b], O.act_klen[b], (const uint8_t*)O.pay_addr[b] + 5);
+}
+
 // after the last tile: K, P[K], Dp[K]
 __device__ __forceinline__ void emit_totals(const TileOut& O, uint64_t K, uint64_t B, uint64_t D) {
     O.Kout[0] = K;
@@ -783,8 +789,12 @@ __device__ void tile_big(Elems E, const uint64_t* bounds, uint32_t k, uint64_t t
         return;
     }
     // pass 1: this tile's totals (dedup + filter), then its global prefix
+    const bool heap = O.act_hi != nullptr;  // heap-order mode: first-per-key on the records' own keys
+    if (heap && O.pop_pos)
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) O.pop_pos[(uint32_t)xc[i]] = base + i;
     auto keep_at = [&](uint32_t i, uint32_t& m) -> bool {
-        const bool first = i == 0 || ekey_cmp(rec_addr, xh[i - 1], xl[i - 1], xc[i - 1], xh[i], xl[i], xc[i]) != 0;
+        const bool first = i == 0 || (heap ? act_key_cmp(O, (uint32_t)xc[i - 1], (uint32_t)xc[i])
+                                           : ekey_cmp(rec_addr, xh[i - 1], xl[i - 1], xc[i - 1], xh[i], xl[i], xc[i])) != 0;
         m = xm[i];
         return first && !(drop_deletes && (m >> 31));
     };
@@ -816,7 +826,8 @@ __device__ void tile_big(Elems E, const uint64_t* bounds, uint32_t k, uint64_t t
         const uint64_t rk = block_excl_scan<uint64_t>(keep ? 1 : 0, ws, ck);
         const uint64_t rb = block_excl_scan<uint64_t>(sz, ws, cb_);
         const uint64_t rd = block_excl_scan<uint64_t>(dl, ws, cd);
-        if (keep) emit_merged(O, g + rk, (uint32_t)xc[i], rec_addr[(uint32_t)xc[i]], pb + rb, pd + rd);
+        if (keep)
+            emit_merged(O, g + rk, (uint32_t)xc[i], (heap ? O.pay_addr : rec_addr)[(uint32_t)xc[i]], pb + rb, pd + rd);
         g += ck;
         pb += cb_;
         pd += cd;
@@ -917,7 +928,7 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
             load_elem<L0>(E, pos, rh[u], rl[u], rc[u]);
             if (L0) {
                 rmeta[u] = rec_meta[pos];
-                raddr[u] = rec_addr[pos];  // coalesced here, instead of a random gather later
+                raddr[u] = (O.pay_addr ? O.pay_addr : rec_addr)[pos];  // coalesced here, not gathered later
                 if (kfp) rfp[u] = kfp[pos];
             }
             rseg[u] = j;
@@ -1008,7 +1019,10 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const uint32_t e = threadIdx.x + u * TILE_THREADS;
-        if (e < n) paddr[rpos[u]] = raddr[u];
+        if (e < n) {
+            paddr[rpos[u]] = raddr[u];
+            if (O.pop_pos) O.pop_pos[(uint32_t)rc[u]] = base + rpos[u];
+        }
     }
     __syncthreads();
     // (a) first-per-key flags by merged position (k_way.rs:146-151)
@@ -1023,7 +1037,9 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
             const uint32_t e = mi[i];
             const uint64_t h = mh[i], c = el_c[e];
             bool first = true;
-            if (i > 0 && mh[i - 1] == h) {  // exact: first-per-key and the check of the fp shortcut
+            if (O.act_hi) {  // heap-order mode: adjacent pops compared on their own keys
+                if (i > 0) first = act_key_cmp(O, (uint32_t)el_c[mi[i - 1]], (uint32_t)c) != 0;
+            } else if (i > 0 && mh[i - 1] == h) {  // exact: first-per-key and the check of the fp shortcut
                 const uint32_t p = mi[i - 1];
                 const uint64_t lp = el_lo[p], le = el_lo[e], cp = el_c[p];
                 int kc = lp != le ? (lp < le ? -1 : 1) : 0;

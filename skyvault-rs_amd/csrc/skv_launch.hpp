@@ -60,9 +60,10 @@ void launch_wal_keys(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint
                      uint8_t* canon, unsigned long long* first_err);
 void launch_wal_flags(hipStream_t, const uint64_t* Kp, uint64_t max_K, const int64_t* tid, const uint32_t* strip,
                       const uint8_t* canon, const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen,
-                      uint64_t* is_new, uint32_t* bad);
+                      uint64_t* is_new, uint32_t* bad, bool exact);
 void launch_wal_index(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint64_t* is_new, const uint64_t* new_ex,
-                      const uint32_t* bad, uint32_t* tix, uint64_t* tstart, uint32_t* tbad);
+                      const uint32_t* bad, uint32_t* tix, uint64_t* tstart, uint32_t* tbad,
+                      unsigned long long* tfirst);
 void launch_wal_tables(hipStream_t, const uint64_t* NTp, uint64_t max_NT, const uint64_t* tstart, const uint64_t* Pw,
                        const uint32_t* tbad, uint64_t max_size, uint64_t* run_len, uint64_t* keep);
 void launch_wal_desc(hipStream_t, const uint64_t* NTp, uint64_t max_NT, const uint64_t* tstart, const uint64_t* Pw,
@@ -76,6 +77,18 @@ void launch_page_prep(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, c
                       const uint64_t* seg_r0, uint64_t* Dst, uint32_t* page_first, uint64_t max_K);
 void launch_gather_pages(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* P, const uint64_t* Dst,
                          const uint64_t* m_src, const uint32_t* page_first, uint8_t* out, uint64_t max_out_bytes);
+// skv_heap.hip — k_way::merge's heap pop order for unsorted streams (heap-order mode)
+void launch_heap_keys(hipStream_t, uint64_t R, const uint64_t* base, uint32_t k, const uint64_t* hi,
+                      const uint64_t* lo, const uint32_t* klen, const uint64_t* addr, uint32_t* eff, uint64_t* blk_agg,
+                      uint32_t* carry, uint64_t* ehi, uint64_t* elo, uint32_t* eklen, uint64_t* eaddr);
+uint64_t heap_key_blocks(uint64_t R);
+void launch_heap_sorted(hipStream_t, uint64_t R, const SElem* S, const uint64_t* hi, const uint64_t* lo,
+                        const uint32_t* klen, const uint64_t* addr, uint64_t* shi, uint64_t* slo, uint32_t* sklen,
+                        uint64_t* saddr, uint32_t* inv);
+void launch_merged_order(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint32_t* m_rec, const uint64_t* hi,
+                         const uint64_t* lo, const uint32_t* klen, const uint64_t* addr, unsigned long long* first_bad);
+void launch_wal_sendfail(hipStream_t, const uint64_t* NTp, uint64_t max_NT, const uint64_t* tstart,
+                         const unsigned long long* tfirst, unsigned long long* first_fail);
 // skv_stride.hip — fused stride path
 void launch_fx_sample(hipStream_t, const FxArgs& A, const uint64_t* off_dst, uint64_t Sstep, uint64_t n_dst,
                       uint64_t* dhi, uint64_t* dlo, uint64_t* dc);

@@ -103,14 +103,15 @@ __device__ __forceinline__ int stripped_cmp(const uint8_t* a, uint64_t la, const
 __global__ void k_wal_flags(const uint64_t* __restrict__ Kp, const int64_t* __restrict__ tid,
                             const uint32_t* __restrict__ strip, const uint8_t* __restrict__ canon,
                             const uint64_t* __restrict__ m_src, const uint32_t* __restrict__ m_rec,
-                            const uint32_t* __restrict__ rec_klen, uint64_t* is_new, uint32_t* bad) {
+                            const uint32_t* __restrict__ rec_klen, uint64_t* is_new, uint32_t* bad, uint32_t exact) {
     const uint64_t K = *Kp;
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= K) return;
     const bool nw = j == 0 || tid[j] != tid[j - 1];
     is_new[j] = nw ? 1 : 0;
     uint32_t b = 0;
-    if (!nw && !(canon[j - 1] && canon[j])) {
+    // (heap-order mode, unsorted inputs: the merged keys are not ascending, compare every pair)
+    if (!nw && (exact || !(canon[j - 1] && canon[j]))) {
         const uint64_t sa = strip[j - 1], sb = strip[j];
         const uint8_t* ka = (const uint8_t*)m_src[j - 1] + 5 + sa;
         const uint8_t* kb = (const uint8_t*)m_src[j] + 5 + sb;
@@ -120,10 +121,10 @@ __global__ void k_wal_flags(const uint64_t* __restrict__ Kp, const int64_t* __re
     bad[j] = b;
 }
 
-// table index per record, table start table, failing tables
+// table index per record, table start table, failing tables and each one's first failing record
 __global__ void k_wal_index(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ is_new,
                             const uint64_t* __restrict__ new_ex, const uint32_t* __restrict__ bad, uint32_t* tix,
-                            uint64_t* tstart, uint32_t* tbad) {
+                            uint64_t* tstart, uint32_t* tbad, unsigned long long* tfirst) {
     const uint64_t K = *Kp;
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= K) return;
@@ -131,7 +132,10 @@ __global__ void k_wal_index(const uint64_t* __restrict__ Kp, const uint64_t* __r
     tix[j] = (uint32_t)t;
     if (is_new[j]) tstart[t] = j;
     if (j == K - 1) tstart[t + 1] = K;
-    if (bad[j]) tbad[t] = 1;
+    if (bad[j]) {
+        tbad[t] = 1;
+        atomicMin(&tfirst[t], (unsigned long long)j);
+    }
 }
 
 // keep/drop per table: no order error and exactly one run (count == 1, or 1 + bytes <= max)
@@ -305,13 +309,15 @@ void launch_wal_keys(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const ui
 }
 void launch_wal_flags(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const int64_t* tid, const uint32_t* strip,
                       const uint8_t* canon, const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen,
-                      uint64_t* is_new, uint32_t* bad) {
+                      uint64_t* is_new, uint32_t* bad, bool exact) {
     if (max_K)
-        k_wal_flags<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, tid, strip, canon, m_src, m_rec, rec_klen, is_new, bad);
+        k_wal_flags<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, tid, strip, canon, m_src, m_rec, rec_klen, is_new, bad,
+                                                           exact ? 1u : 0u);
 }
 void launch_wal_index(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* is_new, const uint64_t* new_ex,
-                      const uint32_t* bad, uint32_t* tix, uint64_t* tstart, uint32_t* tbad) {
-    if (max_K) k_wal_index<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, is_new, new_ex, bad, tix, tstart, tbad);
+                      const uint32_t* bad, uint32_t* tix, uint64_t* tstart, uint32_t* tbad,
+                      unsigned long long* tfirst) {
+    if (max_K) k_wal_index<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, is_new, new_ex, bad, tix, tstart, tbad, tfirst);
 }
 void launch_wal_tables(hipStream_t s, const uint64_t* NTp, uint64_t max_NT, const uint64_t* tstart, const uint64_t* Pw,
                        const uint32_t* tbad, uint64_t max_size, uint64_t* run_len, uint64_t* keep) {

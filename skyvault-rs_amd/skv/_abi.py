@@ -25,6 +25,7 @@ SKV_E_INVALID_INPUT = 5
 SKV_E_INVALID_ARG = 6
 SKV_E_DEVICE = 7
 SKV_E_UNSUPPORTED = 8
+SKV_E_INTERNAL = 9
 
 SKV_DROP_TOMBSTONES = 1
 SKV_SPLIT_BY_TABLE = 2
@@ -38,6 +39,7 @@ ERROR_NAMES = {
     SKV_E_INVALID_ARG: "InvalidArgument",
     SKV_E_DEVICE: "Device",
     SKV_E_UNSUPPORTED: "Unsupported",
+    SKV_E_INTERNAL: "Internal",
 }
 
 
@@ -225,6 +227,28 @@ class StreamArgs:
 
 
 _STREAM_DT = _stream_dtype()
+
+
+def stream_table(seq_nos, run_ptrs, run_lens) -> StreamArgs:
+    """skv_stream[] of one member run per stream straight from numpy arrays (no Python loop per
+    stream): seq_nos int64, run_ptrs / run_lens uint64 (host or device addresses)."""
+    import numpy as np
+
+    seq = np.ascontiguousarray(seq_nos, dtype=np.int64)
+    ptrs = np.ascontiguousarray(run_ptrs, dtype=np.uint64)
+    lens = np.ascontiguousarray(run_lens, dtype=np.uint64)
+    n = seq.size
+    sa = StreamArgs.__new__(StreamArgs)
+    tbl = np.zeros(max(1, n), dtype=_STREAM_DT)
+    idx = np.arange(n, dtype=np.uint64) * np.uint64(8)
+    tbl["runs"][:n] = np.uint64(ptrs.ctypes.data) + idx
+    tbl["run_lens"][:n] = np.uint64(lens.ctypes.data) + idx
+    tbl["n_runs"][:n] = 1
+    tbl["seq_no"][:n] = seq
+    sa._keep = [ptrs, lens, tbl]
+    sa.n = n
+    sa.ptr = C.c_void_p(tbl.ctypes.data)
+    return sa
 
 
 def result_to_runs(res: SkvResult, host_bytes: Optional[bytes] = None) -> List[OutRun]:

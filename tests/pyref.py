@@ -14,6 +14,12 @@ from __future__ import annotations
 import heapq
 
 EMPTY, VERSION, IO, FORMAT, INVALID_INPUT = 1, 2, 3, 4, 5
+INTERNAL = 9
+# mpsc::channel(100) of a WAL table task (wal_compaction.rs:113): once the task's build_runs has
+# failed on an order error it drops its receiver; the job's sends to that table keep succeeding
+# only while they can be buffered, and the 101st send after the failing op can never succeed.
+# (Sends 1..100 may or may not fail -- a scheduling race; modelled here as succeeding.)
+WAL_SENDS_AFTER_FAIL = 101
 
 
 class Err(Exception):
@@ -175,27 +181,31 @@ def _parse_i64(s: bytes):
     return r, None
 
 
-def compact(streams, max_size, flags=0):
-    """The job composition. Returns [(run_bytes, stats, table_id)], dropped_tables."""
+def compact(streams, max_size, flags=0, races=None):
+    """The job composition. Returns [(run_bytes, stats, table_id)], dropped_tables. races (a list):
+    receives one entry per WAL table whose failed task races with 1..100 later sends to it."""
     seqs = [s for s, _ in streams]
     assert len(set(seqs)) == len(seqs)
     if flags & 2:
-        return _wal(streams, max_size)
+        return _wal(streams, max_size, races)
     ops = merge(streams)
     if flags & 1:
         ops = (o for o in ops if o[0] == "put")
     return [(b, st, 0) for b, st in build_runs(ops, max_size)], 0
 
 
-def _wal(streams, max_size):
+def _wal(streams, max_size, races=None):
     result = []
     dropped = 0
     cur_table = None
     cur_ops = []
+    fail_at = None  # index in cur_ops of the op whose order check fails the table's build_runs
     have = False
 
     def finish():
         nonlocal dropped
+        if races is not None and fail_at is not None and 0 < len(cur_ops) - 1 - fail_at < WAL_SENDS_AFTER_FAIL:
+            races.append(cur_table)
         try:
             runs = build_runs(cur_ops, max_size)
         except Err:
@@ -220,7 +230,12 @@ def _wal(streams, max_size):
             have = True
             cur_table = tid
             cur_ops = []
+            fail_at = None
         cur_ops.append((kind, k[strip:], v))
+        if fail_at is None and len(cur_ops) > 1 and cur_ops[-1][1] <= cur_ops[-2][1]:
+            fail_at = len(cur_ops) - 1  # runs.rs:190-198 inside the table task
+        if fail_at is not None and len(cur_ops) - 1 - fail_at == WAL_SENDS_AFTER_FAIL:
+            raise Err(INTERNAL, "Internal error: Failed to send operation to table channel")  # :157-161
     if have:
         finish()
     return result, dropped

@@ -1,0 +1,301 @@
+"""GPU parity at BASELINE.json's full sizes, through the device-resident entry point that
+bench.py measures (skv_compact_dev), against the oracle (oracle/skv_oracle.c).
+
+  config 2A / 2B  64 x 1 run x 238,821 records (4.0 GiB), built in HBM exactly as bench.py
+                  builds them: R = 15.3 M records, above the fused path's 2^22-record sampling
+                  switch. The oracle compacts the whole input in one call; every output byte and
+                  every one of the ~1,025 descriptors must match.
+  config 5        10^6 WAL runs x 83 records (3.8 GiB), SKV_SPLIT_BY_TABLE, at max 2^62 (one run
+                  per table) and at the jobs' 4 MiB (the exactly-one-run rule drops every table).
+                  The oracle runs per group of tables (whole tables are independent in
+                  wal_compaction.rs:66-174: the merged order visits them one after another), the
+                  groups in parallel threads; concatenated in table order they are the full
+                  expected output.
+  config 3F       256 x 1 run x 256 MiB (64 GiB, 206 M records, variable keys, 10 % Deletes),
+                  flags 0 and SKV_DROP_TOMBSTONES. The oracle merges 256 disjoint key ranges
+                  separately (k_way::merge restricted to a key range is the merge of the streams'
+                  sub-ranges; the Delete filter is per op) with an unbounded max run size, and
+                  ONE streaming build_runs (pyoracle.StreamBuilder, runs.rs:166-282) splits their
+                  concatenation into 4 MiB runs — so the greedy split, the order check and
+                  StatsV1 carry across ranges exactly as in one call. Every output byte and
+                  descriptor is compared.
+
+Device output is read back in slices with hipMemcpy, so host memory stays a few GiB (config 2:
+~20 GiB for the one-call oracle).
+"""
+import ctypes as C
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from skv import _abi
+from skv.api import Compactor
+
+import pyoracle
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+MiB = 1 << 20
+MAX_RUN = 4 * MiB
+SEED = 0x5EEDC0DE  # bench.rank_seed(0): the bench's own rank-0 input
+THREADS = int(os.environ.get("SKV_TEST_THREADS", "12"))
+
+
+@pytest.fixture(scope="module")
+def torch():
+    t = pytest.importorskip("torch")
+    t.cuda.init()
+    return t
+
+
+@pytest.fixture(scope="module")
+def dev(torch):
+    c = Compactor(0, profiling=True)
+    yield c
+    c.close()
+
+
+_hip = None
+_PROGRESS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "fullsize_progress.log")
+
+
+def _progress(msg: str):
+    """A line per step to gpurun_out/ (pytest captures stdout/stderr; a GPU-box run that writes
+    nothing for minutes is taken to be hung)."""
+    import time
+
+    os.makedirs(os.path.dirname(_PROGRESS), exist_ok=True)
+    with open(_PROGRESS, "a") as f:
+        f.write(f"{time.strftime('%H:%M:%S')} {msg}\n")
+
+
+def d2h(ptr: int, n: int) -> np.ndarray:
+    """n bytes at device address ptr -> a host numpy array (hipMemcpy, device-to-host)."""
+    global _hip
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so")
+    out = np.empty(n, dtype=np.uint8)
+    if n:
+        rc = _hip.hipMemcpy(C.c_void_p(out.ctypes.data), C.c_void_p(ptr), C.c_size_t(n), 2)
+        assert rc == 0, f"hipMemcpy D2H failed: {rc}"
+    return out
+
+
+def _first_diff(a: np.ndarray, b: np.ndarray):
+    n = min(a.size, b.size)
+    d = np.nonzero(a[:n] != b[:n])[0]
+    return int(d[0]) if d.size else n
+
+
+def _compare_bytes(res, pos: int, exp: np.ndarray, what: str, chunk: int = 1 << 30):
+    for q in range(0, exp.size, chunk):
+        part = exp[q:q + chunk]
+        got = d2h(res.dev_ptr + pos + q, part.size)
+        if not np.array_equal(got, part):
+            raise AssertionError(f"{what}: output byte {pos + q + _first_diff(got, part)} differs")
+
+
+# ------------------------------------------------------------------------------------------
+# config 2A / 2B: one oracle call over the whole 4 GiB input
+
+
+@pytest.mark.parametrize("variant", ["A", "B"])
+def test_config2_full_size(dev, torch, variant):
+    from skv.devgen import make_cfg2_on_device
+
+    device = torch.device("cuda", 0)
+    _progress(f"config 2{variant}: generating")
+    runs = make_cfg2_on_device(device, SEED, 64, 238821, 256, variant)
+    streams = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(runs)]
+    res = dev.compact_dev(streams, MAX_RUN, 0)
+    t = dev.timings()
+    assert t["path"] == _abi.PATH_FUSED, t
+    assert res.in_records == 64 * 238821 and res.in_records >= 1 << 22  # the fused level-1 switch
+    host = [r.cpu().numpy() for r in runs]
+    del runs
+    sa = _abi.stream_table(np.arange(1, 65), [h.ctypes.data for h in host], [h.size for h in host])
+    _progress(f"config 2{variant}: oracle")
+    exp, descs, info = pyoracle.compact_np(sa, MAX_RUN, 0)
+    _progress(f"config 2{variant}: compare")
+    assert (res.n_bytes, res.n_runs, res.out_records) == (exp.size, len(descs), info["out_records"])
+    _compare_bytes(res, 0, exp, f"config 2{variant}")
+    assert res.descs == descs
+    if variant == "A":
+        assert res.n_runs == 1025 and res.out_records == res.in_records
+    res.free()
+
+
+# ------------------------------------------------------------------------------------------
+# config 5: 10^6 WAL runs, oracle per group of whole tables
+
+
+def _table_rank(n_tables: int = 64) -> np.ndarray:
+    """rank of table t in merged (bytewise key) order: "{t}." sorts like str(t)."""
+    order = sorted(range(n_tables), key=str)
+    rank = np.empty(n_tables, dtype=np.int64)
+    rank[order] = np.arange(n_tables)
+    return rank
+
+
+def _wal_group_inputs(host: np.ndarray, groups: int):
+    """Per group of consecutive tables (in key order): one host buffer holding, for every WAL run
+    with records of those tables, a version byte + those records, and its stream table."""
+    n, rl = host.shape
+    recs = host[:, 1:].reshape(n, (rl - 1) // 49, 49)
+    k0, k1 = recs[:, :, 5].astype(np.int64) - 48, recs[:, :, 6]
+    table = np.where(k1 == ord("."), k0, 10 * k0 + (k1.astype(np.int64) - 48))
+    grp = _table_rank()[table] // (64 // groups)
+    assert (np.diff(grp, axis=1) >= 0).all()  # each run visits the tables in key order
+    for g in range(groups):
+        mask = grp == g
+        cnt = mask.sum(axis=1)
+        live = np.nonzero(cnt)[0]
+        c = cnt[live]
+        flat = recs[mask].reshape(-1)
+        starts = np.zeros(live.size, dtype=np.int64)
+        starts[1:] = np.cumsum(49 * c[:-1])
+        buf = np.insert(flat, starts, 1).astype(np.uint8)
+        run_off = starts + np.arange(live.size)
+        yield buf, live + 1, buf.ctypes.data + run_off.astype(np.uint64), 1 + 49 * c
+
+
+def _wal_oracle(host: np.ndarray, max_run: int, groups: int = 16):
+    def one(args):
+        buf, seqs, ptrs, lens = args
+        sa = _abi.stream_table(seqs, ptrs, lens)
+        data, descs, info = pyoracle.compact_np(sa, max_run, _abi.SKV_SPLIT_BY_TABLE)
+        _progress(f"config 5: table group of {len(seqs)} runs done")
+        del buf
+        return data, descs, info
+
+    with ThreadPoolExecutor(THREADS) as ex:
+        parts = list(ex.map(one, _wal_group_inputs(host, groups)))
+    data = np.concatenate([p[0] for p in parts]) if parts else np.empty(0, np.uint8)
+    descs, base = [], 0
+    for d, ds, _ in parts:
+        for x in ds:
+            descs.append((x[0] + base, x[1], x[2], x[3], x[4] + base, x[5], x[6] + base, x[7], x[8]))
+        base += d.size
+    dropped = sum(p[2]["dropped_tables"] for p in parts)
+    out_records = sum(p[2]["out_records"] for p in parts)
+    return data, descs, dropped, out_records
+
+
+def test_config5_full_size(dev, torch):
+    from skv.devgen import make_cfg5_on_device
+
+    n_streams = 1_000_000
+    device = torch.device("cuda", 0)
+    _progress("config 5: generating")
+    buf = make_cfg5_on_device(device, SEED, n_streams)
+    rl = buf.shape[1]
+    sa = _abi.stream_table(np.arange(1, n_streams + 1), buf.data_ptr() + rl * np.arange(n_streams, dtype=np.uint64),
+                           np.full(n_streams, rl))
+    host = buf.cpu().numpy()
+    for max_run in (1 << 62, MAX_RUN):
+        res = dev.compact_dev(sa, max_run, _abi.SKV_SPLIT_BY_TABLE)
+        assert dev.timings()["sorted"] == 1  # 10^6-way fan-in takes the record sort
+        raw = res._res.contents
+        exp, descs, dropped, out_records = _wal_oracle(host, max_run)
+        assert (res.n_bytes, res.n_runs, raw.dropped_tables, res.out_records) == \
+            (exp.size, len(descs), dropped, out_records)
+        _compare_bytes(res, 0, exp, f"config 5 max {max_run}")
+        assert res.descs == descs
+        if max_run == MAX_RUN:  # ~63 MB per table > 4 MiB: the one-run rule drops all of them
+            assert res.n_runs == 0 and dropped == 64
+        else:
+            assert res.n_runs == 64 and dropped == 0
+        res.free()
+
+
+# ------------------------------------------------------------------------------------------
+# config 3 at 256 x 256 MiB: key-range merges + one streaming build_runs
+
+
+@pytest.fixture(scope="module")
+def cfg3_full(torch):
+    from skv.devgen import make_cfg3_full_on_device
+
+    device = torch.device("cuda", 0)
+    n_streams, run_mib = 256, 256
+    _progress("config 3F: generating")
+    runs, index = make_cfg3_full_on_device(device, SEED, n_streams, run_mib, with_index=True)
+    _progress("config 3F: generated")
+    n = (run_mib << 20) // 333
+    universe = n * n_streams * 2
+    P = 256  # key ranges (id ranges: keys sort like their ids)
+    bounds = torch.linspace(0, universe, P + 1, device=device).to(torch.int64)
+    bounds[-1] = universe
+    cuts = []
+    for r, (ids, off) in zip(runs, index):
+        pos = torch.searchsorted(ids, bounds)
+        off_ext = torch.cat([off, torch.tensor([r.numel()], device=device, dtype=off.dtype)])
+        cuts.append(off_ext[pos].cpu().numpy())
+    del index
+    torch.cuda.synchronize()
+    yield runs, np.stack(cuts), P
+    del runs
+
+
+def _range_input(torch, runs, cuts, p):
+    """Key range p of every stream as one host buffer (version byte + the range's records per
+    non-empty stream) and its stream table."""
+    one = torch.ones(1, dtype=torch.uint8, device=runs[0].device)
+    parts, seqs, lens = [], [], []
+    for s, r in enumerate(runs):
+        a, b = int(cuts[s, p]), int(cuts[s, p + 1])
+        if b > a:
+            parts += [one, r[a:b]]
+            seqs.append(s + 1)
+            lens.append(1 + b - a)
+    if not parts:
+        return None
+    buf = torch.cat(parts).cpu().numpy()
+    offs = np.zeros(len(lens), dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1])
+    return buf, np.array(seqs), buf.ctypes.data + offs, np.array(lens)
+
+
+@pytest.mark.parametrize("flags", [0, _abi.SKV_DROP_TOMBSTONES], ids=["flags0", "drop_tombstones"])
+def test_config3_full_size(dev, torch, cfg3_full, flags):
+    runs, cuts, P = cfg3_full
+    streams = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(runs)]
+    res = dev.compact_dev(streams, MAX_RUN, flags)
+    assert dev.timings()["path"] == _abi.PATH_GENERAL
+    in_bytes = sum(r.numel() for r in runs)
+    assert res.in_bytes == in_bytes and in_bytes > 63 * (1 << 30)
+
+    def merge_range(p):
+        inp = _range_input(torch, runs, cuts, p)
+        if inp is None:
+            return None
+        buf, seqs, ptrs, lens = inp
+        data, _, _ = pyoracle.compact_np(_abi.stream_table(seqs, ptrs, lens), 1 << 62, flags)
+        return data
+
+    sb = pyoracle.StreamBuilder(MAX_RUN)
+    pos = 0
+    window = 2 * THREADS  # key ranges in flight (each ~250 MB in + out)
+    with ThreadPoolExecutor(THREADS) as ex:
+        futs = {p: ex.submit(merge_range, p) for p in range(min(window, P))}
+        for p in range(P):
+            data = futs.pop(p).result()
+            if p + window < P:
+                futs[p + window] = ex.submit(merge_range, p + window)
+            if data is None or data.size == 0:
+                continue
+            out = sb.feed(data)
+            _compare_bytes(res, pos, out, f"config 3F range {p}")
+            if p % 16 == 0:
+                _progress(f"config 3F flags {flags}: range {p}/{P} ok")
+            pos += out.size
+    tail, descs = sb.finish()
+    tail = np.frombuffer(tail, dtype=np.uint8)
+    _compare_bytes(res, pos, tail, "config 3F tail")
+    assert res.n_bytes == pos + tail.size
+    assert res.descs == descs
+    assert all(d[1] <= MAX_RUN for d in descs)
+    if flags:
+        assert all(d[3] == 0 for d in descs)
+    res.free()
