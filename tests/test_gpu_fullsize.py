@@ -264,7 +264,7 @@ def test_config3_full_size(dev, torch, cfg3_full, flags):
     res = dev.compact_dev(streams, MAX_RUN, flags)
     assert dev.timings()["path"] == _abi.PATH_GENERAL
     in_bytes = sum(r.numel() for r in runs)
-    assert res.in_bytes == in_bytes and in_bytes > 63 * (1 << 30)
+    assert res.in_bytes == in_bytes and in_bytes > 63e9  # 256 x ~249 MB
 
     def merge_range(p):
         inp = _range_input(torch, runs, cuts, p)
