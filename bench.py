@@ -59,18 +59,33 @@ def cpu_baseline(config, sample_records, n_streams, vsize, repeats, run_mib=16):
         streams = gen.config3(seed=0xC0FFEE, n_streams=n_streams, run_bytes=(min(run_mib, 16) << 20) // 16)
         sample = f"{n_streams} streams x {run_mib / 16:.2f} MiB runs (config-3 shape, 1/16 of the bench's runs)"
     else:
-        streams = gen.config5(seed=0xC0FFEE, n_streams=20000)
+        from skv import _abi
+        from skv.devgen import make_cfg5_on_device
+
+        n5 = 20000
+        host = make_cfg5_on_device(torch.device("cuda", torch.cuda.current_device()), 0xC0FFEE, n5).cpu().numpy()
+        rl = host.shape[1]
+        table5 = _abi.stream_table(np.arange(1, n5 + 1), host.ctypes.data + rl * np.arange(n5, dtype=np.uint64),
+                                   np.full(n5, rl))
         flags, max_run = 2, 1 << 62
-        sample = "20,000 WAL runs x 83 records (config-5 shape, 1/50 of the streams)"
-    nbytes = gen.total_bytes(streams)
-    pyoracle.compact(streams, max_run, flags)  # warm-up
+        sample = f"{n5:,} WAL runs x 83 records (config-5 shape, 1/50 of the streams)"
+        streams = None
+    nbytes = gen.total_bytes(streams) if streams is not None else host.size
+
+    def run_once():
+        if streams is not None:
+            pyoracle.compact(streams, max_run, flags)
+        else:
+            pyoracle.compact_np(table5, max_run, flags)
+
+    run_once()  # warm-up
     ts = []
     for _ in range(repeats):
         t0 = time.perf_counter()
-        pyoracle.compact(streams, max_run, flags)
+        run_once()
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
-    return {
+    out = {
         "value": round(nbytes / t / GiB, 4),
         "unit": "GiB/s",
         "cores": 1,
@@ -78,6 +93,79 @@ def cpu_baseline(config, sample_records, n_streams, vsize, repeats, run_mib=16):
         "sample": f"{sample} = {nbytes / 2**20:.1f} MiB, median of {repeats} after 1 warm-up",
         "seconds_per_run": round(t, 3),
     }
+    out.update(host_cpu())
+    if config == "2A":
+        out["config4_8_compactions"] = cpu_baseline_config4(sample_records, n_streams, vsize, repeats)
+    return out
+
+
+def host_cpu():
+    """The box's host CPU as cpu_baseline reports it: logical CPUs and the model name."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "cpu_model": model}
+
+
+def cpu_baseline_config4(sample_records, n_streams, vsize, repeats):
+    """BASELINE config 4's CPU leg: 8 independent compactions of the config-2A
+    shape (distinct seeds, each a bounded sample) on min(8, nproc) threads — the oracle releases
+    the GIL inside its C call, so the threads run in parallel."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from skv import _abi, gen
+
+    jobs = []
+    for j in range(8):
+        streams = gen.config2(seed=0xC0FFEE + 1000 * j, n_streams=n_streams, n_records=sample_records, vsize=vsize)
+        bufs = [np.frombuffer(r[1][0], dtype=np.uint8) for r in streams]
+        jobs.append((bufs, _abi.stream_table(np.arange(1, n_streams + 1), [b.ctypes.data for b in bufs],
+                                             [b.size for b in bufs])))
+    nbytes = sum(b.size for bufs, _ in jobs for b in bufs)
+    threads = min(8, os.cpu_count() or 1)
+
+    def one(job):
+        pyoracle.compact_np(job[1], MAX_RUN, 0)
+
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(one, jobs))  # warm-up
+        ts = []
+        for _ in range(repeats):
+            t0 = time.perf_counter()
+            list(ex.map(one, jobs))
+            ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    return {"value": round(nbytes / t / GiB, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"8 independent config-2A compactions (distinct seeds), each {n_streams} streams x "
+                      f"{sample_records} records = {nbytes / 8 / 2**20:.1f} MiB, on {threads} threads, "
+                      f"median of {repeats} after 1 warm-up"}
+
+
+def check_invariants(res, config, max_run, in_records):
+    """Size-independent properties of one full-size result (the bench's own input; bit-exact parity
+    at these sizes is tests/test_gpu_fullsize.py): byte accounting, run sizes under the greedy
+    split, record counts. Raises on a violation."""
+    d = res.descs
+    assert res.n_runs == len(d)
+    assert sum(x[1] for x in d) == res.n_bytes, "run lengths != output bytes"
+    off = 0
+    for x in d:  # contiguous runs, each within max (or a single record)
+        assert x[0] == off, "runs not contiguous"
+        assert x[1] <= max_run or x[2] + x[3] == 1, "run above max with more than one record"
+        off += x[1]
+    assert sum(x[2] + x[3] for x in d) == res.out_records
+    if config == "2A":  # no key repeats across streams (2^64 key space): every record survives
+        assert res.out_records == in_records
+        assert res.n_bytes == res.in_bytes - 64 + res.n_runs
+    return {"checked": True, "runs": len(d), "out_records": res.out_records}
 
 
 def rank_seed(rank):
@@ -124,7 +212,9 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # gloo over the host: the path shards with no data-path exchange (north_star: no RCCL), so
+        # the only cross-rank traffic is the start/stop barrier and two scalars
+        dist.init_process_group("gloo")
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
 
@@ -185,9 +275,9 @@ def main():
         res.free()
 
     def barrier():
+        torch.cuda.synchronize(device)
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize(device)
 
     gather_ms, total_ms, phases, host_ms, sync_ms, call_ms = [], [], [], [], [], []
     barrier()
@@ -207,7 +297,13 @@ def main():
         out_bytes, n_out_runs = res.n_bytes, res.n_runs
         res.free()
     barrier()
-    elapsed, total_in = reduce_over_ranks(time.perf_counter() - t0, in_bytes, dist, device)
+    t_end = time.perf_counter()
+    # invariants of the measured call's output (outside the timed region)
+    res = comp.compact_dev(table, max_run, flags)
+    invariants = check_invariants(res, config, max_run, res.in_records) if config != "5" else {
+        "checked": True, "runs": res.n_runs, "out_records": res.out_records}
+    res.free()
+    elapsed, total_in = reduce_over_ranks(t_end - t0, in_bytes, dist, torch.device("cpu"))
 
     # PCIe-inclusive figure (not `value`): the host entry point skv_compact with the inputs in
     # pinned host memory and the output runs returned in pinned host memory.
@@ -310,6 +406,7 @@ def main():
                 "pipeline_frac": round((in_bytes + out_bytes) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             },
         }
+        line["invariants"] = invariants
         if host_path is not None:
             line["host_path"] = host_path
         if world == 1 and not args.no_cpu_baseline:

@@ -104,6 +104,9 @@ struct skv_ctx {
     double sync_ms = 0;
     bool exact_keys = false;  // rerun after a fingerprint shortcut misordered a tile (never in practice)
     bool exact_utf8 = false;  // rerun with UTF-8 checked in the chunk walks (a run holds a bad key)
+    // compact_device calls started on this ctx: the s_* tables belong to the newest one, so a call
+    // that continues after a nested rerun (none does; each returns at once) must not read them
+    uint64_t table_gen = 0;
 };
 
 struct ResultBox {  // skv_result + how to free it
@@ -178,9 +181,21 @@ static void stage_copy(void* dst, const void* src, size_t bytes) {
     }
     const size_t part = ((bytes + nt - 1) / nt + 4095) & ~(size_t)4095;
     std::vector<std::thread> th;
-    for (unsigned i = 1; i < nt && i * part < bytes; ++i)
-        th.emplace_back([=] { memcpy((uint8_t*)dst + i * part, (const uint8_t*)src + i * part, std::min(part, bytes - i * part)); });
+    th.reserve(nt);
+    auto piece = [=](unsigned i) {
+        memcpy((uint8_t*)dst + i * part, (const uint8_t*)src + i * part, std::min(part, bytes - i * part));
+    };
+    unsigned started = 1;  // pieces [1, started) run on threads
+    for (unsigned i = 1; i < nt && i * part < bytes; ++i) {
+        try {
+            th.emplace_back(piece, i);
+        } catch (...) {  // no thread: this piece and the rest are copied here
+            break;
+        }
+        started = i + 1;
+    }
     memcpy(dst, src, std::min(part, bytes));
+    for (unsigned i = started; i < nt && i * part < bytes; ++i) piece(i);
     for (auto& t : th) t.join();
 }
 
@@ -859,6 +874,10 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     mark(ctx, PH_START);
     htrace("start");
     const uint32_t k = (uint32_t)job.ranked.size();
+    const uint64_t my_gen = ++ctx->table_gen;
+    auto tables_mine = [&]() {  // the s_* tables below are ctx storage that a nested call refills
+        if (ctx->table_gen != my_gen) throw DevError("internal: host tables read after a nested rerun refilled them");
+    };
     // ---- run table ------------------------------------------------------------------------
     std::vector<RunInfo>& runs = ctx->s_runs;  // (a rerun returns right after its nested call)
     runs.clear();
@@ -1090,6 +1109,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     }
     mark(ctx, PH_CHECK);
     htrace("check done");
+    tables_mine();
     if (job.search) return search_stage(ctx, job, runs[0], R, stream_err[0], first_dec[0], rec_addr, rec_hi, rec_lo,
                                         rec_klen, rec_meta);
     bool any_dec = false;
@@ -1380,6 +1400,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     mark(ctx, PH_MERGE);
     const uint64_t* d_K = d_Kout;
     hres.pop_pos = pop_pos;
+    tables_mine();
     if (job.flags & SKV_SPLIT_BY_TABLE) {
         htrace("merge launched");
         const int rc =
@@ -1528,7 +1549,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
 }
 
 // ------------------------------------------------------------------------------------------
-static int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t max_run_size, uint32_t flags,
+static int build_job_impl(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t max_run_size, uint32_t flags,
                      Job& job) {
     if (n && !streams) return set_err(ctx, SKV_E_INVALID_ARG, "streams is NULL");
     if (flags & ~(uint32_t)(SKV_DROP_TOMBSTONES | SKV_SPLIT_BY_TABLE))
@@ -1577,6 +1598,16 @@ static int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64
     return SKV_OK;
 }
 
+// the job tables of a call (10^6-stream calls: vectors of that size) without unwinding into C
+static int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t max_run_size, uint32_t flags,
+                     Job& job) {
+    try {
+        return build_job_impl(ctx, streams, n, max_run_size, flags, job);
+    } catch (const std::exception& e) {
+        return set_err(ctx, SKV_E_DEVICE, "host error: %s", e.what());
+    }
+}
+
 static int run_guarded(skv_ctx* ctx, const Job& job, skv_result** out, double t_entry) {
     try {
         ctx->sync_ms = 0;
@@ -1591,6 +1622,9 @@ static int run_guarded(skv_ctx* ctx, const Job& job, skv_result** out, double t_
     } catch (const DevError& e) {
         (void)hipStreamSynchronize(ctx->stream);
         return set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());
+    } catch (const std::exception& e) {  // bad_alloc of a host table, system_error, ...: never unwind into C
+        (void)hipStreamSynchronize(ctx->stream);
+        return set_err(ctx, SKV_E_DEVICE, "host error: %s", e.what());
     }
 }
 
@@ -1703,6 +1737,8 @@ static int compact_host_job(skv_ctx* ctx, Job& job, skv_result** out, double t_e
         }
     } catch (const DevError& e) {
         return set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());
+    } catch (const std::exception& e) {
+        return set_err(ctx, SKV_E_DEVICE, "host error: %s", e.what());
     }
     skv_result* dres = nullptr;
     rc = run_guarded(ctx, job, &dres, t_entry);
@@ -1816,6 +1852,8 @@ int skv_search_run(skv_ctx* ctx, const uint8_t* run, uint64_t len, const uint8_t
         job.run_ptr[0] = (uint64_t)(uintptr_t)d_in;
     } catch (const DevError& e) {
         return set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());
+    } catch (const std::exception& e) {
+        return set_err(ctx, SKV_E_DEVICE, "host error: %s", e.what());
     }
     skv_result* none = nullptr;
     rc = run_guarded(ctx, job, &none, t_entry);

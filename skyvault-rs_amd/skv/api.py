@@ -77,9 +77,12 @@ def exported_symbols_present() -> List[str]:
 class DeviceResult:
     """Output of compact_dev: run bytes stay in HBM (device pointer owned by the ctx)."""
 
-    def __init__(self, lib, res_ptr):
+    def __init__(self, lib, res_ptr, owner=None):
         self._lib = lib
         self._res = res_ptr
+        # the bytes live in the ctx's "out" buffer: keep the Compactor (and so the ctx) alive
+        # while this result is (skv.h: valid until the next call on the ctx or skv_result_free)
+        self._owner = owner
         r = res_ptr.contents
         self.dev_ptr = int(r.bytes or 0)
         self.n_bytes = int(r.n_bytes)
@@ -160,7 +163,7 @@ class Compactor:
         rc = self.lib.skv_compact_dev(self.ctx, sa.ptr, sa.n, max_run_size, flags, C.byref(res))
         if rc != SKV_OK:
             raise self._err(rc)
-        return DeviceResult(self.lib, res)
+        return DeviceResult(self.lib, res, self)
 
     def compact_host_ptrs(self, streams: Sequence[Tuple[int, Sequence[Tuple[int, int]]]],
                           max_run_size: int = MAX_RUN_SIZE, flags: int = 0) -> Tuple[int, int]:
@@ -197,7 +200,7 @@ class Compactor:
         rc = self.lib.skv_encode_batch_dev(self.ctx, C.c_void_p(ptr), length, max_run_size, C.byref(res))
         if rc != SKV_OK:
             raise self._err(rc)
-        return DeviceResult(self.lib, res)
+        return DeviceResult(self.lib, res, self)
 
     def search_run(self, run: bytes, keys: Sequence[bytes]):
         """runs::search_run (runs.rs:285-398) for every key at once on the device. Returns one

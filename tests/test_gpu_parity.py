@@ -441,3 +441,46 @@ def test_threaded_table_staging(dev):
             assert exp == got, _diff(exp, got)
     finally:
         del os.environ["SKV_PAR_COPY_MIN"]
+
+
+def test_device_entry_reuse_across_calls(dev):
+    """skv_compact_dev lends the ctx's job tables to each call: a 2000-stream call, a call that
+    fails in build_job (duplicate seq_no), a failing decode and a small call on one ctx, each
+    checked against the oracle."""
+    import ctypes
+
+    torch = pytest.importorskip("torch")
+    hip = ctypes.CDLL("libamdhip64.so")
+
+    def on_device(streams):
+        keep = [(s, [torch.frombuffer(bytearray(r), dtype=torch.uint8).cuda() if len(r) else
+                     torch.empty(0, dtype=torch.uint8, device="cuda") for r in runs]) for s, runs in streams]
+        torch.cuda.synchronize()
+        return keep, [(s, [(t.data_ptr(), t.numel()) for t in ts]) for s, ts in keep]
+
+    def blob(res):
+        out = torch.empty(max(1, res.n_bytes), dtype=torch.uint8, device="cuda")
+        assert hip.hipMemcpy(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(res.dev_ptr),
+                             ctypes.c_size_t(res.n_bytes), 3) == 0
+        return bytes(out[: res.n_bytes].cpu().numpy())
+
+    big = gen.config5(n_streams=2000)
+    small = gen.config2(n_streams=3, n_records=500, vsize=16, variant="B")
+    dup = [(1, [small[0][1][0]]), (1, [small[1][1][0]])]
+    corrupt = [(2, [small[0][1][0][:-3]]), (1, [small[1][1][0]])]
+    for streams, flags in ((big, _abi.SKV_SPLIT_BY_TABLE), (dup, 0), (corrupt, 0), (small, 0), (big, 0)):
+        keep, dstreams = on_device(streams)
+        try:
+            exp = pyoracle.compact_bytes(streams, 64 * KiB, flags)
+        except _abi.RunError as e:
+            exp = ("err", e.code, e.message)
+        try:
+            res = dev.compact_dev(dstreams, 64 * KiB, flags)
+            got = (blob(res), res.descs)
+            res.free()
+        except _abi.RunError as e:
+            got = ("err", e.code, e.message)
+        if exp[0] == "err" and exp[1] == _abi.SKV_E_INVALID_ARG:  # API misuse: code only
+            assert got[0] == "err" and got[1] == _abi.SKV_E_INVALID_ARG
+        else:
+            assert got == exp
