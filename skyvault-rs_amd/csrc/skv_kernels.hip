@@ -1155,8 +1155,20 @@ __device__ uint64_t chain_search(const uint64_t* P, uint64_t lo, uint64_t hi, ui
     return lo;
 }
 
-constexpr int CH_D = 8;   // predicted windows in flight
-constexpr int CH_Q = 8;   // entries per lane per window (512 per window)
+#ifndef SKV_CH_D
+#define SKV_CH_D 32
+#endif
+#ifndef SKV_CH_Q
+#define SKV_CH_Q 1
+#endif
+// Predicted windows in flight and entries per lane per window. With every record fitting a run,
+// run d+1 from a known start ends within (d+1) x (largest record) bytes of its lower bound, so
+// 32 windows of 64 consecutive P entries (one load per lane each, all independent) cover 32 run
+// ends per round for records of ~300 B (config 3: 3F chain 26.6 ms with 8 x 512-entry windows,
+// whose 64 loads per lane per round kept one wave latency-bound); rounds shrink to fewer
+// windows when the records are small relative to the largest (see ch_d below).
+constexpr int CH_D = SKV_CH_D;
+constexpr int CH_Q = SKV_CH_Q;
 constexpr uint32_t CH_SHIFT = 10;  // byte -> record table granularity (1 KiB)
 
 // tbl[t] = the surviving record j with P[j] <= t * 2^CH_SHIFT < P[j+1] (K past the end): lets the
@@ -1228,6 +1240,14 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
         if (L == 0) L = 1;
         if (L > K) L = K;
     }
+    // windows per round: keep the byte uncertainty of the last one, ch_d x mr, within ~3/4 of a
+    // window's records at the average record size
+    int ch_d = CH_D;
+    if (all_fit && tbl) {
+        const uint64_t avg = PK / K > 0 ? PK / K : 1;
+        const uint64_t cap = (uint64_t)(48 * CH_Q) * avg / (mr > 0 ? mr : 1);
+        ch_d = cap < 1 ? 1 : (cap < (uint64_t)CH_D ? (int)cap : CH_D);
+    }
     while (b < K) {
         // prefetch CH_D windows of P around the predicted ends of the next CH_D runs
         uint64_t wv[CH_D][CH_Q];
@@ -1240,10 +1260,11 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
             if (tbl && all_fit) {
                 const uint64_t low = Pb + (uint64_t)(d + 1) * (max_size - 1 - mr);
                 const uint64_t t = low >> CH_SHIFT;
-                wsd[d] = low >= PK ? K : tbl[t];
+                wsd[d] = (low >= PK || d >= ch_d) ? K : tbl[t];
             } else {
                 const uint64_t c = b + (uint64_t)(d + 1) * L;
-                wsd[d] = c > 128 ? c - 128 : 0;
+                const uint64_t back = 16ull * CH_Q;
+                wsd[d] = c > back ? c - back : 0;
             }
         }
 #pragma unroll
@@ -1254,12 +1275,12 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
 #pragma unroll
             for (int q = 0; q < CH_Q; ++q) {
                 uint64_t pos = ws + (uint64_t)lane * CH_Q + q;
-                wv[d][q] = pos <= K ? P[pos] : ~0ull;
+                wv[d][q] = (pos <= K && d < ch_d) ? P[pos] : ~0ull;
             }
         }
 #pragma unroll
         for (int d = 0; d < CH_D; ++d) {
-            if (b < K) {  // (no break: keeps the loop fully unrolled, windows in registers)
+            if (b < K && d < ch_d) {  // (no break: keeps the loop fully unrolled, windows in registers)
             uint64_t e, Pe = 0;
             if (max_size == 0 || (!all_fit && P[b + 1] - Pb + 1 > max_size)) {
                 e = b + 1;  // a run of one record that alone exceeds max (runs.rs:219 needs !first)

@@ -1,0 +1,92 @@
+"""Independent compactions across the GPUs of one node (BASELINE config 4).
+
+The path shards with no exchange: each compaction (one table's buffer, one tree level, one WAL
+flush; orchestrator_service.rs:119-170 schedules them independently) runs whole on one GPU.
+`MultiCompactor` keeps one skv_ctx and one host thread per device; `submit` queues a compaction
+to the device with the least queued input bytes (the jobs differ in size, so round-robin would
+leave GPUs idle behind one large job) and returns a Future. The C call releases the GIL, so the
+device threads run their compactions concurrently. There is no collective and no RCCL: results
+come back to the caller's thread through the futures.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+from concurrent.futures import Future
+from typing import Callable, List, Optional, Sequence
+
+
+class MultiCompactor:
+    def __init__(self, devices: Sequence[int], factory: Optional[Callable[[int], object]] = None):
+        """devices: HIP ordinals, one worker each (an ordinal may repeat: several ctxs on one GPU
+        overlap one job's copies with another's kernels). factory(device) -> compactor; default
+        skv.api.Compactor."""
+        if factory is None:
+            from .api import Compactor
+
+            factory = Compactor
+        self._lock = threading.Lock()
+        self._workers: List[_Worker] = [_Worker(factory, d, self._lock) for d in devices]
+        for w in self._workers:
+            w.start()
+
+    def submit(self, streams, max_run_size: int, flags: int = 0, with_info: bool = False) -> Future:
+        size = sum(len(r) if isinstance(r, (bytes, bytearray, memoryview)) else r[1]
+                   for _, runs in streams for r in runs)
+        with self._lock:
+            w = min(self._workers, key=lambda x: x.queued_bytes)
+            w.queued_bytes += size
+        fut: Future = Future()
+        w.q.put((streams, max_run_size, flags, with_info, size, fut))
+        return fut
+
+    def map(self, jobs: Sequence[tuple]) -> List[object]:
+        """jobs: [(streams, max_run_size, flags)] -> results in job order (raises the first error)."""
+        futs = [self.submit(*j) for j in jobs]
+        return [f.result() for f in futs]
+
+    def close(self):
+        for w in self._workers:
+            w.q.put(None)
+        for w in self._workers:
+            w.join()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class _Worker(threading.Thread):
+    def __init__(self, factory, device: int, lock: threading.Lock):
+        super().__init__(daemon=True)
+        self.lock = lock
+        self.factory = factory
+        self.device = device
+        self.q: "queue.Queue" = queue.Queue()
+        self.queued_bytes = 0
+        self.error: Optional[BaseException] = None
+
+    def run(self):
+        try:
+            comp = self.factory(self.device)  # the ctx is created and used on this thread only
+        except BaseException as e:  # every later job fails with the ctx error
+            comp, self.error = None, e
+        while True:
+            item = self.q.get()
+            if item is None:
+                break
+            streams, max_run_size, flags, with_info, size, fut = item
+            try:
+                if comp is None:
+                    raise self.error
+                fut.set_result(comp.compact(streams, max_run_size, flags, with_info=with_info))
+            except BaseException as e:
+                fut.set_exception(e)
+            finally:
+                with self.lock:
+                    self.queued_bytes -= size
+        close = getattr(comp, "close", None)
+        if close:
+            close()
