@@ -211,6 +211,19 @@ enum {
 int skv_search_run(skv_ctx* ctx, const uint8_t* run, uint64_t len, const uint8_t* keys, const uint64_t* key_offs,
                    uint32_t n_keys, skv_lookup* out);
 
+/*
+ * A run parsed once for many lookup batches: the cache service keeps a run for many GetFromRun /
+ * Prefetch calls (cache_service.rs:52-94), so its boundary index is built once. create stages the
+ * run (host memory) into HBM owned by the index and parses it; search is skv_search_run's
+ * contract (same outcomes, same panic texts) without re-staging or re-parsing. An index is used
+ * with ctxs of the device it was created on; free it with skv_run_index_free.
+ */
+typedef struct skv_run_index skv_run_index;
+int skv_run_index_create(skv_ctx* ctx, const uint8_t* run, uint64_t len, skv_run_index** out);
+int skv_run_index_search(skv_ctx* ctx, const skv_run_index* index, const uint8_t* keys, const uint64_t* key_offs,
+                         uint32_t n_keys, skv_lookup* out);
+void skv_run_index_free(skv_run_index* index);
+
 void skv_result_free(skv_result* r);
 
 #ifdef __cplusplus

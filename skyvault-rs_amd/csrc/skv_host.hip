@@ -285,6 +285,7 @@ struct Job {
     uint32_t sr_n = 0;
     skv_lookup* sr_out = nullptr;
     bool search = false;
+    struct skv_run_index* index_out = nullptr;  // skv_run_index_create: keep the parse, search nothing
 };
 
 // a record's key bytes (host copy) for error-trigger comparisons
@@ -836,29 +837,77 @@ static void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo,
     cmp_klen = ncklen;
 }
 
+// A run parsed once for many lookup batches (skv_run_index_create): the run bytes and its record
+// arrays stay in HBM, owned by the index (the cache service keeps one per cached run,
+// cache_service.rs:52-94).
+struct skv_run_index {
+    int device = 0;
+    uint64_t len = 0;
+    uint32_t panic_all = 0;  // empty run / bad version: every lookup panics (runs.rs:288-297)
+    bool clean = false;      // parsed without error or key decrease: binary search, else the scan
+    uint64_t R = 0;
+    void* mem = nullptr;     // one allocation: run bytes | rec_addr | rec_hi | rec_lo | rec_klen | rec_meta
+    const uint8_t* run = nullptr;
+    const uint64_t *addr = nullptr, *hi = nullptr, *lo = nullptr;
+    const uint32_t *klen = nullptr, *meta = nullptr;
+};
+
+// the lookups of one batch against parsed arrays (bsearch) or the run bytes (scan)
+static void search_launch(skv_ctx* ctx, const uint8_t* run, uint64_t len, bool clean, uint64_t R,
+                          const uint64_t* rec_addr, const uint64_t* rec_hi, const uint64_t* rec_lo,
+                          const uint32_t* rec_klen, const uint32_t* rec_meta, const uint8_t* keys,
+                          const uint64_t* key_offs, uint32_t n, skv_lookup* out) {
+    hipStream_t st = ctx->stream;
+    const uint64_t qbytes = key_offs[n];
+    uint8_t* d_q = dbuf<uint8_t>(ctx, "sr_keys", qbytes + 16);
+    uint64_t* d_off = dbuf<uint64_t>(ctx, "sr_offs", n + 1);
+    SrResult* d_out = dbuf<SrResult>(ctx, "sr_out", n);
+    if (qbytes) h2d(ctx, d_q, keys, qbytes);
+    h2d(ctx, d_off, key_offs, (n + 1) * 8);
+    if (clean)
+        launch_search_bsearch(st, run, len, R, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, d_q, d_off, n, d_out);
+    else
+        launch_search_scan(st, run, len, d_q, d_off, n, d_out);
+    HIPCHK(hipGetLastError());
+    static_assert(sizeof(SrResult) == sizeof(skv_lookup), "lookup layout");
+    if (n) HIPCHK(hipMemcpyAsync(out, d_out, (size_t)n * sizeof(SrResult), hipMemcpyDeviceToHost, st));
+    sync(ctx);
+}
+
 // skv_search_run after the parse: a run that parsed clean with no key decrease takes one binary
 // search per key over its record arrays; any other run the reference's scan (skv_search.hip).
 static int search_stage(skv_ctx* ctx, const Job& job, const RunInfo& run, uint64_t R, uint32_t run_err,
                         uint64_t first_dec, const uint64_t* rec_addr, const uint64_t* rec_hi, const uint64_t* rec_lo,
                         const uint32_t* rec_klen, const uint32_t* rec_meta) {
-    hipStream_t st = ctx->stream;
-    const uint32_t n = job.sr_n;
-    const uint64_t qbytes = job.sr_offs[n];
-    uint8_t* d_q = dbuf<uint8_t>(ctx, "sr_keys", qbytes + 16);
-    uint64_t* d_off = dbuf<uint64_t>(ctx, "sr_offs", n + 1);
-    SrResult* d_out = dbuf<SrResult>(ctx, "sr_out", n);
-    if (qbytes) h2d(ctx, d_q, job.sr_keys, qbytes);
-    h2d(ctx, d_off, job.sr_offs, (n + 1) * 8);
     const bool clean = run_err == 0 && first_dec == ~0ull;
-    if (clean)
-        launch_search_bsearch(st, (const uint8_t*)run.ptr, run.len, R, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
-                              d_q, d_off, n, d_out);
-    else
-        launch_search_scan(st, (const uint8_t*)run.ptr, run.len, d_q, d_off, n, d_out);
-    HIPCHK(hipGetLastError());
-    static_assert(sizeof(SrResult) == sizeof(skv_lookup), "lookup layout");
-    if (n) HIPCHK(hipMemcpyAsync(job.sr_out, d_out, (size_t)n * sizeof(SrResult), hipMemcpyDeviceToHost, st));
-    sync(ctx);
+    if (skv_run_index* ix = job.index_out) {  // keep the parsed arrays in the index's memory
+        ix->clean = clean;
+        ix->R = clean ? R : 0;
+        if (clean && R) {
+            hipStream_t st = ctx->stream;
+            uint8_t* base = (uint8_t*)ix->mem + ((ix->len + 255) & ~(uint64_t)255);
+            uint64_t* a = (uint64_t*)base;
+            uint64_t* h = a + R;
+            uint64_t* l = h + R;
+            uint32_t* kl = (uint32_t*)(l + R);
+            uint32_t* m = kl + R;
+            HIPCHK(hipMemcpyAsync(a, rec_addr, R * 8, hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipMemcpyAsync(h, rec_hi, R * 8, hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipMemcpyAsync(l, rec_lo, R * 8, hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipMemcpyAsync(kl, rec_klen, R * 4, hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipMemcpyAsync(m, rec_meta, R * 4, hipMemcpyDeviceToDevice, st));
+            sync(ctx);
+            ix->addr = a;
+            ix->hi = h;
+            ix->lo = l;
+            ix->klen = kl;
+            ix->meta = m;
+        }
+        ctx->timings.path = clean ? SKV_PATH_FIXED : SKV_PATH_GENERAL;
+        return SKV_OK;
+    }
+    search_launch(ctx, (const uint8_t*)run.ptr, run.len, clean, R, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
+                  job.sr_keys, job.sr_offs, job.sr_n, job.sr_out);
     ctx->timings.path = clean ? SKV_PATH_FIXED : SKV_PATH_GENERAL;
     return SKV_OK;
 }
@@ -1861,6 +1910,85 @@ int skv_search_run(skv_ctx* ctx, const uint8_t* run, uint64_t len, const uint8_t
     for (uint32_t i = 0; i < n_keys; ++i)
         if (out[i].kind == SKV_LOOKUP_PANIC) return set_err(ctx, SKV_E_FORMAT, "%s", search_panic_text(out[i].panic).c_str());
     return SKV_OK;
+}
+
+int skv_run_index_create(skv_ctx* ctx, const uint8_t* run, uint64_t len, skv_run_index** out) {
+    const double t_entry = now_ms();
+    if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
+    *out = nullptr;
+    if (len && !run) return set_err(ctx, SKV_E_INVALID_ARG, "run is NULL");
+    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    std::unique_ptr<skv_run_index> ix(new (std::nothrow) skv_run_index());
+    if (!ix) return set_err(ctx, SKV_E_DEVICE, "host allocation failed");
+    ix->device = ctx->device;
+    ix->len = len;
+    if (len == 0 || run[0] != 1) {  // every lookup panics before the scan loop (runs.rs:288-297)
+        ix->panic_all = len == 0 ? (uint32_t)SKV_PANIC_EMPTY : (SKV_PANIC_VERSION | ((uint32_t)run[0] << 8));
+        *out = ix.release();
+        return SKV_OK;
+    }
+    // worst case: every record 5 bytes (an empty-key Delete) -> R <= len / 5
+    const uint64_t maxR = len / 5 + 1;
+    const size_t bytes = ((len + 255) & ~(uint64_t)255) + maxR * 32 + 256;
+    if (hipMalloc(&ix->mem, bytes) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "index allocation of %zu bytes failed", bytes);
+    ix->run = (const uint8_t*)ix->mem;
+    if (hipMemcpy(ix->mem, run, len, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(ix->mem);
+        return set_err(ctx, SKV_E_DEVICE, "index staging copy failed");
+    }
+    Job job;
+    int rc = batch_job(ctx, ix->run, len, 1ull << 62, job);
+    if (rc) {
+        (void)hipFree(ix->mem);
+        return rc;
+    }
+    job.batch = false;
+    job.search = true;
+    job.index_out = ix.get();
+    skv_result* none = nullptr;
+    rc = run_guarded(ctx, job, &none, t_entry);
+    if (rc) {
+        (void)hipFree(ix->mem);
+        return rc;
+    }
+    *out = ix.release();
+    return SKV_OK;
+}
+
+int skv_run_index_search(skv_ctx* ctx, const skv_run_index* ix, const uint8_t* keys, const uint64_t* key_offs,
+                         uint32_t n_keys, skv_lookup* out) {
+    if (!ctx || !ix) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/index is NULL");
+    if (ix->device != ctx->device) return set_err(ctx, SKV_E_INVALID_ARG, "index belongs to device %d", ix->device);
+    if (n_keys && (!out || !key_offs)) return set_err(ctx, SKV_E_INVALID_ARG, "out/key_offs is NULL");
+    if (n_keys && key_offs[n_keys] && !keys) return set_err(ctx, SKV_E_INVALID_ARG, "keys is NULL");
+    for (uint32_t i = 0; i < n_keys; ++i)
+        if (key_offs[i + 1] < key_offs[i]) return set_err(ctx, SKV_E_INVALID_ARG, "key_offs not ascending at %u", i);
+    if (n_keys == 0) return SKV_OK;
+    if (ix->panic_all) {
+        for (uint32_t i = 0; i < n_keys; ++i) out[i] = skv_lookup{SKV_LOOKUP_PANIC, ix->panic_all, 0, 0};
+        return set_err(ctx, SKV_E_FORMAT, "%s", search_panic_text(ix->panic_all).c_str());
+    }
+    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    try {
+        search_launch(ctx, ix->run, ix->len, ix->clean, ix->R, ix->addr, ix->hi, ix->lo, ix->klen, ix->meta, keys,
+                      key_offs, n_keys, out);
+    } catch (const DevError& e) {
+        return set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());
+    } catch (const std::exception& e) {
+        return set_err(ctx, SKV_E_DEVICE, "host error: %s", e.what());
+    }
+    for (uint32_t i = 0; i < n_keys; ++i)
+        if (out[i].kind == SKV_LOOKUP_PANIC) return set_err(ctx, SKV_E_FORMAT, "%s", search_panic_text(out[i].panic).c_str());
+    return SKV_OK;
+}
+
+void skv_run_index_free(skv_run_index* ix) {
+    if (!ix) return;
+    if (ix->mem) {
+        (void)hipSetDevice(ix->device);
+        (void)hipFree(ix->mem);
+    }
+    delete ix;
 }
 
 int skv_encode_batch_dev(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_t max_run_size,

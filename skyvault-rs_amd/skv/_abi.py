@@ -133,6 +133,9 @@ EXPORTED_SYMBOLS = [
     "skv_encode_batch",
     "skv_encode_batch_dev",
     "skv_search_run",
+    "skv_run_index_create",
+    "skv_run_index_search",
+    "skv_run_index_free",
     "skv_result_free",
 ]
 

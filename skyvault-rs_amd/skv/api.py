@@ -60,6 +60,12 @@ def load():
     l.skv_search_run.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32,
                                  C.c_void_p]
     l.skv_search_run.restype = C.c_int
+    l.skv_run_index_create.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]
+    l.skv_run_index_create.restype = C.c_int
+    l.skv_run_index_search.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
+    l.skv_run_index_search.restype = C.c_int
+    l.skv_run_index_free.argtypes = [C.c_void_p]
+    l.skv_run_index_free.restype = None
     for fn in (l.skv_encode_batch, l.skv_encode_batch_dev):
         fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.POINTER(SkvResult))]
         fn.restype = C.c_int
@@ -202,6 +208,43 @@ class Compactor:
             raise self._err(rc)
         return DeviceResult(self.lib, res, self)
 
+    def run_index(self, run: bytes) -> "RunIndex":
+        """skv_run_index_create: the run staged and parsed once for many lookup batches."""
+        run = bytes(run)
+        buf = C.create_string_buffer(run, max(1, len(run)))
+        h = C.c_void_p()
+        rc = self.lib.skv_run_index_create(self.ctx, C.cast(buf, C.c_void_p), len(run), C.byref(h))
+        if rc != SKV_OK:
+            raise self._err(rc)
+        return RunIndex(self, h, run)
+
+    def _lookup(self, fn, run: bytes, keys: Sequence[bytes]):
+        import numpy as np
+
+        from ._abi import LOOKUP_FOUND, LOOKUP_NOT_FOUND, LOOKUP_TOMBSTONE, PANIC_TEXT, SkvLookup
+
+        kb = b"".join(bytes(k) for k in keys)
+        offs = np.zeros(len(keys) + 1, dtype=np.uint64)
+        if keys:
+            offs[1:] = np.cumsum([len(k) for k in keys])
+        qbuf = C.create_string_buffer(kb, max(1, len(kb)))
+        out = (SkvLookup * max(1, len(keys)))()
+        rc = fn(C.cast(qbuf, C.c_void_p), C.c_void_p(offs.ctypes.data), len(keys), C.cast(out, C.c_void_p))
+        if rc not in (SKV_OK, 4):  # 4 = SKV_E_FORMAT: some key panicked, outcomes filled in
+            raise self._err(rc)
+        res = []
+        for i in range(len(keys)):
+            o = out[i]
+            if o.kind == LOOKUP_FOUND:
+                res.append(("found", run[o.val_off:o.val_off + o.val_len]))
+            elif o.kind == LOOKUP_TOMBSTONE:
+                res.append(("tombstone", None))
+            elif o.kind == LOOKUP_NOT_FOUND:
+                res.append(("not_found", None))
+            else:
+                res.append(("panic", PANIC_TEXT[o.panic & 0xFF].format(o.panic >> 8)))
+        return res
+
     def search_run(self, run: bytes, keys: Sequence[bytes]):
         """runs::search_run (runs.rs:285-398) for every key at once on the device. Returns one
         outcome per key: ("found", value) | ("tombstone", None) | ("not_found", None) |
@@ -241,6 +284,31 @@ class Compactor:
         t = SkvTimings()
         self.lib.skv_ctx_get_timings(self.ctx, C.byref(t))
         return {f: getattr(t, f) for f, _ in SkvTimings._fields_}
+
+
+class RunIndex:
+    """A run parsed once (skv_run_index_create); search() takes any number of lookup batches."""
+
+    def __init__(self, owner: Compactor, handle, run: bytes):
+        self._owner = owner  # the ctx the index was built with (same device) stays alive
+        self._h = handle
+        self._run = run
+
+    def search(self, keys: Sequence[bytes]):
+        lib, ctx, h = self._owner.lib, self._owner.ctx, self._h
+        return self._owner._lookup(lambda q, o, n, out: lib.skv_run_index_search(ctx, h, q, o, n, out), self._run,
+                                   keys)
+
+    def close(self):
+        if self._h:
+            self._owner.lib.skv_run_index_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def device_count() -> int:

@@ -86,3 +86,31 @@ def test_search_panics(dev):
     cases.append(bytes(bad2))
     for c in cases:
         _check(dev, c, qs)
+
+
+def test_run_index_many_batches(dev):
+    """skv_run_index_*: the run staged and parsed once, then several lookup batches, each equal to
+    skv_search_run and to the restatement — clean runs (binary search), unsorted / duplicate /
+    corrupt runs (the scan) and the panic-only runs; two indexes alive on one ctx."""
+    r = random.Random(12)
+    runs = []
+    run, keys = _sorted_run(r, 3000)
+    runs.append((run, keys))
+    run2, keys2 = _sorted_run(r, 500, dup=0.3)
+    runs.append((run2, keys2))
+    ops = [fmt.put(f"k{i:03d}", bytes([i & 255])) for i in r.sample(range(300), 300)]
+    runs.append((fmt.encode_run(ops), [f"k{i:03d}".encode() for i in range(0, 320, 3)]))
+    runs.append((run[: len(run) // 2], keys[::5]))
+    runs.append((b"", [b"a"]))
+    runs.append((b"\x03" + run[1:], [b"a"]))
+    idx = [(dev.run_index(rb), rb, ks) for rb, ks in runs]
+    try:
+        for batch in range(3):
+            for ix, rb, ks in idx:
+                q = [k for k in ks if r.random() < 0.5][:200] + [b"zz%d" % batch, b""]
+                exp = [pyoracle.search_run(rb, k) for k in q]
+                assert ix.search(q) == exp
+                assert dev.search_run(rb, q) == exp
+    finally:
+        for ix, _, _ in idx:
+            ix.close()
