@@ -1196,6 +1196,10 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
                                               const uint32_t* __restrict__ tbl, uint64_t n_tbl) {
     const uint64_t K = *Kp;
     const int lane = threadIdx.x;
+#if SKV_CHAIN_PROF
+    uint64_t cp_t0 = __builtin_amdgcn_s_memrealtime(), cp_mm = 0, cp_p1 = 0, cp_p2 = 0, cp_p3 = 0, cp_fb = 0,
+             cp_rounds = 0;
+#endif
     // n_runs_out = {runs, K, output record bytes P[K]}: the host's single readback
     if (K == 0) {
         if (lane == 0) { run_b[0] = 0; n_runs_out[0] = 0; n_runs_out[1] = 0; n_runs_out[2] = 0; }
@@ -1218,6 +1222,9 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
         o = __shfl_xor(mn, d, 64);
         mn = o < mn ? o : mn;
     }
+#if SKV_CHAIN_PROF
+    cp_mm = __builtin_amdgcn_s_memrealtime() - cp_t0;
+#endif
     // every record fits a run on its own when 1 + largest record <= max: no oversize probe
     const bool all_fit = max_size >= 1 && (uint64_t)mr + 1 <= max_size;
     if (all_fit && mn == mr) {
@@ -1249,24 +1256,38 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
         ch_d = cap < 1 ? 1 : (cap < (uint64_t)CH_D ? (int)cap : CH_D);
     }
     while (b < K) {
+#if SKV_CHAIN_PROF
+        uint64_t cp_a = __builtin_amdgcn_s_memrealtime();
+        ++cp_rounds;
+#endif
         // prefetch CH_D windows of P around the predicted ends of the next CH_D runs
+        const uint64_t m_round = m;
+        uint64_t rb = 0;
         uint64_t wv[CH_D][CH_Q];
         uint64_t wsd[CH_D];
         // window starts: with every record fitting a run, run d+1 from here ends at a record
         // starting in (Pb + (d+1)(max-1-mr), Pb + (d+1)(max-1)] bytes: the byte table gives the
         // record at the low end with one load (all CH_D loads independent); else by count
-#pragma unroll
-        for (int d = 0; d < CH_D; ++d) {
+        // lane d computes window d's start (the table entries as ONE vector load: a uniform
+        // address per window made them scalar loads, waited for one by one, 13 us per round)
+        {
+            uint64_t wl;
             if (tbl && all_fit) {
-                const uint64_t low = Pb + (uint64_t)(d + 1) * (max_size - 1 - mr);
-                const uint64_t t = low >> CH_SHIFT;
-                wsd[d] = (low >= PK || d >= ch_d) ? K : tbl[t];
+                const uint64_t low = Pb + (uint64_t)(lane + 1) * (max_size - 1 - mr);
+                wl = (low >= PK || lane >= ch_d) ? K : (uint64_t)tbl[low >> CH_SHIFT];
             } else {
-                const uint64_t c = b + (uint64_t)(d + 1) * L;
+                const uint64_t c = b + (uint64_t)(lane + 1) * L;
                 const uint64_t back = 16ull * CH_Q;
-                wsd[d] = c > back ? c - back : 0;
+                wl = c > back ? c - back : 0;
             }
+#pragma unroll
+            for (int d = 0; d < CH_D; ++d) wsd[d] = readlane_u64(wl, d);
         }
+#if SKV_CHAIN_PROF
+        { uint64_t x = 0; for (int d = 0; d < CH_D; ++d) x += wsd[d]; if (x == 7) run_b[0] = x; }
+        uint64_t cp_b = __builtin_amdgcn_s_memrealtime();
+        cp_p1 += cp_b - cp_a;
+#endif
 #pragma unroll
         for (int d = 0; d < CH_D; ++d) {
             uint64_t ws = wsd[d];
@@ -1278,6 +1299,11 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
                 wv[d][q] = (pos <= K && d < ch_d) ? P[pos] : ~0ull;
             }
         }
+#if SKV_CHAIN_PROF
+        { uint64_t x = 0; for (int d = 0; d < CH_D; ++d) x += wv[d][0]; if (x == 7) run_b[0] = x; }
+        uint64_t cp_c = __builtin_amdgcn_s_memrealtime();
+        cp_p2 += cp_c - cp_b;
+#endif
 #pragma unroll
         for (int d = 0; d < CH_D; ++d) {
             if (b < K && d < ch_d) {  // (no break: keeps the loop fully unrolled, windows in registers)
@@ -1318,16 +1344,30 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
                     else if (ws > b + 1) hi = ws - 1;  // window all > v: answer before it
                     e = chain_search(P, lo, hi, v, lane);
                     Pe = P[e];
+#if SKV_CHAIN_PROF
+                    ++cp_fb;
+#endif
                 }
             }
-            if (lane == 0) run_b[m] = b;
+            rb = lane == d ? b : rb;  // this round's run starts, stored together below
             ++m;
             L = e - b;
             b = e;
             Pb = Pe;
             }
         }
+        if ((uint64_t)lane < m - m_round) run_b[m_round + lane] = rb;
+#if SKV_CHAIN_PROF
+        cp_p3 += __builtin_amdgcn_s_memrealtime() - cp_c;
+#endif
     }
+#if SKV_CHAIN_PROF
+    if (lane == 0)
+        printf("[chain] total %llu ticks: minmax %llu, rounds %llu, p1 %llu p2 %llu p3 %llu, fallbacks %llu, ch_d %d, runs %llu\n",
+               (unsigned long long)(__builtin_amdgcn_s_memrealtime() - cp_t0), (unsigned long long)cp_mm,
+               (unsigned long long)cp_rounds, (unsigned long long)cp_p1, (unsigned long long)cp_p2,
+               (unsigned long long)cp_p3, (unsigned long long)cp_fb, ch_d, (unsigned long long)m);
+#endif
     if (lane == 0) {
         run_b[m] = K;
         *n_runs_out = m;
