@@ -199,6 +199,45 @@ static void stage_copy(void* dst, const void* src, size_t bytes) {
     for (auto& t : th) t.join();
 }
 
+// [0, n) as nb contiguous blocks fn(b, lo, hi) on host threads: the per-run and per-stream
+// table loops of a 10^6-stream call (config 5) are memory-bound at one core's bandwidth, ~10 ns
+// per entry. Below min_par entries one block runs on the calling thread; a block whose thread
+// cannot be started runs here too.
+static unsigned par_nblocks(uint64_t n, uint64_t min_par = 1u << 16) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    const unsigned nt = std::min<unsigned>(8, hw ? hw : 1);
+    return n < min_par ? 1u : nt;
+}
+template <typename F>
+static void par_run(uint64_t n, unsigned nb, F&& fn) {
+    auto lo = [&](unsigned b) { return n * b / nb; };
+    std::vector<std::thread> th;
+    th.reserve(nb);
+    unsigned started = 1;
+    for (unsigned b = 1; b < nb; ++b) {
+        try {
+            th.emplace_back([&, b] { fn(b, lo(b), lo(b + 1)); });
+        } catch (...) {
+            break;
+        }
+        started = b + 1;
+    }
+    fn(0u, lo(0), lo(1));
+    for (unsigned b = started; b < nb; ++b) fn(b, lo(b), lo(b + 1));
+    for (auto& t : th) t.join();
+}
+// two-pass block scan: count(lo, hi) -> items of the block; fill(b, lo, hi, base) with base = the
+// items of all earlier blocks. Returns the total.
+template <typename C, typename F>
+static uint64_t par_scan(uint64_t n, C&& count, F&& fill, uint64_t min_par = 1u << 16) {
+    const unsigned nb = par_nblocks(n, min_par);
+    std::vector<uint64_t> base(nb + 1, 0);
+    par_run(n, nb, [&](unsigned b, uint64_t lo, uint64_t hi) { base[b + 1] = count(lo, hi); });
+    for (unsigned b = 0; b < nb; ++b) base[b + 1] += base[b];
+    par_run(n, nb, [&](unsigned b, uint64_t lo, uint64_t hi) { fill(b, lo, hi, base[b]); });
+    return base[nb];
+}
+
 // async H2D of a host table through the pinned upload arena
 static void h2d_up(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
     if (!bytes) return;
@@ -418,9 +457,7 @@ static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
     unsigned long long* tfirst = dbuf<unsigned long long>(ctx, "w_tfirst", K + 1);
     uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "w_scan_tmp", scan_tmp_words(K + 1) + 64);
     DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", K + 1);
-    uint64_t total_rec_bytes = 0;
-    for (uint64_t l : job.run_len) total_rec_bytes += l;
-    uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + K + 16);
+    uint8_t* d_out = dbuf<uint8_t>(ctx, "out", job.in_bytes + K + 16);  // in_bytes: the run lengths' sum
     HIPCHK(hipMemsetAsync(first_err, 0xFF, 16, st));
     HIPCHK(hipMemsetAsync(tfirst, 0xFF, (K + 1) * 8, st));
     HIPCHK(hipMemsetAsync(tbad, 0, (K + 1) * 4, st));
@@ -929,24 +966,45 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     };
     // ---- run table ------------------------------------------------------------------------
     std::vector<RunInfo>& runs = ctx->s_runs;  // (a rerun returns right after its nested call)
-    runs.clear();
-    runs.reserve(job.run_ptr.size());
+    runs.resize(job.run_ptr.size());  // same size as the last call: no fill
     std::vector<uint32_t>& stream_first_run = ctx->s_sfr;
-    stream_first_run.assign(k + 1, 0);
+    stream_first_run.resize(k + 1);
+    auto n_chunks_of = [](uint64_t len) { return len >= 2 ? (uint32_t)((len - 1 + CHUNK - 1) / CHUNK) : 0u; };
     uint64_t n_chunks = 0;
-    for (uint32_t s = 0; s < k; ++s) {
-        stream_first_run[s] = (uint32_t)runs.size();
-        const InStream& S = job.ranked[s];
-        for (uint32_t m = 0; m < S.n_runs; ++m) {
-            RunInfo R;
-            R.ptr = job.run_ptr[S.first + m];
-            R.len = job.run_len[S.first + m];
-            R.chunk_base = n_chunks;
-            R.n_chunks = R.len >= 2 ? (uint32_t)((R.len - 1 + CHUNK - 1) / CHUNK) : 0;
-            R.stream = s;
-            n_chunks += R.n_chunks;
-            runs.push_back(R);
+    {  // blocks of streams (rank order) on host threads: runs and chunks before each block, then fill
+        const unsigned nb = par_nblocks(k);
+        std::vector<uint64_t> rb(nb + 1, 0), cb(nb + 1, 0);
+        par_run(k, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+            uint64_t nr = 0, nc = 0;
+            for (uint64_t s = lo; s < hi; ++s) {
+                const InStream& S = job.ranked[s];
+                nr += S.n_runs;
+                for (uint32_t m = 0; m < S.n_runs; ++m) nc += n_chunks_of(job.run_len[S.first + m]);
+            }
+            rb[b + 1] = nr;
+            cb[b + 1] = nc;
+        });
+        for (unsigned b = 0; b < nb; ++b) {
+            rb[b + 1] += rb[b];
+            cb[b + 1] += cb[b];
         }
+        par_run(k, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+            uint64_t at = rb[b], nc = cb[b];
+            for (uint64_t s = lo; s < hi; ++s) {
+                stream_first_run[s] = (uint32_t)at;
+                const InStream& S = job.ranked[s];
+                for (uint32_t m = 0; m < S.n_runs; ++m, ++at) {
+                    RunInfo& R = runs[at];
+                    R.ptr = job.run_ptr[S.first + m];
+                    R.len = job.run_len[S.first + m];
+                    R.chunk_base = nc;
+                    R.n_chunks = n_chunks_of(R.len);
+                    R.stream = (uint32_t)s;
+                    nc += R.n_chunks;
+                }
+            }
+        });
+        n_chunks = cb[nb];
     }
     stream_first_run[k] = (uint32_t)runs.size();
     const uint32_t n_runs = (uint32_t)runs.size();
@@ -976,13 +1034,13 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     launch_run_header(st, d_runs, n_runs, d_hdr, d_fmt);
 
     std::vector<RunSummary>& sum = ctx->s_sum;
-    sum.assign(n_runs, RunSummary{});
+    sum.resize(n_runs);  // every entry is written by whichever parse runs
     std::vector<uint64_t>& stream_base = ctx->s_sbase;
     std::vector<uint64_t>& stream_valid = ctx->s_svalid;
     std::vector<uint32_t>& stream_err = ctx->s_serr;
-    stream_base.assign(k + 1, 0);
-    stream_valid.assign(k, 0);
-    stream_err.assign(k, 0);
+    stream_base.resize(k + 1);  // written by stream_tables() before any read
+    stream_valid.resize(k);
+    stream_err.resize(k);
     bool any_err = false;
     uint64_t R = 0;
     uint64_t* rec_addr = nullptr;
@@ -996,28 +1054,40 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     uint64_t* d_stream_base = dbuf<uint64_t>(ctx, "stream_base", k + 1);
     unsigned long long* d_first_dec = dbuf<unsigned long long>(ctx, "first_dec", k);
     std::vector<uint64_t>& first_dec = ctx->s_first_dec;
-    first_dec.assign(k, 0);
+    first_dec.resize(k);  // read back, or filled with ~0 on the deferred path
     uint32_t hflags[4];
     // per stream (rank order): base index, valid record count n_s and the first error
-    auto stream_tables = [&]() {
-        uint64_t acc = 0;
-        for (uint32_t s = 0; s < k; ++s) {
-            stream_base[s] = acc;
-            uint64_t valid = 0;
-            bool dead = false;
-            for (uint32_t r = stream_first_run[s]; r < stream_first_run[s + 1]; ++r) {
-                acc += sum[r].records;
-                if (!dead) {
-                    valid += sum[r].records;
-                    if (sum[r].err) {
-                        stream_err[s] = sum[r].err;
-                        dead = true;
-                        any_err = true;
+    auto stream_tables = [&]() {  // blocks of streams on host threads (10^6-stream calls)
+        const unsigned nb = par_nblocks(k);
+        std::vector<uint8_t> blk_err(nb, 0);
+        const uint64_t acc = par_scan(
+            k,
+            [&](uint64_t lo, uint64_t hi) {
+                uint64_t a = 0;
+                for (uint32_t r = stream_first_run[lo]; r < stream_first_run[hi]; ++r) a += sum[r].records;
+                return a;
+            },
+            [&](unsigned b, uint64_t lo, uint64_t hi, uint64_t acc) {
+                for (uint64_t s = lo; s < hi; ++s) {
+                    stream_base[s] = acc;
+                    uint64_t valid = 0;
+                    bool dead = false;
+                    stream_err[s] = 0;
+                    for (uint32_t r = stream_first_run[s]; r < stream_first_run[s + 1]; ++r) {
+                        acc += sum[r].records;
+                        if (!dead) {
+                            valid += sum[r].records;
+                            if (sum[r].err) {
+                                stream_err[s] = sum[r].err;
+                                dead = true;
+                                blk_err[b] = 1;
+                            }
+                        }
                     }
+                    stream_valid[s] = valid;
                 }
-            }
-            stream_valid[s] = valid;
-        }
+            });
+        for (uint8_t e : blk_err) any_err = any_err || e;
         stream_base[k] = acc;
         if (acc != R) throw DevError("internal: record count mismatch");
     };
@@ -1067,21 +1137,44 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         sync(ctx);
         htrace("header synced");
         htrace("run formats read");
-        bool all_fixed = n_runs > 0;
-        for (uint32_t r = 0; r < n_runs && all_fixed; ++r) all_fixed = hf[r].S != 0;
+        // blocks of runs on host threads: every run fixed-stride? one format everywhere?
+        const unsigned nbr = par_nblocks(n_runs);
+        std::vector<uint8_t> blk_fixed(nbr, 1), blk_uni(nbr, 1);
+        par_run(n_runs, nbr, [&](unsigned b, uint64_t lo, uint64_t hi) {
+            bool fx = true, un = true;
+            for (uint64_t r = lo; r < hi; ++r) {
+                fx = fx && hf[r].S != 0;
+                un = un && hf[r].S == hf[0].S && hf[r].K == hf[0].K;
+            }
+            blk_fixed[b] = fx;
+            blk_uni[b] = un;
+        });
+        bool all_fixed = n_runs > 0, uniform = true;
+        for (unsigned b = 0; b < nbr; ++b) {
+            all_fixed = all_fixed && blk_fixed[b];
+            uniform = uniform && blk_uni[b];
+        }
         if (all_fixed) {
             std::vector<uint64_t>& recb = ctx->s_recb;
-            recb.assign(n_runs + 1, 0);
-            for (uint32_t r = 0; r < n_runs; ++r) {
-                sum[r].records = (runs[r].len - 1) / hf[r].S;
-                sum[r].err = 0;
-                sum[r].pad = 0;
-                recb[r + 1] = recb[r] + sum[r].records;
-            }
-            R = recb[n_runs];
+            recb.resize(n_runs + 1);
+            recb[0] = 0;
+            R = par_scan(
+                n_runs,
+                [&](uint64_t lo, uint64_t hi) {
+                    uint64_t a = 0;
+                    for (uint64_t r = lo; r < hi; ++r) a += (runs[r].len - 1) / hf[r].S;
+                    return a;
+                },
+                [&](unsigned, uint64_t lo, uint64_t hi, uint64_t acc) {
+                    for (uint64_t r = lo; r < hi; ++r) {
+                        sum[r].records = (runs[r].len - 1) / hf[r].S;
+                        sum[r].err = 0;
+                        sum[r].pad = 0;
+                        acc += sum[r].records;
+                        recb[r + 1] = acc;
+                    }
+                });
             // one record size and one key length <= 16 everywhere: the fused stride path
-            bool uniform = true;
-            for (uint32_t r = 1; r < n_runs && uniform; ++r) uniform = hf[r].S == hf[0].S && hf[r].K == hf[0].K;
             const RunFmt f0 = hf[0];
             const char* fenv = getenv("SKV_FUSED");
             if (allow_deferred && uniform && !job.batch && !job.search && !(job.flags & SKV_SPLIT_BY_TABLE) &&
@@ -1499,15 +1592,13 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     uint64_t* d_nruns = dbuf<uint64_t>(ctx, "n_runs", 4);  // {runs, K, P[K]} (k_chain)
     DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", R + 1);
     uint64_t* seg_r0 = dbuf<uint64_t>(ctx, "seg_r0", R / GATHER_SEG + 2);
-    uint64_t in_rec_bytes = 0;  // bounds P[K]
-    for (uint64_t l : job.run_len) in_rec_bytes += l;
+    const uint64_t in_rec_bytes = job.in_bytes;  // bounds P[K]
     uint32_t* chain_tbl = dbuf<uint32_t>(ctx, "chain_tbl", chain_table_entries(in_rec_bytes));
     launch_chain(st, d_K, m_P, job.max_run_size, tile_max, T0, run_b, d_nruns, chain_tbl, R, in_rec_bytes);
     launch_run_stats(st, d_nruns, run_b, m_P, m_Dp, m_rec, rec_klen, d_desc, seg_r0, R);
     mark(ctx, PH_CHAIN);
     // ---- gather -----------------------------------------------------------------------------
-    uint64_t total_rec_bytes = 0;
-    for (uint64_t l : job.run_len) total_rec_bytes += l;
+    const uint64_t total_rec_bytes = job.in_bytes;
     uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + R + 16);
 #if SKV_PAGE_GATHER
     {
@@ -1607,43 +1698,80 @@ static int build_job_impl(skv_ctx* ctx, const skv_stream* streams, uint32_t n, u
         return set_err(ctx, SKV_E_INVALID_ARG, "SKV_SPLIT_BY_TABLE and SKV_DROP_TOMBSTONES are exclusive");
     job.max_run_size = max_run_size;
     job.flags = flags;
-    {  // one allocation per table (10^6 WAL runs: no regrowth copies)
-        uint64_t total_runs = 0;
-        for (uint32_t i = 0; i < n; ++i) total_runs += streams[i].n_runs;
-        job.run_ptr.reserve(total_runs);
-        job.run_len.reserve(total_runs);
-        job.ranked.reserve(n);
-    }
-    for (uint32_t i = 0; i < n; ++i) {
-        const skv_stream& s = streams[i];
-        if (s.n_runs && (!s.runs || !s.run_lens))
-            return set_err(ctx, SKV_E_INVALID_ARG, "stream %u: runs/run_lens is NULL", i);
-        InStream S;
-        S.seq = s.seq_no;
-        S.vec_idx = i;
-        S.n_runs = s.n_runs;
-        S.first = job.run_ptr.size();
-        for (uint32_t r = 0; r < s.n_runs; ++r) {
-            if (s.run_lens[r] && !s.runs[r]) return set_err(ctx, SKV_E_INVALID_ARG, "stream %u run %u: NULL data", i, r);
-            job.run_ptr.push_back((uint64_t)(uintptr_t)s.runs[r]);
-            job.run_len.push_back(s.run_lens[r]);
-            job.in_bytes += s.run_lens[r];
+    // pass 1 (blocks of streams on host threads): NULL checks, run counts, input bytes, and
+    // whether the caller's order is strictly ascending / descending by seq_no
+    const unsigned nb = par_nblocks(n);
+    struct Blk {
+        uint64_t runs = 0, bytes = 0, bad = ~0ull;
+        uint32_t bad_run = ~0u;
+        bool asc = true, desc = true;
+    };
+    std::vector<Blk> B(nb);
+    par_run(n, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+        Blk& K = B[b];
+        for (uint64_t i = lo; i < hi; ++i) {
+            const skv_stream& s = streams[i];
+            if (s.n_runs && (!s.runs || !s.run_lens)) {
+                K.bad = i;
+                return;
+            }
+            for (uint32_t r = 0; r < s.n_runs; ++r) {
+                if (s.run_lens[r] && !s.runs[r]) {
+                    K.bad = i;
+                    K.bad_run = r;
+                    return;
+                }
+                K.bytes += s.run_lens[r];
+            }
+            K.runs += s.n_runs;
+            if (i > 0) {
+                K.asc = K.asc && streams[i - 1].seq_no < s.seq_no;
+                K.desc = K.desc && streams[i - 1].seq_no > s.seq_no;
+            }
         }
-        job.ranked.push_back(S);
-    }
-    // rank order = seq_no descending (callers usually hand streams in one of the two orders)
+    });
     bool asc = true, desc = true;
-    for (size_t i = 1; i < job.ranked.size() && (asc || desc); ++i) {
-        asc = asc && job.ranked[i - 1].seq < job.ranked[i].seq;
-        desc = desc && job.ranked[i - 1].seq > job.ranked[i].seq;
+    uint64_t total_runs = 0;
+    for (unsigned b = 0; b < nb; ++b) {  // the first invalid stream in the caller's order
+        if (B[b].bad != ~0ull) {
+            if (B[b].bad_run == ~0u)
+                return set_err(ctx, SKV_E_INVALID_ARG, "stream %u: runs/run_lens is NULL", (uint32_t)B[b].bad);
+            return set_err(ctx, SKV_E_INVALID_ARG, "stream %u run %u: NULL data", (uint32_t)B[b].bad, B[b].bad_run);
+        }
+        const uint64_t r = B[b].runs;
+        B[b].runs = total_runs;  // now the block's first run
+        total_runs += r;
+        job.in_bytes += B[b].bytes;
+        asc = asc && B[b].asc;
+        desc = desc && B[b].desc;
     }
-    if (asc) std::reverse(job.ranked.begin(), job.ranked.end());
-    else if (!desc)
+    // pass 2: the tables, streams already in rank order (seq_no descending) when the caller's
+    // order is either strict one; resize keeps a lent table's entries (no zero fill per call)
+    job.run_ptr.resize(total_runs);
+    job.run_len.resize(total_runs);
+    job.ranked.resize(n);
+    par_run(n, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+        uint64_t at = B[b].runs;
+        for (uint64_t i = lo; i < hi; ++i) {
+            const skv_stream& s = streams[i];
+            InStream& S = job.ranked[asc ? n - 1 - i : i];
+            S.seq = s.seq_no;
+            S.vec_idx = (uint32_t)i;
+            S.n_runs = s.n_runs;
+            S.first = at;
+            for (uint32_t r = 0; r < s.n_runs; ++r, ++at) {
+                job.run_ptr[at] = (uint64_t)(uintptr_t)s.runs[r];
+                job.run_len[at] = s.run_lens[r];
+            }
+        }
+    });
+    if (!asc && !desc) {
         std::stable_sort(job.ranked.begin(), job.ranked.end(),
                          [](const InStream& a, const InStream& b) { return a.seq > b.seq; });
-    for (size_t i = 1; i < job.ranked.size(); ++i)
-        if (job.ranked[i].seq == job.ranked[i - 1].seq)
-            return set_err(ctx, SKV_E_INVALID_ARG, "duplicate seq_no %" PRId64, job.ranked[i].seq);
+        for (size_t i = 1; i < job.ranked.size(); ++i)
+            if (job.ranked[i].seq == job.ranked[i - 1].seq)
+                return set_err(ctx, SKV_E_INVALID_ARG, "duplicate seq_no %" PRId64, job.ranked[i].seq);
+    }
     return SKV_OK;
 }
 
@@ -1756,9 +1884,6 @@ int skv_compact_dev(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams,
     job.ranked.swap(ctx->j_ranked);
     job.run_ptr.swap(ctx->j_ptr);
     job.run_len.swap(ctx->j_len);
-    job.ranked.clear();
-    job.run_ptr.clear();
-    job.run_len.clear();
     int rc = build_job(ctx, streams, n_streams, max_run_size, flags, job);
     htrace("job built");
     if (!rc) rc = run_guarded(ctx, job, out, t_entry);
@@ -1832,10 +1957,16 @@ int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uin
     if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
     *out = nullptr;
     if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
-    Job job;
+    Job job;  // lent ctx tables, as in skv_compact_dev
+    job.ranked.swap(ctx->j_ranked);
+    job.run_ptr.swap(ctx->j_ptr);
+    job.run_len.swap(ctx->j_len);
     int rc = build_job(ctx, streams, n_streams, max_run_size, flags, job);
-    if (rc) return rc;
-    return compact_host_job(ctx, job, out, t_entry);
+    if (!rc) rc = compact_host_job(ctx, job, out, t_entry);
+    job.ranked.swap(ctx->j_ranked);
+    job.run_ptr.swap(ctx->j_ptr);
+    job.run_len.swap(ctx->j_len);
+    return rc;
 }
 
 int skv_encode_batch(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_t max_run_size, skv_result** out) {

@@ -156,7 +156,16 @@ __device__ __forceinline__ void sk_ext(const uint8_t* key, uint32_t klen, uint64
     x1 = ((uint64_t)__builtin_bswap32(v.z & dword_mask(0, m, 2)) << 32) | __builtin_bswap32(v.w & dword_mask(0, m, 3));
 }
 
-__global__ void k_sort_splitters(const SElem* __restrict__ Ss, uint64_t ov, uint64_t nsp, SSplit* sp) {
+// The first 32 key bytes of a splitter (big-endian words, zero past the key's end). Zero-padded
+// windows order as the keys do wherever they differ (a proper prefix pads with zeros, which sort
+// first), so the bucket search compares windows and reads the full SSplit only on a tie. 32 bytes,
+// not 16: WAL keys ("{table}." + a zero-filled decimal, gen.wal_run) share their first 16 bytes
+// within a table.
+struct SWin {
+    uint64_t hi, lo, x0, x1;
+};
+
+__global__ void k_sort_splitters(const SElem* __restrict__ Ss, uint64_t ov, uint64_t nsp, SSplit* sp, SWin* win) {
     const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nsp) return;
     const SElem e = Ss[(b + 1) * ov - 1];
@@ -168,6 +177,7 @@ __global__ void k_sort_splitters(const SElem* __restrict__ Ss, uint64_t ov, uint
     o.klen = e.klen;
     o.pad = 0;
     sp[b] = o;
+    win[b] = SWin{o.hi, o.lo, o.x0, o.x1};
 }
 
 // splitter vs element key order (<0, 0, >0)
@@ -186,39 +196,89 @@ __device__ __forceinline__ int sk_scmp(const SSplit& a, const SElem& b, uint64_t
     return a.klen < b.klen ? -1 : (a.klen > b.klen ? 1 : 0);
 }
 
-// Bucket of each element = the splitters whose key orders strictly before its key; slot by an
-// atomic count (the bucket sort restores a deterministic order). Two-level search: every
-// top-th splitter sits in LDS (one table per workgroup of SB_PER elements per thread), the
-// final <= top splitters are searched in global memory.
-constexpr int SB_THREADS = 256, SB_PER = 16, SB_TOP = 1024;
+// does splitter j (window w) order strictly before x? The full entry only on a window tie.
+__device__ __forceinline__ bool sk_sbefore(const SWin& w, const SSplit* __restrict__ sp, uint64_t j, const SElem& x,
+                                           uint64_t x0, uint64_t x1) {
+    int c = 0;
+    if (w.hi != x.hi) c = w.hi < x.hi ? -1 : 1;
+    else if (w.lo != x.lo) c = w.lo < x.lo ? -1 : 1;
+    else if (w.x0 != x0) c = w.x0 < x0 ? -1 : 1;
+    else if (w.x1 != x1) c = w.x1 < x1 ? -1 : 1;
+    if (c == 0) c = sk_scmp(sp[j], x, x0, x1);
+    return c < 0;
+}
+
+// Bucket of each element = the number of splitters ordered strictly before its key; slot by an
+// atomic count (the bucket sort restores a deterministic order). Two-level search: the windows of
+// every top-th splitter sit in LDS, the final < top splitters are searched in the global window
+// table (32 B per splitter: 3.4 MB at config 5's 10^5 splitters, L2-resident, where the 48-byte
+// SSplit table was not). Both levels are branch-free power-of-two searches with a step count
+// uniform over the wave, run for SB_ILP elements at once so their loads overlap.
+constexpr int SB_THREADS = 256, SB_PER = 16, SB_TOP = 1024, SB_ILP = 4;
 __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restrict__ E, uint64_t n,
-                                                            const SSplit* __restrict__ sp, uint64_t nsp, uint64_t top,
+                                                            const SSplit* __restrict__ sp,
+                                                            const SWin* __restrict__ win, uint64_t nsp, uint64_t top,
                                                             unsigned long long* cnt, uint64_t* bs) {
-    __shared__ SSplit tt[SB_TOP];
-    const uint64_t nt = nsp / top;  // top entry j = splitter (j + 1) * top - 1
-    for (uint64_t j = threadIdx.x; j < nt; j += SB_THREADS) tt[j] = sp[(j + 1) * top - 1];
+    __shared__ SWin tt[SB_TOP];
+    const uint32_t nt = (uint32_t)(nsp / top);  // top entry j = splitter (j + 1) * top - 1
+    for (uint32_t j = threadIdx.x; j < nt; j += SB_THREADS) tt[j] = win[(uint64_t)(j + 1) * top - 1];
     __syncthreads();
+    uint32_t s1 = 0;
+    if (nt) {
+        s1 = 1;
+        while (s1 * 2 <= nt) s1 *= 2;
+    }
     const uint64_t base = (uint64_t)blockIdx.x * SB_THREADS * SB_PER;
-    for (int u = 0; u < SB_PER; ++u) {
-        const uint64_t i = base + (uint64_t)u * SB_THREADS + threadIdx.x;
-        if (i >= n) break;
-        const SElem x = E[i];
-        uint64_t x0, x1;
-        sk_ext(sk_key(x), x.klen, x0, x1);
-        uint64_t a = 0, b = nt;  // top entries ordered strictly before x
-        while (a < b) {
-            const uint64_t mid = (a + b) >> 1;
-            if (sk_scmp(tt[mid], x, x0, x1) < 0) a = mid + 1;
-            else b = mid;
+    for (int u0 = 0; u0 < SB_PER; u0 += SB_ILP) {
+        SElem x[SB_ILP];
+        uint64_t x0[SB_ILP], x1[SB_ILP], g[SB_ILP], len[SB_ILP], c[SB_ILP];
+        uint32_t a[SB_ILP];
+        bool live[SB_ILP];
+#pragma unroll
+        for (int u = 0; u < SB_ILP; ++u) {
+            const uint64_t i = base + (uint64_t)(u0 + u) * SB_THREADS + threadIdx.x;
+            live[u] = i < n;
+            x[u] = E[live[u] ? i : 0];
         }
-        uint64_t lo = a * top, hi = a * top + top - 1 < nsp ? a * top + top - 1 : nsp;
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (sk_scmp(sp[mid], x, x0, x1) < 0) lo = mid + 1;
-            else hi = mid;
+#pragma unroll
+        for (int u = 0; u < SB_ILP; ++u) {
+            sk_ext(sk_key(x[u]), x[u].klen, x0[u], x1[u]);
+            a[u] = 0;
         }
-        const uint64_t slot = atomicAdd(cnt + lo, 1ull);
-        bs[i] = (lo << 32) | slot;
+        for (uint32_t st = s1; st; st >>= 1) {
+#pragma unroll
+            for (int u = 0; u < SB_ILP; ++u) {
+                const uint32_t p = a[u] + st;
+                if (p <= nt) {
+                    const bool before = sk_sbefore(tt[p - 1], sp, (uint64_t)p * top - 1, x[u], x0[u], x1[u]);
+                    if (before) a[u] = p;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < SB_ILP; ++u) {
+            g[u] = (uint64_t)a[u] * top;
+            len[u] = a[u] < nt ? top - 1 : nsp - (uint64_t)nt * top;
+            c[u] = 0;
+        }
+        for (uint64_t st = top >> 1; st; st >>= 1) {
+#pragma unroll
+            for (int u = 0; u < SB_ILP; ++u) {
+                const uint64_t p = c[u] + st;
+                if (p <= len[u]) {
+                    const bool before = sk_sbefore(win[g[u] + p - 1], sp, g[u] + p - 1, x[u], x0[u], x1[u]);
+                    if (before) c[u] = p;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < SB_ILP; ++u) {
+            if (!live[u]) continue;
+            const uint64_t i = base + (uint64_t)(u0 + u) * SB_THREADS + threadIdx.x;
+            const uint64_t b = g[u] + c[u];
+            const uint64_t slot = atomicAdd(cnt + b, 1ull);
+            bs[i] = (b << 32) | slot;
+        }
     }
 }
 
@@ -360,14 +420,15 @@ void launch_sort_prefix(hipStream_t s, const SElem* Ss, uint64_t ov, uint64_t Tb
 void launch_sort_bucket(hipStream_t s, const SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
                         void* split_buf, uint64_t* cnt, uint64_t* bs) {
     SSplit* sp = (SSplit*)split_buf;
-    if (nsp) k_sort_splitters<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, sp);
-    uint64_t top = 1;
+    SWin* win = (SWin*)(sp + nsp + 1);
+    if (nsp) k_sort_splitters<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, sp, win);
+    uint64_t top = 1;  // a power of two: the global search level is a full power-of-two search
     while (nsp / top > (uint64_t)SB_TOP) top <<= 1;
     const uint64_t per_wg = (uint64_t)SB_THREADS * SB_PER;
-    if (n) k_sort_bucket<<<(unsigned)((n + per_wg - 1) / per_wg), SB_THREADS, 0, s>>>(E, n, sp, nsp, top,
+    if (n) k_sort_bucket<<<(unsigned)((n + per_wg - 1) / per_wg), SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top,
                                                                                      (unsigned long long*)cnt, bs);
 }
-size_t sort_split_bytes(uint64_t nsp) { return (size_t)(nsp + 1) * sizeof(SSplit); }
+size_t sort_split_bytes(uint64_t nsp) { return (size_t)(nsp + 1) * (sizeof(SSplit) + sizeof(SWin)); }
 void launch_sort_scatter(hipStream_t s, const SElem* E, uint64_t n, const uint64_t* bs, const uint64_t* start,
                          SElem* out) {
     if (n) k_sort_scatter<<<sk_blocks(n), 256, 0, s>>>(E, n, bs, start, out);
