@@ -318,10 +318,13 @@ def main():
             hb, _ = comp.compact_host_ptrs(hstreams, max_run, flags)
             hts.append(time.perf_counter() - t1)
         ht = min(hts)
+        parts = int(comp.timings()["host_parts"])
         host_path = {"value": round(in_bytes / ht / GiB, 3), "unit": "GiB/s", "ms": round(ht * 1e3, 3),
-                     "h2d_bytes": in_bytes, "d2h_bytes": hb,
+                     "h2d_bytes": in_bytes, "d2h_bytes": hb, "parts": parts,
                      "note": "skv_compact: pinned host inputs -> HBM -> compaction -> pinned host output, "
-                             "best of 2 after 1 warm-up, serial copies (no overlap)"}
+                             "best of 2 after 1 warm-up, " + (
+                                 f"{parts} key-range parts with H2D, kernels and D2H overlapped" if parts
+                                 else "serial copies (no overlap)")}
         # two ctxs (two HIP streams) on the same GPU, each compacting from its own host thread:
         # one job's D2H overlaps the next job's H2D on the separate copy engines (skv.h threading
         # contract: different ctxs run concurrently)
@@ -347,6 +350,33 @@ def main():
             "value": round(2 * n_jobs * in_bytes / tp / GiB, 3), "unit": "GiB/s",
             "note": f"2 ctxs x {n_jobs} skv_compact calls from 2 host threads, same pinned inputs"}
         del host_runs
+        # the ceiling of this figure: the box's PCIe with both directions busy at once (1 GiB H2D on
+        # one stream while 1 GiB D2H runs on another, pinned buffers); a host call moves its input
+        # bytes in and about as many output bytes out, so value <= bidir / 2
+        try:
+            nb = 1 << 30
+            dbuf_a = torch.empty(nb, dtype=torch.uint8, device=device)
+            dbuf_b = torch.empty(nb, dtype=torch.uint8, device=device)
+            h_a = torch.empty(nb, dtype=torch.uint8).pin_memory()
+            h_b = torch.empty(nb, dtype=torch.uint8).pin_memory()
+            s_in, s_out = torch.cuda.Stream(device), torch.cuda.Stream(device)
+            best = None
+            for _ in range(3):
+                torch.cuda.synchronize(device)
+                t1 = time.perf_counter()
+                with torch.cuda.stream(s_in):
+                    dbuf_a.copy_(h_a, non_blocking=True)
+                with torch.cuda.stream(s_out):
+                    h_b.copy_(dbuf_b, non_blocking=True)
+                torch.cuda.synchronize(device)
+                dt = time.perf_counter() - t1
+                best = dt if best is None else min(best, dt)
+            bidir = 2 * nb / best / 1e9
+            host_path["pcie_bidir_GBps"] = round(bidir, 1)
+            host_path["frac_of_pcie"] = round((in_bytes + hb) / ht / 1e9 / bidir, 3)
+            del dbuf_a, dbuf_b, h_a, h_b
+        except Exception as e:  # a figure for the record, never the bench's outcome
+            host_path["pcie_bidir_GBps"] = f"unmeasured: {e}"
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SKV_ABI_VERSION 2  /* 2: skv_timings gained sorted, fp_rerun */
+#define SKV_ABI_VERSION 3  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts */
 
 typedef struct skv_ctx skv_ctx;
 
@@ -133,6 +133,9 @@ typedef struct {
     uint32_t sorted;         /* 1: merge fan-in above 1536 streams took the record sort (one list) */
     uint32_t fp_rerun;       /* 1: the merge's key-fingerprint shortcut misordered a tile and the
                                 call was rerun with exact key compares (a 64-bit collision) */
+    uint32_t host_parts;     /* skv_compact: key-range parts whose H2D, kernels and D2H overlapped
+                                (0: the serial copy -> compact -> copy) */
+    uint32_t reserved;
 } skv_timings;
 
 /* skv_timings.path */

@@ -99,6 +99,11 @@ size_t fx_tile_lds_bytes(uint32_t k);
 hipError_t launch_fx_tile(hipStream_t, const FxArgs& A);
 uint64_t fx_tile_slots(uint32_t k);
 void launch_fx_desc(hipStream_t, const FxArgs& A, DevRunDesc* descs, uint64_t* n_runs_out, uint64_t max_runs);
+// *dst = *src with a system-scope store: dst is host-mapped pinned memory the host polls
+void launch_fx_publish(hipStream_t, const uint64_t* src, uint64_t* dst);
+// n bytes src -> dst by a kernel (src may be host-mapped pinned memory): small table uploads that
+// must not queue behind bulk DMA on a copy engine (pipelined host calls)
+void launch_copy_bytes(hipStream_t, uint8_t* dst, const uint8_t* src, uint64_t n);
 // skv_sort.hip — record sort (fan-in above TILE_TARGET / 2)
 void launch_sort_load(hipStream_t, uint64_t R, const uint64_t* hi, const uint64_t* lo, const uint64_t* addr,
                       const uint32_t* klen, SElem* E, bool last_wins);

@@ -936,7 +936,7 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     const uint32_t cnt = total;
     FXPROF(4);
     if (tid < 64) {
-        const uint64_t g0 = fx_lookback(A.tstate, t, cnt);
+        const uint64_t g0 = fx_lookback(A.tstate, t, cnt) + (A.gbase ? *A.gbase : 0ull);
         if (tid == 0) {
             s_g0 = g0;
             if (t == A.T - 1) *A.Kout = g0 + cnt;
@@ -1137,6 +1137,21 @@ __global__ void k_fx_desc(FxArgs A, DevRunDesc* descs, uint64_t* n_runs_out, uin
     }
 }
 
+// a part's survivor count to host-mapped memory (pipelined host calls): one lane, a vector
+// store with system scope, so the host sees it once the part's completion event has fired
+__global__ void k_fx_publish(const uint64_t* __restrict__ src, uint64_t* dst) {
+    if (threadIdx.x == 0) __hip_atomic_store(dst, *src, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void k_copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t n) {
+    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+    if (i + 16 <= n && !(((uintptr_t)dst | (uintptr_t)src) & 15)) {
+        *(uint4*)(dst + i) = *(const uint4*)(src + i);
+    } else {
+        for (uint64_t b = i; b < i + 16 && b < n; ++b) dst[b] = src[b];
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 static inline unsigned fx_blocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
@@ -1181,6 +1196,10 @@ uint64_t fx_tile_slots(uint32_t k) {  // fused tiles resident at once on the cur
     cached_k[dev & 63] = k;
     return cached[dev & 63] = (uint64_t)(cus > 0 ? cus : 256) * (uint64_t)(per > 0 ? per : 1);
 }
+void launch_copy_bytes(hipStream_t s, uint8_t* dst, const uint8_t* src, uint64_t n) {
+    if (n) k_copy_bytes<<<fx_blocks((n + 15) / 16, 256), 256, 0, s>>>(dst, src, n);
+}
+void launch_fx_publish(hipStream_t s, const uint64_t* src, uint64_t* dst) { k_fx_publish<<<1, 64, 0, s>>>(src, dst); }
 void launch_fx_desc(hipStream_t s, const FxArgs& A, DevRunDesc* descs, uint64_t* n_runs_out, uint64_t max_runs) {
     unsigned blocks = fx_blocks(max_runs ? max_runs : 1, 256);
     if (blocks > 4096) blocks = 4096;

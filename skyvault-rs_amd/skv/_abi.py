@@ -111,6 +111,8 @@ class SkvTimings(C.Structure):
         ("hot_write_bytes", C.c_uint64),
         ("sorted", C.c_uint32),
         ("fp_rerun", C.c_uint32),
+        ("host_parts", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 
