@@ -16,7 +16,10 @@
 
 namespace skv {
 
-constexpr uint64_t CHUNK = 4096;          // bytes of run body per speculative walk lane
+#ifndef SKV_CHUNK
+#define SKV_CHUNK 4096
+#endif
+constexpr uint64_t CHUNK = SKV_CHUNK;     // bytes of run body per speculative walk lane
 #ifndef SKV_TILE_CAP
 #define SKV_TILE_CAP 4096
 #define SKV_TILE_TARGET 3072
@@ -324,6 +327,12 @@ __device__ __forceinline__ uint4 gblk(uintptr_t a) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Block loader of the record parsers below (a template parameter, so a parser can be pointed at
+// another copy of the bytes)
+struct GLoad {
+    __device__ __forceinline__ uint4 operator()(uintptr_t a) const { return gblk(a); }
+};
+
 // 16 bytes from an arbitrary (unaligned) address using two aligned 16-byte loads. The second
 // aligned block contains p+15, so it holds at least one byte the caller owns and never crosses
 // into an unmapped page.
@@ -371,13 +380,14 @@ __device__ __forceinline__ uint4 funnel16(uint4 x, uint4 y, uint32_t sh) {
 
 // bytes [p, p+n) (1 <= n <= 16) at bytes 0..n-1 of the result (the rest unspecified). Only the
 // aligned 16-byte blocks holding a requested byte are read, so no page beyond them is touched.
-__device__ __forceinline__ uint4 load_window16(const uint8_t* p, uint32_t n) {
+template <class L = GLoad>
+__device__ __forceinline__ uint4 load_window16(const uint8_t* p, uint32_t n, L ld = L()) {
     uintptr_t a = (uintptr_t)p;
     const uintptr_t b0 = a & ~(uintptr_t)15;
     uint32_t sh = (uint32_t)(a & 15);
-    uint4 x = gblk(b0);
+    uint4 x = ld(b0);
     uint4 y = make_uint4(0, 0, 0, 0);
-    if (sh + n > 16) y = gblk(b0 + 16);
+    if (sh + n > 16) y = ld(b0 + 16);
     return funnel16(x, y, sh);
 }
 
@@ -428,15 +438,17 @@ __device__ inline int key_cmp(uint64_t ahi, uint64_t alo, uint32_t alen, const u
 
 // 32 bytes at run+p into w[0..7] (bytes at or past run+len read as zero). Only aligned 16-byte
 // blocks holding a byte below run+len are loaded.
-__device__ __forceinline__ void window32(const uint8_t* run, uint64_t len, uint64_t p, uint32_t w[8]) {
+template <class L = GLoad>
+__device__ __forceinline__ void window32(const uint8_t* run, uint64_t len, uint64_t p, uint32_t w[8],
+                                         L ld = L()) {
     uintptr_t a = (uintptr_t)(run + p);
     uintptr_t end = (uintptr_t)(run + len);
     uintptr_t base = a & ~(uintptr_t)15;
     uint32_t sh = (uint32_t)(a & 15);
     uint4 z = make_uint4(0, 0, 0, 0);
-    uint4 b0 = gblk(base);
-    uint4 b1 = base + 16 < end ? gblk(base + 16) : z;
-    uint4 b2 = (sh && base + 32 < end) ? gblk(base + 32) : z;
+    uint4 b0 = ld(base);
+    uint4 b1 = base + 16 < end ? ld(base + 16) : z;
+    uint4 b2 = (sh && base + 32 < end) ? ld(base + 32) : z;
     uint4 lo = funnel16(b0, b1, sh), hi = funnel16(b1, b2, sh);
     w[0] = lo.x; w[1] = lo.y; w[2] = lo.z; w[3] = lo.w;
     w[4] = hi.x; w[5] = hi.y; w[6] = hi.z; w[7] = hi.w;
@@ -477,14 +489,15 @@ __device__ __forceinline__ bool ascii_prefix(const uint32_t kd[7], uint32_t n /*
 // UTF-8 validity with an all-ASCII vector fast path: the aligned 16-byte blocks of the key are
 // loaded 4 at a time with no dependence between them (one memory round trip per 64 bytes), their
 // bytes past the key masked off; any high bit falls back to the exact scalar check.
-__device__ inline bool utf8_valid_fast(const uint8_t* s, uint64_t n) {
+template <class L = GLoad>
+__device__ inline bool utf8_valid_fast(const uint8_t* s, uint64_t n, L ld = L()) {
     if (n == 0) return true;
     const uintptr_t a0 = (uintptr_t)s, a1 = a0 + n;  // bytes [a0, a1)
     const uintptr_t b0 = a0 & ~(uintptr_t)15, b1 = (a1 + 15) & ~(uintptr_t)15;
     for (uintptr_t b = b0; b < b1; b += 64) {
         uint4 v[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = b + 16 * q < b1 ? gblk(b + 16 * q) : make_uint4(0, 0, 0, 0);
+        for (int q = 0; q < 4; ++q) v[q] = b + 16 * q < b1 ? ld(b + 16 * q) : make_uint4(0, 0, 0, 0);
         uint32_t acc = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -524,13 +537,13 @@ struct RecHdr {
 // UTF8: 0 no key check (structure only), 1 the exact check, 2 a heuristic for speculative chunk
 // starts (a key whose in-window bytes are ASCII passes unchecked; any other key gets the exact
 // check): random bytes taken for a record fail it, real keys cost no extra loads
-template <bool PREFIX, int UTF8 = 1>
-__device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, uint64_t p) {
+template <bool PREFIX, int UTF8 = 1, class L = GLoad>
+__device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, uint64_t p, L ld = L()) {
     RecHdr h;
     h.size = 0;
     h.hi = h.lo = 0;
     uint32_t w[8];
-    window32(run, len, p, w);
+    window32(run, len, p, w, ld);
     h.marker = w[0] & 0xFFu;
     if (p + 5 > len) { h.err = DERR_IO; h.klen = 0; return h; }
     h.klen = __builtin_bswap32(__builtin_amdgcn_alignbyte(w[1], w[0], 1));
@@ -540,7 +553,7 @@ __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, ui
     win_key(w, kd);
     bool ok = UTF8 == 0 || (UTF8 == 2 ? ascii_prefix(kd, h.klen < 27 ? (uint32_t)h.klen : 27u)
                                       : (h.klen <= 27 && ascii_prefix(kd, (uint32_t)h.klen)));
-    if (!ok) ok = utf8_valid_fast(run + kp, h.klen);
+    if (!ok) ok = utf8_valid_fast(run + kp, h.klen, ld);
     if (!ok) { h.err = DERR_UTF8; return h; }
     if (PREFIX) win_prefix(kd, h.klen, h.hi, h.lo);
     if (h.marker == 1) {
@@ -549,7 +562,7 @@ __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, ui
         uint64_t vlen;
         if (vo + 4 <= 32) vlen = win_be32(w, (uint32_t)vo);
         else {
-            uint4 v = load_window16(run + p + vo, 4);
+            uint4 v = load_window16(run + p + vo, 4, ld);
             vlen = __builtin_bswap32(v.x);
         }
         if (kp + h.klen + 4 + vlen > len) { h.err = DERR_VAL; return h; }
@@ -566,12 +579,15 @@ __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, ui
 
 // walk_checked with vectorized headers: one dependent round trip per record. UTF8 = false: the
 // structure only (k_spec's fast mode; k_emit checks the keys and flags a bad one for an exact rerun)
-template <int UTF8 = 1>
-__device__ inline WalkRes walk_fast(const uint8_t* run, uint64_t len, uint64_t p, uint64_t stop, uint32_t max_recs) {
+// slot (cap > 0): the first cap record starts, as offsets from cs (k_emit reads them back)
+template <int UTF8 = 1, class L = GLoad>
+__device__ inline WalkRes walk_fast(const uint8_t* run, uint64_t len, uint64_t p, uint64_t stop, uint32_t max_recs,
+                                   L ld = L(), uint16_t* slot = nullptr, uint32_t cap = 0, uint64_t cs = 0) {
     uint32_t cnt = 0;
     while (p < stop && cnt < max_recs) {
-        RecHdr h = parse_rec<false, UTF8>(run, len, p);
+        RecHdr h = parse_rec<false, UTF8>(run, len, p, ld);
         if (h.err) return {p, cnt, h.err};
+        if (cnt < cap) slot[cnt] = (uint16_t)(p - cs);
         ++cnt;
         p += h.size;
     }
@@ -589,7 +605,8 @@ __device__ __forceinline__ uint64_t fp_mix(uint64_t x) {
     x ^= x >> 33;
     return x;
 }
-__device__ inline uint64_t key_tail_fp(const uint8_t* key, uint32_t klen, bool& ascii) {
+template <class L = GLoad>
+__device__ inline uint64_t key_tail_fp(const uint8_t* key, uint32_t klen, bool& ascii, L ld = L()) {
     ascii = true;
     if (klen <= 16) return 0;
     const uint8_t* k = key + 16;
@@ -606,7 +623,7 @@ __device__ inline uint64_t key_tail_fp(const uint8_t* key, uint32_t klen, bool& 
         const uint32_t q0 = o >> 4;
         uint4 B[5];
 #pragma unroll
-        for (int i = 0; i < 5; ++i) B[i] = q0 + i < nblk ? gblk(base + 16ull * (q0 + i)) : make_uint4(0, 0, 0, 0);
+        for (int i = 0; i < 5; ++i) B[i] = q0 + i < nblk ? ld(base + 16ull * (q0 + i)) : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
             if (o + 16 * w < n) {

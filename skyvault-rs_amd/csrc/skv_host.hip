@@ -1021,7 +1021,14 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     runs.resize(job.run_ptr.size());  // same size as the last call: no fill
     std::vector<uint32_t>& stream_first_run = ctx->s_sfr;
     stream_first_run.resize(k + 1);
-    auto n_chunks_of = [](uint64_t len) { return len >= 2 ? (uint32_t)((len - 1 + CHUNK - 1) / CHUNK) : 0u; };
+    // speculative walk length: CHUNK, doubled up to 4x while a call still has >= 2^20 walks (a big
+    // call spends fewer re-synchronising starts per record; 4 KiB walks of 64 GB: 56 ms, 16 KiB: 44)
+    uint64_t chunk = CHUNK;
+    if (const char* ce = getenv("SKV_CHUNK_BYTES"))  // slot offsets are 16-bit: at most 64 KiB
+        chunk = std::min<uint64_t>(65536, std::max<uint64_t>(CHUNK, strtoull(ce, nullptr, 10)));
+    else
+        while (chunk < 4 * CHUNK && job.in_bytes / (2 * chunk) >= (1ull << 20)) chunk *= 2;
+    auto n_chunks_of = [chunk](uint64_t len) { return len >= 2 ? (uint32_t)((len - 1 + chunk - 1) / chunk) : 0u; };
     uint64_t n_chunks = 0;
     {  // blocks of streams (rank order) on host threads: runs and chunks before each block, then fill
         const unsigned nb = par_nblocks(k);
@@ -1261,14 +1268,18 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     }
     // ---- general path: speculative chunk walks ----------------------------------------------
     if (!parsed) {
+        // record starts of each chunk as the walks find them (16-bit offsets), chunk / 64 per chunk:
+        // k_emit parses the records of a chunk in parallel instead of walking its chain again
+        const uint32_t slot_cap = (uint32_t)(chunk / 64);
+        uint16_t* ch_slots = dbuf<uint16_t>(ctx, "ch_slots", n_chunks * slot_cap);
         HIPCHK(hipMemsetAsync(bad_bits, 0, (n_chunks / 64 + 1) * 8, st));
         HIPCHK(hipMemsetAsync(first_bad, 0xFF, n_runs * 4, st));
         HIPCHK(hipMemsetAsync(err_chunk, 0xFF, n_runs * 4, st));
         launch_spec(st, d_runs, n_runs, n_chunks, d_hdr, d_fmt, d_broken, ch_start, ch_end, ch_cnt, ch_err,
-                    ctx->exact_utf8);
+                    ctx->exact_utf8, chunk, ch_slots, slot_cap);
         launch_validate(st, d_runs, n_runs, n_chunks, d_hdr, ch_start, ch_end, ch_err, bad_bits, first_bad);
         launch_fixup(st, d_runs, n_runs, d_hdr, first_bad, bad_bits, ch_start, ch_end, ch_cnt, ch_err,
-                     ctx->exact_utf8);
+                     ctx->exact_utf8, chunk, ch_slots, slot_cap);
         launch_err_chunk(st, d_runs, n_runs, n_chunks, d_hdr, ch_err, err_chunk);
         launch_mask(st, d_runs, n_runs, n_chunks, d_hdr, err_chunk, ch_cnt, cnt64);
         launch_scan(st, cnt64, n_chunks, ch_rec_base, scan_tmp);
@@ -1285,7 +1296,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         stream_tables();
         alloc_records();
         launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, R, rec_addr, rec_hi,
-                    rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad);
+                    rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad, ch_slots, slot_cap, chunk);
         mark(ctx, PH_PARSE);
         check_and_read(false);
         if (utf8_flag && !ctx->exact_utf8) {  // a key the chunk walks did not check: exact walks

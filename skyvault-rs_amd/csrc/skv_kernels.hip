@@ -113,11 +113,11 @@ __global__ void k_run_header(const RunInfo* runs, uint32_t n_runs, uint32_t* hdr
 // Speculative start of chunk `local` (> 0): a record start must lie in [cs, ce). Scan for the
 // first position whose next three records decode cleanly. Wrong guesses are caught by
 // k_validate and repaired by k_fixup.
-template <int UTF8>
-__device__ uint64_t spec_start(const uint8_t* run, uint64_t len, uint64_t cs, uint64_t ce) {
+template <int UTF8, class L = GLoad>
+__device__ uint64_t spec_start(const uint8_t* run, uint64_t len, uint64_t cs, uint64_t ce, L ld = L()) {
     for (uint64_t p0 = cs; p0 < ce; p0 += 16) {  // 16 bytes per load; marker candidates as a mask
         const uint32_t m = (uint32_t)(ce - p0 < 16 ? ce - p0 : 16);
-        const uint4 v = load_window16(run + p0, m);
+        const uint4 v = load_window16(run + p0, m, ld);
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
         uint32_t cand = 0;
 #pragma unroll
@@ -130,42 +130,45 @@ __device__ uint64_t spec_start(const uint8_t* run, uint64_t len, uint64_t cs, ui
             cand &= cand - 1;
             // candidates are checked with the keys (the heuristic form in the structure-only mode),
             // which rejects random bytes taken for a record far more often than structure alone
-            const WalkRes r = walk_fast<UTF8 ? 1 : 2>(run, len, p0 + i, len, 3);
+            const WalkRes r = walk_fast<UTF8 ? 1 : 2>(run, len, p0 + i, len, 3, ld);
             if (r.err == DERR_NONE) return p0 + i;
         }
     }
     return NO_POS;
 }
 
-__device__ __forceinline__ bool fixed_rec_ok(const uint8_t* run, uint64_t len, uint64_t q, const RunFmt& f) {
+template <class L = GLoad>
+__device__ __forceinline__ bool fixed_rec_ok(const uint8_t* run, uint64_t len, uint64_t q, const RunFmt& f,
+                                             L ld = L()) {
     uint32_t w[8];
-    window32(run, len, q, w);
+    window32(run, len, q, w, ld);
     if ((w[0] & 0xFFu) != 1u) return false;
     uint32_t klen = __builtin_bswap32(__builtin_amdgcn_alignbyte(w[1], w[0], 1));
     if (klen != f.K) return false;
     uint32_t kd[7];
     win_key(w, kd);
     bool ok = f.K <= 27 ? ascii_prefix(kd, f.K) : false;
-    if (!ok && !utf8_valid_fast(run + q + 5, f.K)) return false;
+    if (!ok && !utf8_valid_fast(run + q + 5, f.K, ld)) return false;
     uint32_t vo = 5 + f.K;
     uint32_t vlen;
     if (vo + 4 <= 32) vlen = win_be32(w, vo);
-    else vlen = __builtin_bswap32(load_window16(run + q + vo, 4).x);
+    else vlen = __builtin_bswap32(load_window16(run + q + vo, 4, ld).x);
     return vlen == f.V;
 }
 
 template <int UTF8>
 __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
                        const uint32_t* __restrict__ hdr_err, const RunFmt* __restrict__ fmt, uint32_t* run_broken,
-                       uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err) {
+                       uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, uint64_t chunk,
+                       uint16_t* slots, uint32_t cap) {
     uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
     uint32_t r = find_run(runs, n_runs, c);
     RunInfo R = runs[r];
     uint64_t local = c - R.chunk_base;
     const uint8_t* run = (const uint8_t*)R.ptr;
-    uint64_t cs = 1 + local * CHUNK;
-    uint64_t ce = cs + CHUNK < R.len ? cs + CHUNK : R.len;
+    uint64_t cs = 1 + local * chunk;
+    uint64_t ce = cs + chunk < R.len ? cs + chunk : R.len;
     if (hdr_err[r]) {
         ch_start[c] = cs;
         ch_end[c] = cs;
@@ -201,6 +204,9 @@ __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
             ch_end[c] = p0 + n * S;
             ch_cnt[c] = (uint32_t)n;
             ch_err[c] = 0;
+            // k_emit reads these when another chunk breaks the run's hypothesis
+            uint16_t* sl = slots + c * cap;
+            for (uint64_t i = 0; i < n && i < cap; ++i) sl[i] = (uint16_t)(p0 + i * S - cs);
             return;
         }
         atomicOr(&run_broken[r], 1u);  // hypothesis broken: this run takes the general path
@@ -215,7 +221,7 @@ __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         ch_err[c] = 0;
         return;
     }
-    const WalkRes w = walk_fast<UTF8>(run, R.len, start, ce, 0xFFFFFFFFu);
+    const WalkRes w = walk_fast<UTF8>(run, R.len, start, ce, 0xFFFFFFFFu, GLoad(), slots + c * cap, cap, cs);
     ch_start[c] = start;
     ch_end[c] = w.end;
     ch_cnt[c] = w.cnt;
@@ -256,7 +262,8 @@ __device__ uint64_t next_bad(const unsigned long long* bits, uint64_t from, uint
 // Sequential repair of each run's bad chunks from the true chain (exact; rare on real data).
 __global__ void k_fixup(const RunInfo* __restrict__ runs, uint32_t n_runs, const uint32_t* __restrict__ hdr_err,
                         const uint32_t* __restrict__ run_first_bad, const unsigned long long* __restrict__ bad_bits,
-                        uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, bool utf8) {
+                        uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, bool utf8,
+                        uint64_t chunk, uint16_t* slots, uint32_t cap) {
     uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_runs) return;
     uint32_t fb = run_first_bad[r];
@@ -269,12 +276,14 @@ __global__ void k_fixup(const RunInfo* __restrict__ runs, uint32_t n_runs, const
         uint64_t g = base + c;
         if (ch_err[g - 1]) break;  // a real error in a valid chunk ends the run
         uint64_t E = ch_end[g - 1];
-        uint64_t cs = 1 + c * CHUNK;
-        uint64_t ce = cs + CHUNK < R.len ? cs + CHUNK : R.len;
+        uint64_t cs = 1 + c * chunk;
+        uint64_t ce = cs + chunk < R.len ? cs + chunk : R.len;
         uint64_t end = E;
         uint32_t cnt = 0, err = 0;
         if (E < ce) {
-            WalkRes w = utf8 ? walk_fast<1>(run, R.len, E, ce, 0xFFFFFFFFu) : walk_fast<0>(run, R.len, E, ce, 0xFFFFFFFFu);
+            uint16_t* sl = slots + g * cap;
+            WalkRes w = utf8 ? walk_fast<1>(run, R.len, E, ce, 0xFFFFFFFFu, GLoad(), sl, cap, cs)
+                             : walk_fast<0>(run, R.len, E, ce, 0xFFFFFFFFu, GLoad(), sl, cap, cs);
             end = w.end;
             cnt = w.cnt;
             err = w.err;
@@ -341,14 +350,21 @@ __device__ __forceinline__ void put_rec(uint64_t o, const uint8_t* rp, const Rec
 }
 
 // Emit the record arrays (address, 16 B key prefix, key length, meta) of every validated chunk of
-// the runs that are not fixed-stride: walk from the chunk's validated start.
+// the runs that are not fixed-stride. The chunk walks (k_spec / k_fixup) left each chunk's record
+// starts in its slot row, so EM_G lanes per chunk parse one record each with independent loads and
+// store consecutive records side by side; a chunk with more records than slots is walked by one
+// lane from its validated start.
+constexpr uint32_t EM_G = 16;  // lanes per chunk
 __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
                        const RunFmt* __restrict__ fmt, const uint32_t* __restrict__ run_broken,
                        const uint64_t* __restrict__ ch_start, const uint64_t* __restrict__ ch_rec_base,
                        uint64_t* __restrict__ rec_addr, uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
                        uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags,
-                       uint64_t* __restrict__ rec_fp, uint32_t* utf8_bad) {
-    uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                       uint64_t* __restrict__ rec_fp, uint32_t* utf8_bad, const uint16_t* __restrict__ slots,
+                       uint32_t cap, uint64_t chunk) {
+    const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t c = gi / EM_G;
+    const uint32_t j0 = (uint32_t)(gi % EM_G);
     if (c >= n_chunks) return;
     uint64_t b0 = ch_rec_base[c], cnt = ch_rec_base[c + 1] - b0;
     if (!cnt) return;
@@ -356,17 +372,31 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
     if (fmt[r].S && !run_broken[r]) return;  // k_emit_fixed
     const uint8_t* run = (const uint8_t*)runs[r].ptr;
     const uint64_t len = runs[r].len;
-    uint64_t p = ch_start[c];
-    for (uint64_t i = 0; i < cnt; ++i) {
-        // structure validated by k_spec / k_fixup's walk; the key's UTF-8 is checked here with the
-        // same loads that fingerprint it (a bad key flags the call for an exact rerun)
-        RecHdr h = parse_rec<true, false>(run, len, p);
+    // structure validated by k_spec / k_fixup's walk; the key's UTF-8 is checked here with the
+    // same loads that fingerprint it (a bad key flags the call for an exact rerun)
+    auto emit = [&](uint64_t i, uint64_t p, const RecHdr& h) {
         bool ascii;
         const uint64_t fpv = key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii);
         if (!(ascii && ((h.hi | h.lo) & 0x8080808080808080ull) == 0) && !utf8_valid(run + p + 5, h.klen))
             atomicOr(utf8_bad, 1u);
         put_rec(b0 + i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp, fpv);
-        p += h.size;
+    };
+    if (cnt > cap) {
+        if (j0) return;
+        uint64_t p = ch_start[c];
+        for (uint64_t i = 0; i < cnt; ++i) {
+            const RecHdr h = parse_rec<true, false>(run, len, p);
+            emit(i, p, h);
+            p += h.size;
+        }
+        return;
+    }
+    const uint64_t cs = 1 + (c - runs[r].chunk_base) * chunk;
+    const uint16_t* sl = slots + c * cap;
+    for (uint64_t i = j0; i < cnt; i += EM_G) {
+        const uint64_t p = cs + sl[i];
+        if (p >= len) continue;  // never: every counted record's start is in its slot
+        emit(i, p, parse_rec<true, false>(run, len, p));
     }
 }
 
@@ -1900,14 +1930,14 @@ void launch_run_header(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint
 }
 void launch_spec(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                  const RunFmt* fmt, uint32_t* run_broken, uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt,
-                 uint32_t* ch_err, bool utf8) {
+                 uint32_t* ch_err, bool utf8, uint64_t chunk, uint16_t* slots, uint32_t cap) {
     if (!n_chunks) return;
     if (utf8)
         k_spec<1><<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, fmt, run_broken, ch_start,
-                                                            ch_end, ch_cnt, ch_err);
+                                                            ch_end, ch_cnt, ch_err, chunk, slots, cap);
     else
         k_spec<0><<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, fmt, run_broken, ch_start,
-                                                            ch_end, ch_cnt, ch_err);
+                                                            ch_end, ch_cnt, ch_err, chunk, slots, cap);
 }
 void launch_validate(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                      const uint64_t* ch_start, const uint64_t* ch_end, const uint32_t* ch_err,
@@ -1918,10 +1948,11 @@ void launch_validate(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64
 }
 void launch_fixup(hipStream_t s, const RunInfo* runs, uint32_t n_runs, const uint32_t* hdr_err,
                   const uint32_t* run_first_bad, const unsigned long long* bad_bits, uint64_t* ch_start,
-                  uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, bool utf8) {
+                  uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, bool utf8, uint64_t chunk, uint16_t* slots,
+                  uint32_t cap) {
     if (n_runs)
         k_fixup<<<blocks_for(n_runs, 64), 64, 0, s>>>(runs, n_runs, hdr_err, run_first_bad, bad_bits, ch_start, ch_end,
-                                                       ch_cnt, ch_err, utf8);
+                                                       ch_cnt, ch_err, utf8, chunk, slots, cap);
 }
 void launch_err_chunk(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                       const uint32_t* ch_err, uint32_t* run_err_chunk) {
@@ -1941,11 +1972,12 @@ void launch_run_summary(hipStream_t s, const RunInfo* runs, uint32_t n_runs, con
 void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const RunFmt* fmt,
                  const uint32_t* run_broken, const uint64_t* ch_start, const uint64_t* ch_rec_base,
                  const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
-                 uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, uint64_t* rec_fp, uint32_t* utf8_bad) {
+                 uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, uint64_t* rec_fp, uint32_t* utf8_bad,
+                 const uint16_t* slots, uint32_t cap, uint64_t chunk) {
     if (n_chunks)
-        k_emit<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, fmt, run_broken, ch_start, ch_rec_base,
-                                                         rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp,
-                                                         utf8_bad);
+        k_emit<<<blocks_for(n_chunks * EM_G, 256), 256, 0, s>>>(runs, n_runs, n_chunks, fmt, run_broken, ch_start,
+                                                                ch_rec_base, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
+                                                                flags, rec_fp, utf8_bad, slots, cap, chunk);
     if (R)
         k_emit_fixed<false><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, R, fmt, (uint32_t*)run_broken, run_recb,
                                                                rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags,

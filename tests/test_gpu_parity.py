@@ -315,6 +315,24 @@ def test_corruption_at_every_position_class(dev):
     assert not bad, bad[:5]
 
 
+@pytest.mark.parametrize("chunk", [8192, 12288, 16384])
+def test_longer_speculative_walks(dev, chunk):
+    """Big calls walk 8-16 KiB per speculative chunk (skv_host.hip picks the length from the call
+    size); SKV_CHUNK_BYTES forces a length on small inputs: fake records in values, records
+    spanning chunks, and corruption everywhere must still give the reference's outcome."""
+    old = os.environ.get("SKV_CHUNK_BYTES")
+    os.environ["SKV_CHUNK_BYTES"] = str(chunk)
+    try:
+        test_values_with_fake_records(dev)
+        test_records_spanning_many_chunks(dev)
+        test_corruption_at_every_position_class(dev)
+    finally:
+        if old is None:
+            os.environ.pop("SKV_CHUNK_BYTES", None)
+        else:
+            os.environ["SKV_CHUNK_BYTES"] = old
+
+
 def test_device_resident_entry_point(dev):
     """skv_compact_dev over HBM-resident inputs returns the same bytes as the host entry point."""
     torch = pytest.importorskip("torch")
