@@ -1189,6 +1189,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
 
     // ---- fast path: every run fixed-stride (one record size per run) -> one verifying pass ------
     bool parsed = false, deferred = false;
+    bool any_fixed = false;  // some run is fixed-stride: the general parse also runs k_emit_fixed
     {
         RunFmt* hf = (RunFmt*)pinned(ctx, (size_t)n_runs * sizeof(RunFmt) + 16);
         d2h(ctx, hf, d_fmt, (size_t)n_runs * sizeof(RunFmt));
@@ -1198,20 +1199,23 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         htrace("run formats read");
         // blocks of runs on host threads: every run fixed-stride? one format everywhere?
         const unsigned nbr = par_nblocks(n_runs);
-        std::vector<uint8_t> blk_fixed(nbr, 1), blk_uni(nbr, 1);
+        std::vector<uint8_t> blk_fixed(nbr, 1), blk_uni(nbr, 1), blk_any(nbr, 0);
         par_run(n_runs, nbr, [&](unsigned b, uint64_t lo, uint64_t hi) {
-            bool fx = true, un = true;
+            bool fx = true, un = true, an = false;
             for (uint64_t r = lo; r < hi; ++r) {
                 fx = fx && hf[r].S != 0;
+                an = an || hf[r].S != 0;
                 un = un && hf[r].S == hf[0].S && hf[r].K == hf[0].K;
             }
             blk_fixed[b] = fx;
             blk_uni[b] = un;
+            blk_any[b] = an;
         });
         bool all_fixed = n_runs > 0, uniform = true;
         for (unsigned b = 0; b < nbr; ++b) {
             all_fixed = all_fixed && blk_fixed[b];
             uniform = uniform && blk_uni[b];
+            any_fixed = any_fixed || blk_any[b];
         }
         if (all_fixed) {
             std::vector<uint64_t>& recb = ctx->s_recb;
@@ -1295,8 +1299,8 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         }
         stream_tables();
         alloc_records();
-        launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, R, rec_addr, rec_hi,
-                    rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad, ch_slots, slot_cap, chunk);
+        launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, any_fixed ? R : 0,
+                    rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad, ch_slots, slot_cap, chunk);
         mark(ctx, PH_PARSE);
         check_and_read(false);
         if (utf8_flag && !ctx->exact_utf8) {  // a key the chunk walks did not check: exact walks

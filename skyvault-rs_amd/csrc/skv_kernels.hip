@@ -1168,8 +1168,18 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     return v;
 }
 
-// largest e in [lo, hi] with P[e] <= v, given P[lo] <= v (64-ary search, exact)
-__device__ uint64_t chain_search(const uint64_t* P, uint64_t lo, uint64_t hi, uint64_t v, int lane) {
+// largest e in [lo, hi] with P[e] <= v, given P[lo] <= v (64-ary search, exact). Not inlined: k_chain
+// unrolls its resolve step CH_D times, and 32 inlined copies of this rare fallback made the kernel
+// ~50 KB of straight-line code, streamed through the instruction cache on every round.
+#ifndef SKV_CH_INLINE
+#define SKV_CH_INLINE 0
+#endif
+#if SKV_CH_INLINE
+#define SKV_CH_SEARCH_ATTR
+#else
+#define SKV_CH_SEARCH_ATTR __noinline__
+#endif
+__device__ SKV_CH_SEARCH_ATTR uint64_t chain_search(const uint64_t* P, uint64_t lo, uint64_t hi, uint64_t v, int lane) {
     while (lo < hi) {
         uint64_t span = hi - lo;
         uint64_t step = (span + 63) / 64;
