@@ -113,10 +113,13 @@ struct TileOut {
     uint64_t T;           // level-0 tile count
     uint64_t* prof;       // SKV_TILE_PROF builds: per-phase time of level-0 tiles (8 counters)
     // level 0: fingerprints of the key bytes past 16 (k_key_fp); equal prefix, length and
-    // fingerprint count as equal inside the merge rounds, every adjacent pair of the result is then
-    // compared exactly and a misorder sets *fp_bad (the host reruns with exact compares)
+    // fingerprint count as equal in the merge rounds and in first-per-key. Each adjacent pair taken
+    // as equal that way goes to vpairs (record positions a << 32 | b); k_fp_verify compares their
+    // bytes, and a pair that differs sets *fp_bad (the host reruns with exact compares)
     const uint64_t* key_fp;
     uint32_t* fp_bad;
+    uint64_t* vpairs;
+    unsigned long long* vcount;
     // global scratch for tiles larger than TILE_CAP
     uint64_t* xhi;
     uint64_t* xlo;

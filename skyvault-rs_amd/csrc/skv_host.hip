@@ -1578,6 +1578,11 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             tile_max = O.tile_mm = dbuf<uint32_t>(ctx, "tile_mm", 2 * T);  // (min, max) record size per tile
             O.key_fp = key_fp;
             O.fp_bad = fp_bad;
+            if (key_fp) {  // pairs taken as equal by fingerprint, verified after the tiles
+                O.vpairs = dbuf<uint64_t>(ctx, "fp_vpairs", R);
+                O.vcount = dbuf<unsigned long long>(ctx, "fp_vcount", 1);
+                HIPCHK(hipMemsetAsync(O.vcount, 0, 8, st));
+            }
             O.tstate = dbuf<uint64_t>(ctx, "tile_state", 3 * T);
             O.tcounter = dbuf<uint32_t>(ctx, "tile_ticket", 1);
             if (heap) {
@@ -1603,6 +1608,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         }
         HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, cmp_klen, bounds, km, T, tile_base, rec_meta, cmp_addr,
                            (job.flags & SKV_DROP_TOMBSTONES) ? 1u : 0u, O, d_flags + 2));
+        if (l0 && key_fp) launch_fp_verify(st, O.vcount, O.vpairs, R, cmp_addr, cmp_klen, fp_bad);
         if (l0) T0 = T;
     }
     HIPCHK(hipGetLastError());

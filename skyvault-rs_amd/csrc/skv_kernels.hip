@@ -573,21 +573,40 @@ __device__ __forceinline__ bool elem_less(const uint64_t* rec_addr, uint64_t ha,
 }
 
 // elem_less with a fingerprint shortcut (level-0 merge rounds): keys with equal prefix, length
-// and fingerprint of the bytes past 16 are taken as equal (no record bytes read); b's fingerprint
-// is in a register, a's read on demand. The tile verifies its result exactly afterwards.
-__device__ __forceinline__ bool elem_less_fp(const uint64_t* fp, const uint64_t* rec_addr, uint64_t ha, uint64_t la_,
-                                             uint64_t ca, uint64_t hb, uint64_t lb_, uint64_t cb, uint64_t fpb) {
+// and fingerprint of the bytes past 16 are taken as equal (no record bytes read); both
+// fingerprints come from registers / LDS. k_fp_verify checks every pair taken as equal.
+__device__ __forceinline__ bool elem_less_fp(bool use_fp, uint64_t fpa, const uint64_t* rec_addr, uint64_t ha,
+                                             uint64_t la_, uint64_t ca, uint64_t hb, uint64_t lb_, uint64_t cb,
+                                             uint64_t fpb) {
     if (ha != hb) return ha < hb;
     if (la_ != lb_) return la_ < lb_;
     const uint32_t la = (uint32_t)(ca >> 32), lb = (uint32_t)(cb >> 32);
     if (la > 16 && lb > 16) {
-        if (!(fp && la == lb && fp[(uint32_t)ca] == fpb)) {
+        if (!(use_fp && la == lb && fpa == fpb)) {
             const int s = suffix_cmp(rec_addr, ca, cb);
             if (s) return s < 0;
         }
     }
     if (la != lb) return la < lb;
     return (uint32_t)ca < (uint32_t)cb;
+}
+
+// The pairs k_tile<true> took as one key on equal prefix, length and fingerprint (O.vpairs, record
+// positions a << 32 | b): their bytes past 16 must be equal, else the call is rerun with exact
+// compares. Every pair is independent: a grid-stride loop with all its loads in flight.
+__global__ void k_fp_verify(const unsigned long long* __restrict__ vcount, const uint64_t* __restrict__ vpairs,
+                            const uint64_t* __restrict__ rec_addr, const uint32_t* __restrict__ klen,
+                            uint32_t* fp_bad) {
+    const uint64_t n = *vcount;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = vpairs[i];
+        const uint32_t a = (uint32_t)(v >> 32), b = (uint32_t)v;
+        const uint32_t la = klen[a], lb = klen[b];
+        int d = la != lb;
+        if (!d && la > 16)
+            d = bytes_cmp16((const uint8_t*)rec_addr[a] + 5 + 16, (const uint8_t*)rec_addr[b] + 5 + 16, la - 16) != 0;
+        if (d) atomicOr(fp_bad, 1u);
+    }
 }
 
 // fingerprints of the key bytes past 16 of the record arrays (records the emit kernels did not
@@ -669,11 +688,11 @@ __device__ __forceinline__ uint32_t seg_of(const uint32_t* cb, uint32_t m, uint3
 
 // Output stage of a level > 0 LDS tile (sorted samples): position i has hi = mh[i] and element
 // mi[i] (its lo and c in el_lo / el_c).
-__device__ void tile_output_samples(uint32_t n, const uint64_t* mh, const uint16_t* mi, const uint64_t* el_lo,
+__device__ void tile_output_samples(uint32_t n, const uint64_t* el_hi, const uint16_t* mi, const uint64_t* el_lo,
                                     const uint64_t* el_c, uint64_t base, const TileOut& O) {
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
         uint32_t e = mi[i];
-        O.ohi[base + i] = mh[i];
+        O.ohi[base + i] = el_hi[e];
         O.olo[base + i] = el_lo[e];
         O.oc[base + i] = el_c[e];
     }
@@ -884,11 +903,15 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                                                       const uint64_t* __restrict__ rec_addr, uint32_t drop_deletes,
                                                       TileOut O) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint64_t* el_lo = (uint64_t*)smem;  // by element id (= load position)
+    // by element id (= load position): key prefix, length | record, fingerprint of the bytes past
+    // 16. The merge rounds reach them through the id at a merged position, so a prefix tie reads
+    // the fingerprint from LDS (it was a global load per tie: at config 3 a third of the records
+    // share their key with another stream, and the ties kept the rounds waiting on HBM)
+    uint64_t* el_hi = (uint64_t*)smem;
+    uint64_t* el_lo = el_hi + TILE_CAP;
     uint64_t* el_c = el_lo + TILE_CAP;
-    uint64_t* mhA = el_c + TILE_CAP;  // key-hi by merged position (ping-pong)
-    uint64_t* mhB = mhA + TILE_CAP;
-    uint16_t* miA = (uint16_t*)(mhB + TILE_CAP);  // element id by merged position (ping-pong)
+    uint64_t* el_fp = el_c + TILE_CAP;
+    uint16_t* miA = (uint16_t*)(el_fp + TILE_CAP);  // element id by merged position (ping-pong)
     uint16_t* miB = miA + TILE_CAP;
     uint32_t* cbA = (uint32_t*)(miB + TILE_CAP);
     uint32_t* cbB = cbA + (k + 1);
@@ -942,29 +965,31 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     // Thread owns elements e = threadIdx.x + u*TILE_THREADS; key, position and segment stay in
     // registers across the merge rounds, so each round is one binary search + one LDS write.
     constexpr int PER = TILE_CAP / TILE_THREADS;
-    uint64_t rh[PER], rl[PER], rc[PER], raddr[PER], rfp[PER];
+    uint64_t rh[PER], rc[PER], raddr[PER];  // key bytes 8..15 and the fingerprint stay in LDS (read on a tie)
     uint32_t rpos[PER], rseg[PER], rmeta[PER];
     const uint64_t* kfp = L0 ? O.key_fp : nullptr;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         uint32_t e = threadIdx.x + u * TILE_THREADS;
-        rh[u] = rl[u] = rc[u] = raddr[u] = rfp[u] = 0;
+        rh[u] = rc[u] = raddr[u] = 0;
         rpos[u] = e;
         rseg[u] = 0;
         rmeta[u] = 0;
         if (e < n) {
             uint32_t j = seg_of(cbA, k + 1, e);
             uint64_t pos = bounds[t * k + j] + (e - cbA[j]);
-            load_elem<L0>(E, pos, rh[u], rl[u], rc[u]);
+            uint64_t lo, fp = 0;
+            load_elem<L0>(E, pos, rh[u], lo, rc[u]);
             if (L0) {
                 rmeta[u] = rec_meta[pos];
                 raddr[u] = (O.pay_addr ? O.pay_addr : rec_addr)[pos];  // coalesced here, not gathered later
-                if (kfp) rfp[u] = kfp[pos];
+                if (kfp) fp = kfp[pos];
             }
             rseg[u] = j;
-            el_lo[e] = rl[u];
+            el_hi[e] = rh[u];
+            el_lo[e] = lo;
             el_c[e] = rc[u];
-            mhA[e] = rh[u];
+            el_fp[e] = fp;
             miA[e] = (uint16_t)e;
         }
     }
@@ -974,8 +999,6 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     uint32_t m = k;
     uint32_t* cb = cbA;
     uint32_t* cbn = cbB;
-    uint64_t* mh = mhA;
-    uint64_t* mhn = mhB;
     uint16_t* mi = miA;
     uint16_t* min_ = miB;
     while (m > 1) {
@@ -1000,12 +1023,14 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
             for (int u = 0; u < PER; ++u) {
                 if (sn[u]) {
                     const uint32_t half = sn[u] >> 1, mid = sb[u] + half;
-                    const uint64_t xh = mh[mid];
+                    const uint32_t x = mi[mid];
+                    const uint64_t xh = el_hi[x];
                     bool less = xh < rh[u];
                     if (xh == rh[u]) {
-                        const uint32_t x = mi[mid];
-                        less = L0 ? elem_less_fp(kfp, rec_addr, xh, el_lo[x], el_c[x], rh[u], rl[u], rc[u], rfp[u])
-                                  : elem_less(rec_addr, xh, el_lo[x], el_c[x], rh[u], rl[u], rc[u]);
+                        const uint32_t me = threadIdx.x + u * TILE_THREADS;
+                        less = L0 ? elem_less_fp(kfp != nullptr, el_fp[x], rec_addr, xh, el_lo[x], el_c[x], rh[u],
+                                                 el_lo[me], rc[u], el_fp[me])
+                                  : elem_less(rec_addr, xh, el_lo[x], el_c[x], rh[u], el_lo[me], rc[u]);
                     }
                     if (less) {
                         sb[u] = mid + 1;
@@ -1023,7 +1048,6 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                 const uint32_t s = rseg[u], ps = s ^ 1u;
                 uint32_t newpos = rpos[u];
                 if (ps < m) newpos = cb[s & ~1u] + (rpos[u] - cb[s]) + (sb[u] - cb[ps]);
-                mhn[newpos] = rh[u];
                 min_[newpos] = (uint16_t)e;
                 rpos[u] = newpos;
                 rseg[u] = s >> 1;
@@ -1033,31 +1057,28 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         uint32_t mn = (m + 1) >> 1;
         for (uint32_t p = threadIdx.x; p <= mn; p += blockDim.x) cbn[p] = p < mn ? cb[2 * p] : cb[m];
         __syncthreads();
-        { uint64_t* tp = mh; mh = mhn; mhn = tp; }
         { uint16_t* tp = mi; mi = min_; min_ = tp; }
         { uint32_t* tp = cb; cb = cbn; cbn = tp; }
         m = mn;
     }
     if (!L0) {
-        tile_output_samples(n, mh, mi, el_lo, el_c, base, O);
+        tile_output_samples(n, el_hi, mi, el_lo, el_c, base, O);
         return;
     }
     TPROF(2);
-    // level 0 output: source addresses by final position first (the free ping-pong buffer), so
-    // that the exact neighbour compares below read the key bytes without a rec_addr lookup
-    uint64_t* paddr = mhn;
+    if (O.pop_pos) {
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-        const uint32_t e = threadIdx.x + u * TILE_THREADS;
-        if (e < n) {
-            paddr[rpos[u]] = raddr[u];
-            if (O.pop_pos) O.pop_pos[(uint32_t)rc[u]] = base + rpos[u];
+        for (int u = 0; u < PER; ++u) {
+            const uint32_t e = threadIdx.x + u * TILE_THREADS;
+            if (e < n) O.pop_pos[(uint32_t)rc[u]] = base + rpos[u];
         }
     }
-    __syncthreads();
-    // (a) first-per-key flags by merged position (k_way.rs:146-151)
+    // (a) first-per-key flags by merged position (k_way.rs:146-151). With fingerprints, a pair
+    // with equal prefix, length and fingerprint is taken as one key and queued for k_fp_verify;
+    // a pair whose lengths or fingerprints differ is two keys (and was ordered by exact compares
+    // in the rounds). Without them (exact mode) the suffixes are compared here.
     const uint32_t i0 = threadIdx.x * PER;
-    uint32_t keep_mask = 0;
+    uint32_t keep_mask = 0, vmask = 0;
     uint32_t idx[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
@@ -1065,34 +1086,58 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         idx[q] = 0;
         if (i < n) {
             const uint32_t e = mi[i];
-            const uint64_t h = mh[i], c = el_c[e];
+            const uint64_t c = el_c[e];
             bool first = true;
             if (O.act_hi) {  // heap-order mode: adjacent pops compared on their own keys
                 if (i > 0) first = act_key_cmp(O, (uint32_t)el_c[mi[i - 1]], (uint32_t)c) != 0;
-            } else if (i > 0 && mh[i - 1] == h) {  // exact: first-per-key and the check of the fp shortcut
+            } else if (i > 0) {
                 const uint32_t p = mi[i - 1];
-                const uint64_t lp = el_lo[p], le = el_lo[e], cp = el_c[p];
-                int kc = lp != le ? (lp < le ? -1 : 1) : 0;
-                const uint32_t kp = (uint32_t)(cp >> 32), ke = (uint32_t)(c >> 32);
-                if (!kc && kp > 16 && ke > 16)
-                    kc = bytes_cmp16((const uint8_t*)paddr[i - 1] + 5 + 16, (const uint8_t*)paddr[i] + 5 + 16,
-                                     (kp < ke ? kp : ke) - 16);
-                if (!kc) kc = kp < ke ? -1 : (kp > ke ? 1 : 0);
-                first = kc != 0;
-                if (O.fp_bad && (kc > 0 || (kc == 0 && (uint32_t)cp > (uint32_t)c))) atomicOr(O.fp_bad, 1u);
+                if (el_hi[p] == el_hi[e]) {
+                    const uint64_t lp = el_lo[p], le = el_lo[e], cp = el_c[p];
+                    int kc = lp != le ? (lp < le ? -1 : 1) : 0;
+                    const uint32_t kp = (uint32_t)(cp >> 32), ke = (uint32_t)(c >> 32);
+                    if (!kc && kp > 16 && ke > 16) {
+                        if (kfp) {
+                            const int same = kp == ke && el_fp[p] == el_fp[e];
+                            kc = same ? 0 : 1;
+                            if (same) vmask |= 1u << q;
+                        } else {
+                            kc = suffix_cmp(rec_addr, cp, c);
+                        }
+                    }
+                    if (!kc) kc = kp < ke ? -1 : (kp > ke ? 1 : 0);
+                    first = kc != 0;
+                }
             }
             idx[q] = (uint32_t)c;
             if (first) keep_mask |= 1u << q;
         }
     }
+    if (kfp) {  // queue the pairs taken as equal (one atomic per tile)
+        uint32_t vtot;
+        uint32_t vex = block_excl_scan<uint32_t>((uint32_t)__builtin_popcount(vmask), (uint32_t*)ws, vtot);
+        if (threadIdx.x == 0) s_flag[31] = vtot ? (uint32_t)atomicAdd(O.vcount, (unsigned long long)vtot) : 0u;
+        __syncthreads();
+        const uint64_t vb = s_flag[31];
+#pragma unroll
+        for (int q = 0; q < PER; ++q)
+            if (vmask & (1u << q)) {
+                const uint32_t i = i0 + q;
+                O.vpairs[vb + vex++] = ((uint64_t)(uint32_t)el_c[mi[i - 1]] << 32) | (uint32_t)el_c[mi[i]];
+            }
+    }
     __syncthreads();
     TPROF(3);
-    // (b) meta by final position (el_lo is free now)
+    // (b) source address and meta by final position (el_hi / el_lo are free now)
+    uint64_t* paddr = el_hi;
     uint32_t* pmeta = (uint32_t*)el_lo;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const uint32_t e = threadIdx.x + u * TILE_THREADS;
-        if (e < n) pmeta[rpos[u]] = rmeta[u];
+        if (e < n) {
+            paddr[rpos[u]] = raddr[u];
+            pmeta[rpos[u]] = rmeta[u];
+        }
     }
     __syncthreads();
     TPROF(4);
@@ -2033,6 +2078,12 @@ void launch_key_fp(hipStream_t s, uint64_t R, const uint64_t* rec_addr, const ui
 void launch_tile_n(hipStream_t s, const uint64_t* bounds, uint32_t k, uint64_t T, uint64_t* tile_n) {
     if (!T) return;
     k_tile_n<<<blocks_for(T, 256), 256, 0, s>>>(bounds, k, T, tile_n);
+}
+void launch_fp_verify(hipStream_t s, const unsigned long long* vcount, const uint64_t* vpairs, uint64_t cap,
+                      const uint64_t* rec_addr, const uint32_t* klen, uint32_t* fp_bad) {
+    unsigned blocks = blocks_for(cap ? cap : 1, 256);
+    if (blocks > 8192) blocks = 8192;
+    k_fp_verify<<<blocks, 256, 0, s>>>(vcount, vpairs, rec_addr, klen, fp_bad);
 }
 size_t tile_lds_bytes(uint32_t k) {
     size_t b = (size_t)TILE_CAP * (4 * 8 + 2 + 2) + 2 * (size_t)(k + 1) * 4;
