@@ -96,6 +96,14 @@ struct RunSummary {       // per run, read back by the host after the parse
     uint32_t pad;
 };
 
+// level-0 bounds narrowed by the level-1 sample counts (k_l1_cnt); cnt == null: plain searches
+struct L1Cnt {
+    const uint32_t* cnt;     // (T + 1) x k
+    const uint64_t* l1off;   // level-1 list offsets (k + 1)
+    const uint64_t *hi, *lo, *c;  // level-1 samples, list order
+    uint64_t S;              // level-1 step (records)
+};
+
 struct TileOut {
     // level > 0: sorted elements
     uint64_t* ohi;

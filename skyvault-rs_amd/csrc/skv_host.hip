@@ -1555,8 +1555,15 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         snprintf(nm, sizeof nm, "bounds%d", li);
         uint64_t* bounds = dbuf<uint64_t>(ctx, nm, (T + 1) * km);
         const Level* U = li + 1 < (int)lv.size() ? &lv[li + 1] : nullptr;
+        L1Cnt C{};
+        if (l0 && U && T > 1) {  // level 0: each search starts inside one level-1 sample gap
+            uint32_t* posof = dbuf<uint32_t>(ctx, "l1_posof", U->N);
+            uint32_t* cnt = dbuf<uint32_t>(ctx, "l1_cnt", (T + 1) * km);
+            launch_l1_cnt(st, U->sc, U->N, L.d_off, U->d_off, km, U->S, m, T, posof, cnt);
+            C = L1Cnt{cnt, U->d_off, U->hi, U->lo, U->c, U->S};
+        }
         launch_bounds(st, l0, L.hi, L.lo, L.c, cmp_klen, L.d_off, km, U ? U->shi : nullptr, U ? U->slo : nullptr,
-                      U ? U->sc : nullptr, m, T, cmp_addr, bounds, d_flags + 2);
+                      U ? U->sc : nullptr, m, T, cmp_addr, bounds, d_flags + 2, C.cnt ? &C : nullptr);
         snprintf(nm, sizeof nm, "tile_n%d", li);
         uint64_t* tile_n = dbuf<uint64_t>(ctx, nm, T);
         snprintf(nm, sizeof nm, "tile_base%d", li);

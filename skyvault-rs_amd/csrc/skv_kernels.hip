@@ -641,10 +641,47 @@ __global__ void k_sample(Elems src, const uint64_t* __restrict__ off_src, const 
 }
 
 // bounds[t*k + j] = first position of list j whose key >= splitter t's key
+// Level-1 sample counts per (splitter, stream) for the level-0 bounds (the fused path's k_fx_posof /
+// k_fx_l1cnt, skv_stride.hip): the level-1 samples of list j are its records off0[j] + c*S; sorted,
+// splitter t is sorted sample t*m. posof[l1off[j] + c] = sorted position of list j's sample c.
+__device__ __forceinline__ uint32_t last_le(const uint64_t* off, uint32_t k, uint64_t x) {
+    uint32_t lo = 0, hi = k;  // the last list j with off[j] <= x (empty lists share their offset)
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (off[mid] <= x) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+__global__ void k_l1_posof(const uint64_t* __restrict__ sc, uint64_t N1, const uint64_t* __restrict__ off0,
+                           const uint64_t* __restrict__ l1off, uint32_t k, uint64_t S, uint32_t* posof) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N1) return;
+    const uint64_t pos = (uint32_t)sc[p];  // level-1 c = key length << 32 | record position
+    const uint32_t j = last_le(off0, k, pos);
+    const uint64_t q = l1off[j] + (pos - off0[j]) / S;
+    if (q < l1off[j + 1]) posof[q] = (uint32_t)p;
+}
+// cnt[t*k + j] = list j's samples at sorted positions < t*m, for t in [1, T): sample c at position
+// p, the next one at pn, writes the splitters t with p < t*m <= pn (c = 0 also those before it)
+__global__ void k_l1_cnt(const uint32_t* __restrict__ posof, uint64_t N1, const uint64_t* __restrict__ l1off,
+                         uint32_t k, uint64_t m, uint64_t T, uint32_t* cnt) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= N1 || T < 2) return;
+    const uint32_t j = last_le(l1off, k, q);
+    const uint64_t c = q - l1off[j], p = posof[q], tmax = T - 1;
+    if (c == 0) {
+        const uint64_t th = p / m < tmax ? p / m : tmax;
+        for (uint64_t t = 1; t <= th; ++t) cnt[t * k + j] = 0;
+    }
+    const uint64_t th = q + 1 < l1off[j + 1] ? (posof[q + 1] / m < tmax ? posof[q + 1] / m : tmax) : tmax;
+    for (uint64_t t = p / m + 1; t <= th; ++t) cnt[t * k + j] = (uint32_t)(c + 1);
+}
+
 template <bool L0>
 __global__ void k_bounds(Elems E, const uint64_t* __restrict__ off, uint32_t k, const uint64_t* __restrict__ shi,
                          const uint64_t* __restrict__ slo, const uint64_t* __restrict__ sc, uint64_t m, uint64_t T,
-                         const uint64_t* __restrict__ rec_addr, uint64_t* bounds) {
+                         const uint64_t* __restrict__ rec_addr, uint64_t* bounds, L1Cnt C) {
     uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= (T + 1) * k || *E.poison) return;
     uint64_t t = g / k;
@@ -654,6 +691,17 @@ __global__ void k_bounds(Elems E, const uint64_t* __restrict__ off, uint32_t k, 
     if (t == T) { bounds[g] = b; return; }
     uint64_t sp = t * m;
     uint64_t h = shi[sp], l = slo[sp], c = sc[sp];
+    if (C.cnt && a < b) {
+        // stream j's level-1 samples sorted before the splitter (k_l1_cnt), minus those equal to it
+        // (lower_bound counts only the smaller ones): the bound lies in one sample gap
+        uint64_t n = C.cnt[t * k + j];
+        const uint64_t q0 = C.l1off[j];
+        while (n > 0 && ekey_cmp(rec_addr, C.hi[q0 + n - 1], C.lo[q0 + n - 1], C.c[q0 + n - 1], h, l, c) == 0) --n;
+        const uint64_t lo = n ? a + (n - 1) * C.S + 1 : a;
+        const uint64_t hi = a + n * C.S < b ? a + n * C.S : b;
+        a = lo;
+        b = hi;
+    }
     while (a < b) {
         uint64_t mid = (a + b) >> 1;
         uint64_t eh, el, ec;
@@ -2065,12 +2113,20 @@ void launch_sample(hipStream_t s, bool l0, const uint64_t* hi, const uint64_t* l
 void launch_bounds(hipStream_t s, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
                    const uint32_t* klen, const uint64_t* off, uint32_t k, const uint64_t* shi, const uint64_t* slo,
                    const uint64_t* sc, uint64_t m, uint64_t T, const uint64_t* rec_addr, uint64_t* bounds,
-                   const uint32_t* poison) {
+                   const uint32_t* poison, const L1Cnt* C) {
     Elems E{hi, lo, c, klen, poison};
     uint64_t n = (T + 1) * k;
     if (!n) return;
-    if (l0) k_bounds<true><<<blocks_for(n, 256), 256, 0, s>>>(E, off, k, shi, slo, sc, m, T, rec_addr, bounds);
-    else k_bounds<false><<<blocks_for(n, 256), 256, 0, s>>>(E, off, k, shi, slo, sc, m, T, rec_addr, bounds);
+    const L1Cnt none{};
+    const L1Cnt& cc = C ? *C : none;
+    if (l0) k_bounds<true><<<blocks_for(n, 256), 256, 0, s>>>(E, off, k, shi, slo, sc, m, T, rec_addr, bounds, cc);
+    else k_bounds<false><<<blocks_for(n, 256), 256, 0, s>>>(E, off, k, shi, slo, sc, m, T, rec_addr, bounds, cc);
+}
+void launch_l1_cnt(hipStream_t s, const uint64_t* sc, uint64_t N1, const uint64_t* off0, const uint64_t* l1off,
+                   uint32_t k, uint64_t S, uint64_t m, uint64_t T, uint32_t* posof, uint32_t* cnt) {
+    if (!N1) return;
+    k_l1_posof<<<blocks_for(N1, 256), 256, 0, s>>>(sc, N1, off0, l1off, k, S, posof);
+    k_l1_cnt<<<blocks_for(N1, 256), 256, 0, s>>>(posof, N1, l1off, k, m, T, cnt);
 }
 void launch_key_fp(hipStream_t s, uint64_t R, const uint64_t* rec_addr, const uint32_t* rec_klen, uint64_t* fp) {
     if (R) k_key_fp<<<blocks_for(R, 256), 256, 0, s>>>(R, rec_addr, rec_klen, fp);

@@ -39,7 +39,10 @@ void launch_sample(hipStream_t, bool l0, const uint64_t* hi, const uint64_t* lo,
 void launch_bounds(hipStream_t, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
                    const uint32_t* klen, const uint64_t* off, uint32_t k, const uint64_t* shi, const uint64_t* slo,
                    const uint64_t* sc, uint64_t m, uint64_t T, const uint64_t* rec_addr, uint64_t* bounds,
-                   const uint32_t* poison);
+                   const uint32_t* poison, const L1Cnt* C = nullptr);
+// level-1 sample counts per (splitter t, list j) for the level-0 bounds (sc: sorted level-1 samples)
+void launch_l1_cnt(hipStream_t, const uint64_t* sc, uint64_t N1, const uint64_t* off0, const uint64_t* l1off,
+                   uint32_t k, uint64_t S, uint64_t m, uint64_t T, uint32_t* posof, uint32_t* cnt);
 void launch_tile_n(hipStream_t, const uint64_t* bounds, uint32_t k, uint64_t T, uint64_t* tile_n);
 void launch_key_fp(hipStream_t, uint64_t R, const uint64_t* rec_addr, const uint32_t* rec_klen, uint64_t* fp);
 size_t tile_lds_bytes(uint32_t k);
