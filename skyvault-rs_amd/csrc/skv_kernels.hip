@@ -1322,6 +1322,14 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
     uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
     return ((uint64_t)hi << 32) | lo;
 }
+// a wave-uniform value the compiler cannot prove uniform (a shuffle reduction, a value merged from
+// branches) moved to scalar registers: the chain's state then stays in SGPRs and its branches are
+// scalar, instead of exec-masked VALU code on every step
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    uint32_t lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
 
 __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ P,
                                               uint64_t max_size, const uint32_t* __restrict__ tile_max,
@@ -1355,6 +1363,8 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
         o = __shfl_xor(mn, d, 64);
         mn = o < mn ? o : mn;
     }
+    mr = __builtin_amdgcn_readfirstlane(mr);  // uniform from here on (see uniform_u64)
+    mn = __builtin_amdgcn_readfirstlane(mn);
 #if SKV_CHAIN_PROF
     cp_mm = __builtin_amdgcn_s_memrealtime() - cp_t0;
 #endif
@@ -1482,6 +1492,8 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
 #endif
                 }
             }
+            e = uniform_u64(e);
+            Pe = uniform_u64(Pe);
             rb = lane == d ? b : rb;  // this round's run starts, stored together below
             ++m;
             L = e - b;
