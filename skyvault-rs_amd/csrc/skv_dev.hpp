@@ -122,7 +122,7 @@ struct TileOut {
     uint64_t* prof;       // SKV_TILE_PROF builds: per-phase time of level-0 tiles (8 counters)
     // level 0: fingerprints of the key bytes past 16 (k_key_fp); equal prefix, length and
     // fingerprint count as equal in the merge rounds and in first-per-key. Each adjacent pair taken
-    // as equal that way goes to vpairs (record positions a << 32 | b); k_fp_verify compares their
+    // as equal that way goes to vpairs (the two records' addresses); k_fp_verify compares their
     // bytes, and a pair that differs sets *fp_bad (the host reruns with exact compares)
     const uint64_t* key_fp;
     uint32_t* fp_bad;

@@ -113,6 +113,9 @@ struct skv_ctx {
     // pipelined host calls (compact_host_pipelined): the copy streams, per-part events, and the
     // host-mapped words the parts publish their survivor counts to
     hipStream_t in_stream = nullptr, out_stream = nullptr;
+    // k_fp_verify runs beside the chain and the gather (its verdict is only read with the result)
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t aux_ev[2] = {};
     std::vector<hipEvent_t> part_ev;
     uint64_t* part_k = nullptr;
     size_t part_k_cap = 0;
@@ -1533,6 +1536,10 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     const uint64_t* key_fp = nullptr;
     uint32_t* fp_bad = dbuf<uint32_t>(ctx, "fp_bad", 1);
     HIPCHK(hipMemsetAsync(fp_bad, 0, 4, st));
+    // k_fp_verify's inputs once the level-0 tiles are queued; it runs on the ctx stream before the
+    // WAL stage, or on the aux stream beside the gather (its verdict is read with the result)
+    std::pair<const unsigned long long*, const uint64_t*> verify_args{nullptr, nullptr};
+    bool verify_pending = false;
     if (km > 1 && !ctx->exact_keys && !heap) {
         const char* te = getenv("SKV_FP_TEST");
         if (te && te[0] == '1') {
@@ -1586,7 +1593,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             O.key_fp = key_fp;
             O.fp_bad = fp_bad;
             if (key_fp) {  // pairs taken as equal by fingerprint, verified after the tiles
-                O.vpairs = dbuf<uint64_t>(ctx, "fp_vpairs", R);
+                O.vpairs = dbuf<uint64_t>(ctx, "fp_vpairs", 2 * R);
                 O.vcount = dbuf<unsigned long long>(ctx, "fp_vcount", 1);
                 HIPCHK(hipMemsetAsync(O.vcount, 0, 8, st));
             }
@@ -1615,7 +1622,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
         }
         HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, cmp_klen, bounds, km, T, tile_base, rec_meta, cmp_addr,
                            (job.flags & SKV_DROP_TOMBSTONES) ? 1u : 0u, O, d_flags + 2));
-        if (l0 && key_fp) launch_fp_verify(st, O.vcount, O.vpairs, R, cmp_addr, cmp_klen, fp_bad);
+        if (l0 && key_fp) verify_args = {O.vcount, O.vpairs};
         if (l0) T0 = T;
     }
     HIPCHK(hipGetLastError());
@@ -1623,7 +1630,30 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     const uint64_t* d_K = d_Kout;
     hres.pop_pos = pop_pos;
     tables_mine();
+    auto fork_verify = [&]() {  // k_fp_verify on the aux stream, after what the ctx stream has queued
+        if (!verify_args.first) return;
+        if (!ctx->aux_stream) {
+            HIPCHK(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&ctx->aux_ev[0], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&ctx->aux_ev[1], hipEventDisableTiming));
+        }
+        HIPCHK(hipEventRecord(ctx->aux_ev[0], st));
+        HIPCHK(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_ev[0], 0));
+        launch_fp_verify(ctx->aux_stream, verify_args.first, verify_args.second, R, fp_bad);
+        HIPCHK(hipEventRecord(ctx->aux_ev[1], ctx->aux_stream));
+        verify_args.first = nullptr;
+        verify_pending = true;
+    };
+    auto join_verify = [&]() {  // fp_bad is read next: the ctx stream waits for k_fp_verify
+        if (verify_args.first) {  // not forked: in order on the ctx stream
+            launch_fp_verify(st, verify_args.first, verify_args.second, R, fp_bad);
+            verify_args.first = nullptr;
+        }
+        if (verify_pending) HIPCHK(hipStreamWaitEvent(st, ctx->aux_ev[1], 0));
+        verify_pending = false;
+    };
     if (job.flags & SKV_SPLIT_BY_TABLE) {
+        join_verify();
         htrace("merge launched");
         const int rc =
             wal_stage(ctx, job, R, d_K, m_rec, m_src, m_P, m_Dp, rec_addr, rec_klen, fp_bad, heap ? &hres : nullptr, out);
@@ -1677,6 +1707,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     launch_chain(st, d_K, m_P, job.max_run_size, tile_max, T0, run_b, d_nruns, chain_tbl, R, in_rec_bytes);
     launch_run_stats(st, d_nruns, run_b, m_P, m_Dp, m_rec, rec_klen, d_desc, seg_r0, R);
     mark(ctx, PH_CHAIN);
+    fork_verify();  // beside the gather (beside the single-wave chain it slowed the chain 3x)
     // ---- gather -----------------------------------------------------------------------------
     const uint64_t total_rec_bytes = job.in_bytes;
     uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + R + 16);
@@ -1703,6 +1734,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     skv_result* res = &box->pub;
     {
         const size_t vbytes = deferred ? 16 + (size_t)n_runs * 4 : 0;  // flags + broken runs
+        join_verify();
         uint8_t* hp = (uint8_t*)pinned(ctx, 64 + guess * sizeof(DevRunDesc) + vbytes);
         uint8_t* hv = hp + 64 + guess * sizeof(DevRunDesc);
         d2h(ctx, hp, d_nruns, 24);
@@ -1865,6 +1897,12 @@ static int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64
     }
 }
 
+// after an error: every stream of the ctx idle before its buffers are reused
+static void drain(skv_ctx* ctx) {
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->aux_stream) (void)hipStreamSynchronize(ctx->aux_stream);
+}
+
 static int run_guarded(skv_ctx* ctx, const Job& job, skv_result** out, double t_entry) {
     try {
         ctx->sync_ms = 0;
@@ -1874,13 +1912,13 @@ static int run_guarded(skv_ctx* ctx, const Job& job, skv_result** out, double t_
         ctx->timings.host_sync_ms = ctx->sync_ms;
         return rc;
     } catch (const ApiError& e) {
-        (void)hipStreamSynchronize(ctx->stream);
+        drain(ctx);
         return set_err(ctx, e.code, "%s", e.msg.c_str());
     } catch (const DevError& e) {
-        (void)hipStreamSynchronize(ctx->stream);
+        drain(ctx);
         return set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());
     } catch (const std::exception& e) {  // bad_alloc of a host table, system_error, ...: never unwind into C
-        (void)hipStreamSynchronize(ctx->stream);
+        drain(ctx);
         return set_err(ctx, SKV_E_DEVICE, "host error: %s", e.what());
     }
 }
@@ -1936,6 +1974,12 @@ void skv_ctx_destroy(skv_ctx* ctx) {
     for (int i = 0; i < PH_N; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
     for (hipEvent_t e : ctx->part_ev) (void)hipEventDestroy(e);
+    if (ctx->aux_stream) {
+        (void)hipStreamSynchronize(ctx->aux_stream);
+        (void)hipStreamDestroy(ctx->aux_stream);
+    }
+    for (hipEvent_t e : ctx->aux_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->part_k) (void)hipHostFree(ctx->part_k);
     if (ctx->in_stream) {
         (void)hipStreamSynchronize(ctx->in_stream);

@@ -591,22 +591,41 @@ __device__ __forceinline__ bool elem_less_fp(bool use_fp, uint64_t fpa, const ui
     return (uint32_t)ca < (uint32_t)cb;
 }
 
-// The pairs k_tile<true> took as one key on equal prefix, length and fingerprint (O.vpairs, record
-// positions a << 32 | b): their bytes past 16 must be equal, else the call is rerun with exact
+// The pairs k_tile<true> took as one key on equal prefix, length and fingerprint (O.vpairs: the two
+// records' addresses): their bytes past 16 must be equal, else the call is rerun with exact
 // compares. Every pair is independent: a grid-stride loop with all its loads in flight.
 __global__ void k_fp_verify(const unsigned long long* __restrict__ vcount, const uint64_t* __restrict__ vpairs,
-                            const uint64_t* __restrict__ rec_addr, const uint32_t* __restrict__ klen,
                             uint32_t* fp_bad) {
     const uint64_t n = *vcount;
+    uint32_t bad = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t v = vpairs[i];
-        const uint32_t a = (uint32_t)(v >> 32), b = (uint32_t)v;
-        const uint32_t la = klen[a], lb = klen[b];
-        int d = la != lb;
-        if (!d && la > 16)
-            d = bytes_cmp16((const uint8_t*)rec_addr[a] + 5 + 16, (const uint8_t*)rec_addr[b] + 5 + 16, la - 16) != 0;
-        if (d) atomicOr(fp_bad, 1u);
+        const uint8_t* ra = (const uint8_t*)vpairs[2 * i];
+        const uint8_t* rb = (const uint8_t*)vpairs[2 * i + 1];
+        const uint32_t la = __builtin_bswap32(load_window16(ra + 1, 4).x);  // key_len of each record
+        const uint32_t lb = __builtin_bswap32(load_window16(rb + 1, 4).x);
+        const uint8_t* ka = ra + 5 + 16;
+        const uint8_t* kb = rb + 5 + 16;
+        bad |= la != lb;
+        const uint32_t nt = la == lb && la > 16 ? la - 16 : 0;
+        // 64 tail bytes of both keys per step, all eight windows loaded before any compare
+        for (uint32_t o = 0; o < nt; o += 64) {
+            uint4 x[4], y[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t m = o + 16 * w < nt ? (nt - o - 16 * w < 16 ? nt - o - 16 * w : 16) : 0;
+                x[w] = m ? load_window16(ka + o + 16 * w, m) : make_uint4(0, 0, 0, 0);
+                y[w] = m ? load_window16(kb + o + 16 * w, m) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t m = o + 16 * w < nt ? (nt - o - 16 * w < 16 ? nt - o - 16 * w : 16) : 0;
+                const uint32_t dx = ((x[w].x ^ y[w].x) & dword_mask(0, m, 0)) | ((x[w].y ^ y[w].y) & dword_mask(0, m, 1)) |
+                                    ((x[w].z ^ y[w].z) & dword_mask(0, m, 2)) | ((x[w].w ^ y[w].w) & dword_mask(0, m, 3));
+                bad |= dx != 0;
+            }
+        }
     }
+    if (bad) atomicOr(fp_bad, 1u);
 }
 
 // fingerprints of the key bytes past 16 of the record arrays (records the emit kernels did not
@@ -1161,18 +1180,14 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
             if (first) keep_mask |= 1u << q;
         }
     }
-    if (kfp) {  // queue the pairs taken as equal (one atomic per tile)
+    uint32_t vex = 0;
+    uint64_t vb = 0;
+    if (kfp) {  // slots for the pairs taken as equal (one atomic per tile), written below
         uint32_t vtot;
-        uint32_t vex = block_excl_scan<uint32_t>((uint32_t)__builtin_popcount(vmask), (uint32_t*)ws, vtot);
+        vex = block_excl_scan<uint32_t>((uint32_t)__builtin_popcount(vmask), (uint32_t*)ws, vtot);
         if (threadIdx.x == 0) s_flag[31] = vtot ? (uint32_t)atomicAdd(O.vcount, (unsigned long long)vtot) : 0u;
         __syncthreads();
-        const uint64_t vb = s_flag[31];
-#pragma unroll
-        for (int q = 0; q < PER; ++q)
-            if (vmask & (1u << q)) {
-                const uint32_t i = i0 + q;
-                O.vpairs[vb + vex++] = ((uint64_t)(uint32_t)el_c[mi[i - 1]] << 32) | (uint32_t)el_c[mi[i]];
-            }
+        vb = s_flag[31];
     }
     __syncthreads();
     TPROF(3);
@@ -1188,6 +1203,15 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         }
     }
     __syncthreads();
+    // the queued pairs as the two records' addresses (k_fp_verify then touches only their keys)
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+        if (vmask & (1u << q)) {
+            const uint32_t i = i0 + q;
+            O.vpairs[2 * (vb + vex)] = paddr[i - 1];
+            O.vpairs[2 * (vb + vex) + 1] = paddr[i];
+            ++vex;
+        }
     TPROF(4);
     // (c) Delete filter, tile totals
     uint32_t mt[PER];
@@ -2148,10 +2172,10 @@ void launch_tile_n(hipStream_t s, const uint64_t* bounds, uint32_t k, uint64_t T
     k_tile_n<<<blocks_for(T, 256), 256, 0, s>>>(bounds, k, T, tile_n);
 }
 void launch_fp_verify(hipStream_t s, const unsigned long long* vcount, const uint64_t* vpairs, uint64_t cap,
-                      const uint64_t* rec_addr, const uint32_t* klen, uint32_t* fp_bad) {
+                      uint32_t* fp_bad) {
     unsigned blocks = blocks_for(cap ? cap : 1, 256);
     if (blocks > 8192) blocks = 8192;
-    k_fp_verify<<<blocks, 256, 0, s>>>(vcount, vpairs, rec_addr, klen, fp_bad);
+    k_fp_verify<<<blocks, 256, 0, s>>>(vcount, vpairs, fp_bad);
 }
 size_t tile_lds_bytes(uint32_t k) {
     size_t b = (size_t)TILE_CAP * (4 * 8 + 2 + 2) + 2 * (size_t)(k + 1) * 4;

@@ -107,7 +107,7 @@ void launch_fx_desc(hipStream_t, const FxArgs& A, DevRunDesc* descs, uint64_t* n
 // *dst = *src with a system-scope store: dst is host-mapped pinned memory the host polls
 // the pairs k_tile<true> took as equal keys by fingerprint: any that differ set *fp_bad
 void launch_fp_verify(hipStream_t, const unsigned long long* vcount, const uint64_t* vpairs, uint64_t cap,
-                      const uint64_t* rec_addr, const uint32_t* klen, uint32_t* fp_bad);
+                      uint32_t* fp_bad);
 void launch_fx_publish(hipStream_t, const uint64_t* src, uint64_t* dst);
 // n bytes src -> dst by a kernel (src may be host-mapped pinned memory): small table uploads that
 // must not queue behind bulk DMA on a copy engine (pipelined host calls)
