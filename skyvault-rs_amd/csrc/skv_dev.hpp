@@ -278,6 +278,20 @@ __device__ inline bool utf8_valid(const uint8_t* s, uint64_t n) {
     return true;
 }
 
+// Compare-exchange i of the bitonic stage (kk = 2^lk, jj = 2^lj) in the ascending-comparator form:
+// the first stage of each merge pairs mirrored positions, the others pairs jj apart. Shifts, not
+// the division by jj (a 32-bit integer division is a long instruction sequence on gfx950).
+__device__ __forceinline__ void bitonic_pair(uint32_t i, uint32_t lk, uint32_t lj, uint32_t& a, uint32_t& c) {
+    const uint32_t off = i & ((1u << lj) - 1), blk = i >> lj;
+    if (lj + 1 == lk) {
+        a = (blk << lk) + off;
+        c = (blk << lk) + (1u << lk) - 1 - off;
+    } else {
+        a = (blk << (lj + 1)) + off;
+        c = a + (1u << lj);
+    }
+}
+
 struct WalkRes {
     uint64_t end;   // first record start >= stop, or the erroring record's start
     uint32_t cnt;   // records decoded

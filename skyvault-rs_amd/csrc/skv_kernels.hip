@@ -868,21 +868,16 @@ __device__ void tile_big(Elems E, const uint64_t* bounds, uint32_t k, uint64_t t
         if (L0) xm[i] = rec_meta[pos];
     }
     __syncthreads();
-    uint32_t P = 1;
-    while (P < n) P <<= 1;
-    for (uint32_t kk = 2; kk <= P; kk <<= 1) {
-        for (uint32_t jj = kk >> 1; jj >= 1; jj >>= 1) {
+    uint32_t P = 1, lp = 0;
+    while (P < n) {
+        P <<= 1;
+        ++lp;
+    }
+    for (uint32_t lk = 1; lk <= lp; ++lk) {
+        for (int lj = (int)lk - 1; lj >= 0; --lj) {
             for (uint32_t i = threadIdx.x; i < P / 2; i += blockDim.x) {
                 uint32_t a, b;
-                if (jj == (kk >> 1)) {
-                    uint32_t blk = i / jj, off = i % jj;
-                    a = blk * kk + off;
-                    b = blk * kk + kk - 1 - off;
-                } else {
-                    uint32_t blk = i / jj, off = i % jj;
-                    a = blk * 2 * jj + off;
-                    b = a + jj;
-                }
+                bitonic_pair(i, lk, (uint32_t)lj, a, b);
                 if (b < n) {
                     if (elem_less(rec_addr, xh[b], xl[b], xc[b], xh[a], xl[a], xc[a])) {
                         uint64_t th = xh[a], tl = xl[a], tc = xc[a];

@@ -360,15 +360,16 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
         id[i] = (uint16_t)i;
     }
     __syncthreads();
-    uint32_t P = 1;
-    while (P < n32) P <<= 1;
-    for (uint32_t kk = 2; kk <= P; kk <<= 1) {
-        for (uint32_t jj = kk >> 1; jj >= 1; jj >>= 1) {
+    uint32_t P = 1, lp = 0;
+    while (P < n32) {
+        P <<= 1;
+        ++lp;
+    }
+    for (uint32_t lk = 1; lk <= lp; ++lk) {
+        for (int lj = (int)lk - 1; lj >= 0; --lj) {
             for (uint32_t i = threadIdx.x; i < P / 2; i += blockDim.x) {
-                const uint32_t blk = i / jj, off = i % jj;
-                const bool first = jj == (kk >> 1);
-                const uint32_t a = first ? blk * kk + off : blk * 2 * jj + off;
-                const uint32_t c = first ? blk * kk + kk - 1 - off : a + jj;
+                uint32_t a, c;
+                bitonic_pair(i, lk, (uint32_t)lj, a, c);
                 if (c < n32) {
                     const SKey ka = key[a], kc = key[c];
                     const uint32_t ia = id[a], ic = id[c];
