@@ -104,6 +104,29 @@ struct L1Cnt {
     uint64_t S;              // level-1 step (records)
 };
 
+// parallel greedy split (k_split_*): the plan k_split_plan leaves for the later kernels
+constexpr uint32_t SPLIT_SERIAL = 0, SPLIT_PAR = 1;
+constexpr uint32_t SPLIT_FB = 0xFFFFFFFFu;  // seg_sel: the stitch walked this segment itself
+struct SplitPlan {
+    uint32_t mode;       // SPLIT_SERIAL: k_chain splits; SPLIT_PAR: k_split_walk/stitch/emit did
+    uint32_t nseg;       // segments with windows
+    uint32_t nseg_sel;   // segments the stitch resolved from a window or walked (seg_sel valid)
+    uint32_t n_fb;       // segments the stitch had to walk (true start outside the window)
+    uint64_t K, PK, L0;  // records, output record bytes, first-run record count guess
+    uint64_t avg, adv;   // average record bytes, expected bytes per run
+};
+struct SplitBufs {
+    SplitPlan* plan;
+    uint64_t* seg_w;     // window: first candidate record of segment s
+    uint32_t* seg_n;     // window: candidates
+    uint32_t* seg_sel;   // the true start's candidate index (SPLIT_FB: walked by the stitch)
+    uint64_t* seg_D;     // guess walks: bytes advanced by segr runs, then their exclusive prefix G_s
+    uint32_t* chain;     // [s][k < segr][candidate] run starts of each candidate's chain
+    uint32_t* ends;      // [s][candidate] where the candidate's segr runs end (next segment's start)
+    uint32_t nseg_cap, segr, nc;  // segments allocated, runs per segment, candidates per window
+    uint64_t min_runs;   // fewer expected runs: SPLIT_SERIAL (the single-wave chain is as fast)
+};
+
 struct TileOut {
     // level > 0: sorted elements
     uint64_t* ohi;

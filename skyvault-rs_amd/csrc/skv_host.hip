@@ -1704,7 +1704,43 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     uint64_t* seg_r0 = dbuf<uint64_t>(ctx, "seg_r0", R / GATHER_SEG + 2);
     const uint64_t in_rec_bytes = job.in_bytes;  // bounds P[K]
     uint32_t* chain_tbl = dbuf<uint32_t>(ctx, "chain_tbl", chain_table_entries(in_rec_bytes));
-    launch_chain(st, d_K, m_P, job.max_run_size, tile_max, T0, run_b, d_nruns, chain_tbl, R, in_rec_bytes);
+    // parallel split buffers (k_split_*; the device plan falls back to k_chain where it does not fit).
+    // SKV_SPLIT=serial: k_chain only; =par: no minimum run count. SKV_SPLIT_NC / SKV_SPLIT_SEG:
+    // candidates per window, runs per segment (tests shrink the window to exercise the stitch's walks)
+    SplitBufs sp{};
+    {
+        const char* mode = getenv("SKV_SPLIT");
+        const bool serial = mode && !strcmp(mode, "serial");
+        sp.segr = 16;
+        sp.nc = 512;
+        sp.min_runs = mode && !strcmp(mode, "par") ? 0 : 1024;
+        if (const char* e = getenv("SKV_SPLIT_NC")) sp.nc = (uint32_t)std::min<uint64_t>(8192, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
+        if (const char* e = getenv("SKV_SPLIT_SEG")) sp.segr = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
+        const uint64_t M = job.max_run_size;
+        if (!serial && M > 8 && R < 0xFFFFFFF0ull) {
+            // runs of >= 8 records (the plan's gate) hold > 7/8 (max - 1) bytes each
+            const uint64_t runs_ub = in_rec_bytes / ((M - 1) - (M - 1) / 8) + 2;
+            const uint64_t want = runs_ub / sp.segr + 2;
+            sp.nseg_cap = (uint32_t)std::min<uint64_t>(want, 16384);
+        }
+        if (sp.nseg_cap) {
+            sp.plan = dbuf<SplitPlan>(ctx, "split_plan", 1);
+            sp.seg_w = dbuf<uint64_t>(ctx, "split_w", sp.nseg_cap);
+            sp.seg_n = dbuf<uint32_t>(ctx, "split_n", sp.nseg_cap);
+            sp.seg_sel = dbuf<uint32_t>(ctx, "split_sel", sp.nseg_cap);
+            sp.seg_D = dbuf<uint64_t>(ctx, "split_D", sp.nseg_cap);
+            sp.chain = dbuf<uint32_t>(ctx, "split_chain", (uint64_t)sp.nseg_cap * sp.segr * sp.nc);
+            sp.ends = dbuf<uint32_t>(ctx, "split_ends", (uint64_t)sp.nseg_cap * sp.nc + 4);
+        }
+    }
+    launch_chain(st, d_K, m_P, job.max_run_size, tile_max, T0, run_b, d_nruns, chain_tbl, R, in_rec_bytes, &sp);
+    if (sp.nseg_cap && getenv("SKV_SPLIT_DEBUG")) {
+        sync(ctx);
+        SplitPlan pl;
+        HIPCHK(hipMemcpy(&pl, sp.plan, sizeof(pl), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[split] mode=%u nseg=%u sel=%u walked=%u K=%llu L0=%llu cap=%u\n", pl.mode, pl.nseg,
+                pl.nseg_sel, pl.n_fb, (unsigned long long)pl.K, (unsigned long long)pl.L0, sp.nseg_cap);
+    }
     launch_run_stats(st, d_nruns, run_b, m_P, m_Dp, m_rec, rec_klen, d_desc, seg_r0, R);
     mark(ctx, PH_CHAIN);
     fork_verify();  // beside the gather (beside the single-wave chain it slowed the chain 3x)

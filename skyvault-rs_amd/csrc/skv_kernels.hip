@@ -1326,14 +1326,15 @@ constexpr uint32_t CH_SHIFT = 10;  // byte -> record table granularity (1 KiB)
 // tbl[t] = the surviving record j with P[j] <= t * 2^CH_SHIFT < P[j+1] (K past the end): lets the
 // chain turn a byte position into a record index with one load
 __global__ void k_chain_table(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ P, uint32_t* tbl,
-                              uint64_t n_tbl) {
+                              uint64_t n_tbl, const SplitPlan* __restrict__ plan) {
+    if (plan && plan->mode == SPLIT_PAR) return;
     const uint64_t K = *Kp;
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j > K) return;
     const uint64_t G = 1ull << CH_SHIFT;
-    const uint64_t lo = P[j];
-    const uint64_t hi = j < K ? P[j + 1] : lo + 1;  // past P[K] the chain clamps to K itself
-    for (uint64_t t = (lo + G - 1) >> CH_SHIFT; t < ((hi + G - 1) >> CH_SHIFT) && t < n_tbl; ++t) tbl[t] = (uint32_t)j;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= K; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t lo = P[j];
+        const uint64_t hi = j < K ? P[j + 1] : lo + 1;  // past P[K] the chain clamps to K itself
+        for (uint64_t t = (lo + G - 1) >> CH_SHIFT; t < ((hi + G - 1) >> CH_SHIFT) && t < n_tbl; ++t) tbl[t] = (uint32_t)j;
+    }
 }
 
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
@@ -1353,7 +1354,9 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
 __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ P,
                                               uint64_t max_size, const uint32_t* __restrict__ tile_max,
                                               uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs_out,
-                                              const uint32_t* __restrict__ tbl, uint64_t n_tbl) {
+                                              const uint32_t* __restrict__ tbl, uint64_t n_tbl,
+                                              const SplitPlan* __restrict__ plan) {
+    if (plan && plan->mode == SPLIT_PAR) return;  // k_split_* wrote run_b and n_runs_out
     const uint64_t K = *Kp;
     const int lane = threadIdx.x;
 #if SKV_CHAIN_PROF
@@ -1536,6 +1539,386 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
         run_b[m] = K;
         *n_runs_out = m;
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// Parallel exact greedy split (build_runs' size split, runs.rs:211-238). With every record
+// fitting a run, the run starting at record b ends at f(b) = the last e with P[e] <= P[b] + max - 1
+// (P[K] included), and the run starts are the chain 0, f(0), f(f(0)), ... f is monotone but no
+// contraction: chains from two starts a record or more apart keep their byte offset, so the chain
+// cannot be guessed from anywhere but its true start. What CAN be guessed is where it is: runs are
+// cut into segments of segr runs, and the byte position of segment s's first run start is the sum
+// of the earlier segments' advances (segr x max minus the slack each run leaves, a sum of
+// independent slacks whose spread grows as sqrt(s)). So:
+//   k_split_plan   the gate (one workgroup);
+//   k_split_guess  one lane per segment walks segr runs from an arbitrary record near its expected
+//                  start: the advance D_s;
+//   k_split_scan   G_s = the exclusive prefix of D: segment s's byte guess;
+//   k_split_walk   the nc records around the record at G_s are segment s's candidate starts; one
+//                  lane per candidate walks segr runs from it (all segments, all candidates at
+//                  once), storing every run start and where the walk ends;
+//   k_split_stitch one thread follows the true chain through the segments: its start of segment s
+//                  is a candidate (index = start - window start, one LDS read of the staged ends)
+//                  whose walk gives the start of segment s + 1; a start outside its window is
+//                  walked by the stitch itself;
+//   k_split_emit   copies the chosen candidates' run starts into run_b.
+// Each f step is three rounds of eight independent probes of P (stride 64 around the previous
+// run's record count, then 9-ary), no lookup table. Inputs it does not fit (runs of < 8 records,
+// record sizes all equal, few runs, K >= 2^32) keep the single-wave k_chain (plan->mode).
+
+// last j in [lo, hi) with P[j] <= v, given P[lo] <= v < P[hi]: a first round of probes at stride
+// 64 around the guess g, then 9-ary rounds, each of eight independent loads
+__device__ uint64_t sp_search(const uint64_t* __restrict__ P, uint64_t lo, uint64_t Plo, uint64_t hi, uint64_t v,
+                              uint64_t g, uint64_t& Pe) {
+    uint64_t st = 64;
+    uint64_t base = g > lo + 4 * 64 ? g - 4 * 64 : lo;  // probes base + st * q, q = 1..8
+    while (hi - lo > 1) {
+        uint64_t x[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t p = base + st * (uint64_t)(q + 1);
+            x[q] = (p > lo && p < hi) ? P[p] : 0;
+        }
+        uint64_t nlo = lo, nPlo = Plo, nhi = hi;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t p = base + st * (uint64_t)(q + 1);
+            if (p > lo && p < hi) {
+                if (x[q] <= v) {
+                    nlo = p;  // probes ascend: the last true one wins
+                    nPlo = x[q];
+                } else if (p < nhi) {
+                    nhi = p;
+                }
+            }
+        }
+        lo = nlo;
+        Plo = nPlo;
+        hi = nhi;
+        st = (hi - lo + 8) / 9;
+        base = lo;
+    }
+    Pe = Plo;
+    return lo;
+}
+
+// f(b) and P[f(b)]; every record fits a run (plan gate); Lg: guessed records in the run
+__device__ __forceinline__ uint64_t sp_step(const uint64_t* __restrict__ P, uint64_t K, uint64_t PK, uint64_t M,
+                                            uint64_t b, uint64_t Pb, uint64_t Lg, uint64_t& Pe) {
+    if (b >= K) {
+        Pe = PK;
+        return K;
+    }
+    const uint64_t v = Pb + M - 1;  // record j fits iff P[j + 1] <= v
+    if (PK <= v) {
+        Pe = PK;
+        return K;
+    }
+    uint64_t g = b + Lg;
+    if (g >= K) g = K - 1;
+    return sp_search(P, b, Pb, K, v, g, Pe);
+}
+
+constexpr int SPLIT_PLAN_THREADS = 1024;
+constexpr int SPLIT_GUESS_SEGS = 16;  // guess walks per 64-lane workgroup: spread over CUs, each
+                                      // walk's probes are cache lines of their own
+
+// gate and constants (one workgroup): smallest / largest surviving record from k_tile<true>
+__global__ void __launch_bounds__(SPLIT_PLAN_THREADS)
+    k_split_plan(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ P, uint64_t M,
+                 const uint32_t* __restrict__ tile_max, uint64_t n_tiles, SplitBufs B) {
+    __shared__ uint32_t s_mm[2];
+    const int tid = threadIdx.x;
+    const uint64_t K = *Kp;
+    if (tid == 0) {
+        s_mm[0] = 0xFFFFFFFFu;
+        s_mm[1] = 0;
+    }
+    __syncthreads();
+    uint32_t mn = 0xFFFFFFFFu, mr = 0;
+    for (uint64_t t = tid; t < n_tiles; t += SPLIT_PLAN_THREADS) {
+        mn = tile_max[2 * t] < mn ? tile_max[2 * t] : mn;
+        mr = tile_max[2 * t + 1] > mr ? tile_max[2 * t + 1] : mr;
+    }
+    atomicMin(&s_mm[0], mn);
+    atomicMax(&s_mm[1], mr);
+    __syncthreads();
+    if (tid) return;
+    mn = s_mm[0];
+    mr = s_mm[1];
+    SplitPlan pl{};
+    pl.mode = SPLIT_SERIAL;
+    // gate: every run holds >= 8 records (so no record exceeds max), record sizes differ (else
+    // k_chain's arithmetic split), enough runs to pay for the passes, u32 record indices
+    if (K > 0 && K < 0xFFFFFFF0ull && B.nseg_cap > 0 && M > 1 && (M - 1) >= 8 * (uint64_t)mr && mn != mr) {
+        const uint64_t PK = P[K];
+        const uint64_t avg = PK / K ? PK / K : 1;
+        const uint64_t adv = (M - 1) - (avg / 2 < M - 1 ? avg / 2 : 0);  // expected bytes per run
+        const uint64_t runs_ub = PK / ((M - 1) - mr) + 1;  // every run but the last holds > max - 1 - mr bytes
+        const uint64_t nseg = (runs_ub + B.segr - 1) / B.segr + 1;
+        if (nseg <= B.nseg_cap && PK / adv + 1 >= B.min_runs) {
+            pl.mode = SPLIT_PAR;
+            pl.nseg = (uint32_t)nseg;
+            pl.K = K;
+            pl.PK = PK;
+            pl.L0 = (M - 1) / avg ? (M - 1) / avg : 1;
+            pl.avg = avg;
+            pl.adv = adv;
+        }
+    }
+    *B.plan = pl;
+}
+
+// guess walks: segment s from the record expected at byte s * segr * adv (indexed by the average
+// record size; any nearby start samples the same slack statistics): seg_D[s] = bytes advanced
+__global__ void __launch_bounds__(64) k_split_guess(const uint64_t* __restrict__ P, uint64_t M, SplitBufs B) {
+    const SplitPlan pl = *B.plan;
+    const uint64_t s = (uint64_t)blockIdx.x * SPLIT_GUESS_SEGS + threadIdx.x;
+    if (pl.mode != SPLIT_PAR || threadIdx.x >= SPLIT_GUESS_SEGS || s >= pl.nseg) return;
+    const uint64_t K = pl.K, PK = pl.PK;
+    const uint32_t segr = B.segr;
+    uint64_t a = (uint64_t)((double)s * segr * pl.adv / pl.avg);
+    if (a > K) a = K;
+    uint64_t b = a, Pb = P[a], L = pl.L0;
+    const uint64_t Pa = Pb;
+    uint32_t k = 0;
+    for (; k < segr && b < K; ++k) {
+        uint64_t Pe;
+        const uint64_t e = sp_step(P, K, PK, M, b, Pb, L, Pe);
+        if (e < K) L = e - b;
+        b = e;
+        Pb = Pe;
+    }
+    B.seg_D[s] = k == segr ? Pb - Pa : segr * pl.adv;  // reached the end early: the expected advance
+}
+
+// seg_D becomes the exclusive prefix G_s (one workgroup; thread tid owns a block of segments)
+__global__ void __launch_bounds__(SPLIT_PLAN_THREADS) k_split_scan(SplitBufs B) {
+    __shared__ uint64_t ws[32];
+    const SplitPlan pl = *B.plan;
+    if (pl.mode != SPLIT_PAR) return;
+    const uint64_t nseg = pl.nseg, tid = threadIdx.x;
+    const uint64_t per = (nseg + SPLIT_PLAN_THREADS - 1) / SPLIT_PLAN_THREADS;
+    const uint64_t s0 = tid * per < nseg ? tid * per : nseg, s1 = s0 + per < nseg ? s0 + per : nseg;
+    uint64_t sum = 0;
+    for (uint64_t s = s0; s < s1; ++s) sum += B.seg_D[s];
+    uint64_t tot;
+    uint64_t G = block_excl_scan(sum, ws, tot);
+    for (uint64_t s = s0; s < s1; ++s) {
+        const uint64_t d = B.seg_D[s];
+        B.seg_D[s] = G;
+        G += d;
+    }
+}
+
+// grid: nseg_cap x ceil(nc / blockDim) workgroups (blockDim >= 64). Wave 0 finds the record at
+// byte G_s (64-ary search over P, 64 independent probes a round); the window is the nc records
+// around it; lane = candidate, walking segr runs and storing every run start
+__global__ void k_split_walk(const uint64_t* __restrict__ P, uint64_t M, SplitBufs B) {
+    __shared__ uint64_t s_c;
+    const SplitPlan& pl = *B.plan;
+    if (pl.mode != SPLIT_PAR) return;
+    const uint32_t per_seg = (B.nc + blockDim.x - 1) / blockDim.x;
+    const uint64_t s = blockIdx.x / per_seg;
+    if (s >= pl.nseg) return;
+    const uint64_t K = pl.K, PK = pl.PK;
+    const uint32_t segr = B.segr, nc = B.nc;
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        const uint64_t G = B.seg_D[s];
+        uint64_t lo = 0, hi = K;  // P[lo] <= G < P[hi]
+        if (G >= PK) {
+            lo = K;
+            hi = K;
+        }
+        while (hi - lo > 1) {
+            const uint64_t st = (hi - lo + 63) / 64;
+            const uint64_t p = lo + st * (uint64_t)(lane + 1);
+            const uint64_t m = __ballot(p < hi && P[p] <= G);  // true lanes: a prefix
+            const uint64_t c = (uint64_t)__builtin_popcountll(m);
+            const uint64_t nhi = lo + st * (c + 1);
+            lo = lo + st * c;
+            hi = nhi < hi ? nhi : hi;
+        }
+        if (lane == 0) s_c = lo;
+    }
+    __syncthreads();
+    const uint64_t c = s_c;
+    const uint64_t w = s == 0 ? 0 : (c > nc / 2 ? c - nc / 2 : 0);
+    const uint32_t n = (uint32_t)(K + 1 - w < nc ? K + 1 - w : nc);
+    const uint32_t i = (blockIdx.x % per_seg) * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        B.seg_w[s] = w;
+        B.seg_n[s] = n;
+    }
+    if (i >= n) return;
+    uint32_t* out = B.chain + s * (uint64_t)segr * nc + i;
+    uint64_t b = w + i, L = pl.L0;
+    uint64_t Pb = P[b];
+    for (uint32_t k = 0; k < segr; ++k) {
+        out[(uint64_t)k * nc] = (uint32_t)b;
+        uint64_t Pe;
+        const uint64_t e = sp_step(P, K, PK, M, b, Pb, L, Pe);
+        if (e < K) L = e - b;
+        b = e;
+        Pb = Pe;
+    }
+    B.ends[s * nc + i] = (uint32_t)b;  // contiguous per segment: the stitch stages whole batches
+}
+
+constexpr int SPLIT_STITCH_THREADS = 256;
+constexpr uint32_t SPLIT_LDS_ENDS = 16384;  // segment ends staged per batch (64 KiB, two batches)
+constexpr uint32_t SPLIT_SB = 256;          // segments per batch at most
+
+// one workgroup: thread 0 follows the chain through batch j while waves 1-3 stage batch j + 1
+__global__ void __launch_bounds__(SPLIT_STITCH_THREADS)
+    k_split_stitch(const uint64_t* __restrict__ P, uint64_t M, SplitBufs B, uint64_t* run_b, uint64_t* n_runs_out) {
+    __shared__ uint32_t s_end[2][SPLIT_LDS_ENDS];
+    __shared__ uint64_t s_w[2][SPLIT_SB];
+    __shared__ uint32_t s_n[2][SPLIT_SB];
+    __shared__ uint64_t s_t;
+    __shared__ uint32_t s_done;
+    SplitPlan& pl = *B.plan;
+    if (pl.mode != SPLIT_PAR) return;
+    const uint64_t K = pl.K, PK = pl.PK;
+    const uint32_t segr = B.segr, nc = B.nc, nseg = pl.nseg;
+    const uint32_t sb = SPLIT_LDS_ENDS / nc < SPLIT_SB ? SPLIT_LDS_ENDS / nc : SPLIT_SB;  // segments per batch
+    const uint32_t nbatch = (nseg + sb - 1) / sb;
+    const int tid = threadIdx.x;
+    // batch j into buffer buf by threads t0, t0 + nt, ...: eight 16-byte loads in flight per thread
+    // (entries past a window's seg_n are copied but never read)
+    auto stage = [&](uint32_t j, int buf, uint32_t t0, uint32_t nt) {
+        const uint32_t s0 = j * sb, nb = nseg - s0 < sb ? nseg - s0 : sb;
+        for (uint32_t b = t0; b < nb; b += nt) {
+            s_w[buf][b] = B.seg_w[s0 + b];
+            s_n[buf][b] = B.seg_n[s0 + b];
+        }
+        const uint32_t cnt = nb * nc;
+        const uint32_t* src = B.ends + (uint64_t)s0 * nc;
+        uint32_t x0 = 0;
+        if ((nc & 3) == 0) {  // 16-byte aligned rows
+            const uint32_t n4 = cnt / 4;
+            const uint4* src4 = (const uint4*)src;
+            uint4* dst4 = (uint4*)s_end[buf];
+            for (uint32_t x = t0; x < n4; x += 8 * nt) {
+                uint4 r[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t y = x + u * nt;
+                    if (y < n4) r[u] = src4[y];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t y = x + u * nt;
+                    if (y < n4) dst4[y] = r[u];
+                }
+            }
+            x0 = n4 * 4;
+        }
+        for (uint32_t x = x0 + t0; x < cnt; x += nt) s_end[buf][x] = src[x];
+    };
+    if (tid == 0) {
+        s_t = 0;
+        s_done = 0;
+    }
+    stage(0, 0, tid, SPLIT_STITCH_THREADS);
+    __syncthreads();
+    uint64_t L = pl.L0;
+    uint32_t n_fb = 0, sel_count = 0;
+    uint32_t walked = 0;  // run starts the last walk_segment wrote
+    // the stitch's own walk of segment s from t (a start outside the window): writes run_b
+    auto walk_segment = [&](uint64_t s, uint64_t t) -> uint64_t {
+        uint64_t Pt = P[t];
+        walked = 0;
+        for (uint32_t k = 0; k < segr && t < K; ++k, ++walked) {
+            run_b[s * segr + k] = t;
+            uint64_t Pe;
+            const uint64_t e = sp_step(P, K, PK, M, t, Pt, L, Pe);
+            if (e < K) L = e - t;
+            t = e;
+            Pt = Pe;
+        }
+        return t;
+    };
+    // the chain ended within segment s (its next start is K): count its runs, close run_b
+    auto finish = [&](uint64_t s, bool by_walk, uint32_t ci) {
+        uint64_t m = s * segr;
+        if (by_walk) {
+            m += walked;
+        } else {
+            const uint32_t* ch = B.chain + s * (uint64_t)segr * nc + ci;
+            for (uint32_t k = 0; k < segr && ch[(uint64_t)k * nc] < K; ++k) ++m;
+        }
+        run_b[m] = K;
+        n_runs_out[0] = m;
+        n_runs_out[1] = K;
+        n_runs_out[2] = PK;
+    };
+    for (uint32_t j = 0; j < nbatch; ++j) {
+        const int buf = j & 1;
+        if (tid < 64) {
+            if (tid == 0 && !s_done) {
+                const uint32_t s0 = j * sb, nb = nseg - s0 < sb ? nseg - s0 : sb;
+                uint64_t t = s_t;
+                for (uint32_t b = 0; b < nb; ++b) {
+                    const uint64_t s = s0 + b;
+                    const uint64_t w = s_w[buf][b];
+                    const uint32_t n = s_n[buf][b];
+                    sel_count = (uint32_t)s + 1;
+                    bool by_walk = false;
+                    uint32_t ci = 0;
+                    if (t >= w && t - w < n) {
+                        ci = (uint32_t)(t - w);
+                        B.seg_sel[s] = ci;
+                        t = s_end[buf][b * nc + ci];
+                    } else {
+                        B.seg_sel[s] = SPLIT_FB;
+                        ++n_fb;
+                        by_walk = true;
+                        t = walk_segment(s, t);
+                    }
+                    if (t >= K) {
+                        finish(s, by_walk, ci);
+                        s_done = 1;
+                        break;
+                    }
+                }
+                s_t = t;
+            }
+        } else if (j + 1 < nbatch) {
+            stage(j + 1, buf ^ 1, tid - 64, SPLIT_STITCH_THREADS - 64);
+        }
+        __syncthreads();
+        if (s_done) break;
+    }
+    if (tid == 0) {
+        if (!s_done) {  // past the last window (more runs than the plan's bound: cannot happen)
+            uint64_t t = s_t;
+            for (uint64_t s = nseg;; ++s) {
+                t = walk_segment(s, t);
+                if (t >= K) {
+                    finish(s, true, 0);
+                    break;
+                }
+            }
+        }
+        pl.nseg_sel = sel_count;
+        pl.n_fb = n_fb;
+    }
+}
+
+// run_b[s * segr + k] = the chosen candidate's k-th run start (segments the stitch walked are written)
+__global__ void k_split_emit(SplitBufs B, uint64_t* run_b) {
+    const SplitPlan& pl = *B.plan;
+    if (pl.mode != SPLIT_PAR) return;
+    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t segr = B.segr;
+    const uint64_t s = x / segr, k = x % segr;
+    if (s >= pl.nseg_sel) return;
+    const uint32_t ci = B.seg_sel[s];
+    if (ci == SPLIT_FB) return;
+    const uint32_t v = B.chain[(s * segr + k) * B.nc + ci];
+    if (v < pl.K) run_b[x] = v;
 }
 
 __global__ void k_run_stats(const uint64_t* __restrict__ n_runs_p, const uint64_t* __restrict__ run_b,
@@ -2202,10 +2585,25 @@ hipError_t launch_tile(hipStream_t s, bool l0, const uint64_t* hi, const uint64_
 }
 void launch_chain(hipStream_t s, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, const uint32_t* tile_max,
                   uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs, uint32_t* tbl, uint64_t max_K,
-                  uint64_t max_bytes) {
+                  uint64_t max_bytes, const SplitBufs* sp) {
     const uint64_t n_tbl = tbl ? (max_bytes >> CH_SHIFT) + 2 : 0;
-    if (tbl) k_chain_table<<<blocks_for(max_K + 1, 256), 256, 0, s>>>(Kp, P, tbl, n_tbl);
-    k_chain<<<1, 64, 0, s>>>(Kp, P, max_size, tile_max, n_tiles, run_b, n_runs, tbl, n_tbl);
+    const SplitPlan* plan = nullptr;
+    if (sp && sp->nseg_cap) {
+        plan = sp->plan;
+        k_split_plan<<<1, SPLIT_PLAN_THREADS, 0, s>>>(Kp, P, max_size, tile_max, n_tiles, *sp);
+        k_split_guess<<<(sp->nseg_cap + SPLIT_GUESS_SEGS - 1) / SPLIT_GUESS_SEGS, 64, 0, s>>>(P, max_size, *sp);
+        k_split_scan<<<1, SPLIT_PLAN_THREADS, 0, s>>>(*sp);
+        const unsigned wb = sp->nc < 64 ? 64 : (sp->nc < 256 ? sp->nc : 256);
+        k_split_walk<<<sp->nseg_cap * ((sp->nc + wb - 1) / wb), wb, 0, s>>>(P, max_size, *sp);
+        k_split_stitch<<<1, SPLIT_STITCH_THREADS, 0, s>>>(P, max_size, *sp, run_b, n_runs);
+        k_split_emit<<<blocks_for((uint64_t)sp->nseg_cap * sp->segr, 256), 256, 0, s>>>(*sp, run_b);
+    }
+    if (tbl) {  // grid-stride (capped grid): with the parallel split it only reads the plan
+        unsigned tb = blocks_for(max_K + 1, 256);
+        if (tb > 8192) tb = 8192;
+        k_chain_table<<<tb, 256, 0, s>>>(Kp, P, tbl, n_tbl, plan);
+    }
+    k_chain<<<1, 64, 0, s>>>(Kp, P, max_size, tile_max, n_tiles, run_b, n_runs, tbl, n_tbl, plan);
 }
 uint64_t chain_table_entries(uint64_t max_bytes) { return (max_bytes >> CH_SHIFT) + 2; }
 void launch_run_stats(hipStream_t s, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,

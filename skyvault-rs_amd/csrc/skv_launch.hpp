@@ -52,7 +52,7 @@ hipError_t launch_tile(hipStream_t, bool l0, const uint64_t* hi, const uint64_t*
                        const uint32_t* poison);
 void launch_chain(hipStream_t, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, const uint32_t* tile_max,
                   uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs, uint32_t* tbl, uint64_t max_K,
-                  uint64_t max_bytes);
+                  uint64_t max_bytes, const SplitBufs* sp = nullptr);
 uint64_t chain_table_entries(uint64_t max_bytes);
 void launch_run_stats(hipStream_t, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
                       const uint64_t* Dp, const uint32_t* m_rec, const uint32_t* rec_klen, DevRunDesc* descs,
