@@ -741,7 +741,7 @@ __global__ void k_tile_n(const uint64_t* __restrict__ bounds, uint32_t k, uint64
 
 
 
-// LDS layout of k_tile (dynamic): el_lo[CAP] el_c[CAP] mhA[CAP] mhB[CAP] u64 | miA[CAP] miB[CAP] u16
+// LDS layout of k_tile (dynamic): hp[CAP] el_lo[CAP] el_c[CAP] el_fp[CAP] u64 | mi[CAP] posof[CAP] u16
 // | cbA[k+1] cbB[k+1] u32 | ws[16] u64 | flag
 __device__ __forceinline__ uint32_t seg_of(const uint32_t* cb, uint32_t m, uint32_t i) {
     uint32_t lo = 0, hi = m;  // last s in [0, m) with cb[s] <= i
@@ -753,13 +753,13 @@ __device__ __forceinline__ uint32_t seg_of(const uint32_t* cb, uint32_t m, uint3
     return lo;
 }
 
-// Output stage of a level > 0 LDS tile (sorted samples): position i has hi = mh[i] and element
+// Output stage of a level > 0 LDS tile (sorted samples): position i has hi = hp[i] and element
 // mi[i] (its lo and c in el_lo / el_c).
-__device__ void tile_output_samples(uint32_t n, const uint64_t* el_hi, const uint16_t* mi, const uint64_t* el_lo,
+__device__ void tile_output_samples(uint32_t n, const uint64_t* hp, const uint16_t* mi, const uint64_t* el_lo,
                                     const uint64_t* el_c, uint64_t base, const TileOut& O) {
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
         uint32_t e = mi[i];
-        O.ohi[base + i] = el_hi[e];
+        O.ohi[base + i] = hp[i];
         O.olo[base + i] = el_lo[e];
         O.oc[base + i] = el_c[e];
     }
@@ -965,17 +965,17 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                                                       const uint64_t* __restrict__ rec_addr, uint32_t drop_deletes,
                                                       TileOut O) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    // by element id (= load position): key prefix, length | record, fingerprint of the bytes past
-    // 16. The merge rounds reach them through the id at a merged position, so a prefix tie reads
-    // the fingerprint from LDS (it was a global load per tie: at config 3 a third of the records
-    // share their key with another stream, and the ties kept the rounds waiting on HBM)
-    uint64_t* el_hi = (uint64_t*)smem;
-    uint64_t* el_lo = el_hi + TILE_CAP;
+    // hp / mi: key bytes 0..7 and element id by merged position (permuted each merge round). By
+    // element id (= load position): key bytes 8..15, length | record, fingerprint of the bytes
+    // past 16, read on a prefix tie (at config 3 a third of the records share their key with
+    // another stream: the fingerprint decides those without reading record bytes)
+    uint64_t* hp = (uint64_t*)smem;
+    uint64_t* el_lo = hp + TILE_CAP;
     uint64_t* el_c = el_lo + TILE_CAP;
     uint64_t* el_fp = el_c + TILE_CAP;
-    uint16_t* miA = (uint16_t*)(el_fp + TILE_CAP);  // element id by merged position (ping-pong)
-    uint16_t* miB = miA + TILE_CAP;
-    uint32_t* cbA = (uint32_t*)(miB + TILE_CAP);
+    uint16_t* mi = (uint16_t*)(el_fp + TILE_CAP);
+    uint16_t* posof = mi + TILE_CAP;  // after the rounds: merged position of each element
+    uint32_t* cbA = (uint32_t*)(posof + TILE_CAP);
     uint32_t* cbB = cbA + (k + 1);
     uint64_t* ws = (uint64_t*)(((uintptr_t)(cbB + (k + 1)) + 15) & ~(uintptr_t)15);
     uint32_t* s_flag = (uint32_t*)(ws + 16);
@@ -1024,18 +1024,17 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         }
         return;
     }
-    // Thread owns elements e = threadIdx.x + u*TILE_THREADS; key, position and segment stay in
-    // registers across the merge rounds, so each round is one binary search + one LDS write.
+    // Thread owns elements e = threadIdx.x + u*TILE_THREADS for the loads (payload stays in
+    // registers) and output positions threadIdx.x * PER + q in the merge rounds.
     constexpr int PER = TILE_CAP / TILE_THREADS;
-    uint64_t rh[PER], rc[PER], raddr[PER];  // key bytes 8..15 and the fingerprint stay in LDS (read on a tie)
-    uint32_t rpos[PER], rseg[PER], rmeta[PER];
+    uint64_t rh[PER], rc[PER], raddr[PER];
+    uint32_t rpos[PER], rmeta[PER];
     const uint64_t* kfp = L0 ? O.key_fp : nullptr;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         uint32_t e = threadIdx.x + u * TILE_THREADS;
         rh[u] = rc[u] = raddr[u] = 0;
         rpos[u] = e;
-        rseg[u] = 0;
         rmeta[u] = 0;
         if (e < n) {
             uint32_t j = seg_of(cbA, k + 1, e);
@@ -1047,84 +1046,120 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                 raddr[u] = (O.pay_addr ? O.pay_addr : rec_addr)[pos];  // coalesced here, not gathered later
                 if (kfp) fp = kfp[pos];
             }
-            rseg[u] = j;
-            el_hi[e] = rh[u];
+            hp[e] = rh[u];
             el_lo[e] = lo;
             el_c[e] = rc[u];
             el_fp[e] = fp;
-            miA[e] = (uint16_t)e;
+            mi[e] = (uint16_t)e;
         }
     }
     __syncthreads();
     TPROF(1);
-    // pairwise merge rounds: each element finds its rank in the partner segment
-    uint32_t m = k;
-    uint32_t* cb = cbA;
-    uint32_t* cbn = cbB;
-    uint16_t* mi = miA;
-    uint16_t* min_ = miB;
-    while (m > 1) {
-        // count, for each element, the partner segment's elements that order before it: the PER
-        // binary searches of a thread run in lockstep (one LDS read of each per step -> ILP)
-        uint32_t sb[PER], sn[PER];
-        uint32_t maxn = 0;
+    // merge-path rounds over pairs of adjacent segments (the key order is strict: c holds the
+    // record index): each thread produces PER consecutive outputs of a round with ONE merge-path
+    // search, then a sequential merge. A compare reads the two prefixes by position, the ids and
+    // by-id words only on a prefix tie.
+    auto less_hx = [&](uint64_t ha, uint32_t xa, uint64_t hb, uint32_t xb) -> bool {
+        if (ha != hb) return ha < hb;
+        return L0 ? elem_less_fp(kfp != nullptr, el_fp[xa], rec_addr, ha, el_lo[xa], el_c[xa], hb, el_lo[xb],
+                                 el_c[xb], el_fp[xb])
+                  : elem_less(rec_addr, ha, el_lo[xa], el_c[xa], hb, el_lo[xb], el_c[xb]);
+    };
+    {
+        const uint32_t o0 = threadIdx.x * PER;
+        uint32_t m = k;
+        uint32_t* cb = cbA;
+        uint32_t* cbn = cbB;
+        while (m > 1) {
+            const uint32_t mp = (m + 1) >> 1;
+            uint64_t oh[PER];
+            uint32_t ox[PER];
+            uint32_t pos = o0, ia = 0, a1 = 0, ib = 0, b1 = 0, xA = 0, xB = 0;
+            uint64_t hA = 0, hB = 0;
+            bool setup = true;
 #pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const uint32_t e = threadIdx.x + u * TILE_THREADS;
-            const uint32_t ps = rseg[u] ^ 1u;
-            sb[u] = 0;
-            sn[u] = 0;
-            if (e < n && ps < m) {
-                sb[u] = cb[ps];
-                sn[u] = cb[ps + 1] - sb[u];
-                maxn = sn[u] > maxn ? sn[u] : maxn;
-            }
-        }
-        for (; maxn; maxn >>= 1) {  // every step at least halves each remaining range
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                if (sn[u]) {
-                    const uint32_t half = sn[u] >> 1, mid = sb[u] + half;
-                    const uint32_t x = mi[mid];
-                    const uint64_t xh = el_hi[x];
-                    bool less = xh < rh[u];
-                    if (xh == rh[u]) {
-                        const uint32_t me = threadIdx.x + u * TILE_THREADS;
-                        less = L0 ? elem_less_fp(kfp != nullptr, el_fp[x], rec_addr, xh, el_lo[x], el_c[x], rh[u],
-                                                 el_lo[me], rc[u], el_fp[me])
-                                  : elem_less(rec_addr, xh, el_lo[x], el_c[x], rh[u], el_lo[me], rc[u]);
+            for (int q = 0; q < PER; ++q) {
+                oh[q] = 0;
+                ox[q] = 0;
+                if (pos < n) {
+                    if (setup || pos >= b1) {
+                        uint32_t lo = 0, hi = mp;  // pair p with cb[2p] <= pos
+                        while (hi - lo > 1) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (cb[2 * mid] <= pos) lo = mid;
+                            else hi = mid;
+                        }
+                        const uint32_t a0 = cb[2 * lo];
+                        a1 = cb[2 * lo + 1 < m ? 2 * lo + 1 : m];
+                        b1 = cb[2 * lo + 2 < m ? 2 * lo + 2 : m];
+                        const uint32_t lenA = a1 - a0, lenB = b1 - a1, d = pos - a0;
+                        uint32_t l = d > lenB ? d - lenB : 0, h = d < lenA ? d : lenA;
+                        while (l < h) {  // how many of the first d outputs come from A
+                            const uint32_t mid = (l + h) >> 1;
+                            const uint32_t pa = a0 + mid, pb = a1 + d - mid - 1;
+                            const uint64_t ha = hp[pa], hb = hp[pb];
+                            const bool lt = ha != hb ? ha < hb : less_hx(ha, mi[pa], hb, mi[pb]);
+                            if (lt) l = mid + 1;
+                            else h = mid;
+                        }
+                        ia = a0 + l;
+                        ib = a1 + (d - l);
+                        if (ia < a1) {
+                            hA = hp[ia];
+                            xA = mi[ia];
+                        }
+                        if (ib < b1) {
+                            hB = hp[ib];
+                            xB = mi[ib];
+                        }
+                        setup = false;
                     }
-                    if (less) {
-                        sb[u] = mid + 1;
-                        sn[u] -= half + 1;
+                    const bool takeA = ia < a1 && (ib >= b1 || less_hx(hA, xA, hB, xB));
+                    if (takeA) {
+                        oh[q] = hA;
+                        ox[q] = xA;
+                        if (++ia < a1) {
+                            hA = hp[ia];
+                            xA = mi[ia];
+                        }
                     } else {
-                        sn[u] = half;
+                        oh[q] = hB;
+                        ox[q] = xB;
+                        if (++ib < b1) {
+                            hB = hp[ib];
+                            xB = mi[ib];
+                        }
                     }
+                    ++pos;
                 }
             }
-        }
+            __syncthreads();  // every thread has read its inputs of this round
 #pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const uint32_t e = threadIdx.x + u * TILE_THREADS;
-            if (e < n) {
-                const uint32_t s = rseg[u], ps = s ^ 1u;
-                uint32_t newpos = rpos[u];
-                if (ps < m) newpos = cb[s & ~1u] + (rpos[u] - cb[s]) + (sb[u] - cb[ps]);
-                min_[newpos] = (uint16_t)e;
-                rpos[u] = newpos;
-                rseg[u] = s >> 1;
+            for (int q = 0; q < PER; ++q) {
+                if (o0 + q < n) {
+                    hp[o0 + q] = oh[q];
+                    mi[o0 + q] = (uint16_t)ox[q];
+                }
+            }
+            for (uint32_t p = threadIdx.x; p <= mp; p += blockDim.x) cbn[p] = p < mp ? cb[2 * p] : cb[m];
+            __syncthreads();
+            uint32_t* tp = cb;
+            cb = cbn;
+            cbn = tp;
+            m = mp;
+        }
+        if (L0) {  // each element's merged position (its payload stays in the loading thread)
+            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) posof[mi[i]] = (uint16_t)i;
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const uint32_t e = threadIdx.x + u * TILE_THREADS;
+                if (e < n) rpos[u] = posof[e];
             }
         }
-        __syncthreads();
-        uint32_t mn = (m + 1) >> 1;
-        for (uint32_t p = threadIdx.x; p <= mn; p += blockDim.x) cbn[p] = p < mn ? cb[2 * p] : cb[m];
-        __syncthreads();
-        { uint16_t* tp = mi; mi = min_; min_ = tp; }
-        { uint32_t* tp = cb; cb = cbn; cbn = tp; }
-        m = mn;
     }
     if (!L0) {
-        tile_output_samples(n, el_hi, mi, el_lo, el_c, base, O);
+        tile_output_samples(n, hp, mi, el_lo, el_c, base, O);
         return;
     }
     TPROF(2);
@@ -1154,7 +1189,7 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                 if (i > 0) first = act_key_cmp(O, (uint32_t)el_c[mi[i - 1]], (uint32_t)c) != 0;
             } else if (i > 0) {
                 const uint32_t p = mi[i - 1];
-                if (el_hi[p] == el_hi[e]) {
+                if (hp[i - 1] == hp[i]) {
                     const uint64_t lp = el_lo[p], le = el_lo[e], cp = el_c[p];
                     int kc = lp != le ? (lp < le ? -1 : 1) : 0;
                     const uint32_t kp = (uint32_t)(cp >> 32), ke = (uint32_t)(c >> 32);
@@ -1186,8 +1221,8 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     }
     __syncthreads();
     TPROF(3);
-    // (b) source address and meta by final position (el_hi / el_lo are free now)
-    uint64_t* paddr = el_hi;
+    // (b) source address and meta by final position (hp / el_lo are free now)
+    uint64_t* paddr = hp;
     uint32_t* pmeta = (uint32_t*)el_lo;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
