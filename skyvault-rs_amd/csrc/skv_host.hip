@@ -1277,7 +1277,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     if (!parsed) {
         // record starts of each chunk as the walks find them (16-bit offsets), chunk / 64 per chunk:
         // k_emit parses the records of a chunk in parallel instead of walking its chain again
-        const uint32_t slot_cap = (uint32_t)(chunk / 64);
+        const uint32_t slot_cap = (uint32_t)((chunk / 64 + 7) & ~7ull);  // rows of 16-byte groups (walk_fast)
         uint16_t* ch_slots = dbuf<uint16_t>(ctx, "ch_slots", n_chunks * slot_cap);
         HIPCHK(hipMemsetAsync(bad_bits, 0, (n_chunks / 64 + 1) * 8, st));
         HIPCHK(hipMemsetAsync(first_bad, 0xFF, n_runs * 4, st));
