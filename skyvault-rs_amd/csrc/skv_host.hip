@@ -865,7 +865,7 @@ static SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth
         uint64_t* start = dbuf<uint64_t>(ctx, nm, 2);
         const uint64_t h[2] = {0, n};
         h2d_up(ctx, start, h, 16);
-        launch_sort_tile(st, E, start, nullptr, 1, T, newkey);
+        launch_sort_tile(st, E, start, nullptr, 1, T, newkey, false);
         return T;
     }
     const uint64_t Ns = (n + SORT_EVERY - 1) / SORT_EVERY;
@@ -890,10 +890,14 @@ static SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth
     HIPCHK(hipMemsetAsync(cnt, 0, (Tb + 1) * 8, st));
     snprintf(nm, sizeof nm, "sort_split%d", depth);
     uint8_t* split_buf = dbuf<uint8_t>(ctx, nm, sort_split_bytes(Tb - 1));
-    launch_sort_bucket(st, E, n, Ss, SORT_OV, Tb - 1, split_buf, cnt, bs);
+    // depth 0 (the records themselves): the bucket search stores each element's window from its
+    // bucket's common prefix on, so the bucket sort reads no record bytes; its output keeps only
+    // addr / pos / klen meaningful (sort_records reads no more). Sample levels keep their keys.
+    const bool pre = depth == 0;
+    launch_sort_bucket(st, E, n, Ss, SORT_OV, Tb - 1, split_buf, cnt, bs, pre ? L : nullptr);
     launch_scan(st, cnt, Tb, start, scan_tmp);
     launch_sort_scatter(st, E, n, bs, start, T);
-    launch_sort_tile(st, T, start, L, Tb, E, newkey);
+    launch_sort_tile(st, T, start, L, Tb, E, newkey, pre);
     return E;
 }
 

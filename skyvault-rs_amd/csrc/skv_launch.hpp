@@ -120,13 +120,13 @@ void launch_sort_store(hipStream_t, uint64_t R, const SElem* E, const uint32_t* 
                        uint32_t* cmp_klen, uint32_t* meta, bool last_wins);
 void launch_sort_sample(hipStream_t, const SElem* E, uint64_t n, uint64_t Ns, SElem* S);
 void launch_sort_prefix(hipStream_t, const SElem* Ss, uint64_t ov, uint64_t Tb, uint32_t* L);
-void launch_sort_bucket(hipStream_t, const SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
-                        void* split_buf, uint64_t* cnt, uint64_t* bs);
+void launch_sort_bucket(hipStream_t, SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
+                        void* split_buf, uint64_t* cnt, uint64_t* bs, const uint32_t* Lb);
 size_t sort_split_bytes(uint64_t nsp);
 void launch_sort_scatter(hipStream_t, const SElem* E, uint64_t n, const uint64_t* bs, const uint64_t* start,
                          SElem* out);
 void launch_sort_tile(hipStream_t, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out,
-                      uint64_t* newkey);
+                      uint64_t* newkey, bool pre);
 // skv_search.hip — batched run lookups
 void launch_search_bsearch(hipStream_t, const uint8_t* run, uint64_t len, uint64_t R, const uint64_t* rec_addr,
                            const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,

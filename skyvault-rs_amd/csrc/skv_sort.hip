@@ -180,6 +180,35 @@ __global__ void k_sort_splitters(const SElem* __restrict__ Ss, uint64_t ov, uint
     win[b] = SWin{o.hi, o.lo, o.x0, o.x1};
 }
 
+// The 8 key bytes from byte c on, big-endian, zero past the key's end.
+__device__ __forceinline__ uint64_t sk_word8(const uint8_t* key, uint32_t klen, uint32_t c) {
+    if (klen <= c) return 0;
+    const uint32_t m = klen - c < 8 ? klen - c : 8;
+    const uint4 v = load_window16(key + c, m);
+    return ((uint64_t)__builtin_bswap32(v.x & dword_mask(0, m, 0)) << 32) | __builtin_bswap32(v.y & dword_mask(0, m, 1));
+}
+
+// Group discriminators for the bucket search's global level. Group g holds splitters
+// [g top, (g + 1) top - 1), searched after the LDS level has placed a key x strictly after
+// boundary splitter g top - 1 and at or before boundary (g + 1) top - 1. Both boundaries share
+// their first cp[g] bytes, so x and every splitter of the group share them too (a key that
+// differed inside that prefix, or ended in it, would order outside the two boundaries).
+// disc[j] = splitter j's 8 key bytes from cp[g] on: where disc differs from x's 8 bytes at cp[g],
+// the zero-padded words order as the keys do (the windows' argument), so one 8-byte read decides
+// the step and the 32-byte window is read only on a tie.
+__global__ void k_sort_disc(const SElem* __restrict__ Ss, uint64_t ov, uint64_t nsp, uint64_t top, uint32_t* cp,
+                            uint64_t* disc) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nsp) return;
+    const uint64_t g = j / top, nt = nsp / top;
+    uint32_t c = 0;
+    if (g > 0 && g < nt) c = sk_common(Ss[(g * top) * ov - 1], Ss[((g + 1) * top) * ov - 1]);
+    if (j % top == 0) cp[g] = c;
+    if (j + 1 == nsp && (j + 1) % top == 0) cp[g + 1] = 0;  // a last, empty group
+    const SElem e = Ss[(j + 1) * ov - 1];
+    disc[j] = sk_word8(sk_key(e), e.klen, c);
+}
+
 // splitter vs element key order (<0, 0, >0)
 __device__ __forceinline__ int sk_scmp(const SSplit& a, const SElem& b, uint64_t bx0, uint64_t bx1) {
     if (a.hi != b.hi) return a.hi < b.hi ? -1 : 1;
@@ -214,10 +243,16 @@ __device__ __forceinline__ bool sk_sbefore(const SWin& w, const SSplit* __restri
 // table (32 B per splitter: 3.4 MB at config 5's 10^5 splitters, L2-resident, where the 48-byte
 // SSplit table was not). Both levels are branch-free power-of-two searches with a step count
 // uniform over the wave, run for SB_ILP elements at once so their loads overlap.
+// With Lb (the buckets' common prefix lengths), each element's (hi, lo) is replaced in place by
+// its 16-byte window from byte Lb[bucket] on, read here while the record's key line is in cache
+// (elements are in record order): the bucket sort then reads no record bytes, where it used to
+// load one window per element from a record at random (~250 B of HBM lines per element).
 constexpr int SB_THREADS = 256, SB_PER = 16, SB_TOP = 1024, SB_ILP = 4;
-__global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restrict__ E, uint64_t n,
+__global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n, const uint32_t* __restrict__ Lb,
                                                             const SSplit* __restrict__ sp,
                                                             const SWin* __restrict__ win, uint64_t nsp, uint64_t top,
+                                                            const uint32_t* __restrict__ gcp,
+                                                            const uint64_t* __restrict__ disc,
                                                             unsigned long long* cnt, uint64_t* bs) {
     __shared__ SWin tt[SB_TOP];
     const uint32_t nt = (uint32_t)(nsp / top);  // top entry j = splitter (j + 1) * top - 1
@@ -231,7 +266,7 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restr
     const uint64_t base = (uint64_t)blockIdx.x * SB_THREADS * SB_PER;
     for (int u0 = 0; u0 < SB_PER; u0 += SB_ILP) {
         SElem x[SB_ILP];
-        uint64_t x0[SB_ILP], x1[SB_ILP], g[SB_ILP], len[SB_ILP], c[SB_ILP];
+        uint64_t x0[SB_ILP], x1[SB_ILP], g[SB_ILP], len[SB_ILP], c[SB_ILP], dx[SB_ILP];
         uint32_t a[SB_ILP];
         bool live[SB_ILP];
 #pragma unroll
@@ -260,13 +295,16 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restr
             g[u] = (uint64_t)a[u] * top;
             len[u] = a[u] < nt ? top - 1 : nsp - (uint64_t)nt * top;
             c[u] = 0;
+            dx[u] = len[u] ? sk_word8(sk_key(x[u]), x[u].klen, gcp[a[u]]) : 0;
         }
         for (uint64_t st = top >> 1; st; st >>= 1) {
 #pragma unroll
             for (int u = 0; u < SB_ILP; ++u) {
                 const uint64_t p = c[u] + st;
                 if (p <= len[u]) {
-                    const bool before = sk_sbefore(win[g[u] + p - 1], sp, g[u] + p - 1, x[u], x0[u], x1[u]);
+                    const uint64_t j = g[u] + p - 1, dj = disc[j];
+                    const bool before =
+                        dj != dx[u] ? dj < dx[u] : sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u]);
                     if (before) c[u] = p;
                 }
             }
@@ -278,6 +316,14 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restr
             const uint64_t b = g[u] + c[u];
             const uint64_t slot = atomicAdd(cnt + b, 1ull);
             bs[i] = (b << 32) | slot;
+            if (Lb) {
+                const uint32_t L = Lb[b];
+                if (L) {
+                    SElem e = x[u];
+                    sk_window(x[u], L, e.hi, e.lo);
+                    E[i] = e;
+                }
+            }
         }
     }
 }
@@ -312,51 +358,103 @@ __device__ __forceinline__ bool sk_wless(const SKey& a, const SKey& b, const SEl
 // One workgroup per bucket: in[start[b], start[b+1]) sorted into out[...]. Bitonic network in
 // the ascending-comparator form (the second element of the first step of each merge is mirrored),
 // so padding past n acts as +inf and is never touched.
+// pre: the elements' (hi, lo) already hold their windows from byte L on (k_sort_bucket with Lb).
+__device__ __forceinline__ SKey sk_skey(const SElem& e, uint32_t L, bool pre) {
+    SKey k;
+    if (pre) {
+        k.wh = e.hi;
+        k.wl = e.lo;
+    } else {
+        sk_window(e, L, k.wh, k.wl);
+    }
+    k.klen = e.klen;
+    k.pos = e.pos;
+    return k;
+}
+// equal keys, given equal first L bytes (the bucket's common prefix)
+__device__ __forceinline__ bool sk_wsame(const SKey& a, const SKey& c, const SElem& ea, const SElem& ec, uint32_t L) {
+    if (a.wh != c.wh || a.wl != c.wl || a.klen != c.klen) return false;
+    return c.klen <= L + 16 || bytes_cmp16(sk_key(ea) + L + 16, sk_key(ec) + L + 16, c.klen - L - 16) == 0;
+}
+
+// The bucket sorted in global memory, in place (bitonic on the full order), then copied out:
+// buckets above SORT_CAP, and LDS sorts that found a long run of equal first words.
+__device__ void sk_sort_global(SElem* bk, uint64_t n, uint32_t L, bool pre, SElem* out, uint64_t s0,
+                               uint64_t* newkey) {
+    uint64_t P = 1;
+    while (P < n) P <<= 1;
+    for (uint64_t kk = 2; kk <= P; kk <<= 1) {
+        for (uint64_t jj = kk >> 1; jj >= 1; jj >>= 1) {
+            for (uint64_t i = threadIdx.x; i < P / 2; i += blockDim.x) {
+                const uint64_t blk = i / jj, off = i % jj;
+                const bool first = jj == (kk >> 1);
+                const uint64_t a = first ? blk * kk + off : blk * 2 * jj + off;
+                const uint64_t c = first ? blk * kk + kk - 1 - off : a + jj;
+                bool sw = false;
+                if (c < n) {
+                    if (pre) {
+                        const SKey kc = sk_skey(bk[c], L, true), ka = sk_skey(bk[a], L, true);
+                        sw = sk_wless(kc, ka, bk, (uint32_t)c, (uint32_t)a, L);
+                    } else {
+                        sw = sk_less(bk[c], bk[a]);
+                    }
+                }
+                if (sw) {
+                    const SElem t = bk[a];
+                    bk[a] = bk[c];
+                    bk[c] = t;
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+    }
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        out[s0 + i] = bk[i];
+        if (newkey) {
+            bool nk = i == 0;
+            if (!nk && pre) nk = !sk_wsame(sk_skey(bk[i - 1], L, true), sk_skey(bk[i], L, true), bk[i - 1], bk[i], L);
+            else if (!nk) nk = sk_kcmp(bk[i - 1], bk[i]) != 0;
+            newkey[s0 + i] = nk ? 1 : 0;
+        }
+    }
+}
+
+// full bucket order of elements x and y (indices into the bucket)
+__device__ __forceinline__ bool sk_eless(const SElem* bk, uint32_t x, uint32_t y, uint32_t L, bool pre) {
+    return sk_wless(sk_skey(bk[x], L, pre), sk_skey(bk[y], L, pre), bk, x, y, L);
+}
+
+constexpr uint32_t SORT_TIE_MAX = 32;  // longest run of equal first words sorted by one thread
+
+// One workgroup per bucket: in[start[b], start[b+1]) sorted into out[...]. The bitonic network
+// runs on the first 8 window bytes (kw) and the element ids only, 10 bytes per element where the
+// full window, length and index took 26: the sort is bound by LDS traffic. Runs of equal kw are
+// then put in the full order (window, bytes past it, key length, record index) by the thread
+// holding the run's first position (insertion sort, elements read from the bucket in HBM/L2); a
+// run longer than SORT_TIE_MAX sends the bucket to the global-memory sort instead.
+// The network is the ascending-comparator form (the second element of the first step of each
+// merge is mirrored), so padding past n acts as +inf and is never touched.
 __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uint64_t* __restrict__ start,
                                                             const uint32_t* __restrict__ Lb, uint64_t Tb,
-                                                            SElem* out, uint64_t* newkey) {
-    __shared__ SKey key[SORT_CAP];
+                                                            SElem* out, uint64_t* newkey, bool pre) {
+    __shared__ uint64_t kw[SORT_CAP];
     __shared__ uint16_t id[SORT_CAP];
+    __shared__ uint32_t s_long;
     const uint64_t b = blockIdx.x;
     if (b >= Tb) return;
     const uint64_t s0 = start[b], n = start[b + 1] - s0;
     const uint32_t L = Lb ? Lb[b] : 0u;
     SElem* bk = in + s0;
     if (n == 0) return;
-    if (n > (uint64_t)SORT_CAP) {  // global-memory bitonic sort on the full order, then copy
-        uint64_t P = 1;
-        while (P < n) P <<= 1;
-        for (uint64_t kk = 2; kk <= P; kk <<= 1) {
-            for (uint64_t jj = kk >> 1; jj >= 1; jj >>= 1) {
-                for (uint64_t i = threadIdx.x; i < P / 2; i += blockDim.x) {
-                    const uint64_t blk = i / jj, off = i % jj;
-                    const bool first = jj == (kk >> 1);
-                    const uint64_t a = first ? blk * kk + off : blk * 2 * jj + off;
-                    const uint64_t c = first ? blk * kk + kk - 1 - off : a + jj;
-                    if (c < n && sk_less(bk[c], bk[a])) {
-                        const SElem t = bk[a];
-                        bk[a] = bk[c];
-                        bk[c] = t;
-                    }
-                }
-                __threadfence_block();
-                __syncthreads();
-            }
-        }
-        for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
-            out[s0 + i] = bk[i];
-            if (newkey) newkey[s0 + i] = (i == 0 || sk_kcmp(bk[i - 1], bk[i]) != 0) ? 1 : 0;
-        }
+    if (n > (uint64_t)SORT_CAP) {
+        sk_sort_global(bk, n, L, pre, out, s0, newkey);
         return;
     }
     const uint32_t n32 = (uint32_t)n;
+    if (threadIdx.x == 0) s_long = 0;
     for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
-        const SElem e = bk[i];
-        SKey k;
-        sk_window(e, L, k.wh, k.wl);
-        k.klen = e.klen;
-        k.pos = e.pos;
-        key[i] = k;
+        kw[i] = sk_skey(bk[i], L, pre).wh;
         id[i] = (uint16_t)i;
     }
     __syncthreads();
@@ -365,34 +463,71 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
         P <<= 1;
         ++lp;
     }
+    // A stage with jj <= 64 pairs elements inside one 128-element chunk, and compare-exchange i
+    // touches chunk i / 64, which is always handled by the same wave (i = threadIdx.x + m *
+    // SORT_THREADS). Those stages need no workgroup barrier: a wave's LDS operations complete in
+    // issue order, so only the stages with jj >= 128 are bracketed by __syncthreads (55 -> 9
+    // barriers for a 1024-element bucket).
+    static_assert(SORT_THREADS % 64 == 0, "whole waves per workgroup");
+    bool local_last = false;
     for (uint32_t lk = 1; lk <= lp; ++lk) {
         for (int lj = (int)lk - 1; lj >= 0; --lj) {
+            const bool wide = lj >= 6 + 1;
+            if (wide && local_last) __syncthreads();
             for (uint32_t i = threadIdx.x; i < P / 2; i += blockDim.x) {
                 uint32_t a, c;
                 bitonic_pair(i, lk, (uint32_t)lj, a, c);
                 if (c < n32) {
-                    const SKey ka = key[a], kc = key[c];
-                    const uint32_t ia = id[a], ic = id[c];
-                    if (sk_wless(kc, ka, bk, ic, ia, L)) {
-                        key[a] = kc;
-                        key[c] = ka;
-                        id[a] = (uint16_t)ic;
-                        id[c] = (uint16_t)ia;
+                    const uint64_t ka = kw[a], kc = kw[c];
+                    if (kc < ka) {
+                        const uint16_t ia = id[a], ic = id[c];
+                        kw[a] = kc;
+                        kw[c] = ka;
+                        id[a] = ic;
+                        id[c] = ia;
                     }
                 }
             }
-            __syncthreads();
+            if (wide) __syncthreads();
+            else __builtin_amdgcn_wave_barrier();
+            local_last = !wide;
         }
     }
+    if (local_last) __syncthreads();
+    // runs of equal kw into the full order
     for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
-        out[s0 + i] = bk[id[i]];
+        const uint64_t w = kw[i];
+        if ((i == 0 || kw[i - 1] != w) && i + 1 < n32 && kw[i + 1] == w) {
+            uint32_t e = i + 2;
+            while (e < n32 && kw[e] == w && e - i <= SORT_TIE_MAX) ++e;
+            if (e - i > SORT_TIE_MAX) {
+                s_long = 1;
+            } else {
+                for (uint32_t t = i + 1; t < e; ++t) {
+                    const uint32_t x = id[t];
+                    uint32_t j = t;
+                    while (j > i && sk_eless(bk, x, id[j - 1], L, pre)) {
+                        id[j] = id[j - 1];
+                        --j;
+                    }
+                    id[j] = (uint16_t)x;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (s_long) {  // uniform: every thread read it after the barrier
+        sk_sort_global(bk, n, L, pre, out, s0, newkey);
+        return;
+    }
+    for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
+        const uint32_t c = id[i];
+        out[s0 + i] = bk[c];
         if (newkey) {  // a key differing from its predecessor's (buckets never share a key)
-            bool nk = i == 0;
+            bool nk = i == 0 || kw[i - 1] != kw[i];
             if (!nk) {
-                const SKey a = key[i - 1], c = key[i];
-                nk = a.wh != c.wh || a.wl != c.wl || a.klen != c.klen;
-                if (!nk && c.klen > L + 16)
-                    nk = bytes_cmp16(sk_key(bk[id[i - 1]]) + L + 16, sk_key(bk[id[i]]) + L + 16, c.klen - L - 16) != 0;
+                const uint32_t a = id[i - 1];
+                nk = !sk_wsame(sk_skey(bk[a], L, pre), sk_skey(bk[c], L, pre), bk[a], bk[c], L);
             }
             newkey[s0 + i] = nk ? 1 : 0;
         }
@@ -418,25 +553,32 @@ void launch_sort_sample(hipStream_t s, const SElem* E, uint64_t n, uint64_t Ns, 
 void launch_sort_prefix(hipStream_t s, const SElem* Ss, uint64_t ov, uint64_t Tb, uint32_t* L) {
     if (Tb) k_sort_prefix<<<sk_blocks(Tb), 256, 0, s>>>(Ss, ov, Tb, L);
 }
-void launch_sort_bucket(hipStream_t s, const SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
-                        void* split_buf, uint64_t* cnt, uint64_t* bs) {
+void launch_sort_bucket(hipStream_t s, SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
+                        void* split_buf, uint64_t* cnt, uint64_t* bs, const uint32_t* Lb) {
     SSplit* sp = (SSplit*)split_buf;
     SWin* win = (SWin*)(sp + nsp + 1);
-    if (nsp) k_sort_splitters<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, sp, win);
+    uint64_t* disc = (uint64_t*)(win + nsp + 1);
+    uint32_t* gcp = (uint32_t*)(disc + nsp + 1);
     uint64_t top = 1;  // a power of two: the global search level is a full power-of-two search
     while (nsp / top > (uint64_t)SB_TOP) top <<= 1;
+    if (nsp) {
+        k_sort_splitters<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, sp, win);
+        k_sort_disc<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, top, gcp, disc);
+    }
     const uint64_t per_wg = (uint64_t)SB_THREADS * SB_PER;
-    if (n) k_sort_bucket<<<(unsigned)((n + per_wg - 1) / per_wg), SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top,
+    if (n) k_sort_bucket<<<(unsigned)((n + per_wg - 1) / per_wg), SB_THREADS, 0, s>>>(E, n, Lb, sp, win, nsp, top, gcp, disc,
                                                                                      (unsigned long long*)cnt, bs);
 }
-size_t sort_split_bytes(uint64_t nsp) { return (size_t)(nsp + 1) * (sizeof(SSplit) + sizeof(SWin)); }
+size_t sort_split_bytes(uint64_t nsp) {
+    return (size_t)(nsp + 1) * (sizeof(SSplit) + sizeof(SWin) + sizeof(uint64_t)) + (size_t)(nsp + 2) * sizeof(uint32_t);
+}
 void launch_sort_scatter(hipStream_t s, const SElem* E, uint64_t n, const uint64_t* bs, const uint64_t* start,
                          SElem* out) {
     if (n) k_sort_scatter<<<sk_blocks(n), 256, 0, s>>>(E, n, bs, start, out);
 }
 void launch_sort_tile(hipStream_t s, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out,
-                      uint64_t* newkey) {
-    if (Tb) k_sort_tile<<<(unsigned)Tb, SORT_THREADS, 0, s>>>(in, start, L, Tb, out, newkey);
+                      uint64_t* newkey, bool pre) {
+    if (Tb) k_sort_tile<<<(unsigned)Tb, SORT_THREADS, 0, s>>>(in, start, L, Tb, out, newkey, pre);
 }
 
 }  // namespace skv

@@ -128,6 +128,24 @@ def test_fan_in_long_shared_prefixes(dev):
     _check(dev, streams, 1 << 16, 0)
 
 
+def test_fan_in_tie_runs_past_the_first_word(dev):
+    """The bucket sort orders 8-byte words first: keys whose words tie and which differ only
+    later (runs of 2-40 equal words, some past SORT_TIE_MAX -> the global-memory bucket sort),
+    duplicates across streams, and keys that are prefixes of others inside one tie run."""
+    r = random.Random(21)
+    streams = []
+    for s in range(1700):
+        ks = set()
+        for _ in range(r.randint(1, 6)):
+            grp = r.randrange(60)
+            head = f"g{grp:04d}-" + "x" * (grp % 9)
+            ks.add((head + "".join(r.choice("pq") for _ in range(r.randint(0, 6 + grp % 5)))).encode())
+        ops = [fmt.put(k, s.to_bytes(2, "big")) if r.random() < 0.9 else fmt.delete(k) for k in sorted(ks)]
+        streams.append((3 * s + 1, [fmt.encode_run(ops)]))
+    _check(dev, streams, 1 << 15, 0)
+    _check(dev, streams, 1 << 15, _abi.SKV_DROP_TOMBSTONES)
+
+
 def test_fan_in_errors_surface_like_the_reference(dev):
     """A corrupt or unsorted stream among 1600: the error is resolved before the sort."""
     r = random.Random(3)
