@@ -189,7 +189,12 @@ static void stage_copy(void* dst, const void* src, size_t bytes) {
     const char* pe = getenv("SKV_PAR_COPY_MIN");  // tests: split small tables too
     const size_t kPar = pe ? (size_t)strtoull(pe, nullptr, 10) : (8u << 20);
     const unsigned hw = std::thread::hardware_concurrency();
-    const unsigned nt = std::min<unsigned>(8, hw ? hw : 1);
+    static const unsigned cap = [] {  // SKV_HOST_THREADS: host threads for 10^6-entry tables (default 8)
+        const char* e = getenv("SKV_HOST_THREADS");
+        const long v = e ? atol(e) : 8;
+        return (unsigned)std::max(1l, std::min(64l, v));
+    }();
+    const unsigned nt = std::min<unsigned>(cap, hw ? hw : 1);
     if (bytes < kPar || nt < 2) {
         memcpy(dst, src, bytes);
         return;
@@ -220,7 +225,12 @@ static void stage_copy(void* dst, const void* src, size_t bytes) {
 // cannot be started runs here too.
 static unsigned par_nblocks(uint64_t n, uint64_t min_par = 1u << 16) {
     const unsigned hw = std::thread::hardware_concurrency();
-    const unsigned nt = std::min<unsigned>(8, hw ? hw : 1);
+    static const unsigned cap = [] {  // SKV_HOST_THREADS: host threads for 10^6-entry tables (default 8)
+        const char* e = getenv("SKV_HOST_THREADS");
+        const long v = e ? atol(e) : 8;
+        return (unsigned)std::max(1l, std::min(64l, v));
+    }();
+    const unsigned nt = std::min<unsigned>(cap, hw ? hw : 1);
     return n < min_par ? 1u : nt;
 }
 template <typename F>
@@ -482,8 +492,8 @@ static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
     HIPCHK(hipMemsetAsync(first_err, 0xFF, 16, st));
     HIPCHK(hipMemsetAsync(tfirst, 0xFF, (K + 1) * 8, st));
     HIPCHK(hipMemsetAsync(tbad, 0, (K + 1) * 4, st));
-    HIPCHK(hipMemsetAsync(run_len, 0, (K + 1) * 8, st));
-    HIPCHK(hipMemsetAsync(keep, 0, (K + 1) * 8, st));
+    // run_len / keep: k_wal_tables writes the first NT (the table count, on the device) and the
+    // scans below read no further
     launch_wal_keys(st, d_K, K, m_src, m_rec, rec_klen, m_P, tid, strip, wsize, canon, first_err);
     launch_wal_flags(st, d_K, K, tid, strip, canon, m_src, m_rec, rec_klen, is_new, bad, heap != nullptr);
     launch_scan(st, is_new, K, new_ex, scan_tmp);  // new_ex[K] = number of tables
@@ -492,8 +502,8 @@ static int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
     launch_scan(st, wsize, K, Pw, scan_tmp);       // stripped record offsets
     const uint64_t* d_NT = new_ex + K;
     launch_wal_tables(st, d_NT, K, tstart, Pw, tbad, job.max_run_size, run_len, keep);
-    launch_scan(st, run_len, K, run_off, scan_tmp);  // output offset per table, total at [K]
-    launch_scan(st, keep, K, keep_ex, scan_tmp);     // run index per kept table, count at [K]
+    launch_scan_dn(st, run_len, d_NT, K, run_off, scan_tmp);  // output offset per table, total at [K]
+    launch_scan_dn(st, keep, d_NT, K, keep_ex, scan_tmp);     // run index per kept table, count at [K]
     launch_wal_desc(st, d_NT, K, tstart, Pw, m_Dp, keep, keep_ex, run_off, tid, strip, m_rec, rec_klen, d_desc);
     mark(ctx, PH_CHAIN);
     launch_wal_gather(st, d_K, K, tix, tstart, keep, run_off, Pw, strip, m_src, m_rec, rec_klen, d_out);
@@ -1259,7 +1269,8 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             htrace("record tables");
             h2d_up(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
             launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
-                               rec_meta, d_flags, d_stream_base, job.batch ? nullptr : d_first_dec, rec_fp);
+                               rec_meta, d_flags, d_stream_base, job.batch ? nullptr : d_first_dec, rec_fp,
+                               dbuf<uint32_t>(ctx, "wave_run", (R + 63) / 64 + 1));
             mark(ctx, PH_PARSE);
             if (allow_deferred && !(job.flags & SKV_SPLIT_BY_TABLE) && !job.search) {
                 deferred = true;  // verdict read with the result

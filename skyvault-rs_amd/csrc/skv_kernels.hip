@@ -405,8 +405,25 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
 // exactly as read_run_stream would (runs.rs:559-626) and must have size S, which by induction
 // proves the whole run decodes to these records; any other outcome marks the run broken and
 // the host reruns the general parse.
+// wave_run[w] = the run holding record 64 w (the last run with run_recb <= 64 w). k_emit_fixed's
+// threads then search only between their wave's first run and the next wave's: with 10^6 runs
+// (config 5) a whole-table search per record was 20 dependent loads and most of the kernel.
+__global__ void k_wave_run(const uint64_t* __restrict__ run_recb, uint32_t n_runs, uint64_t nw, uint32_t* wave_run) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    const uint64_t i = w << 6;
+    uint32_t lo = 0, hi = n_runs;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (run_recb[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    wave_run[w] = lo;
+}
+
 template <bool VERIFY>
-__global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t R_total,
+__global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, const uint32_t* __restrict__ wave_run,
+                             uint64_t R_total,
                              const RunFmt* __restrict__ fmt, uint32_t* run_broken,
                              const uint64_t* __restrict__ run_recb, uint64_t* __restrict__ rec_addr,
                              uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
@@ -421,7 +438,12 @@ __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, 
     uint64_t p = 0, len = 0;
     RecHdr h{};
     if (act) {
-        uint32_t hi = n_runs;  // last run with run_recb <= i
+        const uint64_t w = i >> 6, nw = (R_total + 63) >> 6;  // last run with run_recb <= i:
+        uint32_t hi = n_runs;                                  // between this wave's first run
+        if (wave_run) {                                        // and the next wave's
+            lo = wave_run[w];
+            if (w + 1 < nw) hi = wave_run[w + 1] + 1;
+        }
         while (hi - lo > 1) {
             uint32_t mid = (lo + hi) >> 1;
             if (run_recb[mid] <= i) lo = mid;
@@ -2531,16 +2553,18 @@ void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n
                                                                 ch_rec_base, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
                                                                 flags, rec_fp, utf8_bad, slots, cap, chunk);
     if (R)
-        k_emit_fixed<false><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, R, fmt, (uint32_t*)run_broken, run_recb,
+        k_emit_fixed<false><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, nullptr, R, fmt, (uint32_t*)run_broken, run_recb,
                                                                rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags,
                                                                nullptr, nullptr, rec_fp);
 }
 void launch_parse_fixed(hipStream_t s, const RunInfo* runs, uint32_t n_runs, const RunFmt* fmt, uint32_t* run_broken,
                         const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                         uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, const uint64_t* stream_base,
-                        unsigned long long* first_dec, uint64_t* rec_fp) {
-    if (R)
-        k_emit_fixed<true><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, R, fmt, run_broken, run_recb, rec_addr,
+                        unsigned long long* first_dec, uint64_t* rec_fp, uint32_t* wave_run) {
+    if (!R) return;
+    const uint64_t nw = (R + 63) >> 6;
+    k_wave_run<<<blocks_for(nw, 256), 256, 0, s>>>(run_recb, n_runs, nw, wave_run);
+    k_emit_fixed<true><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, wave_run, R, fmt, run_broken, run_recb, rec_addr,
                                                               rec_hi, rec_lo, rec_klen, rec_meta, flags, stream_base,
                                                               first_dec, rec_fp);
 }
@@ -2677,6 +2701,69 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_single(const uint64_t* in
         carry += tot;
     }
     if (threadIdx.x == 0) out[n] = carry;
+}
+
+// The same scan over a count known only on the device (n = min(*dn, max_n)): blocks past n do no
+// memory work, and the total goes to out[n] and out[max_n] (where readers of the host-sized form
+// look). Entries of `in` past n are never read. (WAL stage: per-table arrays sized by the merged
+// record count, of which the first NT, the table count, are live.)
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_reduce_dn(const uint64_t* in, const uint64_t* dn,
+                                                                uint64_t max_n, uint64_t* partial) {
+    __shared__ uint64_t ws[16];
+    const uint64_t n = *dn < max_n ? *dn : max_n;
+    const uint64_t b0 = blockIdx.x * SCAN_BLOCK;
+    if (b0 >= n) {
+        if (threadIdx.x == 0) partial[blockIdx.x] = 0;
+        return;
+    }
+    uint64_t s = 0;
+#pragma unroll
+    for (int q = 0; q < SCAN_PER; ++q) {
+        uint64_t i = b0 + (uint64_t)threadIdx.x * SCAN_PER + q;
+        if (i < n) s += in[i];
+    }
+    uint64_t t = block_reduce_sum<uint64_t>(s, ws);
+    if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply_dn(const uint64_t* in, const uint64_t* dn, uint64_t max_n,
+                                                               const uint64_t* partial_ex, uint64_t nb, uint64_t* out) {
+    __shared__ uint64_t ws[16];
+    const uint64_t n = *dn < max_n ? *dn : max_n;
+    const uint64_t b0 = blockIdx.x * SCAN_BLOCK;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        out[n] = partial_ex[nb];
+        out[max_n] = partial_ex[nb];
+    }
+    if (b0 >= n) return;
+    uint64_t v[SCAN_PER];
+    uint64_t s = 0;
+#pragma unroll
+    for (int q = 0; q < SCAN_PER; ++q) {
+        uint64_t i = b0 + (uint64_t)threadIdx.x * SCAN_PER + q;
+        v[q] = i < n ? in[i] : 0;
+        s += v[q];
+    }
+    uint64_t tot;
+    uint64_t ex = block_excl_scan<uint64_t>(s, ws, tot) + partial_ex[blockIdx.x];
+#pragma unroll
+    for (int q = 0; q < SCAN_PER; ++q) {
+        uint64_t i = b0 + (uint64_t)threadIdx.x * SCAN_PER + q;
+        if (i < n) out[i] = ex;
+        ex += v[q];
+    }
+}
+void launch_scan_dn(hipStream_t s, const uint64_t* in, const uint64_t* dn, uint64_t max_n, uint64_t* out,
+                    uint64_t* tmp) {
+    const uint64_t nb = (max_n + SCAN_BLOCK - 1) / SCAN_BLOCK;
+    if (nb == 0) {
+        (void)hipMemsetAsync(out, 0, 8, s);
+        return;
+    }
+    uint64_t* partial = tmp;
+    uint64_t* partial_ex = tmp + nb;
+    k_scan_reduce_dn<<<(unsigned)nb, SCAN_THREADS, 0, s>>>(in, dn, max_n, partial);
+    launch_scan(s, partial, nb, partial_ex, tmp + 2 * nb + 2);
+    k_scan_apply_dn<<<(unsigned)nb, SCAN_THREADS, 0, s>>>(in, dn, max_n, partial_ex, nb, out);
 }
 
 // exclusive scan of n u64 values into out[0..n] (out[n] = total); tmp needs scan_tmp_words(n)

@@ -29,7 +29,7 @@ void launch_emit(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_c
 void launch_parse_fixed(hipStream_t, const RunInfo* runs, uint32_t n_runs, const RunFmt* fmt, uint32_t* run_broken,
                         const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                         uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, const uint64_t* stream_base,
-                        unsigned long long* first_dec, uint64_t* rec_fp);
+                        unsigned long long* first_dec, uint64_t* rec_fp, uint32_t* wave_run);
 void launch_order_check(hipStream_t, uint64_t R, const uint64_t* stream_base, uint32_t k, const uint64_t* rec_addr,
                         const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,
                         unsigned long long* first_dec, uint32_t* any_dec);
@@ -136,4 +136,5 @@ void launch_search_scan(hipStream_t, const uint8_t* run, uint64_t len, const uin
                         uint32_t n_q, SrResult* out);
 uint64_t scan_tmp_words(uint64_t n);
 void launch_scan(hipStream_t, const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tmp);
+void launch_scan_dn(hipStream_t, const uint64_t* in, const uint64_t* dn, uint64_t max_n, uint64_t* out, uint64_t* tmp);
 }  // namespace skv

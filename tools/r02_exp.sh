@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_sort.py tests/test_gpu_parity.py -m "gpu and not slow" -x -q --timeout 200 --timeout-method thread \
+timeout -k 10 300 python -u -m pytest tests -m "gpu and not slow" -x -q --timeout 200 --timeout-method thread \
   > gpurun_out/exp_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/exp_tests.log; exit 1; }
 tail -1 gpurun_out/exp_tests.log
 timeout -k 10 200 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline --no-host-path > gpurun_out/exp_5.log 2>&1 || { echo "bench 5 failed"; exit 1; }
