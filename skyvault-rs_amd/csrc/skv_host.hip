@@ -1515,10 +1515,16 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     // 4.02 vs 3.26 ms (the level-1 sample tiles lose their balance), so the default is 1.
     const char* hse = getenv("SKV_HI_STEP");
     const uint64_t hi_f = hse ? std::max<uint64_t>(1, strtoull(hse, nullptr, 10)) : 1;
+    // Level 1 (the level-0 tiles' splitters) at twice the step from 128 lists on: a tile's size
+    // spreads by ~sqrt(k) x step / 2.4 records around TILE_TARGET, which at k >= 128 stays under
+    // 1/4.6 of the TILE_CAP margin, and half the samples halve their sort (3F merge 27.3 -> 25.7 ms,
+    // config 3 2.22 -> 1.92 ms; a step of 3 unbalanced the tiles: 31.4 ms). SKV_L1_STEP=f overrides.
+    const char* l1e = getenv("SKV_L1_STEP");
+    const uint64_t l1_f = l1e ? std::max<uint64_t>(1, strtoull(l1e, nullptr, 10)) : (km >= 128 ? 2 : 1);
     while (lv.back().N > (uint64_t)TILE_CAP) {
         const Level& P = lv.back();
         Level L;
-        L.S = lv.size() >= 2 ? S_step * hi_f : S_step;
+        L.S = lv.size() >= 2 ? S_step * hi_f : S_step * l1_f;
         L.off.resize(km + 1);
         uint64_t acc = 0;
         for (uint32_t j = 0; j < km; ++j) {
