@@ -179,6 +179,10 @@ struct TileOut {
 #ifndef SKV_FX_CAP
 #define SKV_FX_CAP 2048                  // 2048: 63 VGPRs, 4 workgroups per CU (4096: 91 VGPRs, 2 per CU; 3 % slower end to end)
 #endif
+#ifndef SKV_FX_EARLY
+#define SKV_FX_EARLY 1                   // 1: fused tiles publish their survivor count before the merge
+#endif
+constexpr int FX_HSLOTS = 4096;          // distinct-key hash slots per fused tile (>= 2 x SKV_FX_CAP)
 #ifndef SKV_FX_NT
 #define SKV_FX_NT 1                      // 1: non-temporal output stores in the fused copy
 #endif

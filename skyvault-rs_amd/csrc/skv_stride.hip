@@ -29,6 +29,8 @@
 
 namespace skv {
 
+static_assert(FX_HSLOTS >= 2 * FX_CAP && FX_CAP < 65535, "distinct-key set: 16-bit slots at <= 1/2 load");
+
 typedef unsigned int fx_u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void fx_store16(uint8_t* p, uint4 v) {
@@ -473,14 +475,19 @@ __global__ void k_fx_bounds(FxArgs A, const uint64_t* __restrict__ shi, const ui
 // decoupled look-back over tiles with one wave (64 predecessors per probe), one 62-bit counter
 // per tile (flag in bits 62-63: 1 aggregate, 2 inclusive prefix). Tiles take tickets in start
 // order, so every predecessor of a waiting tile is resident or done. Called by wave 0.
-__device__ uint64_t fx_lookback(uint64_t* st, uint64_t t, uint64_t agg) {
+// published: the tile stored its aggregate already (fx_publish_early)
+__device__ __forceinline__ void fx_publish_early(uint64_t* st, uint64_t t, uint64_t agg) {
+    constexpr uint64_t FA = 1ull << 62, FI = 2ull << 62;
+    __hip_atomic_store(&st[t], (t == 0 ? FI : FA) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ uint64_t fx_lookback(uint64_t* st, uint64_t t, uint64_t agg, bool published = false) {
     constexpr uint64_t FA = 1ull << 62, FI = 2ull << 62, VM = FA - 1;
     const int lane = threadIdx.x & 63;
     if (t == 0) {
-        if (lane == 0) __hip_atomic_store(&st[0], FI | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0 && !published) __hip_atomic_store(&st[0], FI | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0;
     }
-    if (lane == 0) __hip_atomic_store(&st[t], FA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0 && !published) __hip_atomic_store(&st[t], FA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t acc = 0;
     int64_t top = (int64_t)t - 1;  // window: predecessors top, top-1, ..., top-63
     for (;;) {
@@ -721,8 +728,15 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     __shared__ uint64_t ws[16];
     __shared__ uint64_t s_t, s_g0;
     __shared__ uint32_t s_dead, s_bad;
+#if SKV_FX_EARLY
+    __shared__ uint32_t hs[FX_HSLOTS / 2];  // distinct-key set: 16-bit slots (element + 1), two per word
+    __shared__ uint32_t s_early;
+#endif
     const uint32_t tid = threadIdx.x;
     const uint64_t S = A.S;
+#if SKV_FX_EARLY
+    for (uint32_t x = tid; x < FX_HSLOTS / 2; x += FX_THREADS) hs[x] = 0;
+#endif
 #if SKV_TILE_PROF
     uint64_t tp_last = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -831,6 +845,45 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
         }
         break;
     }
+#if SKV_FX_EARLY
+    // ---- the tile's survivor count before its merge: first-per-key keeps one record per distinct
+    // key (k_way.rs:146-151; the fused path holds Puts only, keys <= 16 bytes, so (hi, lo) is the
+    // whole key), so the count is the number of distinct keys, found with an LDS hash set. Published
+    // now, successors' look-backs stop waiting on this tile's merge rounds; the merge's own count
+    // is checked against it below.
+    {
+        uint32_t distinct = 0;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const uint32_t e = tid + u * FX_THREADS;
+            if (e >= n) continue;
+            const ulong2 kv = key[e];
+            uint32_t h = (uint32_t)((kv.x * 0x9E3779B97F4A7C15ull ^ kv.y * 0xC2B2AE3D27D4EB4Full) >> 40) & (FX_HSLOTS - 1);
+            for (;;) {
+                const uint32_t sh = (h & 1u) * 16u;
+                const uint32_t w = hs[h >> 1];
+                const uint32_t cur = (w >> sh) & 0xFFFFu;
+                if (cur == 0) {
+                    const uint32_t nw = w | ((e + 1) << sh);
+                    if (atomicCAS(&hs[h >> 1], w, nw) == w) {
+                        ++distinct;
+                        break;
+                    }
+                    continue;  // the word changed: look at this slot again
+                }
+                const ulong2 o = key[cur - 1];
+                if (o.x == kv.x && o.y == kv.y) break;  // a duplicate of a key already in the set
+                h = (h + 1) & (FX_HSLOTS - 1);
+            }
+        }
+        uint32_t tot_d;
+        fx_block_excl<uint32_t>(distinct, (uint32_t*)ws, tot_d);  // barriers
+        if (tid == 0) {
+            s_early = tot_d;
+            fx_publish_early(A.tstate, t, tot_d);
+        }
+    }
+#endif
     // ---- k_way::merge order (k_way.rs:20-27, :113-179): pairwise merge-path rounds over the k
     // stream segments (segment s pairs with s ^ 1, the left one holds newer seq_nos and wins ties,
     // so equal keys end up seq_no-descending, and in stream order within a stream). Each thread
@@ -936,9 +989,12 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     const uint32_t cnt = total;
     FXPROF(4);
     if (tid < 64) {
-        const uint64_t g0 = fx_lookback(A.tstate, t, cnt) + (A.gbase ? *A.gbase : 0ull);
+        const uint64_t g0 = fx_lookback(A.tstate, t, cnt, SKV_FX_EARLY != 0) + (A.gbase ? *A.gbase : 0ull);
         if (tid == 0) {
             s_g0 = g0;
+#if SKV_FX_EARLY
+            if (s_early != cnt) fx_poison(A, FXR_RECORD);  // never: the merge kept another count
+#endif
             if (t == A.T - 1) *A.Kout = g0 + cnt;
             s_dead = __hip_atomic_load(A.flags + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
