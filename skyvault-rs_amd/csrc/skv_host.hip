@@ -1018,11 +1018,20 @@ static int search_stage(skv_ctx* ctx, const Job& job, const RunInfo& run, uint64
     return SKV_OK;
 }
 
+static void ensure_aux(skv_ctx* ctx) {  // the ctx's second stream and its two events
+    if (ctx->aux_stream) return;
+    HIPCHK(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&ctx->aux_ev[0], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ctx->aux_ev[1], hipEventDisableTiming));
+}
+
 // allow_deferred: on the fixed-stride fast path, launch the merge without waiting for the parse's
 // verdict (broken runs / order errors / oversized records) and check it with the final readback;
 // a bad verdict discards the result and reruns the call on the exact general path.
 static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_deferred) {
     hipStream_t st = ctx->stream;
+    // nothing of an earlier call may still read this ctx's buffers on the aux stream
+    if (ctx->aux_stream) HIPCHK(hipStreamSynchronize(ctx->aux_stream));
     ctx->syncs = 0;
     ctx->up_chunk = 0;
     ctx->up_off = 0;
@@ -1560,6 +1569,7 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     // k_fp_verify's inputs once the level-0 tiles are queued; it runs on the ctx stream before the
     // WAL stage, or on the aux stream beside the gather (its verdict is read with the result)
     std::pair<const unsigned long long*, const uint64_t*> verify_args{nullptr, nullptr};
+    const unsigned long long* verify_lo = nullptr;  // pairs before it verified beside the merge
     bool verify_pending = false;
     if (km > 1 && !ctx->exact_keys && !heap) {
         const char* te = getenv("SKV_FP_TEST");
@@ -1641,8 +1651,41 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
             snprintf(nm, sizeof nm, "s%d_lo", li); L.slo = O.olo = dbuf<uint64_t>(ctx, nm, L.N);
             snprintf(nm, sizeof nm, "s%d_c", li); L.sc = O.oc = dbuf<uint64_t>(ctx, nm, L.N);
         }
-        HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, cmp_klen, bounds, km, T, tile_base, rec_meta, cmp_addr,
-                           (job.flags & SKV_DROP_TOMBSTONES) ? 1u : 0u, O, d_flags + 2));
+        const uint32_t drop = (job.flags & SKV_DROP_TOMBSTONES) ? 1u : 0u;
+        // SKV_FP_PIECE_MIN=T: split level 0 from T tiles on (off by default: at 3F the verify beside
+        // the merge pieces slowed the merge by what it saved beside the gather, 89.6 vs 89.3 ms)
+        const char* pme = getenv("SKV_FP_PIECE_MIN");
+        const uint64_t piece_min = pme ? std::max<uint64_t>(1, strtoull(pme, nullptr, 10)) : ~0ull;
+        if (l0 && key_fp && T >= piece_min && T >= 4) {
+            // Level 0 in FP_PIECES launches (tickets continue across them): after each piece but
+            // the last, a one-lane kernel snapshots the pair count, and k_fp_verify checks that
+            // piece's pairs on the aux stream while the next piece merges; the last piece's pairs
+            // are checked beside the gather. Measured neutral: the verify's random record reads
+            // cost the LDS-bound merge about what they cost the gather.
+            constexpr int FP_PIECES = 4;
+            uint64_t* snap = dbuf<uint64_t>(ctx, "fp_vsnap", FP_PIECES);
+            ensure_aux(ctx);
+            uint64_t done = 0;
+            for (int p = 0; p < FP_PIECES; ++p) {
+                const uint64_t upto = T * (uint64_t)(p + 1) / FP_PIECES;
+                HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, cmp_klen, bounds, km, T, tile_base, rec_meta, cmp_addr,
+                                   drop, O, d_flags + 2, upto - done));
+                done = upto;
+                if (p + 1 < FP_PIECES) {
+                    launch_fx_publish(st, (const uint64_t*)O.vcount, snap + p);
+                    HIPCHK(hipEventRecord(ctx->aux_ev[0], st));
+                    HIPCHK(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_ev[0], 0));
+                    launch_fp_verify(ctx->aux_stream, p ? (const unsigned long long*)(snap + p - 1) : nullptr,
+                                     (const unsigned long long*)(snap + p), O.vpairs, R, fp_bad, 1024);
+                    verify_pending = true;
+                }
+            }
+            HIPCHK(hipEventRecord(ctx->aux_ev[1], ctx->aux_stream));
+            verify_lo = (const unsigned long long*)(snap + FP_PIECES - 2);
+        } else {
+            HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, cmp_klen, bounds, km, T, tile_base, rec_meta, cmp_addr, drop,
+                               O, d_flags + 2));
+        }
         if (l0 && key_fp) verify_args = {O.vcount, O.vpairs};
         if (l0) T0 = T;
     }
@@ -1653,21 +1696,17 @@ static int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool a
     tables_mine();
     auto fork_verify = [&]() {  // k_fp_verify on the aux stream, after what the ctx stream has queued
         if (!verify_args.first) return;
-        if (!ctx->aux_stream) {
-            HIPCHK(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
-            HIPCHK(hipEventCreateWithFlags(&ctx->aux_ev[0], hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&ctx->aux_ev[1], hipEventDisableTiming));
-        }
+        ensure_aux(ctx);
         HIPCHK(hipEventRecord(ctx->aux_ev[0], st));
         HIPCHK(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_ev[0], 0));
-        launch_fp_verify(ctx->aux_stream, verify_args.first, verify_args.second, R, fp_bad);
+        launch_fp_verify(ctx->aux_stream, verify_lo, verify_args.first, verify_args.second, R, fp_bad);
         HIPCHK(hipEventRecord(ctx->aux_ev[1], ctx->aux_stream));
         verify_args.first = nullptr;
         verify_pending = true;
     };
     auto join_verify = [&]() {  // fp_bad is read next: the ctx stream waits for k_fp_verify
         if (verify_args.first) {  // not forked: in order on the ctx stream
-            launch_fp_verify(st, verify_args.first, verify_args.second, R, fp_bad);
+            launch_fp_verify(st, verify_lo, verify_args.first, verify_args.second, R, fp_bad);
             verify_args.first = nullptr;
         }
         if (verify_pending) HIPCHK(hipStreamWaitEvent(st, ctx->aux_ev[1], 0));

@@ -616,11 +616,12 @@ __device__ __forceinline__ bool elem_less_fp(bool use_fp, uint64_t fpa, const ui
 // The pairs k_tile<true> took as one key on equal prefix, length and fingerprint (O.vpairs: the two
 // records' addresses): their bytes past 16 must be equal, else the call is rerun with exact
 // compares. Every pair is independent: a grid-stride loop with all its loads in flight.
-__global__ void k_fp_verify(const unsigned long long* __restrict__ vcount, const uint64_t* __restrict__ vpairs,
-                            uint32_t* fp_bad) {
-    const uint64_t n = *vcount;
+// pairs [*vlo, *vcount) (vlo null: from 0): a slice of the queue whose tiles have finished
+__global__ void k_fp_verify(const unsigned long long* __restrict__ vlo, const unsigned long long* __restrict__ vcount,
+                            const uint64_t* __restrict__ vpairs, uint32_t* fp_bad) {
+    const uint64_t n = *vcount, n0 = vlo ? *vlo : 0;
     uint32_t bad = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    for (uint64_t i = n0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint8_t* ra = (const uint8_t*)vpairs[2 * i];
         const uint8_t* rb = (const uint8_t*)vpairs[2 * i + 1];
         const uint32_t la = __builtin_bswap32(load_window16(ra + 1, 4).x);  // key_len of each record
@@ -2608,11 +2609,11 @@ void launch_tile_n(hipStream_t s, const uint64_t* bounds, uint32_t k, uint64_t T
     if (!T) return;
     k_tile_n<<<blocks_for(T, 256), 256, 0, s>>>(bounds, k, T, tile_n);
 }
-void launch_fp_verify(hipStream_t s, const unsigned long long* vcount, const uint64_t* vpairs, uint64_t cap,
-                      uint32_t* fp_bad) {
+void launch_fp_verify(hipStream_t s, const unsigned long long* vlo, const unsigned long long* vcount,
+                      const uint64_t* vpairs, uint64_t cap, uint32_t* fp_bad, unsigned max_blocks) {
     unsigned blocks = blocks_for(cap ? cap : 1, 256);
-    if (blocks > 8192) blocks = 8192;
-    k_fp_verify<<<blocks, 256, 0, s>>>(vcount, vpairs, fp_bad);
+    if (blocks > max_blocks) blocks = max_blocks;
+    k_fp_verify<<<blocks, 256, 0, s>>>(vlo, vcount, vpairs, fp_bad);
 }
 size_t tile_lds_bytes(uint32_t k) {
     size_t b = (size_t)TILE_CAP * (4 * 8 + 2 + 2) + 2 * (size_t)(k + 1) * 4;
@@ -2622,8 +2623,9 @@ size_t tile_lds_bytes(uint32_t k) {
 hipError_t launch_tile(hipStream_t s, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
                        const uint32_t* klen, const uint64_t* bounds, uint32_t k, uint64_t T, const uint64_t* tile_base,
                        const uint32_t* rec_meta, const uint64_t* rec_addr, uint32_t drop, TileOut O,
-                       const uint32_t* poison) {
+                       const uint32_t* poison, uint64_t grid) {
     Elems E{hi, lo, c, klen, poison};
+    if (!grid) grid = T;  // level 0 takes tickets: launches of grid < T tiles continue each other
     size_t lds = tile_lds_bytes(k);
     // raise the dynamic LDS limit once per device and size, not per call
     static size_t lds_set[64][2] = {};
@@ -2636,7 +2638,7 @@ hipError_t launch_tile(hipStream_t s, bool l0, const uint64_t* hi, const uint64_
         done = lds;
     }
     if (l0) {
-        k_tile<true><<<(unsigned)T, TILE_THREADS, lds, s>>>(E, bounds, k, tile_base, rec_meta, rec_addr, drop, O);
+        k_tile<true><<<(unsigned)grid, TILE_THREADS, lds, s>>>(E, bounds, k, tile_base, rec_meta, rec_addr, drop, O);
     } else {
         k_tile<false><<<(unsigned)T, TILE_THREADS, lds, s>>>(E, bounds, k, tile_base, rec_meta, rec_addr, drop, O);
     }

@@ -49,7 +49,7 @@ size_t tile_lds_bytes(uint32_t k);
 hipError_t launch_tile(hipStream_t, bool l0, const uint64_t* hi, const uint64_t* lo, const uint64_t* c,
                        const uint32_t* klen, const uint64_t* bounds, uint32_t k, uint64_t T, const uint64_t* tile_base,
                        const uint32_t* rec_meta, const uint64_t* rec_addr, uint32_t drop, TileOut O,
-                       const uint32_t* poison);
+                       const uint32_t* poison, uint64_t grid = 0);
 void launch_chain(hipStream_t, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, const uint32_t* tile_max,
                   uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs, uint32_t* tbl, uint64_t max_K,
                   uint64_t max_bytes, const SplitBufs* sp = nullptr);
@@ -106,8 +106,8 @@ uint64_t fx_tile_slots(uint32_t k);
 void launch_fx_desc(hipStream_t, const FxArgs& A, DevRunDesc* descs, uint64_t* n_runs_out, uint64_t max_runs);
 // *dst = *src with a system-scope store: dst is host-mapped pinned memory the host polls
 // the pairs k_tile<true> took as equal keys by fingerprint: any that differ set *fp_bad
-void launch_fp_verify(hipStream_t, const unsigned long long* vcount, const uint64_t* vpairs, uint64_t cap,
-                      uint32_t* fp_bad);
+void launch_fp_verify(hipStream_t, const unsigned long long* vlo, const unsigned long long* vcount,
+                      const uint64_t* vpairs, uint64_t cap, uint32_t* fp_bad, unsigned max_blocks = 8192);
 void launch_fx_publish(hipStream_t, const uint64_t* src, uint64_t* dst);
 // n bytes src -> dst by a kernel (src may be host-mapped pinned memory): small table uploads that
 // must not queue behind bulk DMA on a copy engine (pipelined host calls)

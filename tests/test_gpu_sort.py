@@ -201,3 +201,25 @@ def test_fp_shortcut_wal_collisions(dev, monkeypatch):
     monkeypatch.setenv("SKV_FP_TEST", "1")
     _check(dev, gen.config5(n_streams=40), 4 * MiB, _abi.SKV_SPLIT_BY_TABLE, expect_sorted=False)
     assert dev.timings()["fp_rerun"] == 1
+
+
+def test_fp_verify_in_pieces(dev, monkeypatch):
+    """Level 0 merged in four launches with each piece's pairs verified beside the next piece
+    (SKV_FP_PIECE_MIN=1 forces the split on small calls): exact output with real fingerprints,
+    and forced collisions (SKV_FP_TEST=1) caught wherever the colliding pairs fall."""
+    monkeypatch.setenv("SKV_FUSED", "0")
+    monkeypatch.setenv("SKV_FP_PIECE_MIN", "1")
+    cases = ((gen.config3(n_streams=64, run_bytes=256 * 1024, vsize=16), 1 << 18, 0),
+             (gen.config3(n_streams=64, run_bytes=256 * 1024, vsize=16), 1 << 18, _abi.SKV_DROP_TOMBSTONES),
+             (_prefix_keys_streams(), 1 << 16, 0))
+    for streams, mx, fl in cases:
+        _check(dev, streams, mx, fl, expect_sorted=False)
+        assert dev.timings()["fp_rerun"] == 0
+    monkeypatch.setenv("SKV_FP_TEST", "1")
+    for streams, mx, fl in cases:  # (config 3 keys rarely tie on prefix and length: exact either way)
+        _check(dev, streams, mx, fl, expect_sorted=False)
+    many = _prefix_keys_streams(n_streams=64, per=1000, seed=12)  # ~20 tiles, colliding everywhere
+    for fl in (0, _abi.SKV_DROP_TOMBSTONES):
+        _check(dev, many, 1 << 16, fl, expect_sorted=False)
+        assert dev.timings()["fp_rerun"] == 1, "forced collisions were not detected"
+    _check(dev, gen.config5(n_streams=40), 4 * MiB, _abi.SKV_SPLIT_BY_TABLE, expect_sorted=False)
