@@ -248,6 +248,7 @@ __device__ __forceinline__ bool sk_sbefore(const SWin& w, const SSplit* __restri
 // (elements are in record order): the bucket sort then reads no record bytes, where it used to
 // load one window per element from a record at random (~250 B of HBM lines per element).
 constexpr int SB_THREADS = 256, SB_PER = 16, SB_TOP = 1024, SB_ILP = 4;
+static_assert(SB_PER % SB_ILP == 0, "a workgroup's elements in whole ILP batches");
 __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n, const uint32_t* __restrict__ Lb,
                                                             const SSplit* __restrict__ sp,
                                                             const SWin* __restrict__ win, uint64_t nsp, uint64_t top,
