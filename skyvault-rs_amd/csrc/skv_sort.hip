@@ -247,7 +247,16 @@ __device__ __forceinline__ bool sk_sbefore(const SWin& w, const SSplit* __restri
 // its 16-byte window from byte Lb[bucket] on, read here while the record's key line is in cache
 // (elements are in record order): the bucket sort then reads no record bytes, where it used to
 // load one window per element from a record at random (~250 B of HBM lines per element).
-constexpr int SB_THREADS = 256, SB_PER = 16, SB_TOP = 1024, SB_ILP = 4;
+#ifndef SKV_SB_THREADS
+#define SKV_SB_THREADS 256
+#endif
+#ifndef SKV_SB_PER
+#define SKV_SB_PER 16
+#endif
+#ifndef SKV_SB_TOP
+#define SKV_SB_TOP 1024
+#endif
+constexpr int SB_THREADS = SKV_SB_THREADS, SB_PER = SKV_SB_PER, SB_TOP = SKV_SB_TOP, SB_ILP = 4;
 static_assert(SB_PER % SB_ILP == 0, "a workgroup's elements in whole ILP batches");
 __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n, const uint32_t* __restrict__ Lb,
                                                             const SSplit* __restrict__ sp,
