@@ -182,7 +182,7 @@ struct TileOut {
 #ifndef SKV_FX_EARLY
 #define SKV_FX_EARLY 1                   // 1: fused tiles publish their survivor count before the merge
 #endif
-constexpr int FX_HSLOTS = 4096;          // distinct-key hash slots per fused tile (>= 2 x SKV_FX_CAP)
+constexpr int FX_HSLOTS = 2 * SKV_FX_CAP;  // distinct-key hash slots per fused tile (load <= 1/2)
 #ifndef SKV_FX_NT
 #define SKV_FX_NT 1                      // 1: non-temporal output stores in the fused copy
 #endif
