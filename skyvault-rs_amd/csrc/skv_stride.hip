@@ -817,7 +817,16 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     __syncthreads();
     FXPROF(1);
     // ---- order check inside each stream (runs.rs:190-198): against the previous record of the
-    // same stream (the previous element of the segment, or the record before the segment)
+    // same stream (the previous element of the segment, or the record before the segment).
+#if SKV_FX_EARLY
+    // In the same pass, the tile's survivor count before its merge: first-per-key keeps one record
+    // per distinct key (k_way.rs:146-151; the fused path holds Puts only, keys <= 16 bytes, so
+    // (hi, lo) is the whole key), so the count is the number of distinct keys, found with an LDS
+    // hash set (16-bit slots holding element + 1, two per word, claimed by CAS). Published before
+    // the merge rounds, successors' look-backs stop waiting on them; the merge's own count is
+    // checked against it after the rounds.
+    uint32_t distinct = 0;
+#endif
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const uint32_t e = tid + u * FX_THREADS;
@@ -832,10 +841,33 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
                 has = prevok[j] != 0;
             }
             if (has && !fx_le(pv, c) && SKV_FX_DIAG != 3) bad |= FXR_ORDER;  // a strict decrease
+#if SKV_FX_EARLY
+            uint32_t h = (uint32_t)((c.x * 0x9E3779B97F4A7C15ull ^ c.y * 0xC2B2AE3D27D4EB4Full) >> 40) & (FX_HSLOTS - 1);
+            for (;;) {
+                const uint32_t sh = (h & 1u) * 16u;
+                const uint32_t w = hs[h >> 1];
+                const uint32_t cur = (w >> sh) & 0xFFFFu;
+                if (cur == 0) {
+                    if (atomicCAS(&hs[h >> 1], w, w | ((e + 1) << sh)) == w) {
+                        ++distinct;
+                        break;
+                    }
+                    continue;  // the word changed: look at this slot again
+                }
+                const ulong2 o = key[cur - 1];
+                if (o.x == c.x && o.y == c.y) break;  // a duplicate of a key already in the set
+                h = (h + 1) & (FX_HSLOTS - 1);
+            }
+#endif
         }
     }
     if (bad) atomicOr(&s_bad, bad);
+#if SKV_FX_EARLY
+    uint32_t tot_d;
+    fx_block_excl<uint32_t>(distinct, (uint32_t*)ws, tot_d);  // barriers: s_bad is settled after it
+#else
     __syncthreads();
+#endif
     FXPROF(2);
     if (s_dead || s_bad) {  // publish an empty aggregate so later tiles never wait on this one
         if (tid == 0) {
@@ -846,42 +878,9 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
         break;
     }
 #if SKV_FX_EARLY
-    // ---- the tile's survivor count before its merge: first-per-key keeps one record per distinct
-    // key (k_way.rs:146-151; the fused path holds Puts only, keys <= 16 bytes, so (hi, lo) is the
-    // whole key), so the count is the number of distinct keys, found with an LDS hash set. Published
-    // now, successors' look-backs stop waiting on this tile's merge rounds; the merge's own count
-    // is checked against it below.
-    {
-        uint32_t distinct = 0;
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const uint32_t e = tid + u * FX_THREADS;
-            if (e >= n) continue;
-            const ulong2 kv = key[e];
-            uint32_t h = (uint32_t)((kv.x * 0x9E3779B97F4A7C15ull ^ kv.y * 0xC2B2AE3D27D4EB4Full) >> 40) & (FX_HSLOTS - 1);
-            for (;;) {
-                const uint32_t sh = (h & 1u) * 16u;
-                const uint32_t w = hs[h >> 1];
-                const uint32_t cur = (w >> sh) & 0xFFFFu;
-                if (cur == 0) {
-                    const uint32_t nw = w | ((e + 1) << sh);
-                    if (atomicCAS(&hs[h >> 1], w, nw) == w) {
-                        ++distinct;
-                        break;
-                    }
-                    continue;  // the word changed: look at this slot again
-                }
-                const ulong2 o = key[cur - 1];
-                if (o.x == kv.x && o.y == kv.y) break;  // a duplicate of a key already in the set
-                h = (h + 1) & (FX_HSLOTS - 1);
-            }
-        }
-        uint32_t tot_d;
-        fx_block_excl<uint32_t>(distinct, (uint32_t*)ws, tot_d);  // barriers
-        if (tid == 0) {
-            s_early = tot_d;
-            fx_publish_early(A.tstate, t, tot_d);
-        }
+    if (tid == 0) {
+        s_early = tot_d;
+        fx_publish_early(A.tstate, t, tot_d);
     }
 #endif
     // ---- k_way::merge order (k_way.rs:20-27, :113-179): pairwise merge-path rounds over the k
