@@ -185,6 +185,17 @@ def reduce_over_ranks(elapsed, in_bytes, dist, device):
     return float(t.item()), float(b.item())
 
 
+def timed_loop(step, steps, barrier):
+    """The bench contract's timed region: barrier (+ device sync) on both sides of exactly `steps`
+    calls of step(); returns this rank's elapsed seconds (reduce_over_ranks takes the max)."""
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    barrier()
+    return time.perf_counter() - t0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -200,7 +211,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-memory figure")
     ap.add_argument("--cpu-sample-records", type=int, default=238821 // 16)
-    ap.add_argument("--cpu-repeats", type=int, default=3)
+    ap.add_argument("--cpu-repeats", type=int, default=5)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes of each kernel measured with rocprofv3 --pmc (tools/traffic.py)")
     args = ap.parse_args()
@@ -236,7 +247,7 @@ def main():
         run_mib = 256 if args.run_mib == 16 else args.run_mib
         runs = make_cfg3_full_on_device(device, seed, n_streams, run_mib)
         workload = (f"config 3: {n_streams}-way compaction, {n_streams} x 1 run of ~{run_mib} MiB, variable-length "
-                    f"keys 11-128 B + 10 % Deletes, 256 B values, max run 4 MiB")
+                    f"keys 8-128 B + 10 % Deletes, 256 B values, max run 4 MiB")
         data = "synthetic: sorted unique ids rendered as order-preserving alnum keys + alnum tails, built in HBM"
     elif config == "3":
         n_streams = 256 if args.streams == 64 else args.streams
@@ -280,9 +291,9 @@ def main():
             dist.barrier()
 
     gather_ms, total_ms, phases, host_ms, sync_ms, call_ms = [], [], [], [], [], []
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
+    last = {}
+
+    def step():
         tc = time.perf_counter()
         res = comp.compact_dev(table, max_run, flags)
         call_ms.append((time.perf_counter() - tc) * 1e3)
@@ -292,18 +303,19 @@ def main():
         gather_ms.append(t["hot_ms"])
         total_ms.append(t["total_ms"])
         phases.append([t[k] for k in ("parse_ms", "check_ms", "merge_ms", "chain_ms", "gather_ms")])
-        gread, gwrite = t["hot_read_bytes"], t["hot_write_bytes"]
-        path = t["path"]
-        out_bytes, n_out_runs = res.n_bytes, res.n_runs
+        last.update(t=t, out=(res.n_bytes, res.n_runs))
         res.free()
-    barrier()
-    t_end = time.perf_counter()
+
+    elapsed_rank = timed_loop(step, args.steps, barrier)
+    t = last["t"]
+    gread, gwrite, path = t["hot_read_bytes"], t["hot_write_bytes"], t["path"]
+    out_bytes, n_out_runs = last["out"]
     # invariants of the measured call's output (outside the timed region)
     res = comp.compact_dev(table, max_run, flags)
     invariants = check_invariants(res, config, max_run, res.in_records) if config != "5" else {
         "checked": True, "runs": res.n_runs, "out_records": res.out_records}
     res.free()
-    elapsed, total_in = reduce_over_ranks(t_end - t0, in_bytes, dist, torch.device("cpu"))
+    elapsed, total_in = reduce_over_ranks(elapsed_rank, in_bytes, dist, torch.device("cpu"))
 
     # PCIe-inclusive figure (not `value`): the host entry point skv_compact with the inputs in
     # pinned host memory and the output runs returned in pinned host memory.
@@ -385,13 +397,23 @@ def main():
         if g_ms <= 0:  # the WAL stage reports no single dominant launch: the whole device time
             g_ms = float(np.mean(total_ms))
         achieved = (gread + gwrite) / (g_ms * 1e-3) / 1e9
-        traffic = None
+        hot_kernel = "k_wal_gather" if config == "5" else HOT_KERNEL.get(path, "?")
+        # PMC counters of THIS config's dominant kernel (tools/traffic.py keys them by config and
+        # kernel); none recorded -> null with the reason, never another config's counters
+        traffic, traffic_note, traffic_rw = None, None, None
         try:
             with open(args.traffic_json) as f:
-                kt = json.load(f).get("kernels", {}).get("skv::" + HOT_KERNEL.get(path, "?"))
-                traffic = kt["hbm_bytes"] if kt else None
-        except (OSError, ValueError):
-            traffic = None
+                cfgs = json.load(f).get("configs", {})
+            kt = cfgs.get(config, {}).get("kernels", {}).get("skv::" + hot_kernel)
+            if kt:
+                traffic = kt["hbm_bytes"]
+                traffic_rw = {"read_bytes": kt["read_bytes"], "write_bytes": kt["write_bytes"],
+                              "ratio_to_algorithmic": round(kt["hbm_bytes"] / max(1, gread + gwrite), 3),
+                              "source": os.path.relpath(args.traffic_json, ROOT) + f" [configs][{config}]"}
+            else:
+                traffic_note = f"no --pmc pass recorded for config {config} / {hot_kernel} in {args.traffic_json}"
+        except (OSError, ValueError) as e:
+            traffic_note = f"traffic file unreadable: {e}"
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -422,13 +444,14 @@ def main():
             "record_sort": bool(t["sorted"]),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_wal_gather" if config == "5" else HOT_KERNEL.get(path, "?"),
+                "kernel": hot_kernel,
                 "path": PATH_NAMES.get(path, "?"),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_detail": traffic_rw if traffic is not None else traffic_note,
                 "algorithmic_bytes_per_launch": int(gread + gwrite),
                 "avg_launch_ms": round(g_ms, 4),
                 # whole compaction against the same peak: SURVEY §8d's (I + O) / t

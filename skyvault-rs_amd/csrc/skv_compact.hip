@@ -1,0 +1,1158 @@
+// skv_compact.hip — compact_device: the general / fixed-stride / record-sort path of one compaction
+// (parse -> merge -> [filter | WAL split] -> split -> gather), the fp-shortcut rerun, the WAL stage
+// and the writer batch entry points. skv_compact_dev is the device-resident C entry.
+#include "skv_host.hpp"
+
+using namespace skv;
+
+// the whole call again with exact key compares in the merge rounds
+int rerun_exact(skv_ctx* ctx, const Job& job, skv_result** out) {
+    ctx->exact_keys = true;
+    int rc;
+    try {
+        rc = compact_device(ctx, job, out, false);
+    } catch (...) {
+        ctx->exact_keys = false;
+        throw;
+    }
+    ctx->exact_keys = false;
+    ctx->timings.fp_rerun = 1;
+    return rc;
+}
+
+// SKV_SPLIT_BY_TABLE after the merge: table split, prefix strip, one run per kept table
+// (skv_wal.hip). One extra host sync reads the surviving record count first.
+int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, const uint32_t* m_rec,
+                     const uint64_t* m_src, const uint64_t* m_P, const uint64_t* m_Dp, const uint64_t* rec_addr,
+                     const uint32_t* rec_klen, const uint32_t* fp_bad, const HeapRes* heap, skv_result** out) {
+    hipStream_t st = ctx->stream;
+    uint64_t K = 0;
+    {
+        uint64_t* hp = (uint64_t*)pinned(ctx, 64);
+        d2h(ctx, hp, d_K, 8);
+        d2h(ctx, hp + 1, fp_bad, 4);
+        sync(ctx);
+        K = hp[0];
+        if ((uint32_t)hp[1]) return RC_RETRY_EXACT;
+    }
+    htrace("wal K read");
+    (void)R;
+    int64_t* tid = dbuf<int64_t>(ctx, "w_tid", K + 1);
+    uint32_t* strip = dbuf<uint32_t>(ctx, "w_strip", K + 1);
+    uint8_t* canon = dbuf<uint8_t>(ctx, "w_canon", K + 1);
+    uint64_t* wsize = dbuf<uint64_t>(ctx, "w_size", K + 1);
+    uint64_t* is_new = dbuf<uint64_t>(ctx, "w_new", K + 1);
+    uint64_t* new_ex = dbuf<uint64_t>(ctx, "w_new_ex", K + 1);
+    uint32_t* bad = dbuf<uint32_t>(ctx, "w_bad", K + 1);
+    uint32_t* tix = dbuf<uint32_t>(ctx, "w_tix", K + 1);
+    uint64_t* tstart = dbuf<uint64_t>(ctx, "w_tstart", K + 2);
+    uint32_t* tbad = dbuf<uint32_t>(ctx, "w_tbad", K + 1);
+    uint64_t* Pw = dbuf<uint64_t>(ctx, "w_P", K + 1);
+    uint64_t* run_len = dbuf<uint64_t>(ctx, "w_run_len", K + 1);
+    uint64_t* keep = dbuf<uint64_t>(ctx, "w_keep", K + 1);
+    uint64_t* run_off = dbuf<uint64_t>(ctx, "w_run_off", K + 1);
+    uint64_t* keep_ex = dbuf<uint64_t>(ctx, "w_keep_ex", K + 1);
+    unsigned long long* first_err = dbuf<unsigned long long>(ctx, "w_first_err", 2);  // bad key, failed send
+    unsigned long long* tfirst = dbuf<unsigned long long>(ctx, "w_tfirst", K + 1);
+    uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "w_scan_tmp", scan_tmp_words(K + 1) + 64);
+    DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", K + 1);
+    uint8_t* d_out = dbuf<uint8_t>(ctx, "out", job.in_bytes + K + 16);  // in_bytes: the run lengths' sum
+    HIPCHK(hipMemsetAsync(first_err, 0xFF, 16, st));
+    HIPCHK(hipMemsetAsync(tfirst, 0xFF, (K + 1) * 8, st));
+    HIPCHK(hipMemsetAsync(tbad, 0, (K + 1) * 4, st));
+    // run_len / keep: k_wal_tables writes the first NT (the table count, on the device) and the
+    // scans below read no further
+    launch_wal_keys(st, d_K, K, m_src, m_rec, rec_klen, m_P, tid, strip, wsize, canon, first_err);
+    launch_wal_flags(st, d_K, K, tid, strip, canon, m_src, m_rec, rec_klen, is_new, bad, heap != nullptr);
+    launch_scan(st, is_new, K, new_ex, scan_tmp);  // new_ex[K] = number of tables
+    launch_wal_index(st, d_K, K, is_new, new_ex, bad, tix, tstart, tbad, tfirst);
+    launch_wal_sendfail(st, new_ex + K, K, tstart, tfirst, first_err + 1);
+    launch_scan(st, wsize, K, Pw, scan_tmp);       // stripped record offsets
+    const uint64_t* d_NT = new_ex + K;
+    launch_wal_tables(st, d_NT, K, tstart, Pw, tbad, job.max_run_size, run_len, keep);
+    launch_scan_dn(st, run_len, d_NT, K, run_off, scan_tmp);  // output offset per table, total at [K]
+    launch_scan_dn(st, keep, d_NT, K, keep_ex, scan_tmp);     // run index per kept table, count at [K]
+    launch_wal_desc(st, d_NT, K, tstart, Pw, m_Dp, keep, keep_ex, run_off, tid, strip, m_rec, rec_klen, d_desc);
+    mark(ctx, PH_CHAIN);
+    launch_wal_gather(st, d_K, K, tix, tstart, keep, run_off, Pw, strip, m_src, m_rec, rec_klen, d_out);
+    HIPCHK(hipGetLastError());
+    mark(ctx, PH_GATHER);
+    uint64_t h[5];
+    {
+        uint64_t* hp = (uint64_t*)pinned(ctx, 64);
+        d2h(ctx, hp, first_err, 8);
+        d2h(ctx, hp + 1, d_NT, 8);
+        d2h(ctx, hp + 2, keep_ex + K, 8);
+        d2h(ctx, hp + 3, run_off + K, 8);
+        d2h(ctx, hp + 4, first_err + 1, 8);
+        sync(ctx);
+        memcpy(h, hp, 40);
+    }
+    htrace("wal outcome read");
+    // The job's first failure in merged order: a bad key (:67-79 `?`), a send to a table whose task
+    // has failed (:157-161), or (heap-order mode) a stream's decode error (:66-67 `result?`).
+    // Sorted inputs without decode errors: survivor indices are the merged order.
+    std::vector<JobEvent> ev;
+    auto pos_of_survivor = [&](uint64_t j) -> uint64_t {
+        return heap ? read_dev(heap->pop_pos + read_dev(m_rec + j)) : j;
+    };
+    if (h[0] != ~0ull)
+        ev.push_back({pos_of_survivor(h[0]), 0, SKV_E_INVALID_INPUT,
+                      wal_key_error(fetch_key(ctx, rec_addr, rec_klen, read_dev(m_rec + h[0])))});
+    if (h[4] != ~0ull)
+        ev.push_back({pos_of_survivor(h[4]), 1, SKV_E_INTERNAL, "Internal error: Failed to send operation to table channel"});
+    if (heap)
+        for (const HeapRes::Dec& d : heap->dec) {
+            std::string msg;
+            const int code = derr_to_api(d.err, msg);
+            ev.push_back({heap->pos_of_original(d.rec), 2, code, msg});
+        }
+    if (getenv("SKV_HEAP_DEBUG")) {
+        fprintf(stderr, "[wal] K=%llu heap=%d badkey=%lld sendfail=%lld\n", (unsigned long long)K, heap ? 1 : 0,
+                (long long)h[0], (long long)h[4]);
+        for (const JobEvent& e : ev) fprintf(stderr, "  event pos=%llu sub=%d code=%d %s\n", (unsigned long long)e.pos, e.sub, e.code, e.msg.c_str());
+        if (heap)
+            for (uint64_t r = 0; r < R && r < 64; ++r)
+                fprintf(stderr, "  rec %llu pop=%llu\n", (unsigned long long)r, (unsigned long long)read_dev(heap->pop_pos + r));
+    }
+    throw_first(ev);
+    const uint64_t n_tables = h[1], n_kept = h[2], n_bytes = h[3];
+    ResultBox* box = new ResultBox();
+    skv_result* res = &box->pub;
+    res->runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, n_kept) * sizeof(skv_run_desc));
+    if (n_kept) HIPCHK(hipMemcpy(res->runs, d_desc, n_kept * sizeof(DevRunDesc), hipMemcpyDeviceToHost));
+    uint64_t out_records = 0;
+    for (uint64_t i = 0; i < n_kept; ++i) out_records += res->runs[i].put_count + res->runs[i].delete_count;
+    res->n_runs = n_kept;
+    res->bytes = d_out;
+    res->n_bytes = n_bytes;
+    res->in_bytes = job.in_bytes;
+    res->in_records = R;
+    res->out_records = out_records;
+    res->dropped_tables = n_tables - n_kept;
+    if (ctx->profiling) {
+        HIPCHK(hipEventSynchronize(ctx->ev[PH_GATHER]));
+        float ms[PH_N] = {};
+        for (int p = PH_PARSE; p < PH_N; ++p) HIPCHK(hipEventElapsedTime(&ms[p], ctx->ev[p - 1], ctx->ev[p]));
+        float tot = 0;
+        HIPCHK(hipEventElapsedTime(&tot, ctx->ev[PH_START], ctx->ev[PH_GATHER]));
+        skv_timings& t = ctx->timings;
+        t.total_ms = tot;
+        t.parse_ms = ms[PH_PARSE];
+        t.check_ms = ms[PH_CHECK];
+        t.merge_ms = ms[PH_MERGE];
+        t.chain_ms = ms[PH_CHAIN];
+        t.gather_ms = ms[PH_GATHER];
+        t.gather_read_bytes = n_bytes - n_kept;
+        t.gather_write_bytes = n_bytes;
+        t.hot_ms = ms[PH_GATHER];
+    }
+    ctx->timings.path = SKV_PATH_GENERAL;  // WAL stage: the dominant launch is k_wal_gather
+    ctx->timings.hot_read_bytes = n_bytes - n_kept;
+    ctx->timings.hot_write_bytes = n_bytes;
+    ctx->timings.host_syncs = ctx->syncs;
+    *out = res;
+    return SKV_OK;
+}
+
+// Sorts n SElems by (key, record index) (skv_sort.hip); E and T are n-element buffers, the
+// result is in the returned one of the two. Samples recurse with their own buffers (depth).
+SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth, uint64_t* newkey) {
+    hipStream_t st = ctx->stream;
+    char nm[64];
+    if (n <= (uint64_t)SORT_CAP) {  // one bucket
+        snprintf(nm, sizeof nm, "sort_one%d", depth);
+        uint64_t* start = dbuf<uint64_t>(ctx, nm, 2);
+        const uint64_t h[2] = {0, n};
+        h2d_up(ctx, start, h, 16);
+        launch_sort_tile(st, E, start, nullptr, 1, T, newkey, false);
+        return T;
+    }
+    const uint64_t Ns = (n + SORT_EVERY - 1) / SORT_EVERY;
+    snprintf(nm, sizeof nm, "sort_s%d", depth);
+    SElem* S = dbuf<SElem>(ctx, nm, Ns);
+    snprintf(nm, sizeof nm, "sort_sT%d", depth);
+    SElem* S2 = dbuf<SElem>(ctx, nm, Ns);
+    launch_sort_sample(st, E, n, Ns, S);
+    const SElem* Ss = sort_elems(ctx, S, S2, Ns, depth + 1);
+    const uint64_t Tb = (Ns + SORT_OV - 1) / SORT_OV;  // buckets; Tb - 1 splitters
+    snprintf(nm, sizeof nm, "sort_L%d", depth);
+    uint32_t* L = dbuf<uint32_t>(ctx, nm, Tb);
+    snprintf(nm, sizeof nm, "sort_cnt%d", depth);
+    uint64_t* cnt = dbuf<uint64_t>(ctx, nm, Tb + 1);
+    snprintf(nm, sizeof nm, "sort_bs%d", depth);
+    uint64_t* bs = dbuf<uint64_t>(ctx, nm, n);
+    snprintf(nm, sizeof nm, "sort_start%d", depth);
+    uint64_t* start = dbuf<uint64_t>(ctx, nm, Tb + 1);
+    snprintf(nm, sizeof nm, "sort_scan%d", depth);
+    uint64_t* scan_tmp = dbuf<uint64_t>(ctx, nm, scan_tmp_words(Tb) + 64);
+    launch_sort_prefix(st, Ss, SORT_OV, Tb, L);
+    HIPCHK(hipMemsetAsync(cnt, 0, (Tb + 1) * 8, st));
+    snprintf(nm, sizeof nm, "sort_split%d", depth);
+    uint8_t* split_buf = dbuf<uint8_t>(ctx, nm, sort_split_bytes(Tb - 1));
+    // depth 0 (the records themselves): the bucket search stores each element's window from its
+    // bucket's common prefix on, so the bucket sort reads no record bytes; its output keeps only
+    // addr / pos / klen meaningful (sort_records reads no more). Sample levels keep their keys.
+    const bool pre = depth == 0;
+    launch_sort_bucket(st, E, n, Ss, SORT_OV, Tb - 1, split_buf, cnt, bs, pre ? L : nullptr);
+    launch_scan(st, cnt, Tb, start, scan_tmp);
+    launch_sort_scatter(st, E, n, bs, start, T);
+    launch_sort_tile(st, T, start, L, Tb, E, newkey, pre);
+    return E;
+}
+
+// The merged order of R records as one sorted list: the record arrays are replaced by sorted
+// copies (merges of more than TILE_TARGET / 2 streams, whose splitter bounds table would be
+// tiles x streams). hi/lo/cmp_klen become dense key ranks for the merge stage; klen stays the real
+// key length (descriptors, WAL split).
+void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo, uint64_t*& addr, uint32_t*& klen,
+                         uint32_t*& meta, const uint32_t*& cmp_klen, bool last_wins, const SElem** sorted) {
+    hipStream_t st = ctx->stream;
+    SElem* E = dbuf<SElem>(ctx, "sort_e", R);
+    SElem* T = dbuf<SElem>(ctx, "sort_t", R);
+    uint64_t* newkey = dbuf<uint64_t>(ctx, "sort_newkey", R + 1);
+    uint64_t* newkey_ex = dbuf<uint64_t>(ctx, "sort_newkey_ex", R + 1);
+    uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "sort_rank_scan", scan_tmp_words(R) + 64);
+    launch_sort_load(st, R, hi, lo, addr, klen, E, last_wins);
+    const SElem* S = sort_elems(ctx, E, T, R, 0, newkey);
+    launch_scan(st, newkey, R, newkey_ex, scan_tmp);
+    uint64_t* nhi = dbuf<uint64_t>(ctx, "srt_hi", R);
+    uint64_t* nlo = dbuf<uint64_t>(ctx, "srt_lo", R);
+    uint64_t* naddr = dbuf<uint64_t>(ctx, "srt_addr", R);
+    uint32_t* nklen = dbuf<uint32_t>(ctx, "srt_klen", R);
+    uint32_t* ncklen = dbuf<uint32_t>(ctx, "srt_cklen", R);
+    uint32_t* nmeta = dbuf<uint32_t>(ctx, "srt_meta", R);
+    launch_sort_store(st, R, S, meta, newkey, newkey_ex, nhi, nlo, naddr, nklen, ncklen, nmeta, last_wins);
+    HIPCHK(hipGetLastError());
+    if (sorted) *sorted = S;
+    hi = nhi;
+    lo = nlo;
+    addr = naddr;
+    klen = nklen;
+    meta = nmeta;
+    cmp_klen = ncklen;
+}
+
+void ensure_aux(skv_ctx* ctx) {  // the ctx's second stream and its two events
+    if (ctx->aux_stream) return;
+    HIPCHK(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&ctx->aux_ev[0], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ctx->aux_ev[1], hipEventDisableTiming));
+}
+
+// allow_deferred: on the fixed-stride fast path, launch the merge without waiting for the parse's
+// verdict (broken runs / order errors / oversized records) and check it with the final readback;
+// a bad verdict discards the result and reruns the call on the exact general path.
+int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_deferred) {
+    hipStream_t st = ctx->stream;
+    // nothing of an earlier call may still read this ctx's buffers on the aux stream
+    if (ctx->aux_stream) HIPCHK(hipStreamSynchronize(ctx->aux_stream));
+    ctx->syncs = 0;
+    ctx->up_chunk = 0;
+    ctx->up_off = 0;
+    mark(ctx, PH_START);
+    htrace("start");
+    const uint32_t k = (uint32_t)job.ranked.size();
+    const uint64_t my_gen = ++ctx->table_gen;
+    auto tables_mine = [&]() {  // the s_* tables below are ctx storage that a nested call refills
+        if (ctx->table_gen != my_gen) throw DevError("internal: host tables read after a nested rerun refilled them");
+    };
+    // ---- run table ------------------------------------------------------------------------
+    std::vector<RunInfo>& runs = ctx->s_runs;  // (a rerun returns right after its nested call)
+    runs.resize(job.run_ptr.size());  // same size as the last call: no fill
+    std::vector<uint32_t>& stream_first_run = ctx->s_sfr;
+    stream_first_run.resize(k + 1);
+    // speculative walk length: CHUNK, doubled up to 4x while a call still has >= 2^20 walks (a big
+    // call spends fewer re-synchronising starts per record; 4 KiB walks of 64 GB: 56 ms, 16 KiB: 44)
+    uint64_t chunk = CHUNK;
+    if (const char* ce = getenv("SKV_CHUNK_BYTES"))  // slot offsets are 16-bit: at most 64 KiB
+        chunk = std::min<uint64_t>(65536, std::max<uint64_t>(CHUNK, strtoull(ce, nullptr, 10)));
+    else
+        while (chunk < 4 * CHUNK && job.in_bytes / (2 * chunk) >= (1ull << 20)) chunk *= 2;
+    auto n_chunks_of = [chunk](uint64_t len) { return len >= 2 ? (uint32_t)((len - 1 + chunk - 1) / chunk) : 0u; };
+    uint64_t n_chunks = 0;
+    {  // blocks of streams (rank order) on host threads: runs and chunks before each block, then fill
+        const unsigned nb = par_nblocks(k);
+        std::vector<uint64_t> rb(nb + 1, 0), cb(nb + 1, 0);
+        par_run(k, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+            uint64_t nr = 0, nc = 0;
+            for (uint64_t s = lo; s < hi; ++s) {
+                const InStream& S = job.ranked[s];
+                nr += S.n_runs;
+                for (uint32_t m = 0; m < S.n_runs; ++m) nc += n_chunks_of(job.run_len[S.first + m]);
+            }
+            rb[b + 1] = nr;
+            cb[b + 1] = nc;
+        });
+        for (unsigned b = 0; b < nb; ++b) {
+            rb[b + 1] += rb[b];
+            cb[b + 1] += cb[b];
+        }
+        par_run(k, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+            uint64_t at = rb[b], nc = cb[b];
+            for (uint64_t s = lo; s < hi; ++s) {
+                stream_first_run[s] = (uint32_t)at;
+                const InStream& S = job.ranked[s];
+                for (uint32_t m = 0; m < S.n_runs; ++m, ++at) {
+                    RunInfo& R = runs[at];
+                    R.ptr = job.run_ptr[S.first + m];
+                    R.len = job.run_len[S.first + m];
+                    R.chunk_base = nc;
+                    R.n_chunks = n_chunks_of(R.len);
+                    R.stream = (uint32_t)s;
+                    nc += R.n_chunks;
+                }
+            }
+        });
+        n_chunks = cb[nb];
+    }
+    stream_first_run[k] = (uint32_t)runs.size();
+    const uint32_t n_runs = (uint32_t)runs.size();
+    htrace("run table built");
+
+    RunInfo* d_runs = dbuf<RunInfo>(ctx, "runs", n_runs);
+    uint32_t* d_hdr = dbuf<uint32_t>(ctx, "hdr_err", n_runs);
+    uint64_t* ch_start = dbuf<uint64_t>(ctx, "ch_start", n_chunks);
+    uint64_t* ch_end = dbuf<uint64_t>(ctx, "ch_end", n_chunks);
+    uint32_t* ch_cnt = dbuf<uint32_t>(ctx, "ch_cnt", n_chunks);
+    uint32_t* ch_err = dbuf<uint32_t>(ctx, "ch_err", n_chunks);
+    unsigned long long* bad_bits = dbuf<unsigned long long>(ctx, "bad_bits", n_chunks / 64 + 1);
+    uint32_t* first_bad = dbuf<uint32_t>(ctx, "first_bad", n_runs);
+    uint32_t* err_chunk = dbuf<uint32_t>(ctx, "err_chunk", n_runs);
+    uint64_t* cnt64 = dbuf<uint64_t>(ctx, "cnt64", n_chunks);
+    uint64_t* ch_rec_base = dbuf<uint64_t>(ctx, "ch_rec_base", n_chunks + 1);
+    uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "scan_tmp", scan_tmp_words(std::max<uint64_t>(n_chunks, 1 << 20)) + 64);
+    RunSummary* d_sum = dbuf<RunSummary>(ctx, "run_sum", n_runs);
+    htrace("buffers");
+
+    h2d_up(ctx, d_runs, runs.data(), n_runs * sizeof(RunInfo));
+    htrace("runs uploaded");
+    RunFmt* d_fmt = dbuf<RunFmt>(ctx, "run_fmt", n_runs);
+    uint32_t* d_broken = dbuf<uint32_t>(ctx, "run_broken", n_runs);
+    uint64_t* d_recb = dbuf<uint64_t>(ctx, "run_recb", n_runs + 1);
+    HIPCHK(hipMemsetAsync(d_broken, 0, (size_t)n_runs * 4, st));
+    launch_run_header(st, d_runs, n_runs, d_hdr, d_fmt);
+
+    std::vector<RunSummary>& sum = ctx->s_sum;
+    sum.resize(n_runs);  // every entry is written by whichever parse runs
+    std::vector<uint64_t>& stream_base = ctx->s_sbase;
+    std::vector<uint64_t>& stream_valid = ctx->s_svalid;
+    std::vector<uint32_t>& stream_err = ctx->s_serr;
+    stream_base.resize(k + 1);  // written by stream_tables() before any read
+    stream_valid.resize(k);
+    stream_err.resize(k);
+    bool any_err = false;
+    uint64_t R = 0;
+    uint64_t* rec_addr = nullptr;
+    uint64_t* rec_hi = nullptr;
+    uint64_t* rec_lo = nullptr;
+    uint32_t* rec_klen = nullptr;
+    uint32_t* rec_meta = nullptr;
+    uint64_t* rec_fp = nullptr;  // fingerprints of the key bytes past 16 (written by the emit kernels)
+    uint32_t* utf8_bad = dbuf<uint32_t>(ctx, "utf8_bad", 1);
+    uint32_t* d_flags = dbuf<uint32_t>(ctx, "flags", 4);
+    uint64_t* d_stream_base = dbuf<uint64_t>(ctx, "stream_base", k + 1);
+    unsigned long long* d_first_dec = dbuf<unsigned long long>(ctx, "first_dec", k);
+    std::vector<uint64_t>& first_dec = ctx->s_first_dec;
+    first_dec.resize(k);  // read back, or filled with ~0 on the deferred path
+    uint32_t hflags[4];
+    // per stream (rank order): base index, valid record count n_s and the first error
+    auto stream_tables = [&]() {  // blocks of streams on host threads (10^6-stream calls)
+        const unsigned nb = par_nblocks(k);
+        std::vector<uint8_t> blk_err(nb, 0);
+        const uint64_t acc = par_scan(
+            k,
+            [&](uint64_t lo, uint64_t hi) {
+                uint64_t a = 0;
+                for (uint32_t r = stream_first_run[lo]; r < stream_first_run[hi]; ++r) a += sum[r].records;
+                return a;
+            },
+            [&](unsigned b, uint64_t lo, uint64_t hi, uint64_t acc) {
+                for (uint64_t s = lo; s < hi; ++s) {
+                    stream_base[s] = acc;
+                    uint64_t valid = 0;
+                    bool dead = false;
+                    stream_err[s] = 0;
+                    for (uint32_t r = stream_first_run[s]; r < stream_first_run[s + 1]; ++r) {
+                        acc += sum[r].records;
+                        if (!dead) {
+                            valid += sum[r].records;
+                            if (sum[r].err) {
+                                stream_err[s] = sum[r].err;
+                                dead = true;
+                                blk_err[b] = 1;
+                            }
+                        }
+                    }
+                    stream_valid[s] = valid;
+                }
+            });
+        for (uint8_t e : blk_err) any_err = any_err || e;
+        stream_base[k] = acc;
+        if (acc != R) throw DevError("internal: record count mismatch");
+    };
+    auto alloc_records = [&]() {
+        rec_addr = dbuf<uint64_t>(ctx, "rec_addr", R);
+        rec_hi = dbuf<uint64_t>(ctx, "rec_hi", R);
+        rec_lo = dbuf<uint64_t>(ctx, "rec_lo", R);
+        rec_klen = dbuf<uint32_t>(ctx, "rec_klen", R);
+        rec_meta = dbuf<uint32_t>(ctx, "rec_meta", R);
+        rec_fp = dbuf<uint64_t>(ctx, "rec_fp", R);
+        HIPCHK(hipMemsetAsync(d_flags, 0, 16, st));
+        HIPCHK(hipMemsetAsync(utf8_bad, 0, 4, st));
+        HIPCHK(hipMemsetAsync(d_first_dec, 0xFF, (size_t)k * 8, st));
+        h2d_up(ctx, d_stream_base, stream_base.data(), (k + 1) * 8);
+    };
+    uint32_t utf8_flag = 0;
+    // order check + readback of its result, the record flags and (fast path) the broken-run flags
+    auto check_and_read = [&](bool read_broken) -> bool {
+        // the fast path's parse kernel already did the order check
+        if (!read_broken && !job.batch)  // a writer batch is unsorted by definition
+            launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
+        HIPCHK(hipGetLastError());
+        uint8_t* hp = (uint8_t*)pinned(ctx, k * 8 + 16 + (read_broken ? n_runs * 4 : 0) + 16);
+        d2h(ctx, hp, d_first_dec, (size_t)k * 8);
+        d2h(ctx, hp + (size_t)k * 8, d_flags, 16);
+        uint8_t* hu = hp + k * 8 + 16 + (read_broken ? n_runs * 4 : 0);
+        d2h(ctx, hu, utf8_bad, 4);
+        if (read_broken) d2h(ctx, hp + (size_t)k * 8 + 16, d_broken, (size_t)n_runs * 4);
+        sync(ctx);
+        memcpy(first_dec.data(), hp, (size_t)k * 8);
+        memcpy(hflags, hp + (size_t)k * 8, 16);
+        memcpy(&utf8_flag, hu, 4);
+        bool broken = false;
+        if (read_broken) {
+            const uint32_t* b = (const uint32_t*)(hp + (size_t)k * 8 + 16);
+            for (uint32_t r = 0; r < n_runs && !broken; ++r) broken = b[r] != 0;
+        }
+        return broken;
+    };
+
+    // ---- fast path: every run fixed-stride (one record size per run) -> one verifying pass ------
+    bool parsed = false, deferred = false;
+    bool any_fixed = false;  // some run is fixed-stride: the general parse also runs k_emit_fixed
+    {
+        RunFmt* hf = (RunFmt*)pinned(ctx, (size_t)n_runs * sizeof(RunFmt) + 16);
+        d2h(ctx, hf, d_fmt, (size_t)n_runs * sizeof(RunFmt));
+        htrace("header launched");
+        sync(ctx);
+        htrace("header synced");
+        htrace("run formats read");
+        // blocks of runs on host threads: every run fixed-stride? one format everywhere?
+        const unsigned nbr = par_nblocks(n_runs);
+        std::vector<uint8_t> blk_fixed(nbr, 1), blk_uni(nbr, 1), blk_any(nbr, 0);
+        par_run(n_runs, nbr, [&](unsigned b, uint64_t lo, uint64_t hi) {
+            bool fx = true, un = true, an = false;
+            for (uint64_t r = lo; r < hi; ++r) {
+                fx = fx && hf[r].S != 0;
+                an = an || hf[r].S != 0;
+                un = un && hf[r].S == hf[0].S && hf[r].K == hf[0].K;
+            }
+            blk_fixed[b] = fx;
+            blk_uni[b] = un;
+            blk_any[b] = an;
+        });
+        bool all_fixed = n_runs > 0, uniform = true;
+        for (unsigned b = 0; b < nbr; ++b) {
+            all_fixed = all_fixed && blk_fixed[b];
+            uniform = uniform && blk_uni[b];
+            any_fixed = any_fixed || blk_any[b];
+        }
+        if (all_fixed) {
+            std::vector<uint64_t>& recb = ctx->s_recb;
+            recb.resize(n_runs + 1);
+            recb[0] = 0;
+            R = par_scan(
+                n_runs,
+                [&](uint64_t lo, uint64_t hi) {
+                    uint64_t a = 0;
+                    for (uint64_t r = lo; r < hi; ++r) a += (runs[r].len - 1) / hf[r].S;
+                    return a;
+                },
+                [&](unsigned, uint64_t lo, uint64_t hi, uint64_t acc) {
+                    for (uint64_t r = lo; r < hi; ++r) {
+                        sum[r].records = (runs[r].len - 1) / hf[r].S;
+                        sum[r].err = 0;
+                        sum[r].pad = 0;
+                        acc += sum[r].records;
+                        recb[r + 1] = acc;
+                    }
+                });
+            // one record size and one key length <= 16 everywhere: the fused stride path
+            const RunFmt f0 = hf[0];
+            const char* fenv = getenv("SKV_FUSED");
+            if (allow_deferred && uniform && !job.batch && !job.search && !(job.flags & SKV_SPLIT_BY_TABLE) &&
+                !(fenv && fenv[0] == '0') &&
+                f0.K <= FX_MAX_K && f0.S >= FX_MIN_S && f0.S <= FX_MAX_S && k <= (uint32_t)TILE_TARGET / 2 &&
+                R < 0xFFFFFFFFull) {
+                if (compact_fused(ctx, job, runs, d_runs, stream_first_run, f0, recb, out)) return SKV_OK;
+                return compact_device(ctx, job, out, false);
+            }
+            stream_tables();
+            alloc_records();
+            htrace("record tables");
+            h2d_up(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
+            launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
+                               rec_meta, d_flags, d_stream_base, job.batch ? nullptr : d_first_dec, rec_fp,
+                               dbuf<uint32_t>(ctx, "wave_run", (R + 63) / 64 + 1));
+            mark(ctx, PH_PARSE);
+            if (allow_deferred && !(job.flags & SKV_SPLIT_BY_TABLE) && !job.search) {
+                deferred = true;  // verdict read with the result
+                parsed = true;
+                std::fill(first_dec.begin(), first_dec.end(), ~0ull);
+                memset(hflags, 0, sizeof hflags);
+            } else {
+                parsed = !check_and_read(true);
+                htrace("parse verdict read");
+            }
+            if (!parsed) {  // a run is not what its first record promised: general parse
+                R = 0;
+                any_err = false;
+                std::fill(stream_err.begin(), stream_err.end(), 0u);
+            }
+        }
+    }
+    // ---- general path: speculative chunk walks ----------------------------------------------
+    if (!parsed) {
+        // record starts of each chunk as the walks find them (16-bit offsets), chunk / 64 per chunk:
+        // k_emit parses the records of a chunk in parallel instead of walking its chain again
+        const uint32_t slot_cap = (uint32_t)((chunk / 64 + 7) & ~7ull);  // rows of 16-byte groups (walk_fast)
+        uint16_t* ch_slots = dbuf<uint16_t>(ctx, "ch_slots", n_chunks * slot_cap);
+        HIPCHK(hipMemsetAsync(bad_bits, 0, (n_chunks / 64 + 1) * 8, st));
+        HIPCHK(hipMemsetAsync(first_bad, 0xFF, n_runs * 4, st));
+        HIPCHK(hipMemsetAsync(err_chunk, 0xFF, n_runs * 4, st));
+        launch_spec(st, d_runs, n_runs, n_chunks, d_hdr, d_fmt, d_broken, ch_start, ch_end, ch_cnt, ch_err,
+                    ctx->exact_utf8, chunk, ch_slots, slot_cap);
+        launch_validate(st, d_runs, n_runs, n_chunks, d_hdr, ch_start, ch_end, ch_err, bad_bits, first_bad);
+        launch_fixup(st, d_runs, n_runs, d_hdr, first_bad, bad_bits, ch_start, ch_end, ch_cnt, ch_err,
+                     ctx->exact_utf8, chunk, ch_slots, slot_cap);
+        launch_err_chunk(st, d_runs, n_runs, n_chunks, d_hdr, ch_err, err_chunk);
+        launch_mask(st, d_runs, n_runs, n_chunks, d_hdr, err_chunk, ch_cnt, cnt64);
+        launch_scan(st, cnt64, n_chunks, ch_rec_base, scan_tmp);
+        launch_run_summary(st, d_runs, n_runs, d_hdr, err_chunk, ch_err, ch_rec_base, d_sum, d_recb);
+        HIPCHK(hipGetLastError());
+        {
+            RunSummary* hs = (RunSummary*)pinned(ctx, n_runs * sizeof(RunSummary) + 16);
+            d2h(ctx, hs, d_sum, n_runs * sizeof(RunSummary));
+            d2h(ctx, (uint8_t*)hs + n_runs * sizeof(RunSummary), ch_rec_base + n_chunks, 8);
+            sync(ctx);
+            memcpy(sum.data(), hs, n_runs * sizeof(RunSummary));
+            memcpy(&R, (uint8_t*)hs + n_runs * sizeof(RunSummary), 8);
+        }
+        stream_tables();
+        alloc_records();
+        launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, any_fixed ? R : 0,
+                    rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad, ch_slots, slot_cap, chunk);
+        mark(ctx, PH_PARSE);
+        check_and_read(false);
+        if (utf8_flag && !ctx->exact_utf8) {  // a key the chunk walks did not check: exact walks
+            ctx->exact_utf8 = true;
+            int rc;
+            try {
+                rc = compact_device(ctx, job, out, false);
+            } catch (...) {
+                ctx->exact_utf8 = false;
+                throw;
+            }
+            ctx->exact_utf8 = false;
+            return rc;
+        }
+    }
+    mark(ctx, PH_CHECK);
+    htrace("check done");
+    tables_mine();
+    if (job.search) return search_stage(ctx, job, runs[0], R, stream_err[0], first_dec[0], rec_addr, rec_hi, rec_lo,
+                                        rec_klen, rec_meta);
+    bool any_dec = false;
+    for (uint32_t s = 0; s < k; ++s)
+        if (first_dec[s] != ~0ull && first_dec[s] + 1 < stream_valid[s]) any_dec = true;
+
+    // ---- errors: which one k_way::merge surfaces first --------------------------------------
+    // Heap-order mode (skv_heap.hip) where the outcome depends on the merge's exact pop sequence
+    // past a stream's first key decrease or decode error: the WAL split with either, and the Delete
+    // filter with a decrease. Everywhere else the first trigger record decides (below).
+    const bool wal = (job.flags & SKV_SPLIT_BY_TABLE) != 0;
+    const bool heap = !job.batch && ((wal && (any_err || any_dec)) || ((job.flags & SKV_DROP_TOMBSTONES) && any_dec));
+    HeapRes hres;
+    if (any_err || any_dec) {
+        // (1) first items are pulled in the caller's vector order (k_way.rs:126-140)
+        std::vector<uint32_t> by_vec(k);
+        for (uint32_t s = 0; s < k; ++s) by_vec[job.ranked[s].vec_idx] = s;
+        for (uint32_t v = 0; v < k; ++v) {
+            uint32_t s = by_vec[v];
+            if (stream_valid[s] == 0 && stream_err[s]) {
+                std::string msg;
+                int code = derr_to_api(stream_err[s], msg);
+                throw ApiError{code, msg};
+            }
+        }
+        if (heap) {
+            for (uint32_t s = 0; s < k; ++s)
+                if (stream_err[s]) hres.dec.push_back({stream_base[s] + stream_valid[s] - 1, stream_err[s]});
+        }
+    }
+    if ((any_err || any_dec) && !heap) {
+        // (2) each stream's earliest trigger item; the one popped first wins
+        struct Cand { uint32_t s; uint64_t idx; bool order; std::string key; };
+        std::vector<Cand> cands;
+        bool any_order = false;
+        for (uint32_t s = 0; s < k; ++s) {
+            uint64_t trig = ~0ull;
+            bool order = false;
+            if (first_dec[s] != ~0ull && first_dec[s] + 1 < stream_valid[s]) { trig = first_dec[s]; order = true; }
+            if (stream_err[s] && stream_valid[s] > 0) {
+                uint64_t t2 = stream_valid[s] - 1;
+                if (t2 < trig) { trig = t2; order = false; }
+            }
+            if (trig == ~0ull) continue;
+            any_order |= order;
+            cands.push_back({s, trig, order, fetch_key(ctx, rec_addr, rec_klen, stream_base[s] + trig)});
+        }
+        if (cands.empty()) throw DevError("internal: error without trigger");
+        // pop order: key ascending, then seq_no descending (== smaller rank)
+        std::sort(cands.begin(), cands.end(), [](const Cand& a, const Cand& b) {
+            if (a.key != b.key) return a.key < b.key;
+            return a.s < b.s;
+        });
+        const Cand& w = cands[0];
+        (void)any_order;
+        if (w.order) throw ApiError{SKV_E_FORMAT, "Data format error: Operations must be sorted by key"};
+        std::string msg;
+        int code = derr_to_api(stream_err[w.s], msg);
+        throw ApiError{code, msg};
+    }
+    if (hflags[0]) throw ApiError{SKV_E_UNSUPPORTED, "record of 2 GiB or more: unsupported by this build"};
+    if (R == 0) {  // nothing survives: build_runs yields no run (runs.rs:270-271)
+        ResultBox* box = new ResultBox();
+        box->pub.runs = (skv_run_desc*)malloc(sizeof(skv_run_desc));
+        box->pub.bytes = dbuf<uint8_t>(ctx, "out", 16);
+        box->pub.in_bytes = job.in_bytes;
+        mark(ctx, PH_MERGE);
+        mark(ctx, PH_CHAIN);
+        mark(ctx, PH_GATHER);
+        ctx->timings = skv_timings{};
+        ctx->timings.host_syncs = ctx->syncs;
+        *out = &box->pub;
+        return SKV_OK;
+    }
+    if (R >= 0xFFFFFFFFull) throw ApiError{SKV_E_UNSUPPORTED, "more than 2^32-1 records in one compaction"};
+
+    // ---- merge ------------------------------------------------------------------------------
+    struct Level {
+        uint64_t N = 0, S = 1;
+        std::vector<uint64_t> off;  // k+1 list offsets
+        uint64_t* hi = nullptr;
+        uint64_t* lo = nullptr;
+        uint64_t* c = nullptr;       // level > 0
+        uint64_t* d_off = nullptr;
+        // sorted output (level > 0)
+        uint64_t* shi = nullptr;
+        uint64_t* slo = nullptr;
+        uint64_t* sc = nullptr;
+    };
+    // Past TILE_TARGET / 2 streams the records are sorted into one list first (skv_sort.hip);
+    // SKV_SORT=1 forces that path (tests).
+    uint32_t km = k;  // lists the splitter merge sees
+    const uint32_t* cmp_klen = rec_klen;  // key lengths the merge compares (dense ranks: 0)
+    // the keys the merge orders by: the records' own, or (heap-order mode with a key decrease) each
+    // record's stream-prefix-maximum record's (skv_heap.hip)
+    uint64_t* cmp_hi = rec_hi;
+    uint64_t* cmp_lo = rec_lo;
+    const uint64_t* cmp_addr = rec_addr;
+    uint64_t* pop_pos = nullptr;
+    if (heap) {
+        // the fixed-stride parse poisons the merge on a key decrease (k_emit_fixed); here the
+        // decrease is what this mode merges exactly (broken runs never get this far: they reparse)
+        HIPCHK(hipMemsetAsync(d_flags + 2, 0, 4, st));
+        pop_pos = dbuf<uint64_t>(ctx, "heap_pop_pos", R);
+        // always the prefix-maximum keys: a stream may be unsorted past its decode error (records of
+        // later member runs), which any_dec does not see, and those records are merged too
+        {
+            uint32_t* eff = dbuf<uint32_t>(ctx, "heap_eff", R);
+            uint64_t* blk = dbuf<uint64_t>(ctx, "heap_blk", heap_key_blocks(R));
+            uint32_t* carry = dbuf<uint32_t>(ctx, "heap_carry", heap_key_blocks(R));
+            uint64_t* ehi = dbuf<uint64_t>(ctx, "heap_hi", R);
+            uint64_t* elo = dbuf<uint64_t>(ctx, "heap_lo", R);
+            uint32_t* ekl = dbuf<uint32_t>(ctx, "heap_klen", R);
+            uint64_t* ead = dbuf<uint64_t>(ctx, "heap_addr", R);
+            launch_heap_keys(st, R, d_stream_base, k, rec_hi, rec_lo, rec_klen, rec_addr, eff, blk, carry, ehi, elo, ekl,
+                             ead);
+            cmp_hi = ehi;
+            cmp_lo = elo;
+            cmp_klen = ekl;
+            cmp_addr = ead;
+        }
+    }
+    std::vector<uint64_t> list_off = stream_base;
+    uint64_t* d_list_off = d_stream_base;
+    {
+        const char* se = getenv("SKV_SORT");
+        if ((k > (uint32_t)TILE_TARGET / 2 && R > (uint64_t)TILE_CAP) || (se && se[0] == '1') || job.batch) {
+            if (heap) {
+                // sort on the merge keys; the records' own keys, payload and meta follow in sorted
+                // order, and inv maps an original record index to its sorted position
+                uint64_t *h2 = cmp_hi, *l2 = cmp_lo, *a2 = (uint64_t*)cmp_addr;
+                uint32_t* k2 = (uint32_t*)cmp_klen;
+                uint32_t* m2 = rec_meta;
+                const uint32_t* ck = nullptr;
+                const SElem* S = nullptr;
+                sort_records(ctx, R, h2, l2, a2, k2, m2, ck, false, &S);
+                uint64_t* shi = dbuf<uint64_t>(ctx, "heap_s_hi", R);
+                uint64_t* slo = dbuf<uint64_t>(ctx, "heap_s_lo", R);
+                uint32_t* skl = dbuf<uint32_t>(ctx, "heap_s_klen", R);
+                uint64_t* sad = dbuf<uint64_t>(ctx, "heap_s_addr", R);
+                uint32_t* inv = dbuf<uint32_t>(ctx, "heap_inv", R);
+                launch_heap_sorted(st, R, S, rec_hi, rec_lo, rec_klen, rec_addr, shi, slo, skl, sad, inv);
+                rec_hi = shi;
+                rec_lo = slo;
+                rec_klen = skl;
+                rec_addr = sad;
+                rec_meta = m2;
+                cmp_hi = h2;
+                cmp_lo = l2;
+                cmp_addr = a2;
+                cmp_klen = ck;
+                hres.inv = inv;
+            } else {
+                sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen, job.batch);
+                cmp_hi = rec_hi;
+                cmp_lo = rec_lo;
+                cmp_addr = rec_addr;
+            }
+            htrace("sort launched");
+            km = 1;
+            list_off = {0, R};
+            d_list_off = dbuf<uint64_t>(ctx, "sorted_off", 2);
+            h2d_up(ctx, d_list_off, list_off.data(), 16);
+            ctx->timings.sorted = 1;
+        }
+    }
+    std::vector<Level> lv(1);
+    lv[0].N = R;
+    lv[0].off = list_off;
+    lv[0].hi = cmp_hi;
+    lv[0].lo = cmp_lo;
+    lv[0].d_off = d_list_off;
+    const uint64_t S_step = std::max<uint64_t>(2, (uint64_t)TILE_TARGET / std::max<uint32_t>(km, 1));
+    // SKV_HI_STEP=f: levels >= 2 (they only pick splitters for the sample sorts) at an f times
+    // coarser step. Measured at config 3 with f = 2: one sample level fewer, but the merge phase
+    // 4.02 vs 3.26 ms (the level-1 sample tiles lose their balance), so the default is 1.
+    const char* hse = getenv("SKV_HI_STEP");
+    const uint64_t hi_f = hse ? std::max<uint64_t>(1, strtoull(hse, nullptr, 10)) : 1;
+    // Level 1 (the level-0 tiles' splitters) at twice the step from 128 lists on: a tile's size
+    // spreads by ~sqrt(k) x step / 2.4 records around TILE_TARGET, which at k >= 128 stays under
+    // 1/4.6 of the TILE_CAP margin, and half the samples halve their sort (3F merge 27.3 -> 25.7 ms,
+    // config 3 2.22 -> 1.92 ms; a step of 3 unbalanced the tiles: 31.4 ms). SKV_L1_STEP=f overrides.
+    const char* l1e = getenv("SKV_L1_STEP");
+    const uint64_t l1_f = l1e ? std::max<uint64_t>(1, strtoull(l1e, nullptr, 10)) : (km >= 128 ? 2 : 1);
+    while (lv.back().N > (uint64_t)TILE_CAP) {
+        const Level& P = lv.back();
+        Level L;
+        L.S = lv.size() >= 2 ? S_step * hi_f : S_step * l1_f;
+        L.off.resize(km + 1);
+        uint64_t acc = 0;
+        for (uint32_t j = 0; j < km; ++j) {
+            L.off[j] = acc;
+            uint64_t nj = P.off[j + 1] - P.off[j];
+            acc += (nj + L.S - 1) / L.S;
+        }
+        L.off[km] = acc;
+        L.N = acc;
+        char nm[64];
+        int li = (int)lv.size();
+        snprintf(nm, sizeof nm, "lv%d_hi", li); L.hi = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "lv%d_lo", li); L.lo = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "lv%d_c", li); L.c = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "lv%d_off", li); L.d_off = dbuf<uint64_t>(ctx, nm, km + 1);
+        h2d_up(ctx, L.d_off, L.off.data(), (km + 1) * 8);
+        launch_sample(st, li == 1, P.hi, P.lo, P.c, cmp_klen, P.d_off, L.d_off, km, L.S, L.N, L.hi, L.lo, L.c);
+        lv.push_back(L);
+    }
+    // top-down: sort each sample level, derive splitters for the level below
+    uint64_t T0 = 1;
+    uint32_t* m_rec = dbuf<uint32_t>(ctx, "m_rec", R + 1);
+    uint64_t* m_src = dbuf<uint64_t>(ctx, "m_src", R + 1);
+    uint64_t* m_P = dbuf<uint64_t>(ctx, "m_P", R + 1);
+    uint64_t* m_Dp = dbuf<uint64_t>(ctx, "m_Dp", R + 1);
+    uint64_t* d_Kout = dbuf<uint64_t>(ctx, "K_out", 1);
+    uint32_t* tile_max = nullptr;
+    // fingerprints of the key bytes past 16 for the level-0 merge rounds (SKV_FP_TEST=1: all zero,
+    // so every same-length key pair with one prefix is taken as equal and the exact check must catch it)
+    const uint64_t* key_fp = nullptr;
+    uint32_t* fp_bad = dbuf<uint32_t>(ctx, "fp_bad", 1);
+    HIPCHK(hipMemsetAsync(fp_bad, 0, 4, st));
+    // k_fp_verify's inputs once the level-0 tiles are queued; it runs on the ctx stream before the
+    // WAL stage, or on the aux stream beside the gather (its verdict is read with the result)
+    std::pair<const unsigned long long*, const uint64_t*> verify_args{nullptr, nullptr};
+    const unsigned long long* verify_lo = nullptr;  // pairs before it verified beside the merge
+    bool verify_pending = false;
+    if (km > 1 && !ctx->exact_keys && !heap) {
+        const char* te = getenv("SKV_FP_TEST");
+        if (te && te[0] == '1') {
+            uint64_t* f = dbuf<uint64_t>(ctx, "rec_fp_test", R);
+            HIPCHK(hipMemsetAsync(f, 0, R * 8, st));
+            key_fp = f;
+        } else {
+            key_fp = rec_fp;  // written by the emit kernels with the record arrays
+        }
+    }
+    for (int li = (int)lv.size() - 1; li >= 0; --li) {
+        Level& L = lv[li];
+        const bool l0 = li == 0;
+        uint64_t T = 1, m = 1;
+        if (li + 1 < (int)lv.size()) {
+            m = std::max<uint64_t>(1, (uint64_t)TILE_TARGET / lv[li + 1].S);
+            T = std::max<uint64_t>(1, (lv[li + 1].N + m - 1) / m);
+        }
+        char nm[64];
+        snprintf(nm, sizeof nm, "bounds%d", li);
+        uint64_t* bounds = dbuf<uint64_t>(ctx, nm, (T + 1) * km);
+        const Level* U = li + 1 < (int)lv.size() ? &lv[li + 1] : nullptr;
+        L1Cnt C{};
+        if (l0 && U && T > 1) {  // level 0: each search starts inside one level-1 sample gap
+            uint32_t* posof = dbuf<uint32_t>(ctx, "l1_posof", U->N);
+            uint32_t* cnt = dbuf<uint32_t>(ctx, "l1_cnt", (T + 1) * km);
+            launch_l1_cnt(st, U->sc, U->N, L.d_off, U->d_off, km, U->S, m, T, posof, cnt);
+            C = L1Cnt{cnt, U->d_off, U->hi, U->lo, U->c, U->S};
+        }
+        launch_bounds(st, l0, L.hi, L.lo, L.c, cmp_klen, L.d_off, km, U ? U->shi : nullptr, U ? U->slo : nullptr,
+                      U ? U->sc : nullptr, m, T, cmp_addr, bounds, d_flags + 2, C.cnt ? &C : nullptr);
+        snprintf(nm, sizeof nm, "tile_n%d", li);
+        uint64_t* tile_n = dbuf<uint64_t>(ctx, nm, T);
+        snprintf(nm, sizeof nm, "tile_base%d", li);
+        uint64_t* tile_base = dbuf<uint64_t>(ctx, nm, T + 1);
+        launch_tile_n(st, bounds, km, T, tile_n);
+        launch_scan(st, tile_n, T, tile_base, scan_tmp);
+        TileOut O{};
+        snprintf(nm, sizeof nm, "x%d_hi", li); O.xhi = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "x%d_lo", li); O.xlo = dbuf<uint64_t>(ctx, nm, L.N);
+        snprintf(nm, sizeof nm, "x%d_c", li); O.xc = dbuf<uint64_t>(ctx, nm, L.N);
+        if (l0) {
+            O.xmeta = dbuf<uint32_t>(ctx, "x0_meta", L.N);
+            O.m_rec = m_rec;
+            O.m_src = m_src;
+            O.m_P = m_P;
+            O.m_Dp = m_Dp;
+            O.Kout = d_Kout;
+            O.T = T;
+            tile_max = O.tile_mm = dbuf<uint32_t>(ctx, "tile_mm", 2 * T);  // (min, max) record size per tile
+            O.key_fp = key_fp;
+            O.fp_bad = fp_bad;
+            if (key_fp) {  // pairs taken as equal by fingerprint, verified after the tiles
+                O.vpairs = dbuf<uint64_t>(ctx, "fp_vpairs", 2 * R);
+                O.vcount = dbuf<unsigned long long>(ctx, "fp_vcount", 1);
+                HIPCHK(hipMemsetAsync(O.vcount, 0, 8, st));
+            }
+            O.tstate = dbuf<uint64_t>(ctx, "tile_state", 3 * T);
+            O.tcounter = dbuf<uint32_t>(ctx, "tile_ticket", 1);
+            if (heap) {
+                O.pay_addr = rec_addr;
+                O.act_hi = rec_hi;
+                O.act_lo = rec_lo;
+                O.act_klen = rec_klen;
+                O.pop_pos = pop_pos;
+            }
+            HIPCHK(hipMemsetAsync(O.tstate, 0, 3 * T * 8, st));
+            HIPCHK(hipMemsetAsync(O.tcounter, 0, 4, st));
+#if SKV_TILE_PROF
+            O.prof = dbuf<uint64_t>(ctx, "tile_prof", 16);
+            if (!ctx->prof_init) {
+                HIPCHK(hipMemsetAsync(O.prof, 0, 128, st));
+                ctx->prof_init = true;
+            }
+#endif
+        } else {
+            snprintf(nm, sizeof nm, "s%d_hi", li); L.shi = O.ohi = dbuf<uint64_t>(ctx, nm, L.N);
+            snprintf(nm, sizeof nm, "s%d_lo", li); L.slo = O.olo = dbuf<uint64_t>(ctx, nm, L.N);
+            snprintf(nm, sizeof nm, "s%d_c", li); L.sc = O.oc = dbuf<uint64_t>(ctx, nm, L.N);
+        }
+        const uint32_t drop = (job.flags & SKV_DROP_TOMBSTONES) ? 1u : 0u;
+        // SKV_FP_PIECE_MIN=T: split level 0 from T tiles on (off by default: at 3F the verify beside
+        // the merge pieces slowed the merge by what it saved beside the gather, 89.6 vs 89.3 ms)
+        const char* pme = getenv("SKV_FP_PIECE_MIN");
+        const uint64_t piece_min = pme ? std::max<uint64_t>(1, strtoull(pme, nullptr, 10)) : ~0ull;
+        if (l0 && key_fp && T >= piece_min && T >= 4) {
+            // Level 0 in FP_PIECES launches (tickets continue across them): after each piece but
+            // the last, a one-lane kernel snapshots the pair count, and k_fp_verify checks that
+            // piece's pairs on the aux stream while the next piece merges; the last piece's pairs
+            // are checked beside the gather. Measured neutral: the verify's random record reads
+            // cost the LDS-bound merge about what they cost the gather.
+            constexpr int FP_PIECES = 4;
+            uint64_t* snap = dbuf<uint64_t>(ctx, "fp_vsnap", FP_PIECES);
+            ensure_aux(ctx);
+            uint64_t done = 0;
+            for (int p = 0; p < FP_PIECES; ++p) {
+                const uint64_t upto = T * (uint64_t)(p + 1) / FP_PIECES;
+                HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, cmp_klen, bounds, km, T, tile_base, rec_meta, cmp_addr,
+                                   drop, O, d_flags + 2, upto - done));
+                done = upto;
+                if (p + 1 < FP_PIECES) {
+                    launch_fx_publish(st, (const uint64_t*)O.vcount, snap + p);
+                    HIPCHK(hipEventRecord(ctx->aux_ev[0], st));
+                    HIPCHK(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_ev[0], 0));
+                    launch_fp_verify(ctx->aux_stream, p ? (const unsigned long long*)(snap + p - 1) : nullptr,
+                                     (const unsigned long long*)(snap + p), O.vpairs, R, fp_bad, 1024);
+                    verify_pending = true;
+                }
+            }
+            HIPCHK(hipEventRecord(ctx->aux_ev[1], ctx->aux_stream));
+            verify_lo = (const unsigned long long*)(snap + FP_PIECES - 2);
+        } else {
+            HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, cmp_klen, bounds, km, T, tile_base, rec_meta, cmp_addr, drop,
+                               O, d_flags + 2));
+        }
+        if (l0 && key_fp) verify_args = {O.vcount, O.vpairs};
+        if (l0) T0 = T;
+    }
+    HIPCHK(hipGetLastError());
+    mark(ctx, PH_MERGE);
+    const uint64_t* d_K = d_Kout;
+    hres.pop_pos = pop_pos;
+    tables_mine();
+    auto fork_verify = [&]() {  // k_fp_verify on the aux stream, after what the ctx stream has queued
+        if (!verify_args.first) return;
+        ensure_aux(ctx);
+        HIPCHK(hipEventRecord(ctx->aux_ev[0], st));
+        HIPCHK(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_ev[0], 0));
+        launch_fp_verify(ctx->aux_stream, verify_lo, verify_args.first, verify_args.second, R, fp_bad);
+        HIPCHK(hipEventRecord(ctx->aux_ev[1], ctx->aux_stream));
+        verify_args.first = nullptr;
+        verify_pending = true;
+    };
+    auto join_verify = [&]() {  // fp_bad is read next: the ctx stream waits for k_fp_verify
+        if (verify_args.first) {  // not forked: in order on the ctx stream
+            launch_fp_verify(st, verify_lo, verify_args.first, verify_args.second, R, fp_bad);
+            verify_args.first = nullptr;
+        }
+        if (verify_pending) HIPCHK(hipStreamWaitEvent(st, ctx->aux_ev[1], 0));
+        verify_pending = false;
+    };
+    if (job.flags & SKV_SPLIT_BY_TABLE) {
+        join_verify();
+        htrace("merge launched");
+        const int rc =
+            wal_stage(ctx, job, R, d_K, m_rec, m_src, m_P, m_Dp, rec_addr, rec_klen, fp_bad, heap ? &hres : nullptr, out);
+        htrace("wal stage done");
+        if (rc == RC_RETRY_EXACT) return rerun_exact(ctx, job, out);
+        return rc;
+    }
+    if (heap) {
+        // Delete filter + unsorted input: build_runs' order check on what the filter let through
+        // (runs.rs:190-198, table_tree_compaction.rs:139-147), against the streams' decode errors
+        unsigned long long* first_bad = dbuf<unsigned long long>(ctx, "heap_first_bad", 1);
+        HIPCHK(hipMemsetAsync(first_bad, 0xFF, 8, st));
+        launch_merged_order(st, d_K, R, m_rec, rec_hi, rec_lo, rec_klen, rec_addr, first_bad);
+        HIPCHK(hipGetLastError());
+        sync(ctx);  // (read_dev copies on the null stream, which does not wait for the ctx stream)
+        const uint64_t v = read_dev((const uint64_t*)first_bad);
+        if (getenv("SKV_HEAP_DEBUG")) {  // diagnostic: the merged sequence of heap-order mode
+            const uint64_t K = read_dev(d_K);
+            fprintf(stderr, "[heap] R=%llu K=%llu first_bad=%lld\n", (unsigned long long)R, (unsigned long long)K,
+                    (long long)v);
+            const uint32_t* effp = (const uint32_t*)ctx->bufs["heap_eff"].p;
+            for (uint64_t i = 0; i < R && i < 40; ++i)
+                fprintf(stderr, "  rec %llu hi=%016llx lo=%016llx klen=%u eff=%u key=%s\n", (unsigned long long)i,
+                        (unsigned long long)read_dev(rec_hi + i), (unsigned long long)read_dev(rec_lo + i),
+                        read_dev(rec_klen + i), effp ? read_dev(effp + i) : 0u, fetch_key(ctx, rec_addr, rec_klen, i).c_str());
+            for (uint64_t g = 0; g < K && g < 200; ++g) {
+                const uint32_t r = read_dev(m_rec + g);
+                fprintf(stderr, "  g=%llu rec=%u pop=%llu key=%s cmpkey=%s\n", (unsigned long long)g, r,
+                        (unsigned long long)read_dev(pop_pos + r), fetch_key(ctx, rec_addr, rec_klen, r).c_str(),
+                        fetch_key(ctx, cmp_addr, cmp_klen, r).c_str());
+            }
+        }
+        std::vector<JobEvent> ev;
+        if (v != ~0ull)
+            ev.push_back({read_dev(pop_pos + read_dev(m_rec + v)), 0, SKV_E_FORMAT,
+                          "Data format error: Operations must be sorted by key"});
+        for (const HeapRes::Dec& d : hres.dec) {
+            std::string msg;
+            const int code = derr_to_api(d.err, msg);
+            ev.push_back({hres.pos_of_original(d.rec), 2, code, msg});
+        }
+        throw_first(ev);
+    }
+    // ---- chain + stats ----------------------------------------------------------------------
+    uint64_t* run_b = dbuf<uint64_t>(ctx, "run_b", R + 2);
+    uint64_t* d_nruns = dbuf<uint64_t>(ctx, "n_runs", 4);  // {runs, K, P[K]} (k_chain)
+    DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", R + 1);
+    uint64_t* seg_r0 = dbuf<uint64_t>(ctx, "seg_r0", R / GATHER_SEG + 2);
+    const uint64_t in_rec_bytes = job.in_bytes;  // bounds P[K]
+    uint32_t* chain_tbl = dbuf<uint32_t>(ctx, "chain_tbl", chain_table_entries(in_rec_bytes));
+    // parallel split buffers (k_split_*; the device plan falls back to k_chain where it does not fit).
+    // SKV_SPLIT=serial: k_chain only; =par: no minimum run count. SKV_SPLIT_NC / SKV_SPLIT_SEG:
+    // candidates per window, runs per segment (tests shrink the window to exercise the stitch's walks)
+    SplitBufs sp{};
+    {
+        const char* mode = getenv("SKV_SPLIT");
+        const bool serial = mode && !strcmp(mode, "serial");
+        sp.segr = 16;
+        sp.nc = 512;
+        sp.min_runs = mode && !strcmp(mode, "par") ? 0 : 1024;
+        if (const char* e = getenv("SKV_SPLIT_NC")) sp.nc = (uint32_t)std::min<uint64_t>(8192, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
+        if (const char* e = getenv("SKV_SPLIT_SEG")) sp.segr = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
+        const uint64_t M = job.max_run_size;
+        if (!serial && M > 8 && R < 0xFFFFFFF0ull) {
+            // runs of >= 8 records (the plan's gate) hold > 7/8 (max - 1) bytes each
+            const uint64_t runs_ub = in_rec_bytes / ((M - 1) - (M - 1) / 8) + 2;
+            const uint64_t want = runs_ub / sp.segr + 2;
+            sp.nseg_cap = (uint32_t)std::min<uint64_t>(want, 16384);
+        }
+        if (sp.nseg_cap) {
+            sp.plan = dbuf<SplitPlan>(ctx, "split_plan", 1);
+            sp.seg_w = dbuf<uint64_t>(ctx, "split_w", sp.nseg_cap);
+            sp.seg_n = dbuf<uint32_t>(ctx, "split_n", sp.nseg_cap);
+            sp.seg_sel = dbuf<uint32_t>(ctx, "split_sel", sp.nseg_cap);
+            sp.seg_D = dbuf<uint64_t>(ctx, "split_D", sp.nseg_cap);
+            sp.chain = dbuf<uint32_t>(ctx, "split_chain", (uint64_t)sp.nseg_cap * sp.segr * sp.nc);
+            sp.ends = dbuf<uint32_t>(ctx, "split_ends", (uint64_t)sp.nseg_cap * sp.nc + 4);
+        }
+    }
+    launch_chain(st, d_K, m_P, job.max_run_size, tile_max, T0, run_b, d_nruns, chain_tbl, R, in_rec_bytes, &sp);
+    if (sp.nseg_cap && getenv("SKV_SPLIT_DEBUG")) {
+        sync(ctx);
+        SplitPlan pl;
+        HIPCHK(hipMemcpy(&pl, sp.plan, sizeof(pl), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[split] mode=%u nseg=%u sel=%u walked=%u K=%llu L0=%llu cap=%u\n", pl.mode, pl.nseg,
+                pl.nseg_sel, pl.n_fb, (unsigned long long)pl.K, (unsigned long long)pl.L0, sp.nseg_cap);
+    }
+    launch_run_stats(st, d_nruns, run_b, m_P, m_Dp, m_rec, rec_klen, d_desc, seg_r0, R);
+    mark(ctx, PH_CHAIN);
+    fork_verify();  // beside the gather (beside the single-wave chain it slowed the chain 3x)
+    // ---- gather -----------------------------------------------------------------------------
+    const uint64_t total_rec_bytes = job.in_bytes;
+    uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + R + 16);
+#if SKV_PAGE_GATHER
+    {
+        const uint64_t max_out = total_rec_bytes + R + 16;
+        uint64_t* Dst = dbuf<uint64_t>(ctx, "g_dst", R + 1);
+        uint32_t* page_first = dbuf<uint32_t>(ctx, "g_page_first", max_out / PAGE_BYTES + 2);
+        launch_page_prep(st, d_K, d_nruns, run_b, m_P, seg_r0, Dst, page_first, R);
+        mark(ctx, PH_CHAIN);
+        launch_gather_pages(st, d_K, d_nruns, m_P, Dst, m_src, page_first, d_out, max_out);
+    }
+#else
+    launch_gather(st, d_K, d_nruns, run_b, m_P, m_src, seg_r0, d_out, R);
+#endif
+    HIPCHK(hipGetLastError());
+    mark(ctx, PH_GATHER);
+    // ---- readback: summary + descriptors in one sync (descriptor count guessed from sizes) -------
+    static_assert(sizeof(skv_run_desc) == sizeof(DevRunDesc), "desc layout");
+    const uint64_t guess = std::min<uint64_t>(
+        R + 1, job.max_run_size > 1 ? 2 * (total_rec_bytes / (job.max_run_size - 1)) + 64 : R + 1);
+    uint64_t h3[4];
+    ResultBox* box = new ResultBox();
+    skv_result* res = &box->pub;
+    {
+        const size_t vbytes = deferred ? 16 + (size_t)n_runs * 4 : 0;  // flags + broken runs
+        join_verify();
+        uint8_t* hp = (uint8_t*)pinned(ctx, 64 + guess * sizeof(DevRunDesc) + vbytes);
+        uint8_t* hv = hp + 64 + guess * sizeof(DevRunDesc);
+        d2h(ctx, hp, d_nruns, 24);
+        d2h(ctx, hp + 32, fp_bad, 4);
+        d2h(ctx, hp + 64, d_desc, guess * sizeof(DevRunDesc));
+        if (deferred) {
+            d2h(ctx, hv, d_flags, 16);
+            d2h(ctx, hv + 16, d_broken, (size_t)n_runs * 4);
+        }
+        sync(ctx);
+        if (deferred) {
+            const uint32_t* f = (const uint32_t*)hv;  // >= 2 GiB record, key decrease, poison
+            bool bad = f[0] || f[1] || f[2];
+            for (uint32_t r = 0; r < n_runs && !bad; ++r) bad = ((const uint32_t*)(hv + 16))[r] != 0;
+            if (bad) {
+                delete box;
+                return compact_device(ctx, job, out, false);
+            }
+        }
+        uint32_t fpb = 0;
+        memcpy(&fpb, hp + 32, 4);
+        if (fpb) {
+            delete box;
+            return rerun_exact(ctx, job, out);
+        }
+        memcpy(h3, hp, 24);
+        const uint64_t n = h3[0];
+        res->runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, n) * sizeof(skv_run_desc));
+        memcpy(res->runs, hp + 64, std::min(n, guess) * sizeof(DevRunDesc));
+        if (n > guess)
+            HIPCHK(hipMemcpy(res->runs + guess, d_desc + guess, (n - guess) * sizeof(DevRunDesc), hipMemcpyDeviceToHost));
+    }
+    const uint64_t n_out_runs = h3[0], K = h3[1], kept_bytes = h3[2];
+    res->n_runs = n_out_runs;
+    res->bytes = d_out;
+    res->n_bytes = kept_bytes + n_out_runs;
+    res->in_bytes = job.in_bytes;
+    res->in_records = R;
+    res->out_records = K;
+    res->dropped_tables = 0;
+    if (ctx->profiling) {
+        HIPCHK(hipEventSynchronize(ctx->ev[PH_GATHER]));
+        float ms[PH_N] = {};
+        for (int p = PH_PARSE; p < PH_N; ++p) HIPCHK(hipEventElapsedTime(&ms[p], ctx->ev[p - 1], ctx->ev[p]));
+        float tot = 0;
+        HIPCHK(hipEventElapsedTime(&tot, ctx->ev[PH_START], ctx->ev[PH_GATHER]));
+        skv_timings& t = ctx->timings;
+        t.total_ms = tot;
+        t.parse_ms = ms[PH_PARSE];
+        t.check_ms = ms[PH_CHECK];
+        t.merge_ms = ms[PH_MERGE];
+        t.chain_ms = ms[PH_CHAIN];
+        t.gather_ms = ms[PH_GATHER];
+        t.gather_read_bytes = kept_bytes;
+        t.gather_write_bytes = kept_bytes + n_out_runs;
+        t.hot_ms = ms[PH_GATHER];
+    }
+    ctx->timings.path = parsed ? SKV_PATH_FIXED : SKV_PATH_GENERAL;
+    ctx->timings.hot_read_bytes = kept_bytes;
+    ctx->timings.hot_write_bytes = kept_bytes + n_out_runs;
+    ctx->timings.host_syncs = ctx->syncs;
+    *out = res;
+    return SKV_OK;
+}
+// the one-run job of a writer batch (writer_service.rs:148-162)
+int batch_job(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_t max_run_size, Job& job) {
+    if (len && !ops_run) return set_err(ctx, SKV_E_INVALID_ARG, "ops_run is NULL");
+    const uint8_t* runs[1] = {ops_run};
+    const uint64_t lens[1] = {len};
+    skv_stream st{runs, lens, 1u, 0};
+    const int rc = build_job(ctx, &st, 1, max_run_size, 0, job);
+    job.batch = true;
+    return rc;
+}
+
+extern "C" {
+
+int skv_compact_dev(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uint64_t max_run_size, uint32_t flags,
+                    skv_result** out) {
+    const double t_entry = now_ms();
+    htrace("entry");
+    if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
+    *out = nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    Job job;  // its tables borrow the ctx's storage for the call (no fresh 10^6-entry vectors)
+    job.ranked.swap(ctx->j_ranked);
+    job.run_ptr.swap(ctx->j_ptr);
+    job.run_len.swap(ctx->j_len);
+    int rc = build_job(ctx, streams, n_streams, max_run_size, flags, job);
+    htrace("job built");
+    if (!rc) rc = run_guarded(ctx, job, out, t_entry);
+    job.ranked.swap(ctx->j_ranked);
+    job.run_ptr.swap(ctx->j_ptr);
+    job.run_len.swap(ctx->j_len);
+    return rc;
+}
+
+int skv_encode_batch_dev(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_t max_run_size,
+                         skv_result** out) {
+    const double t_entry = now_ms();
+    if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
+    *out = nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    Job job;
+    int rc = batch_job(ctx, ops_run, len, max_run_size, job);
+    if (rc) return rc;
+    return run_guarded(ctx, job, out, t_entry);
+}
+
+}  // extern "C"

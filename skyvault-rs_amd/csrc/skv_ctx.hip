@@ -1,0 +1,421 @@
+// skv_ctx.hip — ctx lifetime, the reference's error text, host staging helpers, the job tables of a
+// call (build_job) and the guarded device call (run_guarded). C ABI: include/skv.h.
+#include "skv_host.hpp"
+
+using namespace skv;
+
+
+int set_err(skv_ctx* ctx, int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    return code;
+}
+
+void* pinned(skv_ctx* ctx, size_t bytes) {
+    if (ctx->pinned_cap < bytes) {
+        if (ctx->pinned) HIPCHK(hipHostFree(ctx->pinned));
+        ctx->pinned = nullptr;
+        size_t cap = std::max<size_t>(bytes, 1 << 16);
+        HIPCHK(hipHostMalloc(&ctx->pinned, cap, hipHostMallocDefault));
+        ctx->pinned_cap = cap;
+    }
+    return ctx->pinned;
+}
+
+// host copy into pinned staging; large tables (10^6-run calls: tens of MB) on several threads
+void stage_copy(void* dst, const void* src, size_t bytes) {
+    const char* pe = getenv("SKV_PAR_COPY_MIN");  // tests: split small tables too
+    const size_t kPar = pe ? (size_t)strtoull(pe, nullptr, 10) : (8u << 20);
+    const unsigned hw = std::thread::hardware_concurrency();
+    static const unsigned cap = [] {  // SKV_HOST_THREADS: host threads for 10^6-entry tables (default 8)
+        const char* e = getenv("SKV_HOST_THREADS");
+        const long v = e ? atol(e) : 8;
+        return (unsigned)std::max(1l, std::min(64l, v));
+    }();
+    const unsigned nt = std::min<unsigned>(cap, hw ? hw : 1);
+    if (bytes < kPar || nt < 2) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t part = ((bytes + nt - 1) / nt + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    th.reserve(nt);
+    auto piece = [=](unsigned i) {
+        memcpy((uint8_t*)dst + i * part, (const uint8_t*)src + i * part, std::min(part, bytes - i * part));
+    };
+    unsigned started = 1;  // pieces [1, started) run on threads
+    for (unsigned i = 1; i < nt && i * part < bytes; ++i) {
+        try {
+            th.emplace_back(piece, i);
+        } catch (...) {  // no thread: this piece and the rest are copied here
+            break;
+        }
+        started = i + 1;
+    }
+    memcpy(dst, src, std::min(part, bytes));
+    for (unsigned i = started; i < nt && i * part < bytes; ++i) piece(i);
+    for (auto& t : th) t.join();
+}
+
+// [0, n) as nb contiguous blocks fn(b, lo, hi) on host threads: the per-run and per-stream
+// table loops of a 10^6-stream call (config 5) are memory-bound at one core's bandwidth, ~10 ns
+// per entry. Below min_par entries one block runs on the calling thread; a block whose thread
+// cannot be started runs here too.
+unsigned par_nblocks(uint64_t n, uint64_t min_par) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    static const unsigned cap = [] {  // SKV_HOST_THREADS: host threads for 10^6-entry tables (default 8)
+        const char* e = getenv("SKV_HOST_THREADS");
+        const long v = e ? atol(e) : 8;
+        return (unsigned)std::max(1l, std::min(64l, v));
+    }();
+    const unsigned nt = std::min<unsigned>(cap, hw ? hw : 1);
+    return n < min_par ? 1u : nt;
+}
+
+// async H2D of a host table through the pinned upload arena
+void h2d_up(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!bytes) return;
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    while (ctx->up_chunk < ctx->up_chunks.size() &&
+           ctx->up_off + need > ctx->up_chunks[ctx->up_chunk].second) {
+        ++ctx->up_chunk;
+        ctx->up_off = 0;
+    }
+    if (ctx->up_chunk == ctx->up_chunks.size()) {
+        const size_t cap = std::max<size_t>(need, 1 << 20);
+        void* p = nullptr;
+        HIPCHK(hipHostMalloc(&p, cap, hipHostMallocDefault));
+        ctx->up_chunks.emplace_back((uint8_t*)p, cap);
+        ctx->up_off = 0;
+    }
+    uint8_t* stage = ctx->up_chunks[ctx->up_chunk].first + ctx->up_off;
+    ctx->up_off += need;
+    stage_copy(stage, src, bytes);
+    if (ctx->kernel_uploads) {  // a DMA copy here would queue behind the pipeline's bulk copies
+        void* dptr = nullptr;
+        HIPCHK(hipHostGetDevicePointer(&dptr, stage, 0));
+        launch_copy_bytes(ctx->stream, (uint8_t*)dst, (const uint8_t*)dptr, bytes);
+        return;
+    }
+    HIPCHK(hipMemcpyAsync(dst, stage, bytes, hipMemcpyHostToDevice, ctx->stream));
+}
+
+void d2h(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!bytes) return;
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+}
+void h2d(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!bytes) return;
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+}
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// SKV_HOST_TRACE=1: host-side milestones of a call on stderr (ms since the call's first one)
+void htrace(const char* what) {
+    static int on = -1;
+    static double t0 = 0;
+    if (on < 0) {
+        const char* e = getenv("SKV_HOST_TRACE");
+        on = e && e[0] == '1';
+    }
+    if (!on) return;
+    const double t = now_ms();
+    if (!strcmp(what, "entry")) t0 = t;  // each API call starts the clock
+    fprintf(stderr, "[skv host] %8.3f ms %s\n", t - t0, what);
+}
+void sync(skv_ctx* ctx) {
+    const double t0 = now_ms();
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->sync_ms += now_ms() - t0;
+    ctx->syncs++;
+}
+void mark(skv_ctx* ctx, Phase p) {
+    if (ctx->profiling) HIPCHK(hipEventRecord(ctx->ev[p], ctx->stream));
+}
+
+// reference Display text of a device error word (runs.rs:83-95, :537-624)
+int derr_to_api(uint32_t e, std::string& msg) {
+    uint32_t code = e & 0xFF, extra = e >> 8;
+    char buf[128];
+    switch (code) {
+        case DERR_EMPTY: msg = "Input list of operations cannot be empty"; return SKV_E_EMPTY_INPUT;
+        case DERR_VERSION: snprintf(buf, sizeof buf, "Unsupported run version: %u", extra); msg = buf; return SKV_E_UNSUPPORTED_VERSION;
+        case DERR_IO: msg = "I/O error: failed to fill whole buffer"; return SKV_E_IO;
+        case DERR_KEY: msg = "Data format error: Incomplete key data"; return SKV_E_FORMAT;
+        case DERR_UTF8: msg = "Data format error: Invalid UTF-8 in key"; return SKV_E_FORMAT;
+        case DERR_VAL: msg = "Data format error: Incomplete value data"; return SKV_E_FORMAT;
+        case DERR_MARKER: snprintf(buf, sizeof buf, "Data format error: Invalid marker byte: %u", extra); msg = buf; return SKV_E_FORMAT;
+        default: snprintf(buf, sizeof buf, "internal: unknown device error %u", e); msg = buf; return SKV_E_DEVICE;
+    }
+}
+
+
+// a record's key bytes (host copy) for error-trigger comparisons
+std::string fetch_key(skv_ctx* ctx, const uint64_t* d_rec_addr, const uint32_t* d_rec_klen, uint64_t rec) {
+    uint64_t addr = 0;
+    uint32_t klen = 0;
+    HIPCHK(hipMemcpy(&addr, d_rec_addr + rec, 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&klen, d_rec_klen + rec, 4, hipMemcpyDeviceToHost));
+    std::string k(klen, '\0');
+    if (klen) HIPCHK(hipMemcpy(&k[0], (const void*)(addr + 5), klen, hipMemcpyDeviceToHost));
+    return k;
+}
+
+// JobError::InvalidInput text of a bad WAL key (wal_compaction.rs:71-79; Rust ParseIntError Display)
+std::string wal_key_error(const std::string& key) {
+    size_t dot = key.find('.');
+    if (dot == std::string::npos) return "Invalid input: Key does not follow 'table_id.key' format: " + key;
+    const std::string pre = key.substr(0, dot);
+    const char* why = nullptr;
+    if (pre.empty()) why = "cannot parse integer from empty string";
+    else {
+        size_t i = 0;
+        bool neg = false;
+        if (pre[0] == '+' || pre[0] == '-') {
+            neg = pre[0] == '-';
+            i = 1;
+            if (pre.size() == 1) why = "invalid digit found in string";
+        }
+        int64_t r = 0;
+        for (; !why && i < pre.size(); ++i) {
+            if (pre[i] < '0' || pre[i] > '9') { why = "invalid digit found in string"; break; }
+            int64_t m, d = pre[i] - '0';
+            if (__builtin_mul_overflow(r, (int64_t)10, &m) ||
+                (neg ? __builtin_sub_overflow(m, d, &r) : __builtin_add_overflow(m, d, &r)))
+                why = neg ? "number too small to fit in target type" : "number too large to fit in target type";
+        }
+    }
+    if (!why) return "internal: WAL key flagged but parses: " + key;
+    return "Invalid input: Invalid table ID '" + pre + "': " + why;
+}
+void throw_first(std::vector<JobEvent>& ev) {
+    if (ev.empty()) return;
+    std::sort(ev.begin(), ev.end(), [](const JobEvent& a, const JobEvent& b) {
+        return a.pos != b.pos ? a.pos < b.pos : a.sub < b.sub;
+    });
+    throw ApiError{ev[0].code, ev[0].msg};
+}
+
+// ------------------------------------------------------------------------------------------
+int build_job_impl(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t max_run_size, uint32_t flags,
+                     Job& job) {
+    if (n && !streams) return set_err(ctx, SKV_E_INVALID_ARG, "streams is NULL");
+    if (flags & ~(uint32_t)(SKV_DROP_TOMBSTONES | SKV_SPLIT_BY_TABLE))
+        return set_err(ctx, SKV_E_INVALID_ARG, "unknown flags 0x%x", flags);
+    if ((flags & SKV_SPLIT_BY_TABLE) && (flags & SKV_DROP_TOMBSTONES))
+        return set_err(ctx, SKV_E_INVALID_ARG, "SKV_SPLIT_BY_TABLE and SKV_DROP_TOMBSTONES are exclusive");
+    job.max_run_size = max_run_size;
+    job.flags = flags;
+    // pass 1 (blocks of streams on host threads): NULL checks, run counts, input bytes, and
+    // whether the caller's order is strictly ascending / descending by seq_no
+    const unsigned nb = par_nblocks(n);
+    struct Blk {
+        uint64_t runs = 0, bytes = 0, bad = ~0ull;
+        uint32_t bad_run = ~0u;
+        bool asc = true, desc = true;
+    };
+    std::vector<Blk> B(nb);
+    par_run(n, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+        Blk& K = B[b];
+        for (uint64_t i = lo; i < hi; ++i) {
+            const skv_stream& s = streams[i];
+            if (s.n_runs && (!s.runs || !s.run_lens)) {
+                K.bad = i;
+                return;
+            }
+            for (uint32_t r = 0; r < s.n_runs; ++r) {
+                if (s.run_lens[r] && !s.runs[r]) {
+                    K.bad = i;
+                    K.bad_run = r;
+                    return;
+                }
+                K.bytes += s.run_lens[r];
+            }
+            K.runs += s.n_runs;
+            if (i > 0) {
+                K.asc = K.asc && streams[i - 1].seq_no < s.seq_no;
+                K.desc = K.desc && streams[i - 1].seq_no > s.seq_no;
+            }
+        }
+    });
+    bool asc = true, desc = true;
+    uint64_t total_runs = 0;
+    for (unsigned b = 0; b < nb; ++b) {  // the first invalid stream in the caller's order
+        if (B[b].bad != ~0ull) {
+            if (B[b].bad_run == ~0u)
+                return set_err(ctx, SKV_E_INVALID_ARG, "stream %u: runs/run_lens is NULL", (uint32_t)B[b].bad);
+            return set_err(ctx, SKV_E_INVALID_ARG, "stream %u run %u: NULL data", (uint32_t)B[b].bad, B[b].bad_run);
+        }
+        const uint64_t r = B[b].runs;
+        B[b].runs = total_runs;  // now the block's first run
+        total_runs += r;
+        job.in_bytes += B[b].bytes;
+        asc = asc && B[b].asc;
+        desc = desc && B[b].desc;
+    }
+    // pass 2: the tables, streams already in rank order (seq_no descending) when the caller's
+    // order is either strict one; resize keeps a lent table's entries (no zero fill per call)
+    job.run_ptr.resize(total_runs);
+    job.run_len.resize(total_runs);
+    job.ranked.resize(n);
+    par_run(n, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+        uint64_t at = B[b].runs;
+        for (uint64_t i = lo; i < hi; ++i) {
+            const skv_stream& s = streams[i];
+            InStream& S = job.ranked[asc ? n - 1 - i : i];
+            S.seq = s.seq_no;
+            S.vec_idx = (uint32_t)i;
+            S.n_runs = s.n_runs;
+            S.first = at;
+            for (uint32_t r = 0; r < s.n_runs; ++r, ++at) {
+                job.run_ptr[at] = (uint64_t)(uintptr_t)s.runs[r];
+                job.run_len[at] = s.run_lens[r];
+            }
+        }
+    });
+    if (!asc && !desc) {
+        std::stable_sort(job.ranked.begin(), job.ranked.end(),
+                         [](const InStream& a, const InStream& b) { return a.seq > b.seq; });
+        for (size_t i = 1; i < job.ranked.size(); ++i)
+            if (job.ranked[i].seq == job.ranked[i - 1].seq)
+                return set_err(ctx, SKV_E_INVALID_ARG, "duplicate seq_no %" PRId64, job.ranked[i].seq);
+    }
+    return SKV_OK;
+}
+
+// the job tables of a call (10^6-stream calls: vectors of that size) without unwinding into C
+int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t max_run_size, uint32_t flags,
+                     Job& job) {
+    try {
+        return build_job_impl(ctx, streams, n, max_run_size, flags, job);
+    } catch (const std::exception& e) {
+        return set_err(ctx, SKV_E_DEVICE, "host error: %s", e.what());
+    }
+}
+
+// after an error: every stream of the ctx idle before its buffers are reused
+void drain(skv_ctx* ctx) {
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->aux_stream) (void)hipStreamSynchronize(ctx->aux_stream);
+    if (ctx->in_stream) (void)hipStreamSynchronize(ctx->in_stream);
+    if (ctx->out_stream) (void)hipStreamSynchronize(ctx->out_stream);
+}
+
+int run_guarded(skv_ctx* ctx, const Job& job, skv_result** out, double t_entry) {
+    try {
+        ctx->sync_ms = 0;
+        ctx->timings = skv_timings{};
+        const int rc = compact_device(ctx, job, out, true);
+        ctx->timings.host_total_ms = now_ms() - t_entry;
+        ctx->timings.host_sync_ms = ctx->sync_ms;
+        return rc;
+    } catch (const ApiError& e) {
+        drain(ctx);
+        return set_err(ctx, e.code, "%s", e.msg.c_str());
+    } catch (const DevError& e) {
+        drain(ctx);
+        return set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());
+    } catch (const std::exception& e) {  // bad_alloc of a host table, system_error, ...: never unwind into C
+        drain(ctx);
+        return set_err(ctx, SKV_E_DEVICE, "host error: %s", e.what());
+    }
+}
+
+extern "C" {
+
+int skv_abi_version(void) { return SKV_ABI_VERSION; }
+
+int skv_device_count(int* out) {
+    if (!out) return SKV_E_INVALID_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *out = n;
+    return SKV_OK;
+}
+
+int skv_ctx_create(int device, skv_ctx** out) {
+    if (!out) return SKV_E_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return SKV_E_DEVICE;
+    if (device < 0 || device >= n) return SKV_E_INVALID_ARG;
+    skv_ctx* ctx = new skv_ctx();
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return SKV_E_DEVICE;
+    }
+    for (int i = 0; i < PH_N; ++i) (void)hipEventCreate(&ctx->ev[i]);
+    *out = ctx;
+    return SKV_OK;
+}
+
+void skv_ctx_destroy(skv_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+#if SKV_TILE_PROF
+    if (ctx->bufs.count("tile_prof")) {
+        uint64_t pr[16] = {};
+        const size_t nb = ctx->bufs["tile_prof"].cap >= 128 ? 128 : 64;
+        if (hipMemcpy(pr, ctx->bufs["tile_prof"].p, nb, hipMemcpyDeviceToHost) == hipSuccess) {
+            fprintf(stderr, "tile phase time (100 MHz ticks summed over tiles; [15] = tiles):");
+            for (int i = 0; i < (int)(nb / 8); ++i) fprintf(stderr, " %d:%llu", i, (unsigned long long)pr[i]);
+            fprintf(stderr, "\n");
+        }
+    }
+#endif
+    for (auto& kv : ctx->bufs)
+        if (kv.second.p) (void)hipFree(kv.second.p);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    for (auto& c : ctx->up_chunks) (void)hipHostFree(c.first);
+    for (int i = 0; i < PH_N; ++i)
+        if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
+    for (hipEvent_t e : ctx->part_ev) (void)hipEventDestroy(e);
+    if (ctx->aux_stream) {
+        (void)hipStreamSynchronize(ctx->aux_stream);
+        (void)hipStreamDestroy(ctx->aux_stream);
+    }
+    for (hipEvent_t e : ctx->aux_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->part_k) (void)hipHostFree(ctx->part_k);
+    if (ctx->in_stream) {
+        (void)hipStreamSynchronize(ctx->in_stream);
+        (void)hipStreamDestroy(ctx->in_stream);
+    }
+    if (ctx->out_stream) {
+        (void)hipStreamSynchronize(ctx->out_stream);
+        (void)hipStreamDestroy(ctx->out_stream);
+    }
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* skv_last_error(const skv_ctx* ctx) { return ctx ? ctx->err.c_str() : "ctx is NULL"; }
+
+int skv_ctx_set_profiling(skv_ctx* ctx, int enable) {
+    if (!ctx) return SKV_E_INVALID_ARG;
+    ctx->profiling = enable != 0;
+    return SKV_OK;
+}
+
+int skv_ctx_get_timings(const skv_ctx* ctx, skv_timings* out) {
+    if (!ctx || !out) return SKV_E_INVALID_ARG;
+    *out = ctx->timings;
+    return SKV_OK;
+}
+
+void skv_result_free(skv_result* r) {
+    if (!r) return;
+    ResultBox* box = (ResultBox*)r;
+    if (box->pool) box->pool->give(r->bytes, box->pool_cap);
+    free(r->runs);
+    delete box;
+}
+
+}  // extern "C"

@@ -1,0 +1,434 @@
+// skv_hostpipe.hip — skv_compact with host inputs: the serial stage -> compact -> copy path and the
+// pipelined key-range paths that overlap H2D, kernels and D2H.
+#include "skv_host.hpp"
+
+using namespace skv;
+
+
+// ---- pipelined host calls ---------------------------------------------------------------------
+// skv_compact with host inputs (the get_run -> compact -> put_run of a job, storage.rs:183-250) as
+// a key-range pipeline: the call is cut into P parts by key, every part holds each stream's records
+// in [B_p, B_p+1) (equal keys never straddle a cut), and three streams overlap:
+//   in_stream   H2D of part p's slices (pinned host runs -> their images in HBM)
+//   ctx->stream the fused path on part p (fx_launch), survivor numbering chained on the device
+//               through part p-1's count (FxArgs::gbase), one shared output buffer and verdict
+//   out_stream  D2H of part p's output bytes as soon as its count is published
+// so the PCIe copies in both directions run at once, and the kernels hide behind them. Taken when
+// the host can see that the fused path applies (one run per stream, every run fixed-stride at one
+// record size, key <= 16 bytes) and the call is large; the device verifies everything as in
+// compact_fused, and a poisoned call (or a stream whose records decrease across a cut) reruns as
+// the serial copy -> compact -> copy of compact_host_job.
+static uint32_t be32(const uint8_t* p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
+
+
+static bool pipe_eligible(const Job& job, RunFmt& f, uint64_t& R) {
+    const char* pe = getenv("SKV_HOST_PIPE");
+    if (pe && pe[0] == '0') return false;
+    const char* me = getenv("SKV_HOST_PIPE_MIN");
+    const uint64_t min_bytes = me ? strtoull(me, nullptr, 10) : (512ull << 20);
+    const uint32_t k = (uint32_t)job.ranked.size();
+    if (job.in_bytes < min_bytes || (job.flags & SKV_SPLIT_BY_TABLE) || job.batch || job.search) return false;
+    if (k == 0 || k > (uint32_t)TILE_TARGET / 2 || job.run_ptr.size() != k) return false;
+    R = 0;
+    for (uint32_t m = 0; m < k; ++m) {
+        const uint8_t* run = (const uint8_t*)(uintptr_t)job.run_ptr[m];
+        const uint64_t len = job.run_len[m];
+        if (len < 1 + 9 || run[0] != 1 || run[1] != 1) return false;
+        const uint64_t K = be32(run + 2);
+        if (K > FX_MAX_K || 1 + 5 + K + 4 > len) return false;
+        const uint64_t S = 9 + K + be32(run + 6 + K);
+        if (S < FX_MIN_S || S > FX_MAX_S || (len - 1) % S) return false;
+        if (m == 0) {
+            f.S = S;
+            f.K = (uint32_t)K;
+            f.V = (uint32_t)(S - 9 - K);
+        } else if (S != f.S || K != f.K) {
+            return false;
+        }
+        R += (len - 1) / S;
+    }
+    return R < 0xFFFFFFFFull;
+}
+
+static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, double t_entry, bool& used) {
+    used = false;
+    RunFmt f{};
+    uint64_t R = 0;
+    if (!pipe_eligible(job, f, R)) return SKV_OK;
+    const uint32_t k = (uint32_t)job.ranked.size();
+    const uint64_t S = f.S, K = f.K;
+    uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(64, job.in_bytes / (256ull << 20)));
+    if (const char* pp = getenv("SKV_HOST_PARTS")) P = std::max<uint64_t>(1, std::min<uint64_t>(256, strtoull(pp, nullptr, 10)));
+    if (R < P * 64) return SKV_OK;
+    htrace("pipe: eligible");
+    auto key_at = [&](uint32_t m, uint64_t i) { return (const uint8_t*)(uintptr_t)job.run_ptr[m] + 1 + i * S + 5; };
+    auto nrec = [&](uint32_t m) { return (job.run_len[m] - 1) / S; };
+    // ---- cut keys: quantiles of an even sample of every run
+    std::vector<std::array<uint8_t, 16>> smp;
+    const uint64_t Q = std::max<uint64_t>(8, 4096 / k);
+    for (uint32_t m = 0; m < k; ++m) {
+        const uint64_t nm = nrec(m);
+        for (uint64_t t = 0; t < Q && t < nm; ++t) {
+            std::array<uint8_t, 16> a{};
+            memcpy(a.data(), key_at(m, (2 * t + 1) * nm / (2 * Q)), K);
+            smp.push_back(a);
+        }
+    }
+    std::sort(smp.begin(), smp.end());
+    std::vector<std::array<uint8_t, 16>> cut;  // P - 1 cut keys B_1..B_{P-1}
+    for (uint64_t p = 1; p < P; ++p) cut.push_back(smp[p * smp.size() / P]);
+    // ---- lb[p * k + m]: first record of run m with key >= B_p (binary search in host memory)
+    std::vector<uint64_t> lb((P + 1) * k);
+    bool cuts_ok = true;
+    {
+        const unsigned nb = par_nblocks(k, 8);
+        std::vector<uint8_t> ok(nb, 1);
+        par_run(k, nb, [&](unsigned b, uint64_t lo_m, uint64_t hi_m) {
+            for (uint64_t m = lo_m; m < hi_m; ++m) {
+                const uint64_t nm = nrec((uint32_t)m);
+                lb[m] = 0;
+                lb[P * k + m] = nm;
+                for (uint64_t p = 1; p < P; ++p) {
+                    uint64_t a = 0, z = nm;
+                    while (a < z) {
+                        const uint64_t mid = (a + z) >> 1;
+                        if (memcmp(key_at((uint32_t)m, mid), cut[p - 1].data(), K) < 0) a = mid + 1;
+                        else z = mid;
+                    }
+                    lb[p * k + m] = a;
+                    // a stream that decreases across a cut is left to the serial path (the device
+                    // checks the order inside each part only)
+                    if (a < lb[(p - 1) * k + m]) ok[b] = 0;
+                    if (a > 0 && a < nm && memcmp(key_at((uint32_t)m, a - 1), key_at((uint32_t)m, a), K) > 0) ok[b] = 0;
+                }
+            }
+        });
+        for (uint8_t o : ok) cuts_ok = cuts_ok && o;
+    }
+    if (!cuts_ok) return SKV_OK;
+    htrace("pipe: cuts");
+    used = true;
+    hipStream_t st = ctx->stream;
+    struct KernelUploads {  // table uploads of this call by kernel, not by a DMA engine
+        skv_ctx* c;
+        explicit KernelUploads(skv_ctx* x) : c(x) { c->kernel_uploads = true; }
+        ~KernelUploads() { c->kernel_uploads = false; }
+    } ku(ctx);
+    ctx->syncs = 0;
+    ctx->up_chunk = 0;  // the upload arena from its start (the last call ended with a sync)
+    ctx->up_off = 0;
+    if (!ctx->in_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->in_stream, hipStreamNonBlocking));
+    if (!ctx->out_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->out_stream, hipStreamNonBlocking));
+    while (ctx->part_ev.size() < 2 * P) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->part_ev.push_back(e);
+    }
+    if (ctx->part_k_cap < P) {
+        if (ctx->part_k) HIPCHK(hipHostFree(ctx->part_k));
+        ctx->part_k = nullptr;
+        ctx->part_k_cap = 0;
+        HIPCHK(hipHostMalloc((void**)&ctx->part_k, std::max<uint64_t>(P, 64) * 8, hipHostMallocCoherent));
+        ctx->part_k_cap = std::max<uint64_t>(P, 64);
+    }
+    volatile uint64_t* hK = ctx->part_k;
+    for (uint64_t p = 0; p < P; ++p) hK[p] = ~0ull;
+    // ---- device buffers (all sized before the first launch: no buffer moves under queued work)
+    std::vector<uint64_t> img(k + 1, 0);
+    for (uint32_t m = 0; m < k; ++m) img[m + 1] = img[m] + ((job.run_len[m] + 15) & ~15ull);
+    uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", img[k] + 16);
+    const uint64_t out_cap = job.in_bytes + R + 16;
+    uint8_t* d_out = dbuf<uint8_t>(ctx, "out", out_cap);
+    uint64_t* d_Kp = dbuf<uint64_t>(ctx, "hp_K", P);
+    uint32_t* d_pflags = dbuf<uint32_t>(ctx, "hp_flags", 4);
+    uint64_t* d_prb = dbuf<uint64_t>(ctx, "hp_rb", 4);
+    const uint64_t n = fx_run_records(job.max_run_size, S, R), W = n * S + 1;
+    const uint64_t max_runs = (R + n - 1) / n;
+    DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", max_runs + 1);
+    // per part: its runs (rank order, empty slices left out), record bases
+    std::vector<RunInfo> hruns(P * k);
+    std::vector<uint32_t> kp(P, 0);
+    std::vector<std::vector<uint64_t>> recbp(P);
+    for (uint64_t p = 0; p < P; ++p) {
+        recbp[p].assign(1, 0);
+        for (uint32_t s = 0; s < k; ++s) {
+            const uint32_t m = (uint32_t)job.ranked[s].first;  // one run per stream
+            const uint64_t a = lb[p * k + m], z = lb[(p + 1) * k + m];
+            if (z == a) continue;
+            RunInfo& ri = hruns[p * k + kp[p]];
+            ri.ptr = (uint64_t)(uintptr_t)(d_in + img[m] + a * S);  // the byte before record a
+            ri.len = 1 + (z - a) * S;
+            ri.chunk_base = 0;
+            ri.n_chunks = 0;
+            ri.stream = kp[p]++;
+            recbp[p].push_back(recbp[p].back() + (z - a));
+        }
+    }
+    RunInfo* d_runs = dbuf<RunInfo>(ctx, "hp_runs", P * k);
+    h2d_up(ctx, d_runs, hruns.data(), P * k * sizeof(RunInfo));
+    HIPCHK(hipMemsetAsync(d_Kp, 0, P * 8, st));
+    HIPCHK(hipMemsetAsync(d_pflags, 0, 16, st));
+    size_t cap = 0;
+    uint8_t* h_out = (uint8_t*)ctx->out_pool->take(out_cap, cap);
+    if (!h_out) throw DevError("pinned host allocation of the output failed");
+    // Unless the result takes h_out, it goes back to the pool once no copy can touch it any more:
+    // on every exit (a throw included) the three streams are drained first, so no H2D still reads
+    // the caller's runs and no D2H still writes h_out after this call returns. Declared before the
+    // egress thread's joiner, so it runs after the thread has been joined.
+    struct OutGuard {
+        skv_ctx* c;
+        uint8_t*& buf;
+        size_t cap;
+        ~OutGuard() {
+            if (c->in_stream) (void)hipStreamSynchronize(c->in_stream);
+            if (c->out_stream) (void)hipStreamSynchronize(c->out_stream);
+            (void)hipStreamSynchronize(c->stream);
+            if (buf) c->out_pool->give(buf, cap);
+        }
+    } out_guard{ctx, h_out, cap};
+    // ---- egress thread: D2H of part p once its count is published
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t issued = 0;
+    bool stop = false;
+    std::string d2h_err;
+    uint64_t egress_end = 0;
+    auto end_of = [&](uint64_t Kc) -> uint64_t {  // output bytes through survivor Kc - 1
+        if (!Kc) return 0;
+        const uint64_t g = Kc - 1;
+        return (g / n) * W + 1 + (g % n) * S + S;
+    };
+    std::thread egress([&] {
+        try {
+            if (hipSetDevice(ctx->device) != hipSuccess) throw DevError("hipSetDevice failed (egress)");
+            uint64_t E = 0, Kprev = 0;
+            for (uint64_t p = 0; p < P; ++p) {
+                {
+                    std::unique_lock<std::mutex> g(mu);
+                    cv.wait(g, [&] { return issued > p || stop; });
+                    if (issued <= p) {  // stopped early: the copies already issued end first
+                        (void)hipStreamSynchronize(ctx->out_stream);
+                        return;
+                    }
+                }
+                HIPCHK(hipEventSynchronize(ctx->part_ev[2 * p + 1]));
+                const uint64_t Kc = hK[p];
+                if (Kc < Kprev || Kc > R) break;  // a poisoned part: the verdict says so
+                Kprev = Kc;
+                const uint64_t E1 = std::min(end_of(Kc), out_cap);
+                if (E1 > E) HIPCHK(hipMemcpyAsync(h_out + E, d_out + E, E1 - E, hipMemcpyDeviceToHost, ctx->out_stream));
+                E = std::max(E, E1);
+                htrace("pipe: part egress issued");
+            }
+            HIPCHK(hipStreamSynchronize(ctx->out_stream));
+            egress_end = E;
+        } catch (const DevError& e) {
+            d2h_err = e.msg;
+        } catch (const std::exception& e) {
+            d2h_err = e.what();
+        }
+    });
+    struct Join {  // the egress thread ends before this frame does, whatever throws
+        std::thread& t;
+        std::mutex& mu;
+        std::condition_variable& cv;
+        bool& stop;
+        ~Join() {
+            {
+                std::lock_guard<std::mutex> g(mu);
+                stop = true;
+            }
+            cv.notify_all();
+            if (t.joinable()) t.join();
+        }
+    } joiner{egress, mu, cv, stop};
+    // ---- ingest + kernels, part by part
+    FxArgs Alast{};
+    bool have_A = false;
+    const char* fail_env = getenv("SKV_TEST_FAIL_PART");  // tests: a failure after part p was queued
+    const uint64_t fail_at = fail_env ? strtoull(fail_env, nullptr, 10) : ~0ull;
+    for (uint64_t p = 0; p < P; ++p) {
+        if (p == fail_at) throw DevError("injected failure before part " + std::to_string(p));
+        for (uint32_t m = 0; m < k; ++m) {
+            const uint64_t lo = p == 0 ? 0 : 1 + lb[p * k + m] * S;
+            const uint64_t hi = p + 1 == P ? job.run_len[m] : 1 + lb[(p + 1) * k + m] * S;
+            if (hi > lo)
+                HIPCHK(hipMemcpyAsync(d_in + img[m] + lo, (const uint8_t*)(uintptr_t)job.run_ptr[m] + lo, hi - lo,
+                                      hipMemcpyHostToDevice, ctx->in_stream));
+        }
+        HIPCHK(hipEventRecord(ctx->part_ev[2 * p], ctx->in_stream));
+        HIPCHK(hipStreamWaitEvent(st, ctx->part_ev[2 * p], 0));
+        if (kp[p]) {
+            std::vector<uint32_t> sfr(kp[p] + 1);
+            for (uint32_t s = 0; s <= kp[p]; ++s) sfr[s] = s;
+            FxPartIO io;
+            io.gbase = p ? d_Kp + p - 1 : nullptr;
+            io.Kout = d_Kp + p;
+            io.flags = d_pflags;
+            io.out = d_out;
+            uint64_t* rb_unused = nullptr;
+            Alast = fx_launch(ctx, kp[p], kp[p], d_runs + p * k, sfr, f, recbp[p], n, out_cap, &io, rb_unused);
+            have_A = true;
+        } else if (p) {
+            launch_copy_bytes(st, (uint8_t*)(d_Kp + p), (const uint8_t*)(d_Kp + p - 1), 8);
+        }
+        launch_fx_publish(st, d_Kp + p, (uint64_t*)hK + p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ctx->part_ev[2 * p + 1], st));
+        {
+            std::lock_guard<std::mutex> g(mu);
+            issued = p + 1;
+        }
+        cv.notify_one();
+    }
+    htrace("pipe: all parts queued");
+    if (!have_A) throw DevError("internal: pipelined call without records");
+    // ---- descriptors over the whole output, one readback with the verdict
+    Alast.Kout = d_Kp + P - 1;
+    launch_fx_desc(st, Alast, d_desc, d_prb, max_runs);
+    HIPCHK(hipGetLastError());
+    const uint64_t guess = std::min<uint64_t>(max_runs, 64 + job.in_bytes / (n * S));
+    uint8_t* hp = (uint8_t*)pinned(ctx, 64 + guess * sizeof(DevRunDesc));
+    d2h(ctx, hp, d_prb, 24);
+    d2h(ctx, hp + 32, d_pflags, 16);
+    d2h(ctx, hp + 64, d_desc, guess * sizeof(DevRunDesc));
+    sync(ctx);
+    {
+        std::lock_guard<std::mutex> g(mu);
+        stop = true;
+    }
+    cv.notify_all();
+    egress.join();
+    htrace("pipe: egress done");
+    uint32_t hf[4];
+    memcpy(hf, hp + 32, 16);
+    uint64_t h3[3];
+    memcpy(h3, hp, 24);
+    const uint64_t n_out = h3[0], Kt = h3[1];
+    if (!d2h_err.empty()) {
+        throw DevError("pipelined egress: " + d2h_err);
+    }
+    if (hf[2] || egress_end != h3[2] + n_out) {  // poisoned (or a part count the verdict rejects)
+        used = false;
+        ctx->timings.fused_reject = hf[3] ? hf[3] : 0x80000000u;
+        return SKV_OK;
+    }
+    ResultBox* box = new ResultBox();
+    skv_result* res = &box->pub;
+    res->runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, n_out) * sizeof(skv_run_desc));
+    memcpy(res->runs, hp + 64, std::min(n_out, guess) * sizeof(DevRunDesc));
+    if (n_out > guess)
+        HIPCHK(hipMemcpy(res->runs + guess, d_desc + guess, (n_out - guess) * sizeof(DevRunDesc), hipMemcpyDeviceToHost));
+    res->n_runs = n_out;
+    res->bytes = h_out;
+    h_out = nullptr;  // the result owns it now
+    res->n_bytes = h3[2] + n_out;
+    res->in_bytes = job.in_bytes;
+    res->in_records = R;
+    res->out_records = Kt;
+    res->dropped_tables = 0;
+    box->pool = ctx->out_pool;
+    box->pool_cap = cap;
+    skv_timings& t = ctx->timings;
+    t = skv_timings{};
+    t.path = SKV_PATH_FUSED;
+    t.hot_read_bytes = R * S;  // every input record is read once
+    t.hot_write_bytes = res->n_bytes;
+    t.host_syncs = ctx->syncs;
+    t.host_total_ms = now_ms() - t_entry;
+    t.host_parts = (uint32_t)P;
+    *out = res;
+    return SKV_OK;
+}
+
+// host inputs: stage them into HBM, compact, return the output bytes in pinned host memory
+int compact_host_job(skv_ctx* ctx, Job& job, skv_result** out, double t_entry) {
+    int rc;
+    try {
+        // stage inputs into HBM (16-byte aligned per run)
+        uint64_t total = 0;
+        for (uint64_t l : job.run_len) total += (l + 15) & ~15ull;
+        uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", total + 16);
+        uint64_t off = 0;
+        for (size_t m = 0; m < job.run_ptr.size(); ++m) {
+            if (job.run_len[m]) h2d(ctx, d_in + off, (const void*)job.run_ptr[m], job.run_len[m]);
+            job.run_ptr[m] = (uint64_t)(uintptr_t)(d_in + off);
+            off += (job.run_len[m] + 15) & ~15ull;
+        }
+    } catch (const DevError& e) {
+        return set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());
+    } catch (const std::exception& e) {
+        return set_err(ctx, SKV_E_DEVICE, "host error: %s", e.what());
+    }
+    skv_result* dres = nullptr;
+    rc = run_guarded(ctx, job, &dres, t_entry);
+    if (rc) return rc;
+    ResultBox* box = (ResultBox*)dres;
+    size_t cap = 0;
+    uint8_t* hb = (uint8_t*)ctx->out_pool->take(std::max<uint64_t>(1, dres->n_bytes), cap);
+    if (!hb) {
+        skv_result_free(dres);
+        return set_err(ctx, SKV_E_DEVICE, "pinned host allocation of %" PRIu64 " output bytes failed", dres->n_bytes);
+    }
+    if (dres->n_bytes && (hipMemcpyAsync(hb, dres->bytes, dres->n_bytes, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+                          hipStreamSynchronize(ctx->stream) != hipSuccess)) {
+        ctx->out_pool->give(hb, cap);
+        skv_result_free(dres);
+        return set_err(ctx, SKV_E_DEVICE, "device-to-host copy of the output failed");
+    }
+    dres->bytes = hb;
+    box->pool = ctx->out_pool;
+    box->pool_cap = cap;
+    *out = dres;
+    return SKV_OK;
+}
+
+
+extern "C" {
+
+int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uint64_t max_run_size, uint32_t flags,
+                skv_result** out) {
+    const double t_entry = now_ms();
+    htrace("entry");
+    if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
+    *out = nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    Job job;  // lent ctx tables, as in skv_compact_dev
+    job.ranked.swap(ctx->j_ranked);
+    job.run_ptr.swap(ctx->j_ptr);
+    job.run_len.swap(ctx->j_len);
+    int rc = build_job(ctx, streams, n_streams, max_run_size, flags, job);
+    if (!rc) {
+        bool used = false;
+        try {
+            ctx->timings = skv_timings{};
+            rc = compact_host_pipelined(ctx, job, out, t_entry, used);
+        } catch (const DevError& e) {
+            (void)hipStreamSynchronize(ctx->stream);
+            rc = set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());
+            used = true;
+        } catch (const std::exception& e) {
+            (void)hipStreamSynchronize(ctx->stream);
+            rc = set_err(ctx, SKV_E_DEVICE, "host error: %s", e.what());
+            used = true;
+        }
+        if (!used) rc = compact_host_job(ctx, job, out, t_entry);
+    }
+    job.ranked.swap(ctx->j_ranked);
+    job.run_ptr.swap(ctx->j_ptr);
+    job.run_len.swap(ctx->j_len);
+    return rc;
+}
+
+int skv_encode_batch(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_t max_run_size, skv_result** out) {
+    const double t_entry = now_ms();
+    if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
+    *out = nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    Job job;
+    int rc = batch_job(ctx, ops_run, len, max_run_size, job);
+    if (rc) return rc;
+    return compact_host_job(ctx, job, out, t_entry);
+}
+
+}  // extern "C"

@@ -30,6 +30,10 @@
 namespace skv {
 
 static_assert(FX_HSLOTS >= 2 * FX_CAP && FX_CAP < 65535, "distinct-key set: 16-bit slots at <= 1/2 load");
+static_assert((FX_HSLOTS & (FX_HSLOTS - 1)) == 0, "distinct-key set: probes wrap with & (FX_HSLOTS - 1)");
+// The early survivor count takes (hi, lo) = the first 16 key bytes as the whole key: true only while
+// the fused path admits keys of at most 16 bytes (and Puts only; the host's fused gate).
+static_assert(FX_MAX_K <= 16, "fused keys must fit the 16-byte (hi, lo) compare key");
 
 typedef unsigned int fx_u32x4 __attribute__((ext_vector_type(4)));
 

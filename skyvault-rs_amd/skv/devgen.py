@@ -47,13 +47,16 @@ def make_cfg3_on_device(device, seed, n_streams, run_mib, vsize=256):
 
 def make_cfg3_full_on_device(device, seed, n_streams, run_mib, vsize=256, with_index=False):
     """Config 3 at BASELINE size, built in HBM: per stream ~run_mib MiB of records whose keys are
-    an order-preserving 11-character base-62 rendering of a sorted unique id (ids drawn from a
-    universe shared by all streams, so streams overlap and equal ids give equal keys) plus a
-    deterministic alnum tail, 11-128 B in all; 10 % Deletes; 256 B random values.
+    an order-preserving 5-character base-62 rendering of a sorted unique id (ids drawn from a
+    universe shared by all streams, so streams overlap and equal ids give equal keys; 62^5 =
+    9.2e8 covers the 4.1e8-id universe of BASELINE's 256 x 256 MiB) plus a deterministic alnum
+    tail, 8-128 B in all (BASELINE's 8-128 B, so keys shorter than the 16-byte
+    prefix, zero-padded in the device key words, occur); 10 % Deletes; 256 B random values.
     with_index: also return each stream's (ids, record offsets) — key order is id order, so the
     full-size tests cut every stream into the same key ranges without parsing it."""
     n = (run_mib << 20) // 333
     universe = n * n_streams * 2
+    assert universe <= 62 ** 5, "ids must fit the 5-character prefix"
     M = 0x7FFFFFFFFFFFFFFF
 
     def h(x):  # a 63-bit integer mix (deterministic, non-negative)
@@ -64,14 +67,14 @@ def make_cfg3_full_on_device(device, seed, n_streams, run_mib, vsize=256, with_i
 
     alnum = torch.tensor(list(b"0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz"), dtype=torch.int64,
                          device=device)
-    pow62 = torch.tensor([62 ** (10 - i) for i in range(11)], dtype=torch.int64, device=device)
+    pow62 = torch.tensor([62 ** (4 - i) for i in range(5)], dtype=torch.int64, device=device)
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     runs, index = [], []
     for s in range(n_streams):
         ids = torch.unique(torch.randint(0, universe, (n + n // 20,), generator=g, device=device))[:n]
         m = ids.numel()
-        klen = 11 + h(ids) % 118
+        klen = 8 + h(ids) % 121
         is_put = h(ids ^ (seed + 7919 * s)) % 1000 >= 100
         size = 5 + klen + torch.where(is_put, 4 + vsize, 0)
         off = torch.cumsum(size, 0) - size + 1
@@ -84,7 +87,7 @@ def make_cfg3_full_on_device(device, seed, n_streams, run_mib, vsize=256, with_i
         kidx = torch.repeat_interleave(torch.arange(m, device=device), klen)
         kpos = torch.arange(kidx.numel(), device=device) - torch.repeat_interleave(torch.cumsum(klen, 0) - klen, klen)
         kid = ids[kidx]
-        digit = torch.where(kpos < 11, (kid // pow62[kpos.clamp(max=10)]) % 62, h(kid * 131 + kpos) % 62)
+        digit = torch.where(kpos < 5, (kid // pow62[kpos.clamp(max=4)]) % 62, h(kid * 131 + kpos) % 62)
         buf[off[kidx] + 5 + kpos] = alnum[digit].to(torch.uint8)
         del kidx, kpos, kid, digit
         pidx = torch.nonzero(is_put).squeeze(1)

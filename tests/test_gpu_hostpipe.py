@@ -153,3 +153,23 @@ def test_config2_shape_large(dev, pipe_env):
         rec[:, 25:] = rng.integers(0, 256, (20_000, 256), dtype=np.uint8)
         streams.append((s + 1, [b"\x01" + rec.tobytes()]))
     _check(dev, streams, 4 * MiB, 0, 16)
+
+
+@pytest.mark.parametrize("fail_at", [0, 1, 3])
+def test_failure_mid_pipeline_leaves_the_ctx_clean(dev, pipe_env, fail_at):
+    """A failure after some parts were queued (SKV_TEST_FAIL_PART) ends the call with
+    SKV_E_DEVICE and its text; the copies it had issued are drained and its pinned output goes
+    back to the pool, so the next calls on the same ctx (pipelined and serial) are exact."""
+    rng = random.Random(40 + fail_at)
+    streams = _streams(rng, 8, 3000, 12000)
+    os.environ["SKV_HOST_PARTS"] = "6"
+    os.environ["SKV_TEST_FAIL_PART"] = str(fail_at)
+    try:
+        with pytest.raises(_abi.RunError) as ei:
+            dev.compact(streams, 4 * MiB, 0)
+    finally:
+        os.environ.pop("SKV_TEST_FAIL_PART", None)
+    assert ei.value.code == _abi.SKV_E_DEVICE and "injected failure" in ei.value.message
+    for _ in range(3):  # the pool's buffer is taken and given back again on every call
+        _check(dev, streams, 4 * MiB, 0, 6)
+    _check(dev, _streams(rng, 3, 500, 4000), 4 * MiB, 0, 4)
