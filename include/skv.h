@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SKV_ABI_VERSION 3  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts */
+#define SKV_ABI_VERSION 4  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts; 4: skv_scan_runs */
 
 typedef struct skv_ctx skv_ctx;
 
@@ -226,6 +226,26 @@ int skv_run_index_create(skv_ctx* ctx, const uint8_t* run, uint64_t len, skv_run
 int skv_run_index_search(skv_ctx* ctx, const skv_run_index* index, const uint8_t* keys, const uint64_t* key_offs,
                          uint32_t n_keys, skv_lookup* out);
 void skv_run_index_free(skv_run_index* index);
+
+/*
+ * The cache service's ScanFromRun (cache_service.rs:97-151) over runs it has fetched: run i is
+ * decoded by runs::read_run_iter (runs.rs:400-510) at SeqNo i64::MAX - i (:113-115), filtered to
+ * keys strictly above exclusive_start_key (:125-129), merged by k_way::merge (:134), and read until
+ * the max_results-th Put (:140-148; Deletes are returned but not counted). The response items come
+ * back as ONE v1 run in response order (an item is a record: Put key + value, or Delete key) with
+ * its StatsV1 in runs[0]; no item -> n_runs == 0. max_results outside 1..=10000 -> SKV_E_INVALID_ARG
+ * with the reference's text ("max_results must be between 1 and 10000", Status::invalid_argument).
+ * A merge error the reader reaches -> its RunError code and Display text, with read_run_iter's
+ * texts ("Data format error: Incomplete key length data" / "... value length data" where
+ * read_run_stream reports an Io error); the service wraps it as "Merge stream error: {e}" (:141).
+ * Unsorted runs are merged in the reference's heap pop order. skv_scan_runs takes host runs and
+ * returns the run in pinned host memory; skv_scan_runs_dev takes device pointers and returns a
+ * device pointer owned by the ctx (as skv_compact_dev).
+ */
+int skv_scan_runs(skv_ctx* ctx, const uint8_t* const* runs, const uint64_t* run_lens, uint32_t n_runs,
+                  const uint8_t* exclusive_start_key, uint64_t start_len, uint64_t max_results, skv_result** out);
+int skv_scan_runs_dev(skv_ctx* ctx, const uint8_t* const* runs, const uint64_t* run_lens, uint32_t n_runs,
+                      const uint8_t* exclusive_start_key, uint64_t start_len, uint64_t max_results, skv_result** out);
 
 void skv_result_free(skv_result* r);
 

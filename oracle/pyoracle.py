@@ -66,6 +66,9 @@ def lib():
                                      C.POINTER(C.c_int64), C.c_uint32,
                                      C.POINTER(C.POINTER(SkvoOpList)), C.c_char_p, C.c_size_t]
         l.skvo_merge_ops.restype = C.c_int
+        l.skvo_scan_runs.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint64,
+                                     C.POINTER(C.POINTER(SkvResult)), C.c_char_p, C.c_size_t]
+        l.skvo_scan_runs.restype = C.c_int
         l.skvo_result_free.argtypes = [C.POINTER(SkvResult)]
         l.skvo_op_list_free.argtypes = [C.POINTER(SkvoOpList)]
         l.skvo_sb_new.argtypes = [C.c_uint64]
@@ -117,6 +120,26 @@ def _op_list(ptr) -> List[Op]:
         else:
             out.append((False, k, None))
     return out
+
+
+def scan_runs(runs: Sequence[bytes], start_key: bytes, max_results: int):
+    """ScanFromRun (cache_service.rs:97-151) over fetched runs: the response items as one v1 run
+    ([OutRun], empty when there is no item), or RunError (the reference wraps it as
+    Status::internal("Merge stream error: {e}")) / SKV_E_INVALID_ARG for max_results."""
+    bufs = [C.create_string_buffer(bytes(r), max(1, len(r))) for r in runs]
+    ptrs = (C.c_void_p * max(1, len(runs)))(*[C.cast(b, C.c_void_p) for b in bufs])
+    lens = (C.c_uint64 * max(1, len(runs)))(*[len(r) for r in runs])
+    sk = C.create_string_buffer(bytes(start_key), max(1, len(start_key)))
+    res = C.POINTER(SkvResult)()
+    eb = C.create_string_buffer(512)
+    rc = lib().skvo_scan_runs(C.cast(ptrs, C.c_void_p), C.cast(lens, C.c_void_p), len(runs), C.cast(sk, C.c_void_p),
+                              len(start_key), max_results, C.byref(res), eb, 512)
+    if rc != SKV_OK:
+        raise RunError(rc, eb.value.decode("utf-8", "replace"))
+    try:
+        return result_to_runs(res.contents)
+    finally:
+        lib().skvo_result_free(res)
 
 
 def compact(streams: Sequence[tuple], max_run_size: int, flags: int = 0, with_result: bool = False):

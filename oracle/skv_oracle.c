@@ -122,6 +122,12 @@ typedef struct {
     uint64_t pos;
     int started;
     int done;
+    /* 1: runs::read_run_iter / RunIterator (runs.rs:400-510) instead of read_run_stream. Same
+     * checks in the same order; the two EOF checks raise Format errors with their own text
+     * ("Incomplete key length data" :428-430, "Incomplete value length data" :457-459) where
+     * read_run_stream raises Io. Its "Unexpected end of data" (:421-423) and the two overflow
+     * checks (:440-442, :469-471) cannot trigger (len == bytes.len(); u32 lengths on u64). */
+    int iter;
 } dec_t;
 
 static void dec_init(dec_t* d, const uint8_t* buf, uint64_t len) {
@@ -130,6 +136,7 @@ static void dec_init(dec_t* d, const uint8_t* buf, uint64_t len) {
     d->pos = 0;
     d->started = 0;
     d->done = 0;
+    d->iter = 0;
 }
 
 /* 1 = op produced, 0 = end of run, <0 = -(error code) */
@@ -146,7 +153,10 @@ static int dec_next(dec_t* d, oop* o, char* eb, size_t en) {
     uint64_t len = d->len, p = d->pos;
     uint8_t marker = b[p];
     p += 1;
-    if (p + 4 > len) { d->done = 1; return -E_EOF(eb, en); }
+    if (p + 4 > len) {
+        d->done = 1;
+        return d->iter ? -E_FORMAT(eb, en, "Incomplete key length data") : -E_EOF(eb, en); /* :428-430 */
+    }
     uint64_t klen = be32(b + p);
     p += 4;
     if (p + klen > len) { d->done = 1; return -E_FORMAT(eb, en, "Incomplete key data"); }
@@ -154,7 +164,11 @@ static int dec_next(dec_t* d, oop* o, char* eb, size_t en) {
     uint8_t* key = dup_bytes(b + p, klen); /* k.to_string() */
     p += klen;
     if (marker == 1) {
-        if (p + 4 > len) { free(key); d->done = 1; return -E_EOF(eb, en); }
+        if (p + 4 > len) {
+            free(key);
+            d->done = 1;
+            return d->iter ? -E_FORMAT(eb, en, "Incomplete value length data") : -E_EOF(eb, en); /* :457-459 */
+        }
         uint64_t vlen = be32(b + p);
         p += 4;
         if (p + vlen > len) { free(key); d->done = 1; return -E_FORMAT(eb, en, "Incomplete value data"); }
@@ -190,6 +204,11 @@ typedef struct {
     /* pre-decoded mode (skvo_merge_ops) */
     const skvo_op* ops;
     uint64_t n_ops, next_op;
+    /* ScanFromRun's per-run filter (cache_service.rs:125-129): try_filter(op.key() > start) drops
+     * Ok items with key <= start and passes errors through */
+    const uint8_t* gt_key;
+    uint64_t gt_len;
+    int filter;
 } sit_t;
 
 static int sit_next(sit_t* it, oop* o, char* eb, size_t en) {
@@ -205,6 +224,10 @@ static int sit_next(sit_t* it, oop* o, char* eb, size_t en) {
     }
     while (it->member < it->s->n_runs) {
         int r = dec_next(&it->dec, o, eb, en);
+        if (r == 1 && it->filter && key_cmp(o->key, o->klen, it->gt_key, it->gt_len) <= 0) {
+            oop_free(o);
+            continue;
+        }
         if (r != 0) return r;
         it->member++;
         if (it->member < it->s->n_runs)
@@ -506,10 +529,17 @@ static int wal_push(walc* w, oop* op, char* eb, size_t en) {
 }
 
 /* ------------------------------------------------------------------------------------ */
+#define SCAN_STOP 1000 /* the scan's reader stopped reading: not an error, and nothing later is seen */
 typedef struct {
     uint32_t flags;
     builder bld;
     walc wal;
+    /* ScanFromRun's reader (cache_service.rs:137-148): every merged op goes into the response (one
+     * v1 run of records here), Puts are counted, and the reader stops after the max_results-th */
+    int scan;
+    uint64_t scan_max, scan_puts;
+    outbuf* scan_out;
+    skv_run_desc scan_desc;
     /* skvo_merge_ops collection */
     int collect;
     skvo_op* col;
@@ -537,6 +567,34 @@ static int consume(consumer* c, oop* op, char* eb, size_t en) {
         c->col_bufs[2 * c->n_col + 1] = op->val;
         c->n_col++;
         return SKV_OK; /* ownership moved */
+    }
+    if (c->scan) {
+        outbuf* o = c->scan_out;
+        const uint64_t sz = op->is_put ? 1 + 4 + (uint64_t)op->klen + 4 + op->vlen : 1 + 4 + (uint64_t)op->klen;
+        ob_reserve(o, (o->n ? 0 : 1) + sz);
+        if (!o->n) o->b[o->n++] = 1; /* the response as one v1 run: version byte first */
+        skv_run_desc* d = &c->scan_desc;
+        if (!d->put_count && !d->delete_count) {
+            d->min_key_off = o->n + 5;
+            d->min_key_len = op->klen;
+        }
+        d->max_key_off = o->n + 5;
+        d->max_key_len = op->klen;
+        uint8_t* w = o->b + o->n;
+        w[0] = op->is_put ? 1 : 2;
+        put_be32(w + 1, op->klen);
+        memcpy(w + 5, op->key, op->klen);
+        if (op->is_put) {
+            put_be32(w + 5 + op->klen, (uint32_t)op->vlen);
+            if (op->vlen) memcpy(w + 9 + op->klen, op->val, (size_t)op->vlen);
+            d->put_count++;
+            c->scan_puts++; /* :143 counts Puts only */
+        } else {
+            d->delete_count++;
+        }
+        o->n += sz;
+        oop_free(op);
+        return c->scan_puts >= c->scan_max ? SCAN_STOP : SKV_OK; /* :145-147 */
     }
     if (c->flags & SKV_SPLIT_BY_TABLE) {
         rc = wal_push(&c->wal, op, eb, en);
@@ -580,7 +638,7 @@ static int run_merge(sit_t* its, const int64_t* seqs, uint32_t n, consumer* c, c
             last_klen = it.op.klen;
             have_last = 1;
             rc = consume(c, &it.op, eb, en);
-            if (rc != SKV_OK) break;
+            if (rc != SKV_OK) break; /* an error, or SCAN_STOP: no refill is ever read */
         } else {
             oop_free(&it.op);
         }
@@ -700,6 +758,67 @@ int skvo_compact(const skv_stream* streams, uint32_t n, uint64_t max_run_size, u
     skv_result* r = finish_result(&ob);
     r->in_bytes = in_bytes;
     r->dropped_tables = dropped;
+    *out = r;
+    return SKV_OK;
+}
+
+/* cache_service.rs:97-151 ScanFromRun over runs already fetched: max_results in 1..=10000
+ * (:101-104), run i decoded by read_run_iter (runs.rs:493-510) at SeqNo i64::MAX - i (:113-115),
+ * filtered to key > exclusive_start_key (:125-129), k_way::merge (:134), read until the
+ * max_results-th Put (:140-148). The response items are returned as one v1 run (records in
+ * response order) with its StatsV1, or no run when there is no item. A merge error the reader
+ * reaches is returned as the RunError (the service wraps it: "Merge stream error: {e}", :141). */
+int skvo_scan_runs(const uint8_t* const* runs, const uint64_t* lens, uint32_t n, const uint8_t* start,
+                   uint64_t start_len, uint64_t max_results, skv_result** out, char* eb, size_t en) {
+    if (!out) return fail(eb, en, SKV_E_INVALID_ARG, "out is NULL");
+    *out = NULL;
+    if (max_results < 1 || max_results > 10000)
+        return fail(eb, en, SKV_E_INVALID_ARG, "max_results must be between 1 and 10000");
+    if (n && (!runs || !lens)) return fail(eb, en, SKV_E_INVALID_ARG, "runs/lens is NULL");
+    if (start_len && !start) return fail(eb, en, SKV_E_INVALID_ARG, "start key is NULL");
+    skv_stream* st = (skv_stream*)calloc(n ? n : 1, sizeof(skv_stream));
+    sit_t* its = (sit_t*)calloc(n ? n : 1, sizeof(sit_t));
+    int64_t* seqs = (int64_t*)xmalloc((size_t)(n ? n : 1) * sizeof(int64_t));
+    uint64_t in_bytes = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        st[i].runs = &runs[i];
+        st[i].run_lens = &lens[i];
+        st[i].n_runs = 1;
+        st[i].seq_no = INT64_MAX - (int64_t)i;
+        its[i].s = &st[i];
+        dec_init(&its[i].dec, runs[i], lens[i]);
+        its[i].dec.iter = 1;
+        its[i].filter = 1;
+        its[i].gt_key = start;
+        its[i].gt_len = start_len;
+        seqs[i] = st[i].seq_no;
+        in_bytes += lens[i];
+    }
+    outbuf ob;
+    memset(&ob, 0, sizeof ob);
+    consumer c;
+    memset(&c, 0, sizeof c);
+    c.scan = 1;
+    c.scan_max = max_results;
+    c.scan_out = &ob;
+    int rc = run_merge(its, seqs, n, &c, eb, en);
+    if (rc == SCAN_STOP) rc = SKV_OK;
+    free(its);
+    free(seqs);
+    free(st);
+    if (rc != SKV_OK) {
+        free(ob.b);
+        free(ob.runs);
+        return rc;
+    }
+    if (ob.n) {
+        c.scan_desc.off = 0;
+        c.scan_desc.len = ob.n;
+        ob_push_run(&ob, &c.scan_desc);
+        ob.out_records = c.scan_desc.put_count + c.scan_desc.delete_count;
+    }
+    skv_result* r = finish_result(&ob);
+    r->in_bytes = in_bytes;
     *out = r;
     return SKV_OK;
 }

@@ -55,6 +55,12 @@ int skvo_merge_ops(const skvo_op* const* ops, const uint64_t* n_ops, const int64
 int skvo_compact(const skv_stream* streams, uint32_t n_streams, uint64_t max_run_size,
                  uint32_t flags, skv_result** out, char* errbuf, size_t errlen);
 
+/* cache_service.rs:97-151 ScanFromRun over fetched runs: read_run_iter decode (runs.rs:400-510),
+ * key > start filter, k_way::merge at SeqNo i64::MAX - index, read until the max_results-th Put.
+ * The response items come back as one v1 run (0 runs when empty). Same contract as skv_scan_runs. */
+int skvo_scan_runs(const uint8_t* const* runs, const uint64_t* lens, uint32_t n_runs, const uint8_t* start_key,
+                   uint64_t start_len, uint64_t max_results, skv_result** out, char* errbuf, size_t errlen);
+
 void skvo_result_free(skv_result* r);
 
 /* Streaming build_runs for full-size checks (test infrastructure): feed the merged op sequence

@@ -481,7 +481,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             // one record size and one key length <= 16 everywhere: the fused stride path
             const RunFmt f0 = hf[0];
             const char* fenv = getenv("SKV_FUSED");
-            if (allow_deferred && uniform && !job.batch && !job.search && !(job.flags & SKV_SPLIT_BY_TABLE) &&
+            if (allow_deferred && uniform && !job.batch && !job.search && !job.scan && !(job.flags & SKV_SPLIT_BY_TABLE) &&
                 !(fenv && fenv[0] == '0') &&
                 f0.K <= FX_MAX_K && f0.S >= FX_MIN_S && f0.S <= FX_MAX_S && k <= (uint32_t)TILE_TARGET / 2 &&
                 R < 0xFFFFFFFFull) {
@@ -496,7 +496,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                                rec_meta, d_flags, d_stream_base, job.batch ? nullptr : d_first_dec, rec_fp,
                                dbuf<uint32_t>(ctx, "wave_run", (R + 63) / 64 + 1));
             mark(ctx, PH_PARSE);
-            if (allow_deferred && !(job.flags & SKV_SPLIT_BY_TABLE) && !job.search) {
+            if (allow_deferred && !(job.flags & SKV_SPLIT_BY_TABLE) && !job.search && !job.scan) {
                 deferred = true;  // verdict read with the result
                 parsed = true;
                 std::fill(first_dec.begin(), first_dec.end(), ~0ull);
@@ -567,14 +567,58 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     for (uint32_t s = 0; s < k; ++s)
         if (first_dec[s] != ~0ull && first_dec[s] + 1 < stream_valid[s]) any_dec = true;
 
+    // ---- ScanFromRun (skv_scan_host.hip): a run's decode error surfaces after the pop of its last
+    // record above the start key, or, with none, at the merge's first pulls in vector order
+    // (k_way.rs:126-140) -- the first such run's error ends the scan before any item
+    std::vector<ScanEvent> scan_ev;
+    uint8_t* d_start = nullptr;
+    if (job.scan) {
+        const uint32_t slen = (uint32_t)job.scan_start.size();
+        d_start = dbuf<uint8_t>(ctx, "scan_start", slen + 32);  // + the aligned blocks key_cmp may read
+        HIPCHK(hipMemsetAsync(d_start, 0, slen + 32, st));
+        if (slen) h2d_up(ctx, d_start, job.scan_start.data(), slen);
+        if (any_err) {
+            unsigned long long* lk = dbuf<unsigned long long>(ctx, "scan_last_kept", k);
+            HIPCHK(hipMemsetAsync(lk, 0, (size_t)k * 8, st));
+            launch_scan_last_kept(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_start, slen, lk);
+            HIPCHK(hipGetLastError());
+            std::vector<unsigned long long> hlk(k);
+            uint8_t* hp = (uint8_t*)pinned(ctx, (size_t)k * 8 + 16);
+            d2h(ctx, hp, lk, (size_t)k * 8);
+            sync(ctx);
+            memcpy(hlk.data(), hp, (size_t)k * 8);
+            int64_t first_v = -1;
+            ScanEvent first_pull{};
+            for (uint32_t s = 0; s < k; ++s) {
+                if (!stream_err[s]) continue;
+                const RunInfo& run = runs[stream_first_run[s]];  // one run per stream
+                uint64_t err_off = 1;
+                if (stream_valid[s]) {
+                    const uint64_t last = stream_base[s] + stream_valid[s] - 1;
+                    err_off = read_dev(rec_addr + last) + (read_dev(rec_meta + last) & 0x7FFFFFFFu) - run.ptr;
+                }
+                ScanEvent e{s, hlk[s] ? hlk[s] - 1 : 0, 0, std::string()};
+                e.code = scan_err_to_api(stream_err[s], err_off, run.len, e.msg);
+                if (hlk[s]) {
+                    scan_ev.push_back(e);
+                } else if (first_v < 0 || job.ranked[s].vec_idx < (uint32_t)first_v) {
+                    first_v = job.ranked[s].vec_idx;
+                    first_pull = e;
+                }
+            }
+            if (first_v >= 0) throw ApiError{first_pull.code, first_pull.msg};
+        }
+    }
+
     // ---- errors: which one k_way::merge surfaces first --------------------------------------
     // Heap-order mode (skv_heap.hip) where the outcome depends on the merge's exact pop sequence
     // past a stream's first key decrease or decode error: the WAL split with either, and the Delete
     // filter with a decrease. Everywhere else the first trigger record decides (below).
     const bool wal = (job.flags & SKV_SPLIT_BY_TABLE) != 0;
-    const bool heap = !job.batch && ((wal && (any_err || any_dec)) || ((job.flags & SKV_DROP_TOMBSTONES) && any_dec));
+    const bool heap = !job.batch && ((wal && (any_err || any_dec)) || ((job.flags & SKV_DROP_TOMBSTONES) && any_dec) ||
+                                     (job.scan && (any_err || any_dec)));
     HeapRes hres;
-    if (any_err || any_dec) {
+    if ((any_err || any_dec) && !job.scan) {  // (the scan resolved its first pulls above)
         // (1) first items are pulled in the caller's vector order (k_way.rs:126-140)
         std::vector<uint32_t> by_vec(k);
         for (uint32_t s = 0; s < k; ++s) by_vec[job.ranked[s].vec_idx] = s;
@@ -927,6 +971,13 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         if (verify_pending) HIPCHK(hipStreamWaitEvent(st, ctx->aux_ev[1], 0));
         verify_pending = false;
     };
+    if (job.scan) {
+        join_verify();
+        const int rc = scan_stage(ctx, job, R, d_K, m_rec, m_src, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, d_start,
+                                  fp_bad, heap ? &hres : nullptr, scan_ev, out);
+        if (rc == RC_RETRY_EXACT) return rerun_exact(ctx, job, out);
+        return rc;
+    }
     if (job.flags & SKV_SPLIT_BY_TABLE) {
         join_verify();
         htrace("merge launched");

@@ -224,6 +224,11 @@ struct Job {
     skv_lookup* sr_out = nullptr;
     bool search = false;
     struct skv_run_index* index_out = nullptr;  // skv_run_index_create: keep the parse, search nothing
+    // skv_scan_runs (ScanFromRun, cache_service.rs:97-151): one run per stream at SeqNo
+    // i64::MAX - index, read_run_iter's error texts, key > start filter, cut at the max-th Put
+    bool scan = false;
+    std::string scan_start;
+    uint64_t scan_max = 0;
 };
 
 std::string fetch_key(skv_ctx* ctx, const uint64_t* d_rec_addr, const uint32_t* d_rec_klen, uint64_t rec);
@@ -314,4 +319,16 @@ int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t max_
 void drain(skv_ctx* ctx);
 int run_guarded(skv_ctx* ctx, const Job& job, skv_result** out, double t_entry);
 int compact_host_job(skv_ctx* ctx, Job& job, skv_result** out, double t_entry);
+// skv_scan_host.hip: the scan's device stage after the merge, and read_run_iter's error text
+struct ScanEvent {  // a run's decode error and the record it surfaces after
+    uint32_t s;             // stream (rank order)
+    uint64_t after_rec;     // original record index of the run's last record above the start key
+    int code;
+    std::string msg;
+};
+int scan_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, const uint32_t* m_rec,
+               const uint64_t* m_src, const uint64_t* rec_addr, const uint64_t* rec_hi, const uint64_t* rec_lo,
+               const uint32_t* rec_klen, const uint32_t* rec_meta, const uint8_t* d_start, const uint32_t* fp_bad,
+               const HeapRes* heap, const std::vector<ScanEvent>& events, skv_result** out);
+int scan_err_to_api(uint32_t derr, uint64_t err_off, uint64_t run_len, std::string& msg);
 int batch_job(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_t max_run_size, Job& job);

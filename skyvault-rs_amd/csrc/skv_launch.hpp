@@ -136,5 +136,16 @@ void launch_search_scan(hipStream_t, const uint8_t* run, uint64_t len, const uin
                         uint32_t n_q, SrResult* out);
 uint64_t scan_tmp_words(uint64_t n);
 void launch_scan(hipStream_t, const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tmp);
+// skv_scan.hip: ScanFromRun after the merge
+void launch_scan_last_kept(hipStream_t, uint64_t R, const uint64_t* stream_base, uint32_t k, const uint64_t* rec_addr,
+                           const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,
+                           const uint8_t* start, uint32_t slen, unsigned long long* last_kept);
+void launch_scan_mark(hipStream_t, const uint64_t* d_K, uint64_t R, const uint32_t* m_rec, const uint64_t* rec_addr,
+                      const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen, const uint32_t* rec_meta,
+                      const uint8_t* start, uint32_t slen, uint64_t* keep, uint64_t* put, uint64_t* size);
+void launch_scan_cut(hipStream_t, const uint64_t* d_K, const uint64_t* putx, const uint64_t* keepx,
+                     const uint64_t* offx, uint64_t max_results, uint64_t* info);
+void launch_scan_gather(hipStream_t, uint64_t R, const uint64_t* info, const uint64_t* keep, const uint64_t* offx,
+                        const uint64_t* size, const uint64_t* m_src, uint8_t* out);
 void launch_scan_dn(hipStream_t, const uint64_t* in, const uint64_t* dn, uint64_t max_n, uint64_t* out, uint64_t* tmp);
 }  // namespace skv

@@ -138,6 +138,8 @@ EXPORTED_SYMBOLS = [
     "skv_run_index_create",
     "skv_run_index_search",
     "skv_run_index_free",
+    "skv_scan_runs",
+    "skv_scan_runs_dev",
     "skv_result_free",
 ]
 

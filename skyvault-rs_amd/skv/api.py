@@ -66,6 +66,10 @@ def load():
     l.skv_run_index_search.restype = C.c_int
     l.skv_run_index_free.argtypes = [C.c_void_p]
     l.skv_run_index_free.restype = None
+    for fn in (l.skv_scan_runs, l.skv_scan_runs_dev):
+        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint64,
+                       C.POINTER(C.POINTER(SkvResult))]
+        fn.restype = C.c_int
     for fn in (l.skv_encode_batch, l.skv_encode_batch_dev):
         fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.POINTER(SkvResult))]
         fn.restype = C.c_int
@@ -279,6 +283,24 @@ class Compactor:
                 assert o.kind == LOOKUP_PANIC
                 res.append(("panic", PANIC_TEXT[o.panic & 0xFF].format(o.panic >> 8)))
         return res
+
+    def scan_runs(self, runs: Sequence[bytes], exclusive_start_key: bytes, max_results: int):
+        """ScanFromRun (cache_service.rs:97-151) over fetched runs on the device: the response items
+        as one v1 run ([OutRun], [] when there is no item). Raises RunError: SKV_E_INVALID_ARG for
+        max_results outside 1..=10000, or the merge error the reader reaches (read_run_iter text)."""
+        bufs = [C.create_string_buffer(bytes(r), max(1, len(r))) for r in runs]
+        ptrs = (C.c_void_p * max(1, len(runs)))(*[C.cast(b, C.c_void_p) for b in bufs])
+        lens = (C.c_uint64 * max(1, len(runs)))(*[len(r) for r in runs])
+        sk = C.create_string_buffer(bytes(exclusive_start_key), max(1, len(exclusive_start_key)))
+        res = C.POINTER(SkvResult)()
+        rc = self.lib.skv_scan_runs(self.ctx, C.cast(ptrs, C.c_void_p), C.cast(lens, C.c_void_p), len(runs),
+                                    C.cast(sk, C.c_void_p), len(exclusive_start_key), max_results, C.byref(res))
+        if rc != SKV_OK:
+            raise self._err(rc)
+        try:
+            return result_to_runs(res.contents)
+        finally:
+            self.lib.skv_result_free(res)
 
     def timings(self) -> dict:
         t = SkvTimings()

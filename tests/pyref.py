@@ -8,6 +8,7 @@ restatements check each other (tests/test_oracle_vs_pyref.py). Test infrastructu
   filter   : Delete drop at Level::max    src/jobs/table_tree_compaction.rs:139-145
   encode   : runs::build_runs             src/runs.rs:166-282
   wal      : table split + prefix strip   src/jobs/wal_compaction.rs:66-174
+  scan     : ScanFromRun over read_run_iter  src/cache_service.rs:97-151, src/runs.rs:400-510
 """
 from __future__ import annotations
 
@@ -36,8 +37,10 @@ def _utf8_ok(b: bytes) -> bool:
         return False
 
 
-def decode(run: bytes):
-    """Generator of ('put'|'del', key, value) then raise Err (runs.rs:517-628)."""
+def decode(run: bytes, iterator: bool = False):
+    """Generator of ('put'|'del', key, value) then raise Err (runs.rs:517-628). iterator=True:
+    runs::read_run_iter's RunIterator (runs.rs:400-510), whose two length-EOF checks are Format
+    errors with their own text instead of Io."""
     if len(run) == 0:
         raise Err(EMPTY, "Input list of operations cannot be empty")
     if run[0] != 1:
@@ -47,6 +50,8 @@ def decode(run: bytes):
         marker = run[pos]
         pos += 1
         if pos + 4 > n:
+            if iterator:
+                raise Err(FORMAT, "Data format error: Incomplete key length data")
             raise Err(IO, "I/O error: failed to fill whole buffer")
         klen = int.from_bytes(run[pos:pos + 4], "big")
         pos += 4
@@ -58,6 +63,8 @@ def decode(run: bytes):
         pos += klen
         if marker == 1:
             if pos + 4 > n:
+                if iterator:
+                    raise Err(FORMAT, "Data format error: Incomplete value length data")
                 raise Err(IO, "I/O error: failed to fill whole buffer")
             vlen = int.from_bytes(run[pos:pos + 4], "big")
             pos += 4
@@ -71,12 +78,14 @@ def decode(run: bytes):
             raise Err(FORMAT, f"Data format error: Invalid marker byte: {marker}")
 
 
-def stream_items(member_runs):
-    """flatten of the members' read_run_stream; Err surfaces as an ('err', Err) item."""
+def stream_items(member_runs, iterator=False, gt=None):
+    """flatten of the members' read_run_stream; Err surfaces as an ('err', Err) item. gt: keep only
+    Ok items whose key is above it (ScanFromRun's try_filter, cache_service.rs:125-129)."""
     for r in member_runs:
         try:
-            for it in decode(r):
-                yield it
+            for it in decode(r, iterator):
+                if gt is None or it[1] > gt:
+                    yield it
         except Err as e:
             yield ("err", e, None)
             return
@@ -96,9 +105,9 @@ class _Key:
         return self.seq > o.seq
 
 
-def merge(streams):
+def merge(streams, iterator=False, gt=None):
     """k_way::merge: yields emitted ops, raises Err at the first Err pulled."""
-    its = [iter(stream_items(runs)) for _, runs in streams]
+    its = [iter(stream_items(runs, iterator, gt)) for _, runs in streams]
     heap = []
     for i, (seq, _) in enumerate(streams):
         x = next(its[i], None)
@@ -239,3 +248,18 @@ def _wal(streams, max_size, races=None):
     if have:
         finish()
     return result, dropped
+
+
+def scan(runs, start: bytes, max_results: int):
+    """ScanFromRun (cache_service.rs:97-151): the response items [(kind, key, value)], or Err. Run i
+    at SeqNo i64::MAX - i, read_run_iter, key > start, merged; the reader stops right after the
+    max_results-th Put, so a merge error past that point is never seen."""
+    if not 1 <= max_results <= 10000:
+        raise Err(6, "max_results must be between 1 and 10000")
+    items, puts = [], 0
+    for op in merge([(2**63 - 1 - i, [r]) for i, r in enumerate(runs)], iterator=True, gt=start):
+        items.append(op)
+        puts += op[0] == "put"
+        if puts >= max_results:
+            break
+    return items
