@@ -331,7 +331,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     uint32_t* d_broken = dbuf<uint32_t>(ctx, "run_broken", n_runs);
     uint64_t* d_recb = dbuf<uint64_t>(ctx, "run_recb", n_runs + 1);
     HIPCHK(hipMemsetAsync(d_broken, 0, (size_t)n_runs * 4, st));
-    launch_run_header(st, d_runs, n_runs, d_hdr, d_fmt);
+    launch_run_header(st, d_runs, n_runs, d_hdr, d_fmt, job.part);
 
     std::vector<RunSummary>& sum = ctx->s_sum;
     sum.resize(n_runs);  // every entry is written by whichever parse runs
@@ -481,7 +481,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             // one record size and one key length <= 16 everywhere: the fused stride path
             const RunFmt f0 = hf[0];
             const char* fenv = getenv("SKV_FUSED");
-            if (allow_deferred && uniform && !job.batch && !job.search && !job.scan && !(job.flags & SKV_SPLIT_BY_TABLE) &&
+            if (allow_deferred && uniform && !job.batch && !job.search && !job.scan && !job.part &&
+                !(job.flags & SKV_SPLIT_BY_TABLE) &&
                 !(fenv && fenv[0] == '0') &&
                 f0.K <= FX_MAX_K && f0.S >= FX_MIN_S && f0.S <= FX_MAX_S && k <= (uint32_t)TILE_TARGET / 2 &&
                 R < 0xFFFFFFFFull) {
@@ -567,9 +568,10 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     for (uint32_t s = 0; s < k; ++s)
         if (first_dec[s] != ~0ull && first_dec[s] + 1 < stream_valid[s]) any_dec = true;
 
-    // ---- ScanFromRun (skv_scan_host.hip): a run's decode error surfaces after the pop of its last
-    // record above the start key, or, with none, at the merge's first pulls in vector order
-    // (k_way.rs:126-140) -- the first such run's error ends the scan before any item
+    // ---- ScanFromRun (skv_scan_host.hip): the per-run key filter (cache_service.rs:125-129) on the
+    // record arrays, before the merge; a run's decode error surfaces after the pop of its last kept
+    // record, or, with none, at the merge's first pulls in vector order (k_way.rs:126-140) -- the
+    // first such run's error ends the scan before any item
     std::vector<ScanEvent> scan_ev;
     uint8_t* d_start = nullptr;
     if (job.scan) {
@@ -577,37 +579,55 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         d_start = dbuf<uint8_t>(ctx, "scan_start", slen + 32);  // + the aligned blocks key_cmp may read
         HIPCHK(hipMemsetAsync(d_start, 0, slen + 32, st));
         if (slen) h2d_up(ctx, d_start, job.scan_start.data(), slen);
-        if (any_err) {
-            unsigned long long* lk = dbuf<unsigned long long>(ctx, "scan_last_kept", k);
-            HIPCHK(hipMemsetAsync(lk, 0, (size_t)k * 8, st));
-            launch_scan_last_kept(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_start, slen, lk);
-            HIPCHK(hipGetLastError());
-            std::vector<unsigned long long> hlk(k);
-            uint8_t* hp = (uint8_t*)pinned(ctx, (size_t)k * 8 + 16);
-            d2h(ctx, hp, lk, (size_t)k * 8);
-            sync(ctx);
-            memcpy(hlk.data(), hp, (size_t)k * 8);
-            int64_t first_v = -1;
-            ScanEvent first_pull{};
-            for (uint32_t s = 0; s < k; ++s) {
-                if (!stream_err[s]) continue;
-                const RunInfo& run = runs[stream_first_run[s]];  // one run per stream
-                uint64_t err_off = 1;
-                if (stream_valid[s]) {
-                    const uint64_t last = stream_base[s] + stream_valid[s] - 1;
-                    err_off = read_dev(rec_addr + last) + (read_dev(rec_meta + last) & 0x7FFFFFFFu) - run.ptr;
-                }
-                ScanEvent e{s, hlk[s] ? hlk[s] - 1 : 0, 0, std::string()};
-                e.code = scan_err_to_api(stream_err[s], err_off, run.len, e.msg);
-                if (hlk[s]) {
-                    scan_ev.push_back(e);
-                } else if (first_v < 0 || job.ranked[s].vec_idx < (uint32_t)first_v) {
-                    first_v = job.ranked[s].vec_idx;
-                    first_pull = e;
-                }
+        std::vector<ScanEvent> errs;  // read_run_iter's text needs the failing record's offset (unfiltered arrays)
+        for (uint32_t s = 0; s < k; ++s) {
+            if (!stream_err[s]) continue;
+            const RunInfo& run = runs[stream_first_run[s]];  // one run per stream
+            uint64_t err_off = 1;
+            if (stream_valid[s]) {
+                const uint64_t last = stream_base[s] + stream_valid[s] - 1;
+                err_off = read_dev(rec_addr + last) + (read_dev(rec_meta + last) & 0x7FFFFFFFu) - run.ptr;
             }
-            if (first_v >= 0) throw ApiError{first_pull.code, first_pull.msg};
+            ScanEvent e{s, 0, 0, std::string()};
+            e.code = scan_err_to_api(stream_err[s], err_off, run.len, e.msg);
+            errs.push_back(e);
         }
+        uint64_t* keep = dbuf<uint64_t>(ctx, "scf_keep", R + 1);
+        uint64_t* keepx = dbuf<uint64_t>(ctx, "scf_keepx", R + 1);
+        uint64_t* ftmp = dbuf<uint64_t>(ctx, "scf_scan_tmp", scan_tmp_words(R + 1) + 64);
+        uint64_t* f_addr = dbuf<uint64_t>(ctx, "scf_addr", R);
+        uint64_t* f_hi = dbuf<uint64_t>(ctx, "scf_hi", R);
+        uint64_t* f_lo = dbuf<uint64_t>(ctx, "scf_lo", R);
+        uint32_t* f_klen = dbuf<uint32_t>(ctx, "scf_klen", R);
+        uint32_t* f_meta = dbuf<uint32_t>(ctx, "scf_meta", R);
+        uint64_t* f_base = dbuf<uint64_t>(ctx, "scf_base", k + 1);
+        launch_scan_filter(st, R, k, d_stream_base, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, d_start, slen, keep,
+                           keepx, ftmp, f_addr, f_hi, f_lo, f_klen, f_meta, f_base);
+        HIPCHK(hipGetLastError());
+        uint8_t* hp = (uint8_t*)pinned(ctx, (size_t)(k + 1) * 8 + 16);
+        d2h(ctx, hp, f_base, (size_t)(k + 1) * 8);
+        sync(ctx);
+        memcpy(stream_base.data(), hp, (size_t)(k + 1) * 8);
+        HIPCHK(hipMemcpyAsync(d_stream_base, f_base, (size_t)(k + 1) * 8, hipMemcpyDeviceToDevice, st));
+        rec_addr = f_addr;
+        rec_hi = f_hi;
+        rec_lo = f_lo;
+        rec_klen = f_klen;
+        rec_meta = f_meta;
+        R = stream_base[k];
+        int64_t first_v = -1;
+        const ScanEvent* first_pull = nullptr;
+        for (const ScanEvent& e : errs) {
+            const uint64_t kept = stream_base[e.s + 1] - stream_base[e.s];
+            if (kept) {
+                scan_ev.push_back(e);
+                scan_ev.back().after_rec = stream_base[e.s + 1] - 1;  // filtered numbering
+            } else if (first_v < 0 || job.ranked[e.s].vec_idx < (uint32_t)first_v) {
+                first_v = job.ranked[e.s].vec_idx;
+                first_pull = &e;
+            }
+        }
+        if (first_pull) throw ApiError{first_pull->code, first_pull->msg};
     }
 
     // ---- errors: which one k_way::merge surfaces first --------------------------------------
@@ -830,7 +850,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     std::pair<const unsigned long long*, const uint64_t*> verify_args{nullptr, nullptr};
     const unsigned long long* verify_lo = nullptr;  // pairs before it verified beside the merge
     bool verify_pending = false;
-    if (km > 1 && !ctx->exact_keys && !heap) {
+    if (km > 1 && !ctx->exact_keys && !heap && !job.scan) {  // (the scan's filtered arrays carry no fingerprints)
         const char* te = getenv("SKV_FP_TEST");
         if (te && te[0] == '1') {
             uint64_t* f = dbuf<uint64_t>(ctx, "rec_fp_test", R);
@@ -1072,7 +1092,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     fork_verify();  // beside the gather (beside the single-wave chain it slowed the chain 3x)
     // ---- gather -----------------------------------------------------------------------------
     const uint64_t total_rec_bytes = job.in_bytes;
-    uint8_t* d_out = dbuf<uint8_t>(ctx, "out", total_rec_bytes + R + 16);
+    // a part of a pipelined host call writes into the call's shared output buffer (job.dev_out)
+    uint8_t* d_out = job.dev_out ? job.dev_out : dbuf<uint8_t>(ctx, "out", total_rec_bytes + R + 16);
 #if SKV_PAGE_GATHER
     {
         const uint64_t max_out = total_rec_bytes + R + 16;

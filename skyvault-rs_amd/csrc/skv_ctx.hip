@@ -104,8 +104,17 @@ void h2d_up(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
     HIPCHK(hipMemcpyAsync(dst, stage, bytes, hipMemcpyHostToDevice, ctx->stream));
 }
 
+// async D2H of a readback into pinned staging (dst is always a pinned() / arena buffer). In a
+// pipelined host call a copy kernel writes it through the mapping: a DMA copy on the ctx stream
+// could wait behind the egress thread's bulk D2H copies.
 void d2h(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
     if (!bytes) return;
+    if (ctx->kernel_uploads) {
+        void* dptr = nullptr;
+        HIPCHK(hipHostGetDevicePointer(&dptr, dst, 0));
+        launch_copy_bytes(ctx->stream, (uint8_t*)dptr, (const uint8_t*)src, bytes);
+        return;
+    }
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
 }
 void h2d(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {

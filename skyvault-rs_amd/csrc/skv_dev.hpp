@@ -622,7 +622,9 @@ __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, ui
     } else if (h.marker == 2) {
         h.size = 5 + h.klen;
     } else {
-        h.err = DERR_MARKER | (h.marker << 8);
+        // the key's UTF-8 check comes before the marker match (runs.rs:585-591 vs :621-624): a walk
+        // that skipped it (structure only / the ASCII heuristic) does it now, at the failing record
+        h.err = UTF8 != 1 && !utf8_valid_fast(run + kp, h.klen, ld) ? DERR_UTF8 : DERR_MARKER | (h.marker << 8);
         return h;
     }
     h.err = DERR_NONE;

@@ -229,6 +229,10 @@ struct Job {
     bool scan = false;
     std::string scan_start;
     uint64_t scan_max = 0;
+    // a key-range part of a pipelined host call (skv_hostpipe.hip): member runs are slices whose
+    // leading byte is not a version byte, and the output goes to dev_out (the call's shared buffer)
+    bool part = false;
+    uint8_t* dev_out = nullptr;
 };
 
 std::string fetch_key(skv_ctx* ctx, const uint64_t* d_rec_addr, const uint32_t* d_rec_klen, uint64_t rec);

@@ -341,6 +341,347 @@ static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, doub
     return SKV_OK;
 }
 
+// ---- the general key-range pipeline (variable-length records, Deletes) --------------------------
+// skv_compact with host inputs that the fused pipeline does not take: the record framing of every
+// run is walked on host threads (every G-th record start kept), P - 1 cut keys are quantiles of
+// those records' keys, and each run is cut at its first record >= each cut key (equal keys never
+// straddle a cut). Part p is then a compaction of its slices (compact_device in part mode: a
+// slice's leading byte stands in for the version byte) on ctx->stream while the H2D of later parts
+// runs on in_stream and the D2H of finished output on out_stream (its own host thread).
+// build_runs' greedy split carries across parts exactly: part p also takes the previous parts'
+// last (still open) output run -- a valid v1 run, already in the output buffer -- as one more input
+// stream, and writes its output from that run's offset on. All open-run keys sort before part p's,
+// so the merge puts them first unchanged and the split restarts at a true run boundary of the
+// whole output; only the bytes before the open run are final, and those go back to the host. Any
+// error, decrease across a cut or oversized open run ends the attempt; the serial path then gives
+// the reference's exact outcome.
+namespace {
+struct RunWalk {
+    std::vector<uint64_t> at;  // byte offset of records 0, G, 2G, ...
+    uint64_t n = 0;            // records
+    bool ok = true;
+};
+constexpr uint32_t WALK_G = 64;
+
+// the reference's framing checks (runs.rs:559-624) without the key's UTF-8 (the device does those)
+bool host_walk(const uint8_t* b, uint64_t len, RunWalk& w) {
+    if (len == 0 || b[0] != 1) return false;
+    uint64_t p = 1, n = 0;
+    w.at.clear();
+    while (p < len) {
+        const uint8_t marker = b[p];
+        if (p + 5 > len) return false;
+        const uint64_t klen = be32(b + p + 1), kp = p + 5;
+        if (kp + klen > len) return false;
+        uint64_t size;
+        if (marker == 1) {
+            if (kp + klen + 4 > len) return false;
+            const uint64_t vlen = be32(b + kp + klen);
+            if (kp + klen + 4 + vlen > len) return false;
+            size = 9 + klen + vlen;
+        } else if (marker == 2) {
+            size = 5 + klen;
+        } else {
+            return false;
+        }
+        if (n % WALK_G == 0) w.at.push_back(p);
+        ++n;
+        p += size;
+    }
+    w.n = n;
+    return true;
+}
+inline uint64_t host_rec_size(const uint8_t* b, uint64_t p) {
+    const uint64_t klen = be32(b + p + 1);
+    return b[p] == 1 ? 9 + klen + be32(b + p + 5 + klen) : 5 + klen;
+}
+// Rust str Ord: bytewise, a proper prefix first
+inline int host_key_cmp(const uint8_t* a, uint64_t al, const uint8_t* c, uint64_t cl) {
+    const int r = memcmp(a, c, al < cl ? al : cl);
+    return r ? r : (al < cl ? -1 : (al > cl ? 1 : 0));
+}
+inline int rec_vs(const uint8_t* b, uint64_t p, const std::string& c) {
+    return host_key_cmp(b + p + 5, be32(b + p + 1), (const uint8_t*)c.data(), c.size());
+}
+}  // namespace
+
+static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** out, double t_entry, bool& used) {
+    used = false;
+    const char* pe = getenv("SKV_HOST_PIPE");
+    if (pe && pe[0] == '0') return SKV_OK;
+    const char* me = getenv("SKV_HOST_PIPE_MIN");
+    const uint64_t min_bytes = me ? strtoull(me, nullptr, 10) : (512ull << 20);
+    const uint32_t k = (uint32_t)job.ranked.size();
+    if (job.in_bytes < min_bytes || (job.flags & SKV_SPLIT_BY_TABLE) || job.batch || job.search || job.scan) return SKV_OK;
+    if (k == 0 || job.run_ptr.size() != k) return SKV_OK;  // one run per stream
+    uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(64, job.in_bytes / (256ull << 20)));
+    if (const char* pp = getenv("SKV_HOST_PARTS")) P = std::max<uint64_t>(1, std::min<uint64_t>(256, strtoull(pp, nullptr, 10)));
+    // the open run is carried into every part: keep it small against a part
+    if (P < 2 || job.max_run_size > job.in_bytes / (4 * P)) return SKV_OK;
+    // ---- framing walk of every run (blocks of runs on host threads)
+    std::vector<RunWalk> walks(k);
+    {
+        const unsigned nb = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+        std::vector<uint8_t> ok(nb, 1);
+        par_run(k, std::min<uint64_t>(nb, k), [&](unsigned b, uint64_t lo, uint64_t hi) {
+            for (uint64_t m = lo; m < hi; ++m)
+                if (!host_walk((const uint8_t*)(uintptr_t)job.run_ptr[m], job.run_len[m], walks[m])) ok[b] = 0;
+        });
+        for (uint8_t o : ok)
+            if (!o) return SKV_OK;  // a broken run: the serial path reports the reference's error
+    }
+    htrace("gpipe: walked");
+    uint64_t R = 0;
+    for (const RunWalk& w : walks) R += w.n;
+    if (R < P * 64 || R >= 0xFFFFFFF0ull) return SKV_OK;
+    auto run_b = [&](uint32_t m) { return (const uint8_t*)(uintptr_t)job.run_ptr[m]; };
+    // ---- cut keys: quantiles of an even sample of every run's walk records
+    std::vector<std::pair<const uint8_t*, uint64_t>> smp;
+    const uint64_t Q = std::max<uint64_t>(4, 4096 / k);
+    for (uint32_t m = 0; m < k; ++m) {
+        const auto& at = walks[m].at;
+        for (uint64_t t = 0; t < Q && t < at.size(); ++t) {
+            const uint64_t p = at[(2 * t + 1) * at.size() / (2 * Q)];
+            smp.emplace_back(run_b(m) + p + 5, be32(run_b(m) + p + 1));
+        }
+    }
+    if (smp.size() < P) return SKV_OK;
+    std::sort(smp.begin(), smp.end(), [](const auto& a, const auto& c) {
+        return host_key_cmp(a.first, a.second, c.first, c.second) < 0;
+    });
+    std::vector<std::string> cut(P - 1);
+    for (uint64_t p = 1; p < P; ++p) {
+        const auto& e = smp[p * smp.size() / P];
+        cut[p - 1].assign((const char*)e.first, e.second);
+    }
+    // ---- bnd[p * k + m]: byte offset of run m's first record >= cut p (1 / len at the ends)
+    std::vector<uint64_t> bnd((P + 1) * k);
+    {
+        const unsigned nb = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+        std::vector<uint8_t> ok(nb, 1);
+        par_run(k, std::min<uint64_t>(nb, k), [&](unsigned b, uint64_t lo, uint64_t hi) {
+            for (uint64_t m = lo; m < hi; ++m) {
+                const uint8_t* rb = run_b((uint32_t)m);
+                const uint64_t len = job.run_len[m];
+                const auto& at = walks[m].at;
+                bnd[m] = 1;
+                bnd[P * k + m] = len;
+                for (uint64_t p = 1; p < P; ++p) {
+                    const std::string& c = cut[p - 1];
+                    uint64_t a = 0, z = at.size();  // first walk record >= c
+                    while (a < z) {
+                        const uint64_t mid = (a + z) >> 1;
+                        if (rec_vs(rb, at[mid], c) < 0) a = mid + 1;
+                        else z = mid;
+                    }
+                    uint64_t q = a ? at[a - 1] : 1;  // < c (or the run's first record)
+                    const uint64_t stop = a < at.size() ? at[a] : len;
+                    uint64_t prev = ~0ull;
+                    while (q < stop && rec_vs(rb, q, c) < 0) {
+                        prev = q;
+                        q += host_rec_size(rb, q);
+                    }
+                    // the record before the cut (prev, the walk's last < c; none when the cut is at
+                    // the run's first record) sorts below it; a run whose walk records decrease
+                    // across cuts is the serial path's (the device checks order inside each slice)
+                    (void)prev;
+                    bnd[p * k + m] = q;
+                    if (q < bnd[(p - 1) * k + m]) ok[b] = 0;
+                }
+            }
+        });
+        for (uint8_t o : ok)
+            if (!o) return SKV_OK;
+    }
+    htrace("gpipe: cuts");
+    used = true;
+    struct KernelIO {  // table uploads and readbacks by copy kernels, not DMA behind the bulk copies
+        skv_ctx* c;
+        explicit KernelIO(skv_ctx* x) : c(x) { c->kernel_uploads = true; }
+        ~KernelIO() { c->kernel_uploads = false; }
+    } kio(ctx);
+    if (!ctx->in_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->in_stream, hipStreamNonBlocking));
+    if (!ctx->out_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->out_stream, hipStreamNonBlocking));
+    while (ctx->part_ev.size() < 2 * P) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->part_ev.push_back(e);
+    }
+    // ---- device images of the runs; the shared output
+    std::vector<uint64_t> img(k + 1, 0);
+    for (uint32_t m = 0; m < k; ++m) img[m + 1] = img[m] + ((job.run_len[m] + 15) & ~15ull);
+    uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", img[k] + 16);
+    const uint64_t out_cap = job.in_bytes + R + 64;
+    uint8_t* d_out = dbuf<uint8_t>(ctx, "gp_out", out_cap);
+    size_t cap = 0;
+    uint8_t* h_out = (uint8_t*)ctx->out_pool->take(out_cap, cap);
+    if (!h_out) throw DevError("pinned host allocation of the output failed");
+    struct OutGuard {  // as in compact_host_pipelined: drain the copies, then the buffer back
+        skv_ctx* c;
+        uint8_t*& buf;
+        size_t cap;
+        ~OutGuard() {
+            if (c->in_stream) (void)hipStreamSynchronize(c->in_stream);
+            if (c->out_stream) (void)hipStreamSynchronize(c->out_stream);
+            (void)hipStreamSynchronize(c->stream);
+            if (buf) c->out_pool->give(buf, cap);
+        }
+    } out_guard{ctx, h_out, cap};
+    // ---- ingest: every part's slices, in part order, on in_stream
+    for (uint64_t p = 0; p < P; ++p) {
+        for (uint32_t m = 0; m < k; ++m) {
+            const uint64_t lo = p == 0 ? 0 : bnd[p * k + m], hi = bnd[(p + 1) * k + m];
+            if (hi > lo)
+                HIPCHK(hipMemcpyAsync(d_in + img[m] + lo, run_b(m) + lo, hi - lo, hipMemcpyHostToDevice, ctx->in_stream));
+        }
+        HIPCHK(hipEventRecord(ctx->part_ev[2 * p], ctx->in_stream));
+    }
+    htrace("gpipe: ingest queued");
+    // ---- egress thread: D2H of every byte range the parts finalize
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t final_end = 0;
+    bool stop = false, done = false;
+    std::string d2h_err;
+    std::thread egress([&] {
+        try {
+            if (hipSetDevice(ctx->device) != hipSuccess) throw DevError("hipSetDevice failed (egress)");
+            uint64_t E = 0;
+            for (;;) {
+                uint64_t F;
+                bool last;
+                {
+                    std::unique_lock<std::mutex> g(mu);
+                    cv.wait(g, [&] { return final_end > E || done || stop; });
+                    if (stop) break;
+                    F = final_end;
+                    last = done;
+                }
+                if (F > E) HIPCHK(hipMemcpyAsync(h_out + E, d_out + E, F - E, hipMemcpyDeviceToHost, ctx->out_stream));
+                E = F;
+                if (last && E == F) break;
+            }
+            HIPCHK(hipStreamSynchronize(ctx->out_stream));
+        } catch (const DevError& e) {
+            d2h_err = e.msg;
+        } catch (const std::exception& e) {
+            d2h_err = e.what();
+        }
+    });
+    struct Join {
+        std::thread& t;
+        std::mutex& mu;
+        std::condition_variable& cv;
+        bool& stop;
+        ~Join() {
+            {
+                std::lock_guard<std::mutex> g(mu);
+                stop = true;
+            }
+            cv.notify_all();
+            if (t.joinable()) t.join();
+        }
+    } joiner{egress, mu, cv, stop};
+    // ---- the parts, in key order, on ctx->stream
+    int64_t seq_extra = INT64_MIN;  // the open run's stream: any SeqNo unused by the job
+    {
+        std::vector<int64_t> seqs;
+        for (const InStream& S : job.ranked) seqs.push_back(S.seq);
+        std::sort(seqs.begin(), seqs.end());
+        while (std::binary_search(seqs.begin(), seqs.end(), seq_extra)) ++seq_extra;
+    }
+    std::vector<skv_run_desc> descs;
+    uint64_t open_off = 0, open_len = 0, out_records = 0;
+    uint64_t syncs = 0;
+    for (uint64_t p = 0; p < P; ++p) {
+        std::vector<const uint8_t*> ptrs;
+        std::vector<uint64_t> lens;
+        std::vector<int64_t> seqv;
+        ptrs.reserve(k + 1);
+        for (uint32_t s = 0; s < k; ++s) {
+            const uint32_t m = (uint32_t)job.ranked[s].first;
+            const uint64_t lo = bnd[p * k + m], hi = bnd[(p + 1) * k + m];
+            ptrs.push_back(d_in + img[m] + lo - 1);  // the byte before the slice: its "version byte"
+            lens.push_back(1 + hi - lo);
+            seqv.push_back(job.ranked[s].seq);
+        }
+        if (open_len) {
+            ptrs.push_back(d_out + open_off);
+            lens.push_back(open_len);
+            seqv.push_back(seq_extra);
+        }
+        std::vector<skv_stream> sv(ptrs.size());
+        for (size_t i = 0; i < sv.size(); ++i) sv[i] = skv_stream{&ptrs[i], &lens[i], 1u, seqv[i]};
+        Job pj;
+        if (build_job(ctx, sv.data(), (uint32_t)sv.size(), job.max_run_size, job.flags, pj) != SKV_OK)
+            throw DevError("internal: part job: " + ctx->err);
+        pj.part = true;
+        pj.dev_out = d_out + open_off;
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->part_ev[2 * p], 0));
+        skv_result* pres = nullptr;
+        int rc;
+        try {
+            rc = compact_device(ctx, pj, &pres, true);
+        } catch (const ApiError&) {
+            rc = -1;  // a data error: the serial path reports it exactly
+        }
+        syncs += ctx->syncs;
+        if (rc != SKV_OK) {
+            drain(ctx);
+            used = false;
+            return SKV_OK;
+        }
+        const uint64_t n = pres->n_runs;
+        const bool last_part = p + 1 == P;
+        for (uint64_t r = 0; r < n; ++r) {
+            skv_run_desc d = pres->runs[r];
+            d.off += open_off;
+            d.min_key_off += open_off;
+            d.max_key_off += open_off;
+            if (!last_part && r + 1 == n) {  // still open: carried into the next part
+                open_off = d.off;
+                open_len = d.len;
+                break;
+            }
+            descs.push_back(d);
+            out_records += d.put_count + d.delete_count;
+        }
+        if (!n) open_len = 0;  // (nothing so far: no open run)
+        skv_result_free(pres);
+        {
+            std::lock_guard<std::mutex> g(mu);
+            final_end = last_part ? (descs.empty() ? 0 : descs.back().off + descs.back().len) : open_off;
+            done = last_part;
+        }
+        cv.notify_all();
+        htrace("gpipe: part done");
+    }
+    egress.join();
+    if (!d2h_err.empty()) throw DevError("pipelined egress: " + d2h_err);
+    ResultBox* box = new ResultBox();
+    skv_result* res = &box->pub;
+    res->runs = (skv_run_desc*)malloc(std::max<size_t>(1, descs.size()) * sizeof(skv_run_desc));
+    if (!descs.empty()) memcpy(res->runs, descs.data(), descs.size() * sizeof(skv_run_desc));
+    res->n_runs = descs.size();
+    res->bytes = h_out;
+    h_out = nullptr;  // the result owns it now
+    res->n_bytes = descs.empty() ? 0 : descs.back().off + descs.back().len;
+    res->in_bytes = job.in_bytes;
+    res->in_records = R;
+    res->out_records = out_records;
+    res->dropped_tables = 0;
+    box->pool = ctx->out_pool;
+    box->pool_cap = cap;
+    skv_timings& t = ctx->timings;
+    t = skv_timings{};
+    t.path = SKV_PATH_GENERAL;
+    t.host_syncs = syncs;
+    t.host_total_ms = now_ms() - t_entry;
+    t.host_parts = (uint32_t)P;
+    *out = res;
+    return SKV_OK;
+}
+
 // host inputs: stage them into HBM, compact, return the output bytes in pinned host memory
 int compact_host_job(skv_ctx* ctx, Job& job, skv_result** out, double t_entry) {
     int rc;
@@ -403,6 +744,7 @@ int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uin
         try {
             ctx->timings = skv_timings{};
             rc = compact_host_pipelined(ctx, job, out, t_entry, used);
+            if (!used) rc = compact_host_pipelined_general(ctx, job, out, t_entry, used);
         } catch (const DevError& e) {
             (void)hipStreamSynchronize(ctx->stream);
             rc = set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());

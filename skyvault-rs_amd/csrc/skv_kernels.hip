@@ -86,7 +86,9 @@ __device__ __forceinline__ uint32_t find_run(const RunInfo* runs, uint32_t n_run
 // a Put of size S and the body is a whole number of S-byte records, every chunk can verify its
 // records at their predicted positions with independent loads (k_spec), and the records can be
 // emitted one thread per record (k_emit_fixed). The hypothesis is verified record by record.
-__global__ void k_run_header(const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err, RunFmt* fmt) {
+// slices: key-range slices of runs (pipelined host calls): the byte before a slice's first record
+// stands in for the version byte and is not checked (the host walked the run's framing)
+__global__ void k_run_header(const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err, RunFmt* fmt, bool slices) {
     uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_runs) return;
     RunInfo R = runs[r];
@@ -95,7 +97,7 @@ __global__ void k_run_header(const RunInfo* runs, uint32_t n_runs, uint32_t* hdr
     const uint8_t* run = (const uint8_t*)R.ptr;
     if (R.len == 0) e = DERR_EMPTY;
     else {
-        uint32_t v = run[0];
+        uint32_t v = slices ? 1u : run[0];
         if (v != 1) e = DERR_VERSION | (v << 8);
         else if (R.len >= 2) {
             RecHdr h = parse_rec<false>(run, R.len, 1);
@@ -2500,8 +2502,8 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(const uint64_t* in,
 
 static inline unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
-void launch_run_header(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err, RunFmt* fmt) {
-    if (n_runs) k_run_header<<<blocks_for(n_runs, 256), 256, 0, s>>>(runs, n_runs, hdr_err, fmt);
+void launch_run_header(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err, RunFmt* fmt, bool slices) {
+    if (n_runs) k_run_header<<<blocks_for(n_runs, 256), 256, 0, s>>>(runs, n_runs, hdr_err, fmt, slices);
 }
 void launch_spec(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                  const RunFmt* fmt, uint32_t* run_broken, uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt,

@@ -3,7 +3,8 @@
 #include "skv_dev.hpp"
 
 namespace skv {
-void launch_run_header(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err, RunFmt* fmt);
+void launch_run_header(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err, RunFmt* fmt,
+                       bool slices = false);
 void launch_spec(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                  const RunFmt* fmt, uint32_t* run_broken, uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt,
                  uint32_t* ch_err, bool utf8, uint64_t chunk, uint16_t* slots, uint32_t cap);
@@ -137,9 +138,11 @@ void launch_search_scan(hipStream_t, const uint8_t* run, uint64_t len, const uin
 uint64_t scan_tmp_words(uint64_t n);
 void launch_scan(hipStream_t, const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tmp);
 // skv_scan.hip: ScanFromRun after the merge
-void launch_scan_last_kept(hipStream_t, uint64_t R, const uint64_t* stream_base, uint32_t k, const uint64_t* rec_addr,
-                           const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,
-                           const uint8_t* start, uint32_t slen, unsigned long long* last_kept);
+void launch_scan_filter(hipStream_t, uint64_t R, uint32_t k, const uint64_t* stream_base, const uint64_t* a_addr,
+                        const uint64_t* a_hi, const uint64_t* a_lo, const uint32_t* a_klen, const uint32_t* a_meta,
+                        const uint8_t* start, uint32_t slen, uint64_t* keep, uint64_t* keepx, uint64_t* scan_tmp,
+                        uint64_t* b_addr, uint64_t* b_hi, uint64_t* b_lo, uint32_t* b_klen, uint32_t* b_meta,
+                        uint64_t* new_base);
 void launch_scan_mark(hipStream_t, const uint64_t* d_K, uint64_t R, const uint32_t* m_rec, const uint64_t* rec_addr,
                       const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen, const uint32_t* rec_meta,
                       const uint8_t* start, uint32_t slen, uint64_t* keep, uint64_t* put, uint64_t* size);

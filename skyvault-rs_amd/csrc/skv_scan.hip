@@ -3,15 +3,13 @@
 // The compaction's parse and merge (k_way::merge order, first record per key; heap-order mode when a
 // run is unsorted or undecodable) run unchanged over the scan's runs (run i at SeqNo
 // i64::MAX - i); these kernels then apply what the service does to the merged stream:
-//   - the per-run filter try_filter(op.key() > exclusive_start_key) (:125-129). A key filter
-//     commutes with the merge: all records of one key are kept or dropped together, and in heap
-//     order a kept record's running-maximum key is unchanged by dropped records (all smaller), so
-//     filtering the merged survivors equals merging the filtered runs;
+//   - the per-run filter try_filter(op.key() > exclusive_start_key) (:125-129), on the record
+//     arrays before the merge (k_scan_keep / k_scan_compact);
 //   - the reader's cut-off: items up to and including the max_results-th Put (:140-148);
 //   - the response: the kept items, in order, as ONE v1 run (an item's record bytes are the
 //     response item: Put key + value or Delete key), version byte first.
-// k_scan_last_kept finds, per run, its last record above the start key (a decode error of that run
-// surfaces right after that record's pop; with none, at the merge's first pulls).
+// A run's decode error surfaces right after the pop of its last record above the start key; with
+// none, at the merge's first pulls (the host resolves both from the filtered stream bases).
 #include "skv_launch.hpp"
 
 namespace skv {
@@ -23,22 +21,41 @@ __device__ __forceinline__ bool scan_above(uint64_t hi, uint64_t lo, uint32_t kl
     return key_cmp(hi, lo, klen, (const uint8_t*)addr + 5, sh, sl, slen, start) > 0;
 }
 
-__global__ void k_scan_last_kept(uint64_t R, const uint64_t* __restrict__ stream_base, uint32_t k,
-                                 const uint64_t* __restrict__ rec_addr, const uint64_t* __restrict__ rec_hi,
-                                 const uint64_t* __restrict__ rec_lo, const uint32_t* __restrict__ rec_klen,
-                                 const uint8_t* __restrict__ start, uint32_t slen, unsigned long long* last_kept) {
+// The per-run filter before the merge (cache_service.rs:125-129): records at or below the start key
+// leave the record arrays, so the merge -- and its first-per-key, which compares consecutive pops
+// (k_way.rs:146-151) -- sees exactly the filtered runs. (Filtering after the merge is not the same
+// in heap order: an unsorted run's dropped record can pop between two kept records of one key.)
+__global__ void k_scan_keep(uint64_t R, const uint64_t* __restrict__ rec_addr, const uint64_t* __restrict__ rec_hi,
+                            const uint64_t* __restrict__ rec_lo, const uint32_t* __restrict__ rec_klen,
+                            const uint8_t* __restrict__ start, uint32_t slen, uint64_t* keep) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R) return;
     uint64_t sh, sl;
     key_prefix(start, slen, sh, sl);
-    if (!scan_above(rec_hi[r], rec_lo[r], rec_klen[r], rec_addr[r], sh, sl, slen, start)) return;
-    uint32_t lo = 0, hi = k;  // stream s: stream_base[s] <= r < stream_base[s + 1]
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (stream_base[mid] <= r) lo = mid;
-        else hi = mid;
-    }
-    atomicMax(last_kept + lo, (unsigned long long)(r + 1));  // 0: no record of the run passes
+    keep[r] = scan_above(rec_hi[r], rec_lo[r], rec_klen[r], rec_addr[r], sh, sl, slen, start) ? 1 : 0;
+}
+
+// kept records to their filtered positions (keepx: exclusive scan of keep)
+__global__ void k_scan_compact(uint64_t R, const uint64_t* __restrict__ keep, const uint64_t* __restrict__ keepx,
+                               const uint64_t* __restrict__ a_addr, const uint64_t* __restrict__ a_hi,
+                               const uint64_t* __restrict__ a_lo, const uint32_t* __restrict__ a_klen,
+                               const uint32_t* __restrict__ a_meta, uint64_t* b_addr, uint64_t* b_hi, uint64_t* b_lo,
+                               uint32_t* b_klen, uint32_t* b_meta) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= R || !keep[r]) return;
+    const uint64_t d = keepx[r];
+    b_addr[d] = a_addr[r];
+    b_hi[d] = a_hi[r];
+    b_lo[d] = a_lo[r];
+    b_klen[d] = a_klen[r];
+    b_meta[d] = a_meta[r];
+}
+
+// filtered stream bases: nb[s] = kept records before stream s's first record (s = 0..k)
+__global__ void k_scan_bases(uint32_t k, const uint64_t* __restrict__ base, const uint64_t* __restrict__ keepx,
+                             uint64_t* nb) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s <= k) nb[s] = keepx[base[s]];
 }
 
 // per merged survivor g < K: kept (key above the start), kept Put, kept bytes
@@ -109,11 +126,17 @@ __global__ void k_scan_gather(const uint64_t* __restrict__ info, const uint64_t*
     }
 }
 
-void launch_scan_last_kept(hipStream_t s, uint64_t R, const uint64_t* stream_base, uint32_t k, const uint64_t* rec_addr,
-                           const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,
-                           const uint8_t* start, uint32_t slen, unsigned long long* last_kept) {
-    if (R) k_scan_last_kept<<<(unsigned)((R + 255) / 256), 256, 0, s>>>(R, stream_base, k, rec_addr, rec_hi, rec_lo,
-                                                                       rec_klen, start, slen, last_kept);
+void launch_scan_filter(hipStream_t s, uint64_t R, uint32_t k, const uint64_t* stream_base, const uint64_t* a_addr,
+                        const uint64_t* a_hi, const uint64_t* a_lo, const uint32_t* a_klen, const uint32_t* a_meta,
+                        const uint8_t* start, uint32_t slen, uint64_t* keep, uint64_t* keepx, uint64_t* scan_tmp,
+                        uint64_t* b_addr, uint64_t* b_hi, uint64_t* b_lo, uint32_t* b_klen, uint32_t* b_meta,
+                        uint64_t* new_base) {
+    const unsigned nb = (unsigned)((R + 255) / 256);
+    if (R) k_scan_keep<<<nb, 256, 0, s>>>(R, a_addr, a_hi, a_lo, a_klen, start, slen, keep);
+    launch_scan(s, keep, R, keepx, scan_tmp);  // keepx[R] = kept records
+    if (R) k_scan_compact<<<nb, 256, 0, s>>>(R, keep, keepx, a_addr, a_hi, a_lo, a_klen, a_meta, b_addr, b_hi, b_lo,
+                                             b_klen, b_meta);
+    k_scan_bases<<<(k + 256) / 256, 256, 0, s>>>(k, stream_base, keepx, new_base);
 }
 void launch_scan_mark(hipStream_t s, const uint64_t* d_K, uint64_t R, const uint32_t* m_rec, const uint64_t* rec_addr,
                       const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen, const uint32_t* rec_meta,

@@ -1,8 +1,10 @@
-"""The pipelined host path (skv_compact with host inputs, skv_host.hip compact_host_pipelined):
-key-range parts whose H2D, fused kernels and D2H overlap on three streams. Its outputs must be
-the oracle's, byte for byte, whatever the cut keys (parts 2..17, equal keys across streams at the
-cuts, empty parts), and a call the device poisons (a key decrease inside a part) or the host
-rejects (a decrease across a cut) must end with the oracle's error through the serial path.
+"""The pipelined host paths (skv_compact with host inputs, skv_hostpipe.hip): key-range parts whose
+H2D, kernels and D2H overlap on three streams -- the fused pipeline (compact_host_pipelined: one
+record size, keys <= 16 B) and the general one (compact_host_pipelined_general: variable-length
+records and Deletes, the open output run carried into the next part). Outputs must be the
+oracle's, byte for byte, whatever the cut keys (parts 2..17, equal keys across streams at the
+cuts, empty parts), and a call the device poisons or rejects (a key decrease inside a part or
+across a cut, a corrupt run) must end with the oracle's outcome through the serial path.
 
 SKV_HOST_PIPE_MIN=0 lets small inputs take the pipeline; SKV_HOST_PARTS fixes the part count.
 `timings()["host_parts"]` says whether the call was pipelined (0: serial).
@@ -128,14 +130,107 @@ def test_decrease_falls_back_to_the_serial_path_with_the_oracles_error(dev, pipe
 
 
 def test_not_eligible_inputs_stay_serial(dev, pipe_env):
-    """variable record sizes: the host sees no fixed stride and never pipelines"""
+    """the WAL split and L0-style multi-run streams never pipeline"""
     rng = random.Random(5)
     streams = []
     for s in range(4):
         keys = sorted(rng.sample(range(9000), 1500))
-        streams.append((s + 1, [fmt.encode_run([fmt.put(f"k{i:06d}", b"v" * (1 + i % 7)) for i in keys])]))
-    _check(dev, streams, 4 * MiB, 0, 4, expect_pipe=False)
+        streams.append((s + 1, [fmt.encode_run([fmt.put(f"{s % 3}.k{i:06d}", b"v" * (1 + i % 7)) for i in keys])]))
+    _check(dev, streams, 1000, _abi.SKV_SPLIT_BY_TABLE, 4, expect_pipe=False)
     assert dev.timings()["host_parts"] == 0
+    l0 = [(1, [streams[0][1][0], streams[1][1][0]])] + streams[2:]
+    _check(dev, l0, 1000, 0, 4, expect_pipe=False)
+    assert dev.timings()["host_parts"] == 0
+
+
+# ---- the general key-range pipeline (variable-length records, Deletes) ------------------------
+
+def _var_streams(rng, k, n, space, del_frac=0.1, same=False, vmax=60):
+    base = sorted(rng.sample(range(space), n)) if same else None
+    out = []
+    for s in range(k):
+        ids = base if same else sorted(rng.sample(range(space), n))
+        ops = []
+        for i in ids:
+            key = f"k{i:07d}" + "abcdefghij" * (i % 7)  # 8..78-byte keys
+            if rng.random() < del_frac:
+                ops.append(fmt.delete(key))
+            else:
+                ops.append(fmt.put(key, bytes([(s * 7 + i) & 0xFF]) * rng.randint(0, vmax)))
+        out.append((s + 1, [fmt.encode_run(ops)]))
+    return out
+
+
+@pytest.mark.parametrize("parts", [2, 3, 7, 17])
+@pytest.mark.parametrize("max_size", [1000, 4096, 20000])
+def test_general_pipeline_matches_oracle(dev, pipe_env, parts, max_size):
+    rng = random.Random(parts * 31 + max_size)
+    streams = _var_streams(rng, 9, 2500, 15000)
+    _check(dev, streams, max_size, 0, parts)
+
+
+@pytest.mark.parametrize("parts", [2, 5, 16])
+def test_general_pipeline_drop_tombstones(dev, pipe_env, parts):
+    rng = random.Random(70 + parts)
+    streams = _var_streams(rng, 7, 3000, 9000, del_frac=0.3)
+    _check(dev, streams, 4096, _abi.SKV_DROP_TOMBSTONES, parts)
+
+
+@pytest.mark.parametrize("parts", [2, 9])
+def test_general_pipeline_equal_keys_at_every_cut(dev, pipe_env, parts):
+    rng = random.Random(90 + parts)
+    _check(dev, _var_streams(rng, 12, 1500, 4000, same=True), 2048, 0, parts)
+
+
+def test_general_pipeline_one_record_runs_and_large_records(dev, pipe_env):
+    """records larger than max (each its own run) and max sizes just above one record"""
+    rng = random.Random(17)
+    streams = []
+    for s in range(5):
+        ids = sorted(rng.sample(range(3000), 400))
+        streams.append((s + 1, [fmt.encode_run([fmt.put(f"r{i:06d}", bytes([s]) * rng.choice([10, 900, 3000]))
+                                                for i in ids])]))
+    for mx in (1, 900, 2500, 8000):
+        _check(dev, streams, mx, 0, 6)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_general_decrease_inside_or_across_parts_gives_the_oracles_error(dev, pipe_env, seed):
+    """a key decrease anywhere (inside a part, or across a cut) ends on the serial path with the
+    oracle's outcome"""
+    rng = random.Random(300 + seed)
+    streams = _var_streams(rng, 5, 2000, 8000, del_frac=0.0)
+    s = rng.randrange(5)
+    ids = sorted(rng.sample(range(8000), 2000))
+    i = rng.randrange(1, 2000)
+    ids[i - 1], ids[i] = ids[i], ids[i - 1]
+    streams[s] = (streams[s][0], [fmt.encode_run([fmt.put(f"k{x:07d}", b"d") for x in ids])])
+    os.environ["SKV_HOST_PARTS"] = str(rng.choice([2, 4, 8]))
+    exp, got = _run_both(dev, streams, 4096, 0)
+    assert exp == got and exp[0] == "err", _diff(exp, got)
+
+
+def test_general_corrupt_run_gives_the_oracles_error(dev, pipe_env):
+    rng = random.Random(41)
+    streams = _var_streams(rng, 4, 1500, 6000)
+    bad = bytearray(streams[2][1][0])
+    bad[len(bad) // 2] = 0x07  # likely inside a value or a length: some decode error or a changed record
+    streams[2] = (streams[2][0], [bytes(bad)])
+    truncated = streams[1][1][0][:-3]
+    streams[1] = (streams[1][0], [truncated])
+    os.environ["SKV_HOST_PARTS"] = "5"
+    exp, got = _run_both(dev, streams, 4096, 0)
+    assert exp == got, _diff(exp, got)
+    assert dev.timings()["host_parts"] == 0
+
+
+def test_general_pipeline_failure_leaves_the_ctx_clean(dev, pipe_env):
+    rng = random.Random(43)
+    streams = _var_streams(rng, 6, 2000, 9000)
+    os.environ["SKV_HOST_PARTS"] = "5"
+    _check(dev, streams, 4096, 0, 5)
+    for _ in range(2):
+        _check(dev, streams, 4096, 0, 5)
 
 
 def test_config2_shape_large(dev, pipe_env):
