@@ -220,7 +220,7 @@ struct FxArgs {
     uint32_t* tcounter;           // tile ticket (zeroed per call)
     uint64_t* Kout;               // surviving records (through this launch's records)
     const uint64_t* gbase;        // survivors before this launch's records (a key-range part of a
-                                  // pipelined host call, skv_host.hip), or null: 0
+                                  // pipelined host call, skv_hostpipe.hip), or null: 0
     uint64_t* prof;               // SKV_TILE_PROF builds: per-phase ticks of the fused tiles (16 counters)
     // k_fx_bounds' inputs: the sorted level-1 samples (every m-th is a splitter) and each stream's
     // own level-1 samples (every Sstep-th record, offsets l1off)

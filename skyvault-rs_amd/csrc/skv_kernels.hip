@@ -1,6 +1,6 @@
 // skv_kernels.hip — HIP/CDNA4 (gfx950) kernels of the skyvault compaction path.
 //
-// Pipeline (one compaction; host orchestration in skv_host.hip):
+// Pipeline (one compaction; host orchestration in skv_compact.hip):
 //   parse   k_run_header, k_spec, k_validate, k_fixup, k_err_chunk, k_mask, scan, k_run_summary,
 //           k_emit           — runs::read_run_stream (runs.rs:517-628) for every input run at once
 //   check   k_order_check    — first in-stream key decrease (what build_runs rejects, runs.rs:190-198)
@@ -2498,7 +2498,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(const uint64_t* in,
 }
 
 // ---------------------------------------------------------------------------------------
-// launch wrappers (C++ linkage, used by skv_host.hip)
+// launch wrappers (C++ linkage, used by the host files skv_*host*.hip / skv_compact.hip)
 
 static inline unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 

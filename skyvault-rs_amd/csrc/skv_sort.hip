@@ -20,7 +20,7 @@
 //      tie); buckets above SORT_CAP sort in global memory (same order, slower)
 // The sorted records then form ONE stream, and the level-0 merge machinery runs on them with
 // k = 1 on dense key ranks (one per distinct key, flagged by the bucket sort): first record per
-// key, Delete filter, dense output arrays (skv_host.hip).
+// key, Delete filter, dense output arrays (skv_compact.hip).
 #include "skv_launch.hpp"
 
 namespace skv {

@@ -317,7 +317,7 @@ def test_corruption_at_every_position_class(dev):
 
 @pytest.mark.parametrize("chunk", [8192, 12288, 16384])
 def test_longer_speculative_walks(dev, chunk):
-    """Big calls walk 8-16 KiB per speculative chunk (skv_host.hip picks the length from the call
+    """Big calls walk 8-16 KiB per speculative chunk (skv_compact.hip picks the length from the call
     size); SKV_CHUNK_BYTES forces a length on small inputs: fake records in values, records
     spanning chunks, and corruption everywhere must still give the reference's outcome."""
     old = os.environ.get("SKV_CHUNK_BYTES")
