@@ -618,6 +618,10 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
         pj.part = true;
         pj.dev_out = d_out + open_off;
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->part_ev[2 * p], 0));
+        if (getenv("SKV_HOST_TRACE")) {  // diagnostics: when part p's slices have landed
+            HIPCHK(hipEventSynchronize(ctx->part_ev[2 * p]));
+            htrace("gpipe: part ingested");
+        }
         skv_result* pres = nullptr;
         int rc;
         try {

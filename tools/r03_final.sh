@@ -27,6 +27,8 @@ for C in $CS; do
       || { echo "prof $C failed"; exit 1; }
     cd "$R"
     python3 tools/kstats_skv.py "$(ls $O/prof_$C/*kernel_stats.csv | head -1)" 5 "$O/kernel_stats_$C.csv" > /dev/null
+    cp "$(ls $O/prof_$C/*kernel_stats.csv | head -1)" "$O/rocprof_stats_$C.csv"
+    rm -rf "$O/prof_$C"  # the raw traces exceed what a call may copy back (64 MiB)
     echo "prof $C done"
   fi
   if [[ " $S " == *" pmc "* ]]; then
@@ -40,6 +42,7 @@ for C in $CS; do
       cd "$R"
     done
     python3 tools/traffic.py "$O/pmc_$C" "$C" "$O/traffic.json" | head -6
+    rm -rf "$O/pmc_$C"
     echo "pmc $C done"
   fi
 done

@@ -45,8 +45,9 @@ if out:
         doc = {}
     doc["source"] = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, last dispatch per kernel"
     doc["correction"] = "FETCH_SIZE x2 (gfx950 wide streaming reads), WRITE_SIZE x1; KiB -> bytes"
-    doc.setdefault("configs", {})[config] = {"pmc_files": [os.path.relpath(f, root) for f in files],
-                                             "kernels": kernels}
+    doc.setdefault("configs", {})[config] = {
+        "pmc_passes": "bench.py --config %s --steps 1 --warmup 1: rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE" % config,
+        "kernels": kernels}
     with open(out, "w") as f:
         json.dump(doc, f, indent=1, sort_keys=True)
     print("wrote", out, "config", config)
