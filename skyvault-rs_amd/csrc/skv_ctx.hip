@@ -17,7 +17,8 @@ int set_err(skv_ctx* ctx, int code, const char* fmt, ...) {
 
 void* pinned(skv_ctx* ctx, size_t bytes) {
     if (ctx->pinned_cap < bytes) {
-        if (ctx->pinned) HIPCHK(hipHostFree(ctx->pinned));
+        if (ctx->pinned && ctx->defer_free) ctx->host_graveyard.push_back(ctx->pinned);  // see dbuf
+        else if (ctx->pinned) HIPCHK(hipHostFree(ctx->pinned));
         ctx->pinned = nullptr;
         size_t cap = std::max<size_t>(bytes, 1 << 16);
         HIPCHK(hipHostMalloc(&ctx->pinned, cap, hipHostMallocDefault));

@@ -122,6 +122,11 @@ struct skv_ctx {
     std::vector<hipEvent_t> part_ev;
     uint64_t* part_k = nullptr;
     size_t part_k_cap = 0;
+    // while a pipelined host call has copies queued on in_stream / out_stream, a buffer that grows
+    // keeps its old allocation here until the call has drained (hipFree waits for the whole device,
+    // which would serialise the pipeline behind every queued copy)
+    bool defer_free = false;
+    std::vector<void*> graveyard, host_graveyard;
 };
 
 struct ResultBox {  // skv_result + how to free it
@@ -155,7 +160,9 @@ inline T* dbuf(skv_ctx* ctx, const char* name, size_t count) {
     bytes = (bytes + 255) & ~(size_t)255;
     DevBuf& b = ctx->bufs[name];
     if (b.cap < bytes) {
-        if (b.p) {  // queued work of this call (pipelined parts) may still use the old buffer
+        if (b.p && ctx->defer_free) {
+            ctx->graveyard.push_back(b.p);  // queued work may still use it: freed after the call
+        } else if (b.p) {  // queued work of this call (pipelined parts) may still use the old buffer
             HIPCHK(hipStreamSynchronize(ctx->stream));
             HIPCHK(hipFree(b.p));
         }

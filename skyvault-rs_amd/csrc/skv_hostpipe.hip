@@ -495,10 +495,26 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     }
     htrace("gpipe: cuts");
     used = true;
-    struct KernelIO {  // table uploads and readbacks by copy kernels, not DMA behind the bulk copies
+    struct KernelIO {  // table uploads and readbacks by copy kernels, not DMA behind the bulk copies;
+                       // buffers that grow keep their old allocation until the streams have drained
         skv_ctx* c;
-        explicit KernelIO(skv_ctx* x) : c(x) { c->kernel_uploads = true; }
-        ~KernelIO() { c->kernel_uploads = false; }
+        explicit KernelIO(skv_ctx* x) : c(x) {
+            c->kernel_uploads = true;
+            c->defer_free = true;
+        }
+        ~KernelIO() {
+            c->kernel_uploads = false;
+            c->defer_free = false;
+            if (!c->graveyard.empty() || !c->host_graveyard.empty()) {
+                if (c->in_stream) (void)hipStreamSynchronize(c->in_stream);
+                if (c->out_stream) (void)hipStreamSynchronize(c->out_stream);
+                (void)hipStreamSynchronize(c->stream);
+                for (void* q : c->graveyard) (void)hipFree(q);
+                for (void* q : c->host_graveyard) (void)hipHostFree(q);
+                c->graveyard.clear();
+                c->host_graveyard.clear();
+            }
+        }
     } kio(ctx);
     if (!ctx->in_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->in_stream, hipStreamNonBlocking));
     if (!ctx->out_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->out_stream, hipStreamNonBlocking));
