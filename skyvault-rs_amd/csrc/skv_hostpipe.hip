@@ -356,44 +356,18 @@ static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, doub
 // error, decrease across a cut or oversized open run ends the attempt; the serial path then gives
 // the reference's exact outcome.
 namespace {
-struct RunWalk {
-    std::vector<uint64_t> at;  // byte offset of records 0, G, 2G, ...
-    uint64_t n = 0;            // records
-    bool ok = true;
-};
-constexpr uint32_t WALK_G = 64;
-
-// the reference's framing checks (runs.rs:559-624) without the key's UTF-8 (the device does those)
-bool host_walk(const uint8_t* b, uint64_t len, RunWalk& w) {
-    if (len == 0 || b[0] != 1) return false;
-    uint64_t p = 1, n = 0;
-    w.at.clear();
-    while (p < len) {
-        const uint8_t marker = b[p];
-        if (p + 5 > len) return false;
-        const uint64_t klen = be32(b + p + 1), kp = p + 5;
-        if (kp + klen > len) return false;
-        uint64_t size;
-        if (marker == 1) {
-            if (kp + klen + 4 > len) return false;
-            const uint64_t vlen = be32(b + kp + klen);
-            if (kp + klen + 4 + vlen > len) return false;
-            size = 9 + klen + vlen;
-        } else if (marker == 2) {
-            size = 5 + klen;
-        } else {
-            return false;
-        }
-        if (n % WALK_G == 0) w.at.push_back(p);
-        ++n;
-        p += size;
-    }
-    w.n = n;
-    return true;
-}
-inline uint64_t host_rec_size(const uint8_t* b, uint64_t p) {
-    const uint64_t klen = be32(b + p + 1);
-    return b[p] == 1 ? 9 + klen + be32(b + p + 5 + klen) : 5 + klen;
+constexpr uint64_t NPOS = ~0ull;
+// the framing of one record at p (runs.rs:559-624 without the key's UTF-8, which the device checks):
+// its size, or 0 when it does not decode
+inline uint64_t host_rec_at(const uint8_t* b, uint64_t len, uint64_t p) {
+    if (p + 5 > len) return 0;
+    const uint8_t marker = b[p];
+    const uint64_t klen = be32(b + p + 1), kp = p + 5;
+    if (kp + klen > len) return 0;
+    if (marker == 2) return 5 + klen;
+    if (marker != 1 || kp + klen + 4 > len) return 0;
+    const uint64_t vlen = be32(b + kp + klen);
+    return kp + klen + 4 + vlen > len ? 0 : 9 + klen + vlen;
 }
 // Rust str Ord: bytewise, a proper prefix first
 inline int host_key_cmp(const uint8_t* a, uint64_t al, const uint8_t* c, uint64_t cl) {
@@ -402,6 +376,54 @@ inline int host_key_cmp(const uint8_t* a, uint64_t al, const uint8_t* c, uint64_
 }
 inline int rec_vs(const uint8_t* b, uint64_t p, const std::string& c) {
     return host_key_cmp(b + p + 5, be32(b + p + 1), (const uint8_t*)c.data(), c.size());
+}
+// A record start near byte x without walking the run from its start: the first p >= x from which
+// RESYNC_N records decode with strictly increasing keys (or the run ends cleanly after fewer). A
+// position that passes but is not a record start of the run's true chain is harmless: the slice
+// that ends there cannot decode (its chain from a true start never lands on it), the device reports
+// an error, and the call takes the serial path.
+constexpr int RESYNC_N = 8;
+constexpr uint64_t RESYNC_SPAN = 1u << 16;
+inline bool plausible(const uint8_t* b, uint64_t len, uint64_t p) {
+    uint64_t prev = NPOS;
+    for (int i = 0; i < RESYNC_N && p < len; ++i) {
+        const uint64_t sz = host_rec_at(b, len, p);
+        if (!sz) return false;
+        if (prev != NPOS && host_key_cmp(b + prev + 5, be32(b + prev + 1), b + p + 5, be32(b + p + 1)) >= 0) return false;
+        prev = p;
+        p += sz;
+    }
+    return true;
+}
+inline uint64_t resync(const uint8_t* b, uint64_t len, uint64_t x) {
+    const uint64_t e = std::min(len, x + RESYNC_SPAN);
+    for (uint64_t p = x; p < e; ++p)
+        if ((b[p] == 1 || b[p] == 2) && plausible(b, len, p)) return p;
+    return NPOS;
+}
+// run m's first record with key >= c: bisection over resynced positions, then a walk of a few
+// records from the last one below c. prev_ok: the record before it sorts below c.
+inline uint64_t host_lower_bound(const uint8_t* b, uint64_t len, const std::string& c) {
+    if (len <= 1) return len;
+    if (rec_vs(b, 1, c) >= 0) return 1;
+    uint64_t lo = 1, hi = len;  // lo: a record start below c; hi: at or past the bound
+    while (hi - lo > 4096) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        const uint64_t q = resync(b, len, mid);
+        if (q == NPOS || q >= hi) {
+            hi = mid;
+            continue;
+        }
+        if (rec_vs(b, q, c) < 0) lo = q;
+        else hi = q;
+    }
+    uint64_t q = lo;
+    while (q < len && rec_vs(b, q, c) < 0) {
+        const uint64_t sz = host_rec_at(b, len, q);
+        if (!sz) return NPOS;  // not decodable here: the serial path
+        q += sz;
+    }
+    return q;
 }
 }  // namespace
 
@@ -414,37 +436,33 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     const uint32_t k = (uint32_t)job.ranked.size();
     if (job.in_bytes < min_bytes || (job.flags & SKV_SPLIT_BY_TABLE) || job.batch || job.search || job.scan) return SKV_OK;
     if (k == 0 || job.run_ptr.size() != k) return SKV_OK;  // one run per stream
+    if (k > (uint32_t)TILE_TARGET / 2) return SKV_OK;       // the splitter merge's fan-in per part
     uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(64, job.in_bytes / (256ull << 20)));
     if (const char* pp = getenv("SKV_HOST_PARTS")) P = std::max<uint64_t>(1, std::min<uint64_t>(256, strtoull(pp, nullptr, 10)));
     // the open run is carried into every part: keep it small against a part
     if (P < 2 || job.max_run_size > job.in_bytes / (4 * P)) return SKV_OK;
-    // ---- framing walk of every run (blocks of runs on host threads)
-    std::vector<RunWalk> walks(k);
-    {
-        const unsigned nb = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
-        std::vector<uint8_t> ok(nb, 1);
-        par_run(k, std::min<uint64_t>(nb, k), [&](unsigned b, uint64_t lo, uint64_t hi) {
-            for (uint64_t m = lo; m < hi; ++m)
-                if (!host_walk((const uint8_t*)(uintptr_t)job.run_ptr[m], job.run_len[m], walks[m])) ok[b] = 0;
-        });
-        for (uint8_t o : ok)
-            if (!o) return SKV_OK;  // a broken run: the serial path reports the reference's error
-    }
-    htrace("gpipe: walked");
-    uint64_t R = 0;
-    for (const RunWalk& w : walks) R += w.n;
-    if (R < P * 64 || R >= 0xFFFFFFF0ull) return SKV_OK;
     auto run_b = [&](uint32_t m) { return (const uint8_t*)(uintptr_t)job.run_ptr[m]; };
-    // ---- cut keys: quantiles of an even sample of every run's walk records
+    for (uint32_t m = 0; m < k; ++m)  // a run without a version byte: the serial path's error
+        if (job.run_len[m] == 0 || run_b(m)[0] != 1) return SKV_OK;
+    // ---- cut keys: quantiles of records found at evenly spaced offsets of every run
     std::vector<std::pair<const uint8_t*, uint64_t>> smp;
     const uint64_t Q = std::max<uint64_t>(4, 4096 / k);
-    for (uint32_t m = 0; m < k; ++m) {
-        const auto& at = walks[m].at;
-        for (uint64_t t = 0; t < Q && t < at.size(); ++t) {
-            const uint64_t p = at[(2 * t + 1) * at.size() / (2 * Q)];
-            smp.emplace_back(run_b(m) + p + 5, be32(run_b(m) + p + 1));
-        }
+    {
+        std::vector<std::vector<std::pair<const uint8_t*, uint64_t>>> part_smp(k);
+        const unsigned nb = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+        par_run(k, std::min<uint64_t>(nb, k), [&](unsigned, uint64_t lo, uint64_t hi) {
+            for (uint64_t m = lo; m < hi; ++m) {
+                const uint8_t* rb = run_b((uint32_t)m);
+                const uint64_t len = job.run_len[m];
+                for (uint64_t t = 0; t < Q; ++t) {
+                    const uint64_t q = resync(rb, len, 1 + (2 * t + 1) * (len - 1) / (2 * Q));
+                    if (q != NPOS) part_smp[m].emplace_back(rb + q + 5, be32(rb + q + 1));
+                }
+            }
+        });
+        for (auto& v : part_smp) smp.insert(smp.end(), v.begin(), v.end());
     }
+    htrace("gpipe: sampled");
     if (smp.size() < P) return SKV_OK;
     std::sort(smp.begin(), smp.end(), [](const auto& a, const auto& c) {
         return host_key_cmp(a.first, a.second, c.first, c.second) < 0;
@@ -463,36 +481,19 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
             for (uint64_t m = lo; m < hi; ++m) {
                 const uint8_t* rb = run_b((uint32_t)m);
                 const uint64_t len = job.run_len[m];
-                const auto& at = walks[m].at;
                 bnd[m] = 1;
                 bnd[P * k + m] = len;
                 for (uint64_t p = 1; p < P; ++p) {
-                    const std::string& c = cut[p - 1];
-                    uint64_t a = 0, z = at.size();  // first walk record >= c
-                    while (a < z) {
-                        const uint64_t mid = (a + z) >> 1;
-                        if (rec_vs(rb, at[mid], c) < 0) a = mid + 1;
-                        else z = mid;
-                    }
-                    uint64_t q = a ? at[a - 1] : 1;  // < c (or the run's first record)
-                    const uint64_t stop = a < at.size() ? at[a] : len;
-                    uint64_t prev = ~0ull;
-                    while (q < stop && rec_vs(rb, q, c) < 0) {
-                        prev = q;
-                        q += host_rec_size(rb, q);
-                    }
-                    // the record before the cut (prev, the walk's last < c; none when the cut is at
-                    // the run's first record) sorts below it; a run whose walk records decrease
-                    // across cuts is the serial path's (the device checks order inside each slice)
-                    (void)prev;
+                    const uint64_t q = host_lower_bound(rb, len, cut[p - 1]);
                     bnd[p * k + m] = q;
-                    if (q < bnd[(p - 1) * k + m]) ok[b] = 0;
+                    if (q == NPOS || q < bnd[(p - 1) * k + m]) ok[b] = 0;
                 }
             }
         });
         for (uint8_t o : ok)
             if (!o) return SKV_OK;
     }
+    const uint64_t R = job.in_bytes / 5 + 1;  // records: at most one per 5 bytes (sizes only)
     htrace("gpipe: cuts");
     used = true;
     struct KernelIO {  // table uploads and readbacks by copy kernels, not DMA behind the bulk copies;
@@ -523,10 +524,30 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ctx->part_ev.push_back(e);
     }
-    // ---- device images of the runs; the shared output
+    // ---- ingest mode: every run in pinned, device-mapped host memory -> the GPU copies each part's
+    // slices itself, one launch per part (k_ingest); else one DMA copy per slice
+    std::vector<uint64_t> hdev(k, 0);
+    bool kernel_ingest = true;
+    {
+        const char* ie = getenv("SKV_INGEST");
+        if (ie && !strcmp(ie, "dma")) kernel_ingest = false;
+        for (uint32_t m = 0; m < k && kernel_ingest; ++m) {
+            hipPointerAttribute_t a;
+            if (hipPointerGetAttributes(&a, run_b(m)) != hipSuccess) {
+                (void)hipGetLastError();
+                kernel_ingest = false;
+            } else if (a.type != hipMemoryTypeHost || !a.devicePointer) {
+                kernel_ingest = false;
+            } else {
+                hdev[m] = (uint64_t)(uintptr_t)a.devicePointer;
+            }
+        }
+    }
+    // ---- device images of the runs (each congruent mod 16 with its host bytes); the shared output
     std::vector<uint64_t> img(k + 1, 0);
-    for (uint32_t m = 0; m < k; ++m) img[m + 1] = img[m] + ((job.run_len[m] + 15) & ~15ull);
+    for (uint32_t m = 0; m < k; ++m) img[m + 1] = img[m] + ((job.run_len[m] + 31) & ~15ull);
     uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", img[k] + 16);
+    for (uint32_t m = 0; m < k; ++m) img[m] += ((uint64_t)(uintptr_t)run_b(m) & 15);  // 16-aligned base + skew
     const uint64_t out_cap = job.in_bytes + R + 64;
     uint8_t* d_out = dbuf<uint8_t>(ctx, "gp_out", out_cap);
     size_t cap = 0;
@@ -544,11 +565,29 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
         }
     } out_guard{ctx, h_out, cap};
     // ---- ingest: every part's slices, in part order, on in_stream
+    IngestSlice* d_sl = nullptr;
+    std::vector<IngestSlice> hsl;
+    if (kernel_ingest) {
+        hsl.resize(P * k);
+        for (uint64_t p = 0; p < P; ++p)
+            for (uint32_t m = 0; m < k; ++m) {
+                const uint64_t lo = p == 0 ? 0 : bnd[p * k + m], hi = bnd[(p + 1) * k + m];
+                hsl[p * k + m] = IngestSlice{hdev[m] + lo, (uint64_t)(uintptr_t)(d_in + img[m] + lo), hi - lo};
+            }
+        d_sl = dbuf<IngestSlice>(ctx, "gp_slices", P * k);
+        HIPCHK(hipMemcpyAsync(d_sl, hsl.data(), P * k * sizeof(IngestSlice), hipMemcpyHostToDevice, ctx->in_stream));
+    }
     for (uint64_t p = 0; p < P; ++p) {
-        for (uint32_t m = 0; m < k; ++m) {
-            const uint64_t lo = p == 0 ? 0 : bnd[p * k + m], hi = bnd[(p + 1) * k + m];
-            if (hi > lo)
-                HIPCHK(hipMemcpyAsync(d_in + img[m] + lo, run_b(m) + lo, hi - lo, hipMemcpyHostToDevice, ctx->in_stream));
+        if (kernel_ingest) {
+            launch_ingest(ctx->in_stream, d_sl + p * k, k, 8);
+            HIPCHK(hipGetLastError());
+        } else {
+            for (uint32_t m = 0; m < k; ++m) {
+                const uint64_t lo = p == 0 ? 0 : bnd[p * k + m], hi = bnd[(p + 1) * k + m];
+                if (hi > lo)
+                    HIPCHK(hipMemcpyAsync(d_in + img[m] + lo, run_b(m) + lo, hi - lo, hipMemcpyHostToDevice,
+                                          ctx->in_stream));
+            }
         }
         HIPCHK(hipEventRecord(ctx->part_ev[2 * p], ctx->in_stream));
     }
@@ -607,7 +646,7 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
         while (std::binary_search(seqs.begin(), seqs.end(), seq_extra)) ++seq_extra;
     }
     std::vector<skv_run_desc> descs;
-    uint64_t open_off = 0, open_len = 0, out_records = 0;
+    uint64_t open_off = 0, open_len = 0, open_recs = 0, out_records = 0, in_records = 0;
     uint64_t syncs = 0;
     for (uint64_t p = 0; p < P; ++p) {
         std::vector<const uint8_t*> ptrs;
@@ -653,6 +692,7 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
         }
         const uint64_t n = pres->n_runs;
         const bool last_part = p + 1 == P;
+        in_records += pres->in_records - (open_len ? open_recs : 0);  // the carried run's records once
         for (uint64_t r = 0; r < n; ++r) {
             skv_run_desc d = pres->runs[r];
             d.off += open_off;
@@ -661,6 +701,7 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
             if (!last_part && r + 1 == n) {  // still open: carried into the next part
                 open_off = d.off;
                 open_len = d.len;
+                open_recs = d.put_count + d.delete_count;
                 break;
             }
             descs.push_back(d);
@@ -687,7 +728,7 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     h_out = nullptr;  // the result owns it now
     res->n_bytes = descs.empty() ? 0 : descs.back().off + descs.back().len;
     res->in_bytes = job.in_bytes;
-    res->in_records = R;
+    res->in_records = in_records;
     res->out_records = out_records;
     res->dropped_tables = 0;
     box->pool = ctx->out_pool;

@@ -137,6 +137,11 @@ void launch_search_scan(hipStream_t, const uint8_t* run, uint64_t len, const uin
                         uint32_t n_q, SrResult* out);
 uint64_t scan_tmp_words(uint64_t n);
 void launch_scan(hipStream_t, const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tmp);
+// skv_stride.hip: a pipelined host call's slices, pinned host -> HBM by the GPU (src == dst mod 16)
+struct IngestSlice {
+    uint64_t src, dst, len;
+};
+void launch_ingest(hipStream_t, const IngestSlice* slices, uint32_t n, uint32_t blocks_per_slice);
 // skv_scan.hip: ScanFromRun after the merge
 void launch_scan_filter(hipStream_t, uint64_t R, uint32_t k, const uint64_t* stream_base, const uint64_t* a_addr,
                         const uint64_t* a_hi, const uint64_t* a_lo, const uint32_t* a_klen, const uint32_t* a_meta,

@@ -1211,6 +1211,32 @@ __global__ void k_copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restric
     }
 }
 
+// Ingest of a pipelined host call's part by the GPU itself: slice y of the part goes from pinned,
+// device-mapped host memory to its run image in HBM (src and dst congruent mod 16), all slices in
+// one launch -- in place of one DMA copy per slice (k slices per part, each a DMA descriptor with its
+// own fixed cost). Blocks x of a slice stride over its 16-byte blocks, four loads in flight per lane.
+__global__ void __launch_bounds__(256) k_ingest(const IngestSlice* __restrict__ sl) {
+    const IngestSlice S = sl[blockIdx.y];
+    const uint8_t* src = (const uint8_t*)S.src;
+    uint8_t* dst = (uint8_t*)S.dst;
+    const uint64_t head = ((16 - (S.src & 15)) & 15) < S.len ? ((16 - (S.src & 15)) & 15) : S.len;
+    const uint64_t nb = (S.len - head) >> 4, tail0 = head + (nb << 4);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    if (t < head) dst[t] = src[t];
+    if (t < S.len - tail0) dst[tail0 + t] = src[tail0 + t];
+    const uint4* s4 = (const uint4*)(src + head);
+    uint4* d4 = (uint4*)(dst + head);
+    uint64_t i = t;
+    for (; i + 3 * stride < nb; i += 4 * stride) {
+        const uint4 a = s4[i], b = s4[i + stride], c = s4[i + 2 * stride], d = s4[i + 3 * stride];
+        d4[i] = a;
+        d4[i + stride] = b;
+        d4[i + 2 * stride] = c;
+        d4[i + 3 * stride] = d;
+    }
+    for (; i < nb; i += stride) d4[i] = s4[i];
+}
+
 // ---------------------------------------------------------------------------------------------
 static inline unsigned fx_blocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
@@ -1254,6 +1280,9 @@ uint64_t fx_tile_slots(uint32_t k) {  // fused tiles resident at once on the cur
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_fx_tile, FX_THREADS, fx_tile_lds_bytes(k));
     cached_k[dev & 63] = k;
     return cached[dev & 63] = (uint64_t)(cus > 0 ? cus : 256) * (uint64_t)(per > 0 ? per : 1);
+}
+void launch_ingest(hipStream_t s, const IngestSlice* slices, uint32_t n, uint32_t blocks_per_slice) {
+    if (n) k_ingest<<<dim3(blocks_per_slice, n), 256, 0, s>>>(slices);
 }
 void launch_copy_bytes(hipStream_t s, uint8_t* dst, const uint8_t* src, uint64_t n) {
     if (n) k_copy_bytes<<<fx_blocks((n + 15) / 16, 256), 256, 0, s>>>(dst, src, n);

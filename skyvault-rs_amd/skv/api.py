@@ -176,17 +176,21 @@ class Compactor:
         return DeviceResult(self.lib, res, self)
 
     def compact_host_ptrs(self, streams: Sequence[Tuple[int, Sequence[Tuple[int, int]]]],
-                          max_run_size: int = MAX_RUN_SIZE, flags: int = 0) -> Tuple[int, int]:
+                          max_run_size: int = MAX_RUN_SIZE, flags: int = 0, with_runs: bool = False):
         """skv_compact on raw host buffers (e.g. pinned tensors): [(seq_no, [(host_ptr, length)])].
-        Returns (output bytes, output runs); the pinned output is released immediately."""
+        Returns (output bytes, output runs) -- or, with_runs, the [OutRun] -- and releases the pinned
+        output."""
         sa = StreamArgs(streams, device=True)
         res = C.POINTER(SkvResult)()
         rc = self.lib.skv_compact(self.ctx, sa.ptr, sa.n, max_run_size, flags, C.byref(res))
         if rc != SKV_OK:
             raise self._err(rc)
-        n = (int(res.contents.n_bytes), int(res.contents.n_runs))
-        self.lib.skv_result_free(res)
-        return n
+        try:
+            if with_runs:
+                return result_to_runs(res.contents)
+            return (int(res.contents.n_bytes), int(res.contents.n_runs))
+        finally:
+            self.lib.skv_result_free(res)
 
     def encode_batch(self, ops_run: bytes, max_run_size: int = MAX_RUN_SIZE, with_info: bool = False):
         """Writer batch encode (writer_service.rs:148-162): ops_run = the batch's ops in request

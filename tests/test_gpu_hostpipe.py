@@ -19,6 +19,7 @@ from skv import _abi
 from skv import format as fmt
 from skv.api import Compactor
 
+import pyoracle
 from test_gpu_parity import _diff, _run_both
 
 pytestmark = pytest.mark.gpu
@@ -268,3 +269,28 @@ def test_failure_mid_pipeline_leaves_the_ctx_clean(dev, pipe_env, fail_at):
     for _ in range(3):  # the pool's buffer is taken and given back again on every call
         _check(dev, streams, 4 * MiB, 0, 6)
     _check(dev, _streams(rng, 3, 500, 4000), 4 * MiB, 0, 4)
+
+
+@pytest.mark.parametrize("parts", [3, 8])
+def test_general_pipeline_pinned_inputs_kernel_ingest(dev, pipe_env, parts):
+    """runs in pinned, device-mapped host memory: the GPU copies each part's slices itself
+    (k_ingest, one launch per part) -- also with run buffers at odd host offsets"""
+    torch = pytest.importorskip("torch")
+    rng = random.Random(500 + parts)
+    streams = _var_streams(rng, 10, 2500, 12000, del_frac=0.15)
+    pinned, pstreams = [], []
+    for i, (seq, runs) in enumerate(streams):
+        r = runs[0]
+        skew = (i * 5) % 16  # host buffers not 16-byte aligned
+        t = torch.empty(len(r) + skew, dtype=torch.uint8).pin_memory()
+        t[skew:] = torch.frombuffer(bytearray(r), dtype=torch.uint8)
+        pinned.append(t)
+        pstreams.append((seq, [(t.data_ptr() + skew, len(r))]))
+    os.environ["SKV_HOST_PARTS"] = str(parts)
+    for mx in (2048, 20000):
+        got = dev.compact_host_ptrs(pstreams, mx, 0, with_runs=True)
+        assert dev.timings()["host_parts"] == parts
+        exp = pyoracle.compact(streams, mx, 0)
+        assert [r.data for r in got] == [r.data for r in exp]
+        assert [(r.stats.min_key, r.stats.max_key, r.stats.put_count, r.stats.delete_count) for r in got] == \
+            [(r.stats.min_key, r.stats.max_key, r.stats.put_count, r.stats.delete_count) for r in exp]

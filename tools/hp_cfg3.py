@@ -1,7 +1,7 @@
 """General host pipeline probe: config 3 (256 streams x --run-mib MiB of variable-length records +
 10 % Deletes) in pinned host memory through skv_compact, serial (SKV_HOST_PIPE=0) against the
 key-range pipeline at several part counts; wall time per call (best of 3). With SKV_HOST_TRACE=1
-the library prints its host-side milestones of the last call of each setting.
+the library prints its host-side milestones of every call.
 
 usage: python tools/hp_cfg3.py [--run-mib 16] [P ...]
 """
@@ -34,7 +34,6 @@ def main():
     streams = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(host)]
     nbytes = sum(r.numel() for r in host)
     comp = Compactor(0)
-    trace = os.environ.pop("SKV_HOST_TRACE", None)
     for P in parts:
         if P == 0:
             os.environ["SKV_HOST_PIPE"] = "0"
@@ -44,12 +43,9 @@ def main():
         comp.compact_host_ptrs(streams, 4 << 20, 0)
         ts = []
         for i in range(3):
-            if i == 2 and trace:
-                os.environ["SKV_HOST_TRACE"] = trace
             t0 = time.perf_counter()
             comp.compact_host_ptrs(streams, 4 << 20, 0)
             ts.append(time.perf_counter() - t0)
-            os.environ.pop("SKV_HOST_TRACE", None)
         t = min(ts)
         print(f"P={P} parts={comp.timings()['host_parts']} best {t * 1e3:.2f} ms = {nbytes / t / 2**30:.2f} GiB/s "
               f"(all: {', '.join(f'{x * 1e3:.1f}' for x in ts)})", flush=True)
