@@ -502,3 +502,32 @@ def test_device_entry_reuse_across_calls(dev):
             assert got[0] == "err" and got[1] == _abi.SKV_E_INVALID_ARG
         else:
             assert got == exp
+
+
+@pytest.mark.parametrize("rows", ["0", "8", "1"])
+def test_staged_chunk_walks(dev, rows):
+    """The chunk walks stage each record's array entries (StageBufs) and k_emit_st copies them; with
+    SKV_STAGE=0 the old emit re-parses every record, with 8 rows per chunk most chunks overflow and
+    the emit parses the rest from the last staged record. Every variant gives the reference's
+    outcome on fake records in values (k_fixup's chunks), corruption, invalid UTF-8 keys and
+    generated general-path configs."""
+    old = os.environ.get("SKV_STAGE")
+    os.environ["SKV_STAGE"] = rows
+    try:
+        test_values_with_fake_records(dev)
+        test_corruption_at_every_position_class(dev)
+        test_invalid_utf8_key_in_variable_runs(dev)
+        for name, mk, mx, fl in [("cfg3", lambda: gen.config3(n_streams=32, run_bytes=192 * KiB), 256 * KiB, 0),
+                                 ("cfg3_drop", lambda: gen.config3(n_streams=32, run_bytes=192 * KiB), 256 * KiB, 1),
+                                 ("small", lambda: gen.config2(n_streams=16, n_records=2000, vsize=40), 64 * KiB, 0)]:
+            exp, got = _run_both(dev, mk(), mx, fl)
+            assert exp == got, (name, _diff(exp, got))
+        for seed in range(0, 600, 5):
+            streams, max_size, flags = _case(seed)
+            exp, got = _run_both(dev, streams, max_size, flags)
+            assert exp == got, (seed, _diff(exp, got))
+    finally:
+        if old is None:
+            os.environ.pop("SKV_STAGE", None)
+        else:
+            os.environ["SKV_STAGE"] = old
