@@ -557,6 +557,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                     sb.off = dbuf<uint16_t>(ctx, "st_off", n);
                     sb.st_start = dbuf<uint64_t>(ctx, "st_start", n_chunks);
                     sb.st_base = dbuf<uint64_t>(ctx, "st_base", n_chunks);
+                    if (const char* de = getenv("SKV_STAGE_DBG")) sb.dbg = (uint32_t)strtoul(de, nullptr, 10);
                 }
             }
             htrace(sb.scap ? "staging rows" : "no staging");

@@ -107,6 +107,7 @@ struct StageBufs {
     uint64_t* st_base;   // per chunk: device address of the chunk start
     uint32_t scap;       // staged records per chunk (a power of two; 0: no staging)
     uint32_t sh;         // log2(scap)
+    uint32_t dbg;        // diagnostic builds of the walk (SKV_STAGE_DBG): 1 no stores, 2 no fingerprint
 };
 
 struct RunSummary {       // per run, read back by the host after the parse

@@ -377,18 +377,45 @@ inline int host_key_cmp(const uint8_t* a, uint64_t al, const uint8_t* c, uint64_
 inline int rec_vs(const uint8_t* b, uint64_t p, const std::string& c) {
     return host_key_cmp(b + p + 5, be32(b + p + 1), (const uint8_t*)c.data(), c.size());
 }
+// core::str::from_utf8 acceptance (runs.rs:585-591)
+inline bool host_utf8(const uint8_t* s, uint64_t n) {
+    uint64_t i = 0;
+    while (i < n) {
+        const uint32_t c = s[i];
+        if (c < 0x80) {
+            ++i;
+            continue;
+        }
+        uint32_t need, lo = 0x80, hi = 0xBF;
+        if (c >= 0xC2 && c <= 0xDF) need = 1;
+        else if (c == 0xE0) { need = 2; lo = 0xA0; }
+        else if ((c >= 0xE1 && c <= 0xEC) || c == 0xEE || c == 0xEF) need = 2;
+        else if (c == 0xED) { need = 2; hi = 0x9F; }
+        else if (c == 0xF0) { need = 3; lo = 0x90; }
+        else if (c >= 0xF1 && c <= 0xF3) need = 3;
+        else if (c == 0xF4) { need = 3; hi = 0x8F; }
+        else return false;
+        if (n - i - 1 < need || s[i + 1] < lo || s[i + 1] > hi) return false;
+        for (uint32_t q = 2; q <= need; ++q)
+            if (s[i + q] < 0x80 || s[i + q] > 0xBF) return false;
+        i += need + 1;
+    }
+    return true;
+}
 // A record start near byte x without walking the run from its start: the first p >= x from which
-// RESYNC_N records decode with strictly increasing keys (or the run ends cleanly after fewer). A
-// position that passes but is not a record start of the run's true chain is harmless: the slice
-// that ends there cannot decode (its chain from a true start never lands on it), the device reports
-// an error, and the call takes the serial path.
+// RESYNC_N records decode with valid UTF-8 keys in strictly increasing order (or the run ends
+// cleanly after fewer). The UTF-8 check matters: a value byte 1 followed by a length that fits the
+// run makes one giant "record" whose end can land on a true record start, and its random-byte
+// "key" sorts below the next key one time in five -- at config 3's scale such positions occur a few
+// hundred times per 4 GB. A position that still passes but is not a true record start would put a
+// slice boundary inside a record; the part's decode then fails and the call takes the serial path.
 constexpr int RESYNC_N = 8;
 constexpr uint64_t RESYNC_SPAN = 1u << 16;
 inline bool plausible(const uint8_t* b, uint64_t len, uint64_t p) {
     uint64_t prev = NPOS;
     for (int i = 0; i < RESYNC_N && p < len; ++i) {
         const uint64_t sz = host_rec_at(b, len, p);
-        if (!sz) return false;
+        if (!sz || !host_utf8(b + p + 5, be32(b + p + 1))) return false;
         if (prev != NPOS && host_key_cmp(b + prev + 5, be32(b + prev + 1), b + p + 5, be32(b + p + 1)) >= 0) return false;
         prev = p;
         p += sz;
@@ -463,7 +490,10 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
         for (auto& v : part_smp) smp.insert(smp.end(), v.begin(), v.end());
     }
     htrace("gpipe: sampled");
-    if (smp.size() < P) return SKV_OK;
+    if (smp.size() < P) {
+        htrace("gpipe: too few samples");
+        return SKV_OK;
+    }
     std::sort(smp.begin(), smp.end(), [](const auto& a, const auto& c) {
         return host_key_cmp(a.first, a.second, c.first, c.second) < 0;
     });
@@ -486,12 +516,15 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
                 for (uint64_t p = 1; p < P; ++p) {
                     const uint64_t q = host_lower_bound(rb, len, cut[p - 1]);
                     bnd[p * k + m] = q;
-                    if (q == NPOS || q < bnd[(p - 1) * k + m]) ok[b] = 0;
+                    if (q == NPOS || q < bnd[(p - 1) * k + m]) ok[b] = q == NPOS ? 2 : 3;
                 }
             }
         });
         for (uint8_t o : ok)
-            if (!o) return SKV_OK;
+            if (o != 1) {
+                htrace(o == 2 ? "gpipe: a cut not found" : "gpipe: cuts out of order");
+                return SKV_OK;
+            }
     }
     const uint64_t R = job.in_bytes / 5 + 1;  // records: at most one per 5 bytes (sizes only)
     htrace("gpipe: cuts");

@@ -160,8 +160,11 @@ __device__ __forceinline__ bool fixed_rec_ok(const uint8_t* run, uint64_t len, u
 }
 
 // walk_fast's record loop with staging (StageBufs): every record decoded is also parsed for the
-// record arrays and stored at row + i * 64. A record the staging cannot hold (key >= 2^30 bytes,
-// record >= 2^31 bytes) clears `staged`, and the chunk is emitted the old way.
+// record arrays and stored at row + i * 64. A record with a key longer than STAGE_MAX_KEY (or a
+// record >= 2^31 bytes) ends the staging of its chunk, which is then emitted the old way: a walk
+// from a wrong speculative start can decode garbage "records" with keys of megabytes, and
+// fingerprinting those would read them whole (k_validate discards such walks anyway).
+constexpr uint64_t STAGE_MAX_KEY = 2048;
 template <int UTF8>
 __device__ inline WalkRes walk_stage(const uint8_t* run, uint64_t len, uint64_t p, uint64_t stop, const StageBufs& sb,
                                      uint64_t row, uint64_t cs, bool& staged) {
@@ -169,18 +172,20 @@ __device__ inline WalkRes walk_stage(const uint8_t* run, uint64_t len, uint64_t 
     while (p < stop) {
         const RecHdr h = parse_rec<true, UTF8>(run, len, p);
         if (h.err) return {p, cnt, h.err};
-        if (cnt < sb.scap) {
-            if (h.klen >= (1ull << 30) || h.size >= (1ull << 31)) staged = false;
-            bool ascii;
-            const uint64_t fpv = key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii);
+        if (h.klen > STAGE_MAX_KEY || h.size >= (1ull << 31)) staged = false;
+        if (staged && cnt < sb.scap) {
+            bool ascii = true;
+            const uint64_t fpv = (sb.dbg & 2) ? 0 : key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii);
             const bool high = !(ascii && ((h.hi | h.lo) & 0x8080808080808080ull) == 0);
             const uint64_t x = row + (uint64_t)cnt * 64;
+            if (!(sb.dbg & 1)) {
             sb.hi[x] = h.hi;
             sb.lo[x] = h.lo;
             sb.fp[x] = fpv;
             sb.klen[x] = (uint32_t)h.klen | (high ? 0x80000000u : 0u);
             sb.meta[x] = (uint32_t)h.size | (h.marker == 2 ? 0x80000000u : 0u);
             sb.off[x] = (uint16_t)(p - cs);
+            }
         }
         ++cnt;
         p += h.size;
@@ -242,8 +247,12 @@ __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
             for (uint64_t i = 0; i < n && i < cap; ++i) sl[i] = (uint16_t)(p0 + i * S - cs);
             return;
         }
-        atomicOr(&run_broken[r], 1u);  // hypothesis broken: this run takes the general path
-        start = p0;
+        // hypothesis broken: this run takes the general path, from a speculative start like any
+        // variable-size run (p0 is only right for a run that is fixed-stride up to some fault; for a
+        // variable run whose first record size happens to divide its body -- ~1 run in 300 of
+        // config 3 -- every chunk's p0 missed the chain and k_fixup walked the whole run: 95 ms)
+        atomicOr(&run_broken[r], 1u);
+        start = local == 0 ? 1 : spec_start<UTF8>(run, R.len, cs, ce);
     } else {
         start = local == 0 ? 1 : spec_start<UTF8>(run, R.len, cs, ce);
     }

@@ -1,5 +1,5 @@
 """General host pipeline probe: config 3 (256 streams x --run-mib MiB of variable-length records +
-10 % Deletes) in pinned host memory through skv_compact, serial (SKV_HOST_PIPE=0) against the
+10 % Deletes, built by the GPU generator) in pinned host memory through skv_compact, serial (SKV_HOST_PIPE=0) against the
 key-range pipeline at several part counts; wall time per call (best of 3). With SKV_HOST_TRACE=1
 the library prints its host-side milestones of every call.
 
@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(ROOT, "skyvault-rs_amd"))
 import torch  # noqa: E402
 
 from skv.api import Compactor  # noqa: E402
-from skv.devgen import make_cfg3_on_device  # noqa: E402
+from skv.devgen import make_cfg3_full_on_device  # noqa: E402
 
 
 def main():
@@ -27,7 +27,7 @@ def main():
     parts = [int(a) for a in args] or [0, 8, 14, 32]
     torch.cuda.init()
     dev = torch.device("cuda:0")
-    runs = make_cfg3_on_device(dev, 0x5EEDC0DE, 256, run_mib)
+    runs = make_cfg3_full_on_device(dev, 0x5EEDC0DE, 256, run_mib)
     host = [r.cpu().pin_memory() for r in runs]
     del runs
     torch.cuda.empty_cache()
