@@ -431,7 +431,6 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // ---- fast path: every run fixed-stride (one record size per run) -> one verifying pass ------
     bool parsed = false, deferred = false;
     bool any_fixed = false;  // some run is fixed-stride: the general parse also runs k_emit_fixed
-    uint64_t first_sum = 0, first_n = 0;  // the runs' first-record sizes (staging rows of the general parse)
     {
         RunFmt* hf = (RunFmt*)pinned(ctx, (size_t)n_runs * sizeof(RunFmt) + 16);
         d2h(ctx, hf, d_fmt, (size_t)n_runs * sizeof(RunFmt));
@@ -442,27 +441,17 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         // blocks of runs on host threads: every run fixed-stride? one format everywhere?
         const unsigned nbr = par_nblocks(n_runs);
         std::vector<uint8_t> blk_fixed(nbr, 1), blk_uni(nbr, 1), blk_any(nbr, 0);
-        std::vector<uint64_t> blk_fs(nbr, 0), blk_fn(nbr, 0);
         par_run(n_runs, nbr, [&](unsigned b, uint64_t lo, uint64_t hi) {
             bool fx = true, un = true, an = false;
-            uint64_t fs = 0, fc = 0;
             for (uint64_t r = lo; r < hi; ++r) {
                 fx = fx && hf[r].S != 0;
                 an = an || hf[r].S != 0;
                 un = un && hf[r].S == hf[0].S && hf[r].K == hf[0].K;
-                fs += hf[r].first;
-                fc += hf[r].first != 0;
             }
             blk_fixed[b] = fx;
             blk_uni[b] = un;
             blk_any[b] = an;
-            blk_fs[b] = fs;
-            blk_fn[b] = fc;
         });
-        for (unsigned b = 0; b < nbr; ++b) {
-            first_sum += blk_fs[b];
-            first_n += blk_fn[b];
-        }
         bool all_fixed = n_runs > 0, uniform = true;
         for (unsigned b = 0; b < nbr; ++b) {
             all_fixed = all_fixed && blk_fixed[b];
@@ -530,43 +519,11 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         // k_emit parses the records of a chunk in parallel instead of walking its chain again
         const uint32_t slot_cap = (uint32_t)((chunk / 64 + 7) & ~7ull);  // rows of 16-byte groups (walk_fast)
         uint16_t* ch_slots = dbuf<uint16_t>(ctx, "ch_slots", n_chunks * slot_cap);
-        // staging rows (StageBufs): scap = the power of two nearest 1.1 x the records a chunk holds
-        // at the runs' mean first-record size; chunks with more records parse the rest at emission
-        StageBufs sb{};
-        {
-            const char* se = getenv("SKV_STAGE");
-            const uint64_t fsum = first_sum, fn = first_n;
-            const unsigned long sv = se ? strtoul(se, nullptr, 10) : 1;  // 0: off, 1: auto, else rows (tests)
-            if (sv && fn && n_chunks) {
-                const double per = (double)chunk * fn / (double)fsum * 1.1;
-                uint32_t sc = 8;
-                while (sc < 256 && sc * 1.41 < per) sc *= 2;
-                const uint64_t rows = (n_chunks + 63) / 64 * 64;
-                const uint64_t budget = std::max<uint64_t>(256ull << 20, job.in_bytes / 4);
-                while (sc >= 8 && rows * sc * 34 > budget) sc /= 2;
-                if (sv > 1) sc = (uint32_t)sv;
-                if (sc >= 1 && (sc & (sc - 1)) == 0) {
-                    sb.scap = sc;
-                    while ((1u << sb.sh) < sc) ++sb.sh;
-                    const uint64_t n = rows * sc;
-                    sb.hi = dbuf<uint64_t>(ctx, "st_hi", n);
-                    sb.lo = dbuf<uint64_t>(ctx, "st_lo", n);
-                    sb.fp = dbuf<uint64_t>(ctx, "st_fp", n);
-                    sb.klen = dbuf<uint32_t>(ctx, "st_klen", n);
-                    sb.meta = dbuf<uint32_t>(ctx, "st_meta", n);
-                    sb.off = dbuf<uint16_t>(ctx, "st_off", n);
-                    sb.st_start = dbuf<uint64_t>(ctx, "st_start", n_chunks);
-                    sb.st_base = dbuf<uint64_t>(ctx, "st_base", n_chunks);
-                    if (const char* de = getenv("SKV_STAGE_DBG")) sb.dbg = (uint32_t)strtoul(de, nullptr, 10);
-                }
-            }
-            htrace(sb.scap ? "staging rows" : "no staging");
-        }
         HIPCHK(hipMemsetAsync(bad_bits, 0, (n_chunks / 64 + 1) * 8, st));
         HIPCHK(hipMemsetAsync(first_bad, 0xFF, n_runs * 4, st));
         HIPCHK(hipMemsetAsync(err_chunk, 0xFF, n_runs * 4, st));
         launch_spec(st, d_runs, n_runs, n_chunks, d_hdr, d_fmt, d_broken, ch_start, ch_end, ch_cnt, ch_err,
-                    ctx->exact_utf8, chunk, ch_slots, slot_cap, sb);
+                    ctx->exact_utf8, chunk, ch_slots, slot_cap);
         launch_validate(st, d_runs, n_runs, n_chunks, d_hdr, ch_start, ch_end, ch_err, bad_bits, first_bad);
         launch_fixup(st, d_runs, n_runs, d_hdr, first_bad, bad_bits, ch_start, ch_end, ch_cnt, ch_err,
                      ctx->exact_utf8, chunk, ch_slots, slot_cap);
@@ -586,8 +543,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         stream_tables();
         alloc_records();
         launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, any_fixed ? R : 0,
-                    rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad, ch_slots, slot_cap, chunk,
-                    sb);
+                    rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad, ch_slots, slot_cap, chunk);
         mark(ctx, PH_PARSE);
         check_and_read(false);
         if (utf8_flag && !ctx->exact_utf8) {  // a key the chunk walks did not check: exact walks

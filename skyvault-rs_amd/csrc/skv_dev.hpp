@@ -91,25 +91,6 @@ struct RunFmt {           // fixed-stride hypothesis of a run (S == 0: none)
     uint64_t first;       // size of the run's first record (0: none, or it does not decode)
 };
 
-// Staging of the general chunk walks (k_spec with scap > 0): each record a walk decodes is also
-// parsed for the record arrays and stored in its chunk's staging row, so the emit step copies it
-// instead of reading the record's header and key lines a second time (k_emit_st). Rows are
-// lane-interleaved per wave of walks: record i of chunk c sits at ((c / 64) * scap + i) * 64 + c % 64,
-// so step i of a wave's 64 walks is one coalesced store per array.
-struct StageBufs {
-    uint64_t* hi;        // 16-byte key prefix (big-endian, zero padded)
-    uint64_t* lo;
-    uint64_t* fp;        // fingerprint of the key bytes past 16 (key_tail_fp)
-    uint32_t* klen;      // key length | 1 << 31 when a key byte has its high bit set (exact UTF-8 check at emission)
-    uint32_t* meta;      // size | Delete << 31
-    uint16_t* off;       // record start - chunk start
-    uint64_t* st_start;  // per chunk: where its walk started (NO_POS: not staged)
-    uint64_t* st_base;   // per chunk: device address of the chunk start
-    uint32_t scap;       // staged records per chunk (a power of two; 0: no staging)
-    uint32_t sh;         // log2(scap)
-    uint32_t dbg;        // diagnostic builds of the walk (SKV_STAGE_DBG): 1 no stores, 2 no fingerprint
-};
-
 struct RunSummary {       // per run, read back by the host after the parse
     uint64_t records;     // records decoded before the first error of the run
     uint32_t err;         // DERR_* | extra << 8 (0 = none)

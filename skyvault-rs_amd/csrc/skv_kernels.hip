@@ -159,45 +159,11 @@ __device__ __forceinline__ bool fixed_rec_ok(const uint8_t* run, uint64_t len, u
     return vlen == f.V;
 }
 
-// walk_fast's record loop with staging (StageBufs): every record decoded is also parsed for the
-// record arrays and stored at row + i * 64. A record with a key longer than STAGE_MAX_KEY (or a
-// record >= 2^31 bytes) ends the staging of its chunk, which is then emitted the old way: a walk
-// from a wrong speculative start can decode garbage "records" with keys of megabytes, and
-// fingerprinting those would read them whole (k_validate discards such walks anyway).
-constexpr uint64_t STAGE_MAX_KEY = 2048;
-template <int UTF8>
-__device__ inline WalkRes walk_stage(const uint8_t* run, uint64_t len, uint64_t p, uint64_t stop, const StageBufs& sb,
-                                     uint64_t row, uint64_t cs, bool& staged) {
-    uint32_t cnt = 0;
-    while (p < stop) {
-        const RecHdr h = parse_rec<true, UTF8>(run, len, p);
-        if (h.err) return {p, cnt, h.err};
-        if (h.klen > STAGE_MAX_KEY || h.size >= (1ull << 31)) staged = false;
-        if (staged && cnt < sb.scap) {
-            bool ascii = true;
-            const uint64_t fpv = (sb.dbg & 2) ? 0 : key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii);
-            const bool high = !(ascii && ((h.hi | h.lo) & 0x8080808080808080ull) == 0);
-            const uint64_t x = row + (uint64_t)cnt * 64;
-            if (!(sb.dbg & 1)) {
-            sb.hi[x] = h.hi;
-            sb.lo[x] = h.lo;
-            sb.fp[x] = fpv;
-            sb.klen[x] = (uint32_t)h.klen | (high ? 0x80000000u : 0u);
-            sb.meta[x] = (uint32_t)h.size | (h.marker == 2 ? 0x80000000u : 0u);
-            sb.off[x] = (uint16_t)(p - cs);
-            }
-        }
-        ++cnt;
-        p += h.size;
-    }
-    return {p, cnt, DERR_NONE};
-}
-
 template <int UTF8>
 __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
                        const uint32_t* __restrict__ hdr_err, const RunFmt* __restrict__ fmt, uint32_t* run_broken,
                        uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, uint64_t chunk,
-                       uint16_t* slots, uint32_t cap, StageBufs sb) {
+                       uint16_t* slots, uint32_t cap) {
     uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
     uint32_t r = find_run(runs, n_runs, c);
@@ -206,7 +172,6 @@ __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
     const uint8_t* run = (const uint8_t*)R.ptr;
     uint64_t cs = 1 + local * chunk;
     uint64_t ce = cs + chunk < R.len ? cs + chunk : R.len;
-    if (sb.scap) sb.st_start[c] = NO_POS;  // staged below only by a general walk
     if (hdr_err[r]) {
         ch_start[c] = cs;
         ch_end[c] = cs;
@@ -261,22 +226,6 @@ __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         ch_end[c] = NO_POS;
         ch_cnt[c] = 0;
         ch_err[c] = 0;
-        return;
-    }
-    if (sb.scap) {
-        bool staged = true;
-        const uint64_t row = ((c >> 6) << sb.sh) * 64 + (c & 63);
-        const WalkRes w = walk_stage<UTF8>(run, R.len, start, ce, sb, row, cs, staged);
-        ch_start[c] = start;
-        ch_end[c] = w.end;
-        ch_cnt[c] = w.cnt;
-        ch_err[c] = w.err;
-        if (staged) {
-            sb.st_start[c] = start;
-            sb.st_base[c] = R.ptr + cs;
-        } else {  // the old emission reads the slots: walk again, keeping the record starts
-            walk_fast<UTF8>(run, R.len, start, ce, 0xFFFFFFFFu, GLoad(), slots + c * cap, cap, cs);
-        }
         return;
     }
     const WalkRes w = walk_fast<UTF8>(run, R.len, start, ce, 0xFFFFFFFFu, GLoad(), slots + c * cap, cap, cs);
@@ -419,14 +368,13 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
                        uint64_t* __restrict__ rec_addr, uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
                        uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags,
                        uint64_t* __restrict__ rec_fp, uint32_t* utf8_bad, const uint16_t* __restrict__ slots,
-                       uint32_t cap, uint64_t chunk, const uint64_t* __restrict__ st_start) {
+                       uint32_t cap, uint64_t chunk) {
     const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t c = gi / EM_G;
     const uint32_t j0 = (uint32_t)(gi % EM_G);
     if (c >= n_chunks) return;
     uint64_t b0 = ch_rec_base[c], cnt = ch_rec_base[c + 1] - b0;
     if (!cnt) return;
-    if (st_start && st_start[c] != NO_POS && st_start[c] == ch_start[c]) return;  // k_emit_st
     uint32_t r = find_run(runs, n_runs, c);
     if (fmt[r].S && !run_broken[r]) return;  // k_emit_fixed
     const uint8_t* run = (const uint8_t*)runs[r].ptr;
@@ -456,52 +404,6 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         const uint64_t p = cs + sl[i];
         if (p >= len) continue;  // never: every counted record's start is in its slot
         emit(i, p, parse_rec<true, false>(run, len, p));
-    }
-}
-
-// Emission of the staged chunks (StageBufs): thread g copies staging entry g -- record i of chunk
-// c for g = ((c / 64) * scap + i) * 64 + c % 64, so the reads are coalesced and each wave's stores
-// land in the dense range of its chunks. A chunk counts as staged when k_spec's walk from
-// st_start[c] is the validated one (k_fixup leaves ch_start alone wherever the speculative start
-// was right). Records past scap (a chunk of unusually small records) are parsed by the chunk's
-// i = 0 thread, from the end of its last staged record.
-__global__ void k_emit_st(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
-                          const uint64_t* __restrict__ ch_start, const uint64_t* __restrict__ ch_rec_base, StageBufs sb,
-                          uint64_t* __restrict__ rec_addr, uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
-                          uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags,
-                          uint64_t* __restrict__ rec_fp, uint32_t* utf8_bad) {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t i = (g >> 6) & (sb.scap - 1);
-    const uint64_t c = ((g >> 6) >> sb.sh) * 64 + (g & 63);
-    if (c >= n_chunks) return;
-    const uint64_t s0 = sb.st_start[c];
-    if (s0 == NO_POS || s0 != ch_start[c]) return;
-    const uint64_t b0 = ch_rec_base[c], cnt = ch_rec_base[c + 1] - b0;
-    if (i < cnt) {
-        const uint64_t addr = sb.st_base[c] + sb.off[g];
-        const uint32_t kl = sb.klen[g];
-        rec_addr[b0 + i] = addr;
-        rec_hi[b0 + i] = sb.hi[g];
-        rec_lo[b0 + i] = sb.lo[g];
-        rec_fp[b0 + i] = sb.fp[g];
-        rec_klen[b0 + i] = kl & 0x7FFFFFFFu;
-        rec_meta[b0 + i] = sb.meta[g];
-        if ((kl >> 31) && !utf8_valid((const uint8_t*)(addr + 5), kl & 0x7FFFFFFFu)) atomicOr(utf8_bad, 1u);
-    }
-    if (i == 0 && cnt > sb.scap) {
-        const RunInfo R = runs[find_run(runs, n_runs, c)];
-        const uint8_t* run = (const uint8_t*)R.ptr;
-        const uint64_t xl = g + (uint64_t)(sb.scap - 1) * 64;  // the last staged record
-        uint64_t p = sb.st_base[c] + sb.off[xl] + (sb.meta[xl] & 0x7FFFFFFFu) - R.ptr;
-        for (uint64_t j = sb.scap; j < cnt; ++j) {
-            const RecHdr h = parse_rec<true, false>(run, R.len, p);
-            bool ascii;
-            const uint64_t fpv = key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii);
-            if (!(ascii && ((h.hi | h.lo) & 0x8080808080808080ull) == 0) && !utf8_valid(run + p + 5, h.klen))
-                atomicOr(utf8_bad, 1u);
-            put_rec(b0 + j, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp, fpv);
-            p += h.size;
-        }
     }
 }
 
@@ -2610,14 +2512,14 @@ void launch_run_header(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint
 }
 void launch_spec(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                  const RunFmt* fmt, uint32_t* run_broken, uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt,
-                 uint32_t* ch_err, bool utf8, uint64_t chunk, uint16_t* slots, uint32_t cap, const StageBufs& sb) {
+                 uint32_t* ch_err, bool utf8, uint64_t chunk, uint16_t* slots, uint32_t cap) {
     if (!n_chunks) return;
     if (utf8)
         k_spec<1><<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, fmt, run_broken, ch_start,
-                                                            ch_end, ch_cnt, ch_err, chunk, slots, cap, sb);
+                                                            ch_end, ch_cnt, ch_err, chunk, slots, cap);
     else
         k_spec<0><<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, fmt, run_broken, ch_start,
-                                                            ch_end, ch_cnt, ch_err, chunk, slots, cap, sb);
+                                                            ch_end, ch_cnt, ch_err, chunk, slots, cap);
 }
 void launch_validate(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                      const uint64_t* ch_start, const uint64_t* ch_end, const uint32_t* ch_err,
@@ -2653,17 +2555,11 @@ void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n
                  const uint32_t* run_broken, const uint64_t* ch_start, const uint64_t* ch_rec_base,
                  const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                  uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, uint64_t* rec_fp, uint32_t* utf8_bad,
-                 const uint16_t* slots, uint32_t cap, uint64_t chunk, const StageBufs& sb) {
-    if (n_chunks) {
+                 const uint16_t* slots, uint32_t cap, uint64_t chunk) {
+    if (n_chunks)
         k_emit<<<blocks_for(n_chunks * EM_G, 256), 256, 0, s>>>(runs, n_runs, n_chunks, fmt, run_broken, ch_start,
                                                                 ch_rec_base, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
-                                                                flags, rec_fp, utf8_bad, slots, cap, chunk,
-                                                                sb.scap ? sb.st_start : nullptr);
-        if (sb.scap)
-            k_emit_st<<<blocks_for(((n_chunks + 63) / 64) * 64 * sb.scap, 256), 256, 0, s>>>(
-                runs, n_runs, n_chunks, ch_start, ch_rec_base, sb, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags,
-                rec_fp, utf8_bad);
-    }
+                                                                flags, rec_fp, utf8_bad, slots, cap, chunk);
     if (R)
         k_emit_fixed<false><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, nullptr, R, fmt, (uint32_t*)run_broken, run_recb,
                                                                rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags,
