@@ -464,7 +464,8 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     if (job.in_bytes < min_bytes || (job.flags & SKV_SPLIT_BY_TABLE) || job.batch || job.search || job.scan) return SKV_OK;
     if (k == 0 || job.run_ptr.size() != k) return SKV_OK;  // one run per stream
     if (k > (uint32_t)TILE_TARGET / 2) return SKV_OK;       // the splitter merge's fan-in per part
-    uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(64, job.in_bytes / (256ull << 20)));
+    // parts of ~512 MiB: each part costs k DMA copies (config 3, 4 GiB: 8 parts 105 ms, 14 parts 123)
+    uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(32, job.in_bytes / (512ull << 20)));
     if (const char* pp = getenv("SKV_HOST_PARTS")) P = std::max<uint64_t>(1, std::min<uint64_t>(256, strtoull(pp, nullptr, 10)));
     // the open run is carried into every part: keep it small against a part
     if (P < 2 || job.max_run_size > job.in_bytes / (4 * P)) return SKV_OK;
@@ -557,13 +558,16 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ctx->part_ev.push_back(e);
     }
-    // ---- ingest mode: every run in pinned, device-mapped host memory -> the GPU copies each part's
-    // slices itself, one launch per part (k_ingest); else one DMA copy per slice
+    // ---- ingest mode: one DMA copy per slice; or (SKV_INGEST=kernel, every run in pinned,
+    // device-mapped host memory) the GPU copies each part's slices itself, one launch per part
+    // (k_ingest). The copy kernels measured slower (config 3, 8 parts: 130 vs 105 ms): while later
+    // parts' copies ran, part 0's kernels did not start (77 ms in), as if in_stream and the ctx
+    // stream shared a hardware queue; the DMA engines take no compute queue.
     std::vector<uint64_t> hdev(k, 0);
-    bool kernel_ingest = true;
+    bool kernel_ingest = false;
     {
         const char* ie = getenv("SKV_INGEST");
-        if (ie && !strcmp(ie, "dma")) kernel_ingest = false;
+        if (ie && !strcmp(ie, "kernel")) kernel_ingest = true;
         for (uint32_t m = 0; m < k && kernel_ingest; ++m) {
             hipPointerAttribute_t a;
             if (hipPointerGetAttributes(&a, run_b(m)) != hipSuccess) {
@@ -610,9 +614,14 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
         d_sl = dbuf<IngestSlice>(ctx, "gp_slices", P * k);
         HIPCHK(hipMemcpyAsync(d_sl, hsl.data(), P * k * sizeof(IngestSlice), hipMemcpyHostToDevice, ctx->in_stream));
     }
+    // a few hundred ingest workgroups in all: the copies are bound by PCIe, and a grid that filled
+    // every CU (8 per slice: 2,048 at config 3) held the part kernels off the GPU until the whole
+    // input had landed (part 0 finished after 77 ms, parts 1-7 in 3 ms each behind it)
+    uint32_t ibps = std::max<uint32_t>(1, 384 / k);
+    if (const char* be = getenv("SKV_INGEST_BLOCKS")) ibps = std::max<uint32_t>(1, (uint32_t)strtoul(be, nullptr, 10));
     for (uint64_t p = 0; p < P; ++p) {
         if (kernel_ingest) {
-            launch_ingest(ctx->in_stream, d_sl + p * k, k, 8);
+            launch_ingest(ctx->in_stream, d_sl + p * k, k, ibps);
             HIPCHK(hipGetLastError());
         } else {
             for (uint32_t m = 0; m < k; ++m) {

@@ -273,8 +273,9 @@ def test_failure_mid_pipeline_leaves_the_ctx_clean(dev, pipe_env, fail_at):
 
 @pytest.mark.parametrize("parts", [3, 8])
 def test_general_pipeline_pinned_inputs_kernel_ingest(dev, pipe_env, parts):
-    """runs in pinned, device-mapped host memory: the GPU copies each part's slices itself
-    (k_ingest, one launch per part) -- also with run buffers at odd host offsets"""
+    """runs in pinned, device-mapped host memory: with SKV_INGEST=kernel the GPU copies each part's
+    slices itself (k_ingest, one launch per part), by default one DMA copy per slice -- also with
+    run buffers at odd host offsets"""
     torch = pytest.importorskip("torch")
     rng = random.Random(500 + parts)
     streams = _var_streams(rng, 10, 2500, 12000, del_frac=0.15)
@@ -287,8 +288,12 @@ def test_general_pipeline_pinned_inputs_kernel_ingest(dev, pipe_env, parts):
         pinned.append(t)
         pstreams.append((seq, [(t.data_ptr() + skew, len(r))]))
     os.environ["SKV_HOST_PARTS"] = str(parts)
-    for mx in (2048, 20000):
-        got = dev.compact_host_ptrs(pstreams, mx, 0, with_runs=True)
+    for mode, mx in (("kernel", 2048), ("kernel", 20000), ("dma", 2048)):
+        os.environ["SKV_INGEST"] = mode
+        try:
+            got = dev.compact_host_ptrs(pstreams, mx, 0, with_runs=True)
+        finally:
+            os.environ.pop("SKV_INGEST", None)
         assert dev.timings()["host_parts"] == parts
         exp = pyoracle.compact(streams, mx, 0)
         assert [r.data for r in got] == [r.data for r in exp]
