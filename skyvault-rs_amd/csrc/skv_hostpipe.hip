@@ -464,8 +464,9 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     if (job.in_bytes < min_bytes || (job.flags & SKV_SPLIT_BY_TABLE) || job.batch || job.search || job.scan) return SKV_OK;
     if (k == 0 || job.run_ptr.size() != k) return SKV_OK;  // one run per stream
     if (k > (uint32_t)TILE_TARGET / 2) return SKV_OK;       // the splitter merge's fan-in per part
-    // parts of ~512 MiB: each part costs k DMA copies (config 3, 4 GiB: 8 parts 105 ms, 14 parts 123)
-    uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(32, job.in_bytes / (512ull << 20)));
+    // parts of ~1 GiB: each part costs k DMA copies (config 3, 3.7 GiB: 4 parts 99.8 ms, 6 parts 102.9,
+    // 8 parts 105.0, 10 parts 110.5)
+    uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(32, job.in_bytes / (1ull << 30)));
     if (const char* pp = getenv("SKV_HOST_PARTS")) P = std::max<uint64_t>(1, std::min<uint64_t>(256, strtoull(pp, nullptr, 10)));
     // the open run is carried into every part: keep it small against a part
     if (P < 2 || job.max_run_size > job.in_bytes / (4 * P)) return SKV_OK;
