@@ -262,13 +262,15 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     runs.resize(job.run_ptr.size());  // same size as the last call: no fill
     std::vector<uint32_t>& stream_first_run = ctx->s_sfr;
     stream_first_run.resize(k + 1);
-    // speculative walk length: CHUNK, doubled up to 4x while a call still has >= 2^20 walks (a big
-    // call spends fewer re-synchronising starts per record; 4 KiB walks of 64 GB: 56 ms, 16 KiB: 44)
+    // speculative walk length: CHUNK, doubled up to 64 KiB while a call still has >= 2^16 walks (a
+    // big call spends fewer re-synchronising starts per record). Parse of config 3 shapes by walk
+    // length (tools/stage_probe.py): 59 GiB 16/32/64 KiB 30.3/26.4/25.2 ms; 3.7 GiB 4/16/32/64 KiB
+    // 3.59/2.27/2.14/2.34; 0.23 GiB 4/8/16 KiB 0.50/0.49/0.53; 0.06 GiB 4/16 KiB 0.38/0.47
     uint64_t chunk = CHUNK;
     if (const char* ce = getenv("SKV_CHUNK_BYTES"))  // slot offsets are 16-bit: at most 64 KiB
         chunk = std::min<uint64_t>(65536, std::max<uint64_t>(CHUNK, strtoull(ce, nullptr, 10)));
     else
-        while (chunk < 4 * CHUNK && job.in_bytes / (2 * chunk) >= (1ull << 20)) chunk *= 2;
+        while (chunk < 65536 && job.in_bytes / (2 * chunk) >= (1ull << 16)) chunk *= 2;
     auto n_chunks_of = [chunk](uint64_t len) { return len >= 2 ? (uint32_t)((len - 1 + chunk - 1) / chunk) : 0u; };
     uint64_t n_chunks = 0;
     {  // blocks of streams (rank order) on host threads: runs and chunks before each block, then fill

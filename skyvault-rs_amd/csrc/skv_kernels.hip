@@ -361,7 +361,10 @@ __device__ __forceinline__ void put_rec(uint64_t o, const uint8_t* rp, const Rec
 // starts in its slot row, so EM_G lanes per chunk parse one record each with independent loads and
 // store consecutive records side by side; a chunk with more records than slots is walked by one
 // lane from its validated start.
-constexpr uint32_t EM_G = 16;  // lanes per chunk
+#ifndef SKV_EM_G
+#define SKV_EM_G 16
+#endif
+constexpr uint32_t EM_G = SKV_EM_G;  // lanes per chunk
 __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
                        const RunFmt* __restrict__ fmt, const uint32_t* __restrict__ run_broken,
                        const uint64_t* __restrict__ ch_start, const uint64_t* __restrict__ ch_rec_base,

@@ -315,9 +315,9 @@ def test_corruption_at_every_position_class(dev):
     assert not bad, bad[:5]
 
 
-@pytest.mark.parametrize("chunk", [8192, 12288, 16384])
+@pytest.mark.parametrize("chunk", [8192, 12288, 16384, 32768, 65536])
 def test_longer_speculative_walks(dev, chunk):
-    """Big calls walk 8-16 KiB per speculative chunk (skv_compact.hip picks the length from the call
+    """Big calls walk 8-64 KiB per speculative chunk (skv_compact.hip picks the length from the call
     size); SKV_CHUNK_BYTES forces a length on small inputs: fake records in values, records
     spanning chunks, and corruption everywhere must still give the reference's outcome."""
     old = os.environ.get("SKV_CHUNK_BYTES")

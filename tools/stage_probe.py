@@ -17,9 +17,11 @@ from skv.devgen import make_cfg3_full_on_device  # noqa: E402
 
 def main():
     args = sys.argv[1:]
-    run_mib = 16
+    run_mib, n_streams = 16, 256
     if args and args[0] == "--run-mib":
         run_mib, args = int(args[1]), args[2:]
+    if args and args[0] == "--streams":
+        n_streams, args = int(args[1]), args[2:]
     host_gen = bool(args) and args[0] == "--host-gen"  # gen.config3's runs (bench --config 3's data)
     if host_gen:
         args = args[1:]
@@ -29,13 +31,13 @@ def main():
         from skv import gen
         n = (run_mib << 20) // 333
         runs = []
-        for s in range(256):
-            r = gen.var_key_run(gen.BASE_SEED + s, n, n * 256 * 2, 256)
+        for s in range(n_streams):
+            r = gen.var_key_run(gen.BASE_SEED + s, n, n * n_streams * 2, 256)
             runs.append(torch.from_numpy(r).to(dev))
             if s % 32 == 31:
                 print(f"  generated {s + 1} runs", flush=True)
     else:
-        runs = make_cfg3_full_on_device(dev, 0x5EEDC0DE, 256, run_mib)
+        runs = make_cfg3_full_on_device(dev, 0x5EEDC0DE, n_streams, run_mib)
     print(f"built {sum(r.numel() for r in runs) / 2**30:.2f} GiB in {time.time() - t0:.1f} s", flush=True)
     table = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(runs)]
     comp = Compactor(0, profiling=True)
