@@ -545,7 +545,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         stream_tables();
         alloc_records();
         launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, any_fixed ? R : 0,
-                    rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad, ch_slots, slot_cap, chunk);
+                    rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad, ch_slots, slot_cap, chunk,
+                    ch_end);
         mark(ctx, PH_PARSE);
         check_and_read(false);
         if (utf8_flag && !ctx->exact_utf8) {  // a key the chunk walks did not check: exact walks

@@ -371,7 +371,7 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
                        uint64_t* __restrict__ rec_addr, uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
                        uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags,
                        uint64_t* __restrict__ rec_fp, uint32_t* utf8_bad, const uint16_t* __restrict__ slots,
-                       uint32_t cap, uint64_t chunk) {
+                       uint32_t cap, uint64_t chunk, const uint64_t* __restrict__ ch_end) {
     const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t c = gi / EM_G;
     const uint32_t j0 = (uint32_t)(gi % EM_G);
@@ -403,10 +403,35 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
     }
     const uint64_t cs = 1 + (c - runs[r].chunk_base) * chunk;
     const uint16_t* sl = slots + c * cap;
-    for (uint64_t i = j0; i < cnt; i += EM_G) {
+    // A record's size is the distance to the next record start (the next slot, or the walk's end:
+    // the first start past the chunk, or the failing record of an error chunk), so the emit reads
+    // no value length: per record one 32-byte header window, then the key tail for the fingerprint.
+    // Two records per lane per step, their loads issued together.
+    const uint64_t cend = ch_end[c];
+    auto hdr = [&](uint64_t p, uint64_t pn) {
+        RecHdr h;
+        uint32_t w[8];
+        window32(run, len, p, w);
+        h.marker = w[0] & 0xFFu;
+        h.err = 0;
+        h.klen = __builtin_bswap32(__builtin_amdgcn_alignbyte(w[1], w[0], 1));
+        uint32_t kd[7];
+        win_key(w, kd);
+        win_prefix(kd, h.klen, h.hi, h.lo);
+        h.size = pn - p;
+        return h;
+    };
+    for (uint64_t i = j0; i < cnt; i += 2 * EM_G) {
+        const uint64_t i2 = i + EM_G;
+        const bool two = i2 < cnt;
         const uint64_t p = cs + sl[i];
-        if (p >= len) continue;  // never: every counted record's start is in its slot
-        emit(i, p, parse_rec<true, false>(run, len, p));
+        const uint64_t pn = i + 1 < cnt ? cs + sl[i + 1] : cend;
+        const uint64_t q = two ? cs + sl[i2] : p;
+        const uint64_t qn = two ? (i2 + 1 < cnt ? cs + sl[i2 + 1] : cend) : pn;
+        const RecHdr ha = hdr(p, pn);
+        const RecHdr hb = hdr(q, qn);
+        emit(i, p, ha);
+        if (two) emit(i2, q, hb);
     }
 }
 
@@ -2558,11 +2583,11 @@ void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n
                  const uint32_t* run_broken, const uint64_t* ch_start, const uint64_t* ch_rec_base,
                  const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                  uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, uint64_t* rec_fp, uint32_t* utf8_bad,
-                 const uint16_t* slots, uint32_t cap, uint64_t chunk) {
+                 const uint16_t* slots, uint32_t cap, uint64_t chunk, const uint64_t* ch_end) {
     if (n_chunks)
         k_emit<<<blocks_for(n_chunks * EM_G, 256), 256, 0, s>>>(runs, n_runs, n_chunks, fmt, run_broken, ch_start,
                                                                 ch_rec_base, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
-                                                                flags, rec_fp, utf8_bad, slots, cap, chunk);
+                                                                flags, rec_fp, utf8_bad, slots, cap, chunk, ch_end);
     if (R)
         k_emit_fixed<false><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, nullptr, R, fmt, (uint32_t*)run_broken, run_recb,
                                                                rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags,
