@@ -35,7 +35,8 @@
 extern "C" {
 #endif
 
-#define SKV_ABI_VERSION 4  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts; 4: skv_scan_runs */
+#define SKV_ABI_VERSION 5  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts; 4: skv_scan_runs;
+                              5: skv_timings.span_parse (was reserved) */
 
 typedef struct skv_ctx skv_ctx;
 
@@ -135,7 +136,8 @@ typedef struct {
                                 call was rerun with exact key compares (a 64-bit collision) */
     uint32_t host_parts;     /* skv_compact: key-range parts whose H2D, kernels and D2H overlapped
                                 (0: the serial copy -> compact -> copy) */
-    uint32_t reserved;
+    uint32_t span_parse;     /* general path: 1 the one-pass span parse produced the record arrays;
+                                2 | fail_bits << 8: it declined and the chunk-walk parse ran; 0 not tried */
 } skv_timings;
 
 /* skv_timings.path */

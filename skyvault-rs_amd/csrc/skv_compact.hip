@@ -266,8 +266,14 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // big call spends fewer re-synchronising starts per record). Parse of config 3 shapes by walk
     // length (tools/stage_probe.py): 59 GiB 16/32/64 KiB 30.3/26.4/25.2 ms; 3.7 GiB 4/16/32/64 KiB
     // 3.59/2.27/2.14/2.34; 0.23 GiB 4/8/16 KiB 0.50/0.49/0.53; 0.06 GiB 4/16 KiB 0.38/0.47
+    // the one-pass span parse (skv_span.hip) walks SPAN_BYTES spans; the chunk-walk parse behind it
+    // (its fallback, or SKV_SPAN=0) then uses the same chunking
+    const char* spe = getenv("SKV_SPAN");
+    const bool use_span = !(spe && spe[0] == '0');
     uint64_t chunk = CHUNK;
-    if (const char* ce = getenv("SKV_CHUNK_BYTES"))  // slot offsets are 16-bit: at most 64 KiB
+    if (use_span)
+        chunk = SPAN_BYTES;
+    else if (const char* ce = getenv("SKV_CHUNK_BYTES"))  // slot offsets are 16-bit: at most 64 KiB
         chunk = std::min<uint64_t>(65536, std::max<uint64_t>(CHUNK, strtoull(ce, nullptr, 10)));
     else
         while (chunk < 65536 && job.in_bytes / (2 * chunk) >= (1ull << 16)) chunk *= 2;
@@ -433,6 +439,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // ---- fast path: every run fixed-stride (one record size per run) -> one verifying pass ------
     bool parsed = false, deferred = false;
     bool any_fixed = false;  // some run is fixed-stride: the general parse also runs k_emit_fixed
+    uint64_t first_sum = 0, first_n = 0;  // the runs' first-record sizes (record capacity of the span parse)
+    bool any_bodyless = false;            // a run of only a version byte (no span: the chunk-walk parse)
     {
         RunFmt* hf = (RunFmt*)pinned(ctx, (size_t)n_runs * sizeof(RunFmt) + 16);
         d2h(ctx, hf, d_fmt, (size_t)n_runs * sizeof(RunFmt));
@@ -442,18 +450,31 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         htrace("run formats read");
         // blocks of runs on host threads: every run fixed-stride? one format everywhere?
         const unsigned nbr = par_nblocks(n_runs);
-        std::vector<uint8_t> blk_fixed(nbr, 1), blk_uni(nbr, 1), blk_any(nbr, 0);
+        std::vector<uint8_t> blk_fixed(nbr, 1), blk_uni(nbr, 1), blk_any(nbr, 0), blk_empty(nbr, 0);
+        std::vector<uint64_t> blk_fs(nbr, 0), blk_fn(nbr, 0);
         par_run(n_runs, nbr, [&](unsigned b, uint64_t lo, uint64_t hi) {
-            bool fx = true, un = true, an = false;
+            bool fx = true, un = true, an = false, em = false;
+            uint64_t fs = 0, fc = 0;
             for (uint64_t r = lo; r < hi; ++r) {
                 fx = fx && hf[r].S != 0;
                 an = an || hf[r].S != 0;
                 un = un && hf[r].S == hf[0].S && hf[r].K == hf[0].K;
+                em = em || runs[r].n_chunks == 0;
+                fs += hf[r].first;
+                fc += hf[r].first != 0;
             }
             blk_fixed[b] = fx;
             blk_uni[b] = un;
             blk_any[b] = an;
+            blk_empty[b] = em;
+            blk_fs[b] = fs;
+            blk_fn[b] = fc;
         });
+        for (unsigned b = 0; b < nbr; ++b) {
+            first_sum += blk_fs[b];
+            first_n += blk_fn[b];
+            any_bodyless = any_bodyless || blk_empty[b];
+        }
         bool all_fixed = n_runs > 0, uniform = true;
         for (unsigned b = 0; b < nbr; ++b) {
             all_fixed = all_fixed && blk_fixed[b];
@@ -513,6 +534,56 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                 any_err = false;
                 std::fill(stream_err.begin(), stream_err.end(), 0u);
             }
+        }
+    }
+    // ---- general path, one pass: spans staged in LDS (skv_span.hip) -----------------------------
+    uint32_t span_state = 0;
+    if (!parsed && use_span && n_chunks && !any_bodyless) {
+        const double mean = first_n ? std::max(5.0, (double)first_sum / (double)first_n) : 64.0;
+        const uint64_t cap = std::min<uint64_t>(job.in_bytes / 5 + 1, (uint64_t)(job.in_bytes / mean * 1.5) + 65536);
+        SpanOut so{};
+        so.rec_addr = dbuf<uint64_t>(ctx, "rec_addr", cap);
+        so.rec_hi = dbuf<uint64_t>(ctx, "rec_hi", cap);
+        so.rec_lo = dbuf<uint64_t>(ctx, "rec_lo", cap);
+        so.rec_klen = dbuf<uint32_t>(ctx, "rec_klen", cap);
+        so.rec_meta = dbuf<uint32_t>(ctx, "rec_meta", cap);
+        so.rec_fp = dbuf<uint64_t>(ctx, "rec_fp", cap);
+        so.run_recb = d_recb;
+        so.first = dbuf<uint64_t>(ctx, "span_first", n_chunks);
+        so.exit = dbuf<uint64_t>(ctx, "span_exit", n_chunks);
+        so.tstate = dbuf<uint64_t>(ctx, "span_state", n_chunks);
+        uint32_t* sw = dbuf<uint32_t>(ctx, "span_words", 2);
+        so.ticket = sw;
+        so.fail = sw + 1;
+        so.hdr_err = d_hdr;
+        so.cap = cap;
+        HIPCHK(hipMemsetAsync(so.tstate, 0, n_chunks * 8, st));
+        HIPCHK(hipMemsetAsync(sw, 0, 8, st));
+        launch_span_parse(st, d_runs, n_runs, n_chunks, so);
+        HIPCHK(hipGetLastError());
+        std::vector<uint64_t>& recb = ctx->s_recb;
+        recb.resize(n_runs + 1);
+        uint8_t* hp = (uint8_t*)pinned(ctx, (n_runs + 1) * 8 + 16);
+        d2h(ctx, hp, so.fail, 4);
+        d2h(ctx, hp + 16, d_recb, (n_runs + 1) * 8);
+        sync(ctx);
+        uint32_t fail;
+        memcpy(&fail, hp, 4);
+        span_state = fail ? 2u | (fail << 8) : 1u;
+        ctx->timings.span_parse = span_state;
+        htrace(fail ? "span parse declined" : "span parse done");
+        if (!fail) {
+            memcpy(recb.data(), hp + 16, (n_runs + 1) * 8);
+            R = recb[n_runs];
+            par_run(n_runs, par_nblocks(n_runs), [&](unsigned, uint64_t lo, uint64_t hi) {
+                for (uint64_t r = lo; r < hi; ++r) sum[r] = RunSummary{recb[r + 1] - recb[r], 0u, 0u};
+            });
+            stream_tables();
+            alloc_records();
+            rec_addr = so.rec_addr;
+            mark(ctx, PH_PARSE);
+            check_and_read(false);
+            parsed = true;
         }
     }
     // ---- general path: speculative chunk walks ----------------------------------------------
@@ -1178,7 +1249,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         t.gather_write_bytes = kept_bytes + n_out_runs;
         t.hot_ms = ms[PH_GATHER];
     }
-    ctx->timings.path = parsed ? SKV_PATH_FIXED : SKV_PATH_GENERAL;
+    ctx->timings.path = parsed && span_state != 1 ? SKV_PATH_FIXED : SKV_PATH_GENERAL;
     ctx->timings.hot_read_bytes = kept_bytes;
     ctx->timings.hot_write_bytes = kept_bytes + n_out_runs;
     ctx->timings.host_syncs = ctx->syncs;

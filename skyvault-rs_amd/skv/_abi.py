@@ -112,7 +112,7 @@ class SkvTimings(C.Structure):
         ("sorted", C.c_uint32),
         ("fp_rerun", C.c_uint32),
         ("host_parts", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("span_parse", C.c_uint32),
     ]
 
 

@@ -52,12 +52,14 @@ def main():
             t = comp.timings()
             if i:
                 res.append((t["parse_ms"], t["total_ms"]))
+            span = t["span_parse"]
         for k, o in old.items():
             if o is None:
                 os.environ.pop(k)
             else:
                 os.environ[k] = o
-        print(f"{v:40s} parse {min(p for p, _ in res):7.2f} ms  total {min(t for _, t in res):7.2f} ms", flush=True)
+        print(f"{v:40s} parse {min(p for p, _ in res):7.2f} ms  total {min(t for _, t in res):7.2f} ms"
+              f"  span_parse {span:#x}", flush=True)
 
 
 if __name__ == "__main__":
