@@ -40,6 +40,7 @@ int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, con
     int64_t* tid = dbuf<int64_t>(ctx, "w_tid", K + 1);
     uint32_t* strip = dbuf<uint32_t>(ctx, "w_strip", K + 1);
     uint8_t* canon = dbuf<uint8_t>(ctx, "w_canon", K + 1);
+    uint32_t* wnk = dbuf<uint32_t>(ctx, "w_nk", K + 1);
     uint64_t* wsize = dbuf<uint64_t>(ctx, "w_size", K + 1);
     uint64_t* is_new = dbuf<uint64_t>(ctx, "w_new", K + 1);
     uint64_t* new_ex = dbuf<uint64_t>(ctx, "w_new_ex", K + 1);
@@ -62,8 +63,8 @@ int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, con
     HIPCHK(hipMemsetAsync(tbad, 0, (K + 1) * 4, st));
     // run_len / keep: k_wal_tables writes the first NT (the table count, on the device) and the
     // scans below read no further
-    launch_wal_keys(st, d_K, K, m_src, m_rec, rec_klen, m_P, tid, strip, wsize, canon, first_err);
-    launch_wal_flags(st, d_K, K, tid, strip, canon, m_src, m_rec, rec_klen, is_new, bad, heap != nullptr);
+    launch_wal_keys(st, d_K, K, m_src, m_P, tid, strip, wnk, wsize, canon, first_err);
+    launch_wal_flags(st, d_K, K, tid, strip, canon, m_src, wnk, is_new, bad, heap != nullptr);
     launch_scan(st, is_new, K, new_ex, scan_tmp);  // new_ex[K] = number of tables
     launch_wal_index(st, d_K, K, is_new, new_ex, bad, tix, tstart, tbad, tfirst);
     launch_wal_sendfail(st, new_ex + K, K, tstart, tfirst, first_err + 1);
@@ -72,9 +73,9 @@ int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, con
     launch_wal_tables(st, d_NT, K, tstart, Pw, tbad, job.max_run_size, run_len, keep);
     launch_scan_dn(st, run_len, d_NT, K, run_off, scan_tmp);  // output offset per table, total at [K]
     launch_scan_dn(st, keep, d_NT, K, keep_ex, scan_tmp);     // run index per kept table, count at [K]
-    launch_wal_desc(st, d_NT, K, tstart, Pw, m_Dp, keep, keep_ex, run_off, tid, strip, m_rec, rec_klen, d_desc);
+    launch_wal_desc(st, d_NT, K, tstart, Pw, m_Dp, keep, keep_ex, run_off, tid, wnk, d_desc);
     mark(ctx, PH_CHAIN);
-    launch_wal_gather(st, d_K, K, tix, tstart, keep, run_off, Pw, strip, m_src, m_rec, rec_klen, d_out);
+    launch_wal_gather(st, d_K, K, tix, tstart, keep, run_off, Pw, strip, m_src, wnk, canon, d_out);
     HIPCHK(hipGetLastError());
     mark(ctx, PH_GATHER);
     uint64_t h[5];
@@ -206,7 +207,8 @@ SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth, uint6
 // tiles x streams). hi/lo/cmp_klen become dense key ranks for the merge stage; klen stays the real
 // key length (descriptors, WAL split).
 void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo, uint64_t*& addr, uint32_t*& klen,
-                         uint32_t*& meta, const uint32_t*& cmp_klen, bool last_wins, const SElem** sorted) {
+                         uint32_t*& meta, const uint32_t*& cmp_klen, bool last_wins, const SElem** sorted,
+                         uint32_t const_meta) {
     hipStream_t st = ctx->stream;
     SElem* E = dbuf<SElem>(ctx, "sort_e", R);
     SElem* T = dbuf<SElem>(ctx, "sort_t", R);
@@ -222,7 +224,7 @@ void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo, uint64
     uint32_t* nklen = dbuf<uint32_t>(ctx, "srt_klen", R);
     uint32_t* ncklen = dbuf<uint32_t>(ctx, "srt_cklen", R);
     uint32_t* nmeta = dbuf<uint32_t>(ctx, "srt_meta", R);
-    launch_sort_store(st, R, S, meta, newkey, newkey_ex, nhi, nlo, naddr, nklen, ncklen, nmeta, last_wins);
+    launch_sort_store(st, R, S, meta, const_meta, newkey, newkey_ex, nhi, nlo, naddr, nklen, ncklen, nmeta, last_wins);
     HIPCHK(hipGetLastError());
     if (sorted) *sorted = S;
     hi = nhi;
@@ -268,8 +270,9 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // 3.59/2.27/2.14/2.34; 0.23 GiB 4/8/16 KiB 0.50/0.49/0.53; 0.06 GiB 4/16 KiB 0.38/0.47
     // the one-pass span parse (skv_span.hip) walks SPAN_BYTES spans; the chunk-walk parse behind it
     // (its fallback, or SKV_SPAN=0) then uses the same chunking
+    // off by default: measured slower than the chunk walks; SKV_SPAN=1 runs it
     const char* spe = getenv("SKV_SPAN");
-    const bool use_span = !(spe && spe[0] == '0');
+    const bool use_span = spe && spe[0] == '1';
     uint64_t chunk = CHUNK;
     if (use_span)
         chunk = SPAN_BYTES;
@@ -439,6 +442,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // ---- fast path: every run fixed-stride (one record size per run) -> one verifying pass ------
     bool parsed = false, deferred = false;
     bool any_fixed = false;  // some run is fixed-stride: the general parse also runs k_emit_fixed
+    uint32_t uniform_meta = 0;  // every record a Put of one size (the fixed path's runs, one format): its meta
     uint64_t first_sum = 0, first_n = 0;  // the runs' first-record sizes (record capacity of the span parse)
     bool any_bodyless = false;            // a run of only a version byte (no span: the chunk-walk parse)
     {
@@ -529,6 +533,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                 parsed = !check_and_read(true);
                 htrace("parse verdict read");
             }
+            // one size everywhere and no Delete among the records (read with the verdict): one meta
+            if (parsed && !deferred && uniform && !(hflags[3] & 1u)) uniform_meta = (uint32_t)f0.S;
             if (!parsed) {  // a run is not what its first record promised: general parse
                 R = 0;
                 any_err = false;
@@ -552,19 +558,25 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         so.first = dbuf<uint64_t>(ctx, "span_first", n_chunks);
         so.exit = dbuf<uint64_t>(ctx, "span_exit", n_chunks);
         so.tstate = dbuf<uint64_t>(ctx, "span_state", n_chunks);
-        uint32_t* sw = dbuf<uint32_t>(ctx, "span_words", 2);
+        uint32_t* sw = dbuf<uint32_t>(ctx, "span_words", 32);
         so.ticket = sw;
         so.fail = sw + 1;
         so.hdr_err = d_hdr;
         so.cap = cap;
         HIPCHK(hipMemsetAsync(so.tstate, 0, n_chunks * 8, st));
-        HIPCHK(hipMemsetAsync(sw, 0, 8, st));
+        HIPCHK(hipMemsetAsync(sw, 0, 128, st));
+        {
+            const char* dg = getenv("SKV_SPAN_DBG");
+            so.dbg = dg && dg[0] == '1' ? sw + 2 : nullptr;
+        }
         launch_span_parse(st, d_runs, n_runs, n_chunks, so);
         HIPCHK(hipGetLastError());
         std::vector<uint64_t>& recb = ctx->s_recb;
         recb.resize(n_runs + 1);
         uint8_t* hp = (uint8_t*)pinned(ctx, (n_runs + 1) * 8 + 16);
         d2h(ctx, hp, so.fail, 4);
+        uint64_t dbgw[16] = {};
+        if (so.dbg) d2h(ctx, (uint8_t*)dbgw, sw, 128);
         d2h(ctx, hp + 16, d_recb, (n_runs + 1) * 8);
         sync(ctx);
         uint32_t fail;
@@ -572,6 +584,10 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         span_state = fail ? 2u | (fail << 8) : 1u;
         ctx->timings.span_parse = span_state;
         htrace(fail ? "span parse declined" : "span parse done");
+        if (so.dbg)
+            fprintf(stderr, "[span] spans %lu fail %#x ticks/span: stage %.0f walk %.0f lookback %.0f emit %.0f\n",
+                    (unsigned long)n_chunks, fail, (double)dbgw[4] / n_chunks, (double)dbgw[5] / n_chunks,
+                    (double)dbgw[6] / n_chunks, (double)dbgw[7] / n_chunks);
         if (!fail) {
             memcpy(recb.data(), hp + 16, (n_runs + 1) * 8);
             R = recb[n_runs];
@@ -834,7 +850,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                 uint32_t* m2 = rec_meta;
                 const uint32_t* ck = nullptr;
                 const SElem* S = nullptr;
-                sort_records(ctx, R, h2, l2, a2, k2, m2, ck, false, &S);
+                sort_records(ctx, R, h2, l2, a2, k2, m2, ck, false, &S, 0);
                 uint64_t* shi = dbuf<uint64_t>(ctx, "heap_s_hi", R);
                 uint64_t* slo = dbuf<uint64_t>(ctx, "heap_s_lo", R);
                 uint32_t* skl = dbuf<uint32_t>(ctx, "heap_s_klen", R);
@@ -852,7 +868,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                 cmp_klen = ck;
                 hres.inv = inv;
             } else {
-                sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen, job.batch);
+                sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen, job.batch, nullptr,
+                             uniform_meta);
                 cmp_hi = rec_hi;
                 cmp_lo = rec_lo;
                 cmp_addr = rec_addr;

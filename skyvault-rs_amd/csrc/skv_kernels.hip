@@ -508,6 +508,9 @@ __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, 
                     key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii));
         }
     }
+    // a Delete of the run's record size (k_run_header's hypothesis is a Put): flags[3] bit 0, so
+    // the host does not take one meta for every record (k_sort_store's const_meta)
+    if (VERIFY && __ballot(act && h.marker == 2) && (threadIdx.x & 63) == 0) atomicOr(flags + 3, 1u);
     if (!VERIFY || !first_dec) return;  // (no order check for a writer batch)
     // fused order check (runs.rs:190-198 as k_order_check does it): compare with the previous
     // record of the same stream — the neighbouring lane's, or parsed here at a run / wave edge

@@ -61,12 +61,12 @@ void launch_run_stats(hipStream_t, const uint64_t* n_runs, const uint64_t* run_b
 void launch_gather(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
                    const uint64_t* m_src, const uint64_t* seg_r0, uint8_t* out, uint64_t max_K);
 // skv_wal.hip — SKV_SPLIT_BY_TABLE (wal_compaction.rs:66-174)
-void launch_wal_keys(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint32_t* m_rec,
-                     const uint32_t* rec_klen, const uint64_t* P, int64_t* tid, uint32_t* strip, uint64_t* wsize,
-                     uint8_t* canon, unsigned long long* first_err);
+void launch_wal_keys(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,
+                     int64_t* tid, uint32_t* strip, uint32_t* wnk, uint64_t* wsize, uint8_t* canon,
+                     unsigned long long* first_err);
 void launch_wal_flags(hipStream_t, const uint64_t* Kp, uint64_t max_K, const int64_t* tid, const uint32_t* strip,
-                      const uint8_t* canon, const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen,
-                      uint64_t* is_new, uint32_t* bad, bool exact);
+                      const uint8_t* canon, const uint64_t* m_src, const uint32_t* wnk, uint64_t* is_new,
+                      uint32_t* bad, bool exact);
 void launch_wal_index(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint64_t* is_new, const uint64_t* new_ex,
                       const uint32_t* bad, uint32_t* tix, uint64_t* tstart, uint32_t* tbad,
                       unsigned long long* tfirst);
@@ -74,11 +74,10 @@ void launch_wal_tables(hipStream_t, const uint64_t* NTp, uint64_t max_NT, const 
                        const uint32_t* tbad, uint64_t max_size, uint64_t* run_len, uint64_t* keep);
 void launch_wal_desc(hipStream_t, const uint64_t* NTp, uint64_t max_NT, const uint64_t* tstart, const uint64_t* Pw,
                      const uint64_t* Dp, const uint64_t* keep, const uint64_t* keep_ex, const uint64_t* run_off,
-                     const int64_t* tid, const uint32_t* strip, const uint32_t* m_rec, const uint32_t* rec_klen,
-                     DevRunDesc* descs);
+                     const int64_t* tid, const uint32_t* wnk, DevRunDesc* descs);
 void launch_wal_gather(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint32_t* tix, const uint64_t* tstart,
                        const uint64_t* keep, const uint64_t* run_off, const uint64_t* Pw, const uint32_t* strip,
-                       const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen, uint8_t* out);
+                       const uint64_t* m_src, const uint32_t* wnk, const uint8_t* canon, uint8_t* out);
 void launch_page_prep(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
                       const uint64_t* seg_r0, uint64_t* Dst, uint32_t* page_first, uint64_t max_K);
 void launch_gather_pages(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* P, const uint64_t* Dst,
@@ -116,9 +115,9 @@ void launch_copy_bytes(hipStream_t, uint8_t* dst, const uint8_t* src, uint64_t n
 // skv_sort.hip — record sort (fan-in above TILE_TARGET / 2)
 void launch_sort_load(hipStream_t, uint64_t R, const uint64_t* hi, const uint64_t* lo, const uint64_t* addr,
                       const uint32_t* klen, SElem* E, bool last_wins);
-void launch_sort_store(hipStream_t, uint64_t R, const SElem* E, const uint32_t* meta_in, const uint64_t* newkey,
-                       const uint64_t* newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr, uint32_t* klen,
-                       uint32_t* cmp_klen, uint32_t* meta, bool last_wins);
+void launch_sort_store(hipStream_t, uint64_t R, const SElem* E, const uint32_t* meta_in, uint32_t const_meta,
+                       const uint64_t* newkey, const uint64_t* newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr,
+                       uint32_t* klen, uint32_t* cmp_klen, uint32_t* meta, bool last_wins);
 void launch_sort_sample(hipStream_t, const SElem* E, uint64_t n, uint64_t Ns, SElem* S);
 void launch_sort_prefix(hipStream_t, const SElem* Ss, uint64_t ov, uint64_t Tb, uint32_t* L);
 void launch_sort_bucket(hipStream_t, SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
@@ -171,6 +170,7 @@ struct SpanOut {
     uint32_t* fail;          // SPF_* bits: any -> the chunk-walk parse runs instead (zeroed per call)
     const uint32_t* hdr_err; // k_run_header's verdict per run
     uint64_t cap;            // entries the record arrays hold
+    uint32_t* dbg;           // SKV_SPAN_DBG=1: printf the first failing lanes (counter); null: off
 };
 void launch_span_parse(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_spans, const SpanOut& O);
 

@@ -109,10 +109,13 @@ __global__ void k_sort_load(uint64_t R, const uint64_t* __restrict__ hi, const u
 // The record arrays in sorted order (meta follows its record). The merge stage then compares
 // dense key ranks (hi = rank of the key among the distinct keys, lo = 0, compare length 0): the
 // same order and the same equal-key groups as the key bytes, with no key bytes read again.
+// const_meta != 0: every record has that meta (one record format in every run, e.g. WAL flushes
+// of one key/value shape) -- no gather of meta_in at the sorted element's record, a random 4-byte
+// read that fetched a line of its own per record.
 __global__ void k_sort_store(uint64_t R, const SElem* __restrict__ E, const uint32_t* __restrict__ meta_in,
-                             const uint64_t* __restrict__ newkey, const uint64_t* __restrict__ newkey_ex,
-                             uint64_t* hi, uint64_t* lo, uint64_t* addr, uint32_t* klen, uint32_t* cmp_klen,
-                             uint32_t* meta, bool last_wins) {
+                             uint32_t const_meta, const uint64_t* __restrict__ newkey,
+                             const uint64_t* __restrict__ newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr,
+                             uint32_t* klen, uint32_t* cmp_klen, uint32_t* meta, bool last_wins) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= R) return;
     const SElem e = E[i];
@@ -122,7 +125,7 @@ __global__ void k_sort_store(uint64_t R, const SElem* __restrict__ E, const uint
     addr[i] = e.addr;
     klen[i] = e.klen;
     cmp_klen[i] = 0;
-    meta[i] = meta_in[src];
+    meta[i] = const_meta ? const_meta : meta_in[src];
 }
 
 // S[j] = E[j * n / Ns]  (n < 2^32)
@@ -550,12 +553,12 @@ void launch_sort_load(hipStream_t s, uint64_t R, const uint64_t* hi, const uint6
                       const uint32_t* klen, SElem* E, bool last_wins) {
     if (R) k_sort_load<<<sk_blocks(R), 256, 0, s>>>(R, hi, lo, addr, klen, E, last_wins);
 }
-void launch_sort_store(hipStream_t s, uint64_t R, const SElem* E, const uint32_t* meta_in, const uint64_t* newkey,
-                       const uint64_t* newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr, uint32_t* klen,
-                       uint32_t* cmp_klen, uint32_t* meta, bool last_wins) {
+void launch_sort_store(hipStream_t s, uint64_t R, const SElem* E, const uint32_t* meta_in, uint32_t const_meta,
+                       const uint64_t* newkey, const uint64_t* newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr,
+                       uint32_t* klen, uint32_t* cmp_klen, uint32_t* meta, bool last_wins) {
     if (R)
-        k_sort_store<<<sk_blocks(R), 256, 0, s>>>(R, E, meta_in, newkey, newkey_ex, hi, lo, addr, klen, cmp_klen, meta,
-                                                  last_wins);
+        k_sort_store<<<sk_blocks(R), 256, 0, s>>>(R, E, meta_in, const_meta, newkey, newkey_ex, hi, lo, addr, klen,
+                                                  cmp_klen, meta, last_wins);
 }
 void launch_sort_sample(hipStream_t s, const SElem* E, uint64_t n, uint64_t Ns, SElem* S) {
     if (Ns) k_sort_sample<<<sk_blocks(Ns), 256, 0, s>>>(E, n, Ns, S);

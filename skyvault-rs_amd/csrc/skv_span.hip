@@ -15,9 +15,10 @@
 //   4. parses its records again from LDS (prefix, key length, size | Delete, fingerprint of the key
 //      bytes past 16, exact UTF-8) and writes the record arrays at their final indices.
 // A span's speculative first start is checked against the previous span's exit by k_span_check.
-// Anything unusual -- a decode error, an invalid UTF-8 key, a lane that started off the record
-// chain, a span in which no record starts (records longer than a span), more records than the
-// arrays hold -- sets a fail bit, and the host runs the chunk-walk parse instead, which reproduces
+// A span in which no record starts (a run's short tail, or inside a record longer than a span) is
+// checked to lie inside the record that crosses it. Anything unusual -- a decode error, an invalid
+// UTF-8 key, a lane that started off the record chain, more records than the arrays hold -- sets a
+// fail bit, and the host runs the chunk-walk parse instead, which reproduces
 // the reference's exact error. Only a clean decode of every run is taken from here.
 #include "skv_dev.hpp"
 #include "skv_launch.hpp"
@@ -33,7 +34,7 @@ constexpr uint32_t SPAN_BLOCKS = (SPAN + SPAN_MARGIN) / 16 + 2;  // staged 16-by
 static_assert(SPAN_SUB * 64 == SPAN && SPAN <= 65536, "u16 offsets, 64 walking lanes");
 static_assert(SPAN_LCAP % 8 == 0, "walk_fast stores record starts eight at a time");
 
-enum : uint32_t { SPF_DECODE = 1, SPF_CHAIN = 2, SPF_EMPTY = 4, SPF_OVER = 8, SPF_UTF8 = 16, SPF_CAP = 32 };
+enum : uint32_t { SPF_DECODE = 1, SPF_CHAIN = 2, SPF_OVER = 8, SPF_UTF8 = 16, SPF_CAP = 32 };
 
 // Loads of the record parsers: blocks inside the staged bytes come from LDS, others from HBM
 struct SpanLoad {
@@ -94,6 +95,8 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
     __shared__ uint64_t s_t, s_base;
     __shared__ uint32_t s_fail;
     const uint32_t tid = threadIdx.x;
+    uint64_t* const tk = O.dbg ? (uint64_t*)(O.dbg + 6) : nullptr;  // phase ticks (SKV_SPAN_DBG)
+    uint64_t t0 = tk ? wall_clock64() : 0, t1 = 0, t2 = 0, t3 = 0;
     if (tid == 0) {
         s_t = atomicAdd(O.ticket, 1u);
         s_fail = 0;
@@ -126,6 +129,7 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
     __syncthreads();
     const SpanLoad ld{buf, g0, g1};
     const uint8_t* bytes = (const uint8_t*)buf;
+    if (tk) t1 = wall_clock64();
     // ---- 2. wave 0 walks the span, lane l the records starting in [a, b)
     uint64_t count = 0;
     if (tid < 64) {
@@ -168,7 +172,7 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
             const bool ok = P >= b ? (st >= b) : (st == P);
             if (!ok) fail |= SPF_CHAIN;
         }
-        if (l == 0 && s0 >= ce) fail |= SPF_EMPTY;  // no record starts in this span
+        // no record start in this span (s0 >= ce): fine when a record crosses it (k_span_check)
         // the span's exit: the end of its last record (the lane with records furthest on)
         const int jl = has ? 63 - __builtin_clzll(has) : -1;
         const uint64_t ex = __shfl(e, jl < 0 ? 0 : jl, 64);
@@ -184,6 +188,11 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
         count = __shfl(inc, 63, 64);
         if (l == 0 && O.hdr_err[r]) fail |= SPF_DECODE;  // a bad version byte: the exact path reports it
         if (fail) atomicOr(O.fail, fail);
+        if (O.dbg && fail && atomicAdd(O.dbg, 1u) < 48)
+            printf("span %lu run %u local %lu cs %lu ce %lu len %lu | lane %u a %lu b %lu st %lu e %lu n %u P %lu fail %u\n",
+                   (unsigned long)s, r, (unsigned long)local, (unsigned long)cs, (unsigned long)ce,
+                   (unsigned long)R.len, l, (unsigned long)a, (unsigned long)b, (unsigned long)st,
+                   (unsigned long)e, n, (unsigned long)P, fail);
         const bool any_fail = __ballot(fail != 0) != 0;
         if (l == 0) {
             O.first[s] = s0 < ce ? s0 : NO_POS;
@@ -191,6 +200,7 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
             if (any_fail) s_fail = 1;
         }
         // ---- 3. global index of the span's first record (the look-back needs every span to publish)
+        if (tk) t2 = wall_clock64();
         const uint64_t base = span_lookback(O.tstate, s, count);
         if (l == 0) {
             s_base = base;
@@ -203,6 +213,7 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
         }
     }
     __syncthreads();
+    if (tk) t3 = wall_clock64();
     if (s_fail) return;
     count = pre[64];
     const uint64_t base = s_base;
@@ -236,18 +247,46 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
         O.rec_fp[o] = fpv;
     }
     if (bad) atomicOr(O.fail, bad);
+    if (tk) {
+        __syncthreads();
+        if (tid == 0) {
+            const uint64_t t4 = wall_clock64();
+            atomicAdd((unsigned long long*)&tk[0], (unsigned long long)(t1 - t0));
+            atomicAdd((unsigned long long*)&tk[1], (unsigned long long)(t2 - t1));
+            atomicAdd((unsigned long long*)&tk[2], (unsigned long long)(t3 - t2));
+            atomicAdd((unsigned long long*)&tk[3], (unsigned long long)(t4 - t3));
+        }
+    }
 }
 
-// every span after a run's first starts where its predecessor ended; a run's last span ends at
-// the run's end
+// every span after a run's first starts where the nearest earlier span with records ended; a span
+// with no record start (the tail of a run, or records longer than a span) must lie inside the record
+// that crosses it; a run's last record ends at the run's end
+constexpr uint32_t SPAN_BACK = 64;  // spans a check looks back over (longer records: the chunk walks)
 __global__ void k_span_check(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_spans, SpanOut O) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_spans) return;
     const uint32_t r = span_run(runs, n_runs, s);
     const RunInfo R = runs[r];
     const uint64_t local = s - R.chunk_base;
-    if (local > 0 && O.first[s] != O.exit[s - 1]) atomicOr(O.fail, SPF_CHAIN);
-    if (local + 1 == R.n_chunks && O.exit[s] != R.len) atomicOr(O.fail, SPF_CHAIN);
+    const uint64_t first = O.first[s];
+    bool bad = false;
+    uint64_t pe = 0;  // exit of the nearest earlier span of this run with records
+    if (local > 0) {
+        uint64_t q = s - 1;
+        uint32_t k = 0;
+        while (O.first[q] == NO_POS && q > R.chunk_base && k < SPAN_BACK) --q, ++k;
+        if (O.first[q] == NO_POS) bad = true;  // span 0 of a run always has records: too far back
+        pe = O.exit[q];
+        const uint64_t cs = 1 + local * SPAN, ce = cs + SPAN < R.len ? cs + SPAN : R.len;
+        bad = bad || (first == NO_POS ? pe < ce : first != pe);
+    }
+    if (local + 1 == R.n_chunks) bad = bad || (first == NO_POS ? pe != R.len : O.exit[s] != R.len);
+    if (bad) atomicOr(O.fail, SPF_CHAIN);
+    if (O.dbg && bad && atomicAdd(O.dbg, 1u) < 64)
+        printf("check span %lu run %u local %lu first %lu prev_exit %lu exit %lu len %lu\n", (unsigned long)s, r,
+               (unsigned long)local, (unsigned long)first, (unsigned long)pe, (unsigned long)O.exit[s],
+               (unsigned long)R.len);
 }
 
 void launch_span_parse(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_spans, const SpanOut& O) {

@@ -40,6 +40,35 @@ __device__ __forceinline__ uint32_t parse_i64_dev(const uint8_t* s, uint64_t n, 
     return 0;
 }
 
+// parse_i64_dev over key bytes 0..n-1 (n <= 27) held in a record's first 32 bytes (key at byte 5):
+// the same outcome, read from registers (unrolled, constant indices) instead of byte loads
+__device__ __forceinline__ uint32_t parse_i64_win(const uint32_t hw[8], uint32_t n, int64_t& out) {
+    if (n == 0) return WERR_EMPTY;
+    const uint32_t c0 = (hw[1] >> 8) & 0xFFu;
+    const bool sign = c0 == '+' || c0 == '-';
+    if (sign && n == 1) return WERR_DIGIT;
+    const bool neg = c0 == '-';
+    int64_t r = 0;
+    uint32_t err = 0;
+#pragma unroll
+    for (int i = 0; i < 27; ++i) {
+        if ((uint32_t)i < n && !err && !(i == 0 && sign)) {
+            const uint32_t c = (hw[(i + 5) >> 2] >> (8 * ((i + 5) & 3))) & 0xFFu;
+            if (c < '0' || c > '9') {
+                err = WERR_DIGIT;  // to_digit before the overflow checks
+            } else {
+                int64_t m;
+                const int64_t d = (int64_t)(c - '0');
+                if (__builtin_mul_overflow(r, (int64_t)10, &m) ||
+                    (neg ? __builtin_sub_overflow(m, d, &r) : __builtin_add_overflow(m, d, &r)))
+                    err = neg ? WERR_NEG : WERR_POS;
+            }
+        }
+    }
+    if (!err) out = r;
+    return err;
+}
+
 // byte length of format!("{id}.")
 __device__ __forceinline__ uint32_t id_prefix_len(int64_t id) {
     uint64_t u = id < 0 ? (uint64_t)0 - (uint64_t)id : (uint64_t)id;
@@ -52,19 +81,34 @@ __device__ __forceinline__ uint32_t id_prefix_len(int64_t id) {
 }
 
 // per merged record: table id, strip length, stripped record size; the first bad key (merged
-// order) is the job's InvalidInput error
+// order) is the job's InvalidInput error. The key length and marker come from the record's own
+// header (the line the key is read from), not from rec_klen[m_rec[j]]: that random 4-byte gather
+// fetched a line of its own per merged record. wnk = the stripped key's length, canon bit 1 a Delete.
 __global__ void k_wal_keys(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ m_src,
-                           const uint32_t* __restrict__ m_rec, const uint32_t* __restrict__ rec_klen,
-                           const uint64_t* __restrict__ P, int64_t* tid, uint32_t* strip, uint64_t* wsize,
-                           uint8_t* canon, unsigned long long* first_err) {
+                           const uint64_t* __restrict__ P, int64_t* tid, uint32_t* strip, uint32_t* wnk,
+                           uint64_t* wsize, uint8_t* canon, unsigned long long* first_err) {
     const uint64_t K = *Kp;
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= K) return;
-    const uint8_t* key = (const uint8_t*)m_src[j] + 5;
-    const uint64_t klen = rec_klen[m_rec[j]];
-    // split_once('.'): the first '.', 16 key bytes per load
+    const uint8_t* rp = (const uint8_t*)m_src[j];
+    const uint64_t size = P[j + 1] - P[j];  // the record's bytes: its first min(32, size) in one round trip
+    const uint4 h0 = load_window16(rp, (uint32_t)(size < 16 ? size : 16));
+    const uint4 h1 = size > 16 ? load_window16(rp + 16, (uint32_t)(size - 16 < 16 ? size - 16 : 16)) : make_uint4(0, 0, 0, 0);
+    const uint32_t hw[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    const uint32_t marker = hw[0] & 0xFFu;
+    const uint64_t klen = __builtin_bswap32(__builtin_amdgcn_alignbyte(hw[1], hw[0], 1));
+    const uint8_t* key = rp + 5;
+    // split_once('.'): the first '.' -- key bytes 0..26 from the window, then 16 per load
     uint64_t dot = klen;
-    for (uint64_t o = 0; o < klen; o += 16) {
+    {
+        const uint32_t n0 = (uint32_t)(klen < 27 ? klen : 27);
+        uint32_t hit = 0;
+#pragma unroll
+        for (int i = 0; i < 27; ++i)
+            if (((hw[(i + 5) >> 2] >> (8 * ((i + 5) & 3))) & 0xFFu) == (uint32_t)'.' && (uint32_t)i < n0) hit |= 1u << i;
+        if (hit) dot = __builtin_ctz(hit);
+    }
+    for (uint64_t o = 27; dot == klen && o < klen; o += 16) {
         const uint32_t m = (uint32_t)(klen - o < 16 ? klen - o : 16);
         const uint4 v = load_window16(key + o, m);
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -72,20 +116,18 @@ __global__ void k_wal_keys(const uint64_t* __restrict__ Kp, const uint64_t* __re
 #pragma unroll
         for (int i = 0; i < 16; ++i)
             if (((w[i >> 2] >> (8 * (i & 3))) & 0xFFu) == (uint32_t)'.' && (uint32_t)i < m) hit |= 1u << i;
-        if (hit) {
-            dot = o + __builtin_ctz(hit);
-            break;
-        }
+        if (hit) dot = o + __builtin_ctz(hit);
     }
     int64_t id = 0;
-    uint32_t e = dot == klen ? WERR_NODOT : parse_i64_dev(key, dot, id);
+    uint32_t e = dot == klen ? WERR_NODOT : (dot <= 27 ? parse_i64_win(hw, (uint32_t)dot, id) : parse_i64_dev(key, dot, id));
     uint32_t st = 0;
     if (e) atomicMin(first_err, (unsigned long long)j);
     else st = id_prefix_len(id);
     tid[j] = id;
     strip[j] = st;
-    canon[j] = (!e && dot + 1 == st) ? 1 : 0;  // the prefix is format!("{id}.") itself
-    wsize[j] = (P[j + 1] - P[j]) - st;
+    wnk[j] = (uint32_t)(klen - st);
+    canon[j] = ((!e && dot + 1 == st) ? 1 : 0) | (marker == 2 ? 2 : 0);  // the prefix is format!("{id}.") itself
+    wsize[j] = size - st;
 }
 
 // stripped key of record j: bytes [src+5+strip, src+5+klen)
@@ -102,8 +144,8 @@ __device__ __forceinline__ int stripped_cmp(const uint8_t* a, uint64_t la, const
 // merged keys (strictly ascending): only non-canonical prefixes ("007.", "+5.") compare bytes.
 __global__ void k_wal_flags(const uint64_t* __restrict__ Kp, const int64_t* __restrict__ tid,
                             const uint32_t* __restrict__ strip, const uint8_t* __restrict__ canon,
-                            const uint64_t* __restrict__ m_src, const uint32_t* __restrict__ m_rec,
-                            const uint32_t* __restrict__ rec_klen, uint64_t* is_new, uint32_t* bad, uint32_t exact) {
+                            const uint64_t* __restrict__ m_src, const uint32_t* __restrict__ wnk, uint64_t* is_new,
+                            uint32_t* bad, uint32_t exact) {
     const uint64_t K = *Kp;
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= K) return;
@@ -111,11 +153,11 @@ __global__ void k_wal_flags(const uint64_t* __restrict__ Kp, const int64_t* __re
     is_new[j] = nw ? 1 : 0;
     uint32_t b = 0;
     // (heap-order mode, unsorted inputs: the merged keys are not ascending, compare every pair)
-    if (!nw && (exact || !(canon[j - 1] && canon[j]))) {
+    if (!nw && (exact || !(canon[j - 1] & canon[j] & 1))) {
         const uint64_t sa = strip[j - 1], sb = strip[j];
         const uint8_t* ka = (const uint8_t*)m_src[j - 1] + 5 + sa;
         const uint8_t* kb = (const uint8_t*)m_src[j] + 5 + sb;
-        const uint64_t la = rec_klen[m_rec[j - 1]] - sa, lb = rec_klen[m_rec[j]] - sb;
+        const uint64_t la = wnk[j - 1], lb = wnk[j];
         b = stripped_cmp(ka, la, kb, lb) >= 0 ? 1u : 0u;
     }
     bad[j] = b;
@@ -156,8 +198,7 @@ __global__ void k_wal_desc(const uint64_t* __restrict__ NTp, const uint64_t* __r
                            const uint64_t* __restrict__ Pw, const uint64_t* __restrict__ Dp,
                            const uint64_t* __restrict__ keep, const uint64_t* __restrict__ keep_ex,
                            const uint64_t* __restrict__ run_off, const int64_t* __restrict__ tid,
-                           const uint32_t* __restrict__ strip, const uint32_t* __restrict__ m_rec,
-                           const uint32_t* __restrict__ rec_klen, DevRunDesc* descs) {
+                           const uint32_t* __restrict__ wnk, DevRunDesc* descs) {
     const uint64_t NT = *NTp;
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= NT || !keep[t]) return;
@@ -168,9 +209,9 @@ __global__ void k_wal_desc(const uint64_t* __restrict__ NTp, const uint64_t* __r
     d.delete_count = Dp[e] - Dp[b];
     d.put_count = (e - b) - d.delete_count;
     d.min_key_off = d.off + 1 + 5;
-    d.min_key_len = rec_klen[m_rec[b]] - strip[b];
+    d.min_key_len = wnk[b];
     d.max_key_off = d.off + 1 + (Pw[e - 1] - Pw[b]) + 5;
-    d.max_key_len = rec_klen[m_rec[e - 1]] - strip[e - 1];
+    d.max_key_len = wnk[e - 1];
     d.table_id = tid[b];
     d.reserved = 0;
     descs[keep_ex[t]] = d;
@@ -231,8 +272,8 @@ __global__ void __launch_bounds__(WAL_G) k_wal_gather(const uint64_t* __restrict
                                                       const uint64_t* __restrict__ Pw,
                                                       const uint32_t* __restrict__ strip,
                                                       const uint64_t* __restrict__ m_src,
-                                                      const uint32_t* __restrict__ m_rec,
-                                                      const uint32_t* __restrict__ rec_klen, uint8_t* out) {
+                                                      const uint32_t* __restrict__ wnk,
+                                                      const uint8_t* __restrict__ canon, uint8_t* out) {
     __shared__ uint64_t os[WAL_G + 1], src[WAL_G], head[WAL_G];
     __shared__ uint32_t hl[WAL_G];
     __shared__ uint32_t s_cnt[WAL_G / 64 + 1];
@@ -250,12 +291,12 @@ __global__ void __launch_bounds__(WAL_G) k_wal_gather(const uint64_t* __restrict
             const uint64_t b = tstart[t];
             const uint8_t* sp = (const uint8_t*)m_src[j];
             const uint32_t st = strip[j];
-            const uint32_t nk = rec_klen[m_rec[j]] - st;
+            const uint32_t nk = wnk[j];
             const bool first = j == b;
             ostart = run_off[t] + 1 + (Pw[j] - Pw[b]) - (first ? 1 : 0);
             olen = (Pw[j + 1] - Pw[j]) + (first ? 1 : 0);
             body = (uint64_t)sp + 5 + st;
-            const uint64_t h5 = (uint64_t)sp[0] | ((uint64_t)(nk >> 24) << 8) | ((uint64_t)((nk >> 16) & 0xFF) << 16) |
+            const uint64_t h5 = (uint64_t)((canon[j] & 2) ? 2u : 1u) | ((uint64_t)(nk >> 24) << 8) | ((uint64_t)((nk >> 16) & 0xFF) << 16) |
                                 ((uint64_t)((nk >> 8) & 0xFF) << 24) | ((uint64_t)(nk & 0xFF) << 32);
             hd = first ? (1ull | (h5 << 8)) : h5;  // CURRENT_VERSION (runs.rs:241-246), marker, key_len
             hlen = first ? 6u : 5u;
@@ -300,18 +341,17 @@ __global__ void __launch_bounds__(WAL_G) k_wal_gather(const uint64_t* __restrict
     }
 }
 
-void launch_wal_keys(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint32_t* m_rec,
-                     const uint32_t* rec_klen, const uint64_t* P, int64_t* tid, uint32_t* strip, uint64_t* wsize,
-                     uint8_t* canon, unsigned long long* first_err) {
+void launch_wal_keys(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,
+                     int64_t* tid, uint32_t* strip, uint32_t* wnk, uint64_t* wsize, uint8_t* canon,
+                     unsigned long long* first_err) {
     if (max_K)
-        k_wal_keys<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, m_src, m_rec, rec_klen, P, tid, strip, wsize, canon,
-                                                          first_err);
+        k_wal_keys<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, m_src, P, tid, strip, wnk, wsize, canon, first_err);
 }
 void launch_wal_flags(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const int64_t* tid, const uint32_t* strip,
-                      const uint8_t* canon, const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen,
-                      uint64_t* is_new, uint32_t* bad, bool exact) {
+                      const uint8_t* canon, const uint64_t* m_src, const uint32_t* wnk, uint64_t* is_new, uint32_t* bad,
+                      bool exact) {
     if (max_K)
-        k_wal_flags<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, tid, strip, canon, m_src, m_rec, rec_klen, is_new, bad,
+        k_wal_flags<<<wal_blocks(max_K, 256), 256, 0, s>>>(Kp, tid, strip, canon, m_src, wnk, is_new, bad,
                                                            exact ? 1u : 0u);
 }
 void launch_wal_index(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* is_new, const uint64_t* new_ex,
@@ -325,18 +365,17 @@ void launch_wal_tables(hipStream_t s, const uint64_t* NTp, uint64_t max_NT, cons
 }
 void launch_wal_desc(hipStream_t s, const uint64_t* NTp, uint64_t max_NT, const uint64_t* tstart, const uint64_t* Pw,
                      const uint64_t* Dp, const uint64_t* keep, const uint64_t* keep_ex, const uint64_t* run_off,
-                     const int64_t* tid, const uint32_t* strip, const uint32_t* m_rec, const uint32_t* rec_klen,
-                     DevRunDesc* descs) {
+                     const int64_t* tid, const uint32_t* wnk, DevRunDesc* descs) {
     if (max_NT)
-        k_wal_desc<<<wal_blocks(max_NT, 256), 256, 0, s>>>(NTp, tstart, Pw, Dp, keep, keep_ex, run_off, tid, strip,
-                                                           m_rec, rec_klen, descs);
+        k_wal_desc<<<wal_blocks(max_NT, 256), 256, 0, s>>>(NTp, tstart, Pw, Dp, keep, keep_ex, run_off, tid, wnk,
+                                                           descs);
 }
 void launch_wal_gather(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint32_t* tix, const uint64_t* tstart,
                        const uint64_t* keep, const uint64_t* run_off, const uint64_t* Pw, const uint32_t* strip,
-                       const uint64_t* m_src, const uint32_t* m_rec, const uint32_t* rec_klen, uint8_t* out) {
+                       const uint64_t* m_src, const uint32_t* wnk, const uint8_t* canon, uint8_t* out) {
     if (max_K)
         k_wal_gather<<<wal_blocks(max_K, WAL_G), WAL_G, 0, s>>>(Kp, tix, tstart, keep, run_off, Pw, strip, m_src,
-                                                                m_rec, rec_klen, out);
+                                                                wnk, canon, out);
 }
 
 }  // namespace skv

@@ -333,6 +333,31 @@ def test_longer_speculative_walks(dev, chunk):
             os.environ["SKV_CHUNK_BYTES"] = old
 
 
+def test_span_parse_opt_in(dev):
+    """The one-pass span parse (SKV_SPAN=1, off by default): variable-length shapes it takes
+    (span_parse == 1, incl. a run whose short tail span holds no record start), and shapes it
+    declines for the chunk-walk parse (fake records in values, records longer than a span,
+    corruption) -- every outcome equal to the oracle's."""
+    old = os.environ.get("SKV_SPAN")
+    os.environ["SKV_SPAN"] = "1"
+    try:
+        taken = 0
+        for n, rb in ((4, 200_000), (32, 192 * KiB), (256, 24 * KiB)):
+            s = gen.config3(n_streams=n, run_bytes=rb, vsize=64 if n == 256 else 256)
+            exp, got = _run_both(dev, s, 256 * KiB, 0)
+            assert exp == got, _diff(exp, got)
+            taken += dev.timings()["span_parse"] == 1
+        assert taken >= 2, "the span parse declined the plain config-3 shapes"
+        test_values_with_fake_records(dev)
+        test_records_spanning_many_chunks(dev)
+        test_corruption_at_every_position_class(dev)
+    finally:
+        if old is None:
+            os.environ.pop("SKV_SPAN", None)
+        else:
+            os.environ["SKV_SPAN"] = old
+
+
 def test_device_resident_entry_point(dev):
     """skv_compact_dev over HBM-resident inputs returns the same bytes as the host entry point."""
     torch = pytest.importorskip("torch")

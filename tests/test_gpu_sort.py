@@ -88,6 +88,30 @@ def test_fan_in_2000_wal_runs(dev):
     _check(dev, gen.config5(n_streams=2000), 4 * MiB, _abi.SKV_SPLIT_BY_TABLE)
 
 
+def test_fan_in_wal_runs_with_same_size_deletes(dev):
+    """Fixed-stride WAL runs of one format take one meta for every sorted record (k_sort_store's
+    const_meta) -- unless a record is a Delete of the runs' record size (key of S - 5 bytes), which
+    the fixed-stride parse accepts: then the meta of each record is gathered. Both outcomes equal the
+    oracle's, with and without the Delete filter."""
+    streams = gen.config5(n_streams=1700)
+    S = len(streams[0][1][0]) // 83  # 49-byte Puts: 1 + 4 + 32 + 4 + 8
+    _check(dev, streams, 4 * MiB, _abi.SKV_SPLIT_BY_TABLE)
+    r = random.Random(17)
+    for i in r.sample(range(len(streams)), 40):
+        seq, (run,) = streams[i]
+        recs = [run[1 + j * S:1 + (j + 1) * S] for j in range(83)]
+        j = r.randrange(83)
+        key = recs[j][5:37] + b"~" * (S - 5 - 32)  # sorts right after its Put's key, before the next
+        if j + 1 < 83 and key >= recs[j + 1][5:5 + 32]:
+            continue
+        dele = fmt.encode_record(fmt.delete(key.decode()))
+        assert len(dele) == S
+        recs[j + 1:j + 1] = [dele]
+        streams[i] = (seq, [run[:1] + b"".join(recs[:83]) + b"".join(recs[83:])])
+    for flags in (_abi.SKV_SPLIT_BY_TABLE, _abi.SKV_SPLIT_BY_TABLE | _abi.SKV_DROP_TOMBSTONES):
+        _check(dev, streams, 4 * MiB, flags)
+
+
 def test_fan_in_1600_overlapping_streams(dev):
     """1600 streams over a shared key universe: superseded records across streams (newest wins)."""
     streams = gen.config2(n_streams=1600, n_records=60, vsize=12, variant="B")
