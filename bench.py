@@ -226,8 +226,12 @@ def main():
         # gloo over the host: the path shards with no data-path exchange (north_star: no RCCL), so
         # the only cross-rank traffic is the start/stop barrier and two scalars
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # SKV_BENCH_SHARE_DEVICE=1: every rank on device 0 -- a rehearsal of the N-rank path on a
+    # one-GPU box (the line then says so; its value is not a scaling figure)
+    shared = os.environ.get("SKV_BENCH_SHARE_DEVICE") == "1"
+    dev_idx = 0 if shared else local_rank
+    torch.cuda.set_device(dev_idx)
+    device = torch.device("cuda", dev_idx)
 
     from skv.api import Compactor
     from skv.devgen import make_cfg2_on_device, make_cfg3_full_on_device, make_cfg3_on_device, make_cfg5_on_device
@@ -271,7 +275,7 @@ def main():
     else:
         in_bytes = sum(r.numel() for r in runs)
         streams = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(runs)]
-    comp = Compactor(local_rank, profiling=True)
+    comp = Compactor(dev_idx, profiling=True)
     # the skv_stream[] table, built once like a caller's Vec (at 10^6 streams building it in Python
     # costs more than the compaction)
     from skv._abi import StreamArgs
@@ -342,7 +346,7 @@ def main():
         # contract: different ctxs run concurrently)
         import threading
 
-        comp2 = Compactor(local_rank)
+        comp2 = Compactor(dev_idx)
         comp2.compact_host_ptrs(hstreams, max_run, flags)
         n_jobs = 3
 
@@ -433,7 +437,8 @@ def main():
                 "input_bytes_per_gpu": in_bytes,
                 "output_bytes_per_gpu": out_bytes,
                 "output_runs_per_gpu": n_out_runs,
-                "parallelism": f"{world} independent compactions (one per GPU), no collective",
+                "parallelism": f"{world} independent compactions (one per GPU), no collective"
+                               + (f" -- REHEARSAL: all {world} ranks share device 0" if shared else ""),
             },
             "device_ms_per_compaction": round(float(np.mean(total_ms)), 4),
             "host_ms": {"python_call": round(float(np.mean(call_ms)), 4),
