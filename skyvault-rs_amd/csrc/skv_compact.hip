@@ -939,6 +939,10 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // k_fp_verify's inputs once the level-0 tiles are queued; it runs on the ctx stream before the
     // WAL stage, or on the aux stream beside the gather (its verdict is read with the result)
     std::pair<const unsigned long long*, const uint64_t*> verify_args{nullptr, nullptr};
+    // in-gather verify of the pairs whose first record survives (TileOut::m_dup): when k_gather is the
+    // output stage and no Delete filter runs (a dropped Delete survivor has no output record to check
+    // against). SKV_FP_GATHER=0: every pair goes to k_fp_verify.
+    uint64_t* m_dup = nullptr;
     const unsigned long long* verify_lo = nullptr;  // pairs before it verified beside the merge
     bool verify_pending = false;
     if (km > 1 && !ctx->exact_keys && !heap && !job.scan) {  // (the scan's filtered arrays carry no fingerprints)
@@ -950,6 +954,9 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         } else {
             key_fp = rec_fp;  // written by the emit kernels with the record arrays
         }
+        const char* ge = getenv("SKV_FP_GATHER");
+        if (!SKV_PAGE_GATHER && !(ge && ge[0] == '0') && !(job.flags & (SKV_SPLIT_BY_TABLE | SKV_DROP_TOMBSTONES)))
+            m_dup = dbuf<uint64_t>(ctx, "m_dup", R + 1);
     }
     for (int li = (int)lv.size() - 1; li >= 0; --li) {
         Level& L = lv[li];
@@ -993,6 +1000,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             tile_max = O.tile_mm = dbuf<uint32_t>(ctx, "tile_mm", 2 * T);  // (min, max) record size per tile
             O.key_fp = key_fp;
             O.fp_bad = fp_bad;
+            O.m_dup = m_dup;
             if (key_fp) {  // pairs taken as equal by fingerprint, verified after the tiles
                 O.vpairs = dbuf<uint64_t>(ctx, "fp_vpairs", 2 * R);
                 O.vcount = dbuf<unsigned long long>(ctx, "fp_vcount", 1);
@@ -1195,7 +1203,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         launch_gather_pages(st, d_K, d_nruns, m_P, Dst, m_src, page_first, d_out, max_out);
     }
 #else
-    launch_gather(st, d_K, d_nruns, run_b, m_P, m_src, seg_r0, d_out, R);
+    launch_gather(st, d_K, d_nruns, run_b, m_P, m_src, seg_r0, d_out, R, m_dup, fp_bad);
 #endif
     HIPCHK(hipGetLastError());
     mark(ctx, PH_GATHER);

@@ -152,6 +152,11 @@ struct TileOut {
     uint32_t* fp_bad;
     uint64_t* vpairs;
     unsigned long long* vcount;
+    // in-gather verify (no Delete filter, k_gather as the output stage): m_dup[g] = the address of
+    // the record dropped right after the g-th survivor as fingerprint-equal to it (0: none); k_gather
+    // compares the two keys while the survivor's lines are in L2 from its own copy, and only the other
+    // pairs (a dropped record after a dropped one) go to vpairs. Null: every pair goes to vpairs.
+    uint64_t* m_dup;
     // global scratch for tiles larger than TILE_CAP
     uint64_t* xhi;
     uint64_t* xlo;

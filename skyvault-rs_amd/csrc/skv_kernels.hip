@@ -651,6 +651,31 @@ __device__ __forceinline__ bool elem_less_fp(bool use_fp, uint64_t fpa, const ui
     return (uint32_t)ca < (uint32_t)cb;
 }
 
+// Key bytes 16.. of two records whose keys have one length klen (> 16): equal? 64 tail bytes of both
+// per step, all eight windows loaded before any compare.
+__device__ __forceinline__ bool key_tails_equal(const uint8_t* ra, const uint8_t* rb, uint32_t klen) {
+    const uint8_t* ka = ra + 5 + 16;
+    const uint8_t* kb = rb + 5 + 16;
+    const uint32_t nt = klen > 16 ? klen - 16 : 0;
+    uint32_t diff = 0;
+    for (uint32_t o = 0; o < nt; o += 64) {
+        uint4 x[4], y[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t m = o + 16 * w < nt ? (nt - o - 16 * w < 16 ? nt - o - 16 * w : 16) : 0;
+            x[w] = m ? load_window16(ka + o + 16 * w, m) : make_uint4(0, 0, 0, 0);
+            y[w] = m ? load_window16(kb + o + 16 * w, m) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t m = o + 16 * w < nt ? (nt - o - 16 * w < 16 ? nt - o - 16 * w : 16) : 0;
+            diff |= ((x[w].x ^ y[w].x) & dword_mask(0, m, 0)) | ((x[w].y ^ y[w].y) & dword_mask(0, m, 1)) |
+                    ((x[w].z ^ y[w].z) & dword_mask(0, m, 2)) | ((x[w].w ^ y[w].w) & dword_mask(0, m, 3));
+        }
+    }
+    return diff == 0;
+}
+
 // The pairs k_tile<true> took as one key on equal prefix, length and fingerprint (O.vpairs: the two
 // records' addresses): their bytes past 16 must be equal, else the call is rerun with exact
 // compares. Every pair is independent: a grid-stride loop with all its loads in flight.
@@ -664,27 +689,7 @@ __global__ void k_fp_verify(const unsigned long long* __restrict__ vlo, const un
         const uint8_t* rb = (const uint8_t*)vpairs[2 * i + 1];
         const uint32_t la = __builtin_bswap32(load_window16(ra + 1, 4).x);  // key_len of each record
         const uint32_t lb = __builtin_bswap32(load_window16(rb + 1, 4).x);
-        const uint8_t* ka = ra + 5 + 16;
-        const uint8_t* kb = rb + 5 + 16;
-        bad |= la != lb;
-        const uint32_t nt = la == lb && la > 16 ? la - 16 : 0;
-        // 64 tail bytes of both keys per step, all eight windows loaded before any compare
-        for (uint32_t o = 0; o < nt; o += 64) {
-            uint4 x[4], y[4];
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const uint32_t m = o + 16 * w < nt ? (nt - o - 16 * w < 16 ? nt - o - 16 * w : 16) : 0;
-                x[w] = m ? load_window16(ka + o + 16 * w, m) : make_uint4(0, 0, 0, 0);
-                y[w] = m ? load_window16(kb + o + 16 * w, m) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const uint32_t m = o + 16 * w < nt ? (nt - o - 16 * w < 16 ? nt - o - 16 * w : 16) : 0;
-                const uint32_t dx = ((x[w].x ^ y[w].x) & dword_mask(0, m, 0)) | ((x[w].y ^ y[w].y) & dword_mask(0, m, 1)) |
-                                    ((x[w].z ^ y[w].z) & dword_mask(0, m, 2)) | ((x[w].w ^ y[w].w) & dword_mask(0, m, 3));
-                bad |= dx != 0;
-            }
-        }
+        bad |= la != lb || !key_tails_equal(ra, rb, la);
     }
     if (bad) atomicOr(fp_bad, 1u);
 }
@@ -888,11 +893,12 @@ __device__ void tile_minmax(uint32_t mn, uint32_t mx, uint32_t* s_mm, uint32_t* 
 // Delete filter of table_tree_compaction.rs:139-145 when asked) at global record g:
 // rec index, source address, output-byte prefix P, delete-count prefix
 __device__ __forceinline__ void emit_merged(const TileOut& O, uint64_t g, uint32_t idx, uint64_t addr, uint64_t pb,
-                                            uint64_t pd) {
+                                            uint64_t pd, uint64_t dup = 0) {
     O.m_rec[g] = idx;
     O.m_src[g] = addr;
     O.m_P[g] = pb;
     O.m_Dp[g] = pd;
+    if (O.m_dup) O.m_dup[g] = dup;
 }
 
 // heap-order mode: the records' own keys (first-per-key compares them, not the merge keys)
@@ -1271,11 +1277,29 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
             if (first) keep_mask |= 1u << q;
         }
     }
+    // in-gather verify (O.m_dup): a pair whose first record is its key's survivor is checked by
+    // k_gather against the survivor's bytes; only the others are queued (qmask). Per merged
+    // position in LDS (posof's bytes, free after the rounds): bit 0 first-per-key, bit 1 a pair with
+    // the record before it.
+    uint32_t qmask = vmask;
+    uint8_t* s_f8 = (uint8_t*)posof;
+    const bool dup_out = O.m_dup != nullptr && !drop_deletes;
+    if (dup_out) {
+        __syncthreads();  // every thread has read posof (rpos)
+#pragma unroll
+        for (int q = 0; q < PER; ++q)
+            if (i0 + q < n) s_f8[i0 + q] = (uint8_t)(((keep_mask >> q) & 1u) | (((vmask >> q) & 1u) << 1));
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; ++q)
+            if ((vmask >> q) & 1u)
+                if (s_f8[i0 + q - 1] & 1u) qmask &= ~(1u << q);
+    }
     uint32_t vex = 0;
     uint64_t vb = 0;
     if (kfp) {  // slots for the pairs taken as equal (one atomic per tile), written below
         uint32_t vtot;
-        vex = block_excl_scan<uint32_t>((uint32_t)__builtin_popcount(vmask), (uint32_t*)ws, vtot);
+        vex = block_excl_scan<uint32_t>((uint32_t)__builtin_popcount(qmask), (uint32_t*)ws, vtot);
         if (threadIdx.x == 0) s_flag[31] = vtot ? (uint32_t)atomicAdd(O.vcount, (unsigned long long)vtot) : 0u;
         __syncthreads();
         vb = s_flag[31];
@@ -1297,7 +1321,7 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     // the queued pairs as the two records' addresses (k_fp_verify then touches only their keys)
 #pragma unroll
     for (int q = 0; q < PER; ++q)
-        if (vmask & (1u << q)) {
+        if (qmask & (1u << q)) {
             const uint32_t i = i0 + q;
             O.vpairs[2 * (vb + vex)] = paddr[i - 1];
             O.vpairs[2 * (vb + vex) + 1] = paddr[i];
@@ -1344,7 +1368,9 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         if (keep_mask & (1u << q)) {
-            emit_merged(O, g, idx[q], ad[q], pb, pd);
+            const uint32_t i = i0 + q;
+            const uint64_t dup = dup_out && i + 1 < n && (s_f8[i + 1] & 2u) ? paddr[i + 1] : 0;
+            emit_merged(O, g, idx[q], ad[q], pb, pd, dup);
             ++g;
             pb += mt[q] & 0x7FFFFFFFu;
             pd += mt[q] >> 31;
@@ -2101,7 +2127,8 @@ __global__ void __launch_bounds__(GATHER_THREADS, SKV_GATHER_WAVES) k_gather(con
                                                            const uint64_t* __restrict__ run_b,
                                                            const uint64_t* __restrict__ P,
                                                            const uint64_t* __restrict__ m_src,
-                                                           const uint64_t* __restrict__ seg_r0, uint8_t* __restrict__ out) {
+                                                           const uint64_t* __restrict__ seg_r0, uint8_t* __restrict__ out,
+                                                           const uint64_t* __restrict__ m_dup, uint32_t* fp_bad) {
     // 20 KB of LDS at 256 records: 8 workgroups (32 waves) per CU
     __shared__ uint64_t s_dst[2 * GATHER_SEG + 1];  // piece p = output bytes [s_dst[p], s_dst[p+1])
     __shared__ uint64_t s_src[2 * GATHER_SEG];      // 0 => version byte
@@ -2122,11 +2149,12 @@ __global__ void __launch_bounds__(GATHER_THREADS, SKV_GATHER_WAVES) k_gather(con
     const uint32_t nrec = (uint32_t)(j1 - j0);
     // independent loads first: this lane's record (P, size, source) and the segment's first run
     const uint64_t j = j0 + threadIdx.x;
-    uint64_t Pj = 0, Pj1 = 0, srcj = 0;
+    uint64_t Pj = 0, Pj1 = 0, srcj = 0, dupj = 0;
     if (threadIdx.x < nrec) {
         Pj = P[j];
         Pj1 = P[j + 1];
         srcj = m_src[j];
+        if (m_dup) dupj = m_dup[j];
     }
     const uint64_t n_runs = *n_runs_p;
     const uint64_t r0 = seg_r0[seg];  // run holding record j0 (k_run_stats)
@@ -2282,6 +2310,13 @@ __global__ void __launch_bounds__(GATHER_THREADS, SKV_GATHER_WAVES) k_gather(con
             uint4 v;
             if (!fast_block(qi, v)) slow_block(qi);
         }
+    }
+    // in-gather verify: this survivor's key against the record dropped after it as fingerprint-equal
+    // (same length by construction); the survivor's lines are in L2 from the copy just done
+    if (dupj) {
+        const uint8_t* ra = (const uint8_t*)srcj;
+        const uint32_t kl = __builtin_bswap32(load_window16(ra + 1, 4).x);
+        if (!key_tails_equal(ra, (const uint8_t*)dupj, kl)) atomicOr(fp_bad, 1u);
     }
 }
 
@@ -2713,9 +2748,11 @@ void launch_run_stats(hipStream_t s, const uint64_t* n_runs, const uint64_t* run
     k_run_stats<<<blocks, 256, 0, s>>>(n_runs, run_b, P, Dp, m_rec, rec_klen, descs, seg_r0);
 }
 void launch_gather(hipStream_t s, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
-                   const uint64_t* m_src, const uint64_t* seg_r0, uint8_t* out, uint64_t max_K) {
+                   const uint64_t* m_src, const uint64_t* seg_r0, uint8_t* out, uint64_t max_K, const uint64_t* m_dup,
+                   uint32_t* fp_bad) {
     if (!max_K) return;
-    k_gather<<<blocks_for(max_K, GATHER_SEG), GATHER_THREADS, 0, s>>>(Kp, n_runs, run_b, P, m_src, seg_r0, out);
+    k_gather<<<blocks_for(max_K, GATHER_SEG), GATHER_THREADS, 0, s>>>(Kp, n_runs, run_b, P, m_src, seg_r0, out, m_dup,
+                                                                      fp_bad);
 }
 // small n: one workgroup walks the input in SCAN_BLOCK pieces with a running carry (one launch)
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_single(const uint64_t* in, uint64_t n, uint64_t* out) {

@@ -59,7 +59,8 @@ void launch_run_stats(hipStream_t, const uint64_t* n_runs, const uint64_t* run_b
                       const uint64_t* Dp, const uint32_t* m_rec, const uint32_t* rec_klen, DevRunDesc* descs,
                       uint64_t* seg_r0, uint64_t max_runs);
 void launch_gather(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
-                   const uint64_t* m_src, const uint64_t* seg_r0, uint8_t* out, uint64_t max_K);
+                   const uint64_t* m_src, const uint64_t* seg_r0, uint8_t* out, uint64_t max_K,
+                   const uint64_t* m_dup = nullptr, uint32_t* fp_bad = nullptr);
 // skv_wal.hip — SKV_SPLIT_BY_TABLE (wal_compaction.rs:66-174)
 void launch_wal_keys(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,
                      int64_t* tid, uint32_t* strip, uint32_t* wnk, uint64_t* wsize, uint8_t* canon,

@@ -209,6 +209,27 @@ def test_fp_shortcut_collisions_are_caught(dev, monkeypatch):
     _check(dev, streams, 1 << 16, _abi.SKV_DROP_TOMBSTONES, expect_sorted=False)
 
 
+def test_fp_collisions_caught_by_the_gather(dev, monkeypatch):
+    """Every forced collision pairs a survivor with the one record dropped after it (two keys per
+    16-byte prefix, in different streams): only k_gather's in-gather verify (TileOut::m_dup) sees
+    them. With SKV_FP_GATHER=0 the same pairs go to k_fp_verify. Both detect and rerun exactly."""
+    monkeypatch.setenv("SKV_FUSED", "0")
+    r = random.Random(21)
+    prefixes = sorted({f"p{r.randrange(10**12):015d}" for _ in range(3000)})
+    a = fmt.encode_run([fmt.put(p + "aaaa", b"A") for p in prefixes])
+    b = fmt.encode_run([fmt.put(p + "bbbb", b"B") for p in prefixes[::2]])
+    c = fmt.encode_run([fmt.put(p + "aaaa", b"C") for p in prefixes[1::2]])  # real duplicates, other prefixes
+    streams = [(3, [a]), (2, [b]), (1, [c])]
+    for gather in ("1", "0"):
+        monkeypatch.setenv("SKV_FP_GATHER", gather)
+        monkeypatch.setenv("SKV_FP_TEST", "1")
+        _check(dev, streams, 1 << 16, 0, expect_sorted=False)
+        assert dev.timings()["fp_rerun"] == 1, f"SKV_FP_GATHER={gather}: forced collisions not detected"
+        monkeypatch.setenv("SKV_FP_TEST", "0")
+        _check(dev, streams, 1 << 16, 0, expect_sorted=False)
+        assert dev.timings()["fp_rerun"] == 0
+
+
 def test_fp_shortcut_no_rerun_on_real_fingerprints(dev, monkeypatch):
     monkeypatch.setenv("SKV_FUSED", "0")
     for streams, mx, fl in ((_prefix_keys_streams(), 1 << 16, 0),
