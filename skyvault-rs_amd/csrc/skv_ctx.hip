@@ -2,6 +2,10 @@
 // call (build_job) and the guarded device call (run_guarded). C ABI: include/skv.h.
 #include "skv_host.hpp"
 
+#include <atomic>
+#include <deque>
+#include <exception>
+
 using namespace skv;
 
 
@@ -27,53 +31,109 @@ void* pinned(skv_ctx* ctx, size_t bytes) {
     return ctx->pinned;
 }
 
-// host copy into pinned staging; large tables (10^6-run calls: tens of MB) on several threads
-void stage_copy(void* dst, const void* src, size_t bytes) {
-    const char* pe = getenv("SKV_PAR_COPY_MIN");  // tests: split small tables too
-    const size_t kPar = pe ? (size_t)strtoull(pe, nullptr, 10) : (8u << 20);
-    const unsigned hw = std::thread::hardware_concurrency();
-    static const unsigned cap = [] {  // SKV_HOST_THREADS: host threads for 10^6-entry tables (default 8)
+namespace {
+struct PoolBatch {
+    void (*run)(void*, unsigned);
+    void* arg;
+    unsigned nb;
+    std::atomic<unsigned> next{0};    // next block to claim
+    std::atomic<unsigned> done{0};    // blocks finished
+    std::atomic<unsigned> active{0};  // workers holding this batch (the caller waits them out)
+    std::exception_ptr err;           // first exception of a worker's block
+    std::mutex err_m;
+};
+struct HostPool {
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<PoolBatch*> q;  // one token per helper wanted; a token names its batch
+    explicit HostPool(unsigned n) {
+        for (unsigned i = 0; i < n; ++i) std::thread([this] { work(); }).detach();
+    }
+    static void drain(PoolBatch* b) {
+        for (;;) {
+            const unsigned i = b->next.fetch_add(1);
+            if (i >= b->nb) return;
+            try {
+                b->run(b->arg, i);
+            } catch (...) {
+                std::lock_guard<std::mutex> l(b->err_m);
+                if (!b->err) b->err = std::current_exception();
+            }
+            b->done.fetch_add(1);
+        }
+    }
+    void work() {
+        for (;;) {
+            PoolBatch* b;
+            {
+                std::unique_lock<std::mutex> l(m);
+                cv.wait(l, [&] { return !q.empty(); });
+                b = q.front();
+                q.pop_front();
+                b->active.fetch_add(1);  // under the lock: the caller's token sweep sees it
+            }
+            drain(b);
+            b->active.fetch_sub(1);  // the last touch of b
+        }
+    }
+};
+unsigned host_threads_cap() {  // SKV_HOST_THREADS: host threads for 10^6-entry tables (default 8)
+    static const unsigned cap = [] {
         const char* e = getenv("SKV_HOST_THREADS");
         const long v = e ? atol(e) : 8;
         return (unsigned)std::max(1l, std::min(64l, v));
     }();
-    const unsigned nt = std::min<unsigned>(cap, hw ? hw : 1);
+    return cap;
+}
+HostPool& host_pool() {  // started on first use, never torn down (detached workers idle in cv.wait)
+    static HostPool* p = new HostPool(host_threads_cap() > 1 ? host_threads_cap() - 1 : 1);
+    return *p;
+}
+}  // namespace
+
+void par_exec(unsigned nb, void (*run)(void*, unsigned), void* arg) {
+    PoolBatch b;
+    b.run = run;
+    b.arg = arg;
+    b.nb = nb;
+    HostPool& P = host_pool();
+    {
+        std::lock_guard<std::mutex> l(P.m);
+        for (unsigned k = 1; k < nb; ++k) P.q.push_back(&b);
+    }
+    P.cv.notify_all();
+    HostPool::drain(&b);  // the caller claims blocks too: the call finishes even with every worker busy
+    {
+        std::lock_guard<std::mutex> l(P.m);  // tokens no worker took
+        P.q.erase(std::remove(P.q.begin(), P.q.end(), &b), P.q.end());
+    }
+    while (b.done.load() != nb || b.active.load() != 0) std::this_thread::yield();
+    if (b.err) std::rethrow_exception(b.err);
+}
+
+// host copy into pinned staging; large tables (10^6-run calls: tens of MB) on the host pool
+void stage_copy(void* dst, const void* src, size_t bytes) {
+    const char* pe = getenv("SKV_PAR_COPY_MIN");  // tests: split small tables too
+    const size_t kPar = pe ? (size_t)strtoull(pe, nullptr, 10) : (8u << 20);
+    const unsigned hw = std::thread::hardware_concurrency();
+    const unsigned nt = std::min<unsigned>(host_threads_cap(), hw ? hw : 1);
     if (bytes < kPar || nt < 2) {
         memcpy(dst, src, bytes);
         return;
     }
     const size_t part = ((bytes + nt - 1) / nt + 4095) & ~(size_t)4095;
-    std::vector<std::thread> th;
-    th.reserve(nt);
-    auto piece = [=](unsigned i) {
-        memcpy((uint8_t*)dst + i * part, (const uint8_t*)src + i * part, std::min(part, bytes - i * part));
-    };
-    unsigned started = 1;  // pieces [1, started) run on threads
-    for (unsigned i = 1; i < nt && i * part < bytes; ++i) {
-        try {
-            th.emplace_back(piece, i);
-        } catch (...) {  // no thread: this piece and the rest are copied here
-            break;
-        }
-        started = i + 1;
-    }
-    memcpy(dst, src, std::min(part, bytes));
-    for (unsigned i = started; i < nt && i * part < bytes; ++i) piece(i);
-    for (auto& t : th) t.join();
+    const unsigned np = (unsigned)((bytes + part - 1) / part);
+    par_run(np, np, [&](unsigned, uint64_t lo, uint64_t) {
+        memcpy((uint8_t*)dst + lo * part, (const uint8_t*)src + lo * part, std::min(part, bytes - lo * part));
+    });
 }
 
-// [0, n) as nb contiguous blocks fn(b, lo, hi) on host threads: the per-run and per-stream
-// table loops of a 10^6-stream call (config 5) are memory-bound at one core's bandwidth, ~10 ns
-// per entry. Below min_par entries one block runs on the calling thread; a block whose thread
-// cannot be started runs here too.
+// Blocks for par_run ([0, n) as nb contiguous blocks fn(b, lo, hi), par_exec's pool): the per-run and
+// per-stream table loops of a 10^6-stream call (config 5) are memory-bound at one core's bandwidth,
+// ~10 ns per entry. Below min_par entries one block runs on the calling thread.
 unsigned par_nblocks(uint64_t n, uint64_t min_par) {
     const unsigned hw = std::thread::hardware_concurrency();
-    static const unsigned cap = [] {  // SKV_HOST_THREADS: host threads for 10^6-entry tables (default 8)
-        const char* e = getenv("SKV_HOST_THREADS");
-        const long v = e ? atol(e) : 8;
-        return (unsigned)std::max(1l, std::min(64l, v));
-    }();
-    const unsigned nt = std::min<unsigned>(cap, hw ? hw : 1);
+    const unsigned nt = std::min<unsigned>(host_threads_cap(), hw ? hw : 1);
     return n < min_par ? 1u : nt;
 }
 
