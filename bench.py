@@ -321,6 +321,36 @@ def main():
     res.free()
     elapsed, total_in = reduce_over_ranks(elapsed_rank, in_bytes, dist, torch.device("cpu"))
 
+    # Not `value`: the same compaction issued from 2 host threads on 2 ctxs (2 HIP streams) of this
+    # GPU, 2 calls in flight -- one call's splitter phase and host gaps beside the other's tile phase
+    # (tools/overlap_probe.py). ms per compaction = wall / calls.
+    concurrent = None
+    if rank == 0 and world == 1 and config in ("2A", "2B"):
+        import threading
+
+        comps = [comp, Compactor(dev_idx)]
+        comps[1].compact_dev(table, max_run, flags).free()
+        n_each = max(2, args.steps // 2)
+
+        def worker(c):
+            for _ in range(n_each):
+                c.compact_dev(table, max_run, flags).free()
+
+        th = [threading.Thread(target=worker, args=(c,)) for c in comps]
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        torch.cuda.synchronize(device)
+        dt = time.perf_counter() - t1
+        concurrent = {"value": round(in_bytes * 2 * n_each / dt / GiB, 3), "unit": "GiB/s",
+                      "ms_per_compaction": round(dt / (2 * n_each) * 1e3, 4), "calls": 2 * n_each,
+                      "note": "2 ctxs x %d skv_compact_dev calls from 2 host threads, same inputs; wall / calls"
+                              % n_each}
+        comps[1].close()
+
     # PCIe-inclusive figure (not `value`): the host entry point skv_compact with the inputs in
     # pinned host memory and the output runs returned in pinned host memory.
     host_path = None
@@ -401,7 +431,7 @@ def main():
         if g_ms <= 0:  # the WAL stage reports no single dominant launch: the whole device time
             g_ms = float(np.mean(total_ms))
         achieved = (gread + gwrite) / (g_ms * 1e-3) / 1e9
-        hot_kernel = "k_wal_gather" if config == "5" else HOT_KERNEL.get(path, "?")
+        hot_kernel = ("k_wal_fused" if t["wal_stage"] == 1 else "k_wal_gather") if config == "5" else HOT_KERNEL.get(path, "?")
         # PMC counters of THIS config's dominant kernel (tools/traffic.py keys them by config and
         # kernel); none recorded -> null with the reason, never another config's counters
         traffic, traffic_note, traffic_rw = None, None, None
@@ -467,6 +497,8 @@ def main():
         line["invariants"] = invariants
         if host_path is not None:
             line["host_path"] = host_path
+        if concurrent is not None:
+            line["concurrent_2ctx"] = concurrent
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(config, args.cpu_sample_records, n_streams if config != "5" else 0,
                                             args.vsize, args.cpu_repeats, args.run_mib)

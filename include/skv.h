@@ -35,8 +35,8 @@
 extern "C" {
 #endif
 
-#define SKV_ABI_VERSION 5  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts; 4: skv_scan_runs;
-                              5: skv_timings.span_parse (was reserved) */
+#define SKV_ABI_VERSION 6  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts; 4: skv_scan_runs;
+                              5: skv_timings.span_parse (was reserved); 6: skv_timings.wal_stage */
 
 typedef struct skv_ctx skv_ctx;
 
@@ -138,6 +138,9 @@ typedef struct {
                                 (0: the serial copy -> compact -> copy) */
     uint32_t span_parse;     /* general path: 1 the one-pass span parse produced the record arrays;
                                 2 | fail_bits << 8: it declined and the chunk-walk parse ran; 0 not tried */
+    uint32_t wal_stage;      /* SKV_SPLIT_BY_TABLE: 1 the one-pass stage (every table kept), 2 the exact
+                                stage (the one-pass stage declined or does not apply), 0 no WAL stage */
+    uint32_t reserved2;
 } skv_timings;
 
 /* skv_timings.path */

@@ -20,12 +20,137 @@ int rerun_exact(skv_ctx* ctx, const Job& job, skv_result** out) {
     return rc;
 }
 
+// the WAL stage's result (both paths): descriptors already on the host
+static int wal_result(skv_ctx* ctx, const Job& job, uint64_t R, uint8_t* d_out, skv_run_desc* runs, uint64_t n_tables,
+                      uint64_t n_kept, uint64_t n_bytes, skv_result** out) {
+    ResultBox* box = new ResultBox();
+    skv_result* res = &box->pub;
+    res->runs = runs;
+    uint64_t out_records = 0;
+    for (uint64_t i = 0; i < n_kept; ++i) out_records += res->runs[i].put_count + res->runs[i].delete_count;
+    res->n_runs = n_kept;
+    res->bytes = d_out;
+    res->n_bytes = n_bytes;
+    res->in_bytes = job.in_bytes;
+    res->in_records = R;
+    res->out_records = out_records;
+    res->dropped_tables = n_tables - n_kept;
+    if (ctx->profiling) {
+        HIPCHK(hipEventSynchronize(ctx->ev[PH_GATHER]));
+        float ms[PH_N] = {};
+        for (int p = PH_PARSE; p < PH_N; ++p) HIPCHK(hipEventElapsedTime(&ms[p], ctx->ev[p - 1], ctx->ev[p]));
+        float tot = 0;
+        HIPCHK(hipEventElapsedTime(&tot, ctx->ev[PH_START], ctx->ev[PH_GATHER]));
+        skv_timings& t = ctx->timings;
+        t.total_ms = tot;
+        t.parse_ms = ms[PH_PARSE];
+        t.check_ms = ms[PH_CHECK];
+        t.merge_ms = ms[PH_MERGE];
+        t.chain_ms = ms[PH_CHAIN];
+        t.gather_ms = ms[PH_GATHER];
+        t.gather_read_bytes = n_bytes - n_kept;
+        t.gather_write_bytes = n_bytes;
+        t.hot_ms = ms[PH_GATHER];
+    }
+    ctx->timings.path = SKV_PATH_GENERAL;  // WAL stage: the dominant launch is k_wal_gather / k_wal_fused
+    ctx->timings.hot_read_bytes = n_bytes - n_kept;
+    ctx->timings.hot_write_bytes = n_bytes;
+    ctx->timings.host_syncs = ctx->syncs;
+    *out = res;
+    return SKV_OK;
+}
+
+// The one-pass WAL stage (k_wal_fused, skv_wal.hip) for sorted inputs: every table kept, checked
+// after the fact. RC_DECLINED when that does not hold (a bad key, an order error, a table over max,
+// more than WF_TCAP tables): the exact stage below then runs and gives the reference's outcome.
+constexpr int RC_DECLINED = -1000;
+constexpr uint32_t WF_TCAP = 1u << 16, WF_GUESS = 1024;
+static int wal_fused(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, const uint64_t* m_src,
+                     const uint64_t* m_P, const uint64_t* m_Dp, const uint32_t* fp_bad, skv_result** out) {
+    hipStream_t st = ctx->stream;
+    uint8_t* d_out = dbuf<uint8_t>(ctx, "out", job.in_bytes + R + 16);
+    const uint64_t nwg = (R + WAL_FUSED_G - 1) / WAL_FUSED_G;
+    uint64_t* tstate = dbuf<uint64_t>(ctx, "wf_state", nwg + 1);
+    uint32_t* words = dbuf<uint32_t>(ctx, "wf_words", 4);  // ticket, fail bits, table count
+    uint64_t* tail = dbuf<uint64_t>(ctx, "wf_tail", 8);
+    WalTStart* tl = dbuf<WalTStart>(ctx, "wf_tlist", WF_TCAP);
+    HIPCHK(hipMemsetAsync(tstate, 0, (nwg + 1) * 8, st));
+    HIPCHK(hipMemsetAsync(words, 0, 16, st));
+    HIPCHK(hipMemsetAsync(tail, 0, 64, st));
+    mark(ctx, PH_CHAIN);
+    const char* fe = getenv("SKV_WAL_FUSED");
+    launch_wal_fused(st, d_K, R, m_src, m_P, m_Dp, d_out, tstate, words, words + 1, tl, words + 2, WF_TCAP, tail,
+                     fe && fe[0] == '2' ? 2u : 0u);
+    HIPCHK(hipGetLastError());
+    mark(ctx, PH_GATHER);
+    uint8_t* hp = (uint8_t*)pinned(ctx, 128 + WF_GUESS * sizeof(WalTStart));
+    d2h(ctx, hp, d_K, 8);
+    d2h(ctx, hp + 8, fp_bad, 4);
+    d2h(ctx, hp + 16, words, 16);
+    d2h(ctx, hp + 32, tail, 64);
+    d2h(ctx, hp + 128, tl, WF_GUESS * sizeof(WalTStart));
+    sync(ctx);
+    htrace("wal fused read");
+    uint64_t K, tw[8];
+    uint32_t fpb, w[4];
+    memcpy(&K, hp, 8);
+    memcpy(&fpb, hp + 8, 4);
+    memcpy(w, hp + 16, 16);
+    memcpy(tw, hp + 32, 64);
+    if (fpb) return RC_RETRY_EXACT;
+    const uint32_t nt = w[2];
+    if (w[1] || nt > WF_TCAP) return RC_DECLINED;
+    std::vector<WalTStart> E(nt);
+    memcpy(E.data(), hp + 128, (size_t)std::min(nt, WF_GUESS) * sizeof(WalTStart));
+    if (nt > WF_GUESS)
+        HIPCHK(hipMemcpy(E.data() + WF_GUESS, tl + WF_GUESS, (nt - WF_GUESS) * sizeof(WalTStart), hipMemcpyDeviceToHost));
+    std::sort(E.begin(), E.end(), [](const WalTStart& a, const WalTStart& b) { return a.b < b.b; });
+    // tw: output bytes of the call, stripped size and key length of the last record, -, deletes
+    const uint64_t n_bytes = tw[0], ws_last = tw[1], nk_last = tw[2], Dp_all = tw[4];
+    skv_run_desc* runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, nt) * sizeof(skv_run_desc));
+    for (uint32_t t = 0; t < nt; ++t) {  // k_wal_desc's fields, and the one-run rule (:126-137)
+        const bool last = t + 1 == nt;
+        const uint64_t b = E[t].b, e = last ? K : E[t + 1].b;
+        const uint64_t off = E[t].W, end = last ? n_bytes : E[t + 1].W;  // [version byte, records]
+        const uint64_t Dpe = last ? Dp_all : E[t + 1].Dp;
+        if (!(e - b == 1 || end - off <= job.max_run_size)) {
+            free(runs);
+            return RC_DECLINED;
+        }
+        skv_run_desc& d = runs[t];
+        d.off = off;
+        d.len = end - off;
+        d.delete_count = Dpe - E[t].Dp;
+        d.put_count = (e - b) - d.delete_count;
+        d.min_key_off = off + 1 + 5;
+        d.min_key_len = E[t].nk;
+        // the last record's piece: its stripped size back from the table's end (+ the version byte
+        // when it is the table's only record)
+        const uint64_t lws = (last ? ws_last : E[t + 1].prev_ws) + (e - b == 1 ? 1 : 0);
+        d.max_key_off = end - lws + (e - b == 1 ? 1 : 0) + 5;
+        d.max_key_len = last ? nk_last : E[t + 1].prev_nk;
+        d.table_id = E[t].tid;
+        d.reserved = 0;
+    }
+    return wal_result(ctx, job, R, d_out, runs, nt, nt, n_bytes, out);
+}
+
 // SKV_SPLIT_BY_TABLE after the merge: table split, prefix strip, one run per kept table
-// (skv_wal.hip). One extra host sync reads the surviving record count first.
+// (skv_wal.hip): the one-pass stage when it applies, else the exact one (one extra host sync reads
+// the surviving record count first).
 int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, const uint32_t* m_rec,
                      const uint64_t* m_src, const uint64_t* m_P, const uint64_t* m_Dp, const uint64_t* rec_addr,
                      const uint32_t* rec_klen, const uint32_t* fp_bad, const HeapRes* heap, skv_result** out) {
     hipStream_t st = ctx->stream;
+    const char* fe = getenv("SKV_WAL_FUSED");
+    if (!heap && !(fe && fe[0] == '0') && R > 0) {
+        const int rc = wal_fused(ctx, job, R, d_K, m_src, m_P, m_Dp, fp_bad, out);
+        if (rc != RC_DECLINED) {
+            ctx->timings.wal_stage = 1;
+            return rc;
+        }
+    }
+    ctx->timings.wal_stage = 2;
     uint64_t K = 0;
     {
         uint64_t* hp = (uint64_t*)pinned(ctx, 64);
@@ -118,42 +243,9 @@ int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, con
     }
     throw_first(ev);
     const uint64_t n_tables = h[1], n_kept = h[2], n_bytes = h[3];
-    ResultBox* box = new ResultBox();
-    skv_result* res = &box->pub;
-    res->runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, n_kept) * sizeof(skv_run_desc));
-    if (n_kept) HIPCHK(hipMemcpy(res->runs, d_desc, n_kept * sizeof(DevRunDesc), hipMemcpyDeviceToHost));
-    uint64_t out_records = 0;
-    for (uint64_t i = 0; i < n_kept; ++i) out_records += res->runs[i].put_count + res->runs[i].delete_count;
-    res->n_runs = n_kept;
-    res->bytes = d_out;
-    res->n_bytes = n_bytes;
-    res->in_bytes = job.in_bytes;
-    res->in_records = R;
-    res->out_records = out_records;
-    res->dropped_tables = n_tables - n_kept;
-    if (ctx->profiling) {
-        HIPCHK(hipEventSynchronize(ctx->ev[PH_GATHER]));
-        float ms[PH_N] = {};
-        for (int p = PH_PARSE; p < PH_N; ++p) HIPCHK(hipEventElapsedTime(&ms[p], ctx->ev[p - 1], ctx->ev[p]));
-        float tot = 0;
-        HIPCHK(hipEventElapsedTime(&tot, ctx->ev[PH_START], ctx->ev[PH_GATHER]));
-        skv_timings& t = ctx->timings;
-        t.total_ms = tot;
-        t.parse_ms = ms[PH_PARSE];
-        t.check_ms = ms[PH_CHECK];
-        t.merge_ms = ms[PH_MERGE];
-        t.chain_ms = ms[PH_CHAIN];
-        t.gather_ms = ms[PH_GATHER];
-        t.gather_read_bytes = n_bytes - n_kept;
-        t.gather_write_bytes = n_bytes;
-        t.hot_ms = ms[PH_GATHER];
-    }
-    ctx->timings.path = SKV_PATH_GENERAL;  // WAL stage: the dominant launch is k_wal_gather
-    ctx->timings.hot_read_bytes = n_bytes - n_kept;
-    ctx->timings.hot_write_bytes = n_bytes;
-    ctx->timings.host_syncs = ctx->syncs;
-    *out = res;
-    return SKV_OK;
+    skv_run_desc* runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, n_kept) * sizeof(skv_run_desc));
+    if (n_kept) HIPCHK(hipMemcpy(runs, d_desc, n_kept * sizeof(DevRunDesc), hipMemcpyDeviceToHost));
+    return wal_result(ctx, job, R, d_out, runs, n_tables, n_kept, n_bytes, out);
 }
 
 // Sorts n SElems by (key, record index) (skv_sort.hip); E and T are n-element buffers, the

@@ -62,6 +62,16 @@ void launch_gather(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, cons
                    const uint64_t* m_src, const uint64_t* seg_r0, uint8_t* out, uint64_t max_K,
                    const uint64_t* m_dup = nullptr, uint32_t* fp_bad = nullptr);
 // skv_wal.hip — SKV_SPLIT_BY_TABLE (wal_compaction.rs:66-174)
+constexpr uint32_t WAL_FUSED_G = 256;  // merged records per k_wal_fused workgroup
+struct WalTStart {  // a table start of k_wal_fused (unordered list; the host sorts by b)
+    uint64_t b, W, Dp;  // first merged record, output offset of the table's version byte, deletes before b
+    int64_t tid;
+    uint32_t nk, prev_nk;  // stripped key length of it and of the record before it
+    uint64_t prev_ws;      // stripped size of the record before it
+};
+void launch_wal_fused(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,
+                      const uint64_t* Dp, uint8_t* out, uint64_t* tstate, uint32_t* ticket, uint32_t* fail,
+                      WalTStart* tlist, uint32_t* tcount, uint32_t tcap, uint64_t* tail, uint32_t diag = 0);
 void launch_wal_keys(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,
                      int64_t* tid, uint32_t* strip, uint32_t* wnk, uint64_t* wsize, uint8_t* canon,
                      unsigned long long* first_err);

@@ -224,6 +224,7 @@ __global__ void k_wal_desc(const uint64_t* __restrict__ NTp, const uint64_t* __r
 // workgroup's output span is contiguous (kept tables are), and each lane then composes whole
 // 16-byte output blocks from the pieces (bytewise only at the span's two edges).
 constexpr int WAL_G = 256;
+static_assert(WAL_G == (int)WAL_FUSED_G, "k_wal_fused's workgroup size (host look-back sizing)");
 
 __device__ __forceinline__ void or_byte(uint4& v, uint32_t pos, uint32_t byte) {
     const uint32_t w = byte << (8 * (pos & 3));
@@ -339,6 +340,227 @@ __global__ void __launch_bounds__(WAL_G) k_wal_gather(const uint64_t* __restrict
             for (uint64_t y = x0; y < x1; ++y) out[y] = (uint8_t)byte_of(v, (uint32_t)(y - B));
         }
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// One pass for the common case (k_wal_fused): every key has a table prefix, every table's stripped
+// keys ascend, and every table fits one run -- then every table is kept and its run is simply
+// [version byte, its records stripped]. Per merged record: the first min(32, size) bytes (the key's
+// prefix and length), the table id, a new-table flag against the previous record, the stripped size;
+// a decoupled look-back over workgroups (ticket order) gives each record's output offset W_j + N_j
+// (stripped bytes before it, table starts up to it); the workgroup then composes its output blocks
+// from the lines it just read (k_wal_gather's pieces). Table starts go to an unordered list that the
+// host sorts into the descriptors. Anything else -- a bad key, an order error, a table over max, more
+// tables than the list holds -- sets a fail bit, and the host runs the exact stage above instead.
+struct WalRec {
+    uint64_t size;
+    int64_t tid;
+    uint32_t strip, klen, marker, err;
+    bool canon;
+};
+__device__ __forceinline__ WalRec wal_parse(const uint8_t* rp, uint64_t size) {
+    WalRec r;
+    r.size = size;
+    const uint4 h0 = load_window16(rp, (uint32_t)(size < 16 ? size : 16));
+    const uint4 h1 = size > 16 ? load_window16(rp + 16, (uint32_t)(size - 16 < 16 ? size - 16 : 16)) : make_uint4(0, 0, 0, 0);
+    const uint32_t hw[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    r.marker = hw[0] & 0xFFu;
+    r.klen = __builtin_bswap32(__builtin_amdgcn_alignbyte(hw[1], hw[0], 1));
+    const uint8_t* key = rp + 5;
+    uint64_t dot = r.klen;
+    {
+        const uint32_t n0 = r.klen < 27 ? r.klen : 27;
+        uint32_t hit = 0;
+#pragma unroll
+        for (int i = 0; i < 27; ++i)
+            if (((hw[(i + 5) >> 2] >> (8 * ((i + 5) & 3))) & 0xFFu) == (uint32_t)'.' && (uint32_t)i < n0) hit |= 1u << i;
+        if (hit) dot = __builtin_ctz(hit);
+    }
+    for (uint64_t o = 27; dot == r.klen && o < r.klen; o += 16) {
+        const uint32_t m = (uint32_t)(r.klen - o < 16 ? r.klen - o : 16);
+        const uint4 v = load_window16(key + o, m);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t hit = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (((w[i >> 2] >> (8 * (i & 3))) & 0xFFu) == (uint32_t)'.' && (uint32_t)i < m) hit |= 1u << i;
+        if (hit) dot = o + __builtin_ctz(hit);
+    }
+    r.tid = 0;
+    r.err = dot == r.klen ? WERR_NODOT : (dot <= 27 ? parse_i64_win(hw, (uint32_t)dot, r.tid) : parse_i64_dev(key, dot, r.tid));
+    r.strip = r.err ? 0u : id_prefix_len(r.tid);
+    r.canon = !r.err && dot + 1 == r.strip;
+    return r;
+}
+
+constexpr uint32_t WF_BADKEY = 1, WF_ORDER = 2, WF_TABLES = 4;
+
+__global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ m_src,
+                                                     const uint64_t* __restrict__ P, const uint64_t* __restrict__ Dp,
+                                                     uint8_t* out, uint64_t* tstate, uint32_t* ticket, uint32_t* fail,
+                                                     WalTStart* tlist, uint32_t* tcount, uint32_t tcap,
+                                                     uint64_t* tail, uint32_t diag) {
+    __shared__ uint64_t os[WAL_G + 1], src[WAL_G], head[WAL_G];
+    __shared__ uint32_t hl[WAL_G];
+    __shared__ uint64_t s_w[WAL_G / 64], s_base[1];
+    __shared__ uint32_t s_t;
+    const uint64_t K = *Kp;
+    if (threadIdx.x == 0) s_t = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint64_t t = s_t;
+    const uint64_t j0 = t * WAL_G;
+    if (j0 >= K) return;  // (tickets past the last workgroup: nothing to publish)
+    const uint64_t j = j0 + threadIdx.x;
+    const bool live = j < K;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    WalRec r{};
+    const uint8_t* rp = nullptr;
+    uint32_t bad = 0;
+    if (live) {
+        rp = (const uint8_t*)m_src[j];
+        r = wal_parse(rp, P[j + 1] - P[j]);
+        if (r.err) bad |= WF_BADKEY;
+    }
+    // the record before: the neighbouring lane, or (a wave's lane 0) parsed again
+    int64_t ptid = __shfl_up(r.tid, 1, 64);
+    uint32_t pstrip = __shfl_up(r.strip, 1, 64), pklen = __shfl_up(r.klen, 1, 64);
+    bool pcanon = __shfl_up(r.canon ? 1 : 0, 1, 64) != 0;
+    uint64_t psize = __shfl_up(r.size, 1, 64);
+    const uint8_t* prp = (const uint8_t*)__shfl_up((uint64_t)rp, 1, 64);
+    if (live && lane == 0 && j > 0) {
+        prp = (const uint8_t*)m_src[j - 1];
+        const WalRec q = wal_parse(prp, P[j] - P[j - 1]);
+        ptid = q.tid;
+        pstrip = q.strip;
+        pklen = q.klen;
+        pcanon = q.canon;
+        psize = q.size;
+        if (q.err) bad |= WF_BADKEY;
+    }
+    const bool nw = live && (j == 0 || ptid != r.tid);
+    if (live && !nw && !(pcanon && r.canon)) {  // stripped keys must ascend inside a table
+        const uint8_t* ka = prp + 5 + pstrip;
+        const uint8_t* kb = rp + 5 + r.strip;
+        const uint64_t la = pklen - pstrip, lb = r.klen - r.strip;
+        const uint64_t n = la < lb ? la : lb;
+        int c = bytes_cmp16(ka, kb, n);
+        if (!c) c = la < lb ? -1 : (la > lb ? 1 : 0);
+        if (c >= 0) bad |= WF_ORDER;
+    }
+    if (bad) atomicOr(fail, bad);
+    const uint64_t ws = live ? r.size - r.strip : 0;
+    // output bytes of record j: its version byte (a table start) + its stripped record. The exclusive
+    // prefix of those is where its piece starts, and a table's version byte sits where its first
+    // record's piece starts, so one sum places everything (no separate table-start count).
+    const uint64_t wo = ws + (nw ? 1 : 0);
+    uint64_t wi = wo;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t a = __shfl_up(wi, d, 64);
+        if (lane >= d) wi += a;
+    }
+    if (lane == 63) s_w[wv] = wi;
+    __syncthreads();
+    uint64_t wb = 0, wt = 0;
+    for (int w = 0; w < WAL_G / 64; ++w) {
+        if (w < wv) wb += s_w[w];
+        wt += s_w[w];
+    }
+    // decoupled look-back over workgroups (ticket order); wave 0 reads 64 predecessors per step --
+    // workgroups are short, so chains of aggregates are long
+    if (threadIdx.x < 64) {
+        constexpr uint64_t FA = 1ull << 62, FI = 2ull << 62, VM = FA - 1;
+        uint64_t acc = 0;
+        if (t == 0) {
+            if (lane == 0) __hip_atomic_store(&tstate[0], FI | wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0) __hip_atomic_store(&tstate[t], FA | wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t top = (int64_t)t - 1;
+            for (;;) {
+                const int64_t p = top - lane;
+                const uint64_t v = p >= 0 ? __hip_atomic_load(&tstate[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : FI;
+                const uint64_t f = v >> 62;
+                const uint64_t incl = __ballot(f == 2), none = __ballot(f == 0);
+                const int first = incl ? __builtin_ctzll(incl) : 64;
+                const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1);
+                if (none & upto) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                uint64_t x = lane <= first ? (v & VM) : 0;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+                acc += x;
+                if (first < 64) break;
+                top -= 64;
+            }
+            if (lane == 0) __hip_atomic_store(&tstate[t], FI | (acc + wt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) s_base[0] = acc;
+    }
+    __syncthreads();
+    const uint64_t ostart = s_base[0] + wb + wi - wo;  // this record's piece (version byte first if nw)
+    if (live && j + 1 == K) {
+        tail[0] = ostart + wo;  // output bytes of the whole call
+        tail[1] = ws;
+        tail[2] = r.klen - r.strip;
+        tail[4] = Dp[j + 1];    // deletes of all records
+    }
+    if (nw) {
+        const uint32_t e = atomicAdd(tcount, 1u);
+        if (e < tcap) {
+            WalTStart x;
+            x.b = j;
+            x.W = ostart;
+            x.Dp = Dp[j];
+            x.tid = r.tid;
+            x.nk = r.klen - r.strip;
+            x.prev_nk = j ? pklen - pstrip : 0;
+            x.prev_ws = j ? psize - pstrip : 0;
+            tlist[e] = x;
+        } else {
+            atomicOr(fail, WF_TABLES);
+        }
+    }
+    // the output pieces: [version byte,] marker, new key_len, then the record body past the prefix
+    if (live) {
+        const uint32_t nk = r.klen - r.strip;
+        const uint64_t h5 = (uint64_t)r.marker | ((uint64_t)(nk >> 24) << 8) | ((uint64_t)((nk >> 16) & 0xFF) << 16) |
+                            ((uint64_t)((nk >> 8) & 0xFF) << 24) | ((uint64_t)(nk & 0xFF) << 32);
+        os[threadIdx.x] = ostart;
+        src[threadIdx.x] = (uint64_t)rp + 5 + r.strip;
+        head[threadIdx.x] = nw ? (1ull | (h5 << 8)) : h5;
+        hl[threadIdx.x] = nw ? 6u : 5u;
+        if (j + 1 == K || threadIdx.x + 1 == WAL_G) os[threadIdx.x + 1] = ostart + wo;
+    }
+    __syncthreads();
+    if (diag == 2) return;  // SKV_WAL_FUSED=2 (diagnostic, wrong output): everything but the output bytes
+    const uint32_t c = (uint32_t)(K - j0 < WAL_G ? K - j0 : WAL_G);
+    const uint64_t lo = os[0], hi = os[c];
+    const uint64_t Blo = lo & ~15ull, Bhi = (hi + 15) & ~15ull;
+    for (uint64_t B = Blo + 16ull * threadIdx.x; B < Bhi; B += 16ull * WAL_G) {
+        const uint64_t x0 = B > lo ? B : lo, x1 = B + 16 < hi ? B + 16 : hi;
+        uint32_t a = 0, bb = c;  // last record with os <= x0
+        while (bb - a > 1) {
+            const uint32_t mid = (a + bb) >> 1;
+            if (os[mid] <= x0) a = mid;
+            else bb = mid;
+        }
+        const uint4 v = wal_compose(B, x0, x1, a, os, src, head, hl);
+        if (x0 == B && x1 == B + 16) {
+            *(uint4*)(out + B) = v;
+        } else {  // span edge: this workgroup's bytes only
+            for (uint64_t y = x0; y < x1; ++y) out[y] = (uint8_t)byte_of(v, (uint32_t)(y - B));
+        }
+    }
+}
+
+void launch_wal_fused(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,
+                      const uint64_t* Dp, uint8_t* out, uint64_t* tstate, uint32_t* ticket, uint32_t* fail,
+                      WalTStart* tlist, uint32_t* tcount, uint32_t tcap, uint64_t* tail, uint32_t diag) {
+    if (max_K)
+        k_wal_fused<<<wal_blocks(max_K, WAL_G), WAL_G, 0, s>>>(Kp, m_src, P, Dp, out, tstate, ticket, fail, tlist,
+                                                                tcount, tcap, tail, diag);
 }
 
 void launch_wal_keys(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,

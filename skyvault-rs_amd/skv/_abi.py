@@ -113,6 +113,8 @@ class SkvTimings(C.Structure):
         ("fp_rerun", C.c_uint32),
         ("host_parts", C.c_uint32),
         ("span_parse", C.c_uint32),
+        ("wal_stage", C.c_uint32),
+        ("reserved2", C.c_uint32),
     ]
 
 

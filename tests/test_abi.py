@@ -21,13 +21,30 @@ def test_header_declares_exactly_the_bound_symbols():
 def test_library_exports_every_symbol():
     api.build()
     assert api.exported_symbols_present() == _abi.EXPORTED_SYMBOLS
-    assert api.load().skv_abi_version() == 5
+    assert api.load().skv_abi_version() == 6
 
 
 def test_struct_layouts_match_header():
     assert C.sizeof(_abi.SkvRunDesc) == 80
     assert C.sizeof(_abi.SkvStream) == 32
     assert C.sizeof(_abi.SkvResult) == 64
+
+
+def test_timings_layout_matches_header(tmp_path):
+    """skv_timings as the C compiler lays it out (include/skv.h) == the ctypes mirror (_abi.py)."""
+    import subprocess
+
+    src = tmp_path / "t.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "skv.h"\n'
+                   'int main(void) { printf("%zu %zu %zu\\n", sizeof(skv_timings), '
+                   'offsetof(skv_timings, span_parse), offsetof(skv_timings, wal_stage)); return 0; }\n')
+    exe = tmp_path / "t"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    subprocess.check_call(["gcc", "-I", inc, str(src), "-o", str(exe)])
+    size, off_span, off_wal = map(int, subprocess.check_output([str(exe)]).split())
+    assert C.sizeof(_abi.SkvTimings) == size
+    assert _abi.SkvTimings.span_parse.offset == off_span
+    assert _abi.SkvTimings.wal_stage.offset == off_wal
 
 
 def test_code_object_targets_gfx950():

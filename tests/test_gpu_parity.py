@@ -196,6 +196,43 @@ def test_wal_split_matches_oracle(dev):
     assert not bad, bad[:5]
 
 
+def test_wal_one_pass_stage(dev):
+    """The one-pass WAL stage (k_wal_fused) where it applies -- sorted streams, good keys, ascending
+    stripped keys, every table within max -- and the exact stage where it declines: many tables across
+    many 256-record workgroups, Deletes, tables of one record, a table over max, a bad key, "007.a"
+    next to "7.0" (one table whose stripped keys decrease). Every outcome equal to the oracle's."""
+    r = random.Random(29)
+    tables = [str(t) for t in range(-40, 300)]
+    streams = []
+    for s in range(12):
+        keys = sorted({f"{r.choice(tables)}.{r.randrange(10**6):06d}" for _ in range(2500)})
+        ops = [fmt.put(k, bytes(r.randrange(256) for _ in range(r.randrange(0, 20)))) if r.random() < .9
+               else fmt.delete(k) for k in keys]
+        streams.append((s + 1, [fmt.encode_run(ops)]))
+    single = [(100, [fmt.encode_run([fmt.put("777.x", b"only")])])]
+    for sts, max_size, stage in ((streams, 4 * MiB, 1), (streams + single, 4 * MiB, 1), (streams, 600, 2)):
+        exp, got = _run_both(dev, sts, max_size, _abi.SKV_SPLIT_BY_TABLE)
+        assert exp == got, _diff(exp, got)
+        assert dev.timings()["wal_stage"] == stage
+    bad_key = [(101, [fmt.encode_run([fmt.put("5.a", b"1"), fmt.put("nodot", b"2")])])]
+    quirk = [(102, [fmt.encode_run([fmt.put("007.a", b"1")])]), (103, [fmt.encode_run([fmt.put("7.0", b"2")])])]
+    for sts in (streams + bad_key, quirk):  # (quirk alone: the two keys must be neighbours in merged order)
+        exp, got = _run_both(dev, sts, 4 * MiB, _abi.SKV_SPLIT_BY_TABLE)
+        assert exp == got, _diff(exp, got)
+        assert dev.timings()["wal_stage"] == 2
+    old = os.environ.get("SKV_WAL_FUSED")
+    os.environ["SKV_WAL_FUSED"] = "0"
+    try:
+        exp, got = _run_both(dev, streams, 4 * MiB, _abi.SKV_SPLIT_BY_TABLE)
+        assert exp == got, _diff(exp, got)
+        assert dev.timings()["wal_stage"] == 2
+    finally:
+        if old is None:
+            os.environ.pop("SKV_WAL_FUSED", None)
+        else:
+            os.environ["SKV_WAL_FUSED"] = old
+
+
 def test_wal_config5_shape(dev):
     """Config-5 record shape (32 B keys "{table}.{suffix}", 8 B values) at a 16-run fan-in like
     the reference job (wal_compaction.rs:18), and at 1000 runs."""
