@@ -328,9 +328,10 @@ def main():
     if rank == 0 and world == 1 and config in ("2A", "2B"):
         import threading
 
-        comps = [comp, Compactor(dev_idx)]
-        comps[1].compact_dev(table, max_run, flags).free()
-        n_each = max(2, args.steps // 2)
+        comps = [Compactor(dev_idx), Compactor(dev_idx)]  # (no per-phase event timing on these)
+        for c in comps:
+            c.compact_dev(table, max_run, flags).free()
+        n_each = max(10, args.steps)
 
         def worker(c):
             for _ in range(n_each):
@@ -349,7 +350,8 @@ def main():
                       "ms_per_compaction": round(dt / (2 * n_each) * 1e3, 4), "calls": 2 * n_each,
                       "note": "2 ctxs x %d skv_compact_dev calls from 2 host threads, same inputs; wall / calls"
                               % n_each}
-        comps[1].close()
+        for c in comps:
+            c.close()
 
     # PCIe-inclusive figure (not `value`): the host entry point skv_compact with the inputs in
     # pinned host memory and the output runs returned in pinned host memory.
