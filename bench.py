@@ -209,7 +209,8 @@ def main():
     ap.add_argument("--run-mib", type=int, default=16, help="config 3 run size")
     ap.add_argument("--wal-runs", type=int, default=1_000_000, help="config 5 stream count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-memory figure")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the extra figures: PCIe-inclusive host memory, two ctxs in flight")
     ap.add_argument("--cpu-sample-records", type=int, default=238821 // 16)
     ap.add_argument("--cpu-repeats", type=int, default=5)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -325,7 +326,7 @@ def main():
     # GPU, 2 calls in flight -- one call's splitter phase and host gaps beside the other's tile phase
     # (tools/overlap_probe.py). ms per compaction = wall / calls.
     concurrent = None
-    if rank == 0 and world == 1 and config in ("2A", "2B"):
+    if rank == 0 and world == 1 and config in ("2A", "2B") and not args.no_host_path:
         import threading
 
         comps = [Compactor(dev_idx), Compactor(dev_idx)]  # (no per-phase event timing on these)
