@@ -390,6 +390,14 @@ __device__ __forceinline__ WalRec wal_parse(const uint8_t* rp, uint64_t size) {
 }
 
 constexpr uint32_t WF_BADKEY = 1, WF_ORDER = 2, WF_TABLES = 4;
+constexpr uint32_t WF_TBL = 4096;  // output blocks of a workgroup's span with a piece table (64 KiB)
+static_assert(WAL_G <= 256, "piece ids in the block table are bytes");
+struct WalPrev {
+    int64_t tid;
+    uint64_t size, rp;
+    uint32_t strip, klen;
+    bool canon;
+};
 
 __global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ m_src,
                                                      const uint64_t* __restrict__ P, const uint64_t* __restrict__ Dp,
@@ -399,6 +407,8 @@ __global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict_
     __shared__ uint64_t os[WAL_G + 1], src[WAL_G], head[WAL_G];
     __shared__ uint32_t hl[WAL_G];
     __shared__ uint64_t s_w[WAL_G / 64], s_base[1];
+    __shared__ WalPrev s_prev[WAL_G / 64];  // each wave's last record, for the next wave's lane 0
+    __shared__ uint8_t s_tbl[WF_TBL];
     __shared__ uint32_t s_t;
     const uint64_t K = *Kp;
     if (threadIdx.x == 0) s_t = atomicAdd(ticket, 1u);
@@ -417,13 +427,32 @@ __global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict_
         r = wal_parse(rp, P[j + 1] - P[j]);
         if (r.err) bad |= WF_BADKEY;
     }
-    // the record before: the neighbouring lane, or (a wave's lane 0) parsed again
+    // the record before: the neighbouring lane; a wave's lane 0 takes the previous wave's last lane
+    // through LDS, and only the workgroup's first record parses its predecessor again
+    if (lane == 63) {
+        s_prev[wv].tid = r.tid;
+        s_prev[wv].strip = r.strip;
+        s_prev[wv].klen = r.klen;
+        s_prev[wv].canon = r.canon;
+        s_prev[wv].size = r.size;
+        s_prev[wv].rp = (uint64_t)rp;
+    }
+    __syncthreads();
     int64_t ptid = __shfl_up(r.tid, 1, 64);
     uint32_t pstrip = __shfl_up(r.strip, 1, 64), pklen = __shfl_up(r.klen, 1, 64);
     bool pcanon = __shfl_up(r.canon ? 1 : 0, 1, 64) != 0;
     uint64_t psize = __shfl_up(r.size, 1, 64);
     const uint8_t* prp = (const uint8_t*)__shfl_up((uint64_t)rp, 1, 64);
-    if (live && lane == 0 && j > 0) {
+    if (lane == 0 && wv > 0) {
+        const WalPrev& q = s_prev[wv - 1];
+        ptid = q.tid;
+        pstrip = q.strip;
+        pklen = q.klen;
+        pcanon = q.canon;
+        psize = q.size;
+        prp = (const uint8_t*)q.rp;
+    }
+    if (live && threadIdx.x == 0 && j > 0) {
         prp = (const uint8_t*)m_src[j - 1];
         const WalRec q = wal_parse(prp, P[j] - P[j - 1]);
         ptid = q.tid;
@@ -536,13 +565,32 @@ __global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict_
     const uint32_t c = (uint32_t)(K - j0 < WAL_G ? K - j0 : WAL_G);
     const uint64_t lo = os[0], hi = os[c];
     const uint64_t Blo = lo & ~15ull, Bhi = (hi + 15) & ~15ull;
+    // block -> piece holding its first byte (lo for the first block), marked by the pieces
+    // themselves when the span fits the table; else a binary search over the pieces per block
+    const uint64_t q0 = Blo >> 4;
+    const bool use_tbl = (Bhi >> 4) - q0 <= WF_TBL;
+    if (use_tbl) {
+        if (live) {
+            uint64_t qs = (ostart + 15) >> 4;
+            const uint64_t qe = (ostart + wo + 15) >> 4;
+            if (threadIdx.x == 0) s_tbl[0] = 0;
+            if (qs <= q0) qs = q0 + 1;
+            for (uint64_t q = qs; q < qe; ++q) s_tbl[q - q0] = (uint8_t)threadIdx.x;
+        }
+        __syncthreads();
+    }
     for (uint64_t B = Blo + 16ull * threadIdx.x; B < Bhi; B += 16ull * WAL_G) {
         const uint64_t x0 = B > lo ? B : lo, x1 = B + 16 < hi ? B + 16 : hi;
-        uint32_t a = 0, bb = c;  // last record with os <= x0
-        while (bb - a > 1) {
-            const uint32_t mid = (a + bb) >> 1;
-            if (os[mid] <= x0) a = mid;
-            else bb = mid;
+        uint32_t a = 0;  // last record with os <= x0
+        if (use_tbl) {
+            a = s_tbl[(B >> 4) - q0];
+        } else {
+            uint32_t bb = c;
+            while (bb - a > 1) {
+                const uint32_t mid = (a + bb) >> 1;
+                if (os[mid] <= x0) a = mid;
+                else bb = mid;
+            }
         }
         const uint4 v = wal_compose(B, x0, x1, a, os, src, head, hl);
         if (x0 == B && x1 == B + 16) {
