@@ -458,6 +458,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     unsigned long long* d_first_dec = dbuf<unsigned long long>(ctx, "first_dec", k);
     std::vector<uint64_t>& first_dec = ctx->s_first_dec;
     first_dec.resize(k);  // read back, or filled with ~0 on the deferred path
+    bool dec_none = false;  // no stream has a decrease (flags[1] clear): first_dec not read back, all ~0
     uint32_t hflags[4];
     // per stream (rank order): base index, valid record count n_s and the first error
     auto stream_tables = [&]() {  // blocks of streams on host threads (10^6-stream calls)
@@ -513,20 +514,25 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         if (!read_broken && !job.batch)  // a writer batch is unsorted by definition
             launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
         HIPCHK(hipGetLastError());
-        uint8_t* hp = (uint8_t*)pinned(ctx, k * 8 + 16 + (read_broken ? n_runs * 4 : 0) + 16);
-        d2h(ctx, hp, d_first_dec, (size_t)k * 8);
-        d2h(ctx, hp + (size_t)k * 8, d_flags, 16);
-        uint8_t* hu = hp + k * 8 + 16 + (read_broken ? n_runs * 4 : 0);
-        d2h(ctx, hu, utf8_bad, 4);
-        if (read_broken) d2h(ctx, hp + (size_t)k * 8 + 16, d_broken, (size_t)n_runs * 4);
+        // the verdict words first; the 10^6-entry tables only when a word says they hold something:
+        // every writer of first_dec also sets flags[1], every broken run also flags[2]
+        uint8_t* hp = (uint8_t*)pinned(ctx, 64);
+        d2h(ctx, hp, d_flags, 16);
+        d2h(ctx, hp + 16, utf8_bad, 4);
         sync(ctx);
-        memcpy(first_dec.data(), hp, (size_t)k * 8);
-        memcpy(hflags, hp + (size_t)k * 8, 16);
-        memcpy(&utf8_flag, hu, 4);
+        memcpy(hflags, hp, 16);
+        memcpy(&utf8_flag, hp + 16, 4);
+        const bool need_dec = hflags[1] != 0, need_broken = read_broken && hflags[2] != 0;
+        dec_none = !need_dec;
         bool broken = false;
-        if (read_broken) {
-            const uint32_t* b = (const uint32_t*)(hp + (size_t)k * 8 + 16);
-            for (uint32_t r = 0; r < n_runs && !broken; ++r) broken = b[r] != 0;
+        if (need_dec || need_broken) {
+            uint8_t* hq = (uint8_t*)pinned(ctx, (size_t)k * 8 + (size_t)n_runs * 4 + 16);
+            if (need_dec) d2h(ctx, hq, d_first_dec, (size_t)k * 8);
+            if (need_broken) d2h(ctx, hq + (size_t)k * 8, d_broken, (size_t)n_runs * 4);
+            sync(ctx);
+            if (need_dec) memcpy(first_dec.data(), hq, (size_t)k * 8);
+            const uint32_t* b = (const uint32_t*)(hq + (size_t)k * 8);
+            for (uint32_t r = 0; need_broken && r < n_runs && !broken; ++r) broken = b[r] != 0;
         }
         return broken;
     };
@@ -744,10 +750,11 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     mark(ctx, PH_CHECK);
     htrace("check done");
     tables_mine();
+    if (dec_none && (any_err || job.search)) std::fill(first_dec.begin(), first_dec.end(), ~0ull);  // (rare paths read it)
     if (job.search) return search_stage(ctx, job, runs[0], R, stream_err[0], first_dec[0], rec_addr, rec_hi, rec_lo,
                                         rec_klen, rec_meta);
     bool any_dec = false;
-    for (uint32_t s = 0; s < k; ++s)
+    for (uint32_t s = 0; !dec_none && s < k; ++s)
         if (first_dec[s] != ~0ull && first_dec[s] + 1 < stream_valid[s]) any_dec = true;
 
     // ---- ScanFromRun (skv_scan_host.hip): the per-run key filter (cache_service.rs:125-129) on the
