@@ -41,7 +41,8 @@ for C in $CS; do
         || { echo "pmc $C $grp failed"; exit 1; }
       cd "$R"
     done
-    python3 tools/traffic.py "$O/pmc_$C" "$C" "$O/traffic.json" | head -6
+    python3 tools/traffic.py "$O/pmc_$C" "$C" "$O/traffic.json" > "$O/traffic_$C.txt" || { echo "traffic $C failed"; exit 1; }
+    head -6 "$O/traffic_$C.txt"  # (a pipe into head broke traffic.py's output before it wrote the file)
     rm -rf "$O/pmc_$C"
     echo "pmc $C done"
   fi
