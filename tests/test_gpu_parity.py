@@ -199,15 +199,18 @@ def test_wal_split_matches_oracle(dev):
 def test_wal_one_pass_stage(dev):
     """The one-pass WAL stage (k_wal_fused) where it applies -- sorted streams, good keys, ascending
     stripped keys, every table within max -- and the exact stage where it declines: many tables across
-    many 256-record workgroups, Deletes, tables of one record, a table over max, a bad key, "007.a"
+    many 256-record workgroups, short and long records, Deletes, tables of one record, a table over
+    max, a bad key, "007.a"
     next to "7.0" (one table whose stripped keys decrease). Every outcome equal to the oracle's."""
     r = random.Random(29)
     tables = [str(t) for t in range(-40, 300)]
     streams = []
     for s in range(12):
         keys = sorted({f"{r.choice(tables)}.{r.randrange(10**6):06d}" for _ in range(2500)})
-        ops = [fmt.put(k, bytes(r.randrange(256) for _ in range(r.randrange(0, 20)))) if r.random() < .9
-               else fmt.delete(k) for k in keys]
+        # short and long records mixed (a workgroup's output span past k_wal_fused's block table too)
+        ops = [fmt.put(k, bytes(r.randrange(256) for _ in range(r.randrange(0, 20) if r.random() < .8
+                                                                 else r.randrange(50, 300))))
+               if r.random() < .9 else fmt.delete(k) for k in keys]
         streams.append((s + 1, [fmt.encode_run(ops)]))
     single = [(100, [fmt.encode_run([fmt.put("777.x", b"only")])])]
     for sts, max_size, stage in ((streams, 4 * MiB, 1), (streams + single, 4 * MiB, 1), (streams, 600, 2)):
