@@ -618,9 +618,13 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             alloc_records();
             htrace("record tables");
             h2d_up(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
+            // the record sort merges on dense key ranks: no key fingerprints to compute then
+            const char* se = getenv("SKV_SORT");
+            const bool will_sort = (k > (uint32_t)TILE_TARGET / 2 && R > (uint64_t)TILE_CAP) || (se && se[0] == '1') ||
+                                   job.batch;
             launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
-                               rec_meta, d_flags, d_stream_base, job.batch ? nullptr : d_first_dec, rec_fp,
-                               dbuf<uint32_t>(ctx, "wave_run", (R + 63) / 64 + 1));
+                               rec_meta, d_flags, d_stream_base, job.batch ? nullptr : d_first_dec,
+                               will_sort ? nullptr : rec_fp, dbuf<uint32_t>(ctx, "wave_run", (R + 63) / 64 + 1));
             mark(ctx, PH_PARSE);
             if (allow_deferred && !(job.flags & SKV_SPLIT_BY_TABLE) && !job.search && !job.scan) {
                 deferred = true;  // verdict read with the result

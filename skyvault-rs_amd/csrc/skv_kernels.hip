@@ -348,7 +348,7 @@ __device__ __forceinline__ void put_rec(uint64_t o, const uint8_t* rp, const Rec
                                         uint64_t* rec_hi, uint64_t* rec_lo, uint32_t* rec_klen, uint32_t* rec_meta,
                                         uint32_t* flags, uint64_t* rec_fp, uint64_t fpv) {
     rec_addr[o] = (uint64_t)rp;
-    rec_fp[o] = fpv;
+    if (rec_fp) rec_fp[o] = fpv;
     rec_hi[o] = h.hi;
     rec_lo[o] = h.lo;
     rec_klen[o] = (uint32_t)h.klen;
@@ -505,7 +505,7 @@ __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, 
         if (act) {
             bool ascii;
             put_rec(i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp,
-                    key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii));
+                    rec_fp ? key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii) : 0);
         }
     }
     // a Delete of the run's record size (k_run_header's hypothesis is a Put): flags[3] bit 0, so
