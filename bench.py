@@ -56,8 +56,12 @@ def cpu_baseline(config, sample_records, n_streams, vsize, repeats, run_mib=16):
         sample = (f"{n_streams} streams x {sample_records} records x {9 + 16 + vsize} B (config-{config} shape, "
                   f"1/{round(238821 / sample_records)} of the records)")
     elif config in ("3", "3F"):
-        streams = gen.config3(seed=0xC0FFEE, n_streams=n_streams, run_bytes=(min(run_mib, 16) << 20) // 16)
-        sample = f"{n_streams} streams x {run_mib / 16:.2f} MiB runs (config-3 shape, 1/16 of the bench's runs)"
+        # runs of run_mib / 16 MiB, at most 1 MiB (the bench's own runs are run_mib MiB: 16 for
+        # config 3, 256 for 3F)
+        sample_bytes = (min(run_mib, 16) << 20) // 16
+        streams = gen.config3(seed=0xC0FFEE, n_streams=n_streams, run_bytes=sample_bytes)
+        sample = (f"{n_streams} streams x {sample_bytes / 2**20:.2f} MiB runs (config-{config} shape, "
+                  f"1/{round((run_mib << 20) / sample_bytes)} of the bench's {run_mib} MiB runs)")
     else:
         from skv import _abi
         from skv.devgen import make_cfg5_on_device
@@ -239,6 +243,7 @@ def main():
 
     seed = rank_seed(rank)
     config = args.config or "2" + args.variant
+    run_mib_used = (256 if args.run_mib == 16 else args.run_mib) if config == "3F" else args.run_mib
     flags, max_run = 0, MAX_RUN
     if config in ("2A", "2B"):
         runs = make_cfg2_on_device(device, seed, args.streams, args.records, args.vsize, config[1])
@@ -368,8 +373,14 @@ def main():
             hts.append(time.perf_counter() - t1)
         ht = min(hts)
         parts = int(comp.timings()["host_parts"])
+        # the drop-in entry point's own output, checked like the device line's (bit-exact parity at
+        # this size: tests/test_gpu_fullsize.py::test_config*_host_entry_full_size)
+        hr = comp.compact_host(hstreams, max_run, flags)
+        host_inv = check_invariants(hr, config, max_run, hr.in_records)
+        host_inv["parts"] = int(comp.timings()["host_parts"])
+        hr.free()
         host_path = {"value": round(in_bytes / ht / GiB, 3), "unit": "GiB/s", "ms": round(ht * 1e3, 3),
-                     "h2d_bytes": in_bytes, "d2h_bytes": hb, "parts": parts,
+                     "h2d_bytes": in_bytes, "d2h_bytes": hb, "parts": parts, "invariants": host_inv,
                      "note": "skv_compact: pinned host inputs -> HBM -> compaction -> pinned host output, "
                              "best of 2 after 1 warm-up, " + (
                                  f"{parts} key-range parts with H2D, kernels and D2H overlapped" if parts
@@ -504,7 +515,7 @@ def main():
             line["concurrent_2ctx"] = concurrent
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(config, args.cpu_sample_records, n_streams if config != "5" else 0,
-                                            args.vsize, args.cpu_repeats, args.run_mib)
+                                            args.vsize, args.cpu_repeats, run_mib_used)
         print(json.dumps(line), flush=True)
     comp.close()
     if dist is not None:

@@ -539,6 +539,17 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
 
     // ---- fast path: every run fixed-stride (one record size per run) -> one verifying pass ------
     bool parsed = false, deferred = false;
+    // The merge's choice between the splitter merge and the record sort (skv_sort.hip): past
+    // TILE_TARGET / 2 streams the splitter table does not fit; SKV_SORT=1 forces the sort (tests).
+    // Made where the fixed-stride parse decides whether to write key fingerprints, and kept: a parse
+    // that skipped them (fp_skipped) commits the call to the sort, which merges on dense ranks -- the
+    // splitter merge would read unwritten fingerprints (a scan's key filter can shrink R in between).
+    const char* sort_env = getenv("SKV_SORT");
+    auto sort_by_fan_in = [&](uint64_t nrec) {
+        return (k > (uint32_t)TILE_TARGET / 2 && nrec > (uint64_t)TILE_CAP) || (sort_env && sort_env[0] == '1') ||
+               job.batch;
+    };
+    bool fp_skipped = false;
     bool any_fixed = false;  // some run is fixed-stride: the general parse also runs k_emit_fixed
     uint32_t uniform_meta = 0;  // every record a Put of one size (the fixed path's runs, one format): its meta
     uint64_t first_sum = 0, first_n = 0;  // the runs' first-record sizes (record capacity of the span parse)
@@ -619,9 +630,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             htrace("record tables");
             h2d_up(ctx, d_recb, recb.data(), (n_runs + 1) * 8);
             // the record sort merges on dense key ranks: no key fingerprints to compute then
-            const char* se = getenv("SKV_SORT");
-            const bool will_sort = (k > (uint32_t)TILE_TARGET / 2 && R > (uint64_t)TILE_CAP) || (se && se[0] == '1') ||
-                                   job.batch;
+            const bool will_sort = sort_by_fan_in(R);
+            fp_skipped = will_sort;  // then the merge below must take the record sort whatever R becomes
             launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
                                rec_meta, d_flags, d_stream_base, job.batch ? nullptr : d_first_dec,
                                will_sort ? nullptr : rec_fp, dbuf<uint32_t>(ctx, "wave_run", (R + 63) / 64 + 1));
@@ -638,6 +648,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             // one size everywhere and no Delete among the records (read with the verdict): one meta
             if (parsed && !deferred && uniform && !(hflags[3] & 1u)) uniform_meta = (uint32_t)f0.S;
             if (!parsed) {  // a run is not what its first record promised: general parse
+                fp_skipped = false;  // (the general parse writes every fingerprint)
                 R = 0;
                 any_err = false;
                 std::fill(stream_err.begin(), stream_err.end(), 0u);
@@ -943,8 +954,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     std::vector<uint64_t> list_off = stream_base;
     uint64_t* d_list_off = d_stream_base;
     {
-        const char* se = getenv("SKV_SORT");
-        if ((k > (uint32_t)TILE_TARGET / 2 && R > (uint64_t)TILE_CAP) || (se && se[0] == '1') || job.batch) {
+        if (sort_by_fan_in(R) || fp_skipped) {
             if (heap) {
                 // sort on the merge keys; the records' own keys, payload and meta follow in sorted
                 // order, and inv maps an original record index to its sorted position
@@ -1403,7 +1413,7 @@ int skv_compact_dev(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams,
     htrace("entry");
     if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
     *out = nullptr;
-    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    SKV_DEVICE_SCOPE(ctx);
     Job job;  // its tables borrow the ctx's storage for the call (no fresh 10^6-entry vectors)
     job.ranked.swap(ctx->j_ranked);
     job.run_ptr.swap(ctx->j_ptr);
@@ -1422,7 +1432,7 @@ int skv_encode_batch_dev(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uin
     const double t_entry = now_ms();
     if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
     *out = nullptr;
-    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    SKV_DEVICE_SCOPE(ctx);
     Job job;
     int rc = batch_job(ctx, ops_run, len, max_run_size, job);
     if (rc) return rc;

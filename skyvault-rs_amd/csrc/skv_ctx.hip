@@ -414,9 +414,10 @@ int skv_ctx_create(int device, skv_ctx** out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return SKV_E_DEVICE;
     if (device < 0 || device >= n) return SKV_E_INVALID_ARG;
+    DeviceScope scope(device);
     skv_ctx* ctx = new skv_ctx();
     ctx->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (!scope.ok || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return SKV_E_DEVICE;
     }
@@ -427,7 +428,7 @@ int skv_ctx_create(int device, skv_ctx** out) {
 
 void skv_ctx_destroy(skv_ctx* ctx) {
     if (!ctx) return;
-    (void)hipSetDevice(ctx->device);
+    DeviceScope scope(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
 #if SKV_TILE_PROF
     if (ctx->bufs.count("tile_prof")) {

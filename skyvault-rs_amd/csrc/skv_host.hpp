@@ -137,6 +137,25 @@ struct ResultBox {  // skv_result + how to free it
 
 int set_err(skv_ctx* ctx, int code, const char* fmt, ...);
 
+// Every C-ABI entry point runs on its ctx's device and leaves the caller's current device as it
+// found it (a host thread that drives several GPUs must not find its device switched by a call).
+struct DeviceScope {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceScope(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
+#define SKV_DEVICE_SCOPE(ctx)                                                                       \
+    DeviceScope dev_scope_((ctx)->device);                                                          \
+    if (!dev_scope_.ok) return set_err((ctx), SKV_E_DEVICE, "hipSetDevice failed")
+
 #define HIPCHK(x)                                                                                   \
     do {                                                                                            \
         hipError_t e_ = (x);                                                                        \

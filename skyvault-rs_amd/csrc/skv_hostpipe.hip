@@ -734,6 +734,16 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
             return SKV_OK;
         }
         const uint64_t n = pres->n_runs;
+        // Part p read the carried open run at d_out + open_off while writing its own output from that
+        // same address. That is safe because the merge re-emits the open run first and unchanged --
+        // every key of it sorts before every key of part p, and it is under max_run_size, so
+        // build_runs keeps it whole as (the start of) part p's first run: each output byte the part
+        // writes there is the byte it read. Checked: part p's first run starts at the open run's offset
+        // and holds at least its bytes; anything else would mean the input was overwritten.
+        if (open_len && (n == 0 || pres->runs[0].off != 0 || pres->runs[0].len < open_len)) {
+            skv_result_free(pres);
+            throw DevError("internal: general pipeline part " + std::to_string(p) + " did not re-emit the open run");
+        }
         const bool last_part = p + 1 == P;
         in_records += pres->in_records - (open_len ? open_recs : 0);  // the carried run's records once
         for (uint64_t r = 0; r < n; ++r) {
@@ -837,7 +847,7 @@ int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams, uin
     htrace("entry");
     if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
     *out = nullptr;
-    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    SKV_DEVICE_SCOPE(ctx);
     Job job;  // lent ctx tables, as in skv_compact_dev
     job.ranked.swap(ctx->j_ranked);
     job.run_ptr.swap(ctx->j_ptr);
@@ -870,7 +880,7 @@ int skv_encode_batch(skv_ctx* ctx, const uint8_t* ops_run, uint64_t len, uint64_
     const double t_entry = now_ms();
     if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
     *out = nullptr;
-    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    SKV_DEVICE_SCOPE(ctx);
     Job job;
     int rc = batch_job(ctx, ops_run, len, max_run_size, job);
     if (rc) return rc;

@@ -99,7 +99,7 @@ int skv_search_run(skv_ctx* ctx, const uint8_t* run, uint64_t len, const uint8_t
         for (uint32_t i = 0; i < n_keys; ++i) out[i] = skv_lookup{SKV_LOOKUP_PANIC, pc, 0, 0};
         return set_err(ctx, SKV_E_FORMAT, "%s", search_panic_text(pc).c_str());
     }
-    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    SKV_DEVICE_SCOPE(ctx);
     Job job;
     int rc = batch_job(ctx, run, len, 1ull << 62, job);
     if (rc) return rc;
@@ -131,7 +131,7 @@ int skv_run_index_create(skv_ctx* ctx, const uint8_t* run, uint64_t len, skv_run
     if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
     *out = nullptr;
     if (len && !run) return set_err(ctx, SKV_E_INVALID_ARG, "run is NULL");
-    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    SKV_DEVICE_SCOPE(ctx);
     std::unique_ptr<skv_run_index> ix(new (std::nothrow) skv_run_index());
     if (!ix) return set_err(ctx, SKV_E_DEVICE, "host allocation failed");
     ix->device = ctx->device;
@@ -182,7 +182,7 @@ int skv_run_index_search(skv_ctx* ctx, const skv_run_index* ix, const uint8_t* k
         for (uint32_t i = 0; i < n_keys; ++i) out[i] = skv_lookup{SKV_LOOKUP_PANIC, ix->panic_all, 0, 0};
         return set_err(ctx, SKV_E_FORMAT, "%s", search_panic_text(ix->panic_all).c_str());
     }
-    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    SKV_DEVICE_SCOPE(ctx);
     try {
         search_launch(ctx, ix->run, ix->len, ix->clean, ix->R, ix->addr, ix->hi, ix->lo, ix->klen, ix->meta, keys,
                       key_offs, n_keys, out);

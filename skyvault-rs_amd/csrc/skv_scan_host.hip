@@ -157,7 +157,7 @@ int skv_scan_runs(skv_ctx* ctx, const uint8_t* const* runs, const uint64_t* run_
     const double t_entry = now_ms();
     if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
     *out = nullptr;
-    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    SKV_DEVICE_SCOPE(ctx);
     Job job;
     const int rc = scan_job(ctx, runs, run_lens, n_runs, start_key, start_len, max_results, job);
     if (rc) return rc;
@@ -169,7 +169,7 @@ int skv_scan_runs_dev(skv_ctx* ctx, const uint8_t* const* runs, const uint64_t* 
     const double t_entry = now_ms();
     if (!ctx || !out) return set_err(ctx, SKV_E_INVALID_ARG, "ctx/out is NULL");
     *out = nullptr;
-    if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, SKV_E_DEVICE, "hipSetDevice failed");
+    SKV_DEVICE_SCOPE(ctx);
     Job job;
     const int rc = scan_job(ctx, runs, run_lens, n_runs, start_key, start_len, max_results, job);
     if (rc) return rc;

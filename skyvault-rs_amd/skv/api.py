@@ -124,6 +124,21 @@ class DeviceResult:
             pass
 
 
+class HostResult(DeviceResult):
+    """Output of skv_compact (host inputs): the run bytes are in pinned host memory owned by the
+    result (skv_result_free gives them back to the ctx's pool)."""
+
+    def host_bytes(self, start: int = 0, length: Optional[int] = None):
+        """A numpy view of output bytes [start, start + length) -- valid until free()."""
+        import numpy as np
+
+        n = self.n_bytes - start if length is None else length
+        assert 0 <= start and start + n <= self.n_bytes
+        if n == 0:
+            return np.empty(0, dtype=np.uint8)
+        return np.ctypeslib.as_array((C.c_uint8 * n).from_address(self.dev_ptr + start))
+
+
 class Compactor:
     def __init__(self, device: int = 0, profiling: bool = False):
         self.lib = load()
@@ -191,6 +206,16 @@ class Compactor:
             return (int(res.contents.n_bytes), int(res.contents.n_runs))
         finally:
             self.lib.skv_result_free(res)
+
+    def compact_host(self, streams, max_run_size: int = MAX_RUN_SIZE, flags: int = 0) -> HostResult:
+        """skv_compact on raw host buffers ([(seq_no, [(host_ptr, length)])] or a StreamArgs built
+        with device=True), keeping the result: bytes in pinned host memory plus the descriptors."""
+        sa = streams if isinstance(streams, StreamArgs) else StreamArgs(streams, device=True)
+        res = C.POINTER(SkvResult)()
+        rc = self.lib.skv_compact(self.ctx, sa.ptr, sa.n, max_run_size, flags, C.byref(res))
+        if rc != SKV_OK:
+            raise self._err(rc)
+        return HostResult(self.lib, res, self)
 
     def encode_batch(self, ops_run: bytes, max_run_size: int = MAX_RUN_SIZE, with_info: bool = False):
         """Writer batch encode (writer_service.rs:148-162): ops_run = the batch's ops in request

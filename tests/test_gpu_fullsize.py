@@ -127,6 +127,86 @@ def test_config2_full_size(dev, torch, variant):
 
 
 # ------------------------------------------------------------------------------------------
+# the host-memory entry point (skv_compact) at BASELINE size, default pipeline thresholds
+
+
+@pytest.fixture
+def default_pipe_env():
+    """skv_compact with its shipped thresholds: no SKV_HOST_PIPE* / SKV_HOST_PARTS override."""
+    keys = ("SKV_HOST_PIPE", "SKV_HOST_PIPE_MIN", "SKV_HOST_PARTS", "SKV_INGEST")
+    old = {k: os.environ.pop(k, None) for k in keys}
+    yield
+    for k, v in old.items():
+        if v is not None:
+            os.environ[k] = v
+
+
+def _pinned_copies(torch, runs):
+    return [r.cpu().pin_memory() for r in runs]
+
+
+def _check_host_result(hr, exp, descs, info, what):
+    assert (hr.n_bytes, hr.n_runs, hr.out_records) == (exp.size, len(descs), info["out_records"]), what
+    for q in range(0, exp.size, 1 << 30):
+        got = hr.host_bytes(q, min(1 << 30, exp.size - q))
+        part = exp[q:q + got.size]
+        if not np.array_equal(got, part):
+            raise AssertionError(f"{what}: output byte {q + _first_diff(got, part)} differs")
+    assert hr.descs == descs, what
+
+
+def test_config2_host_entry_full_size(dev, torch, default_pipe_env):
+    """config 2A through skv_compact with pinned host inputs (storage.rs:226-250 get_run -> compact
+    -> put_run, table_buffer_compaction.rs:103-121): 4 GiB, so the fused key-range pipeline runs
+    with its own part count (15 parts); every byte and descriptor equal to the oracle's."""
+    from skv.devgen import make_cfg2_on_device
+
+    device = torch.device("cuda", 0)
+    _progress("config 2A host entry: generating")
+    runs = make_cfg2_on_device(device, SEED, 64, 238821, 256, "A")
+    host = _pinned_copies(torch, runs)
+    del runs
+    torch.cuda.empty_cache()
+    streams = [(s + 1, [(h.data_ptr(), h.numel())]) for s, h in enumerate(host)]
+    hr = dev.compact_host(streams, MAX_RUN, 0)
+    t = dev.timings()
+    assert t["host_parts"] >= 2, t  # the pipeline, not the serial copies
+    _progress(f"config 2A host entry: {t['host_parts']} parts; oracle")
+    arrs = [h.numpy() for h in host]
+    sa = _abi.stream_table(np.arange(1, 65), [a.ctypes.data for a in arrs], [a.size for a in arrs])
+    exp, descs, info = pyoracle.compact_np(sa, MAX_RUN, 0)
+    _check_host_result(hr, exp, descs, info, "config 2A host entry")
+    assert hr.n_runs == 1025
+    hr.free()
+
+
+def test_config3_host_entry_full_size(dev, torch, default_pipe_env):
+    """config 3's shape (256 streams, variable 8-128 B keys, 10 % Deletes) at 256 x 16 MiB (3.7 GiB)
+    through skv_compact with pinned host inputs: the general key-range pipeline with its own part
+    count (~1 GiB parts) and the open output run carried across parts. Flags 0 and the Delete
+    filter; every byte and descriptor equal to the oracle's."""
+    from skv.devgen import make_cfg3_on_device
+
+    device = torch.device("cuda", 0)
+    _progress("config 3 host entry: generating")
+    runs = make_cfg3_on_device(device, SEED, 256, 16)
+    host = _pinned_copies(torch, runs)
+    del runs
+    torch.cuda.empty_cache()
+    streams = [(s + 1, [(h.data_ptr(), h.numel())]) for s, h in enumerate(host)]
+    arrs = [h.numpy() for h in host]
+    sa = _abi.stream_table(np.arange(1, 257), [a.ctypes.data for a in arrs], [a.size for a in arrs])
+    for flags in (0, _abi.SKV_DROP_TOMBSTONES):
+        hr = dev.compact_host(streams, MAX_RUN, flags)
+        t = dev.timings()
+        assert t["host_parts"] >= 2 and t["path"] == _abi.PATH_GENERAL, t
+        _progress(f"config 3 host entry flags {flags}: {t['host_parts']} parts; oracle")
+        exp, descs, info = pyoracle.compact_np(sa, MAX_RUN, flags)
+        _check_host_result(hr, exp, descs, info, f"config 3 host entry flags {flags}")
+        hr.free()
+
+
+# ------------------------------------------------------------------------------------------
 # config 5: 10^6 WAL runs, oracle per group of whole tables
 
 
