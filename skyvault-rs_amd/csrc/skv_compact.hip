@@ -68,7 +68,8 @@ constexpr uint32_t WF_TCAP = 1u << 16, WF_GUESS = 1024;
 static int wal_fused(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, const uint64_t* m_src,
                      const uint64_t* m_P, const uint64_t* m_Dp, const uint32_t* fp_bad, skv_result** out) {
     hipStream_t st = ctx->stream;
-    uint8_t* d_out = dbuf<uint8_t>(ctx, "out", job.in_bytes + R + 16);
+    // a part of a pipelined host call writes into the call's shared output buffer
+    uint8_t* d_out = job.dev_out ? job.dev_out : dbuf<uint8_t>(ctx, "out", job.in_bytes + R + 16);
     const uint64_t nwg = (R + WAL_FUSED_G - 1) / WAL_FUSED_G;
     uint64_t* tstate = dbuf<uint64_t>(ctx, "wf_state", nwg + 1);
     uint32_t* words = dbuf<uint32_t>(ctx, "wf_words", 4);  // ticket, fail bits, table count
@@ -79,8 +80,10 @@ static int wal_fused(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
     HIPCHK(hipMemsetAsync(tail, 0, 64, st));
     mark(ctx, PH_CHAIN);
     const char* fe = getenv("SKV_WAL_FUSED");
+    // in a key-range part every key must carry the canonical "{id}." prefix: the cuts are canonical
+    // prefixes, so only then does no table straddle two parts (WAL_STRICT_CANON)
     launch_wal_fused(st, d_K, R, m_src, m_P, m_Dp, d_out, tstate, words, words + 1, tl, words + 2, WF_TCAP, tail,
-                     fe && fe[0] == '2' ? 2u : 0u);
+                     (fe && fe[0] == '2' ? 2u : 0u) | (job.part ? WAL_STRICT_CANON : 0u));
     HIPCHK(hipGetLastError());
     mark(ctx, PH_GATHER);
     uint8_t* hp = (uint8_t*)pinned(ctx, 128 + WF_GUESS * sizeof(WalTStart));
@@ -150,6 +153,10 @@ int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, con
             return rc;
         }
     }
+    // A part of a pipelined host call takes only the one-pass outcome (every table kept, whole inside
+    // the part): a dropped table, a bad key or a non-canonical prefix ends the attempt, and the serial
+    // path gives the reference's outcome for the whole call.
+    if (job.part) throw ApiError{SKV_E_FORMAT, "part: the WAL stage needs the exact path"};
     ctx->timings.wal_stage = 2;
     uint64_t K = 0;
     {
@@ -771,6 +778,11 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     bool any_dec = false;
     for (uint32_t s = 0; !dec_none && s < k; ++s)
         if (first_dec[s] != ~0ull && first_dec[s] + 1 < stream_valid[s]) any_dec = true;
+    // A key-range part of a pipelined host call (skv_hostpipe.hip) holds the slices a cut by key
+    // gave: with a decode error or a key decrease in a slice, the cut itself is not a key range and
+    // the reference's outcome depends on the whole call's pop order (heap-order mode, error order).
+    // The part ends the attempt; the serial path gives the exact outcome.
+    if (job.part && (any_err || any_dec)) throw ApiError{SKV_E_FORMAT, "part: error or decrease in a slice"};
 
     // ---- ScanFromRun (skv_scan_host.hip): the per-run key filter (cache_service.rs:125-129) on the
     // record arrays, before the merge; a run's decode error surfaces after the pop of its last kept

@@ -28,9 +28,10 @@ static bool pipe_eligible(const Job& job, RunFmt& f, uint64_t& R) {
     const uint64_t min_bytes = me ? strtoull(me, nullptr, 10) : (512ull << 20);
     const uint32_t k = (uint32_t)job.ranked.size();
     if (job.in_bytes < min_bytes || (job.flags & SKV_SPLIT_BY_TABLE) || job.batch || job.search) return false;
-    if (k == 0 || k > (uint32_t)TILE_TARGET / 2 || job.run_ptr.size() != k) return false;
+    const uint64_t nr = job.run_ptr.size();
+    if (k == 0 || k > (uint32_t)TILE_TARGET / 2 || nr == 0) return false;
     R = 0;
-    for (uint32_t m = 0; m < k; ++m) {
+    for (uint64_t m = 0; m < nr; ++m) {
         const uint8_t* run = (const uint8_t*)(uintptr_t)job.run_ptr[m];
         const uint64_t len = job.run_len[m];
         if (len < 1 + 9 || run[0] != 1 || run[1] != 1) return false;
@@ -47,6 +48,14 @@ static bool pipe_eligible(const Job& job, RunFmt& f, uint64_t& R) {
         }
         R += (len - 1) / S;
     }
+    // member runs of one stream (an L0 / next-level concatenation) must ascend as one sorted stream:
+    // member i's last key below member i + 1's first (each member's own order: the device and the cuts)
+    for (const InStream& st : job.ranked)
+        for (uint64_t m = st.first; m + 1 < st.first + st.n_runs; ++m) {
+            const uint8_t* a = (const uint8_t*)(uintptr_t)job.run_ptr[m];
+            const uint8_t* b = (const uint8_t*)(uintptr_t)job.run_ptr[m + 1];
+            if (memcmp(a + job.run_len[m] - f.S + 5, b + 1 + 5, f.K) >= 0) return false;
+        }
     return R < 0xFFFFFFFFull;
 }
 
@@ -56,17 +65,18 @@ static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, doub
     uint64_t R = 0;
     if (!pipe_eligible(job, f, R)) return SKV_OK;
     const uint32_t k = (uint32_t)job.ranked.size();
+    const uint64_t nr = job.run_ptr.size();  // member runs (one per stream unless a stream concatenates)
     const uint64_t S = f.S, K = f.K;
     uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(64, job.in_bytes / (256ull << 20)));
     if (const char* pp = getenv("SKV_HOST_PARTS")) P = std::max<uint64_t>(1, std::min<uint64_t>(256, strtoull(pp, nullptr, 10)));
     if (R < P * 64) return SKV_OK;
     htrace("pipe: eligible");
-    auto key_at = [&](uint32_t m, uint64_t i) { return (const uint8_t*)(uintptr_t)job.run_ptr[m] + 1 + i * S + 5; };
-    auto nrec = [&](uint32_t m) { return (job.run_len[m] - 1) / S; };
+    auto key_at = [&](uint64_t m, uint64_t i) { return (const uint8_t*)(uintptr_t)job.run_ptr[m] + 1 + i * S + 5; };
+    auto nrec = [&](uint64_t m) { return (job.run_len[m] - 1) / S; };
     // ---- cut keys: quantiles of an even sample of every run
     std::vector<std::array<uint8_t, 16>> smp;
-    const uint64_t Q = std::max<uint64_t>(8, 4096 / k);
-    for (uint32_t m = 0; m < k; ++m) {
+    const uint64_t Q = std::max<uint64_t>(2, 4096 / nr);
+    for (uint64_t m = 0; m < nr; ++m) {
         const uint64_t nm = nrec(m);
         for (uint64_t t = 0; t < Q && t < nm; ++t) {
             std::array<uint8_t, 16> a{};
@@ -77,29 +87,29 @@ static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, doub
     std::sort(smp.begin(), smp.end());
     std::vector<std::array<uint8_t, 16>> cut;  // P - 1 cut keys B_1..B_{P-1}
     for (uint64_t p = 1; p < P; ++p) cut.push_back(smp[p * smp.size() / P]);
-    // ---- lb[p * k + m]: first record of run m with key >= B_p (binary search in host memory)
-    std::vector<uint64_t> lb((P + 1) * k);
+    // ---- lb[p * nr + m]: first record of run m with key >= B_p (binary search in host memory)
+    std::vector<uint64_t> lb((P + 1) * nr);
     bool cuts_ok = true;
     {
-        const unsigned nb = par_nblocks(k, 8);
+        const unsigned nb = par_nblocks(nr, 8);
         std::vector<uint8_t> ok(nb, 1);
-        par_run(k, nb, [&](unsigned b, uint64_t lo_m, uint64_t hi_m) {
+        par_run(nr, nb, [&](unsigned b, uint64_t lo_m, uint64_t hi_m) {
             for (uint64_t m = lo_m; m < hi_m; ++m) {
-                const uint64_t nm = nrec((uint32_t)m);
+                const uint64_t nm = nrec(m);
                 lb[m] = 0;
-                lb[P * k + m] = nm;
+                lb[P * nr + m] = nm;
                 for (uint64_t p = 1; p < P; ++p) {
                     uint64_t a = 0, z = nm;
                     while (a < z) {
                         const uint64_t mid = (a + z) >> 1;
-                        if (memcmp(key_at((uint32_t)m, mid), cut[p - 1].data(), K) < 0) a = mid + 1;
+                        if (memcmp(key_at(m, mid), cut[p - 1].data(), K) < 0) a = mid + 1;
                         else z = mid;
                     }
-                    lb[p * k + m] = a;
-                    // a stream that decreases across a cut is left to the serial path (the device
+                    lb[p * nr + m] = a;
+                    // a run that decreases across a cut is left to the serial path (the device
                     // checks the order inside each part only)
-                    if (a < lb[(p - 1) * k + m]) ok[b] = 0;
-                    if (a > 0 && a < nm && memcmp(key_at((uint32_t)m, a - 1), key_at((uint32_t)m, a), K) > 0) ok[b] = 0;
+                    if (a < lb[(p - 1) * nr + m]) ok[b] = 0;
+                    if (a > 0 && a < nm && memcmp(key_at(m, a - 1), key_at(m, a), K) > 0) ok[b] = 0;
                 }
             }
         });
@@ -134,9 +144,9 @@ static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, doub
     volatile uint64_t* hK = ctx->part_k;
     for (uint64_t p = 0; p < P; ++p) hK[p] = ~0ull;
     // ---- device buffers (all sized before the first launch: no buffer moves under queued work)
-    std::vector<uint64_t> img(k + 1, 0);
-    for (uint32_t m = 0; m < k; ++m) img[m + 1] = img[m] + ((job.run_len[m] + 15) & ~15ull);
-    uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", img[k] + 16);
+    std::vector<uint64_t> img(nr + 1, 0);
+    for (uint64_t m = 0; m < nr; ++m) img[m + 1] = img[m] + ((job.run_len[m] + 15) & ~15ull);
+    uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", img[nr] + 16);
     const uint64_t out_cap = job.in_bytes + R + 16;
     uint8_t* d_out = dbuf<uint8_t>(ctx, "out", out_cap);
     uint64_t* d_Kp = dbuf<uint64_t>(ctx, "hp_K", P);
@@ -145,27 +155,38 @@ static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, doub
     const uint64_t n = fx_run_records(job.max_run_size, S, R), W = n * S + 1;
     const uint64_t max_runs = (R + n - 1) / n;
     DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", max_runs + 1);
-    // per part: its runs (rank order, empty slices left out), record bases
-    std::vector<RunInfo> hruns(P * k);
-    std::vector<uint32_t> kp(P, 0);
+    // per part: its runs (streams in rank order, each stream's member slices in member order, empty
+    // slices and streams left out), the first run of each stream, record bases
+    std::vector<RunInfo> hruns(P * nr);
+    std::vector<uint32_t> kp(P, 0), np(P, 0);
+    std::vector<std::vector<uint32_t>> sfrp(P);
     std::vector<std::vector<uint64_t>> recbp(P);
     for (uint64_t p = 0; p < P; ++p) {
         recbp[p].assign(1, 0);
+        sfrp[p].clear();
         for (uint32_t s = 0; s < k; ++s) {
-            const uint32_t m = (uint32_t)job.ranked[s].first;  // one run per stream
-            const uint64_t a = lb[p * k + m], z = lb[(p + 1) * k + m];
-            if (z == a) continue;
-            RunInfo& ri = hruns[p * k + kp[p]];
-            ri.ptr = (uint64_t)(uintptr_t)(d_in + img[m] + a * S);  // the byte before record a
-            ri.len = 1 + (z - a) * S;
-            ri.chunk_base = 0;
-            ri.n_chunks = 0;
-            ri.stream = kp[p]++;
-            recbp[p].push_back(recbp[p].back() + (z - a));
+            const InStream& st = job.ranked[s];
+            const uint32_t n0 = np[p];
+            for (uint64_t m = st.first; m < st.first + st.n_runs; ++m) {
+                const uint64_t a = lb[p * nr + m], z = lb[(p + 1) * nr + m];
+                if (z == a) continue;
+                RunInfo& ri = hruns[p * nr + np[p]++];
+                ri.ptr = (uint64_t)(uintptr_t)(d_in + img[m] + a * S);  // the byte before record a
+                ri.len = 1 + (z - a) * S;
+                ri.chunk_base = 0;
+                ri.n_chunks = 0;
+                ri.stream = kp[p];
+                recbp[p].push_back(recbp[p].back() + (z - a));
+            }
+            if (np[p] > n0) {
+                sfrp[p].push_back(n0);
+                ++kp[p];
+            }
         }
+        sfrp[p].push_back(np[p]);
     }
-    RunInfo* d_runs = dbuf<RunInfo>(ctx, "hp_runs", P * k);
-    h2d_up(ctx, d_runs, hruns.data(), P * k * sizeof(RunInfo));
+    RunInfo* d_runs = dbuf<RunInfo>(ctx, "hp_runs", P * nr);
+    h2d_up(ctx, d_runs, hruns.data(), P * nr * sizeof(RunInfo));
     HIPCHK(hipMemsetAsync(d_Kp, 0, P * 8, st));
     HIPCHK(hipMemsetAsync(d_pflags, 0, 16, st));
     size_t cap = 0;
@@ -249,9 +270,9 @@ static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, doub
     const uint64_t fail_at = fail_env ? strtoull(fail_env, nullptr, 10) : ~0ull;
     for (uint64_t p = 0; p < P; ++p) {
         if (p == fail_at) throw DevError("injected failure before part " + std::to_string(p));
-        for (uint32_t m = 0; m < k; ++m) {
-            const uint64_t lo = p == 0 ? 0 : 1 + lb[p * k + m] * S;
-            const uint64_t hi = p + 1 == P ? job.run_len[m] : 1 + lb[(p + 1) * k + m] * S;
+        for (uint64_t m = 0; m < nr; ++m) {
+            const uint64_t lo = p == 0 ? 0 : 1 + lb[p * nr + m] * S;
+            const uint64_t hi = p + 1 == P ? job.run_len[m] : 1 + lb[(p + 1) * nr + m] * S;
             if (hi > lo)
                 HIPCHK(hipMemcpyAsync(d_in + img[m] + lo, (const uint8_t*)(uintptr_t)job.run_ptr[m] + lo, hi - lo,
                                       hipMemcpyHostToDevice, ctx->in_stream));
@@ -259,15 +280,14 @@ static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, doub
         HIPCHK(hipEventRecord(ctx->part_ev[2 * p], ctx->in_stream));
         HIPCHK(hipStreamWaitEvent(st, ctx->part_ev[2 * p], 0));
         if (kp[p]) {
-            std::vector<uint32_t> sfr(kp[p] + 1);
-            for (uint32_t s = 0; s <= kp[p]; ++s) sfr[s] = s;
+            const std::vector<uint32_t>& sfr = sfrp[p];
             FxPartIO io;
             io.gbase = p ? d_Kp + p - 1 : nullptr;
             io.Kout = d_Kp + p;
             io.flags = d_pflags;
             io.out = d_out;
             uint64_t* rb_unused = nullptr;
-            Alast = fx_launch(ctx, kp[p], kp[p], d_runs + p * k, sfr, f, recbp[p], n, out_cap, &io, rb_unused);
+            Alast = fx_launch(ctx, kp[p], np[p], d_runs + p * nr, sfr, f, recbp[p], n, out_cap, &io, rb_unused);
             have_A = true;
         } else if (p) {
             launch_copy_bytes(st, (uint8_t*)(d_Kp + p), (const uint8_t*)(d_Kp + p - 1), 8);
@@ -452,7 +472,99 @@ inline uint64_t host_lower_bound(const uint8_t* b, uint64_t len, const std::stri
     }
     return q;
 }
+// "{id}." at the start of key k when id is a canonical Rust i64 Display text (the prefix
+// wal_compaction.rs strips is format!("{id}."), :76-98): its length, else 0
+inline uint64_t wal_canon_prefix(const uint8_t* k, uint64_t n) {
+    uint64_t i = 0;
+    if (i < n && k[i] == '-') ++i;
+    const uint64_t d0 = i;
+    while (i < n && k[i] >= '0' && k[i] <= '9') ++i;
+    const uint64_t nd = i - d0;
+    if (nd == 0 || nd > 19 || i >= n || k[i] != '.') return 0;
+    if (nd > 1 && k[d0] == '0') return 0;    // leading zero
+    if (d0 && nd == 1 && k[d0] == '0') return 0;  // "-0"
+    if (nd == 19 && memcmp(k + d0, d0 ? "9223372036854775808" : "9223372036854775807", 19) > 0) return 0;
+    return i + 1;
+}
 }  // namespace
+
+// Key-range cuts of a general pipelined call: every member run m is cut at its first record >= each
+// cut key. bnd[p * nr + m] is that byte offset (1 and len at the ends). Small runs are walked once
+// for all cuts; large ones bisect over resynced positions (host_lower_bound). False: a run that does
+// not decode where the cut search looked, or cuts that come out of order (the serial path then).
+static bool cut_runs(const Job& job, const std::vector<std::string>& cut, uint64_t P, std::vector<uint64_t>& bnd) {
+    const uint64_t nr = job.run_ptr.size();
+    bnd.assign((P + 1) * nr, 0);
+    const unsigned nb = std::max(1u, std::min<unsigned>(16, (unsigned)((nr + 63) / 64)));
+    std::vector<uint8_t> ok(nb, 1);
+    par_run(nr, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+        for (uint64_t m = lo; m < hi && ok[b]; ++m) {
+            const uint8_t* rb = (const uint8_t*)(uintptr_t)job.run_ptr[m];
+            const uint64_t len = job.run_len[m];
+            bnd[m] = 1;
+            bnd[P * nr + m] = len;
+            if (len <= (1u << 16)) {  // one walk over the run finds every cut
+                uint64_t q = 1;
+                for (uint64_t p = 1; p < P; ++p) {
+                    while (q < len) {
+                        const uint64_t sz = host_rec_at(rb, len, q);
+                        if (!sz) {
+                            ok[b] = 0;
+                            break;
+                        }
+                        if (rec_vs(rb, q, cut[p - 1]) >= 0) break;
+                        q += sz;
+                    }
+                    bnd[p * nr + m] = q;
+                }
+            } else {
+                for (uint64_t p = 1; p < P; ++p) {
+                    const uint64_t q = host_lower_bound(rb, len, cut[p - 1]);
+                    if (q == NPOS || q < bnd[(p - 1) * nr + m]) ok[b] = 0;
+                    bnd[p * nr + m] = q;
+                }
+            }
+        }
+    });
+    for (uint8_t o : ok)
+        if (!o) return false;
+    return true;
+}
+
+// A stream of several member runs (an L0 or next-level concatenation, table_buffer_compaction.rs:
+// 66-100, table_tree_compaction.rs:103-135) is cut member by member; that is a key range of the
+// stream only when the concatenation ascends: every record of member i below member i + 1's first
+// key (checked here, empty members skipped; each member's own order is checked by the parts).
+static bool members_ascend(const Job& job) {
+    std::vector<std::pair<uint64_t, uint64_t>> pairs;  // (member i, member j): the next non-empty one
+    for (const InStream& s : job.ranked) {
+        uint64_t prev = NPOS;
+        for (uint64_t r = s.first; r < s.first + s.n_runs; ++r) {
+            if (job.run_len[r] <= 1) continue;
+            if (prev != NPOS) pairs.emplace_back(prev, r);
+            prev = r;
+        }
+    }
+    if (pairs.empty()) return true;
+    const unsigned nb = std::max(1u, std::min<unsigned>(16, (unsigned)((pairs.size() + 15) / 16)));
+    std::vector<uint8_t> ok(nb, 1);
+    par_run(pairs.size(), nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+        for (uint64_t x = lo; x < hi && ok[b]; ++x) {
+            const uint64_t i = pairs[x].first, j = pairs[x].second;
+            const uint8_t* bj = (const uint8_t*)(uintptr_t)job.run_ptr[j];
+            if (!host_rec_at(bj, job.run_len[j], 1)) {
+                ok[b] = 0;
+                break;
+            }
+            const std::string f((const char*)bj + 6, be32(bj + 2));
+            const uint8_t* bi = (const uint8_t*)(uintptr_t)job.run_ptr[i];
+            if (host_lower_bound(bi, job.run_len[i], f) != job.run_len[i]) ok[b] = 0;
+        }
+    });
+    for (uint8_t o : ok)
+        if (!o) return false;
+    return true;
+}
 
 static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** out, double t_entry, bool& used) {
     used = false;
@@ -461,36 +573,47 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     const char* me = getenv("SKV_HOST_PIPE_MIN");
     const uint64_t min_bytes = me ? strtoull(me, nullptr, 10) : (512ull << 20);
     const uint32_t k = (uint32_t)job.ranked.size();
-    if (job.in_bytes < min_bytes || (job.flags & SKV_SPLIT_BY_TABLE) || job.batch || job.search || job.scan) return SKV_OK;
-    if (k == 0 || job.run_ptr.size() != k) return SKV_OK;  // one run per stream
-    if (k > (uint32_t)TILE_TARGET / 2) return SKV_OK;       // the splitter merge's fan-in per part
-    // parts of ~1 GiB: each part costs k DMA copies (config 3, 3.7 GiB: 4 parts 99.8 ms, 6 parts 102.9,
-    // 8 parts 105.0, 10 parts 110.5)
+    const uint64_t nr = job.run_ptr.size();
+    const bool wal = (job.flags & SKV_SPLIT_BY_TABLE) != 0;
+    if (job.in_bytes < min_bytes || job.batch || job.search || job.scan) return SKV_OK;
+    if (k == 0 || nr == 0) return SKV_OK;
+    // parts of ~1 GiB: each part costs a DMA copy per slice (config 3, 3.7 GiB: 4 parts 99.8 ms, 6
+    // parts 102.9, 8 parts 105.0, 10 parts 110.5)
     uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(32, job.in_bytes / (1ull << 30)));
     if (const char* pp = getenv("SKV_HOST_PARTS")) P = std::max<uint64_t>(1, std::min<uint64_t>(256, strtoull(pp, nullptr, 10)));
-    // the open run is carried into every part: keep it small against a part
-    if (P < 2 || job.max_run_size > job.in_bytes / (4 * P)) return SKV_OK;
-    auto run_b = [&](uint32_t m) { return (const uint8_t*)(uintptr_t)job.run_ptr[m]; };
-    for (uint32_t m = 0; m < k; ++m)  // a run without a version byte: the serial path's error
+    // the open output run is carried into every part (not for WAL flushes, whose parts hold whole
+    // tables): keep it small against a part
+    if (P < 2 || (!wal && job.max_run_size > job.in_bytes / (4 * P))) return SKV_OK;
+    auto run_b = [&](uint64_t m) { return (const uint8_t*)(uintptr_t)job.run_ptr[m]; };
+    for (uint64_t m = 0; m < nr; ++m)  // a run without a version byte: the serial path's error
         if (job.run_len[m] == 0 || run_b(m)[0] != 1) return SKV_OK;
-    // ---- cut keys: quantiles of records found at evenly spaced offsets of every run
-    std::vector<std::pair<const uint8_t*, uint64_t>> smp;
-    const uint64_t Q = std::max<uint64_t>(4, 4096 / k);
-    {
-        std::vector<std::vector<std::pair<const uint8_t*, uint64_t>>> part_smp(k);
-        const unsigned nb = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
-        par_run(k, std::min<uint64_t>(nb, k), [&](unsigned, uint64_t lo, uint64_t hi) {
-            for (uint64_t m = lo; m < hi; ++m) {
-                const uint8_t* rb = run_b((uint32_t)m);
-                const uint64_t len = job.run_len[m];
-                for (uint64_t t = 0; t < Q; ++t) {
-                    const uint64_t q = resync(rb, len, 1 + (2 * t + 1) * (len - 1) / (2 * Q));
-                    if (q != NPOS) part_smp[m].emplace_back(rb + q + 5, be32(rb + q + 1));
-                }
+    // ---- cut keys: quantiles of records found at evenly spaced offsets of the whole input (about
+    // 8192 samples whatever the fan-in: a WAL flush of 10^6 tiny runs samples a subset of them).
+    // WAL flushes cut at canonical table prefixes "{id}.": every key of a table sorts at or after
+    // its prefix and before the next table's, so a part holds whole tables (the one-run rule and the
+    // prefix strip stay per table); a key that is not canonical ends the attempt in its part.
+    std::vector<uint64_t> rpre(nr + 1, 0);
+    for (uint64_t m = 0; m < nr; ++m) rpre[m + 1] = rpre[m] + job.run_len[m];
+    const uint64_t NS = 8192;
+    std::vector<std::pair<const uint8_t*, uint64_t>> smp(NS, {nullptr, 0});
+    par_run(NS, 16, [&](unsigned, uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi; ++i) {
+            const uint64_t g = (2 * i + 1) * rpre[nr] / (2 * NS);
+            const uint64_t m = (uint64_t)(std::upper_bound(rpre.begin(), rpre.end(), g) - rpre.begin()) - 1;
+            const uint8_t* rb = run_b(m);
+            const uint64_t len = job.run_len[m];
+            const uint64_t q = resync(rb, len, std::max<uint64_t>(1, g - rpre[m]));
+            if (q == NPOS || q >= len) continue;
+            const uint64_t kl = be32(rb + q + 1);
+            if (wal) {
+                const uint64_t pl = wal_canon_prefix(rb + q + 5, kl);
+                if (pl) smp[i] = {rb + q + 5, pl};
+            } else {
+                smp[i] = {rb + q + 5, kl};
             }
-        });
-        for (auto& v : part_smp) smp.insert(smp.end(), v.begin(), v.end());
-    }
+        }
+    });
+    smp.erase(std::remove_if(smp.begin(), smp.end(), [](const auto& e) { return e.first == nullptr; }), smp.end());
     htrace("gpipe: sampled");
     if (smp.size() < P) {
         htrace("gpipe: too few samples");
@@ -499,36 +622,56 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     std::sort(smp.begin(), smp.end(), [](const auto& a, const auto& c) {
         return host_key_cmp(a.first, a.second, c.first, c.second) < 0;
     });
-    std::vector<std::string> cut(P - 1);
+    std::vector<std::string> cut;
     for (uint64_t p = 1; p < P; ++p) {
         const auto& e = smp[p * smp.size() / P];
-        cut[p - 1].assign((const char*)e.first, e.second);
+        std::string c((const char*)e.first, e.second);
+        if (cut.empty() || cut.back() < c) cut.push_back(c);  // (Rust str order = bytewise = std::string's)
     }
-    // ---- bnd[p * k + m]: byte offset of run m's first record >= cut p (1 / len at the ends)
-    std::vector<uint64_t> bnd((P + 1) * k);
+    P = cut.size() + 1;
+    if (P < 2 || (!wal && job.max_run_size > job.in_bytes / (4 * P))) return SKV_OK;
+    // ---- bnd[p * nr + m]: byte offset of run m's first record >= cut p (1 / len at the ends)
+    std::vector<uint64_t> bnd;
+    if (!cut_runs(job, cut, P, bnd)) {
+        htrace("gpipe: a cut not found");
+        return SKV_OK;
+    }
+    if (!members_ascend(job)) {
+        htrace("gpipe: member runs overlap");
+        return SKV_OK;
+    }
+    // ---- ingest mode: one DMA copy per non-empty slice while the call has few enough of them, else
+    // (and with SKV_INGEST=kernel) the GPU copies each part's slices itself from pinned, device-mapped
+    // host memory (k_ingest, one launch per part). The copy kernels measured slower on config 3 (8 parts:
+    // 130 vs 105 ms: part 0's kernels waited behind the later parts' ingest); a WAL flush of 10^6 tiny
+    // runs has millions of slices, each a DMA descriptor with its own fixed cost.
+    uint64_t n_slices = 0;
+    for (uint64_t p = 0; p < P; ++p)
+        for (uint64_t m = 0; m < nr; ++m) n_slices += bnd[(p + 1) * nr + m] > bnd[p * nr + m];
+    std::vector<uint64_t> hdev;
+    bool kernel_ingest = n_slices > (1u << 15);
     {
-        const unsigned nb = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
-        std::vector<uint8_t> ok(nb, 1);
-        par_run(k, std::min<uint64_t>(nb, k), [&](unsigned b, uint64_t lo, uint64_t hi) {
-            for (uint64_t m = lo; m < hi; ++m) {
-                const uint8_t* rb = run_b((uint32_t)m);
-                const uint64_t len = job.run_len[m];
-                bnd[m] = 1;
-                bnd[P * k + m] = len;
-                for (uint64_t p = 1; p < P; ++p) {
-                    const uint64_t q = host_lower_bound(rb, len, cut[p - 1]);
-                    bnd[p * k + m] = q;
-                    if (q == NPOS || q < bnd[(p - 1) * k + m]) ok[b] = q == NPOS ? 2 : 3;
+        const char* ie = getenv("SKV_INGEST");
+        if (ie && !strcmp(ie, "kernel")) kernel_ingest = true;
+        if (kernel_ingest) {
+            hdev.assign(nr, 0);
+            for (uint64_t m = 0; m < nr && kernel_ingest; ++m) {
+                hipPointerAttribute_t a;
+                if (hipPointerGetAttributes(&a, run_b(m)) != hipSuccess) {
+                    (void)hipGetLastError();
+                    kernel_ingest = false;
+                } else if (a.type != hipMemoryTypeHost || !a.devicePointer) {
+                    kernel_ingest = false;
+                } else {
+                    hdev[m] = (uint64_t)(uintptr_t)a.devicePointer;
                 }
             }
-        });
-        for (uint8_t o : ok)
-            if (o != 1) {
-                htrace(o == 2 ? "gpipe: a cut not found" : "gpipe: cuts out of order");
+            if (!kernel_ingest && n_slices > (1u << 15)) {
+                htrace("gpipe: too many slices for DMA copies, runs not device-mapped");
                 return SKV_OK;
             }
+        }
     }
-    const uint64_t R = job.in_bytes / 5 + 1;  // records: at most one per 5 bytes (sizes only)
     htrace("gpipe: cuts");
     used = true;
     struct KernelIO {  // table uploads and readbacks by copy kernels, not DMA behind the bulk copies;
@@ -559,33 +702,12 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ctx->part_ev.push_back(e);
     }
-    // ---- ingest mode: one DMA copy per slice; or (SKV_INGEST=kernel, every run in pinned,
-    // device-mapped host memory) the GPU copies each part's slices itself, one launch per part
-    // (k_ingest). The copy kernels measured slower (config 3, 8 parts: 130 vs 105 ms): while later
-    // parts' copies ran, part 0's kernels did not start (77 ms in), as if in_stream and the ctx
-    // stream shared a hardware queue; the DMA engines take no compute queue.
-    std::vector<uint64_t> hdev(k, 0);
-    bool kernel_ingest = false;
-    {
-        const char* ie = getenv("SKV_INGEST");
-        if (ie && !strcmp(ie, "kernel")) kernel_ingest = true;
-        for (uint32_t m = 0; m < k && kernel_ingest; ++m) {
-            hipPointerAttribute_t a;
-            if (hipPointerGetAttributes(&a, run_b(m)) != hipSuccess) {
-                (void)hipGetLastError();
-                kernel_ingest = false;
-            } else if (a.type != hipMemoryTypeHost || !a.devicePointer) {
-                kernel_ingest = false;
-            } else {
-                hdev[m] = (uint64_t)(uintptr_t)a.devicePointer;
-            }
-        }
-    }
     // ---- device images of the runs (each congruent mod 16 with its host bytes); the shared output
-    std::vector<uint64_t> img(k + 1, 0);
-    for (uint32_t m = 0; m < k; ++m) img[m + 1] = img[m] + ((job.run_len[m] + 31) & ~15ull);
-    uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", img[k] + 16);
-    for (uint32_t m = 0; m < k; ++m) img[m] += ((uint64_t)(uintptr_t)run_b(m) & 15);  // 16-aligned base + skew
+    std::vector<uint64_t> img(nr + 1, 0);
+    for (uint64_t m = 0; m < nr; ++m) img[m + 1] = img[m] + ((job.run_len[m] + 31) & ~15ull);
+    uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", img[nr] + 16);
+    for (uint64_t m = 0; m < nr; ++m) img[m] += ((uint64_t)(uintptr_t)run_b(m) & 15);  // 16-aligned base + skew
+    const uint64_t R = job.in_bytes / 5 + 1;  // records: at most one per 5 bytes (sizes only)
     const uint64_t out_cap = job.in_bytes + R + 64;
     uint8_t* d_out = dbuf<uint8_t>(ctx, "gp_out", out_cap);
     size_t cap = 0;
@@ -604,32 +726,36 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     } out_guard{ctx, h_out, cap};
     // ---- ingest: every part's slices, in part order, on in_stream
     IngestSlice* d_sl = nullptr;
-    std::vector<IngestSlice> hsl;
+    std::vector<uint64_t> sl_base(P + 1, 0);
     if (kernel_ingest) {
-        hsl.resize(P * k);
-        for (uint64_t p = 0; p < P; ++p)
-            for (uint32_t m = 0; m < k; ++m) {
-                const uint64_t lo = p == 0 ? 0 : bnd[p * k + m], hi = bnd[(p + 1) * k + m];
-                hsl[p * k + m] = IngestSlice{hdev[m] + lo, (uint64_t)(uintptr_t)(d_in + img[m] + lo), hi - lo};
+        std::vector<IngestSlice> hsl;
+        hsl.reserve(n_slices);
+        for (uint64_t p = 0; p < P; ++p) {
+            sl_base[p] = hsl.size();
+            for (uint64_t m = 0; m < nr; ++m) {
+                const uint64_t lo = p == 0 ? 0 : bnd[p * nr + m], hi = bnd[(p + 1) * nr + m];
+                if (hi > lo) hsl.push_back(IngestSlice{hdev[m] + lo, (uint64_t)(uintptr_t)(d_in + img[m] + lo), hi - lo});
             }
-        d_sl = dbuf<IngestSlice>(ctx, "gp_slices", P * k);
-        HIPCHK(hipMemcpyAsync(d_sl, hsl.data(), P * k * sizeof(IngestSlice), hipMemcpyHostToDevice, ctx->in_stream));
+        }
+        sl_base[P] = hsl.size();
+        d_sl = dbuf<IngestSlice>(ctx, "gp_slices", hsl.size() + 1);
+        HIPCHK(hipMemcpyAsync(d_sl, hsl.data(), hsl.size() * sizeof(IngestSlice), hipMemcpyHostToDevice, ctx->in_stream));
+        HIPCHK(hipStreamSynchronize(ctx->in_stream));  // (hsl is a local: the copy is from pageable memory)
     }
     // a few hundred ingest workgroups in all: the copies are bound by PCIe, and a grid that filled
     // every CU (8 per slice: 2,048 at config 3) held the part kernels off the GPU until the whole
     // input had landed (part 0 finished after 77 ms, parts 1-7 in 3 ms each behind it)
-    uint32_t ibps = std::max<uint32_t>(1, 384 / k);
-    if (const char* be = getenv("SKV_INGEST_BLOCKS")) ibps = std::max<uint32_t>(1, (uint32_t)strtoul(be, nullptr, 10));
+    uint32_t igrid = 384;
+    if (const char* be = getenv("SKV_INGEST_BLOCKS")) igrid = std::max<uint32_t>(1, (uint32_t)strtoul(be, nullptr, 10));
     for (uint64_t p = 0; p < P; ++p) {
         if (kernel_ingest) {
-            launch_ingest(ctx->in_stream, d_sl + p * k, k, ibps);
+            launch_ingest_slices(ctx->in_stream, d_sl + sl_base[p], sl_base[p + 1] - sl_base[p], igrid);
             HIPCHK(hipGetLastError());
         } else {
-            for (uint32_t m = 0; m < k; ++m) {
-                const uint64_t lo = p == 0 ? 0 : bnd[p * k + m], hi = bnd[(p + 1) * k + m];
+            for (uint64_t m = 0; m < nr; ++m) {
+                const uint64_t lo = p == 0 ? 0 : bnd[p * nr + m], hi = bnd[(p + 1) * nr + m];
                 if (hi > lo)
-                    HIPCHK(hipMemcpyAsync(d_in + img[m] + lo, run_b(m) + lo, hi - lo, hipMemcpyHostToDevice,
-                                          ctx->in_stream));
+                    HIPCHK(hipMemcpyAsync(d_in + img[m] + lo, run_b(m) + lo, hi - lo, hipMemcpyHostToDevice, ctx->in_stream));
             }
         }
         HIPCHK(hipEventRecord(ctx->part_ev[2 * p], ctx->in_stream));
@@ -689,32 +815,54 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
         while (std::binary_search(seqs.begin(), seqs.end(), seq_extra)) ++seq_extra;
     }
     std::vector<skv_run_desc> descs;
-    uint64_t open_off = 0, open_len = 0, open_recs = 0, out_records = 0, in_records = 0;
+    uint64_t open_off = 0, open_len = 0, open_recs = 0, out_records = 0, in_records = 0, dropped = 0;
+    uint64_t wal_off = 0;  // WAL flushes: output bytes of the parts so far (every part's tables are final)
     uint64_t syncs = 0;
+    std::vector<const uint8_t*> ptrs;
+    std::vector<uint64_t> lens;
+    std::vector<skv_stream> sv;
     for (uint64_t p = 0; p < P; ++p) {
-        std::vector<const uint8_t*> ptrs;
-        std::vector<uint64_t> lens;
-        std::vector<int64_t> seqv;
-        ptrs.reserve(k + 1);
+        // part p's streams: each stream's member slices in member order (empty ones left out), the
+        // streams in rank order, then the carried open run
+        ptrs.clear();
+        lens.clear();
+        sv.clear();
+        std::vector<std::pair<int64_t, uint64_t>> sfirst;  // (seq, first slice) per non-empty stream
         for (uint32_t s = 0; s < k; ++s) {
-            const uint32_t m = (uint32_t)job.ranked[s].first;
-            const uint64_t lo = bnd[p * k + m], hi = bnd[(p + 1) * k + m];
-            ptrs.push_back(d_in + img[m] + lo - 1);  // the byte before the slice: its "version byte"
-            lens.push_back(1 + hi - lo);
-            seqv.push_back(job.ranked[s].seq);
+            const InStream& S = job.ranked[s];
+            const uint64_t f0 = ptrs.size();
+            for (uint64_t m = S.first; m < S.first + S.n_runs; ++m) {
+                const uint64_t lo = bnd[p * nr + m], hi = bnd[(p + 1) * nr + m];
+                if (hi <= lo) continue;
+                ptrs.push_back(d_in + img[m] + lo - 1);  // the byte before the slice: its "version byte"
+                lens.push_back(1 + hi - lo);
+            }
+            if (ptrs.size() > f0) sfirst.emplace_back(S.seq, f0);
         }
         if (open_len) {
+            sfirst.emplace_back(seq_extra, ptrs.size());
             ptrs.push_back(d_out + open_off);
             lens.push_back(open_len);
-            seqv.push_back(seq_extra);
         }
-        std::vector<skv_stream> sv(ptrs.size());
-        for (size_t i = 0; i < sv.size(); ++i) sv[i] = skv_stream{&ptrs[i], &lens[i], 1u, seqv[i]};
+        const bool last_part = p + 1 == P;
+        if (sfirst.empty()) {  // no records in this key range
+            if (last_part) {
+                std::lock_guard<std::mutex> g(mu);
+                final_end = wal ? wal_off : (descs.empty() ? 0 : descs.back().off + descs.back().len);
+                done = true;
+            }
+            cv.notify_all();
+            continue;
+        }
+        for (size_t i = 0; i < sfirst.size(); ++i) {
+            const uint64_t a = sfirst[i].second, z = i + 1 < sfirst.size() ? sfirst[i + 1].second : ptrs.size();
+            sv.push_back(skv_stream{&ptrs[a], &lens[a], (uint32_t)(z - a), sfirst[i].first});
+        }
         Job pj;
         if (build_job(ctx, sv.data(), (uint32_t)sv.size(), job.max_run_size, job.flags, pj) != SKV_OK)
             throw DevError("internal: part job: " + ctx->err);
         pj.part = true;
-        pj.dev_out = d_out + open_off;
+        pj.dev_out = d_out + (wal ? wal_off : open_off);
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->part_ev[2 * p], 0));
         if (getenv("SKV_HOST_TRACE")) {  // diagnostics: when part p's slices have landed
             HIPCHK(hipEventSynchronize(ctx->part_ev[2 * p]));
@@ -734,6 +882,29 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
             return SKV_OK;
         }
         const uint64_t n = pres->n_runs;
+        if (wal) {
+            // whole tables: every run of the part is final at its offset in the call's output
+            for (uint64_t r = 0; r < n; ++r) {
+                skv_run_desc d = pres->runs[r];
+                d.off += wal_off;
+                d.min_key_off += wal_off;
+                d.max_key_off += wal_off;
+                descs.push_back(d);
+                out_records += d.put_count + d.delete_count;
+            }
+            in_records += pres->in_records;
+            dropped += pres->dropped_tables;
+            wal_off += pres->n_bytes;
+            skv_result_free(pres);
+            {
+                std::lock_guard<std::mutex> g(mu);
+                final_end = wal_off;
+                done = last_part;
+            }
+            cv.notify_all();
+            htrace("gpipe: part done");
+            continue;
+        }
         // Part p read the carried open run at d_out + open_off while writing its own output from that
         // same address. That is safe because the merge re-emits the open run first and unchanged --
         // every key of it sorts before every key of part p, and it is under max_run_size, so
@@ -744,7 +915,6 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
             skv_result_free(pres);
             throw DevError("internal: general pipeline part " + std::to_string(p) + " did not re-emit the open run");
         }
-        const bool last_part = p + 1 == P;
         in_records += pres->in_records - (open_len ? open_recs : 0);  // the carried run's records once
         for (uint64_t r = 0; r < n; ++r) {
             skv_run_desc d = pres->runs[r];
@@ -779,11 +949,11 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     res->n_runs = descs.size();
     res->bytes = h_out;
     h_out = nullptr;  // the result owns it now
-    res->n_bytes = descs.empty() ? 0 : descs.back().off + descs.back().len;
+    res->n_bytes = wal ? wal_off : (descs.empty() ? 0 : descs.back().off + descs.back().len);
     res->in_bytes = job.in_bytes;
     res->in_records = in_records;
     res->out_records = out_records;
-    res->dropped_tables = 0;
+    res->dropped_tables = dropped;
     box->pool = ctx->out_pool;
     box->pool_cap = cap;
     skv_timings& t = ctx->timings;
@@ -792,6 +962,7 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     t.host_syncs = syncs;
     t.host_total_ms = now_ms() - t_entry;
     t.host_parts = (uint32_t)P;
+    t.wal_stage = wal ? 1 : 0;
     *out = res;
     return SKV_OK;
 }

@@ -63,6 +63,9 @@ void launch_gather(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, cons
                    const uint64_t* m_dup = nullptr, uint32_t* fp_bad = nullptr);
 // skv_wal.hip — SKV_SPLIT_BY_TABLE (wal_compaction.rs:66-174)
 constexpr uint32_t WAL_FUSED_G = 256;  // merged records per k_wal_fused workgroup
+// k_wal_fused's mode word: bits 0-1 diagnostics (2: no output bytes); WAL_STRICT_CANON: a key whose
+// prefix is not the canonical "{id}." fails the stage (key-range parts of a pipelined host call)
+constexpr uint32_t WAL_STRICT_CANON = 4;
 struct WalTStart {  // a table start of k_wal_fused (unordered list; the host sorts by b)
     uint64_t b, W, Dp;  // first merged record, output offset of the table's version byte, deletes before b
     int64_t tid;
@@ -152,6 +155,7 @@ struct IngestSlice {
     uint64_t src, dst, len;
 };
 void launch_ingest(hipStream_t, const IngestSlice* slices, uint32_t n, uint32_t blocks_per_slice);
+void launch_ingest_slices(hipStream_t, const IngestSlice* slices, uint64_t n, uint32_t grid);
 // skv_scan.hip: ScanFromRun after the merge
 void launch_scan_filter(hipStream_t, uint64_t R, uint32_t k, const uint64_t* stream_base, const uint64_t* a_addr,
                         const uint64_t* a_hi, const uint64_t* a_lo, const uint32_t* a_klen, const uint32_t* a_meta,

@@ -1237,6 +1237,24 @@ __global__ void __launch_bounds__(256) k_ingest(const IngestSlice* __restrict__ 
     for (; i < nb; i += stride) d4[i] = s4[i];
 }
 
+// The same ingest for calls with many slices (a WAL flush of 10^6 tiny runs: a few KiB each):
+// workgroups stride over the slices, one slice at a time, so the grid stays small (the copies are
+// bound by PCIe) whatever the slice count.
+__global__ void __launch_bounds__(256) k_ingest_slices(const IngestSlice* __restrict__ sl, uint64_t n) {
+    for (uint64_t y = blockIdx.x; y < n; y += gridDim.x) {
+        const IngestSlice S = sl[y];
+        const uint8_t* src = (const uint8_t*)S.src;
+        uint8_t* dst = (uint8_t*)S.dst;
+        const uint64_t head = ((16 - (S.src & 15)) & 15) < S.len ? ((16 - (S.src & 15)) & 15) : S.len;
+        const uint64_t nb = (S.len - head) >> 4, tail0 = head + (nb << 4);
+        if (threadIdx.x < head) dst[threadIdx.x] = src[threadIdx.x];
+        if (threadIdx.x < S.len - tail0) dst[tail0 + threadIdx.x] = src[tail0 + threadIdx.x];
+        const uint4* s4 = (const uint4*)(src + head);
+        uint4* d4 = (uint4*)(dst + head);
+        for (uint64_t i = threadIdx.x; i < nb; i += blockDim.x) d4[i] = s4[i];
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 static inline unsigned fx_blocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
@@ -1283,6 +1301,9 @@ uint64_t fx_tile_slots(uint32_t k) {  // fused tiles resident at once on the cur
 }
 void launch_ingest(hipStream_t s, const IngestSlice* slices, uint32_t n, uint32_t blocks_per_slice) {
     if (n) k_ingest<<<dim3(blocks_per_slice, n), 256, 0, s>>>(slices);
+}
+void launch_ingest_slices(hipStream_t s, const IngestSlice* slices, uint64_t n, uint32_t grid) {
+    if (n) k_ingest_slices<<<(unsigned)std::min<uint64_t>(n, grid ? grid : 1), 256, 0, s>>>(slices, n);
 }
 void launch_copy_bytes(hipStream_t s, uint8_t* dst, const uint8_t* src, uint64_t n) {
     if (n) k_copy_bytes<<<fx_blocks((n + 15) / 16, 256), 256, 0, s>>>(dst, src, n);

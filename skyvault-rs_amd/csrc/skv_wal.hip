@@ -425,7 +425,7 @@ __global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict_
     if (live) {
         rp = (const uint8_t*)m_src[j];
         r = wal_parse(rp, P[j + 1] - P[j]);
-        if (r.err) bad |= WF_BADKEY;
+        if (r.err || ((diag & WAL_STRICT_CANON) && !r.canon)) bad |= WF_BADKEY;
     }
     // the record before: the neighbouring lane; a wave's lane 0 takes the previous wave's last lane
     // through LDS, and only the workgroup's first record parses its predecessor again
@@ -559,7 +559,7 @@ __global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict_
         if (j + 1 == K || threadIdx.x + 1 == WAL_G) os[threadIdx.x + 1] = ostart + wo;
     }
     __syncthreads();
-    if (diag == 2) return;  // SKV_WAL_FUSED=2 (diagnostic, wrong output): everything but the output bytes
+    if ((diag & 3) == 2) return;  // SKV_WAL_FUSED=2 (diagnostic, wrong output): everything but the output bytes
     // consecutive threads compose consecutive aligned output blocks (coalesced stores; a thread per
     // record instead, its blocks in a loop, measured slower: 10.1 vs 8.9 ms at config 5)
     const uint32_t c = (uint32_t)(K - j0 < WAL_G ? K - j0 : WAL_G);

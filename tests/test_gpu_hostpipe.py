@@ -131,7 +131,8 @@ def test_decrease_falls_back_to_the_serial_path_with_the_oracles_error(dev, pipe
 
 
 def test_not_eligible_inputs_stay_serial(dev, pipe_env):
-    """the WAL split and L0-style multi-run streams never pipeline"""
+    """a WAL flush whose tables break the one-run rule (each over max: dropped) and an L0-style stream
+    whose member runs overlap (not one sorted stream) end on the serial path with the oracle's outcome"""
     rng = random.Random(5)
     streams = []
     for s in range(4):
@@ -299,3 +300,120 @@ def test_general_pipeline_pinned_inputs_kernel_ingest(dev, pipe_env, parts):
         assert [r.data for r in got] == [r.data for r in exp]
         assert [(r.stats.min_key, r.stats.max_key, r.stats.put_count, r.stats.delete_count) for r in got] == \
             [(r.stats.min_key, r.stats.max_key, r.stats.put_count, r.stats.delete_count) for r in exp]
+
+
+# ---- real job shapes: L0 / next-level concatenations, WAL flushes ---------------------------------
+
+def _check_pipe(dev, streams, max_size, flags, parts, min_parts=2):
+    """as _check, but the part count may come out lower than asked (WAL cuts are distinct tables)"""
+    os.environ["SKV_HOST_PARTS"] = str(parts)
+    exp, got = _run_both(dev, streams, max_size, flags)
+    assert exp == got, _diff(exp, got)
+    hp = dev.timings()["host_parts"]
+    assert min_parts <= hp <= parts, f"host_parts={hp}"
+    return hp
+
+
+def _l0_stream(rng, n_members, per, space, fixed, seq=0, vmax=60):
+    """one stream of n_members ascending, non-overlapping member runs (the L0 concatenation of
+    table_buffer_compaction.rs:66-100 at SeqNo 0)"""
+    ids = sorted(rng.sample(range(space), n_members * per))
+    members = []
+    for i in range(n_members):
+        chunk = ids[i * per:(i + 1) * per]
+        if fixed:
+            members.append(_fixed_run([f"k{x:011d}" for x in chunk], 40, 200 + i))
+        else:
+            ops = [fmt.put(f"k{x:07d}" + "abcdefghij" * (x % 7), bytes([i & 0xFF]) * rng.randint(0, vmax))
+                   if rng.random() < .9 else fmt.delete(f"k{x:07d}" + "abcdefghij" * (x % 7)) for x in chunk]
+            members.append(fmt.encode_run(ops))
+    return (seq, members)
+
+
+@pytest.mark.parametrize("parts", [2, 5, 11])
+def test_fused_pipeline_l0_concatenation_across_cuts(dev, pipe_env, parts):
+    """buffer streams + one stream of 40 ascending L0 member runs (one record size: the fused
+    pipeline); the cuts fall inside and between member runs"""
+    rng = random.Random(600 + parts)
+    streams = [(s + 1, [_fixed_run([f"k{x:011d}" for x in sorted(rng.sample(range(40000), 1500))], 40, s)])
+               for s in range(6)]
+    streams.append(_l0_stream(rng, 40, 150, 40000, fixed=True))
+    _check(dev, streams, 4 * MiB, 0, parts)
+    _check(dev, streams, 3000, 0, parts)
+
+
+@pytest.mark.parametrize("parts", [2, 6, 13])
+def test_general_pipeline_l0_concatenation_across_cuts(dev, pipe_env, parts):
+    """variable-length records and Deletes: buffer streams + an L0 concatenation (25 member runs,
+    one of them empty) + a next-level concatenation at another SeqNo (table_tree_compaction.rs:
+    103-135); flags 0 and the Delete filter"""
+    rng = random.Random(700 + parts)
+    streams = _var_streams(rng, 5, 1500, 30000)
+    l0 = _l0_stream(rng, 25, 120, 30000, fixed=False, seq=0)
+    l0[1].insert(7, b"\x01")  # a member of only a version byte yields nothing
+    streams.append(l0)
+    streams.append(_l0_stream(rng, 9, 300, 30000, fixed=False, seq=-5))
+    for flags in (0, _abi.SKV_DROP_TOMBSTONES):
+        _check(dev, streams, 4096, flags, parts)
+
+
+def _wal_streams(rng, k, n, tables, vmax=30, dels=0.1):
+    out = []
+    for s in range(k):
+        keys = sorted({f"{rng.choice(tables)}.{rng.randrange(10 ** 7):07d}" for _ in range(n)})
+        out.append((s + 1, [fmt.encode_run([fmt.put(x, bytes([s]) * rng.randint(0, vmax)) if rng.random() >= dels
+                                            else fmt.delete(x) for x in keys])]))
+    return out
+
+
+@pytest.mark.parametrize("parts", [2, 4, 9])
+def test_wal_flush_pipelined_across_table_cuts(dev, pipe_env, parts):
+    """a WAL flush (wal_compaction.rs:18-174) of 16 WAL runs over 300 tables (negative ids too):
+    parts cut at canonical table prefixes, each part's tables whole, the one-pass WAL stage per part;
+    output bytes, descriptors (table ids) and dropped-table count equal to the oracle's"""
+    rng = random.Random(800 + parts)
+    streams = _wal_streams(rng, 16, 2500, [str(t) for t in range(-20, 280)])
+    _check_pipe(dev, streams, 4 * MiB, _abi.SKV_SPLIT_BY_TABLE, parts)
+    assert dev.timings()["wal_stage"] == 1
+
+
+def test_wal_flush_pipeline_declines_to_the_serial_path(dev, pipe_env):
+    """what a part cannot decide alone ends the attempt, and the serial path gives the oracle's
+    outcome: a non-canonical prefix ("007." is table 7, far from "7." in key order), a table over
+    max (dropped by the one-run rule), a key without a table prefix (the job fails)"""
+    rng = random.Random(901)
+    base = _wal_streams(rng, 8, 2000, [str(t) for t in range(100)])
+    cases = [
+        base + [(50, [fmt.encode_run([fmt.put("007.a", b"x")])])],
+        base,  # at max 600 some tables exceed max
+        base + [(51, [fmt.encode_run([fmt.put("nodot", b"y")])])],
+    ]
+    for streams, mx in zip(cases, (4 * MiB, 600, 4 * MiB)):
+        os.environ["SKV_HOST_PARTS"] = "4"
+        exp, got = _run_both(dev, streams, mx, _abi.SKV_SPLIT_BY_TABLE)
+        assert exp == got, _diff(exp, got)
+        assert dev.timings()["host_parts"] == 0
+
+
+def test_wal_flush_of_many_tiny_runs_kernel_ingest(dev, pipe_env):
+    """config 5's shape at small scale: 20,000 WAL runs of 10 records in pinned, device-mapped host
+    memory -- more slices than one DMA copy each is worth, so the GPU copies each part's slices
+    itself (k_ingest_slices); outputs equal to the oracle's"""
+    torch = pytest.importorskip("torch")
+    rng = random.Random(902)
+    tables = [str(t) for t in range(64)]
+    runs = []
+    for s in range(20000):
+        keys = sorted({f"{rng.choice(tables)}.{rng.randrange(10 ** 9):09d}" for _ in range(10)})
+        runs.append(fmt.encode_run([fmt.put(x, bytes([s & 0xFF]) * 8) for x in keys]))
+    blob = b"".join(runs)
+    t = torch.empty(len(blob), dtype=torch.uint8).pin_memory()
+    t[:] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+    offs = np.cumsum([0] + [len(r) for r in runs[:-1]])
+    pstreams = [(s + 1, [(t.data_ptr() + int(o), len(r))]) for s, (o, r) in enumerate(zip(offs, runs))]
+    os.environ["SKV_HOST_PARTS"] = "4"
+    got = dev.compact_host_ptrs(pstreams, 1 << 40, _abi.SKV_SPLIT_BY_TABLE, with_runs=True)
+    assert 2 <= dev.timings()["host_parts"] <= 4
+    exp = pyoracle.compact([(s + 1, [r]) for s, r in enumerate(runs)], 1 << 40, _abi.SKV_SPLIT_BY_TABLE)
+    assert [r.data for r in got] == [r.data for r in exp]
+    assert [r.table_id for r in got] == [r.table_id for r in exp]
