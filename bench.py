@@ -20,6 +20,9 @@ oracle/, faithful shape, 1 core, on a bounded sample of the same workload).
   5   10^6 WAL runs x 83 records (32 B "{table}.{suffix}" keys, 8 B values), SKV_SPLIT_BY_TABLE,
       built in HBM; max run size 2^62 so every table keeps its one run (at the reference's 4 MiB
       every table of this size would be dropped by the exactly-one-run rule)
+  L0  a table-buffer compaction as table_buffer_compaction.rs:31-100 builds it: 16 buffer runs
+      (SeqNo 1..16) + ONE stream at SeqNo 0 concatenating 1,024 ascending L0 runs (4 MiB each,
+      config 2's records), built in HBM
 """
 import argparse
 import json
@@ -55,6 +58,9 @@ def cpu_baseline(config, sample_records, n_streams, vsize, repeats, run_mib=16):
                               variant=config[1])
         sample = (f"{n_streams} streams x {sample_records} records x {9 + 16 + vsize} B (config-{config} shape, "
                   f"1/{round(238821 / sample_records)} of the records)")
+    elif config == "L0":
+        streams = gen.config_l0(seed=0xC0FFEE, n_buffer=16, n_l0=1024, run_records=14925 // 16)
+        sample = "16 buffer runs + one stream of 1,024 L0 runs, 932 records each (config-L0 shape, 1/16 of the records)"
     elif config in ("3", "3F"):
         # runs of run_mib / 16 MiB, at most 1 MiB (the bench's own runs are run_mib MiB: 16 for
         # config 3, 256 for 3F)
@@ -209,7 +215,7 @@ def main():
     ap.add_argument("--records", type=int, default=238821)
     ap.add_argument("--vsize", type=int, default=256)
     ap.add_argument("--variant", default="A", help="config 2 variant (same as --config 2A / 2B)")
-    ap.add_argument("--config", default=None, choices=["2A", "2B", "3", "3F", "5"])
+    ap.add_argument("--config", default=None, choices=["2A", "2B", "3", "3F", "5", "L0"])
     ap.add_argument("--run-mib", type=int, default=16, help="config 3 run size")
     ap.add_argument("--wal-runs", type=int, default=1_000_000, help="config 5 stream count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -239,7 +245,8 @@ def main():
     device = torch.device("cuda", dev_idx)
 
     from skv.api import Compactor
-    from skv.devgen import make_cfg2_on_device, make_cfg3_full_on_device, make_cfg3_on_device, make_cfg5_on_device
+    from skv.devgen import (make_cfg2_on_device, make_cfg3_full_on_device, make_cfg3_on_device, make_cfg5_on_device,
+                            make_l0_on_device)
 
     seed = rank_seed(rank)
     config = args.config or "2" + args.variant
@@ -259,6 +266,14 @@ def main():
         workload = (f"config 3: {n_streams}-way compaction, {n_streams} x 1 run of ~{run_mib} MiB, variable-length "
                     f"keys 8-128 B + 10 % Deletes, 256 B values, max run 4 MiB")
         data = "synthetic: sorted unique ids rendered as order-preserving alnum keys + alnum tails, built in HBM"
+    elif config == "L0":
+        bruns, lruns = make_l0_on_device(device, seed)
+        runs = bruns + lruns
+        n_streams = len(bruns) + 1
+        workload = (f"table-buffer compaction with L0: {len(bruns)} buffer runs (SeqNo 1..{len(bruns)}) + one stream "
+                    f"at SeqNo 0 concatenating {len(lruns)} ascending L0 runs of 14,925 records (281 B: 16 B keys / "
+                    f"256 B values, 4 MiB runs), max run 4 MiB")
+        data = "synthetic: splitmix64 ids from one universe (buffer records supersede some L0 records), built in HBM"
     elif config == "3":
         n_streams = 256 if args.streams == 64 else args.streams
         runs = make_cfg3_on_device(device, seed, n_streams, args.run_mib)
@@ -278,6 +293,10 @@ def main():
         base = buf.data_ptr()
         in_bytes = buf.numel()
         streams = [(s + 1, [(base + s * rl, rl)]) for s in range(n_streams)]
+    elif config == "L0":
+        in_bytes = sum(r.numel() for r in runs)
+        streams = [(b + 1, [(r.data_ptr(), r.numel())]) for b, r in enumerate(bruns)]
+        streams.append((0, [(r.data_ptr(), r.numel()) for r in lruns]))
     else:
         in_bytes = sum(r.numel() for r in runs)
         streams = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(runs)]
@@ -362,9 +381,19 @@ def main():
     # PCIe-inclusive figure (not `value`): the host entry point skv_compact with the inputs in
     # pinned host memory and the output runs returned in pinned host memory.
     host_path = None
-    if rank == 0 and world == 1 and not args.no_host_path and config in ("2A", "2B", "3"):  # not 3F / 5
-        host_runs = [r.cpu().pin_memory() for r in runs]
-        hstreams = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(host_runs)]
+    if rank == 0 and world == 1 and not args.no_host_path and config != "3F":  # 3F: 64 GB of pinned host memory
+        if config == "5":  # one pinned buffer of 10^6 WAL runs; the stream table built once
+            host_runs = [buf.cpu().pin_memory()]
+            hb0 = host_runs[0].data_ptr()
+            hstreams = StreamArgs([(s + 1, [(hb0 + s * rl, rl)]) for s in range(n_streams)], device=True)
+        elif config == "L0":
+            host_runs = [r.cpu().pin_memory() for r in runs]
+            nb_ = len(bruns)
+            hstreams = [(b + 1, [(r.data_ptr(), r.numel())]) for b, r in enumerate(host_runs[:nb_])]
+            hstreams.append((0, [(r.data_ptr(), r.numel()) for r in host_runs[nb_:]]))
+        else:
+            host_runs = [r.cpu().pin_memory() for r in runs]
+            hstreams = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(host_runs)]
         comp.compact_host_ptrs(hstreams, max_run, flags)  # warm-up (allocates the staging buffers)
         hts = []
         for _ in range(2):

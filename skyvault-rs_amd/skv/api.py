@@ -194,8 +194,8 @@ class Compactor:
                           max_run_size: int = MAX_RUN_SIZE, flags: int = 0, with_runs: bool = False):
         """skv_compact on raw host buffers (e.g. pinned tensors): [(seq_no, [(host_ptr, length)])].
         Returns (output bytes, output runs) -- or, with_runs, the [OutRun] -- and releases the pinned
-        output."""
-        sa = StreamArgs(streams, device=True)
+        output. streams may also be a StreamArgs built with device=True (a table reused across calls)."""
+        sa = streams if isinstance(streams, StreamArgs) else StreamArgs(streams, device=True)
         res = C.POINTER(SkvResult)()
         rc = self.lib.skv_compact(self.ctx, sa.ptr, sa.n, max_run_size, flags, C.byref(res))
         if rc != SKV_OK:

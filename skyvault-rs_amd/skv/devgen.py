@@ -36,6 +36,32 @@ def make_cfg2_on_device(device, seed, n_streams, n_records, vsize, variant="A"):
     return runs
 
 
+def _hex_run_on_device(device, ids, vsize, g):
+    """One v1 run of Puts with 16 B hex keys of the sorted ids and device-RNG values, in HBM."""
+    rec = 9 + 16 + vsize
+    n = int(ids.size)
+    run = torch.empty(1 + n * rec, dtype=torch.uint8, device=device)
+    run[0] = 1
+    body = run[1:].view(n, rec)
+    body[:, 0:5] = torch.tensor([1, 0, 0, 0, 16], dtype=torch.uint8, device=device)
+    body[:, 5:21] = torch.from_numpy(np.ascontiguousarray(gen.hex16(ids))).to(device)
+    body[:, 21:25] = torch.tensor(list(int(vsize).to_bytes(4, "big")), dtype=torch.uint8, device=device)
+    body[:, 25:] = torch.randint(0, 256, (n, vsize), dtype=torch.uint8, device=device, generator=g)
+    return run
+
+
+def make_l0_on_device(device, seed, n_buffer=16, n_l0=1024, run_records=14925, vsize=256):
+    """gen.config_l0's shape built in HBM: (buffer runs, L0 member runs). Stream table: buffer run b
+    at SeqNo b + 1, the L0 runs concatenated as one stream at SeqNo 0."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    buf, l0 = gen.l0_ids(seed, n_buffer, n_l0, run_records)
+    bruns = [_hex_run_on_device(device, ids, vsize, g) for ids in buf]
+    lruns = [_hex_run_on_device(device, ids, vsize, g) for ids in l0]
+    torch.cuda.synchronize(device)
+    return bruns, lruns
+
+
 def make_cfg3_on_device(device, seed, n_streams, run_mib, vsize=256):
     """Config 3 (scaled): gen.config3's runs (variable-length sorted alnum keys, 10 % Deletes)
     built on the host, copied to HBM."""

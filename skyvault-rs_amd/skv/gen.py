@@ -159,6 +159,32 @@ def config2(seed: int = BASE_SEED, n_streams: int = 64, n_records: int = 238821,
     return [(s + 1, [hex_key_run(seed + s, n_records, vsize, universe).tobytes()]) for s in range(n_streams)]
 
 
+def l0_ids(seed: int, n_buffer: int, n_l0: int, run_records: int):
+    """Key ids of a table-buffer compaction with a concatenated L0: (buffer id arrays, L0 id arrays).
+    One universe of 2 x all records, so buffer records supersede some L0 records; the L0 runs hold
+    consecutive slices of one sorted id set (ascending, disjoint key ranges, as build_runs' outputs)."""
+    universe = 2 * (n_buffer + n_l0) * run_records
+    l0 = unique_sorted_u64(seed, n_l0 * run_records, universe)
+    buf = [unique_sorted_u64(seed + 1 + b, run_records, universe) for b in range(n_buffer)]
+    return buf, [l0[i * run_records:(i + 1) * run_records] for i in range(n_l0)]
+
+
+def config_l0(seed: int = BASE_SEED, n_buffer: int = 16, n_l0: int = 1024, run_records: int = 14925,
+              vsize: int = 256):
+    """Table-buffer compaction with L0 (table_buffer_compaction.rs:31-100): n_buffer buffer runs at
+    SeqNo 1..n_buffer plus ONE stream at SeqNo 0 concatenating n_l0 ascending L0 runs; config 2's
+    record shape (16 B hex keys, vsize B values; 14,925 records = one 4 MiB run)."""
+    buf, l0 = l0_ids(seed, n_buffer, n_l0, run_records)
+
+    def run(ids, tag):
+        vals = random_bytes(seed ^ (0x3C3C + tag), ids.size * vsize).reshape(ids.size, vsize)
+        return assemble_run(hex16(ids), vals, np.ones(ids.size, dtype=bool)).tobytes()
+
+    streams = [(b + 1, [run(ids, b)]) for b, ids in enumerate(buf)]
+    streams.append((0, [run(ids, 1000 + i) for i, ids in enumerate(l0)]))
+    return streams
+
+
 def alnum_keys(ids: np.ndarray, min_len: int = 8, max_len: int = 128):
     """Deterministic alnum key of each id (length min..max); returns (flat, lengths)."""
     h = mix64(ids)
