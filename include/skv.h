@@ -35,8 +35,9 @@
 extern "C" {
 #endif
 
-#define SKV_ABI_VERSION 6  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts; 4: skv_scan_runs;
-                              5: skv_timings.span_parse (was reserved); 6: skv_timings.wal_stage */
+#define SKV_ABI_VERSION 7  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts; 4: skv_scan_runs;
+                              5: skv_timings.span_parse (was reserved); 6: skv_timings.wal_stage;
+                              7: skv_ctx_host_info */
 
 typedef struct skv_ctx skv_ctx;
 
@@ -160,6 +161,11 @@ void skv_ctx_destroy(skv_ctx* ctx);
 const char* skv_last_error(const skv_ctx* ctx); /* reference Display text of the last error */
 int skv_ctx_set_profiling(skv_ctx* ctx, int enable);
 int skv_ctx_get_timings(const skv_ctx* ctx, skv_timings* out);
+/* The host side of a ctx's device: the NUMA node its GPU hangs off (-1: unknown) and the host
+ * threads of that device's worker pool (the 10^6-entry table passes of a call run on it). Each
+ * device has its own pool, bound to the CPUs of that node, and a ctx's pinned staging and output
+ * buffers are allocated on that node. */
+int skv_ctx_host_info(const skv_ctx* ctx, int* numa_node, int* host_threads);
 
 /*
  * Host-memory entry point: the shape skyvault's jobs have (Bytes in from get_run,

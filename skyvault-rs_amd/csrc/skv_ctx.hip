@@ -2,11 +2,20 @@
 // call (build_job) and the guarded device call (run_guarded). C ABI: include/skv.h.
 #include "skv_host.hpp"
 
+#include <pthread.h>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <deque>
 #include <exception>
+#include <fstream>
+#include <sstream>
 
 using namespace skv;
+
+thread_local int skv_tl_device = -1;
 
 
 int set_err(skv_ctx* ctx, int code, const char* fmt, ...) {
@@ -25,7 +34,7 @@ void* pinned(skv_ctx* ctx, size_t bytes) {
         else if (ctx->pinned) HIPCHK(hipHostFree(ctx->pinned));
         ctx->pinned = nullptr;
         size_t cap = std::max<size_t>(bytes, 1 << 16);
-        HIPCHK(hipHostMalloc(&ctx->pinned, cap, hipHostMallocDefault));
+        HIPCHK(host_alloc_near(ctx->device, &ctx->pinned, cap, hipHostMallocDefault));
         ctx->pinned_cap = cap;
     }
     return ctx->pinned;
@@ -46,8 +55,27 @@ struct HostPool {
     std::mutex m;
     std::condition_variable cv;
     std::deque<PoolBatch*> q;  // one token per helper wanted; a token names its batch
-    explicit HostPool(unsigned n) {
-        for (unsigned i = 0; i < n; ++i) std::thread([this] { work(); }).detach();
+    // n detached workers, each bound to `cpus` (the GPU's NUMA node) when that leaves it any CPU the
+    // process may run on
+    HostPool(unsigned n, const std::vector<int>& cpus) {
+        for (unsigned i = 0; i < n; ++i)
+            std::thread([this, cpus] {
+                bind_to(cpus);
+                work();
+            }).detach();
+    }
+    static void bind_to(const std::vector<int>& cpus) {
+        if (cpus.empty()) return;
+        cpu_set_t allowed, want;
+        if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
+        CPU_ZERO(&want);
+        int n = 0;
+        for (int c : cpus)
+            if (c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &allowed)) {
+                CPU_SET(c, &want);
+                ++n;
+            }
+        if (n) (void)pthread_setaffinity_np(pthread_self(), sizeof want, &want);
     }
     static void drain(PoolBatch* b) {
         for (;;) {
@@ -85,18 +113,101 @@ unsigned host_threads_cap() {  // SKV_HOST_THREADS: host threads for 10^6-entry 
     }();
     return cap;
 }
-HostPool& host_pool() {  // started on first use, never torn down (detached workers idle in cv.wait)
-    static HostPool* p = new HostPool(host_threads_cap() > 1 ? host_threads_cap() - 1 : 1);
-    return *p;
+std::string read_text(const std::string& path) {
+    std::ifstream f(path);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    return ss.str();
+}
+std::vector<int> parse_cpulist(const std::string& s) {  // "0-63,128-191"
+    std::vector<int> out;
+    std::stringstream ss(s);
+    std::string item;
+    while (std::getline(ss, item, ',')) {
+        const size_t d = item.find('-');
+        try {
+            if (d == std::string::npos) {
+                if (!item.empty() && item[0] != '\n') out.push_back(std::stoi(item));
+            } else {
+                const int a = std::stoi(item.substr(0, d)), b = std::stoi(item.substr(d + 1));
+                for (int c = a; c <= b && c - a < 65536; ++c) out.push_back(c);
+            }
+        } catch (...) {
+        }
+    }
+    return out;
+}
+// The host side of one GPU: its NUMA node (from the PCI bus via sysfs), that node's CPUs, and a
+// host worker pool of its own. One process driving the 8 GPUs of a node (skv.multi.MultiCompactor,
+// skv_pool) then runs each device's 10^6-entry table passes on threads near that device instead of
+// queueing every device's passes on one shared pool. Pool size: SKV_HOST_THREADS (default 8), at
+// most the machine's CPUs / devices.
+struct DevHost {
+    int numa = -1;
+    std::vector<int> cpus;
+    unsigned threads = 1;  // the caller + threads - 1 workers
+    HostPool* pool = nullptr;
+};
+DevHost& dev_host(int device) {  // created on first use, never torn down (like the workers)
+    static std::mutex mu;
+    static std::map<int, DevHost*> hosts;
+    std::lock_guard<std::mutex> g(mu);
+    if (device < 0) device = 0;
+    auto it = hosts.find(device);
+    if (it != hosts.end()) return *it->second;
+    DevHost* d = new DevHost();
+    char bus[64] = {};
+    if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, device) == hipSuccess) {
+        for (char* c = bus; *c; ++c) *c = (char)tolower(*c);
+        const std::string nn = read_text(std::string("/sys/bus/pci/devices/") + bus + "/numa_node");
+        try {
+            d->numa = nn.empty() ? -1 : std::stoi(nn);
+        } catch (...) {
+            d->numa = -1;
+        }
+        if (d->numa >= 0)
+            d->cpus = parse_cpulist(read_text("/sys/devices/system/node/node" + std::to_string(d->numa) + "/cpulist"));
+    } else {
+        (void)hipGetLastError();
+    }
+    int ndev = 1;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) ndev = 1;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    d->threads = std::max(1u, std::min(host_threads_cap(), std::max(1u, hw / (unsigned)ndev)));
+    d->pool = new HostPool(d->threads > 1 ? d->threads - 1 : 1, d->cpus);
+    hosts[device] = d;
+    return *d;
 }
 }  // namespace
+
+int device_numa_node(int device) { return dev_host(device).numa; }
+
+hipError_t host_alloc_near(int device, void** p, size_t bytes, unsigned flags) {
+    const char* ne = getenv("SKV_NUMA");
+    const int node = device >= 0 && !(ne && ne[0] == '0') ? dev_host(device).numa : -1;
+    if (node < 0 || node >= 1024) return hipHostMalloc(p, bytes, flags);
+    // prefer the GPU's node for this thread while the pages are allocated (and pinned), then put the
+    // thread's own policy back; hipHostMallocNumaUser makes the allocation follow it
+    constexpr int MPOL_PREFERRED_ = 1;
+    unsigned long old_mask[16] = {}, mask[16] = {};
+    int old_mode = 0;
+    const bool have_old = syscall(SYS_get_mempolicy, &old_mode, old_mask, 1024ul, nullptr, 0ul) == 0;
+    mask[node / 64] |= 1ul << (node % 64);
+    const bool set = syscall(SYS_set_mempolicy, MPOL_PREFERRED_, mask, 1024ul) == 0;
+    const hipError_t e = hipHostMalloc(p, bytes, flags | (set ? hipHostMallocNumaUser : 0u));
+    if (set) {
+        if (have_old) (void)syscall(SYS_set_mempolicy, old_mode, old_mode ? old_mask : nullptr, old_mode ? 1024ul : 0ul);
+        else (void)syscall(SYS_set_mempolicy, 0, nullptr, 0ul);
+    }
+    return e;
+}
 
 void par_exec(unsigned nb, void (*run)(void*, unsigned), void* arg) {
     PoolBatch b;
     b.run = run;
     b.arg = arg;
     b.nb = nb;
-    HostPool& P = host_pool();
+    HostPool& P = *dev_host(skv_tl_device).pool;
     {
         std::lock_guard<std::mutex> l(P.m);
         for (unsigned k = 1; k < nb; ++k) P.q.push_back(&b);
@@ -115,8 +226,7 @@ void par_exec(unsigned nb, void (*run)(void*, unsigned), void* arg) {
 void stage_copy(void* dst, const void* src, size_t bytes) {
     const char* pe = getenv("SKV_PAR_COPY_MIN");  // tests: split small tables too
     const size_t kPar = pe ? (size_t)strtoull(pe, nullptr, 10) : (8u << 20);
-    const unsigned hw = std::thread::hardware_concurrency();
-    const unsigned nt = std::min<unsigned>(host_threads_cap(), hw ? hw : 1);
+    const unsigned nt = dev_host(skv_tl_device).threads;
     if (bytes < kPar || nt < 2) {
         memcpy(dst, src, bytes);
         return;
@@ -132,9 +242,7 @@ void stage_copy(void* dst, const void* src, size_t bytes) {
 // per-stream table loops of a 10^6-stream call (config 5) are memory-bound at one core's bandwidth,
 // ~10 ns per entry. Below min_par entries one block runs on the calling thread.
 unsigned par_nblocks(uint64_t n, uint64_t min_par) {
-    const unsigned hw = std::thread::hardware_concurrency();
-    const unsigned nt = std::min<unsigned>(host_threads_cap(), hw ? hw : 1);
-    return n < min_par ? 1u : nt;
+    return n < min_par ? 1u : dev_host(skv_tl_device).threads;
 }
 
 // async H2D of a host table through the pinned upload arena
@@ -149,7 +257,7 @@ void h2d_up(skv_ctx* ctx, void* dst, const void* src, size_t bytes) {
     if (ctx->up_chunk == ctx->up_chunks.size()) {
         const size_t cap = std::max<size_t>(need, 1 << 20);
         void* p = nullptr;
-        HIPCHK(hipHostMalloc(&p, cap, hipHostMallocDefault));
+        HIPCHK(host_alloc_near(ctx->device, &p, cap, hipHostMallocDefault));
         ctx->up_chunks.emplace_back((uint8_t*)p, cap);
         ctx->up_off = 0;
     }
@@ -417,6 +525,7 @@ int skv_ctx_create(int device, skv_ctx** out) {
     DeviceScope scope(device);
     skv_ctx* ctx = new skv_ctx();
     ctx->device = device;
+    ctx->out_pool->device = device;
     if (!scope.ok || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return SKV_E_DEVICE;
@@ -472,6 +581,14 @@ const char* skv_last_error(const skv_ctx* ctx) { return ctx ? ctx->err.c_str() :
 int skv_ctx_set_profiling(skv_ctx* ctx, int enable) {
     if (!ctx) return SKV_E_INVALID_ARG;
     ctx->profiling = enable != 0;
+    return SKV_OK;
+}
+
+int skv_ctx_host_info(const skv_ctx* ctx, int* numa_node, int* host_threads) {
+    if (!ctx) return SKV_E_INVALID_ARG;
+    DeviceScope scope(ctx->device);
+    if (numa_node) *numa_node = dev_host(ctx->device).numa;
+    if (host_threads) *host_threads = (int)dev_host(ctx->device).threads;
     return SKV_OK;
 }
 

@@ -33,6 +33,12 @@
 
 using namespace skv;
 
+// Pinned host memory on the NUMA node of `device`'s GPU (its node from the PCI bus via sysfs; the
+// thread's memory policy prefers that node while the pages are allocated). device < 0 or an unknown
+// node: a plain hipHostMalloc.
+hipError_t host_alloc_near(int device, void** p, size_t bytes, unsigned flags);
+int device_numa_node(int device);
+
 // ------------------------------------------------------------------------------------------
 struct DevBuf {
     void* p = nullptr;
@@ -44,6 +50,7 @@ enum Phase { PH_START = 0, PH_PARSE, PH_CHECK, PH_MERGE, PH_CHAIN, PH_GATHER, PH
 // Pinned host buffers for skv_compact outputs. Shared by the ctx and its live results, so a
 // result may outlive its ctx; a freed result's buffer is kept for the next call.
 struct PinnedPool {
+    int device = -1;  // buffers on this GPU's NUMA node
     std::mutex mu;
     std::vector<std::pair<void*, size_t>> free_list;
     ~PinnedPool() {
@@ -63,7 +70,7 @@ struct PinnedPool {
         }
         void* p = nullptr;
         cap = std::max<size_t>(bytes, 1 << 20);
-        if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+        if (host_alloc_near(device, &p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
         return p;
     }
     void give(void* p, size_t cap) {
@@ -139,14 +146,19 @@ int set_err(skv_ctx* ctx, int code, const char* fmt, ...);
 
 // Every C-ABI entry point runs on its ctx's device and leaves the caller's current device as it
 // found it (a host thread that drives several GPUs must not find its device switched by a call).
+// It also names the device whose host worker pool the call's table passes use (skv_tl_device).
+extern thread_local int skv_tl_device;
 struct DeviceScope {
-    int prev = -1;
+    int prev = -1, prev_tl = -1;
     bool ok = false;
     explicit DeviceScope(int dev) {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
         ok = hipSetDevice(dev) == hipSuccess;
+        prev_tl = skv_tl_device;
+        skv_tl_device = dev;
     }
     ~DeviceScope() {
+        skv_tl_device = prev_tl;
         if (prev >= 0) (void)hipSetDevice(prev);
     }
     DeviceScope(const DeviceScope&) = delete;

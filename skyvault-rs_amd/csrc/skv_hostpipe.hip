@@ -138,7 +138,7 @@ static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, doub
         if (ctx->part_k) HIPCHK(hipHostFree(ctx->part_k));
         ctx->part_k = nullptr;
         ctx->part_k_cap = 0;
-        HIPCHK(hipHostMalloc((void**)&ctx->part_k, std::max<uint64_t>(P, 64) * 8, hipHostMallocCoherent));
+        HIPCHK(host_alloc_near(ctx->device, (void**)&ctx->part_k, std::max<uint64_t>(P, 64) * 8, hipHostMallocCoherent));
         ctx->part_k_cap = std::max<uint64_t>(P, 64);
     }
     volatile uint64_t* hK = ctx->part_k;

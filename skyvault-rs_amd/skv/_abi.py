@@ -132,6 +132,7 @@ EXPORTED_SYMBOLS = [
     "skv_last_error",
     "skv_ctx_set_profiling",
     "skv_ctx_get_timings",
+    "skv_ctx_host_info",
     "skv_compact",
     "skv_compact_dev",
     "skv_encode_batch",

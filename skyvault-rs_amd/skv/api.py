@@ -54,6 +54,8 @@ def load():
     l.skv_last_error.restype = C.c_char_p
     l.skv_ctx_set_profiling.argtypes = [C.c_void_p, C.c_int]
     l.skv_ctx_get_timings.argtypes = [C.c_void_p, C.POINTER(SkvTimings)]
+    l.skv_ctx_host_info.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    l.skv_ctx_host_info.restype = C.c_int
     for fn in (l.skv_compact, l.skv_compact_dev):
         fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.POINTER(C.POINTER(SkvResult))]
         fn.restype = C.c_int
@@ -159,6 +161,14 @@ class Compactor:
             self.close()
         except Exception:
             pass
+
+    def host_info(self) -> dict:
+        """skv_ctx_host_info: the NUMA node of this ctx's GPU (-1: unknown) and its host pool's threads."""
+        node, threads = C.c_int(-1), C.c_int(0)
+        rc = self.lib.skv_ctx_host_info(self.ctx, C.byref(node), C.byref(threads))
+        if rc != SKV_OK:
+            raise self._err(rc)
+        return {"numa_node": node.value, "host_threads": threads.value}
 
     def _err(self, rc):
         return RunError(rc, self.lib.skv_last_error(self.ctx).decode("utf-8", "replace"))

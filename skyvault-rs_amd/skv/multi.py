@@ -10,10 +10,29 @@ come back to the caller's thread through the futures.
 """
 from __future__ import annotations
 
+import os
 import queue
 import threading
 from concurrent.futures import Future
-from typing import Callable, List, Optional, Sequence
+from typing import Callable, List, Optional, Sequence, Set
+
+
+def numa_cpus(node: int) -> Set[int]:
+    """CPUs of NUMA node `node` that this process may run on (sysfs cpulist; empty if unknown)."""
+    try:
+        with open(f"/sys/devices/system/node/node{int(node)}/cpulist") as f:
+            text = f.read().strip()
+    except OSError:
+        return set()
+    cpus = set()
+    for part in filter(None, text.split(",")):
+        a, _, b = part.partition("-")
+        cpus.update(range(int(a), int(b or a) + 1))
+    try:
+        cpus &= os.sched_getaffinity(0)
+    except (AttributeError, OSError):
+        pass
+    return cpus
 
 
 class MultiCompactor:
@@ -67,12 +86,25 @@ class _Worker(threading.Thread):
         self.q: "queue.Queue" = queue.Queue()
         self.queued_bytes = 0
         self.error: Optional[BaseException] = None
+        self.cpus: Set[int] = set()  # the NUMA-node CPUs this worker is bound to (empty: not bound)
 
     def run(self):
         try:
             comp = self.factory(self.device)  # the ctx is created and used on this thread only
         except BaseException as e:  # every later job fails with the ctx error
             comp, self.error = None, e
+        # this device's host thread runs near its GPU: bound to the CPUs of the GPU's NUMA node (the
+        # library allocates the ctx's pinned buffers there and runs its table passes on a pool bound
+        # there too), so eight devices' host work does not cross the socket link
+        info = getattr(comp, "host_info", None)
+        if info is not None:
+            try:
+                cpus = numa_cpus(info()["numa_node"])
+                if cpus:
+                    os.sched_setaffinity(0, cpus)
+                    self.cpus = cpus
+            except (OSError, ValueError, KeyError):
+                pass
         while True:
             item = self.q.get()
             if item is None:
