@@ -237,6 +237,8 @@ struct FxArgs {
     uint64_t T1, m2;
     const uint32_t* l1cnt;        // (T + 1) x k: stream j's level-1 samples sorted before splitter t
                                   // (k_fx_l1cnt), or null: k_fx_bounds searches them
+    const ulong2* keys;           // SKV_FX_DIAG=4 builds only: every record's (hi, lo) key, by record
+                                  // index, written before the tiles (the tiles read no record heads)
 };
 // flags[3] reason bits of a poisoned fused call
 enum : uint32_t { FXR_RECORD = 1, FXR_OVERSIZE = 2, FXR_SPLIT = 4, FXR_ORDER = 8, FXR_SAMPLE = 16 };

@@ -192,6 +192,10 @@ FxArgs fx_launch(skv_ctx* ctx, uint32_t k, uint32_t n_runs, const RunInfo* d_run
     A.tstate = (uint64_t*)(d_blob + o_tstate);  // zeroed by the blob upload
     A.tcounter = (uint32_t*)(d_blob + o_tick);
     A.out = io && io->out ? io->out : dbuf<uint8_t>(ctx, "out", out_bytes);
+#if SKV_FX_DIAG == 4
+    A.keys = dbuf<ulong2>(ctx, "fx_keys", R + 1);
+    launch_fx_keys(st, A, R, (ulong2*)A.keys);
+#endif
     mark(ctx, PH_CHECK);
     // ---- the fused tiles
     HIPCHK(launch_fx_tile(st, A));

@@ -882,6 +882,17 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
             return SKV_OK;
         }
         const uint64_t n = pres->n_runs;
+        if (getenv("SKV_GPIPE_DEBUG")) {
+            fprintf(stderr, "[gpipe] part %llu/%llu max %llu streams %zu runs %llu bytes %llu open %llu+%llu\n",
+                    (unsigned long long)p, (unsigned long long)P, (unsigned long long)job.max_run_size, sv.size(),
+                    (unsigned long long)n, (unsigned long long)pres->n_bytes, (unsigned long long)open_off,
+                    (unsigned long long)open_len);
+            for (uint64_t r = 0; r < n; ++r)
+                if (r < 3 || r + 3 >= n)
+                    fprintf(stderr, "   run %llu off %llu len %llu recs %llu\n", (unsigned long long)r,
+                            (unsigned long long)pres->runs[r].off, (unsigned long long)pres->runs[r].len,
+                            (unsigned long long)(pres->runs[r].put_count + pres->runs[r].delete_count));
+        }
         if (wal) {
             // whole tables: every run of the part is final at its offset in the call's output
             for (uint64_t r = 0; r < n; ++r) {
@@ -912,8 +923,13 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
         // writes there is the byte it read. Checked: part p's first run starts at the open run's offset
         // and holds at least its bytes; anything else would mean the input was overwritten.
         if (open_len && (n == 0 || pres->runs[0].off != 0 || pres->runs[0].len < open_len)) {
+            const std::string why = "internal: general pipeline part " + std::to_string(p) +
+                                    " did not re-emit the open run (runs " + std::to_string(n) + ", first at " +
+                                    std::to_string(n ? pres->runs[0].off : 0) + " len " +
+                                    std::to_string(n ? pres->runs[0].len : 0) + ", open run " + std::to_string(open_off) +
+                                    " len " + std::to_string(open_len) + ")";
             skv_result_free(pres);
-            throw DevError("internal: general pipeline part " + std::to_string(p) + " did not re-emit the open run");
+            throw DevError(why);
         }
         in_records += pres->in_records - (open_len ? open_recs : 0);  // the carried run's records once
         for (uint64_t r = 0; r < n; ++r) {

@@ -1628,7 +1628,10 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
                 } else {
                     uint64_t lo = b + 1, hi = K;
                     if (m0) lo = best;                 // window all <= v: answer at or past its end
-                    else if (ws > b + 1) hi = ws - 1;  // window all > v: answer before it
+                    // window all > v: the answer lies before it. A window predicted past the last
+                    // record (its entries past K read as ~0) says nothing beyond K: the search stays
+                    // inside P[0..K] (it read past the end and closed the last run too late)
+                    else if (ws > b + 1) hi = ws - 1 < K ? ws - 1 : K;
                     e = chain_search(P, lo, hi, v, lane);
                     Pe = P[e];
 #if SKV_CHAIN_PROF

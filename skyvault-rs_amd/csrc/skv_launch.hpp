@@ -156,6 +156,9 @@ struct IngestSlice {
 };
 void launch_ingest(hipStream_t, const IngestSlice* slices, uint32_t n, uint32_t blocks_per_slice);
 void launch_ingest_slices(hipStream_t, const IngestSlice* slices, uint64_t n, uint32_t grid);
+#if SKV_FX_DIAG == 4
+void launch_fx_keys(hipStream_t, const FxArgs& A, uint64_t R, ulong2* keys);
+#endif
 // skv_scan.hip: ScanFromRun after the merge
 void launch_scan_filter(hipStream_t, uint64_t R, uint32_t k, const uint64_t* stream_base, const uint64_t* a_addr,
                         const uint64_t* a_hi, const uint64_t* a_lo, const uint32_t* a_klen, const uint32_t* a_meta,

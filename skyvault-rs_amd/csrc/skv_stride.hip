@@ -24,7 +24,10 @@
 
 #ifndef SKV_FX_DIAG
 #define SKV_FX_DIAG 0  // diagnostic builds only (output invalid): 1 skip the copy, 2 skip the merge
-                       // rounds, 3 copy only (no key loads, no merge: records in load order)
+                       // rounds, 3 copy only (no key loads, no merge: records in load order);
+                       // 4 (output valid): the tiles take every key from a compact array written
+                       // before them (k_fx_keys), so they read no record head lines for the keys --
+                       // the price of the key phase's head-line traffic, measured
 #endif
 
 namespace skv {
@@ -793,6 +796,9 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     uint32_t bad = 0;
     {
         uint64_t ad[PER];
+#if SKV_FX_DIAG == 4
+        uint64_t gi[PER];
+#endif
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const uint32_t e = tid + u * FX_THREADS;
@@ -801,8 +807,23 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
                 const uint32_t j = fx_seg(cb0, k + 1, e);
                 const uint64_t sa = segaddr[j];
                 ad[u] = sa ? sa + (uint64_t)(e - cb0[j]) * S : fx_addr(A, j, sbase[j] + (e - cb0[j]));
+#if SKV_FX_DIAG == 4
+                gi[u] = sbase[j] + (e - cb0[j]);
+#endif
             }
         }
+#if SKV_FX_DIAG == 4
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            if (ad[u]) {
+                const uint32_t e = tid + u * FX_THREADS;
+                key[e] = A.keys[gi[u]];
+                id[e] = (uint16_t)e;
+            }
+        }
+        if (false)
+#endif
+        {
         FxRec rec[PER];
 #pragma unroll
         for (int u = 0; u < PER; ++u)
@@ -816,6 +837,7 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
                 key[e] = make_ulong2(h, l);
                 id[e] = (uint16_t)e;
             }
+        }
         }
     }
     __syncthreads();
@@ -1195,6 +1217,26 @@ __global__ void k_fx_desc(FxArgs A, DevRunDesc* descs, uint64_t* n_runs_out, uin
         descs[r] = d;
     }
 }
+
+#if SKV_FX_DIAG == 4
+// every record's key by record index (rank order), verified as k_fx_tile would (SKV_FX_DIAG=4 only)
+__global__ void k_fx_keys(FxArgs A, uint64_t R, ulong2* keys) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R) return;
+    uint32_t lo = 0, hi = A.k;  // stream j: stream_base[j] <= i < stream_base[j + 1]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (A.stream_base[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    uint64_t h = 0, l = 0;
+    if (!fx_key(A, fx_addr(A, lo, i), h, l)) fx_poison(A, FXR_RECORD);
+    keys[i] = make_ulong2(h, l);
+}
+void launch_fx_keys(hipStream_t s, const FxArgs& A, uint64_t R, ulong2* keys) {
+    if (R) k_fx_keys<<<(unsigned)((R + 255) / 256), 256, 0, s>>>(A, R, keys);
+}
+#endif
 
 // a part's survivor count to host-mapped memory (pipelined host calls): one lane, a vector
 // store with system scope, so the host sees it once the part's completion event has fired

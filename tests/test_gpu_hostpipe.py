@@ -140,9 +140,13 @@ def test_not_eligible_inputs_stay_serial(dev, pipe_env):
         streams.append((s + 1, [fmt.encode_run([fmt.put(f"{s % 3}.k{i:06d}", b"v" * (1 + i % 7)) for i in keys])]))
     _check(dev, streams, 1000, _abi.SKV_SPLIT_BY_TABLE, 4, expect_pipe=False)
     assert dev.timings()["host_parts"] == 0
-    l0 = [(1, [streams[0][1][0], streams[1][1][0]])] + streams[2:]
+    # member runs in descending key order ("1.*" before "0.*"): the concatenation decreases
+    l0 = [(1, [streams[1][1][0], streams[0][1][0]])] + streams[2:]
     _check(dev, l0, 1000, 0, 4, expect_pipe=False)
     assert dev.timings()["host_parts"] == 0
+    # in ascending order it is one sorted stream, and pipelines
+    l0 = [(1, [streams[0][1][0], streams[1][1][0]])] + streams[2:]
+    _check(dev, l0, 1000, 0, 4)
 
 
 # ---- the general key-range pipeline (variable-length records, Deletes) ------------------------

@@ -236,6 +236,54 @@ def test_wal_one_pass_stage(dev):
             os.environ["SKV_WAL_FUSED"] = old
 
 
+def test_chain_window_predicted_past_the_end(dev):
+    """k_chain (the single-wave greedy split) with records above max among small ones: near the end
+    of the merged records a run's predicted window lies wholly past the last record, and its
+    fallback search must stay inside P[0..K] -- it used to read past the end and close the last run
+    too late (one 36-record, 41,837-byte run at max 900). The input is the key range where the
+    general host pipeline's part 2 met it: five streams of 26 / 916 / 3,016-byte records cut to one
+    key range, plus the previous range's last output run at the lowest SeqNo."""
+    rng = random.Random(17)
+    ops_by_stream = []
+    for s in range(5):
+        ids = sorted(rng.sample(range(3000), 400))
+        ops_by_stream.append([fmt.put(f"r{i:06d}", bytes([s]) * rng.choice([10, 900, 3000])) for i in ids])
+    keys = sorted({op[1] for ops in ops_by_stream for op in ops})
+    cuts = [None] + [keys[p * len(keys) // 6] for p in range(1, 6)] + [None]
+    carry = None
+    for p in range(6):
+        lo, hi = cuts[p], cuts[p + 1]
+        sts = [(s + 1, [fmt.encode_run([op for op in ops if (lo is None or op[1] >= lo) and (hi is None or op[1] < hi)])])
+               for s, ops in enumerate(ops_by_stream)]
+        if carry is not None:
+            sts.append((-100, [carry]))
+        for mx in (900, 2500):
+            exp, got = _run_both(dev, sts, mx, 0)
+            assert exp == got, (p, mx, _diff(exp, got))
+        carry = pyoracle.compact(sts, 900, 0)[-1].data
+
+
+def test_greedy_split_random_sizes_with_oversized_records(dev):
+    """build_runs' greedy split (runs.rs:211-238) where records above max sit among small ones:
+    300 random inputs (record sizes 10 B to 4 KB in runs of similar sizes, max 20 B to 6 KB), each
+    equal to the oracle -- the single-wave chain's windows, its fallback searches near the end and
+    the one-record runs of oversized records."""
+    r = random.Random(53)
+    bad = []
+    for seed in range(300):
+        streams = []
+        for s in range(r.randint(1, 6)):
+            n = r.randint(0, 600)
+            keys = sorted(r.sample(range(5000), n))
+            sizes = [r.choice([1, 5, 30, 200, 900, 3000]) for _ in range(3)]
+            streams.append((s + 1, [fmt.encode_run([fmt.put(f"q{k:05d}", bytes([s]) * r.choice(sizes)) for k in keys])]))
+        mx = r.choice([20, 100, 500, 900, 1500, 3000, 6000])
+        exp, got = _run_both(dev, streams, mx, 0)
+        if exp != got:
+            bad.append((seed, mx, _diff(exp, got)))
+    assert not bad, bad[:5]
+
+
 def test_wal_one_pass_stage_many_tables(dev):
     """k_wal_fused's table-start list past the readback it reads with the verdict (WF_GUESS = 1024
     starts: the rest comes in a second copy) and past its capacity (WF_TCAP = 65536: the exact stage
