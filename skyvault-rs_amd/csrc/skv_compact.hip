@@ -502,6 +502,11 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         stream_base[k] = acc;
         if (acc != R) throw DevError("internal: record count mismatch");
     };
+    // Wide fixed-stride calls (config 5: 10^6 one-run streams) keep their run and stream tables on
+    // the device: record counts, flags and record bases come from k_run_tables + a scan, and the host
+    // copies (sum, stream_base / _valid / _err) are read back only if an error path needs them
+    // (materialize_tables). dev_tables: this call's tables live on the device only.
+    bool dev_tables = false;
     auto alloc_records = [&]() {
         rec_addr = dbuf<uint64_t>(ctx, "rec_addr", R);
         rec_hi = dbuf<uint64_t>(ctx, "rec_hi", R);
@@ -512,7 +517,19 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         HIPCHK(hipMemsetAsync(d_flags, 0, 16, st));
         HIPCHK(hipMemsetAsync(utf8_bad, 0, 4, st));
         HIPCHK(hipMemsetAsync(d_first_dec, 0xFF, (size_t)k * 8, st));
-        h2d_up(ctx, d_stream_base, stream_base.data(), (k + 1) * 8);
+        if (dev_tables)  // one run per stream, rank order: stream bases are the run record bases
+            HIPCHK(hipMemcpyAsync(d_stream_base, d_recb, (size_t)(k + 1) * 8, hipMemcpyDeviceToDevice, st));
+        else
+            h2d_up(ctx, d_stream_base, stream_base.data(), (k + 1) * 8);
+    };
+    auto materialize_tables = [&]() {  // the host tables of a dev_tables call (error paths only)
+        if (!dev_tables) return;
+        std::vector<uint64_t>& recb = ctx->s_recb;
+        recb.resize(n_runs + 1);
+        HIPCHK(hipMemcpy(recb.data(), d_recb, (size_t)(n_runs + 1) * 8, hipMemcpyDeviceToHost));
+        for (uint32_t r = 0; r < n_runs; ++r) sum[r] = RunSummary{recb[r + 1] - recb[r], 0u, 0u};
+        dev_tables = false;
+        stream_tables();
     };
     uint32_t utf8_flag = 0;
     // order check + readback of its result, the record flags and (fast path) the broken-run flags
@@ -561,7 +578,62 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     uint32_t uniform_meta = 0;  // every record a Put of one size (the fixed path's runs, one format): its meta
     uint64_t first_sum = 0, first_n = 0;  // the runs' first-record sizes (record capacity of the span parse)
     bool any_bodyless = false;            // a run of only a version byte (no span: the chunk-walk parse)
-    {
+    // the device-table variant: past the splitter merge's fan-in (the fused path cannot apply), one
+    // run per stream, a plain compaction or WAL flush (SKV_HOST_TABLES=1: the host tables always)
+    const bool try_dev_tables = k > (uint32_t)TILE_TARGET / 2 && n_runs == k && !job.scan && !job.search &&
+                                !job.batch && !job.part && !use_span && !getenv("SKV_HOST_TABLES");
+    if (try_dev_tables) {
+        uint64_t* d_cnt = dbuf<uint64_t>(ctx, "run_cnt", n_runs + 1);
+        uint32_t* d_rfl = dbuf<uint32_t>(ctx, "run_tflags", 4);
+        uint64_t* tmp = dbuf<uint64_t>(ctx, "run_scan_tmp", scan_tmp_words(n_runs) + 64);
+        HIPCHK(hipMemsetAsync(d_rfl, 0, 16, st));
+        launch_run_tables(st, d_runs, d_fmt, n_runs, d_cnt, d_rfl);
+        launch_scan(st, d_cnt, n_runs, d_recb, tmp);  // d_recb[n_runs] = R
+        uint8_t* hp = (uint8_t*)pinned(ctx, 64 + sizeof(RunFmt));
+        d2h(ctx, hp, d_rfl, 16);
+        d2h(ctx, hp + 16, d_recb + n_runs, 8);
+        d2h(ctx, hp + 32, d_fmt, sizeof(RunFmt));
+        sync(ctx);
+        htrace("run tables on the device");
+        uint32_t fl[4];
+        memcpy(fl, hp, 16);
+        const uint64_t Rd = *(const uint64_t*)(hp + 16);
+        if (!fl[RT_NOT_FIXED] && Rd < 0xFFFFFFFFull) {  // every run fixed-stride: the parse below
+            RunFmt f0;
+            memcpy(&f0, hp + 32, sizeof f0);
+            any_fixed = true;
+            dev_tables = true;
+            R = Rd;
+            any_err = false;  // (the fixed-stride parse decodes every record or marks its run broken)
+            alloc_records();
+            const bool will_sort = sort_by_fan_in(R);
+            fp_skipped = will_sort;
+            launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
+                               rec_meta, d_flags, d_stream_base, d_first_dec, will_sort ? nullptr : rec_fp,
+                               dbuf<uint32_t>(ctx, "wave_run", (R + 63) / 64 + 1));
+            mark(ctx, PH_PARSE);
+            if (allow_deferred && !(job.flags & SKV_SPLIT_BY_TABLE)) {
+                deferred = true;  // verdict read with the result
+                parsed = true;
+                std::fill(first_dec.begin(), first_dec.end(), ~0ull);
+                memset(hflags, 0, sizeof hflags);
+            } else {
+                parsed = !check_and_read(true);
+                htrace("parse verdict read");
+            }
+            if (parsed && !deferred && !fl[RT_NOT_UNIFORM] && !(hflags[3] & 1u)) uniform_meta = (uint32_t)f0.S;
+            if (!parsed) {  // a run is not what its first record promised: general parse, host tables
+                dev_tables = false;
+                fp_skipped = false;
+                R = 0;
+                any_err = false;
+                std::fill(stream_err.begin(), stream_err.end(), 0u);
+            }
+        } else {
+            any_fixed = fl[RT_ANY_FIXED] != 0;  // the general parse also runs k_emit_fixed then
+        }
+    }
+    if (!try_dev_tables) {
         RunFmt* hf = (RunFmt*)pinned(ctx, (size_t)n_runs * sizeof(RunFmt) + 16);
         d2h(ctx, hf, d_fmt, (size_t)n_runs * sizeof(RunFmt));
         htrace("header launched");
@@ -777,7 +849,10 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                                         rec_klen, rec_meta);
     bool any_dec = false;
     for (uint32_t s = 0; !dec_none && s < k; ++s)
-        if (first_dec[s] != ~0ull && first_dec[s] + 1 < stream_valid[s]) any_dec = true;
+        if (first_dec[s] != ~0ull) {
+            materialize_tables();
+            if (first_dec[s] + 1 < stream_valid[s]) any_dec = true;
+        }
     // A key-range part of a pipelined host call (skv_hostpipe.hip) holds the slices a cut by key
     // gave: with a decode error or a key decrease in a slice, the cut itself is not a key range and
     // the reference's outcome depends on the whole call's pop order (heap-order mode, error order).
@@ -854,6 +929,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     const bool heap = !job.batch && ((wal && (any_err || any_dec)) || ((job.flags & SKV_DROP_TOMBSTONES) && any_dec) ||
                                      (job.scan && (any_err || any_dec)));
     HeapRes hres;
+    if (any_err || any_dec) materialize_tables();
     if ((any_err || any_dec) && !job.scan) {  // (the scan resolved its first pulls above)
         // (1) first items are pulled in the caller's vector order (k_way.rs:126-140)
         std::vector<uint32_t> by_vec(k);
@@ -963,10 +1039,12 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             cmp_addr = ead;
         }
     }
-    std::vector<uint64_t> list_off = stream_base;
+    const bool sorting = sort_by_fan_in(R) || fp_skipped;
+    if (!sorting) materialize_tables();  // the splitter merge's list offsets are the stream bases
+    std::vector<uint64_t> list_off = sorting ? std::vector<uint64_t>{0, R} : stream_base;  // (no 10^6-entry copy)
     uint64_t* d_list_off = d_stream_base;
     {
-        if (sort_by_fan_in(R) || fp_skipped) {
+        if (sorting) {
             if (heap) {
                 // sort on the merge keys; the records' own keys, payload and meta follow in sorted
                 // order, and inv maps an original record index to its sorted position

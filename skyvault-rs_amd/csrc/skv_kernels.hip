@@ -1402,6 +1402,36 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     return v;
 }
 
+// Run tables of a wide fixed-stride call on the device (in place of a 10^6-entry RunFmt readback and
+// host loops): cnt[r] = the records of run r under its fixed-stride hypothesis, flags[RT_*] = 1 if any
+// run is not fixed-stride / differs from run 0's format / is fixed-stride / has no body (one wave
+// ballot, one atomic per wave).
+__global__ void k_run_tables(const RunInfo* __restrict__ runs, const RunFmt* __restrict__ fmt, uint32_t n_runs,
+                             uint64_t* cnt, uint32_t* flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool nf = false, nu = false, af = false, bl = false;
+    if (i < n_runs) {
+        const RunFmt f = fmt[i], f0 = fmt[0];
+        const uint64_t len = runs[i].len;
+        cnt[i] = f.S && len >= 1 ? (len - 1) / f.S : 0;
+        nf = f.S == 0;
+        nu = f.S != f0.S || f.K != f0.K;
+        af = f.S != 0;
+        bl = runs[i].n_chunks == 0;
+    }
+    const uint64_t bnf = __ballot(nf), bnu = __ballot(nu), baf = __ballot(af), bbl = __ballot(bl);
+    if ((threadIdx.x & 63) == 0) {
+        if (bnf) atomicOr(flags + RT_NOT_FIXED, 1u);
+        if (bnu) atomicOr(flags + RT_NOT_UNIFORM, 1u);
+        if (baf) atomicOr(flags + RT_ANY_FIXED, 1u);
+        if (bbl) atomicOr(flags + RT_BODYLESS, 1u);
+    }
+}
+void launch_run_tables(hipStream_t s, const RunInfo* runs, const RunFmt* fmt, uint32_t n_runs, uint64_t* cnt,
+                       uint32_t* flags) {
+    if (n_runs) k_run_tables<<<(n_runs + 255) / 256, 256, 0, s>>>(runs, fmt, n_runs, cnt, flags);
+}
+
 // largest e in [lo, hi] with P[e] <= v, given P[lo] <= v (64-ary search, exact). Not inlined: k_chain
 // unrolls its resolve step CH_D times, and 32 inlined copies of this rare fallback made the kernel
 // ~50 KB of straight-line code, streamed through the instruction cache on every round.

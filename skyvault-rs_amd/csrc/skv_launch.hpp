@@ -156,6 +156,11 @@ struct IngestSlice {
 };
 void launch_ingest(hipStream_t, const IngestSlice* slices, uint32_t n, uint32_t blocks_per_slice);
 void launch_ingest_slices(hipStream_t, const IngestSlice* slices, uint64_t n, uint32_t grid);
+// per-run record counts of fixed-stride runs ((len - 1) / S) and run-table flags, for calls whose
+// run tables stay on the device (skv_compact.hip, wide fixed-stride calls)
+enum : uint32_t { RT_NOT_FIXED = 0, RT_NOT_UNIFORM = 1, RT_ANY_FIXED = 2, RT_BODYLESS = 3 };
+void launch_run_tables(hipStream_t, const RunInfo* runs, const RunFmt* fmt, uint32_t n_runs, uint64_t* cnt,
+                       uint32_t* flags);
 #if SKV_FX_DIAG == 4
 void launch_fx_keys(hipStream_t, const FxArgs& A, uint64_t R, ulong2* keys);
 #endif
