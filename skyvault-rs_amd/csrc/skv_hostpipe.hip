@@ -577,6 +577,11 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     const bool wal = (job.flags & SKV_SPLIT_BY_TABLE) != 0;
     if (job.in_bytes < min_bytes || job.batch || job.search || job.scan) return SKV_OK;
     if (k == 0 || nr == 0) return SKV_OK;
+    // Past 2^16 member runs the host's cut search costs what the transfers do: every run is walked up
+    // to its last cut (10^6 config-5 runs: 125-147 ms on 8 threads by a walk or a batched binary
+    // search, measured on a host harness, against ~80 ms for the whole H2D), so such calls (a WAL
+    // flush of 10^6 tiny runs) take the serial path.
+    if (nr > (1u << 16)) return SKV_OK;
     // parts of ~1 GiB: each part costs a DMA copy per slice (config 3, 3.7 GiB: 4 parts 99.8 ms, 6
     // parts 102.9, 8 parts 105.0, 10 parts 110.5)
     uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(32, job.in_bytes / (1ull << 30)));

@@ -11,14 +11,26 @@ R="$PWD"
 O="$R/gpurun_out/r04f"
 mkdir -p "$O"
 export TMPDIR=/tmp
-S="${STAGE:-bench prof pmc}"
+S="${STAGE:-bench pmc}"
 CS="${CONFIGS:-2A 2B 3 3F 5 L0}"
 for C in $CS; do
   if [[ " $S " == *" bench "* ]]; then
-    if [ "$C" = 2A ]; then A="--steps 20 --warmup 5"; else A="--config $C --steps 5 --warmup 1"; fi
-    [ "$C" = 3F ] && A="$A --no-host-path"
-    timeout -k 10 420 python3 bench.py $A > "$O/bench_$C.log" 2>&1 || { echo "bench $C failed"; tail -5 "$O/bench_$C.log"; exit 1; }
+    # the bench line under rocprofv3 --kernel-trace --stats: its roofline (HIP-event launch time) and
+    # the committed kernel stats come from the same process (no host-path / 2-ctx calls in it, so
+    # every skv launch in the trace is one of the bench's compactions: warm-up + steps + the check)
+    if [ "$C" = 2A ]; then A="--steps 20 --warmup 5"; N=26; else A="--config $C --steps 5 --warmup 1"; N=7; fi
+    cd /tmp
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/bprof_$C" -o run -- \
+      python3 "$R/bench.py" $A --no-host-path > "$O/bench_$C.log" 2>&1 || { echo "bench $C failed"; tail -5 "$O/bench_$C.log"; exit 1; }
+    cd "$R"
+    python3 tools/kstats_skv.py "$(ls $O/bprof_$C/*kernel_stats.csv | head -1)" $N "$O/kernel_stats_$C.csv" > /dev/null
+    cp "$(ls $O/bprof_$C/*kernel_stats.csv | head -1)" "$O/rocprof_stats_$C.csv"
+    rm -rf "$O/bprof_$C"
     echo "bench $C: $(tail -1 $O/bench_$C.log | cut -c1-300)"
+    if [ "$C" != 3F ] && [ "${HOST:-1}" = 1 ]; then  # the PCIe-inclusive figure, its own run
+      timeout -k 10 600 python3 bench.py $A --no-cpu-baseline > "$O/host_$C.log" 2>&1 || { echo "host $C failed"; tail -5 "$O/host_$C.log"; exit 1; }
+      echo "host $C: $(tail -1 $O/host_$C.log | grep -o '"host_path": {[^}]*' | cut -c1-200)"
+    fi
   fi
   if [[ " $S " == *" prof "* ]]; then
     cd /tmp

@@ -11,7 +11,7 @@ if [ "${DIAG:-1}" = 1 ]; then
 fi
 if [ "${AB:-1}" = 1 ]; then
   for r in 0 1; do
-    for v in base u1 u1w8; do
+    for v in base u1 u1w8 cap1024; do
       lib=skyvault-rs_amd/skv/libskv.so
       [ "$v" != base ] && lib=skyvault-rs_amd/skv/variants/libskv_$v.so
       SKV_LIB=$lib timeout -k 10 120 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-path \
@@ -24,5 +24,10 @@ if [ "${C5:-1}" = 1 ]; then
   SKV_HOST_TRACE=1 timeout -k 10 300 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline --no-host-path \
     > "$O/c5_trace.log" 2>&1 || { echo "config 5 failed"; tail -5 "$O/c5_trace.log"; exit 1; }
   tail -1 "$O/c5_trace.log" | cut -c1-400
+  # the PCIe-inclusive figure of config 5 (10^6 tiny WAL runs: the cut search over every run on the
+  # host, the kernel ingest), with the host milestones of each call
+  SKV_HOST_TRACE=1 timeout -k 10 400 python bench.py --config 5 --steps 2 --warmup 1 --no-cpu-baseline \
+    > "$O/c5_host.log" 2>&1 || { echo "config 5 host failed"; tail -5 "$O/c5_host.log"; exit 1; }
+  tail -1 "$O/c5_host.log" | grep -o '"host_path": {[^}]*' | cut -c1-300
 fi
 exit 0
