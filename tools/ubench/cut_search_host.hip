@@ -1,3 +1,6 @@
+// Host-side harness (plain C++, builds with g++ or hipcc): the general pipeline's cut search over 10^6
+// config-5 WAL runs (83 x 49-byte records), one walk per run for all cuts vs a batched binary search.
+// g++ -O2 -pthread -x c++ cut_search_host.hip -o cut_search && ./cut_search 8
 #include <cstdint>
 #include <cstring>
 #include <string>
