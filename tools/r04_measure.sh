@@ -20,6 +20,17 @@ if [ "${AB:-1}" = 1 ]; then
     done
   done
 fi
+if [ "${T2K:-1}" = 1 ]; then  # general merge tiles of 2048 (2 workgroups per CU) vs 4096 (1 per CU)
+  for c in 3F 3; do
+    for v in base tile2k seg512 seg1024; do
+      lib=skyvault-rs_amd/skv/libskv.so
+      [ "$v" != base ] && lib=skyvault-rs_amd/skv/variants/libskv_$v.so
+      SKV_LIB=$lib timeout -k 10 300 python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline --no-host-path \
+        > "$O/t2k_${c}_$v.log" 2>&1 || { echo "tile variant $v $c failed"; tail -3 "$O/t2k_${c}_$v.log"; exit 1; }
+      echo "$c $v $(grep -o '"ms_per_step": [0-9.]*' $O/t2k_${c}_$v.log) $(grep -o '"phases_ms": {[^}]*' $O/t2k_${c}_$v.log)"
+    done
+  done
+fi
 if [ "${C5:-1}" = 1 ]; then
   SKV_HOST_TRACE=1 timeout -k 10 300 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline --no-host-path \
     > "$O/c5_trace.log" 2>&1 || { echo "config 5 failed"; tail -5 "$O/c5_trace.log"; exit 1; }
