@@ -307,7 +307,7 @@ SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth, uint6
 // key length (descriptors, WAL split).
 void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo, uint64_t*& addr, uint32_t*& klen,
                          uint32_t*& meta, const uint32_t*& cmp_klen, bool last_wins, const SElem** sorted,
-                         uint32_t const_meta) {
+                         uint32_t const_meta, const SortMerged* merged, uint64_t** d_K) {
     hipStream_t st = ctx->stream;
     SElem* E = dbuf<SElem>(ctx, "sort_e", R);
     SElem* T = dbuf<SElem>(ctx, "sort_t", R);
@@ -323,8 +323,10 @@ void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo, uint64
     uint32_t* nklen = dbuf<uint32_t>(ctx, "srt_klen", R);
     uint32_t* ncklen = dbuf<uint32_t>(ctx, "srt_cklen", R);
     uint32_t* nmeta = dbuf<uint32_t>(ctx, "srt_meta", R);
-    launch_sort_store(st, R, S, meta, const_meta, newkey, newkey_ex, nhi, nlo, naddr, nklen, ncklen, nmeta, last_wins);
+    launch_sort_store(st, R, S, meta, const_meta, newkey, newkey_ex, nhi, nlo, naddr, nklen, ncklen, nmeta, last_wins,
+                      merged ? *merged : SortMerged{});
     HIPCHK(hipGetLastError());
+    if (d_K) *d_K = newkey_ex + R;  // distinct keys (the survivors when merged arrays were asked for)
     if (sorted) *sorted = S;
     hi = nhi;
     lo = nlo;
@@ -1040,6 +1042,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         }
     }
     const bool sorting = sort_by_fan_in(R) || fp_skipped;
+    bool sorted_merged = false;     // the sort emitted the merged arrays (no level-0 merge tiles)
+    uint64_t* sorted_K = nullptr;   // then: the survivor count, on the device
     if (!sorting) materialize_tables();  // the splitter merge's list offsets are the stream bases
     std::vector<uint64_t> list_off = sorting ? std::vector<uint64_t>{0, R} : stream_base;  // (no 10^6-entry copy)
     uint64_t* d_list_off = d_stream_base;
@@ -1071,8 +1075,25 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                 cmp_klen = ck;
                 hres.inv = inv;
             } else {
+                // Without the Delete filter (and outside writer batches and scans) the survivors of the
+                // one sorted list are the first record of each key: the sort's store emits the merged
+                // arrays itself and the level-0 merge tiles are skipped (SKV_SORT_MERGED=0: the tiles)
+                const char* sme = getenv("SKV_SORT_MERGED");
+                const bool direct = !(job.flags & SKV_DROP_TOMBSTONES) && !job.batch && !job.scan &&
+                                    !(sme && sme[0] == '0');
+                SortMerged M{};
+                if (direct) {
+                    M.m_rec = dbuf<uint32_t>(ctx, "m_rec", R + 1);
+                    M.m_src = dbuf<uint64_t>(ctx, "m_src", R + 1);
+                    M.size = dbuf<uint64_t>(ctx, "sm_size", R + 1);
+                    M.del = dbuf<uint64_t>(ctx, "sm_del", R + 1);
+                    M.mm = dbuf<uint32_t>(ctx, "tile_mm", 2);
+                    const uint32_t mm0[2] = {0xFFFFFFFFu, 0u};
+                    h2d_up(ctx, M.mm, mm0, 8);
+                }
                 sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen, job.batch, nullptr,
-                             uniform_meta);
+                             uniform_meta, direct ? &M : nullptr, direct ? &sorted_K : nullptr);
+                sorted_merged = direct;
                 cmp_hi = rec_hi;
                 cmp_lo = rec_lo;
                 cmp_addr = rec_addr;
@@ -1086,7 +1107,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         }
     }
     std::vector<Level> lv(1);
-    lv[0].N = R;
+    if (sorted_merged) lv[0].N = 0;  // (no sample levels: nothing below is merged again)
+    else lv[0].N = R;
     lv[0].off = list_off;
     lv[0].hi = cmp_hi;
     lv[0].lo = cmp_lo;
@@ -1161,7 +1183,15 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         if (!SKV_PAGE_GATHER && !(ge && ge[0] == '0') && !(job.flags & (SKV_SPLIT_BY_TABLE | SKV_DROP_TOMBSTONES)))
             m_dup = dbuf<uint64_t>(ctx, "m_dup", R + 1);
     }
-    for (int li = (int)lv.size() - 1; li >= 0; --li) {
+    if (sorted_merged) {  // m_P / m_Dp: exclusive scans of the survivors' sizes / Delete bits
+        uint64_t* tmp = dbuf<uint64_t>(ctx, "sm_scan_tmp", scan_tmp_words(R + 1) + 64);
+        launch_scan_dn(st, dbuf<uint64_t>(ctx, "sm_size", R + 1), sorted_K, R, m_P, tmp);
+        launch_scan_dn(st, dbuf<uint64_t>(ctx, "sm_del", R + 1), sorted_K, R, m_Dp, tmp);
+        HIPCHK(hipMemcpyAsync(d_Kout, sorted_K, 8, hipMemcpyDeviceToDevice, st));
+        tile_max = dbuf<uint32_t>(ctx, "tile_mm", 2);
+        T0 = 1;
+    }
+    for (int li = sorted_merged ? -1 : (int)lv.size() - 1; li >= 0; --li) {
         Level& L = lv[li];
         const bool l0 = li == 0;
         uint64_t T = 1, m = 1;

@@ -129,9 +129,20 @@ void launch_copy_bytes(hipStream_t, uint8_t* dst, const uint8_t* src, uint64_t n
 // skv_sort.hip — record sort (fan-in above TILE_TARGET / 2)
 void launch_sort_load(hipStream_t, uint64_t R, const uint64_t* hi, const uint64_t* lo, const uint64_t* addr,
                       const uint32_t* klen, SElem* E, bool last_wins);
+// The merged arrays of a record-sorted call taken straight from the sort (no level-0 merge tiles):
+// survivor g = the first record of the g-th distinct key. size / del are the survivors' record sizes
+// and Delete bits (scanned into m_P / m_Dp afterwards); mm = (min, max) survivor size. All null: the
+// merge stage runs its tiles over the sorted list instead.
+struct SortMerged {
+    uint32_t* m_rec = nullptr;
+    uint64_t* m_src = nullptr;
+    uint64_t* size = nullptr;
+    uint64_t* del = nullptr;
+    uint32_t* mm = nullptr;
+};
 void launch_sort_store(hipStream_t, uint64_t R, const SElem* E, const uint32_t* meta_in, uint32_t const_meta,
                        const uint64_t* newkey, const uint64_t* newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr,
-                       uint32_t* klen, uint32_t* cmp_klen, uint32_t* meta, bool last_wins);
+                       uint32_t* klen, uint32_t* cmp_klen, uint32_t* meta, bool last_wins, SortMerged M = SortMerged{});
 void launch_sort_sample(hipStream_t, const SElem* E, uint64_t n, uint64_t Ns, SElem* S);
 void launch_sort_prefix(hipStream_t, const SElem* Ss, uint64_t ov, uint64_t Tb, uint32_t* L);
 void launch_sort_bucket(hipStream_t, SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,

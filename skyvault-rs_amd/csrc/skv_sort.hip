@@ -115,17 +115,44 @@ __global__ void k_sort_load(uint64_t R, const uint64_t* __restrict__ hi, const u
 __global__ void k_sort_store(uint64_t R, const SElem* __restrict__ E, const uint32_t* __restrict__ meta_in,
                              uint32_t const_meta, const uint64_t* __restrict__ newkey,
                              const uint64_t* __restrict__ newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr,
-                             uint32_t* klen, uint32_t* cmp_klen, uint32_t* meta, bool last_wins) {
+                             uint32_t* klen, uint32_t* cmp_klen, uint32_t* meta, bool last_wins, SortMerged M) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= R) return;
-    const SElem e = E[i];
-    const uint64_t src = last_wins ? R - 1 - e.pos : e.pos;
-    hi[i] = newkey_ex[i] + newkey[i] - 1;
-    lo[i] = 0;
-    addr[i] = e.addr;
-    klen[i] = e.klen;
-    cmp_klen[i] = 0;
-    meta[i] = const_meta ? const_meta : meta_in[src];
+    const bool live = i < R;
+    uint32_t sz = 0xFFFFFFFFu, szx = 0;
+    if (live) {
+        const SElem e = E[i];
+        const uint64_t src = last_wins ? R - 1 - e.pos : e.pos;
+        const uint64_t nk = newkey[i];
+        hi[i] = newkey_ex[i] + nk - 1;
+        lo[i] = 0;
+        addr[i] = e.addr;
+        klen[i] = e.klen;
+        cmp_klen[i] = 0;
+        const uint32_t m = const_meta ? const_meta : meta_in[src];
+        meta[i] = m;
+        // the merged arrays of the one sorted list, straight from the sort: the first record of each
+        // key is its survivor (k_way.rs:146-151), and its index among the survivors is its key's rank
+        if (M.m_rec && nk) {
+            const uint64_t g = newkey_ex[i];
+            M.m_rec[g] = (uint32_t)i;
+            M.m_src[g] = e.addr;
+            M.size[g] = m & 0x7FFFFFFFu;
+            M.del[g] = m >> 31;
+            sz = szx = m & 0x7FFFFFFFu;
+        }
+    }
+    if (M.m_rec) {  // (min, max) surviving record size, for the split (k_chain)
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t a = __shfl_xor(sz, d, 64), b = __shfl_xor(szx, d, 64);
+            sz = a < sz ? a : sz;
+            szx = b > szx ? b : szx;
+        }
+        if ((threadIdx.x & 63) == 0 && szx) {
+            atomicMin(M.mm, sz);
+            atomicMax(M.mm + 1, szx);
+        }
+    }
 }
 
 // S[j] = E[j * n / Ns]  (n < 2^32)
@@ -555,10 +582,10 @@ void launch_sort_load(hipStream_t s, uint64_t R, const uint64_t* hi, const uint6
 }
 void launch_sort_store(hipStream_t s, uint64_t R, const SElem* E, const uint32_t* meta_in, uint32_t const_meta,
                        const uint64_t* newkey, const uint64_t* newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr,
-                       uint32_t* klen, uint32_t* cmp_klen, uint32_t* meta, bool last_wins) {
+                       uint32_t* klen, uint32_t* cmp_klen, uint32_t* meta, bool last_wins, SortMerged M) {
     if (R)
         k_sort_store<<<sk_blocks(R), 256, 0, s>>>(R, E, meta_in, const_meta, newkey, newkey_ex, hi, lo, addr, klen,
-                                                  cmp_klen, meta, last_wins);
+                                                  cmp_klen, meta, last_wins, M);
 }
 void launch_sort_sample(hipStream_t s, const SElem* E, uint64_t n, uint64_t Ns, SElem* S) {
     if (Ns) k_sort_sample<<<sk_blocks(Ns), 256, 0, s>>>(E, n, Ns, S);
