@@ -1,0 +1,26 @@
+#!/bin/bash
+# Builds the round-4 measurement variants of libskv.so (skv/variants/libskv_<tag>.so) from the
+# current sources, one object directory per tag (skyvault-rs_amd/Makefile `variant`). CPU only.
+#   diag3    k_fx_tile copy-only diagnostic (no key phase; wrong output)
+#   diag4    k_fx_tile keys from a compact (hi, lo) array (k_fx_keys) instead of the record lines
+#   u1, u1w8 k_fx_tile unroll 1 / unroll 1 with 8 waves (occupancy A/B)
+#   cap1024  fused tiles of 1024 records
+#   tile2k   general merge tiles of 2048 elements, 512 threads (2 workgroups per CU)
+#   seg512, seg1024  k_gather segments of 512 / 1024 records
+set -eu
+cd "$(dirname "$0")/../skyvault-rs_amd"
+J=${J:-8}
+declare -A F=(
+  [diag3]="-DSKV_FX_DIAG=3"
+  [diag4]="-DSKV_FX_DIAG=4"
+  [u1]="-DSKV_FX_U=1"
+  [u1w8]="-DSKV_FX_U=1 -DSKV_FX_WAVES=8"
+  [cap1024]="-DSKV_FX_CAP=1024"
+  [tile2k]="-DSKV_TILE_CAP=2048 -DSKV_TILE_TARGET=1536 -DSKV_TILE_THREADS=512"
+  [seg512]="-DSKV_GATHER_SEG=512"
+  [seg1024]="-DSKV_GATHER_SEG=1024"
+)
+for tag in ${TAGS:-${!F[@]}}; do
+  make -s -j"$J" variant TAG="$tag" VFLAGS="${F[$tag]}"
+  echo "built skv/variants/libskv_$tag.so (${F[$tag]})"
+done
