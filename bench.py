@@ -525,6 +525,8 @@ def main():
             "phases_ms": dict(zip(("parse", "check", "merge", "chain", "gather"),
                                   [round(float(x), 4) for x in np.mean(np.array(phases), axis=0)])),
             "record_sort": bool(t["sorted"]),
+            # general path: 1 the one-pass span parse ran, 2 | bits << 8 it declined, 0 not tried
+            "span_parse": int(t["span_parse"]),
             "roofline": {
                 "bound": "hbm",
                 "kernel": hot_kernel,

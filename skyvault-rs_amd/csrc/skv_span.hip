@@ -2,37 +2,51 @@
 // (runs.rs:559-626) for every input run at once, reading every run byte exactly once.
 //
 // The chunk-walk parse (k_spec / k_emit, skv_kernels.hip) reads each record's header lines twice
-// from HBM with dependent loads: 88 GB of line traffic for config 3F's 64 GB of runs. Here one
+// from HBM with dependent loads: 104 GB of line traffic for config 3F's 63 GB of runs. Here one
 // workgroup takes one SPAN-byte span of a run and:
 //   1. stages the span (+ MARGIN bytes of the next, for records that start near its end) in LDS
 //      with coalesced 16-byte loads;
-//   2. wave 0 walks it in LDS: lane l owns SPAN/64 bytes, finds its first record start
-//      speculatively (a marker byte from which 3 records decode), walks the records starting in
-//      its bytes and keeps their offsets; the lanes' walks are then checked against each other
-//      (lane l must start where the nearest earlier lane with records ended);
+//   2. resolves its record chain in LDS with every thread: each thread marks the marker-valued
+//      bytes (1 Put, 2 Delete) of its 64 staged bytes as candidate record starts; each candidate
+//      decodes its header from LDS (key length, a Put's value length) into the candidate its record
+//      ends on, or EXIT (the record ends past the span), or DEAD (no candidate there, or a header
+//      that does not decode); pointer jumping (one jump table per power of two) gives every
+//      candidate its chain length and terminal. The span's first record is its run's first byte
+//      (span 0), else the first candidate whose chain reaches EXIT with at least min(3, longest)
+//      records; the chain's records are listed by composing jumps (one lookup per set bit);
 //   3. publishes its record count (decoupled look-back over spans in ticket order) to learn the
 //      global index of its first record;
 //   4. parses its records again from LDS (prefix, key length, size | Delete, fingerprint of the key
 //      bytes past 16, exact UTF-8) and writes the record arrays at their final indices.
-// A span's speculative first start is checked against the previous span's exit by k_span_check.
+// A span's chosen first start is checked against the previous span's exit by k_span_check.
 // A span in which no record starts (a run's short tail, or inside a record longer than a span) is
 // checked to lie inside the record that crosses it. Anything unusual -- a decode error, an invalid
-// UTF-8 key, a lane that started off the record chain, more records than the arrays hold -- sets a
-// fail bit, and the host runs the chunk-walk parse instead, which reproduces
-// the reference's exact error. Only a clean decode of every run is taken from here.
+// UTF-8 key, a first start off the record chain, more candidates than a span resolves, more records
+// than the arrays hold -- sets a fail bit, and the host runs the chunk-walk parse instead, which
+// reproduces the reference's exact error. Only a clean decode of every run is taken from here.
+// (Round 3's walk -- 64 lanes of wave 0 scanning their bytes one at a time with a 3-record decode at
+// every marker-valued byte -- spent 350 us per span in lane divergence; tools/r03_spandbg.sh.)
 #include "skv_dev.hpp"
 #include "skv_launch.hpp"
 
 namespace skv {
 
 constexpr uint32_t SPAN = SPAN_BYTES;
-constexpr uint32_t SPAN_MARGIN = 512;               // bytes staged past the span
-constexpr uint32_t SPAN_SUB = SPAN / 64;            // bytes per walking lane
-constexpr uint32_t SPAN_LCAP = 64;                  // record starts a lane keeps (multiple of 8)
+constexpr uint32_t SPAN_MARGIN = 512;                       // bytes staged past the span
 constexpr uint32_t SPAN_THREADS = 256;
+constexpr uint32_t SPAN_PT = SPAN / SPAN_THREADS;           // staged bytes a thread scans for markers
 constexpr uint32_t SPAN_BLOCKS = (SPAN + SPAN_MARGIN) / 16 + 2;  // staged 16-byte blocks
-static_assert(SPAN_SUB * 64 == SPAN && SPAN <= 65536, "u16 offsets, 64 walking lanes");
-static_assert(SPAN_LCAP % 8 == 0, "walk_fast stores record starts eight at a time");
+constexpr uint32_t SPAN_WORDS = SPAN / 32;                  // candidate bitmap words
+constexpr uint32_t SPAN_WPT = (SPAN_WORDS + SPAN_THREADS - 1) / SPAN_THREADS;
+constexpr uint32_t SPAN_CCAP = 512;                         // candidates a span resolves (more: the chunk walks)
+constexpr uint32_t SPAN_CPT = SPAN_CCAP / SPAN_THREADS;     // candidates per thread in the chain phases
+constexpr uint32_t SPAN_LV = 10;                            // jump levels: 2^(LV-1) >= CCAP
+constexpr uint16_t SJ_EXIT = 0xFFFE, SJ_DEAD = 0xFFFF;      // jump terminals
+constexpr uint32_t SNX_LONG = 0xFFFFFFFFu;                  // a record end past the staged bytes
+static_assert(SPAN_PT % 16 == 0 && SPAN_PT <= 64, "a thread's marker bits fit one 64-bit mask");
+static_assert(SPAN <= 65536 && SPAN_WORDS % SPAN_THREADS == 0, "u16 offsets, whole bitmap words per thread");
+static_assert((1u << (SPAN_LV - 1)) >= SPAN_CCAP && SPAN_CCAP < SJ_EXIT && SPAN_CCAP % SPAN_THREADS == 0,
+              "jump levels cover the longest chain");
 
 enum : uint32_t { SPF_DECODE = 1, SPF_CHAIN = 2, SPF_OVER = 8, SPF_UTF8 = 16, SPF_CAP = 32 };
 
@@ -44,6 +58,14 @@ struct SpanLoad {
         return (a >= g0 && a < g1) ? lds[(a - g0) >> 4] : gblk(a);
     }
 };
+
+// big-endian u32 at staged byte bo (bo + 4 <= staged bytes)
+__device__ __forceinline__ uint32_t span_be32(const uint4* buf, uint32_t bo) {
+    const uint32_t q = bo >> 4, sh = bo & 15;
+    const uint4 a = buf[q];
+    const uint4 b = sh > 12 ? buf[q + 1] : make_uint4(0, 0, 0, 0);
+    return __builtin_bswap32(funnel16(a, b, sh).x);
+}
 
 __device__ __forceinline__ uint64_t span_lookback(uint64_t* st, uint64_t t, uint64_t agg) {
     constexpr uint64_t FA = 1ull << 62, FI = 2ull << 62, VM = FA - 1;
@@ -90,17 +112,30 @@ __device__ __forceinline__ uint32_t span_run(const RunInfo* runs, uint32_t n_run
 __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __restrict__ runs, uint32_t n_runs,
                                                              uint64_t n_spans, SpanOut O) {
     __shared__ uint4 buf[SPAN_BLOCKS];
-    __shared__ __attribute__((aligned(16))) uint16_t lst[64 * SPAN_LCAP];
-    __shared__ uint32_t pre[65];
-    __shared__ uint64_t s_t, s_base;
-    __shared__ uint32_t s_fail;
+    __shared__ uint32_t cbits[SPAN_WORDS];            // candidate starts, bit x
+    __shared__ uint16_t crank[SPAN_WORDS];            // candidates before each bitmap word
+    __shared__ uint16_t cpos[SPAN_CCAP];              // candidate i's offset x (ascending)
+    __shared__ uint32_t cnx[SPAN_CCAP];               // its record's end (offset), SNX_LONG past the stage
+    __shared__ uint16_t jmp[SPAN_LV * SPAN_CCAP];     // level r: the candidate 2^r records on, or a terminal
+    __shared__ uint16_t lst[SPAN_CCAP];               // the chosen chain's record offsets, in order
+    __shared__ uint32_t ws[SPAN_THREADS / 64];
+    __shared__ uint32_t s_more[3];
+    __shared__ uint64_t s_t, s_base, s_exit;
+    __shared__ uint32_t s_fail, s_maxlen, s_s0, s_len, s_last;
     const uint32_t tid = threadIdx.x;
     uint64_t* const tk = O.dbg ? (uint64_t*)(O.dbg + 6) : nullptr;  // phase ticks (SKV_SPAN_DBG)
     uint64_t t0 = tk ? wall_clock64() : 0, t1 = 0, t2 = 0, t3 = 0;
     if (tid == 0) {
         s_t = atomicAdd(O.ticket, 1u);
         s_fail = 0;
+        s_maxlen = 0;
+        s_s0 = NO_POS32;
+        s_len = 0;
+        s_last = 0;
+        s_exit = NO_POS;
+        s_more[0] = s_more[1] = s_more[2] = 0;
     }
+    for (uint32_t w = tid; w < SPAN_WORDS; w += SPAN_THREADS) cbits[w] = 0;
     __syncthreads();
     const uint64_t s = s_t;
     const uint32_t r = span_run(runs, n_runs, s);
@@ -130,103 +165,229 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
     const SpanLoad ld{buf, g0, g1};
     const uint8_t* bytes = (const uint8_t*)buf;
     if (tk) t1 = wall_clock64();
-    // ---- 2. wave 0 walks the span, lane l the records starting in [a, b)
-    uint64_t count = 0;
-    if (tid < 64) {
-        const uint32_t l = tid;
-        const uint64_t a = cs + (uint64_t)l * SPAN_SUB, b = a + SPAN_SUB < ce ? a + SPAN_SUB : ce;
-        uint32_t fail = 0;
-        uint64_t st = NO_POS, e = NO_POS;  // NO_POS: at or past ce
-        uint32_t n = 0;
-        if (a < ce) {
-            if (local == 0 && l == 0) {
-                st = 1;
-            } else {
-                for (uint64_t p = a; p < ce; ++p) {  // the first marker from which 3 records decode
-                    const uint32_t m = bytes[(uintptr_t)run + p - g0];
-                    if ((m == 1 || m == 2) && walk_fast<2>(run, R.len, p, R.len, 3, ld).err == DERR_NONE) {
-                        st = p;
-                        break;
+    // offsets x are relative to cs; staged byte of x: x + d0
+    const uint32_t d0 = (uint32_t)((uintptr_t)run + cs - g0);
+    const uint32_t nspan = (uint32_t)(ce - cs);
+    const uint64_t rel = R.len - cs;                          // run bytes from x = 0
+    const uint32_t avail = (uint32_t)(g1 - g0) - d0;           // staged bytes from x = 0 (>= min(rel, nspan + MARGIN))
+    // ---- 2a. candidates: marker-valued bytes at x in [0, nspan); bit i of cm <-> x = xs + i
+    const int32_t xs = (int32_t)(tid * SPAN_PT) - (int32_t)d0;
+    uint64_t cm = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < SPAN_PT / 16; ++q) {
+        const uint32_t b = tid * (SPAN_PT / 16) + q;
+        const uint4 v = b < nb ? buf[b] : make_uint4(0, 0, 0, 0);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) {
+            const uint32_t by = (w4[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+            if (by - 1u < 2u) cm |= 1ull << (q * 16 + i);
+        }
+    }
+    if (xs < 0) cm &= ~0ull << (uint32_t)(-xs);  // bytes before cs (-xs <= 15)
+    {
+        const int32_t lim = (int32_t)nspan - xs;  // bits from lim on are past the span
+        if (lim <= 0) cm = 0;
+        else if (lim < 64) cm &= (1ull << (uint32_t)lim) - 1;
+    }
+    for (uint64_t c = cm; c; c &= c - 1) {
+        const uint32_t x = (uint32_t)(xs + (int32_t)__builtin_ctzll(c));
+        atomicOr(&cbits[x >> 5], 1u << (x & 31));
+    }
+    __syncthreads();
+    // ---- 2b. candidate ranks: exclusive prefix of the bitmap's popcounts
+    uint32_t m;
+    {
+        uint32_t pc[SPAN_WPT], mine = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < SPAN_WPT; ++u) {
+            pc[u] = __builtin_popcount(cbits[tid * SPAN_WPT + u]);
+            mine += pc[u];
+        }
+        const uint32_t lane = tid & 63, wv = tid >> 6;
+        uint32_t inc = mine;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += o;
+        }
+        if (lane == 63) ws[wv] = inc;
+        __syncthreads();
+        uint32_t before = 0;
+        m = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < SPAN_THREADS / 64; ++w) {
+            before += w < wv ? ws[w] : 0u;
+            m += ws[w];
+        }
+        uint32_t ex = before + inc - mine;
+#pragma unroll
+        for (uint32_t u = 0; u < SPAN_WPT; ++u) {
+            crank[tid * SPAN_WPT + u] = (uint16_t)ex;
+            ex += pc[u];
+        }
+    }
+    __syncthreads();
+    auto rank_of = [&](uint32_t x) -> uint32_t {
+        return crank[x >> 5] + __builtin_popcount(cbits[x >> 5] & ((1u << (x & 31)) - 1u));
+    };
+    const bool over = m > SPAN_CCAP;  // (uniform)
+    // ---- 2c. each candidate's record: its end, and the candidate there (level-0 jump)
+    if (!over) {
+        for (uint64_t c = cm; c; c &= c - 1) {
+            const uint32_t x = (uint32_t)(xs + (int32_t)__builtin_ctzll(c));
+            const uint32_t i = rank_of(x);
+            cpos[i] = (uint16_t)x;
+            uint16_t j0 = SJ_DEAD;
+            uint32_t nx = SNX_LONG;
+            if ((uint64_t)x + 5 <= rel) {  // runs.rs:570-576: the key length is in the run
+                const uint64_t kend = (uint64_t)x + 5 + span_be32(buf, x + d0 + 1);
+                bool ok = false, known = false;
+                uint64_t e = 0;
+                if (kend <= rel) {  // :580-583 the key is in the run
+                    if (bytes[x + d0] == 2) {  // Delete: marker, key length, key
+                        ok = known = true;
+                        e = kend;
+                    } else if (kend + 4 <= rel) {  // :598-604 the value length is in the run
+                        if (kend + 4 <= avail) {
+                            e = kend + 4 + span_be32(buf, (uint32_t)kend + d0);
+                            ok = known = e <= rel;  // :608-611 the value is in the run
+                        } else {
+                            ok = true;  // ends past the staged bytes, so past the span: EXIT
+                        }
                     }
                 }
+                if (ok) {
+                    if (known && e < nspan) j0 = ((cbits[e >> 5] >> (e & 31)) & 1u) ? (uint16_t)rank_of((uint32_t)e) : SJ_DEAD;
+                    else j0 = SJ_EXIT;
+                    nx = known && e < SNX_LONG ? (uint32_t)e : SNX_LONG;
+                }
             }
-            if (st < b) {
-                const WalkRes w = walk_fast<0>(run, R.len, st, b, 0xFFFFFFFFu, ld, lst + l * SPAN_LCAP, SPAN_LCAP, cs);
-                if (w.err) fail |= SPF_DECODE;
-                if (w.cnt > SPAN_LCAP) fail |= SPF_OVER;
-                n = w.cnt;
-                e = w.end;
-            } else {
-                e = st;
+            jmp[i] = j0;
+            cnx[i] = nx;
+        }
+    }
+    __syncthreads();
+    // ---- 2d. pointer jumping: level r = level r-1 twice; stops once every chain has ended
+    uint32_t lv = 1;
+    if (!over && m > 0) {
+        for (uint32_t rr = 1; rr < SPAN_LV; ++rr) {
+            uint32_t more = 0;
+            for (uint32_t i = tid; i < m; i += SPAN_THREADS) {
+                const uint16_t y = jmp[(rr - 1) * SPAN_CCAP + i];
+                const uint16_t z = y < SJ_EXIT ? jmp[(rr - 1) * SPAN_CCAP + y] : y;
+                jmp[rr * SPAN_CCAP + i] = z;
+                more |= z < SJ_EXIT ? 1u : 0u;
             }
+            if (more) s_more[rr % 3] = 1;
+            if (tid == 0) s_more[(rr + 1) % 3] = 0;
+            __syncthreads();
+            lv = rr + 1;
+            if (!s_more[rr % 3]) break;  // (uniform: read between this barrier and the next clear)
         }
-        // the chain check: lane l starts where the nearest earlier lane with records ended (or, with
-        // none, where lane 0 started); a lane whose bytes hold no record start found none before b
-        const uint64_t has = __ballot(n > 0);
-        const uint64_t s0 = __shfl(st, 0, 64);
-        const uint64_t below = has & ((1ull << l) - 1);
-        const int j = below ? 63 - __builtin_clzll(below) : -1;
-        const uint64_t ej = __shfl(e, j < 0 ? 0 : j, 64);
-        const uint64_t P = j < 0 ? s0 : ej;
-        if (a < ce && l > 0) {
-            const bool ok = P >= b ? (st >= b) : (st == P);
-            if (!ok) fail |= SPF_CHAIN;
-        }
-        // no record start in this span (s0 >= ce): fine when a record crosses it (k_span_check)
-        // the span's exit: the end of its last record (the lane with records furthest on)
-        const int jl = has ? 63 - __builtin_clzll(has) : -1;
-        const uint64_t ex = __shfl(e, jl < 0 ? 0 : jl, 64);
-        // lane prefix of the record counts
-        uint32_t inc = n;
+    }
+    // ---- 2e. chain length and terminal of each candidate (binary lifting), then the first start
+    uint32_t clen[SPAN_CPT], clast[SPAN_CPT];
+    bool cexit[SPAN_CPT];
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(inc, d, 64);
-            if (l >= (uint32_t)d) inc += o;
+    for (uint32_t u = 0; u < SPAN_CPT; ++u) {
+        const uint32_t i = tid + u * SPAN_THREADS;
+        clen[u] = 0;
+        clast[u] = 0;
+        cexit[u] = false;
+        if (!over && i < m) {
+            uint32_t x = i, len = 1;
+            for (int rr = (int)lv - 1; rr >= 0; --rr) {
+                const uint16_t y = jmp[rr * SPAN_CCAP + x];
+                if (y < SJ_EXIT) {
+                    x = y;
+                    len += 1u << rr;
+                }
+            }
+            clen[u] = len;
+            clast[u] = x;
+            cexit[u] = jmp[x] == SJ_EXIT;
+            if (cexit[u]) atomicMax(&s_maxlen, len);
         }
-        pre[l + 1] = inc;
-        if (l == 0) pre[0] = 0;
-        count = __shfl(inc, 63, 64);
-        if (l == 0 && O.hdr_err[r]) fail |= SPF_DECODE;  // a bad version byte: the exact path reports it
-        if (fail) atomicOr(O.fail, fail);
-        if (O.dbg && fail && atomicAdd(O.dbg, 1u) < 48)
-            printf("span %lu run %u local %lu cs %lu ce %lu len %lu | lane %u a %lu b %lu st %lu e %lu n %u P %lu fail %u\n",
+    }
+    __syncthreads();
+    {
+        const uint32_t need = s_maxlen < 3 ? s_maxlen : 3u;
+#pragma unroll
+        for (uint32_t u = 0; u < SPAN_CPT; ++u) {
+            const uint32_t i = tid + u * SPAN_THREADS;
+            if (local == 0) {  // the run's first record starts at its byte 1 (x = 0)
+                if (i == 0 && m > 0 && !over && (cbits[0] & 1u) && cexit[u]) s_s0 = 0;
+            } else if (cexit[u] && clen[u] >= need) {
+                atomicMin(&s_s0, i);
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t s0 = s_s0;
+#pragma unroll
+    for (uint32_t u = 0; u < SPAN_CPT; ++u)
+        if (tid + u * SPAN_THREADS == s0) {
+            s_len = clen[u];
+            s_last = clast[u];
+        }
+    __syncthreads();
+    // ---- 2f. the chain's records (jumps composed by the bits of d) and its exit
+    const uint32_t n0 = s0 != NO_POS32 ? s_len : 0u;
+    for (uint32_t d = tid; d < n0; d += SPAN_THREADS) {
+        uint32_t x = s0;
+        for (uint32_t rr = 0; rr < lv; ++rr)
+            if ((d >> rr) & 1u) x = jmp[rr * SPAN_CCAP + x];
+        lst[d] = cpos[x];
+    }
+    if (tid == 0) {
+        uint32_t f = 0;
+        if (over) f |= SPF_OVER;
+        if (local == 0 && s0 == NO_POS32) f |= SPF_DECODE;  // the run's first record does not decode
+        if (O.hdr_err[r]) f |= SPF_DECODE;                 // a bad version byte: the exact path reports it
+        if (n0) {
+            const uint32_t L = s_last;
+            if (cnx[L] != SNX_LONG) {
+                s_exit = cs + cnx[L];
+            } else {  // a record running past the staged bytes: its value length from HBM
+                const RecHdr h = parse_rec<false, 0>(run, R.len, cs + cpos[L], ld);
+                if (h.err) f |= SPF_DECODE;
+                s_exit = cs + cpos[L] + h.size;
+            }
+        }
+        if (f) s_fail = f;
+    }
+    __syncthreads();
+    uint32_t count = s_fail ? 0u : n0;
+    if (tid < 64) {
+        const uint64_t first = n0 ? cs + cpos[s0] : NO_POS;
+        if (tid == 0) {
+            O.first[s] = first;
+            O.exit[s] = s_exit;
+        }
+        if (O.dbg && s_fail && tid == 0 && atomicAdd(O.dbg, 1u) < 48)
+            printf("span %lu run %u local %lu cs %lu ce %lu len %lu | cand %u levels %u first %lu exit %lu n %u fail %u\n",
                    (unsigned long)s, r, (unsigned long)local, (unsigned long)cs, (unsigned long)ce,
-                   (unsigned long)R.len, l, (unsigned long)a, (unsigned long)b, (unsigned long)st,
-                   (unsigned long)e, n, (unsigned long)P, fail);
-        const bool any_fail = __ballot(fail != 0) != 0;
-        if (l == 0) {
-            O.first[s] = s0 < ce ? s0 : NO_POS;
-            O.exit[s] = ex;
-            if (any_fail) s_fail = 1;
-        }
+                   (unsigned long)R.len, m, lv, (unsigned long)first, (unsigned long)s_exit, n0, s_fail);
         // ---- 3. global index of the span's first record (the look-back needs every span to publish)
         if (tk) t2 = wall_clock64();
         const uint64_t base = span_lookback(O.tstate, s, count);
-        if (l == 0) {
+        if (tid == 0) {
             s_base = base;
             if (local == 0) O.run_recb[r] = base;
             if (s + 1 == n_spans) O.run_recb[n_runs] = base + count;
-            if (base + count > O.cap) {
-                atomicOr(O.fail, SPF_CAP);
-                s_fail = SPF_CAP;
-            }
+            if (base + count > O.cap) s_fail |= SPF_CAP;
+            if (s_fail) atomicOr(O.fail, s_fail);
         }
     }
     __syncthreads();
     if (tk) t3 = wall_clock64();
     if (s_fail) return;
-    count = pre[64];
     const uint64_t base = s_base;
     // ---- 4. the record arrays: thread t parses records t, t + 256, ... from LDS
     uint32_t bad = 0;
-    for (uint32_t k = tid; k < count; k += SPAN_THREADS) {
-        uint32_t lo = 0, hi = 64;  // lane holding record k: pre[lo] <= k < pre[lo + 1]
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (pre[mid] <= k) lo = mid;
-            else hi = mid;
-        }
-        const uint64_t p = cs + lst[lo * SPAN_LCAP + (k - pre[lo])];
+    for (uint32_t d = tid; d < count; d += SPAN_THREADS) {
+        const uint64_t p = cs + lst[d];
         const RecHdr h = parse_rec<true, 1>(run, R.len, p, ld);
         if (h.err) {
             bad |= h.err == DERR_UTF8 ? SPF_UTF8 : SPF_DECODE;
@@ -238,7 +399,7 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
         }
         bool ascii;
         const uint64_t fpv = key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii, ld);
-        const uint64_t o = base + k;
+        const uint64_t o = base + d;
         O.rec_addr[o] = (uint64_t)(run + p);
         O.rec_hi[o] = h.hi;
         O.rec_lo[o] = h.lo;
