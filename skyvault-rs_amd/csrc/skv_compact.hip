@@ -509,16 +509,21 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // copies (sum, stream_base / _valid / _err) are read back only if an error path needs them
     // (materialize_tables). dev_tables: this call's tables live on the device only.
     bool dev_tables = false;
-    auto alloc_records = [&]() {
+    // zeroed verdict words: record flags, the UTF-8 flag, each stream's first decrease (none)
+    auto reset_verdict = [&]() {
+        HIPCHK(hipMemsetAsync(d_flags, 0, 16, st));
+        HIPCHK(hipMemsetAsync(utf8_bad, 0, 4, st));
+        HIPCHK(hipMemsetAsync(d_first_dec, 0xFF, (size_t)k * 8, st));
+    };
+    // reset = false: the span parse already produced the verdict words (its order check)
+    auto alloc_records = [&](bool reset = true) {
         rec_addr = dbuf<uint64_t>(ctx, "rec_addr", R);
         rec_hi = dbuf<uint64_t>(ctx, "rec_hi", R);
         rec_lo = dbuf<uint64_t>(ctx, "rec_lo", R);
         rec_klen = dbuf<uint32_t>(ctx, "rec_klen", R);
         rec_meta = dbuf<uint32_t>(ctx, "rec_meta", R);
         rec_fp = dbuf<uint64_t>(ctx, "rec_fp", R);
-        HIPCHK(hipMemsetAsync(d_flags, 0, 16, st));
-        HIPCHK(hipMemsetAsync(utf8_bad, 0, 4, st));
-        HIPCHK(hipMemsetAsync(d_first_dec, 0xFF, (size_t)k * 8, st));
+        if (reset) reset_verdict();
         if (dev_tables)  // one run per stream, rank order: stream bases are the run record bases
             HIPCHK(hipMemcpyAsync(d_stream_base, d_recb, (size_t)(k + 1) * 8, hipMemcpyDeviceToDevice, st));
         else
@@ -535,9 +540,10 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     };
     uint32_t utf8_flag = 0;
     // order check + readback of its result, the record flags and (fast path) the broken-run flags
-    auto check_and_read = [&](bool read_broken) -> bool {
+    // span_order: the span parse did the order check, its first decreases as global record indices
+    auto check_and_read = [&](bool read_broken, bool span_order = false) -> bool {
         // the fast path's parse kernel already did the order check
-        if (!read_broken && !job.batch)  // a writer batch is unsorted by definition
+        if (!read_broken && !job.batch && !span_order)  // a writer batch is unsorted by definition
             launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
         HIPCHK(hipGetLastError());
         // the verdict words first; the 10^6-entry tables only when a word says they hold something:
@@ -557,6 +563,9 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             if (need_broken) d2h(ctx, hq + (size_t)k * 8, d_broken, (size_t)n_runs * 4);
             sync(ctx);
             if (need_dec) memcpy(first_dec.data(), hq, (size_t)k * 8);
+            if (need_dec && span_order)
+                for (uint32_t s = 0; s < k; ++s)
+                    if (first_dec[s] != ~0ull) first_dec[s] -= stream_base[s];
             const uint32_t* b = (const uint32_t*)(hq + (size_t)k * 8);
             for (uint32_t r = 0; need_broken && r < n_runs && !broken; ++r) broken = b[r] != 0;
         }
@@ -757,6 +766,10 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         so.fail = sw + 1;
         so.hdr_err = d_hdr;
         so.cap = cap;
+        so.sbase = dbuf<uint64_t>(ctx, "span_base", n_chunks);
+        so.first_dec = job.batch ? nullptr : d_first_dec;  // (a writer batch is unsorted by definition)
+        so.any_dec = d_flags + 1;
+        reset_verdict();
         HIPCHK(hipMemsetAsync(so.tstate, 0, n_chunks * 8, st));
         HIPCHK(hipMemsetAsync(sw, 0, 128, st));
         {
@@ -789,10 +802,10 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                 for (uint64_t r = lo; r < hi; ++r) sum[r] = RunSummary{recb[r + 1] - recb[r], 0u, 0u};
             });
             stream_tables();
-            alloc_records();
+            alloc_records(false);
             rec_addr = so.rec_addr;
             mark(ctx, PH_PARSE);
-            check_and_read(false);
+            check_and_read(false, true);
             parsed = true;
         }
     }

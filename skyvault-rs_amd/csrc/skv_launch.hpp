@@ -205,6 +205,10 @@ struct SpanOut {
     const uint32_t* hdr_err; // k_run_header's verdict per run
     uint64_t cap;            // entries the record arrays hold
     uint32_t* dbg;           // SKV_SPAN_DBG=1: printf the first failing lanes (counter); null: off
+    uint64_t* sbase;         // per span: global index of its first record
+    unsigned long long* first_dec;  // in-stream order check (runs.rs:190-198): per stream, the global
+                                    // index of the record before its first decrease; null: no check
+    uint32_t* any_dec;       // set with any first_dec entry
 };
 void launch_span_parse(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_spans, const SpanOut& O);
 

@@ -67,6 +67,29 @@ __device__ __forceinline__ uint32_t span_be32(const uint4* buf, uint32_t bo) {
     return __builtin_bswap32(funnel16(a, b, sh).x);
 }
 
+// Rust str Ord of two parsed keys (runs.rs:190-198's comparison), the bytes past the 16-byte
+// prefixes through the span loader (LDS when staged)
+__device__ inline int span_key_cmp(const RecHdr& a, const uint8_t* ka, const RecHdr& b, const uint8_t* kb,
+                                   const SpanLoad& ld) {
+    if (a.hi != b.hi) return a.hi < b.hi ? -1 : 1;
+    if (a.lo != b.lo) return a.lo < b.lo ? -1 : 1;
+    if (a.klen > 16 && b.klen > 16) {
+        const uint64_t n = (a.klen < b.klen ? a.klen : b.klen) - 16;
+        for (uint64_t i = 0; i < n; i += 16) {
+            const uint32_t m = (uint32_t)(n - i < 16 ? n - i : 16);
+            const uint4 x = load_window16(ka + 16 + i, m, ld), y = load_window16(kb + 16 + i, m, ld);
+            const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                const uint32_t mk = dword_mask(0, m, q);
+                const uint32_t xa = __builtin_bswap32(xs[q] & mk), ya = __builtin_bswap32(ys[q] & mk);
+                if (xa != ya) return xa < ya ? -1 : 1;
+            }
+        }
+    }
+    return a.klen < b.klen ? -1 : (a.klen > b.klen ? 1 : 0);
+}
+
 __device__ __forceinline__ uint64_t span_lookback(uint64_t* st, uint64_t t, uint64_t agg) {
     constexpr uint64_t FA = 1ull << 62, FI = 2ull << 62, VM = FA - 1;
     const int lane = threadIdx.x & 63;
@@ -374,6 +397,7 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
         const uint64_t base = span_lookback(O.tstate, s, count);
         if (tid == 0) {
             s_base = base;
+            O.sbase[s] = base;
             if (local == 0) O.run_recb[r] = base;
             if (s + 1 == n_spans) O.run_recb[n_runs] = base + count;
             if (base + count > O.cap) s_fail |= SPF_CAP;
@@ -400,6 +424,14 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
         bool ascii;
         const uint64_t fpv = key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii, ld);
         const uint64_t o = base + d;
+        if (O.first_dec && d > 0) {  // in-stream order against the span's record before (k_span_check: its first)
+            const uint64_t q = cs + lst[d - 1];
+            const RecHdr hq = parse_rec<true, 0>(run, R.len, q, ld);
+            if (span_key_cmp(hq, run + q + 5, h, run + p + 5, ld) > 0) {
+                atomicMin(&O.first_dec[R.stream], (unsigned long long)(o - 1));
+                atomicOr(O.any_dec, 1u);
+            }
+        }
         O.rec_addr[o] = (uint64_t)(run + p);
         O.rec_hi[o] = h.hi;
         O.rec_lo[o] = h.lo;
@@ -444,6 +476,22 @@ __global__ void k_span_check(const RunInfo* __restrict__ runs, uint32_t n_runs, 
     }
     if (local + 1 == R.n_chunks) bad = bad || (first == NO_POS ? pe != R.len : O.exit[s] != R.len);
     if (bad) atomicOr(O.fail, SPF_CHAIN);
+    // the order check across span edges: a span's first record against the record before it in its
+    // stream (the previous span's last one, or the last one of the stream's previous member run)
+    // (only when every span emitted: a failed span left its records unwritten, and the host discards
+    // the arrays anyway)
+    if (!bad && O.first_dec && first != NO_POS && (local > 0 || (r > 0 && runs[r - 1].stream == R.stream)) &&
+        __hip_atomic_load(O.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        const uint64_t g = O.sbase[s];
+        if (g > 0) {
+            const int c = key_cmp(O.rec_hi[g - 1], O.rec_lo[g - 1], O.rec_klen[g - 1], (const uint8_t*)O.rec_addr[g - 1] + 5,
+                                  O.rec_hi[g], O.rec_lo[g], O.rec_klen[g], (const uint8_t*)O.rec_addr[g] + 5);
+            if (c > 0) {
+                atomicMin(&O.first_dec[R.stream], (unsigned long long)(g - 1));
+                atomicOr(O.any_dec, 1u);
+            }
+        }
+    }
     if (O.dbg && bad && atomicAdd(O.dbg, 1u) < 64)
         printf("check span %lu run %u local %lu first %lu prev_exit %lu exit %lu len %lu\n", (unsigned long)s, r,
                (unsigned long)local, (unsigned long)first, (unsigned long)pe, (unsigned long)O.exit[s],
