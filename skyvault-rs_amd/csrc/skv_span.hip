@@ -3,7 +3,7 @@
 //
 // The chunk-walk parse (k_spec / k_emit, skv_kernels.hip) reads each record's header lines twice
 // from HBM with dependent loads: 104 GB of line traffic for config 3F's 63 GB of runs. Here one
-// workgroup takes one SPAN-byte span of a run and:
+// workgroup (SPAN / 64 threads) takes one SPAN-byte span of a run and:
 //   1. stages the span (+ MARGIN bytes of the next, for records that start near its end) in LDS
 //      with coalesced 16-byte loads;
 //   2. resolves its record chain in LDS with every thread: each thread marks the marker-valued
@@ -33,18 +33,20 @@ namespace skv {
 
 constexpr uint32_t SPAN = SPAN_BYTES;
 constexpr uint32_t SPAN_MARGIN = 512;                       // bytes staged past the span
-constexpr uint32_t SPAN_THREADS = 256;
+constexpr uint32_t SPAN_THREADS = SPAN / 64;               // 64 staged bytes per thread
 constexpr uint32_t SPAN_PT = SPAN / SPAN_THREADS;           // staged bytes a thread scans for markers
 constexpr uint32_t SPAN_BLOCKS = (SPAN + SPAN_MARGIN) / 16 + 2;  // staged 16-byte blocks
 constexpr uint32_t SPAN_WORDS = SPAN / 32;                  // candidate bitmap words
 constexpr uint32_t SPAN_WPT = (SPAN_WORDS + SPAN_THREADS - 1) / SPAN_THREADS;
-constexpr uint32_t SPAN_CCAP = 512;                         // candidates a span resolves (more: the chunk walks)
+constexpr uint32_t SPAN_CCAP = SPAN / 32;                   // candidates a span resolves (more: the chunk walks)
 constexpr uint32_t SPAN_CPT = SPAN_CCAP / SPAN_THREADS;     // candidates per thread in the chain phases
-constexpr uint32_t SPAN_LV = 10;                            // jump levels: 2^(LV-1) >= CCAP
+constexpr uint32_t span_log2(uint32_t v) { return v <= 1 ? 0 : 1 + span_log2(v >> 1); }
+constexpr uint32_t SPAN_LV = span_log2(SPAN_CCAP) + 1;     // jump levels: 2^(LV-1) >= CCAP
 constexpr uint16_t SJ_EXIT = 0xFFFE, SJ_DEAD = 0xFFFF;      // jump terminals
 constexpr uint32_t SNX_LONG = 0xFFFFFFFFu;                  // a record end past the staged bytes
 static_assert(SPAN_PT % 16 == 0 && SPAN_PT <= 64, "a thread's marker bits fit one 64-bit mask");
-static_assert(SPAN <= 65536 && SPAN_WORDS % SPAN_THREADS == 0, "u16 offsets, whole bitmap words per thread");
+static_assert(SPAN <= 65536 && SPAN_WORDS % SPAN_THREADS == 0 && SPAN_THREADS <= 1024 && SPAN_THREADS % 64 == 0,
+              "u16 offsets, whole bitmap words per thread, whole waves");
 static_assert((1u << (SPAN_LV - 1)) >= SPAN_CCAP && SPAN_CCAP < SJ_EXIT && SPAN_CCAP % SPAN_THREADS == 0,
               "jump levels cover the longest chain");
 
@@ -408,7 +410,7 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
     if (tk) t3 = wall_clock64();
     if (s_fail) return;
     const uint64_t base = s_base;
-    // ---- 4. the record arrays: thread t parses records t, t + 256, ... from LDS
+    // ---- 4. the record arrays: thread t parses records t, t + SPAN_THREADS, ... from LDS
     uint32_t bad = 0;
     for (uint32_t d = tid; d < count; d += SPAN_THREADS) {
         const uint64_t p = cs + lst[d];

@@ -7,6 +7,7 @@
 #   cap1024  fused tiles of 1024 records
 #   tile2k   general merge tiles of 2048 elements, 512 threads (2 workgroups per CU)
 #   seg512, seg1024  k_gather segments of 512 / 1024 records
+#   span8k, span32k  span parse spans of 8 / 32 KiB (128 / 512 threads)
 set -eu
 cd "$(dirname "$0")/../skyvault-rs_amd"
 J=${J:-8}
@@ -19,6 +20,8 @@ declare -A F=(
   [tile2k]="-DSKV_TILE_CAP=2048 -DSKV_TILE_TARGET=1536 -DSKV_TILE_THREADS=512"
   [seg512]="-DSKV_GATHER_SEG=512"
   [seg1024]="-DSKV_GATHER_SEG=1024"
+  [span8k]="-DSKV_SPAN_BYTES=8192"
+  [span32k]="-DSKV_SPAN_BYTES=32768"
 )
 for tag in ${TAGS:-${!F[@]}}; do
   make -s -j"$J" variant TAG="$tag" VFLAGS="${F[$tag]}"

@@ -21,6 +21,13 @@ for c in 3 3F; do
     echo "$c span=$v $(grep -o '"ms_per_step": [0-9.]*' $O/span_${c}_$v.log) $(grep -o '"span_parse": [0-9]*' $O/span_${c}_$v.log) $(grep -o '"phases_ms": {[^}]*' $O/span_${c}_$v.log)"
   done
 done
+for v in span8k span32k; do  # span sizes (the chunk walks' fallback keeps the same chunking)
+  for c in 3 3F; do
+    SKV_SPAN=1 SKV_LIB=skyvault-rs_amd/skv/variants/libskv_$v.so timeout -k 10 300 python bench.py --config $c --steps 5 \
+      --warmup 1 --no-cpu-baseline --no-host-path > "$O/span_${c}_$v.log" 2>&1 || { echo "bench $c $v failed"; tail -5 "$O/span_${c}_$v.log"; exit 1; }
+    echo "$c $v $(grep -o '"ms_per_step": [0-9.]*' $O/span_${c}_$v.log) $(grep -o '"span_parse": [0-9]*' $O/span_${c}_$v.log) $(grep -o '"phases_ms": {[^}]*' $O/span_${c}_$v.log)"
+  done
+done
 SKV_SPAN=1 SKV_SPAN_DBG=1 timeout -k 10 300 python bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline \
   --no-host-path > "$O/span_3_ticks.log" 2>&1 || { tail -5 "$O/span_3_ticks.log"; exit 1; }
 grep "\[span\]" "$O/span_3_ticks.log" | tail -2
