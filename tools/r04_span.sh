@@ -6,6 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O="$PWD/gpurun_out/r04"
 mkdir -p "$O"
+if [ "${PARITY:-1}" = 1 ]; then
 SKV_SPAN=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 \
   --timeout-method thread > "$O/span_parity.log" 2>&1
 rc=$?
@@ -14,6 +15,8 @@ tail -3 "$O/span_parity.log"
 SKV_SPAN=1 SKV_SPAN_DBG=1 timeout -k 10 120 python tools/span_dbg.py 16 4000000 > "$O/span_dbg.log" 2>&1 \
   || { tail -20 "$O/span_dbg.log"; exit 1; }
 grep -E "span_parse|\[span\]|equal" "$O/span_dbg.log" | head -8
+fi
+[ "${BENCH:-1}" = 1 ] || exit 0
 for c in 3 3F; do
   for v in 0 1; do
     SKV_SPAN=$v timeout -k 10 300 python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline \
