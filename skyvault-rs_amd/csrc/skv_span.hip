@@ -215,8 +215,28 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
         if (lim <= 0) cm = 0;
         else if (lim < 64) cm &= (1ull << (uint32_t)lim) - 1;
     }
+    // the span's last d0 bytes sit in staged block SPAN / 16: the last thread scans it too
+    // (bit i of cm2 <-> x = SPAN - d0 + i)
+    uint32_t cm2 = 0;
+    if (tid == SPAN_THREADS - 1 && d0) {
+        const uint32_t b = SPAN / 16;
+        const uint4 v = b < nb ? buf[b] : make_uint4(0, 0, 0, 0);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) {
+            const uint32_t by = (w4[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+            if (by - 1u < 2u) cm2 |= 1u << i;
+        }
+        const int32_t lim2 = (int32_t)nspan - (int32_t)(SPAN - d0);
+        if (lim2 <= 0) cm2 = 0;
+        else if (lim2 < 32) cm2 &= (1u << (uint32_t)lim2) - 1u;
+    }
     for (uint64_t c = cm; c; c &= c - 1) {
         const uint32_t x = (uint32_t)(xs + (int32_t)__builtin_ctzll(c));
+        atomicOr(&cbits[x >> 5], 1u << (x & 31));
+    }
+    for (uint32_t c = cm2; c; c &= c - 1) {
+        const uint32_t x = SPAN - d0 + (uint32_t)__builtin_ctz(c);
         atomicOr(&cbits[x >> 5], 1u << (x & 31));
     }
     __syncthreads();
@@ -258,39 +278,40 @@ __global__ void __launch_bounds__(SPAN_THREADS) k_span_parse(const RunInfo* __re
     };
     const bool over = m > SPAN_CCAP;  // (uniform)
     // ---- 2c. each candidate's record: its end, and the candidate there (level-0 jump)
-    if (!over) {
-        for (uint64_t c = cm; c; c &= c - 1) {
-            const uint32_t x = (uint32_t)(xs + (int32_t)__builtin_ctzll(c));
-            const uint32_t i = rank_of(x);
-            cpos[i] = (uint16_t)x;
-            uint16_t j0 = SJ_DEAD;
-            uint32_t nx = SNX_LONG;
-            if ((uint64_t)x + 5 <= rel) {  // runs.rs:570-576: the key length is in the run
-                const uint64_t kend = (uint64_t)x + 5 + span_be32(buf, x + d0 + 1);
-                bool ok = false, known = false;
-                uint64_t e = 0;
-                if (kend <= rel) {  // :580-583 the key is in the run
-                    if (bytes[x + d0] == 2) {  // Delete: marker, key length, key
-                        ok = known = true;
-                        e = kend;
-                    } else if (kend + 4 <= rel) {  // :598-604 the value length is in the run
-                        if (kend + 4 <= avail) {
-                            e = kend + 4 + span_be32(buf, (uint32_t)kend + d0);
-                            ok = known = e <= rel;  // :608-611 the value is in the run
-                        } else {
-                            ok = true;  // ends past the staged bytes, so past the span: EXIT
-                        }
+    auto candidate = [&](uint32_t x) {
+        const uint32_t i = rank_of(x);
+        cpos[i] = (uint16_t)x;
+        uint16_t j0 = SJ_DEAD;
+        uint32_t nx = SNX_LONG;
+        if ((uint64_t)x + 5 <= rel) {  // runs.rs:570-576: the key length is in the run
+            const uint64_t kend = (uint64_t)x + 5 + span_be32(buf, x + d0 + 1);
+            bool ok = false, known = false;
+            uint64_t e = 0;
+            if (kend <= rel) {  // :580-583 the key is in the run
+                if (bytes[x + d0] == 2) {  // Delete: marker, key length, key
+                    ok = known = true;
+                    e = kend;
+                } else if (kend + 4 <= rel) {  // :598-604 the value length is in the run
+                    if (kend + 4 <= avail) {
+                        e = kend + 4 + span_be32(buf, (uint32_t)kend + d0);
+                        ok = known = e <= rel;  // :608-611 the value is in the run
+                    } else {
+                        ok = true;  // ends past the staged bytes, so past the span: EXIT
                     }
                 }
-                if (ok) {
-                    if (known && e < nspan) j0 = ((cbits[e >> 5] >> (e & 31)) & 1u) ? (uint16_t)rank_of((uint32_t)e) : SJ_DEAD;
-                    else j0 = SJ_EXIT;
-                    nx = known && e < SNX_LONG ? (uint32_t)e : SNX_LONG;
-                }
             }
-            jmp[i] = j0;
-            cnx[i] = nx;
+            if (ok) {
+                if (known && e < nspan) j0 = ((cbits[e >> 5] >> (e & 31)) & 1u) ? (uint16_t)rank_of((uint32_t)e) : SJ_DEAD;
+                else j0 = SJ_EXIT;
+                nx = known && e < SNX_LONG ? (uint32_t)e : SNX_LONG;
+            }
         }
+        jmp[i] = j0;
+        cnx[i] = nx;
+    };
+    if (!over) {
+        for (uint64_t c = cm; c; c &= c - 1) candidate((uint32_t)(xs + (int32_t)__builtin_ctzll(c)));
+        for (uint32_t c = cm2; c; c &= c - 1) candidate(SPAN - d0 + (uint32_t)__builtin_ctz(c));
     }
     __syncthreads();
     // ---- 2d. pointer jumping: level r = level r-1 twice; stops once every chain has ended
