@@ -1100,9 +1100,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                     M.m_src = dbuf<uint64_t>(ctx, "m_src", R + 1);
                     M.size = dbuf<uint64_t>(ctx, "sm_size", R + 1);
                     M.del = dbuf<uint64_t>(ctx, "sm_del", R + 1);
-                    M.mm = dbuf<uint32_t>(ctx, "tile_mm", 2);
-                    const uint32_t mm0[2] = {0xFFFFFFFFu, 0u};
-                    h2d_up(ctx, M.mm, mm0, 8);
+                    M.mm = dbuf<uint32_t>(ctx, "tile_mm", 2 * std::max<uint64_t>(1, sort_store_blocks(R)));
                 }
                 sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen, job.batch, nullptr,
                              uniform_meta, direct ? &M : nullptr, direct ? &sorted_K : nullptr);
@@ -1201,8 +1199,11 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         launch_scan_dn(st, dbuf<uint64_t>(ctx, "sm_size", R + 1), sorted_K, R, m_P, tmp);
         launch_scan_dn(st, dbuf<uint64_t>(ctx, "sm_del", R + 1), sorted_K, R, m_Dp, tmp);
         HIPCHK(hipMemcpyAsync(d_Kout, sorted_K, 8, hipMemcpyDeviceToDevice, st));
-        tile_max = dbuf<uint32_t>(ctx, "tile_mm", 2);
-        T0 = 1;
+        // one (min, max) pair per k_sort_store block, reduced to SORT_MM_OUT pairs for the split
+        tile_max = dbuf<uint32_t>(ctx, "tile_mm2", 2 * SORT_MM_OUT);
+        launch_sort_mm_reduce(st, dbuf<uint32_t>(ctx, "tile_mm", 2 * std::max<uint64_t>(1, sort_store_blocks(R))),
+                              sort_store_blocks(R), tile_max);
+        T0 = SORT_MM_OUT;
     }
     for (int li = sorted_merged ? -1 : (int)lv.size() - 1; li >= 0; --li) {
         Level& L = lv[li];

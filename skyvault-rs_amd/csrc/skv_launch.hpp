@@ -138,8 +138,11 @@ struct SortMerged {
     uint64_t* m_src = nullptr;
     uint64_t* size = nullptr;
     uint64_t* del = nullptr;
-    uint32_t* mm = nullptr;
+    uint32_t* mm = nullptr;  // (min, max) surviving record size per k_sort_store block (sort_store_blocks(R) pairs)
 };
+uint64_t sort_store_blocks(uint64_t R);
+constexpr uint32_t SORT_MM_OUT = 256;  // pairs after launch_sort_mm_reduce
+void launch_sort_mm_reduce(hipStream_t, const uint32_t* in, uint64_t n, uint32_t* out);
 void launch_sort_store(hipStream_t, uint64_t R, const SElem* E, const uint32_t* meta_in, uint32_t const_meta,
                        const uint64_t* newkey, const uint64_t* newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr,
                        uint32_t* klen, uint32_t* cmp_klen, uint32_t* meta, bool last_wins, SortMerged M = SortMerged{});

@@ -141,16 +141,27 @@ __global__ void k_sort_store(uint64_t R, const SElem* __restrict__ E, const uint
             sz = szx = m & 0x7FFFFFFFu;
         }
     }
-    if (M.m_rec) {  // (min, max) surviving record size, for the split (k_chain)
+    if (M.m_rec) {  // (min, max) surviving record size of this block's records, for the split (k_chain)
+        __shared__ uint32_t s_mm[2 * (256 / 64)];
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) {
             const uint32_t a = __shfl_xor(sz, d, 64), b = __shfl_xor(szx, d, 64);
             sz = a < sz ? a : sz;
             szx = b > szx ? b : szx;
         }
-        if ((threadIdx.x & 63) == 0 && szx) {
-            atomicMin(M.mm, sz);
-            atomicMax(M.mm + 1, szx);
+        const uint32_t w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) {
+            s_mm[2 * w] = sz;
+            s_mm[2 * w + 1] = szx;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {  // one pair per block (one address for every block's atomics was 29 ms at config 5)
+            for (uint32_t q = 1; q < (blockDim.x >> 6); ++q) {
+                sz = s_mm[2 * q] < sz ? s_mm[2 * q] : sz;
+                szx = s_mm[2 * q + 1] > szx ? s_mm[2 * q + 1] : szx;
+            }
+            M.mm[2 * blockIdx.x] = sz;
+            M.mm[2 * blockIdx.x + 1] = szx;
         }
     }
 }
@@ -574,7 +585,43 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
     }
 }
 
+// (min, max) pairs of k_sort_store's blocks reduced to SORT_MM_OUT pairs (the split's tile_max
+// table: k_chain reads it with one wave)
+__global__ void __launch_bounds__(256) k_sort_mm_reduce(const uint32_t* __restrict__ in, uint64_t n, uint32_t* out) {
+    __shared__ uint32_t s_mm[2 * (256 / 64)];
+    const uint64_t b = blockIdx.x, a0 = b * n / gridDim.x, a1 = (b + 1) * n / gridDim.x;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0;
+    for (uint64_t i = a0 + threadIdx.x; i < a1; i += 256) {
+        mn = in[2 * i] < mn ? in[2 * i] : mn;
+        mx = in[2 * i + 1] > mx ? in[2 * i + 1] : mx;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t x = __shfl_xor(mn, d, 64), y = __shfl_xor(mx, d, 64);
+        mn = x < mn ? x : mn;
+        mx = y > mx ? y : mx;
+    }
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_mm[2 * w] = mn;
+        s_mm[2 * w + 1] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t q = 1; q < 256 / 64; ++q) {
+            mn = s_mm[2 * q] < mn ? s_mm[2 * q] : mn;
+            mx = s_mm[2 * q + 1] > mx ? s_mm[2 * q + 1] : mx;
+        }
+        out[2 * b] = mn;
+        out[2 * b + 1] = mx;
+    }
+}
+void launch_sort_mm_reduce(hipStream_t s, const uint32_t* in, uint64_t n, uint32_t* out) {
+    k_sort_mm_reduce<<<SORT_MM_OUT, 256, 0, s>>>(in, n, out);
+}
+
 static inline unsigned sk_blocks(uint64_t n) { return (unsigned)((n + 255) / 256); }
+uint64_t sort_store_blocks(uint64_t R) { return sk_blocks(R); }
 
 void launch_sort_load(hipStream_t s, uint64_t R, const uint64_t* hi, const uint64_t* lo, const uint64_t* addr,
                       const uint32_t* klen, SElem* E, bool last_wins) {
