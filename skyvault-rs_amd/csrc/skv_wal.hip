@@ -12,6 +12,9 @@
 // keep/drop; kept tables become one output run each (version byte + rewritten records).
 #include "skv_launch.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace skv {
 
 static inline unsigned wal_blocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
@@ -604,9 +607,14 @@ __global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict_
 void launch_wal_fused(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,
                       const uint64_t* Dp, uint8_t* out, uint64_t* tstate, uint32_t* ticket, uint32_t* fail,
                       WalTStart* tlist, uint32_t* tcount, uint32_t tcap, uint64_t* tail, uint32_t diag) {
+    // SKV_WAL_LDS=<bytes>: pad the workgroup's LDS request (caps workgroups per CU: a smaller set of
+    // record lines in flight per XCD, so the composition's re-read can hit L2; occupancy studies)
+    static const size_t pad = getenv("SKV_WAL_LDS") ? (size_t)atol(getenv("SKV_WAL_LDS")) : 0;
+    const size_t lds = std::min<size_t>(pad, 96 * 1024);
+    if (lds) (void)hipFuncSetAttribute((const void*)k_wal_fused, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (max_K)
-        k_wal_fused<<<wal_blocks(max_K, WAL_G), WAL_G, 0, s>>>(Kp, m_src, P, Dp, out, tstate, ticket, fail, tlist,
-                                                                tcount, tcap, tail, diag);
+        k_wal_fused<<<wal_blocks(max_K, WAL_G), WAL_G, lds, s>>>(Kp, m_src, P, Dp, out, tstate, ticket, fail, tlist,
+                                                                  tcount, tcap, tail, diag);
 }
 
 void launch_wal_keys(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,
