@@ -540,10 +540,13 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     };
     uint32_t utf8_flag = 0;
     // order check + readback of its result, the record flags and (fast path) the broken-run flags
-    // span_order: the span parse did the order check, its first decreases as global record indices
-    auto check_and_read = [&](bool read_broken, bool span_order = false) -> bool {
+    // order: ORDER_LAUNCH runs k_order_check here; ORDER_DONE the parse did it (first decreases as
+    // stream-local indices); ORDER_SPAN the span parse did it (global record indices)
+    enum { ORDER_LAUNCH = 0, ORDER_DONE = 1, ORDER_SPAN = 2 };
+    auto check_and_read = [&](bool read_broken, int order = ORDER_LAUNCH) -> bool {
+        const bool span_order = order == ORDER_SPAN;
         // the fast path's parse kernel already did the order check
-        if (!read_broken && !job.batch && !span_order)  // a writer batch is unsorted by definition
+        if (!read_broken && !job.batch && order == ORDER_LAUNCH)  // a writer batch is unsorted by definition
             launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
         HIPCHK(hipGetLastError());
         // the verdict words first; the 10^6-entry tables only when a word says they hold something:
@@ -805,7 +808,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             alloc_records(false);
             rec_addr = so.rec_addr;
             mark(ctx, PH_PARSE);
-            check_and_read(false, true);
+            check_and_read(false, ORDER_SPAN);
             parsed = true;
         }
     }
@@ -838,11 +841,16 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         }
         stream_tables();
         alloc_records();
+        // the order check fused into k_emit (+ k_chunk_order at chunk edges) when every record comes from
+        // it (fixed-stride runs' records, from k_emit_fixed<false>, are not checked there; a writer batch is
+        // unsorted by definition; SKV_EMIT_ORDER=0: k_order_check)
+        const char* eo = getenv("SKV_EMIT_ORDER");
+        const bool emit_order = !any_fixed && !job.batch && !(eo && eo[0] == '0');
         launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, any_fixed ? R : 0,
                     rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad, ch_slots, slot_cap, chunk,
-                    ch_end);
+                    ch_end, emit_order ? d_stream_base : nullptr, emit_order ? d_first_dec : nullptr);
         mark(ctx, PH_PARSE);
-        check_and_read(false);
+        check_and_read(false, emit_order ? ORDER_DONE : ORDER_LAUNCH);
         if (utf8_flag && !ctx->exact_utf8) {  // a key the chunk walks did not check: exact walks
             ctx->exact_utf8 = true;
             int rc;

@@ -371,7 +371,8 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
                        uint64_t* __restrict__ rec_addr, uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
                        uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags,
                        uint64_t* __restrict__ rec_fp, uint32_t* utf8_bad, const uint16_t* __restrict__ slots,
-                       uint32_t cap, uint64_t chunk, const uint64_t* __restrict__ ch_end) {
+                       uint32_t cap, uint64_t chunk, const uint64_t* __restrict__ ch_end,
+                       const uint64_t* __restrict__ stream_base, unsigned long long* first_dec) {
     const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t c = gi / EM_G;
     const uint32_t j0 = (uint32_t)(gi % EM_G);
@@ -391,12 +392,28 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
             atomicOr(utf8_bad, 1u);
         put_rec(b0 + i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp, fpv);
     };
+    // the in-stream order check (runs.rs:190-198, k_order_check's comparison) fused in: each record
+    // against the one before it in the chunk (the neighbouring lane's, through shuffles); a chunk's
+    // first record against the record before it is k_chunk_order's
+    const uint32_t sidx = runs[r].stream;
+    const uint64_t sbase = first_dec ? stream_base[sidx] : 0;
+    auto decrease = [&](uint64_t i) {  // record i - 1 of the chunk sorts after record i
+        atomicMin(&first_dec[sidx], (unsigned long long)(b0 + i - 1 - sbase));
+        atomicOr(flags + 1, 1u);
+    };
     if (cnt > cap) {
         if (j0) return;
         uint64_t p = ch_start[c];
+        RecHdr hp{};
+        uint64_t pp = 0;
         for (uint64_t i = 0; i < cnt; ++i) {
             const RecHdr h = parse_rec<true, false>(run, len, p);
             emit(i, p, h);
+            if (first_dec && i > 0 &&
+                key_cmp(hp.hi, hp.lo, (uint32_t)hp.klen, run + pp + 5, h.hi, h.lo, (uint32_t)h.klen, run + p + 5) > 0)
+                decrease(i);
+            hp = h;
+            pp = p;
             p += h.size;
         }
         return;
@@ -421,17 +438,68 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         h.size = pn - p;
         return h;
     };
-    for (uint64_t i = j0; i < cnt; i += 2 * EM_G) {
-        const uint64_t i2 = i + EM_G;
-        const bool two = i2 < cnt;
-        const uint64_t p = cs + sl[i];
-        const uint64_t pn = i + 1 < cnt ? cs + sl[i + 1] : cend;
+    // steps are uniform over the chunk's EM_G lanes (the order check shuffles inside the group)
+    const uint64_t nit = (cnt + 2 * EM_G - 1) / (2 * EM_G);
+    uint64_t c_hi = 0, c_lo = 0, c_ad = 0;  // lane EM_G - 1's second record of the previous step
+    uint32_t c_kl = 0;
+    for (uint64_t t = 0; t < nit; ++t) {
+        const uint64_t i = j0 + t * 2 * EM_G, i2 = i + EM_G;
+        const bool one = i < cnt, two = i2 < cnt;
+        const uint64_t ia = one ? i : 0;
+        const uint64_t p = cs + sl[ia];
+        const uint64_t pn = ia + 1 < cnt ? cs + sl[ia + 1] : cend;
         const uint64_t q = two ? cs + sl[i2] : p;
         const uint64_t qn = two ? (i2 + 1 < cnt ? cs + sl[i2 + 1] : cend) : pn;
         const RecHdr ha = hdr(p, pn);
         const RecHdr hb = hdr(q, qn);
-        emit(i, p, ha);
+        if (one) emit(i, p, ha);
         if (two) emit(i2, q, hb);
+        if (first_dec) {
+            const uint64_t pa = (uint64_t)(uintptr_t)(run + p), pb = (uint64_t)(uintptr_t)(run + q);
+            const uint32_t ka = (uint32_t)ha.klen, kb = (uint32_t)hb.klen;
+            // before record i: lane j0 - 1's first record (lane 0: the carried one)
+            uint64_t x_hi = __shfl_up(ha.hi, 1, EM_G), x_lo = __shfl_up(ha.lo, 1, EM_G), x_ad = __shfl_up(pa, 1, EM_G);
+            uint32_t x_kl = __shfl_up(ka, 1, EM_G);
+            // before record i2: lane j0 - 1's second record (lane 0: lane EM_G - 1's first record)
+            uint64_t y_hi = __shfl_up(hb.hi, 1, EM_G), y_lo = __shfl_up(hb.lo, 1, EM_G), y_ad = __shfl_up(pb, 1, EM_G);
+            uint32_t y_kl = __shfl_up(kb, 1, EM_G);
+            const uint64_t l_hi = __shfl(ha.hi, EM_G - 1, EM_G), l_lo = __shfl(ha.lo, EM_G - 1, EM_G);
+            const uint64_t l_ad = __shfl(pa, EM_G - 1, EM_G);
+            const uint32_t l_kl = __shfl(ka, EM_G - 1, EM_G);
+            if (j0 == 0) {
+                x_hi = c_hi; x_lo = c_lo; x_ad = c_ad; x_kl = c_kl;
+                y_hi = l_hi; y_lo = l_lo; y_ad = l_ad; y_kl = l_kl;
+            }
+            c_hi = __shfl(hb.hi, EM_G - 1, EM_G);
+            c_lo = __shfl(hb.lo, EM_G - 1, EM_G);
+            c_ad = __shfl(pb, EM_G - 1, EM_G);
+            c_kl = __shfl(kb, EM_G - 1, EM_G);
+            if (one && i > 0 &&
+                key_cmp(x_hi, x_lo, x_kl, (const uint8_t*)x_ad + 5, ha.hi, ha.lo, ka, run + p + 5) > 0)
+                decrease(i);
+            if (two && key_cmp(y_hi, y_lo, y_kl, (const uint8_t*)y_ad + 5, hb.hi, hb.lo, kb, run + q + 5) > 0)
+                decrease(i2);
+        }
+    }
+}
+
+// The order check across chunk edges (k_emit's fused check): a chunk's first record against the
+// record before it in its stream (records are numbered stream by stream, chunk by chunk)
+__global__ void k_chunk_order(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
+                              const uint64_t* __restrict__ ch_rec_base, const uint64_t* __restrict__ stream_base,
+                              const uint64_t* __restrict__ rec_addr, const uint64_t* __restrict__ rec_hi,
+                              const uint64_t* __restrict__ rec_lo, const uint32_t* __restrict__ rec_klen,
+                              unsigned long long* first_dec, uint32_t* any_dec) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_chunks) return;
+    const uint64_t g = ch_rec_base[c];
+    if (ch_rec_base[c + 1] == g) return;
+    const uint32_t sidx = runs[find_run(runs, n_runs, c)].stream;
+    if (g == stream_base[sidx]) return;  // the stream's first record
+    if (key_cmp(rec_hi[g - 1], rec_lo[g - 1], rec_klen[g - 1], (const uint8_t*)rec_addr[g - 1] + 5, rec_hi[g],
+                rec_lo[g], rec_klen[g], (const uint8_t*)rec_addr[g] + 5) > 0) {
+        atomicMin(&first_dec[sidx], (unsigned long long)(g - 1 - stream_base[sidx]));
+        atomicOr(any_dec, 1u);
     }
 }
 
@@ -2654,15 +2722,20 @@ void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n
                  const uint32_t* run_broken, const uint64_t* ch_start, const uint64_t* ch_rec_base,
                  const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                  uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, uint64_t* rec_fp, uint32_t* utf8_bad,
-                 const uint16_t* slots, uint32_t cap, uint64_t chunk, const uint64_t* ch_end) {
+                 const uint16_t* slots, uint32_t cap, uint64_t chunk, const uint64_t* ch_end,
+                 const uint64_t* stream_base, unsigned long long* first_dec) {
     if (n_chunks)
         k_emit<<<blocks_for(n_chunks * EM_G, 256), 256, 0, s>>>(runs, n_runs, n_chunks, fmt, run_broken, ch_start,
                                                                 ch_rec_base, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
-                                                                flags, rec_fp, utf8_bad, slots, cap, chunk, ch_end);
+                                                                flags, rec_fp, utf8_bad, slots, cap, chunk, ch_end,
+                                                                stream_base, first_dec);
     if (R)
         k_emit_fixed<false><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, nullptr, R, fmt, (uint32_t*)run_broken, run_recb,
                                                                rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags,
                                                                nullptr, nullptr, rec_fp);
+    if (n_chunks && first_dec)
+        k_chunk_order<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, ch_rec_base, stream_base,
+                                                                rec_addr, rec_hi, rec_lo, rec_klen, first_dec, flags + 1);
 }
 void launch_parse_fixed(hipStream_t s, const RunInfo* runs, uint32_t n_runs, const RunFmt* fmt, uint32_t* run_broken,
                         const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,

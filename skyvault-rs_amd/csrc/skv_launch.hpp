@@ -26,7 +26,8 @@ void launch_emit(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_c
                  const uint32_t* run_broken, const uint64_t* ch_start, const uint64_t* ch_rec_base,
                  const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                  uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, uint64_t* rec_fp, uint32_t* utf8_bad,
-                 const uint16_t* slots, uint32_t cap, uint64_t chunk, const uint64_t* ch_end);
+                 const uint16_t* slots, uint32_t cap, uint64_t chunk, const uint64_t* ch_end,
+                 const uint64_t* stream_base = nullptr, unsigned long long* first_dec = nullptr);
 void launch_parse_fixed(hipStream_t, const RunInfo* runs, uint32_t n_runs, const RunFmt* fmt, uint32_t* run_broken,
                         const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                         uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, const uint64_t* stream_base,
