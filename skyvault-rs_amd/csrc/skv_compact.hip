@@ -231,7 +231,7 @@ int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, con
     };
     if (h[0] != ~0ull)
         ev.push_back({pos_of_survivor(h[0]), 0, SKV_E_INVALID_INPUT,
-                      wal_key_error(fetch_key(ctx, rec_addr, rec_klen, read_dev(m_rec + h[0])))});
+                      wal_key_error(fetch_key_at(ctx, read_dev(m_src + h[0])))});
     if (h[4] != ~0ull)
         ev.push_back({pos_of_survivor(h[4]), 1, SKV_E_INTERNAL, "Internal error: Failed to send operation to table channel"});
     if (heap)
@@ -307,14 +307,14 @@ SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth, uint6
 // key length (descriptors, WAL split).
 void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo, uint64_t*& addr, uint32_t*& klen,
                          uint32_t*& meta, const uint32_t*& cmp_klen, bool last_wins, const SElem** sorted,
-                         uint32_t const_meta, const SortMerged* merged, uint64_t** d_K) {
+                         uint32_t const_meta, const SortMerged* merged, uint64_t** d_K, bool e_ready) {
     hipStream_t st = ctx->stream;
-    SElem* E = dbuf<SElem>(ctx, "sort_e", R);
+    SElem* E = dbuf<SElem>(ctx, "sort_e", R);  // e_ready: the fixed-stride parse wrote it
     SElem* T = dbuf<SElem>(ctx, "sort_t", R);
     uint64_t* newkey = dbuf<uint64_t>(ctx, "sort_newkey", R + 1);
     uint64_t* newkey_ex = dbuf<uint64_t>(ctx, "sort_newkey_ex", R + 1);
     uint64_t* scan_tmp = dbuf<uint64_t>(ctx, "sort_rank_scan", scan_tmp_words(R) + 64);
-    launch_sort_load(st, R, hi, lo, addr, klen, E, last_wins);
+    if (!e_ready) launch_sort_load(st, R, hi, lo, addr, klen, E, last_wins);
     const SElem* S = sort_elems(ctx, E, T, R, 0, newkey);
     launch_scan(st, newkey, R, newkey_ex, scan_tmp);
     uint64_t* nhi = dbuf<uint64_t>(ctx, "srt_hi", R);
@@ -588,6 +588,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                job.batch;
     };
     bool fp_skipped = false;
+    bool e_direct = false;  // the fixed-stride parse wrote the record sort's elements (sort_e)
     bool any_fixed = false;  // some run is fixed-stride: the general parse also runs k_emit_fixed
     uint32_t uniform_meta = 0;  // every record a Put of one size (the fixed path's runs, one format): its meta
     uint64_t first_sum = 0, first_n = 0;  // the runs' first-record sizes (record capacity of the span parse)
@@ -622,9 +623,14 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             alloc_records();
             const bool will_sort = sort_by_fan_in(R);
             fp_skipped = will_sort;
+            // the record sort follows: the parse writes the sort's elements itself (no k_sort_load
+            // pass; the record arrays are filled from them only if a key decrease needs them)
+            const char* sde = getenv("SKV_SORT_DIRECT");
+            e_direct = will_sort && !job.batch && !job.scan && !job.search && !(sde && sde[0] == '0');
             launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
                                rec_meta, d_flags, d_stream_base, d_first_dec, will_sort ? nullptr : rec_fp,
-                               dbuf<uint32_t>(ctx, "wave_run", (R + 63) / 64 + 1));
+                               dbuf<uint32_t>(ctx, "wave_run", (R + 63) / 64 + 1),
+                               e_direct ? dbuf<SElem>(ctx, "sort_e", R) : nullptr);
             mark(ctx, PH_PARSE);
             if (allow_deferred && !(job.flags & SKV_SPLIT_BY_TABLE)) {
                 deferred = true;  // verdict read with the result
@@ -636,9 +642,14 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                 htrace("parse verdict read");
             }
             if (parsed && !deferred && !fl[RT_NOT_UNIFORM] && !(hflags[3] & 1u)) uniform_meta = (uint32_t)f0.S;
+            if (parsed && e_direct && !deferred && hflags[1]) {  // a decrease: its paths read the record arrays
+                launch_sort_unload(st, R, dbuf<SElem>(ctx, "sort_e", R), rec_hi, rec_lo, rec_addr, rec_klen);
+                e_direct = false;
+            }
             if (!parsed) {  // a run is not what its first record promised: general parse, host tables
                 dev_tables = false;
                 fp_skipped = false;
+                e_direct = false;
                 R = 0;
                 any_err = false;
                 std::fill(stream_err.begin(), stream_err.end(), 0u);
@@ -1109,9 +1120,12 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                     M.size = dbuf<uint64_t>(ctx, "sm_size", R + 1);
                     M.del = dbuf<uint64_t>(ctx, "sm_del", R + 1);
                     M.mm = dbuf<uint32_t>(ctx, "tile_mm", 2 * std::max<uint64_t>(1, sort_store_blocks(R)));
+                    // the WAL stage reads the merged arrays only (its error text fetches keys through
+                    // m_src): no sorted record arrays
+                    M.arrays = !(job.flags & SKV_SPLIT_BY_TABLE);
                 }
                 sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen, job.batch, nullptr,
-                             uniform_meta, direct ? &M : nullptr, direct ? &sorted_K : nullptr);
+                             uniform_meta, direct ? &M : nullptr, direct ? &sorted_K : nullptr, e_direct);
                 sorted_merged = direct;
                 cmp_hi = rec_hi;
                 cmp_lo = rec_lo;

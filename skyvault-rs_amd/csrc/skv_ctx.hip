@@ -344,6 +344,15 @@ std::string fetch_key(skv_ctx* ctx, const uint64_t* d_rec_addr, const uint32_t* 
     return k;
 }
 
+std::string fetch_key_at(skv_ctx* ctx, uint64_t addr) {
+    uint8_t h[5] = {};
+    HIPCHK(hipMemcpy(h, (const void*)addr, 5, hipMemcpyDeviceToHost));
+    const uint32_t klen = ((uint32_t)h[1] << 24) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 8) | h[4];
+    std::string k(klen, '\0');
+    if (klen) HIPCHK(hipMemcpy(&k[0], (const void*)(addr + 5), klen, hipMemcpyDeviceToHost));
+    return k;
+}
+
 // JobError::InvalidInput text of a bad WAL key (wal_compaction.rs:71-79; Rust ParseIntError Display)
 std::string wal_key_error(const std::string& key) {
     size_t dot = key.find('.');

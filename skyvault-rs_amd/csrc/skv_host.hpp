@@ -276,6 +276,8 @@ struct Job {
 };
 
 std::string fetch_key(skv_ctx* ctx, const uint64_t* d_rec_addr, const uint32_t* d_rec_klen, uint64_t rec);
+// the key of the record at device address addr (its header read first)
+std::string fetch_key_at(skv_ctx* ctx, uint64_t addr);
 std::string wal_key_error(const std::string& key);
 
 constexpr int RC_RETRY_EXACT = -100;  // internal: the merge's fingerprint shortcut misordered a tile
@@ -336,7 +338,8 @@ bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInfo>& run
 SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth, uint64_t* newkey = nullptr);
 void sort_records(skv_ctx* ctx, uint64_t R, uint64_t*& hi, uint64_t*& lo, uint64_t*& addr, uint32_t*& klen,
                          uint32_t*& meta, const uint32_t*& cmp_klen, bool last_wins, const SElem** sorted = nullptr,
-                         uint32_t const_meta = 0, const SortMerged* merged = nullptr, uint64_t** d_K = nullptr);
+                         uint32_t const_meta = 0, const SortMerged* merged = nullptr, uint64_t** d_K = nullptr,
+                         bool e_ready = false);
 
 // A run parsed once for many lookup batches (skv_run_index_create): the run bytes and its record
 // arrays stay in HBM, owned by the index (the cache service keeps one per cached run,

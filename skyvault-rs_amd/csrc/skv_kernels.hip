@@ -532,9 +532,26 @@ __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, 
                              uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
                              uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags,
                              const uint64_t* __restrict__ stream_base, unsigned long long* first_dec,
-                             uint64_t* __restrict__ rec_fp) {
+                             uint64_t* __restrict__ rec_fp, SElem* __restrict__ E = nullptr) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool act = i < R_total;
+    // E (the record sort follows): the sort's element {prefix, address, index, key length} in place of
+    // rec_hi / rec_lo / rec_addr / rec_klen -- k_sort_load's pass over them is skipped
+    auto put = [&](uint64_t o, const uint8_t* rp, const RecHdr& h, uint64_t fpv) {
+        if (E) {
+            SElem e;
+            e.hi = h.hi;
+            e.lo = h.lo;
+            e.addr = (uint64_t)(uintptr_t)rp;
+            e.pos = (uint32_t)o;
+            e.klen = (uint32_t)h.klen;
+            E[o] = e;
+            if (h.size >= (1ull << 31)) atomicOr(flags, 1u);
+            rec_meta[o] = (uint32_t)h.size | (h.marker == 2 ? 0x80000000u : 0u);
+        } else {
+            put_rec(o, rp, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp, fpv);
+        }
+    };
     uint32_t lo = 0;
     RunFmt f{0, 0, 0};
     const uint8_t* run = nullptr;
@@ -568,12 +585,11 @@ __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, 
             // never follows a garbage address; the host reruns the general parse
             RecHdr z{};
             z.marker = 1;
-            put_rec(i, run, z, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp, 0);
+            put(i, run, z, 0);
         }
         if (act) {
             bool ascii;
-            put_rec(i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp,
-                    rec_fp ? key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii) : 0);
+            put(i, run + p, h, rec_fp ? key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii) : 0);
         }
     }
     // a Delete of the run's record size (k_run_header's hypothesis is a Put): flags[3] bit 0, so
@@ -2740,13 +2756,13 @@ void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n
 void launch_parse_fixed(hipStream_t s, const RunInfo* runs, uint32_t n_runs, const RunFmt* fmt, uint32_t* run_broken,
                         const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                         uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, const uint64_t* stream_base,
-                        unsigned long long* first_dec, uint64_t* rec_fp, uint32_t* wave_run) {
+                        unsigned long long* first_dec, uint64_t* rec_fp, uint32_t* wave_run, SElem* E) {
     if (!R) return;
     const uint64_t nw = (R + 63) >> 6;
     k_wave_run<<<blocks_for(nw, 256), 256, 0, s>>>(run_recb, n_runs, nw, wave_run);
     k_emit_fixed<true><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, wave_run, R, fmt, run_broken, run_recb, rec_addr,
                                                               rec_hi, rec_lo, rec_klen, rec_meta, flags, stream_base,
-                                                              first_dec, rec_fp);
+                                                              first_dec, rec_fp, E);
 }
 void launch_order_check(hipStream_t s, uint64_t R, const uint64_t* stream_base, uint32_t k, const uint64_t* rec_addr,
                         const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,

@@ -31,7 +31,8 @@ void launch_emit(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_c
 void launch_parse_fixed(hipStream_t, const RunInfo* runs, uint32_t n_runs, const RunFmt* fmt, uint32_t* run_broken,
                         const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                         uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, const uint64_t* stream_base,
-                        unsigned long long* first_dec, uint64_t* rec_fp, uint32_t* wave_run);
+                        unsigned long long* first_dec, uint64_t* rec_fp, uint32_t* wave_run,
+                        SElem* E = nullptr);
 void launch_order_check(hipStream_t, uint64_t R, const uint64_t* stream_base, uint32_t k, const uint64_t* rec_addr,
                         const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,
                         unsigned long long* first_dec, uint32_t* any_dec);
@@ -140,7 +141,11 @@ struct SortMerged {
     uint64_t* size = nullptr;
     uint64_t* del = nullptr;
     uint32_t* mm = nullptr;  // (min, max) surviving record size per k_sort_store block (sort_store_blocks(R) pairs)
+    bool arrays = true;      // also the sorted record arrays (hi / lo / addr / klen / cmp_klen / meta)
 };
+// the record arrays from the sort's elements in record order (the fixed-stride parse wrote the elements)
+void launch_sort_unload(hipStream_t, uint64_t R, const SElem* E, uint64_t* hi, uint64_t* lo, uint64_t* addr,
+                        uint32_t* klen);
 uint64_t sort_store_blocks(uint64_t R);
 constexpr uint32_t SORT_MM_OUT = 256;  // pairs after launch_sort_mm_reduce
 void launch_sort_mm_reduce(hipStream_t, const uint32_t* in, uint64_t n, uint32_t* out);

@@ -123,13 +123,15 @@ __global__ void k_sort_store(uint64_t R, const SElem* __restrict__ E, const uint
         const SElem e = E[i];
         const uint64_t src = last_wins ? R - 1 - e.pos : e.pos;
         const uint64_t nk = newkey[i];
-        hi[i] = newkey_ex[i] + nk - 1;
-        lo[i] = 0;
-        addr[i] = e.addr;
-        klen[i] = e.klen;
-        cmp_klen[i] = 0;
         const uint32_t m = const_meta ? const_meta : meta_in[src];
-        meta[i] = m;
+        if (!M.m_rec || M.arrays) {
+            hi[i] = newkey_ex[i] + nk - 1;
+            lo[i] = 0;
+            addr[i] = e.addr;
+            klen[i] = e.klen;
+            cmp_klen[i] = 0;
+            meta[i] = m;
+        }
         // the merged arrays of the one sorted list, straight from the sort: the first record of each
         // key is its survivor (k_way.rs:146-151), and its index among the survivors is its key's rank
         if (M.m_rec && nk) {
@@ -583,6 +585,21 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
             newkey[s0 + i] = nk ? 1 : 0;
         }
     }
+}
+
+__global__ void k_sort_unload(uint64_t R, const SElem* __restrict__ E, uint64_t* hi, uint64_t* lo, uint64_t* addr,
+                              uint32_t* klen) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R) return;
+    const SElem e = E[i];
+    hi[i] = e.hi;
+    lo[i] = e.lo;
+    addr[i] = e.addr;
+    klen[i] = e.klen;
+}
+void launch_sort_unload(hipStream_t s, uint64_t R, const SElem* E, uint64_t* hi, uint64_t* lo, uint64_t* addr,
+                        uint32_t* klen) {
+    if (R) k_sort_unload<<<(unsigned)((R + 255) / 256), 256, 0, s>>>(R, E, hi, lo, addr, klen);
 }
 
 // (min, max) pairs of k_sort_store's blocks reduced to SORT_MM_OUT pairs (the split's tile_max
