@@ -8,6 +8,7 @@
 #   tile2k   general merge tiles of 2048 elements, 512 threads (2 workgroups per CU)
 #   seg512, seg1024  k_gather segments of 512 / 1024 records
 #   span8k, span32k  span parse spans of 8 / 32 KiB (128 / 512 threads)
+#   sbtop256, sbtop2048, sbper8, sbper32  record-sort bucket search: LDS top-level entries, elements per thread
 set -eu
 cd "$(dirname "$0")/../skyvault-rs_amd"
 J=${J:-8}
@@ -22,6 +23,10 @@ declare -A F=(
   [seg1024]="-DSKV_GATHER_SEG=1024"
   [span8k]="-DSKV_SPAN_BYTES=8192"
   [span32k]="-DSKV_SPAN_BYTES=32768"
+  [sbtop256]="-DSKV_SB_TOP=256"
+  [sbtop2048]="-DSKV_SB_TOP=2048"
+  [sbper8]="-DSKV_SB_PER=8"
+  [sbper32]="-DSKV_SB_PER=32"
 )
 for tag in ${TAGS:-${!F[@]}}; do
   make -s -j"$J" variant TAG="$tag" VFLAGS="${F[$tag]}"
