@@ -1132,6 +1132,13 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                 cmp_addr = rec_addr;
             }
             htrace("sort launched");
+            if (getenv("SKV_SORT_PROF_PRINT")) {  // (SKV_SORT_PROF=1 builds; zeros otherwise)
+                unsigned long long pr[16];
+                sort_prof_read(pr);
+                fprintf(stderr, "[sort prof] bucket: load %llu top %llu group %llu slot+store %llu | tile: load %llu "
+                                "bitonic %llu ties %llu out %llu | tiles %llu (100 MHz ticks, cumulative)\n",
+                        pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], pr[15]);
+            }
             km = 1;
             list_off = {0, R};
             d_list_off = dbuf<uint64_t>(ctx, "sorted_off", 2);

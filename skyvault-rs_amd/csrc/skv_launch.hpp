@@ -147,7 +147,8 @@ struct SortMerged {
 void launch_sort_unload(hipStream_t, uint64_t R, const SElem* E, uint64_t* hi, uint64_t* lo, uint64_t* addr,
                         uint32_t* klen);
 uint64_t sort_store_blocks(uint64_t R);
-constexpr uint32_t SORT_MM_OUT = 256;  // pairs after launch_sort_mm_reduce
+constexpr uint32_t SORT_MM_OUT = 256;
+void sort_prof_read(unsigned long long* out16);  // SKV_SORT_PROF builds: the record sort's phase ticks  // pairs after launch_sort_mm_reduce
 void launch_sort_mm_reduce(hipStream_t, const uint32_t* in, uint64_t n, uint32_t* out);
 void launch_sort_store(hipStream_t, uint64_t R, const SElem* E, const uint32_t* meta_in, uint32_t const_meta,
                        const uint64_t* newkey, const uint64_t* newkey_ex, uint64_t* hi, uint64_t* lo, uint64_t* addr,

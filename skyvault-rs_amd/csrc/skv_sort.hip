@@ -89,6 +89,28 @@ __device__ inline void sk_window(const SElem& e, uint32_t L, uint64_t& wh, uint6
 }
 
 // ---------------------------------------------------------------------------------------------
+// SKV_SORT_PROF=1 (diagnostic builds): per-phase wall ticks of k_sort_bucket / k_sort_tile summed by
+// each workgroup's thread 0 into g_sort_prof (read with sort_prof_read)
+#ifndef SKV_SORT_PROF
+#define SKV_SORT_PROF 0
+#endif
+#if SKV_SORT_PROF
+__device__ unsigned long long g_sort_prof[16];
+#define SPROF_T(v) const uint64_t v = threadIdx.x == 0 ? wall_clock64() : 0
+#define SPROF_ADD(i, a, b) \
+    do { if (threadIdx.x == 0) atomicAdd(&g_sort_prof[i], (unsigned long long)((b) - (a))); } while (0)
+#else
+#define SPROF_T(v) do {} while (0)
+#define SPROF_ADD(i, a, b) do {} while (0)
+#endif
+void sort_prof_read(unsigned long long* out16) {
+#if SKV_SORT_PROF
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_sort_prof), 16 * 8);
+#else
+    for (int i = 0; i < 16; ++i) out16[i] = 0;
+#endif
+}
 
 // pos is the tie-break: the record index (newer stream first), or for a writer batch the index
 // from the end (the last op of a key wins, BTreeMap insertion in writer_service.rs:153-157)
@@ -318,6 +340,7 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
     }
     const uint64_t base = (uint64_t)blockIdx.x * SB_THREADS * SB_PER;
     for (int u0 = 0; u0 < SB_PER; u0 += SB_ILP) {
+        SPROF_T(pa);
         SElem x[SB_ILP];
         uint64_t x0[SB_ILP], x1[SB_ILP], g[SB_ILP], len[SB_ILP], c[SB_ILP], dx[SB_ILP];
         uint32_t a[SB_ILP];
@@ -333,6 +356,8 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
             sk_ext(sk_key(x[u]), x[u].klen, x0[u], x1[u]);
             a[u] = 0;
         }
+        SPROF_T(pb);
+        SPROF_ADD(0, pa, pb);
         for (uint32_t st = s1; st; st >>= 1) {
 #pragma unroll
             for (int u = 0; u < SB_ILP; ++u) {
@@ -343,6 +368,8 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
                 }
             }
         }
+        SPROF_T(pc);
+        SPROF_ADD(1, pb, pc);
 #pragma unroll
         for (int u = 0; u < SB_ILP; ++u) {
             g[u] = (uint64_t)a[u] * top;
@@ -362,6 +389,8 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
                 }
             }
         }
+        SPROF_T(pd);
+        SPROF_ADD(2, pc, pd);
 #pragma unroll
         for (int u = 0; u < SB_ILP; ++u) {
             if (!live[u]) continue;
@@ -378,6 +407,11 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
                 }
             }
         }
+#if SKV_SORT_PROF
+        __builtin_amdgcn_s_waitcnt(0);
+#endif
+        SPROF_T(pe);
+        SPROF_ADD(3, pd, pe);
     }
 }
 
@@ -505,12 +539,15 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
         return;
     }
     const uint32_t n32 = (uint32_t)n;
+    SPROF_T(q0);
     if (threadIdx.x == 0) s_long = 0;
     for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
         kw[i] = sk_skey(bk[i], L, pre).wh;
         id[i] = (uint16_t)i;
     }
     __syncthreads();
+    SPROF_T(q1);
+    SPROF_ADD(4, q0, q1);
     uint32_t P = 1, lp = 0;
     while (P < n32) {
         P <<= 1;
@@ -547,6 +584,8 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
         }
     }
     if (local_last) __syncthreads();
+    SPROF_T(q2);
+    SPROF_ADD(5, q1, q2);
     // runs of equal kw into the full order
     for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
         const uint64_t w = kw[i];
@@ -569,6 +608,8 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
         }
     }
     __syncthreads();
+    SPROF_T(q3);
+    SPROF_ADD(6, q2, q3);
     if (s_long) {  // uniform: every thread read it after the barrier
         sk_sort_global(bk, n, L, pre, out, s0, newkey);
         return;
@@ -585,6 +626,12 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
             newkey[s0 + i] = nk ? 1 : 0;
         }
     }
+#if SKV_SORT_PROF
+    __syncthreads();
+    SPROF_T(q4);
+    SPROF_ADD(7, q3, q4);
+    if (threadIdx.x == 0) atomicAdd(&g_sort_prof[15], 1ull);
+#endif
 }
 
 __global__ void k_sort_unload(uint64_t R, const SElem* __restrict__ E, uint64_t* hi, uint64_t* lo, uint64_t* addr,

@@ -9,6 +9,7 @@
 #   seg512, seg1024  k_gather segments of 512 / 1024 records
 #   span8k, span32k  span parse spans of 8 / 32 KiB (128 / 512 threads)
 #   sbtop256, sbtop2048, sbper8, sbper32  record-sort bucket search: LDS top-level entries, elements per thread
+#   sortprof  the record sort's phase ticks (SKV_SORT_PROF_PRINT=1 prints them; diagnostic)
 set -eu
 cd "$(dirname "$0")/../skyvault-rs_amd"
 J=${J:-8}
@@ -27,6 +28,7 @@ declare -A F=(
   [sbtop2048]="-DSKV_SB_TOP=2048"
   [sbper8]="-DSKV_SB_PER=8"
   [sbper32]="-DSKV_SB_PER=32"
+  [sortprof]="-DSKV_SORT_PROF=1"
 )
 for tag in ${TAGS:-${!F[@]}}; do
   make -s -j"$J" variant TAG="$tag" VFLAGS="${F[$tag]}"

@@ -11,3 +11,6 @@ for v in ${VARIANTS:-base sbtop256 sbtop2048 sbper8 sbper32}; do
     > "$O/sortvar_$v.log" 2>&1 || { echo "variant $v failed"; tail -5 "$O/sortvar_$v.log"; exit 1; }
   echo "$v $(grep -o '"ms_per_step": [0-9.]*' $O/sortvar_$v.log) $(grep -o '"phases_ms": {[^}]*' $O/sortvar_$v.log)"
 done
+SKV_LIB=skyvault-rs_amd/skv/variants/libskv_sortprof.so SKV_SORT_PROF_PRINT=1 timeout -k 10 300 python bench.py --config 5 \
+  --steps 2 --warmup 1 --no-cpu-baseline --no-host-path > "$O/sortprof.log" 2>&1 || { tail -5 "$O/sortprof.log"; exit 1; }
+grep "sort prof" "$O/sortprof.log" | tail -4
