@@ -10,6 +10,7 @@
 #   span8k, span32k  span parse spans of 8 / 32 KiB (128 / 512 threads)
 #   sbtop256, sbtop2048, sbper8, sbper32  record-sort bucket search: LDS top-level entries, elements per thread
 #   sortprof  the record sort's phase ticks (SKV_SORT_PROF_PRINT=1 prints them; diagnostic)
+#   t512     general merge tiles of 4096 elements on 512 threads (8 per thread)
 set -eu
 cd "$(dirname "$0")/../skyvault-rs_amd"
 J=${J:-8}
@@ -29,6 +30,7 @@ declare -A F=(
   [sbper8]="-DSKV_SB_PER=8"
   [sbper32]="-DSKV_SB_PER=32"
   [sortprof]="-DSKV_SORT_PROF=1"
+  [t512]="-DSKV_TILE_THREADS=512"
 )
 for tag in ${TAGS:-${!F[@]}}; do
   make -s -j"$J" variant TAG="$tag" VFLAGS="${F[$tag]}"
