@@ -312,6 +312,9 @@ __device__ __forceinline__ bool sk_sbefore(const SWin& w, const SSplit* __restri
 // its 16-byte window from byte Lb[bucket] on, read here while the record's key line is in cache
 // (elements are in record order): the bucket sort then reads no record bytes, where it used to
 // load one window per element from a record at random (~250 B of HBM lines per element).
+#ifndef SKV_SB_ATOM2
+#define SKV_SB_ATOM2 0
+#endif
 #ifndef SKV_SB_THREADS
 #define SKV_SB_THREADS 256
 #endif
@@ -398,6 +401,9 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
             const uint64_t b = g[u] + c[u];
             const uint64_t slot = atomicAdd(cnt + b, 1ull);
             bs[i] = (b << 32) | slot;
+#if SKV_SB_ATOM2  // diagnostic: a second returning atomic on the same counter (adds 0): the atomics' share
+            if (atomicAdd(cnt + b, 0ull) == ~0ull) bs[i] = 0;
+#endif
             if (Lb) {
                 const uint32_t L = Lb[b];
                 if (L) {

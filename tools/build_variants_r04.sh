@@ -11,6 +11,7 @@
 #   sbtop256, sbtop2048, sbper8, sbper32  record-sort bucket search: LDS top-level entries, elements per thread
 #   sortprof  the record sort's phase ticks (SKV_SORT_PROF_PRINT=1 prints them; diagnostic)
 #   t512     general merge tiles of 4096 elements on 512 threads (8 per thread)
+#   sbatom2  record-sort bucket pass with a second returning atomic per element (diagnostic: their cost)
 set -eu
 cd "$(dirname "$0")/../skyvault-rs_amd"
 J=${J:-8}
@@ -31,6 +32,7 @@ declare -A F=(
   [sbper32]="-DSKV_SB_PER=32"
   [sortprof]="-DSKV_SORT_PROF=1"
   [t512]="-DSKV_TILE_THREADS=512"
+  [sbatom2]="-DSKV_SB_ATOM2=1"
 )
 for tag in ${TAGS:-${!F[@]}}; do
   make -s -j"$J" variant TAG="$tag" VFLAGS="${F[$tag]}"

@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O="$PWD/gpurun_out/r04"
 mkdir -p "$O"
-for v in ${VARIANTS:-base sbtop256 sbtop2048 sbper8 sbper32}; do
+for v in ${VARIANTS:-base sbatom2 sbtop256 sbtop2048 sbper8 sbper32}; do
   lib=skyvault-rs_amd/skv/libskv.so
   [ "$v" != base ] && lib=skyvault-rs_amd/skv/variants/libskv_$v.so
   SKV_LIB=$lib timeout -k 10 300 python bench.py --config 5 --steps 5 --warmup 1 --no-cpu-baseline --no-host-path \
