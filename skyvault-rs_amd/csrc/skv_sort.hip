@@ -315,6 +315,9 @@ __device__ __forceinline__ bool sk_sbefore(const SWin& w, const SSplit* __restri
 #ifndef SKV_SB_ATOM2
 #define SKV_SB_ATOM2 0
 #endif
+#ifndef SKV_SB_K4
+#define SKV_SB_K4 1  // 4-ary group-level search (0: binary lifting)
+#endif
 #ifndef SKV_SB_THREADS
 #define SKV_SB_THREADS 256
 #endif
@@ -380,6 +383,33 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
             c[u] = 0;
             dx[u] = len[u] ? sk_word8(sk_key(x[u]), x[u].klen, gcp[a[u]]) : 0;
         }
+#if SKV_SB_K4
+        // 4-ary: two bits of the count per round from three independent probes (after one binary
+        // round when log2(top) is odd): 4 dependent rounds at top = 128 where binary lifting took 7
+        // (the group level was 65 % of this kernel's time, SKV_SORT_PROF). A probe past the group's
+        // end loads a valid entry and counts as not before.
+        auto probe = [&](int u, uint64_t p) -> bool {
+            const uint64_t pp = p <= len[u] ? p : (len[u] ? len[u] : 1);
+            const uint64_t j = g[u] + pp - 1, dj = disc[j];
+            const bool before = dj != dx[u] ? dj < dx[u] : sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u]);
+            return p <= len[u] && before;
+        };
+        uint64_t st = top >> 1;
+        if (st && (__builtin_ctzll(top) & 1)) {
+#pragma unroll
+            for (int u = 0; u < SB_ILP; ++u)
+                if (probe(u, c[u] + st)) c[u] += st;
+            st >>= 1;
+        }
+        for (; st; st >>= 2) {
+            const uint64_t s = st >> 1;
+#pragma unroll
+            for (int u = 0; u < SB_ILP; ++u) {
+                const bool b1 = probe(u, c[u] + s), b2 = probe(u, c[u] + 2 * s), b3 = probe(u, c[u] + 3 * s);
+                c[u] += s * ((b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u));
+            }
+        }
+#else
         for (uint64_t st = top >> 1; st; st >>= 1) {
 #pragma unroll
             for (int u = 0; u < SB_ILP; ++u) {
@@ -392,6 +422,7 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
                 }
             }
         }
+#endif
         SPROF_T(pd);
         SPROF_ADD(2, pc, pd);
 #pragma unroll
