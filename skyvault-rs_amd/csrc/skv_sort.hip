@@ -551,6 +551,125 @@ __device__ __forceinline__ bool sk_eless(const SElem* bk, uint32_t x, uint32_t y
 
 constexpr uint32_t SORT_TIE_MAX = 32;  // longest run of equal first words sorted by one thread
 
+#ifndef SKV_SORT_REGS
+#define SKV_SORT_REGS 1  // 1: the bucket's bitonic network in registers (shuffles / LDS across waves)
+#endif
+// One compare-exchange of the network on (first word, element id) pairs: the lower index keeps the
+// smaller pair (the ascending-comparator form). Ids are distinct; padding is (~0, 0xFFFF).
+__device__ __forceinline__ void sk_cx(uint64_t& k, uint32_t& d, uint64_t pk, uint32_t pd, bool lower) {
+    const bool pless = pk < k || (pk == k && pd < d);
+    const bool pmore = pk > k || (pk == k && pd > d);
+    if (lower ? pless : pmore) {
+        k = pk;
+        d = pd;
+    }
+}
+// The bitonic network of k_sort_tile on P = 256 EPT elements held in registers: element
+// e = w * 64 EPT + u * 64 + l (wave w, register u, lane l). A pair inside a wave's span is exchanged
+// through a lane shuffle or between two registers of one lane; a pair across waves through LDS
+// (xk / xd; 3 of the 55 stages at P = 1024). The stages are template instances (LK = log2 of the
+// merge block, LJ = log2 of the pair distance), so every register index is a compile-time constant.
+template <int EPT, int LK, int LJ>
+__device__ __forceinline__ void sk_stage(uint64_t (&k)[EPT], uint32_t (&d)[EPT], uint64_t* xk, uint16_t* xd) {
+    constexpr bool flip = LJ == LK - 1;
+    constexpr uint32_t B = 1u << LK, jj = 1u << LJ, WSPAN = 64 * EPT;
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if constexpr (flip ? B <= 64 : jj < 64) {  // partner lane l ^ mask, same register
+        constexpr uint32_t mask = flip ? B - 1 : jj;
+        const bool lower = (l & (flip ? (B >> 1) : jj)) == 0;
+#pragma unroll
+        for (int u = 0; u < EPT; ++u) {
+            const uint64_t pk = __shfl_xor(k[u], (int)mask, 64);
+            const uint32_t pd = __shfl_xor(d[u], (int)mask, 64);
+            sk_cx(k[u], d[u], pk, pd, lower);
+        }
+    } else if constexpr (!flip && jj < WSPAN) {  // same lane, register u ^ jj / 64
+        constexpr int jm = (int)(jj >> 6);
+#pragma unroll
+        for (int u = 0; u < EPT; ++u) {
+            if ((u & jm) == 0) {
+                const int v = u | jm;
+                if (k[v] < k[u] || (k[v] == k[u] && d[v] < d[u])) {
+                    const uint64_t tk = k[u];
+                    const uint32_t td = d[u];
+                    k[u] = k[v];
+                    d[u] = d[v];
+                    k[v] = tk;
+                    d[v] = td;
+                }
+            }
+        }
+    } else if constexpr (flip && B <= WSPAN) {  // mirror inside the wave: lane l ^ 63, register u ^ (B / 64 - 1)
+        constexpr int mm = (int)(B >> 6) - 1;
+        uint64_t pk[EPT];
+        uint32_t pd[EPT];
+#pragma unroll
+        for (int u = 0; u < EPT; ++u) {
+            pk[u] = __shfl_xor(k[u ^ mm], 63, 64);
+            pd[u] = __shfl_xor(d[u ^ mm], 63, 64);
+        }
+#pragma unroll
+        for (int u = 0; u < EPT; ++u) sk_cx(k[u], d[u], pk[u], pd[u], (u & (int)(B >> 7)) == 0);
+    } else {  // across waves, through LDS
+#pragma unroll
+        for (int u = 0; u < EPT; ++u) {
+            const uint32_t e = w * WSPAN + (uint32_t)u * 64 + l;
+            xk[e] = k[u];
+            xd[e] = (uint16_t)d[u];
+        }
+        __syncthreads();
+        uint64_t pk[EPT];
+        uint32_t pd[EPT];
+#pragma unroll
+        for (int u = 0; u < EPT; ++u) {
+            const uint32_t e = w * WSPAN + (uint32_t)u * 64 + l, p = flip ? (e ^ (B - 1)) : (e ^ jj);
+            pk[u] = xk[p];
+            pd[u] = xd[p];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < EPT; ++u) {
+            const uint32_t e = w * WSPAN + (uint32_t)u * 64 + l, p = flip ? (e ^ (B - 1)) : (e ^ jj);
+            sk_cx(k[u], d[u], pk[u], pd[u], e < p);
+        }
+    }
+}
+template <int EPT, int LK, int LJ>
+__device__ __forceinline__ void sk_bitonic_regs(uint64_t (&k)[EPT], uint32_t (&d)[EPT], uint64_t* xk, uint16_t* xd) {
+    constexpr int LP = EPT == 1 ? 8 : (EPT == 2 ? 9 : (EPT == 4 ? 10 : 11));  // log2(256 EPT)
+    if constexpr (LK <= LP) {
+        if constexpr (LJ >= 0) {
+            sk_stage<EPT, LK, LJ>(k, d, xk, xd);
+            sk_bitonic_regs<EPT, LK, LJ - 1>(k, d, xk, xd);
+        } else {
+            sk_bitonic_regs<EPT, LK + 1, LK>(k, d, xk, xd);
+        }
+    }
+}
+// load the bucket's first words into registers (padding past n), sort, store them by position
+template <int EPT>
+__device__ void sk_sort_regs(const SElem* bk, uint32_t n, uint32_t L, bool pre, uint64_t* kw, uint16_t* id) {
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t k[EPT];
+    uint32_t d[EPT];
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+        const uint32_t e = w * 64 * EPT + (uint32_t)u * 64 + l;
+        k[u] = e < n ? sk_skey(bk[e], L, pre).wh : ~0ull;
+        d[u] = e < n ? e : 0xFFFFu;
+    }
+    sk_bitonic_regs<EPT, 1, 0>(k, d, kw, id);
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+        const uint32_t e = w * 64 * EPT + (uint32_t)u * 64 + l;
+        if (e < n) {
+            kw[e] = k[u];
+            id[e] = (uint16_t)d[u];
+        }
+    }
+}
+
+
 // One workgroup per bucket: in[start[b], start[b+1]) sorted into out[...]. The bitonic network
 // runs on the first 8 window bytes (kw) and the element ids only, 10 bytes per element where the
 // full window, length and index took 26: the sort is bound by LDS traffic. Runs of equal kw are
@@ -578,6 +697,18 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
     const uint32_t n32 = (uint32_t)n;
     SPROF_T(q0);
     if (threadIdx.x == 0) s_long = 0;
+#if SKV_SORT_REGS
+    static_assert(SORT_THREADS == 256 && SORT_CAP == 2048, "register network: 256 threads, <= 8 elements each");
+    if (n32 <= 256) sk_sort_regs<1>(bk, n32, L, pre, kw, id);
+    else if (n32 <= 512) sk_sort_regs<2>(bk, n32, L, pre, kw, id);
+    else if (n32 <= 1024) sk_sort_regs<4>(bk, n32, L, pre, kw, id);
+    else sk_sort_regs<8>(bk, n32, L, pre, kw, id);
+    __syncthreads();
+    SPROF_T(q1);
+    SPROF_ADD(4, q0, q1);
+    SPROF_T(q2);
+    SPROF_ADD(5, q1, q2);
+#else
     for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
         kw[i] = sk_skey(bk[i], L, pre).wh;
         id[i] = (uint16_t)i;
@@ -623,6 +754,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
     if (local_last) __syncthreads();
     SPROF_T(q2);
     SPROF_ADD(5, q1, q2);
+#endif
     // runs of equal kw into the full order
     for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
         const uint64_t w = kw[i];

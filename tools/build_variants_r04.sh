@@ -13,6 +13,7 @@
 #   t512     general merge tiles of 4096 elements on 512 threads (8 per thread)
 #   sbatom2  record-sort bucket pass with a second returning atomic per element (diagnostic: their cost)
 #   sbk2     record-sort group-level search by binary lifting (the round-3 form) instead of 4-ary
+#   sortlds  record-sort bucket network in LDS (the round-3 form) instead of registers
 set -eu
 cd "$(dirname "$0")/../skyvault-rs_amd"
 J=${J:-8}
@@ -35,6 +36,7 @@ declare -A F=(
   [t512]="-DSKV_TILE_THREADS=512"
   [sbatom2]="-DSKV_SB_ATOM2=1"
   [sbk2]="-DSKV_SB_K4=0"
+  [sortlds]="-DSKV_SORT_REGS=0"
 )
 for tag in ${TAGS:-${!F[@]}}; do
   make -s -j"$J" variant TAG="$tag" VFLAGS="${F[$tag]}"

@@ -1,10 +1,15 @@
 #!/bin/bash
-# Record-sort bucket-search variants (tools/build_variants_r04.sh sb*) on config 5.
+# Record-sort variants (tools/build_variants_r04.sh) on config 5, after the sort's parity tests.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O="$PWD/gpurun_out/r04"
 mkdir -p "$O"
-for v in ${VARIANTS:-base sbatom2 sbtop256 sbtop2048 sbper8 sbper32}; do
+timeout -k 10 500 python -u -m pytest tests/test_gpu_sort.py tests/test_gpu_parity.py tests/test_gpu_batch.py tests/test_gpu_fullsize.py \
+  -k "sort or wal or batch or config5 or fan_in" -m gpu -x -q --timeout 300 --timeout-method thread > "$O/sortvar_tests.log" 2>&1
+rc=$?
+tail -2 "$O/sortvar_tests.log"
+[ $rc -ne 0 ] && { grep -E "^(FAILED|ERROR)" "$O/sortvar_tests.log" | head -20; exit $rc; }
+for v in ${VARIANTS:-base sbk2 sortlds}; do
   lib=skyvault-rs_amd/skv/libskv.so
   [ "$v" != base ] && lib=skyvault-rs_amd/skv/variants/libskv_$v.so
   SKV_LIB=$lib timeout -k 10 300 python bench.py --config 5 --steps 5 --warmup 1 --no-cpu-baseline --no-host-path \
