@@ -387,9 +387,10 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
         // 4-ary: two bits of the count per round from three independent probes (after one binary
         // round when log2(top) is odd): 4 dependent rounds at top = 128 where binary lifting took 7
         // (the group level was 65 % of this kernel's time, SKV_SORT_PROF). A probe past the group's
-        // end loads a valid entry and counts as not before.
+        // end loads the group's last entry and counts as not before.
         auto probe = [&](int u, uint64_t p) -> bool {
-            const uint64_t pp = p <= len[u] ? p : (len[u] ? len[u] : 1);
+            if (!len[u]) return false;  // (an empty last group: g[u] = nsp, no entry to load)
+            const uint64_t pp = p <= len[u] ? p : len[u];
             const uint64_t j = g[u] + pp - 1, dj = disc[j];
             const bool before = dj != dx[u] ? dj < dx[u] : sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u]);
             return p <= len[u] && before;
