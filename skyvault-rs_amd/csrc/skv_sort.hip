@@ -327,7 +327,10 @@ __device__ __forceinline__ bool sk_sbefore(const SWin& w, const SSplit* __restri
 #ifndef SKV_SB_TOP
 #define SKV_SB_TOP 1024
 #endif
-constexpr int SB_THREADS = SKV_SB_THREADS, SB_PER = SKV_SB_PER, SB_TOP = SKV_SB_TOP, SB_ILP = 4;
+#ifndef SKV_SB_ILP
+#define SKV_SB_ILP 4  // elements a thread searches at once
+#endif
+constexpr int SB_THREADS = SKV_SB_THREADS, SB_PER = SKV_SB_PER, SB_TOP = SKV_SB_TOP, SB_ILP = SKV_SB_ILP;
 static_assert(SB_PER % SB_ILP == 0, "a workgroup's elements in whole ILP batches");
 __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n, const uint32_t* __restrict__ Lb,
                                                             const SSplit* __restrict__ sp,

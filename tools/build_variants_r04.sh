@@ -14,6 +14,7 @@
 #   sbatom2  record-sort bucket pass with a second returning atomic per element (diagnostic: their cost)
 #   sbk2     record-sort group-level search by binary lifting (the round-3 form) instead of 4-ary
 #   sortlds  record-sort bucket network in LDS (the round-3 form) instead of registers
+#   sbilp2   record-sort bucket pass searching 2 elements per thread at once (fewer registers)
 set -eu
 cd "$(dirname "$0")/../skyvault-rs_amd"
 J=${J:-8}
@@ -37,6 +38,7 @@ declare -A F=(
   [sbatom2]="-DSKV_SB_ATOM2=1"
   [sbk2]="-DSKV_SB_K4=0"
   [sortlds]="-DSKV_SORT_REGS=0"
+  [sbilp2]="-DSKV_SB_ILP=2"
 )
 for tag in ${TAGS:-${!F[@]}}; do
   make -s -j"$J" variant TAG="$tag" VFLAGS="${F[$tag]}"

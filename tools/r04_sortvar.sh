@@ -9,7 +9,7 @@ timeout -k 10 500 python -u -m pytest tests/test_gpu_sort.py tests/test_gpu_pari
 rc=$?
 tail -2 "$O/sortvar_tests.log"
 [ $rc -ne 0 ] && { grep -E "^(FAILED|ERROR)" "$O/sortvar_tests.log" | head -20; exit $rc; }
-for v in ${VARIANTS:-base sbk2 sortlds}; do
+for v in ${VARIANTS:-base sbk2 sortlds sbilp2}; do
   lib=skyvault-rs_amd/skv/libskv.so
   [ "$v" != base ] && lib=skyvault-rs_amd/skv/variants/libskv_$v.so
   SKV_LIB=$lib timeout -k 10 300 python bench.py --config 5 --steps 5 --warmup 1 --no-cpu-baseline --no-host-path \
