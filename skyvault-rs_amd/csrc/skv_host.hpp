@@ -110,6 +110,7 @@ struct skv_ctx {
     std::vector<RunInfo> s_runs;
     std::vector<RunSummary> s_sum;
     std::vector<uint64_t> s_sbase, s_svalid, s_first_dec, s_recb;
+    std::vector<size_t> s_span_end;  // compact_host_job: the host-contiguous spans of its runs
     std::vector<uint32_t> s_sfr, s_serr;
     std::vector<InStream> j_ranked;  // skv_compact_dev's job tables, lent to each call
     std::vector<uint64_t> j_ptr, j_len;

@@ -992,15 +992,47 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
 int compact_host_job(skv_ctx* ctx, Job& job, skv_result** out, double t_entry) {
     int rc;
     try {
-        // stage inputs into HBM (16-byte aligned per run)
+        // stage inputs into HBM: one copy per span of runs that tile one host range (consecutive in
+        // rank order, ascending or descending in memory -- a caller's buffer of 10^6 WAL runs is one
+        // span; per-run copies cost ~2.5 us each), each span 16-byte aligned, its runs at their
+        // offsets inside it (the kernels take unaligned runs)
+        const size_t n = job.run_ptr.size();
+        std::vector<size_t>& sp_end = ctx->s_span_end;  // span s: members [sp_end[s-1], sp_end[s])
+        sp_end.clear();
         uint64_t total = 0;
-        for (uint64_t l : job.run_len) total += (l + 15) & ~15ull;
+        for (size_t m = 0; m < n;) {
+            size_t e = m + 1;
+            uint64_t lo = job.run_ptr[m], hi = lo + job.run_len[m];
+            if (job.run_len[m]) {
+                int dir = 0;  // +1 ascending, -1 descending
+                while (e < n && job.run_len[e]) {
+                    const uint64_t p = job.run_ptr[e], l = job.run_len[e];
+                    const int d = p == hi ? 1 : (p + l == lo ? -1 : 0);
+                    if (!d || (dir && d != dir)) break;
+                    dir = d;
+                    if (d > 0) hi += l;
+                    else lo = p;
+                    ++e;
+                }
+            }
+            total += (hi - lo + 15) & ~15ull;
+            sp_end.push_back(e);
+            m = e;
+        }
         uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", total + 16);
         uint64_t off = 0;
-        for (size_t m = 0; m < job.run_ptr.size(); ++m) {
-            if (job.run_len[m]) h2d(ctx, d_in + off, (const void*)job.run_ptr[m], job.run_len[m]);
-            job.run_ptr[m] = (uint64_t)(uintptr_t)(d_in + off);
-            off += (job.run_len[m] + 15) & ~15ull;
+        for (size_t s = 0, m = 0; s < sp_end.size(); ++s) {
+            const size_t e = sp_end[s];
+            uint64_t lo = job.run_ptr[m], hi = lo + job.run_len[m];
+            for (size_t i = m + 1; i < e; ++i) {
+                lo = std::min<uint64_t>(lo, job.run_ptr[i]);
+                hi = std::max<uint64_t>(hi, job.run_ptr[i] + job.run_len[i]);
+            }
+            if (hi > lo) h2d(ctx, d_in + off, (const void*)lo, hi - lo);
+            for (size_t i = m; i < e; ++i)
+                job.run_ptr[i] = (uint64_t)(uintptr_t)(d_in + off + (job.run_len[i] ? job.run_ptr[i] - lo : 0));
+            off += (hi - lo + 15) & ~15ull;
+            m = e;
         }
     } catch (const DevError& e) {
         return set_err(ctx, SKV_E_DEVICE, "%s", e.msg.c_str());
