@@ -20,7 +20,7 @@ from skv import format as fmt
 from skv.api import Compactor
 
 import pyoracle
-from test_gpu_parity import _diff, _run_both
+from test_gpu_parity import _diff, _norm, _run_both
 
 pytestmark = pytest.mark.gpu
 MiB = 1 << 20
@@ -421,3 +421,40 @@ def test_wal_flush_of_many_tiny_runs_kernel_ingest(dev, pipe_env):
     exp = pyoracle.compact([(s + 1, [r]) for s, r in enumerate(runs)], 1 << 40, _abi.SKV_SPLIT_BY_TABLE)
     assert [r.data for r in got] == [r.data for r in exp]
     assert [r.table_id for r in got] == [r.table_id for r in exp]
+
+
+@pytest.mark.parametrize("order", ["ascending", "descending", "mixed"])
+def test_serial_path_stages_host_contiguous_runs_as_spans(dev, order):
+    """the serial host path (SKV_HOST_PIPE=0) stages runs that tile one host buffer with one copy
+    per span: the runs of a WAL flush in one numpy buffer, laid out in rank order (ascending
+    addresses), against it (descending, as a caller's seq 1..N buffer ranks), or shuffled (spans of
+    one run); an empty stream and a run of only a version byte inside the buffer -- bytes,
+    descriptors and the dropped-table count equal to the oracle's"""
+    rng = random.Random({"ascending": 11, "descending": 12, "mixed": 13}[order])
+    streams = _wal_streams(rng, 40, 300, [str(t) for t in range(30)])
+    streams[5] = (streams[5][0], [b"\x01"])
+    runs = [r[0] for _, r in streams]
+    idx = list(range(len(runs)))
+    if order == "ascending":
+        idx.reverse()  # rank order is seq descending: lay the highest seq first
+    elif order == "mixed":
+        rng.shuffle(idx)
+    buf = np.frombuffer(b"".join(runs[i] for i in idx), dtype=np.uint8).copy()
+    offs, at = [0] * len(runs), 0
+    for i in idx:
+        offs[i] = at
+        at += len(runs[i])
+    base = buf.ctypes.data
+    pstreams = [(seq, [(base + offs[i], len(runs[i]))]) for i, (seq, _) in enumerate(streams)]
+    pstreams.append((100, []))
+    old = os.environ.get("SKV_HOST_PIPE")
+    os.environ["SKV_HOST_PIPE"] = "0"
+    try:
+        got = dev.compact_host_ptrs(pstreams, 4 * MiB, _abi.SKV_SPLIT_BY_TABLE, with_runs=True)
+    finally:
+        if old is None:
+            os.environ.pop("SKV_HOST_PIPE", None)
+        else:
+            os.environ["SKV_HOST_PIPE"] = old
+    exp = pyoracle.compact(streams + [(100, [])], 4 * MiB, _abi.SKV_SPLIT_BY_TABLE)
+    assert _norm(got) == _norm(exp)
