@@ -66,7 +66,8 @@ static int wal_result(skv_ctx* ctx, const Job& job, uint64_t R, uint8_t* d_out, 
 constexpr int RC_DECLINED = -1000;
 constexpr uint32_t WF_TCAP = 1u << 16, WF_GUESS = 1024;
 static int wal_fused(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, const uint64_t* m_src,
-                     const uint64_t* m_P, const uint64_t* m_Dp, const uint32_t* fp_bad, skv_result** out) {
+                     const uint64_t* m_P, const uint64_t* m_Dp, const uint32_t* fp_bad, skv_result** out,
+                     const SElem* S, const uint32_t* m_rec) {
     hipStream_t st = ctx->stream;
     // a part of a pipelined host call writes into the call's shared output buffer
     uint8_t* d_out = job.dev_out ? job.dev_out : dbuf<uint8_t>(ctx, "out", job.in_bytes + R + 16);
@@ -83,7 +84,7 @@ static int wal_fused(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
     // in a key-range part every key must carry the canonical "{id}." prefix: the cuts are canonical
     // prefixes, so only then does no table straddle two parts (WAL_STRICT_CANON)
     launch_wal_fused(st, d_K, R, m_src, m_P, m_Dp, d_out, tstate, words, words + 1, tl, words + 2, WF_TCAP, tail,
-                     (fe && fe[0] == '2' ? 2u : 0u) | (job.part ? WAL_STRICT_CANON : 0u));
+                     (fe && fe[0] == '2' ? 2u : 0u) | (job.part ? WAL_STRICT_CANON : 0u), S, m_rec);
     HIPCHK(hipGetLastError());
     mark(ctx, PH_GATHER);
     uint8_t* hp = (uint8_t*)pinned(ctx, 128 + WF_GUESS * sizeof(WalTStart));
@@ -143,11 +144,15 @@ static int wal_fused(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
 // the surviving record count first).
 int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, const uint32_t* m_rec,
                      const uint64_t* m_src, const uint64_t* m_P, const uint64_t* m_Dp, const uint64_t* rec_addr,
-                     const uint32_t* rec_klen, const uint32_t* fp_bad, const HeapRes* heap, skv_result** out) {
+                     const uint32_t* rec_klen, const uint32_t* fp_bad, const HeapRes* heap, skv_result** out,
+                     const SElem* sorted) {
     hipStream_t st = ctx->stream;
     const char* fe = getenv("SKV_WAL_FUSED");
     if (!heap && !(fe && fe[0] == '0') && R > 0) {
-        const int rc = wal_fused(ctx, job, R, d_K, m_src, m_P, m_Dp, fp_bad, out);
+        // sorted: the record sort's output, its elements' true key prefixes by sorted position (m_rec)
+        const char* pe = getenv("SKV_WAL_PREFIX");
+        const int rc = wal_fused(ctx, job, R, d_K, m_src, m_P, m_Dp, fp_bad, out,
+                                 pe && pe[0] == '0' ? nullptr : sorted, m_rec);
         if (rc != RC_DECLINED) {
             ctx->timings.wal_stage = 1;
             return rc;
@@ -297,7 +302,8 @@ SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth, uint6
     launch_sort_bucket(st, E, n, Ss, SORT_OV, Tb - 1, split_buf, cnt, bs, pre ? L : nullptr);
     launch_scan(st, cnt, Tb, start, scan_tmp);
     launch_sort_scatter(st, E, n, bs, start, T);
-    launch_sort_tile(st, T, start, L, Tb, E, newkey, pre);
+    // (the records' level: the output elements carry their keys' true prefixes again)
+    launch_sort_tile(st, T, start, L, Tb, E, newkey, pre, pre ? split_buf : nullptr);
     return E;
 }
 
@@ -1076,6 +1082,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     const bool sorting = sort_by_fan_in(R) || fp_skipped;
     bool sorted_merged = false;     // the sort emitted the merged arrays (no level-0 merge tiles)
     uint64_t* sorted_K = nullptr;   // then: the survivor count, on the device
+    const SElem* sorted_S = nullptr;  // then: the sorted elements, true key prefixes (WAL table ids)
     if (!sorting) materialize_tables();  // the splitter merge's list offsets are the stream bases
     std::vector<uint64_t> list_off = sorting ? std::vector<uint64_t>{0, R} : stream_base;  // (no 10^6-entry copy)
     uint64_t* d_list_off = d_stream_base;
@@ -1124,8 +1131,9 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                     // m_src): no sorted record arrays
                     M.arrays = !(job.flags & SKV_SPLIT_BY_TABLE);
                 }
-                sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen, job.batch, nullptr,
-                             uniform_meta, direct ? &M : nullptr, direct ? &sorted_K : nullptr, e_direct);
+                sort_records(ctx, R, rec_hi, rec_lo, rec_addr, rec_klen, rec_meta, cmp_klen, job.batch,
+                             direct ? &sorted_S : nullptr, uniform_meta, direct ? &M : nullptr,
+                             direct ? &sorted_K : nullptr, e_direct);
                 sorted_merged = direct;
                 cmp_hi = rec_hi;
                 cmp_lo = rec_lo;
@@ -1377,7 +1385,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         join_verify();
         htrace("merge launched");
         const int rc =
-            wal_stage(ctx, job, R, d_K, m_rec, m_src, m_P, m_Dp, rec_addr, rec_klen, fp_bad, heap ? &hres : nullptr, out);
+            wal_stage(ctx, job, R, d_K, m_rec, m_src, m_P, m_Dp, rec_addr, rec_klen, fp_bad, heap ? &hres : nullptr, out,
+                      sorted_merged ? sorted_S : nullptr);
         htrace("wal stage done");
         if (rc == RC_RETRY_EXACT) return rerun_exact(ctx, job, out);
         return rc;

@@ -318,7 +318,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
 int rerun_exact(skv_ctx* ctx, const Job& job, skv_result** out);
 int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, const uint32_t* m_rec,
               const uint64_t* m_src, const uint64_t* m_P, const uint64_t* m_Dp, const uint64_t* rec_addr,
-              const uint32_t* rec_klen, const uint32_t* fp_bad, const HeapRes* heap, skv_result** out);
+              const uint32_t* rec_klen, const uint32_t* fp_bad, const HeapRes* heap, skv_result** out,
+              const SElem* sorted = nullptr);
 uint64_t fx_run_records(uint64_t max_run_size, uint64_t S, uint64_t R);
 
 // Where a fused launch's survivors go: a key-range part of a pipelined host call chains its

@@ -76,7 +76,8 @@ struct WalTStart {  // a table start of k_wal_fused (unordered list; the host so
 };
 void launch_wal_fused(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,
                       const uint64_t* Dp, uint8_t* out, uint64_t* tstate, uint32_t* ticket, uint32_t* fail,
-                      WalTStart* tlist, uint32_t* tcount, uint32_t tcap, uint64_t* tail, uint32_t diag = 0);
+                      WalTStart* tlist, uint32_t* tcount, uint32_t tcap, uint64_t* tail, uint32_t diag = 0,
+                      const SElem* S = nullptr, const uint32_t* m_rec = nullptr);
 void launch_wal_keys(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,
                      int64_t* tid, uint32_t* strip, uint32_t* wnk, uint64_t* wsize, uint8_t* canon,
                      unsigned long long* first_err);
@@ -161,7 +162,8 @@ size_t sort_split_bytes(uint64_t nsp);
 void launch_sort_scatter(hipStream_t, const SElem* E, uint64_t n, const uint64_t* bs, const uint64_t* start,
                          SElem* out);
 void launch_sort_tile(hipStream_t, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out,
-                      uint64_t* newkey, bool pre);
+                      uint64_t* newkey, bool pre,
+                      const void* split_buf = nullptr);
 // skv_search.hip — batched run lookups
 void launch_search_bsearch(hipStream_t, const uint8_t* run, uint64_t len, uint64_t R, const uint64_t* rec_addr,
                            const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,

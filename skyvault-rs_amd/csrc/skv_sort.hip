@@ -212,6 +212,26 @@ struct SSplit {
     uint32_t klen, pad;
 };
 
+// The key's true 16-byte prefix of an element whose (hi, lo) hold its window from byte L on (the
+// bucket pass, pre): bytes [0, L) are the bucket's common prefix -- its splitter's -- and bytes
+// [L, 16) the window's first 16 - L. Every key of the bucket is longer than L, so no byte of the
+// splitter's part lies past the key's end; the window is zero past it.
+__device__ __forceinline__ void sk_restore(SElem& e, uint32_t L, const SSplit* s) {
+    if (!L) return;
+    if (L >= 16) {
+        e.hi = s->hi;
+        e.lo = s->lo;
+        return;
+    }
+    const uint32_t sh = 8 * L;  // 8 .. 120: the window moves right by L bytes
+    const uint64_t rh = sh < 64 ? e.hi >> sh : 0;
+    const uint64_t rl = sh < 64 ? (e.lo >> sh) | (e.hi << (64 - sh)) : (e.hi >> (sh - 64));
+    const uint64_t mh = sh >= 64 ? ~0ull : ~0ull << (64 - sh);
+    const uint64_t ml = sh <= 64 ? 0ull : ~0ull << (128 - sh);
+    e.hi = (s->hi & mh) | rh;
+    e.lo = (s->lo & ml) | rl;
+}
+
 __device__ __forceinline__ void sk_ext(const uint8_t* key, uint32_t klen, uint64_t& x0, uint64_t& x1) {
     x0 = x1 = 0;
     if (klen <= 16) return;
@@ -508,7 +528,7 @@ __device__ __forceinline__ bool sk_wsame(const SKey& a, const SKey& c, const SEl
 // The bucket sorted in global memory, in place (bitonic on the full order), then copied out:
 // buckets above SORT_CAP, and LDS sorts that found a long run of equal first words.
 __device__ void sk_sort_global(SElem* bk, uint64_t n, uint32_t L, bool pre, SElem* out, uint64_t s0,
-                               uint64_t* newkey) {
+                               uint64_t* newkey, const SSplit* spb) {
     uint64_t P = 1;
     while (P < n) P <<= 1;
     for (uint64_t kk = 2; kk <= P; kk <<= 1) {
@@ -538,7 +558,9 @@ __device__ void sk_sort_global(SElem* bk, uint64_t n, uint32_t L, bool pre, SEle
         }
     }
     for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
-        out[s0 + i] = bk[i];
+        SElem o = bk[i];
+        if (pre && spb) sk_restore(o, L, spb);
+        out[s0 + i] = o;
         if (newkey) {
             bool nk = i == 0;
             if (!nk && pre) nk = !sk_wsame(sk_skey(bk[i - 1], L, true), sk_skey(bk[i], L, true), bk[i - 1], bk[i], L);
@@ -684,7 +706,8 @@ __device__ void sk_sort_regs(const SElem* bk, uint32_t n, uint32_t L, bool pre, 
 // merge is mirrored), so padding past n acts as +inf and is never touched.
 __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uint64_t* __restrict__ start,
                                                             const uint32_t* __restrict__ Lb, uint64_t Tb,
-                                                            SElem* out, uint64_t* newkey, bool pre) {
+                                                            SElem* out, uint64_t* newkey, bool pre,
+                                                            const SSplit* __restrict__ sp) {
     __shared__ uint64_t kw[SORT_CAP];
     __shared__ uint16_t id[SORT_CAP];
     __shared__ uint32_t s_long;
@@ -693,9 +716,12 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
     const uint64_t s0 = start[b], n = start[b + 1] - s0;
     const uint32_t L = Lb ? Lb[b] : 0u;
     SElem* bk = in + s0;
+    // sp (the records' level, pre): the output elements get their keys' true prefixes back (the WAL
+    // stage reads table ids from them). L > 0 only between two splitters: splitter b bounds bucket b.
+    const SSplit* spb = sp && L ? sp + b : nullptr;
     if (n == 0) return;
     if (n > (uint64_t)SORT_CAP) {
-        sk_sort_global(bk, n, L, pre, out, s0, newkey);
+        sk_sort_global(bk, n, L, pre, out, s0, newkey, spb);
         return;
     }
     const uint32_t n32 = (uint32_t)n;
@@ -784,12 +810,14 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
     SPROF_T(q3);
     SPROF_ADD(6, q2, q3);
     if (s_long) {  // uniform: every thread read it after the barrier
-        sk_sort_global(bk, n, L, pre, out, s0, newkey);
+        sk_sort_global(bk, n, L, pre, out, s0, newkey, spb);
         return;
     }
     for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
         const uint32_t c = id[i];
-        out[s0 + i] = bk[c];
+        SElem o = bk[c];
+        if (pre && spb) sk_restore(o, L, spb);
+        out[s0 + i] = o;
         if (newkey) {  // a key differing from its predecessor's (buckets never share a key)
             bool nk = i == 0 || kw[i - 1] != kw[i];
             if (!nk) {
@@ -901,8 +929,10 @@ void launch_sort_scatter(hipStream_t s, const SElem* E, uint64_t n, const uint64
     if (n) k_sort_scatter<<<sk_blocks(n), 256, 0, s>>>(E, n, bs, start, out);
 }
 void launch_sort_tile(hipStream_t s, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out,
-                      uint64_t* newkey, bool pre) {
-    if (Tb) k_sort_tile<<<(unsigned)Tb, SORT_THREADS, 0, s>>>(in, start, L, Tb, out, newkey, pre);
+                      uint64_t* newkey, bool pre, const void* split_buf) {
+    if (Tb)
+        k_sort_tile<<<(unsigned)Tb, SORT_THREADS, 0, s>>>(in, start, L, Tb, out, newkey, pre,
+                                                         (const SSplit*)split_buf);
 }
 
 }  // namespace skv

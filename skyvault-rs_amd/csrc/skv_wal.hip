@@ -392,6 +392,42 @@ __device__ __forceinline__ WalRec wal_parse(const uint8_t* rp, uint64_t size) {
     return r;
 }
 
+// wal_parse from a record's 16-byte key prefix (the record sort's output element: no record line
+// read): the window words are rebuilt as the record's first 21 bytes (marker, key length, key bytes
+// 0..15); a dot inside those 16 bytes (or a key of at most 16 bytes) decides it exactly, else the
+// record itself is parsed (ok = false)
+__device__ __forceinline__ WalRec wal_parse_pfx(uint64_t hi, uint64_t lo, uint32_t klen, uint32_t marker,
+                                               uint64_t size, bool& ok) {
+    WalRec r;
+    r.size = size;
+    r.marker = marker;
+    r.klen = klen;
+    r.tid = 0;
+    uint32_t k[4] = {__builtin_bswap32((uint32_t)(hi >> 32)), __builtin_bswap32((uint32_t)hi),
+                     __builtin_bswap32((uint32_t)(lo >> 32)), __builtin_bswap32((uint32_t)lo)};  // key bytes LE
+    const uint32_t kb = __builtin_bswap32(klen);
+    uint32_t hw[8];  // bytes: [marker, klen BE x4, key 0..15, zeros]
+    hw[0] = marker | (kb << 8);
+    hw[1] = (kb >> 24) | (k[0] << 8);
+    hw[2] = (k[0] >> 24) | (k[1] << 8);
+    hw[3] = (k[1] >> 24) | (k[2] << 8);
+    hw[4] = (k[2] >> 24) | (k[3] << 8);
+    hw[5] = k[3] >> 24;
+    hw[6] = hw[7] = 0;
+    const uint32_t n0 = klen < 16 ? klen : 16;
+    uint32_t hit = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if (((hw[(i + 5) >> 2] >> (8 * ((i + 5) & 3))) & 0xFFu) == (uint32_t)'.' && (uint32_t)i < n0) hit |= 1u << i;
+    ok = hit || klen <= 16;
+    if (!ok) return r;
+    const uint32_t dot = hit ? (uint32_t)__builtin_ctz(hit) : klen;
+    r.err = dot == klen ? WERR_NODOT : parse_i64_win(hw, dot, r.tid);
+    r.strip = r.err ? 0u : id_prefix_len(r.tid);
+    r.canon = !r.err && dot + 1 == r.strip;
+    return r;
+}
+
 constexpr uint32_t WF_BADKEY = 1, WF_ORDER = 2, WF_TABLES = 4;
 constexpr uint32_t WF_TBL = 4096;  // output blocks of a workgroup's span with a piece table (64 KiB)
 static_assert(WAL_G <= 256, "piece ids in the block table are bytes");
@@ -406,7 +442,8 @@ __global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict_
                                                      const uint64_t* __restrict__ P, const uint64_t* __restrict__ Dp,
                                                      uint8_t* out, uint64_t* tstate, uint32_t* ticket, uint32_t* fail,
                                                      WalTStart* tlist, uint32_t* tcount, uint32_t tcap,
-                                                     uint64_t* tail, uint32_t diag) {
+                                                     uint64_t* tail, uint32_t diag,
+                                                     const SElem* __restrict__ S, const uint32_t* __restrict__ m_rec) {
     __shared__ uint64_t os[WAL_G + 1], src[WAL_G], head[WAL_G];
     __shared__ uint32_t hl[WAL_G];
     __shared__ uint64_t s_w[WAL_G / 64], s_base[1];
@@ -427,7 +464,12 @@ __global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict_
     uint32_t bad = 0;
     if (live) {
         rp = (const uint8_t*)m_src[j];
-        r = wal_parse(rp, P[j + 1] - P[j]);
+        bool ok = false;
+        if (S) {  // the record sort's element: its key prefix, no record line read for the parse
+            const SElem e = S[m_rec[j]];
+            r = wal_parse_pfx(e.hi, e.lo, e.klen, Dp[j + 1] != Dp[j] ? 2u : 1u, P[j + 1] - P[j], ok);
+        }
+        if (!ok) r = wal_parse(rp, P[j + 1] - P[j]);
         if (r.err || ((diag & WAL_STRICT_CANON) && !r.canon)) bad |= WF_BADKEY;
     }
     // the record before: the neighbouring lane; a wave's lane 0 takes the previous wave's last lane
@@ -606,7 +648,8 @@ __global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict_
 
 void launch_wal_fused(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,
                       const uint64_t* Dp, uint8_t* out, uint64_t* tstate, uint32_t* ticket, uint32_t* fail,
-                      WalTStart* tlist, uint32_t* tcount, uint32_t tcap, uint64_t* tail, uint32_t diag) {
+                      WalTStart* tlist, uint32_t* tcount, uint32_t tcap, uint64_t* tail, uint32_t diag,
+                      const SElem* S, const uint32_t* m_rec) {
     // SKV_WAL_LDS=<bytes>: pad the workgroup's LDS request (caps workgroups per CU: a smaller set of
     // record lines in flight per XCD, so the composition's re-read can hit L2; occupancy studies)
     static const size_t pad = getenv("SKV_WAL_LDS") ? (size_t)atol(getenv("SKV_WAL_LDS")) : 0;
@@ -614,7 +657,7 @@ void launch_wal_fused(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const u
     if (lds) (void)hipFuncSetAttribute((const void*)k_wal_fused, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (max_K)
         k_wal_fused<<<wal_blocks(max_K, WAL_G), WAL_G, lds, s>>>(Kp, m_src, P, Dp, out, tstate, ticket, fail, tlist,
-                                                                  tcount, tcap, tail, diag);
+                                                                  tcount, tcap, tail, diag, S, m_rec);
 }
 
 void launch_wal_keys(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,

@@ -4,15 +4,16 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O="$PWD/gpurun_out/r04"
 mkdir -p "$O"
-timeout -k 10 500 python -u -m pytest tests/test_gpu_sort.py tests/test_gpu_parity.py tests/test_gpu_batch.py tests/test_gpu_fullsize.py \
-  -k "sort or wal or batch or config5 or fan_in" -m gpu -x -q --timeout 300 --timeout-method thread > "$O/sortvar_tests.log" 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_gpu_sort.py tests/test_gpu_parity.py tests/test_gpu_batch.py tests/test_gpu_fullsize.py tests/test_gpu_hostpipe.py \
+  -k "sort or wal or batch or config5 or fan_in or span" -m gpu -x -q --timeout 300 --timeout-method thread > "$O/sortvar_tests.log" 2>&1
 rc=$?
 tail -2 "$O/sortvar_tests.log"
 [ $rc -ne 0 ] && { grep -E "^(FAILED|ERROR)" "$O/sortvar_tests.log" | head -20; exit $rc; }
-for v in ${VARIANTS:-base sbk2 sortlds sbilp2}; do
-  lib=skyvault-rs_amd/skv/libskv.so
-  [ "$v" != base ] && lib=skyvault-rs_amd/skv/variants/libskv_$v.so
-  SKV_LIB=$lib timeout -k 10 300 python bench.py --config 5 --steps 5 --warmup 1 --no-cpu-baseline --no-host-path \
+for v in ${VARIANTS:-base nopfx sbk2 sortlds sbilp2}; do
+  lib=skyvault-rs_amd/skv/libskv.so pfx=1
+  # nopfx: the base library with the WAL stage parsing every record line (SKV_WAL_PREFIX=0)
+  case $v in base) ;; nopfx) pfx=0 ;; *) lib=skyvault-rs_amd/skv/variants/libskv_$v.so ;; esac
+  SKV_WAL_PREFIX=$pfx SKV_LIB=$lib timeout -k 10 300 python bench.py --config 5 --steps 5 --warmup 1 --no-cpu-baseline --no-host-path \
     > "$O/sortvar_$v.log" 2>&1 || { echo "variant $v failed"; tail -5 "$O/sortvar_$v.log"; exit 1; }
   echo "$v $(grep -o '"ms_per_step": [0-9.]*' $O/sortvar_$v.log) $(grep -o '"phases_ms": {[^}]*' $O/sortvar_$v.log)"
 done
