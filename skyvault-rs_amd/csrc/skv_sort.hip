@@ -282,7 +282,7 @@ __device__ __forceinline__ uint64_t sk_word8(const uint8_t* key, uint32_t klen, 
 // the zero-padded words order as the keys do (the windows' argument), so one 8-byte read decides
 // the step and the 32-byte window is read only on a tie.
 __global__ void k_sort_disc(const SElem* __restrict__ Ss, uint64_t ov, uint64_t nsp, uint64_t top, uint32_t* cp,
-                            uint64_t* disc) {
+                            uint64_t* disc, uint64_t* discA) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nsp) return;
     const uint64_t g = j / top, nt = nsp / top;
@@ -291,7 +291,11 @@ __global__ void k_sort_disc(const SElem* __restrict__ Ss, uint64_t ov, uint64_t 
     if (j % top == 0) cp[g] = c;
     if (j + 1 == nsp && (j + 1) % top == 0) cp[g + 1] = 0;  // a last, empty group
     const SElem e = Ss[(j + 1) * ov - 1];
-    disc[j] = sk_word8(sk_key(e), e.klen, c);
+    const uint64_t d = sk_word8(sk_key(e), e.klen, c);
+    disc[j] = d;
+    // the level-A table of the two-line search: group g's every (top / 16)-th discriminator
+    const uint64_t sbs = top >> 4, jj = j % top;
+    if (sbs && (jj + 1) % sbs == 0) discA[g * 16 + (jj + 1) / sbs - 1] = d;
 }
 
 // splitter vs element key order (<0, 0, >0)
@@ -335,8 +339,8 @@ __device__ __forceinline__ bool sk_sbefore(const SWin& w, const SSplit* __restri
 #ifndef SKV_SB_ATOM2
 #define SKV_SB_ATOM2 0
 #endif
-#ifndef SKV_SB_K4
-#define SKV_SB_K4 1  // 4-ary group-level search (0: binary lifting)
+#ifndef SKV_SB_BT
+#define SKV_SB_BT 1  // two-line cooperative group-level search (0: binary lifting)
 #endif
 #ifndef SKV_SB_THREADS
 #define SKV_SB_THREADS 256
@@ -357,6 +361,7 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
                                                             const SWin* __restrict__ win, uint64_t nsp, uint64_t top,
                                                             const uint32_t* __restrict__ gcp,
                                                             const uint64_t* __restrict__ disc,
+                                                            const uint64_t* __restrict__ discA,
                                                             unsigned long long* cnt, uint64_t* bs) {
     __shared__ SWin tt[SB_TOP];
     const uint32_t nt = (uint32_t)(nsp / top);  // top entry j = splitter (j + 1) * top - 1
@@ -406,47 +411,104 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
             c[u] = 0;
             dx[u] = len[u] ? sk_word8(sk_key(x[u]), x[u].klen, gcp[a[u]]) : 0;
         }
-#if SKV_SB_K4
-        // 4-ary: two bits of the count per round from three independent probes (after one binary
-        // round when log2(top) is odd): 4 dependent rounds at top = 128 where binary lifting took 7
-        // (the group level was 65 % of this kernel's time, SKV_SORT_PROF). A probe past the group's
-        // end loads the group's last entry and counts as not before.
-        auto probe = [&](int u, uint64_t p) -> bool {
-            if (!len[u]) return false;  // (an empty last group: g[u] = nsp, no entry to load)
-            const uint64_t pp = p <= len[u] ? p : len[u];
-            const uint64_t j = g[u] + pp - 1, dj = disc[j];
-            const bool before = dj != dx[u] ? dj < dx[u] : sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u]);
-            return p <= len[u] && before;
-        };
-        uint64_t st = top >> 1;
-        if (st && (__builtin_ctzll(top) & 1)) {
-#pragma unroll
-            for (int u = 0; u < SB_ILP; ++u)
-                if (probe(u, c[u] + st)) c[u] += st;
-            st >>= 1;
-        }
-        for (; st; st >>= 2) {
-            const uint64_t s = st >> 1;
+#if SKV_SB_BT
+        if (top >= 64 && top <= 256) {  // (uniform over the grid)
+            // Two-line search of the group: level A reads the group's every sbs-th discriminator (16
+            // entries, one 128-byte line), level B the sbs - 1 before the entry level A stopped at
+            // (<= 128 bytes). Eight lanes take one element's line together (one 16- or 8-byte load
+            // each) and count with ballots, so a wave instruction touches 8 lines where a probe per
+            // lane touched 64 -- the binary lifting's 7 dependent probes were 65 % of this kernel.
+            // Equal discriminators (rare) are settled by the owner lane in entry order, monotone.
+            const uint32_t sbs = (uint32_t)(top >> 4);
+            const int ln = threadIdx.x & 63, grp = ln >> 3, sub = ln & 7;
+            uint32_t ca[SB_ILP], te[SB_ILP];
 #pragma unroll
             for (int u = 0; u < SB_ILP; ++u) {
-                const bool b1 = probe(u, c[u] + s), b2 = probe(u, c[u] + 2 * s), b3 = probe(u, c[u] + 3 * s);
-                c[u] += s * ((b1 ? 1u : 0u) + (b2 ? 1u : 0u) + (b3 ? 1u : 0u));
+                ca[u] = te[u] = 0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int sl = q * 8 + grp;  // the element's owner lane (its slot u)
+                    const uint32_t aq = __shfl(a[u], sl, 64), lq = __shfl((uint32_t)len[u], sl, 64);
+                    const uint64_t dq = __shfl(dx[u], sl, 64);
+                    const uint32_t k0 = 2 * sub;
+                    const bool v0 = (k0 + 1) * sbs - 1 < lq, v1 = (k0 + 2) * sbs - 1 < lq;
+                    const ulong2 w = *(const ulong2*)(discA + (uint64_t)(v0 ? aq : 0) * 16 + k0);
+                    const uint64_t m0 = __ballot(v0 && w.x < dq), m1 = __ballot(v1 && w.y < dq);
+                    const uint64_t me = __ballot((v0 && w.x == dq) || (v1 && w.y == dq));
+                    if (grp == q) {
+                        ca[u] = __popcll((m0 >> (8 * sub)) & 0xFFu) + __popcll((m1 >> (8 * sub)) & 0xFFu);
+                        te[u] = (uint32_t)((me >> (8 * sub)) & 0xFFu);
+                    }
+                }
             }
-        }
-#else
-        for (uint64_t st = top >> 1; st; st >>= 1) {
 #pragma unroll
             for (int u = 0; u < SB_ILP; ++u) {
-                const uint64_t p = c[u] + st;
-                if (p <= len[u]) {
-                    const uint64_t j = g[u] + p - 1, dj = disc[j];
-                    const bool before =
-                        dj != dx[u] ? dj < dx[u] : sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u]);
-                    if (before) c[u] = p;
+                for (uint32_t k = ca[u]; te[u] && k < 16; ++k) {
+                    const uint64_t idx = (uint64_t)(k + 1) * sbs - 1;
+                    if (idx >= len[u]) break;
+                    const uint64_t j = g[u] + idx;
+                    if (disc[j] != dx[u] || !sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u])) break;
+                    ++ca[u];
+                }
+            }
+            uint32_t cb[SB_ILP], tb[SB_ILP];
+            const uint32_t epl = sbs >= 16 ? 2u : 1u;
+#pragma unroll
+            for (int u = 0; u < SB_ILP; ++u) {
+                cb[u] = tb[u] = 0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int sl = q * 8 + grp;
+                    const uint32_t aq = __shfl(a[u], sl, 64), lq = __shfl((uint32_t)len[u], sl, 64);
+                    const uint32_t bq = __shfl(ca[u], sl, 64) * sbs;  // the sub-block's first entry
+                    const uint64_t dq = __shfl(dx[u], sl, 64);
+                    const uint32_t i0 = sub * epl;
+                    const bool v0 = i0 < sbs - 1 && bq + i0 < lq;
+                    const bool v1 = epl == 2 && i0 + 1 < sbs - 1 && bq + i0 + 1 < lq;
+                    const uint64_t* pd = disc + (v0 ? (uint64_t)aq * top + bq + i0 : 0);
+                    uint64_t d0, d1 = 0;
+                    if (epl == 2) {
+                        const ulong2 w = *(const ulong2*)pd;
+                        d0 = w.x;
+                        d1 = w.y;
+                    } else {
+                        d0 = *pd;
+                    }
+                    const uint64_t m0 = __ballot(v0 && d0 < dq), m1 = __ballot(v1 && d1 < dq);
+                    const uint64_t me = __ballot((v0 && d0 == dq) || (v1 && d1 == dq));
+                    if (grp == q) {
+                        cb[u] = __popcll((m0 >> (8 * sub)) & 0xFFu) + __popcll((m1 >> (8 * sub)) & 0xFFu);
+                        tb[u] = (uint32_t)((me >> (8 * sub)) & 0xFFu);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < SB_ILP; ++u) {
+                const uint64_t b0 = (uint64_t)ca[u] * sbs;
+                for (uint32_t i = cb[u]; tb[u] && i + 1 < sbs; ++i) {
+                    if (b0 + i >= len[u]) break;
+                    const uint64_t j = g[u] + b0 + i;
+                    if (disc[j] != dx[u] || !sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u])) break;
+                    ++cb[u];
+                }
+                c[u] = b0 + cb[u];
+            }
+        } else
+#endif
+        {
+            for (uint64_t st = top >> 1; st; st >>= 1) {
+#pragma unroll
+                for (int u = 0; u < SB_ILP; ++u) {
+                    const uint64_t p = c[u] + st;
+                    if (p <= len[u]) {
+                        const uint64_t j = g[u] + p - 1, dj = disc[j];
+                        const bool before =
+                            dj != dx[u] ? dj < dx[u] : sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u]);
+                        if (before) c[u] = p;
+                    }
                 }
             }
         }
-#endif
         SPROF_T(pd);
         SPROF_ADD(2, pc, pd);
 #pragma unroll
@@ -911,18 +973,20 @@ void launch_sort_bucket(hipStream_t s, SElem* E, uint64_t n, const SElem* Ss, ui
     SWin* win = (SWin*)(sp + nsp + 1);
     uint64_t* disc = (uint64_t*)(win + nsp + 1);
     uint32_t* gcp = (uint32_t*)(disc + nsp + 1);
+    uint64_t* discA = (uint64_t*)(((uintptr_t)(gcp + nsp + 2) + 15) & ~(uintptr_t)15);  // (SB_TOP + 2) groups
     uint64_t top = 1;  // a power of two: the global search level is a full power-of-two search
     while (nsp / top > (uint64_t)SB_TOP) top <<= 1;
     if (nsp) {
         k_sort_splitters<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, sp, win);
-        k_sort_disc<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, top, gcp, disc);
+        k_sort_disc<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, top, gcp, disc, discA);
     }
     const uint64_t per_wg = (uint64_t)SB_THREADS * SB_PER;
     if (n) k_sort_bucket<<<(unsigned)((n + per_wg - 1) / per_wg), SB_THREADS, 0, s>>>(E, n, Lb, sp, win, nsp, top, gcp, disc,
-                                                                                     (unsigned long long*)cnt, bs);
+                                                                                     discA, (unsigned long long*)cnt, bs);
 }
 size_t sort_split_bytes(uint64_t nsp) {
-    return (size_t)(nsp + 1) * (sizeof(SSplit) + sizeof(SWin) + sizeof(uint64_t)) + (size_t)(nsp + 2) * sizeof(uint32_t);
+    return (size_t)(nsp + 1) * (sizeof(SSplit) + sizeof(SWin) + sizeof(uint64_t)) + (size_t)(nsp + 2) * sizeof(uint32_t) +
+           16 + (size_t)(SB_TOP + 2) * 16 * sizeof(uint64_t);
 }
 void launch_sort_scatter(hipStream_t s, const SElem* E, uint64_t n, const uint64_t* bs, const uint64_t* start,
                          SElem* out) {

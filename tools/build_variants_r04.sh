@@ -12,7 +12,7 @@
 #   sortprof  the record sort's phase ticks (SKV_SORT_PROF_PRINT=1 prints them; diagnostic)
 #   t512     general merge tiles of 4096 elements on 512 threads (8 per thread)
 #   sbatom2  record-sort bucket pass with a second returning atomic per element (diagnostic: their cost)
-#   sbk2     record-sort group-level search by binary lifting (the round-3 form) instead of 4-ary
+#   sbbt0    record-sort group-level search by binary lifting (the round-3 form) instead of the two-line search
 #   sortlds  record-sort bucket network in LDS (the round-3 form) instead of registers
 #   sbilp2   record-sort bucket pass searching 2 elements per thread at once (fewer registers)
 set -eu
@@ -36,7 +36,7 @@ declare -A F=(
   [sortprof]="-DSKV_SORT_PROF=1"
   [t512]="-DSKV_TILE_THREADS=512"
   [sbatom2]="-DSKV_SB_ATOM2=1"
-  [sbk2]="-DSKV_SB_K4=0"
+  [sbbt0]="-DSKV_SB_BT=0"
   [sortlds]="-DSKV_SORT_REGS=0"
   [sbilp2]="-DSKV_SB_ILP=2"
 )
