@@ -295,13 +295,13 @@ SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth, uint6
     HIPCHK(hipMemsetAsync(cnt, 0, (Tb + 1) * 8, st));
     snprintf(nm, sizeof nm, "sort_split%d", depth);
     uint8_t* split_buf = dbuf<uint8_t>(ctx, nm, sort_split_bytes(Tb - 1));
-    // depth 0 (the records themselves): the bucket search stores each element's window from its
-    // bucket's common prefix on, so the bucket sort reads no record bytes; its output keeps only
-    // addr / pos / klen meaningful (sort_records reads no more). Sample levels keep their keys.
+    // depth 0 (the records themselves): the scatter stores each element's window from its bucket's
+    // common prefix on, so the bucket sort reads no record bytes (and restores the true prefixes on
+    // output from the bucket's splitter). Sample levels keep their keys.
     const bool pre = depth == 0;
-    launch_sort_bucket(st, E, n, Ss, SORT_OV, Tb - 1, split_buf, cnt, bs, pre ? L : nullptr);
+    launch_sort_bucket(st, E, n, Ss, SORT_OV, Tb - 1, split_buf, cnt, bs, pre);
     launch_scan(st, cnt, Tb, start, scan_tmp);
-    launch_sort_scatter(st, E, n, bs, start, T);
+    launch_sort_scatter(st, E, n, bs, start, pre ? L : nullptr, T);
     // (the records' level: the output elements carry their keys' true prefixes again)
     launch_sort_tile(st, T, start, L, Tb, E, newkey, pre, pre ? split_buf : nullptr);
     return E;

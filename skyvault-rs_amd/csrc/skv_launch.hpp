@@ -156,11 +156,11 @@ void launch_sort_store(hipStream_t, uint64_t R, const SElem* E, const uint32_t* 
                        uint32_t* klen, uint32_t* cmp_klen, uint32_t* meta, bool last_wins, SortMerged M = SortMerged{});
 void launch_sort_sample(hipStream_t, const SElem* E, uint64_t n, uint64_t Ns, SElem* S);
 void launch_sort_prefix(hipStream_t, const SElem* Ss, uint64_t ov, uint64_t Tb, uint32_t* L);
-void launch_sort_bucket(hipStream_t, SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
-                        void* split_buf, uint64_t* cnt, uint64_t* bs, const uint32_t* Lb);
+void launch_sort_bucket(hipStream_t, const SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
+                        void* split_buf, uint64_t* cnt, uint64_t* bs, bool diag = false);
 size_t sort_split_bytes(uint64_t nsp);
 void launch_sort_scatter(hipStream_t, const SElem* E, uint64_t n, const uint64_t* bs, const uint64_t* start,
-                         SElem* out);
+                         const uint32_t* Lb, SElem* out);
 void launch_sort_tile(hipStream_t, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out,
                       uint64_t* newkey, bool pre,
                       const void* split_buf = nullptr);

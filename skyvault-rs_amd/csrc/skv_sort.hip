@@ -293,9 +293,9 @@ __global__ void k_sort_disc(const SElem* __restrict__ Ss, uint64_t ov, uint64_t 
     const SElem e = Ss[(j + 1) * ov - 1];
     const uint64_t d = sk_word8(sk_key(e), e.klen, c);
     disc[j] = d;
-    // the level-A table of the two-line search: group g's every (top / 16)-th discriminator
+    // the two-line search's level-A table (SKV_SB_BT): group g's every (top / 16)-th discriminator
     const uint64_t sbs = top >> 4, jj = j % top;
-    if (sbs && (jj + 1) % sbs == 0) discA[g * 16 + (jj + 1) / sbs - 1] = d;
+    if (discA && sbs && (jj + 1) % sbs == 0) discA[g * 16 + (jj + 1) / sbs - 1] = d;
 }
 
 // splitter vs element key order (<0, 0, >0)
@@ -332,15 +332,14 @@ __device__ __forceinline__ bool sk_sbefore(const SWin& w, const SSplit* __restri
 // table (32 B per splitter: 3.4 MB at config 5's 10^5 splitters, L2-resident, where the 48-byte
 // SSplit table was not). Both levels are branch-free power-of-two searches with a step count
 // uniform over the wave, run for SB_ILP elements at once so their loads overlap.
-// With Lb (the buckets' common prefix lengths), each element's (hi, lo) is replaced in place by
-// its 16-byte window from byte Lb[bucket] on, read here while the record's key line is in cache
-// (elements are in record order): the bucket sort then reads no record bytes, where it used to
-// load one window per element from a record at random (~250 B of HBM lines per element).
-#ifndef SKV_SB_ATOM2
-#define SKV_SB_ATOM2 0
+#ifndef SKV_SB_DIAGK
+#define SKV_SB_DIAGK 0
 #endif
 #ifndef SKV_SB_BT
-#define SKV_SB_BT 1  // two-line cooperative group-level search (0: binary lifting)
+#define SKV_SB_BT 0  // two-line cooperative group-level search (0: binary lifting)
+#endif
+#ifndef SKV_SB_ATOM2
+#define SKV_SB_ATOM2 0
 #endif
 #ifndef SKV_SB_THREADS
 #define SKV_SB_THREADS 256
@@ -356,7 +355,10 @@ __device__ __forceinline__ bool sk_sbefore(const SWin& w, const SSplit* __restri
 #endif
 constexpr int SB_THREADS = SKV_SB_THREADS, SB_PER = SKV_SB_PER, SB_TOP = SKV_SB_TOP, SB_ILP = SKV_SB_ILP;
 static_assert(SB_PER % SB_ILP == 0, "a workgroup's elements in whole ILP batches");
-__global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n, const uint32_t* __restrict__ Lb,
+// D (SKV_SB_DIAGK builds only, timing diagnostics with scratch outputs): bit 0 skips the LDS level
+// (a hashed group instead), bit 1 the global level, bit 2 the slot atomic
+template <int D>
+__global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restrict__ E, uint64_t n,
                                                             const SSplit* __restrict__ sp,
                                                             const SWin* __restrict__ win, uint64_t nsp, uint64_t top,
                                                             const uint32_t* __restrict__ gcp,
@@ -392,7 +394,11 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
         }
         SPROF_T(pb);
         SPROF_ADD(0, pa, pb);
-        for (uint32_t st = s1; st; st >>= 1) {
+        if (D & 1) {
+#pragma unroll
+            for (int u = 0; u < SB_ILP; ++u) a[u] = (x[u].pos * 2654435761u) % (nt + 1);
+        }
+        for (uint32_t st = (D & 1) ? 0 : s1; st; st >>= 1) {
 #pragma unroll
             for (int u = 0; u < SB_ILP; ++u) {
                 const uint32_t p = a[u] + st;
@@ -411,101 +417,109 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
             c[u] = 0;
             dx[u] = len[u] ? sk_word8(sk_key(x[u]), x[u].klen, gcp[a[u]]) : 0;
         }
+        if (D & 2) {
+#pragma unroll
+            for (int u = 0; u < SB_ILP; ++u) c[u] = len[u] ? dx[u] % len[u] : 0;
+        }
+        bool bt = false;
 #if SKV_SB_BT
-        if (top >= 64 && top <= 256) {  // (uniform over the grid)
+        bt = discA && top >= 64 && top <= 256 && !(D & 2);  // (uniform over the grid)
+        if (bt) {
             // Two-line search of the group: level A reads the group's every sbs-th discriminator (16
-            // entries, one 128-byte line), level B the sbs - 1 before the entry level A stopped at
-            // (<= 128 bytes). Eight lanes take one element's line together (one 16- or 8-byte load
-            // each) and count with ballots, so a wave instruction touches 8 lines where a probe per
-            // lane touched 64 -- the binary lifting's 7 dependent probes were 65 % of this kernel.
-            // Equal discriminators (rare) are settled by the owner lane in entry order, monotone.
-            const uint32_t sbs = (uint32_t)(top >> 4);
+            // entries, one 128-byte line), level B the sbs - 1 before the entry level A stopped at.
+            // Eight lanes take one element's line together (a 16- or 8-byte load each) and count with
+            // ballots: two line reads per element where the binary lifting's 7 dependent probes read
+            // 7 lines. Every load of a level is issued before its first ballot (a ballot is
+            // convergent: loads are not moved across it). Equal discriminators (rare) are settled by
+            // the owner lane in entry order (the order is monotone).
+            const uint32_t sbs = (uint32_t)(top >> 4), epl = sbs >= 16 ? 2u : 1u;
             const int ln = threadIdx.x & 63, grp = ln >> 3, sub = ln & 7;
-            uint32_t ca[SB_ILP], te[SB_ILP];
 #pragma unroll
             for (int u = 0; u < SB_ILP; ++u) {
-                ca[u] = te[u] = 0;
+                uint32_t aq[8], lq[8];
+                uint64_t dq[8];
+                ulong2 w[8];
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     const int sl = q * 8 + grp;  // the element's owner lane (its slot u)
-                    const uint32_t aq = __shfl(a[u], sl, 64), lq = __shfl((uint32_t)len[u], sl, 64);
-                    const uint64_t dq = __shfl(dx[u], sl, 64);
-                    const uint32_t k0 = 2 * sub;
-                    const bool v0 = (k0 + 1) * sbs - 1 < lq, v1 = (k0 + 2) * sbs - 1 < lq;
-                    const ulong2 w = *(const ulong2*)(discA + (uint64_t)(v0 ? aq : 0) * 16 + k0);
-                    const uint64_t m0 = __ballot(v0 && w.x < dq), m1 = __ballot(v1 && w.y < dq);
-                    const uint64_t me = __ballot((v0 && w.x == dq) || (v1 && w.y == dq));
+                    aq[q] = __shfl(a[u], sl, 64);
+                    lq[q] = __shfl((uint32_t)len[u], sl, 64);
+                    dq[q] = __shfl(dx[u], sl, 64);
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const bool v0 = (2 * sub + 1) * sbs - 1 < lq[q];
+                    w[q] = *(const ulong2*)(discA + (uint64_t)(v0 ? aq[q] : 0) * 16 + 2 * sub);
+                }
+                uint32_t ca = 0, te = 0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const bool v0 = (2 * sub + 1) * sbs - 1 < lq[q], v1 = (2 * sub + 2) * sbs - 1 < lq[q];
+                    const uint64_t m0 = __ballot(v0 && w[q].x < dq[q]), m1 = __ballot(v1 && w[q].y < dq[q]);
+                    const uint64_t me = __ballot((v0 && w[q].x == dq[q]) || (v1 && w[q].y == dq[q]));
                     if (grp == q) {
-                        ca[u] = __popcll((m0 >> (8 * sub)) & 0xFFu) + __popcll((m1 >> (8 * sub)) & 0xFFu);
-                        te[u] = (uint32_t)((me >> (8 * sub)) & 0xFFu);
+                        ca = __popcll((m0 >> (8 * sub)) & 0xFFu) + __popcll((m1 >> (8 * sub)) & 0xFFu);
+                        te = (uint32_t)((me >> (8 * sub)) & 0xFFu);
                     }
                 }
-            }
-#pragma unroll
-            for (int u = 0; u < SB_ILP; ++u) {
-                for (uint32_t k = ca[u]; te[u] && k < 16; ++k) {
+                for (uint32_t k = ca; te && k < 16; ++k) {
                     const uint64_t idx = (uint64_t)(k + 1) * sbs - 1;
                     if (idx >= len[u]) break;
                     const uint64_t j = g[u] + idx;
                     if (disc[j] != dx[u] || !sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u])) break;
-                    ++ca[u];
+                    ++ca;
                 }
-            }
-            uint32_t cb[SB_ILP], tb[SB_ILP];
-            const uint32_t epl = sbs >= 16 ? 2u : 1u;
+                // level B: entries ca * sbs + [0, sbs - 1)
+                uint32_t bq[8];
 #pragma unroll
-            for (int u = 0; u < SB_ILP; ++u) {
-                cb[u] = tb[u] = 0;
+                for (int q = 0; q < 8; ++q) bq[q] = __shfl(ca, q * 8 + grp, 64) * sbs;
+                uint64_t d0[8], d1[8];
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    const int sl = q * 8 + grp;
-                    const uint32_t aq = __shfl(a[u], sl, 64), lq = __shfl((uint32_t)len[u], sl, 64);
-                    const uint32_t bq = __shfl(ca[u], sl, 64) * sbs;  // the sub-block's first entry
-                    const uint64_t dq = __shfl(dx[u], sl, 64);
                     const uint32_t i0 = sub * epl;
-                    const bool v0 = i0 < sbs - 1 && bq + i0 < lq;
-                    const bool v1 = epl == 2 && i0 + 1 < sbs - 1 && bq + i0 + 1 < lq;
-                    const uint64_t* pd = disc + (v0 ? (uint64_t)aq * top + bq + i0 : 0);
-                    uint64_t d0, d1 = 0;
+                    const bool v0 = i0 + 1 < sbs && bq[q] + i0 < lq[q];
+                    const uint64_t* pd = disc + (v0 ? (uint64_t)aq[q] * top + bq[q] + i0 : 0);
                     if (epl == 2) {
-                        const ulong2 w = *(const ulong2*)pd;
-                        d0 = w.x;
-                        d1 = w.y;
+                        const ulong2 t = *(const ulong2*)pd;
+                        d0[q] = t.x;
+                        d1[q] = t.y;
                     } else {
-                        d0 = *pd;
-                    }
-                    const uint64_t m0 = __ballot(v0 && d0 < dq), m1 = __ballot(v1 && d1 < dq);
-                    const uint64_t me = __ballot((v0 && d0 == dq) || (v1 && d1 == dq));
-                    if (grp == q) {
-                        cb[u] = __popcll((m0 >> (8 * sub)) & 0xFFu) + __popcll((m1 >> (8 * sub)) & 0xFFu);
-                        tb[u] = (uint32_t)((me >> (8 * sub)) & 0xFFu);
+                        d0[q] = *pd;
+                        d1[q] = 0;
                     }
                 }
-            }
+                uint32_t cb = 0, tb = 0;
 #pragma unroll
-            for (int u = 0; u < SB_ILP; ++u) {
-                const uint64_t b0 = (uint64_t)ca[u] * sbs;
-                for (uint32_t i = cb[u]; tb[u] && i + 1 < sbs; ++i) {
+                for (int q = 0; q < 8; ++q) {
+                    const uint32_t i0 = sub * epl;
+                    const bool v0 = i0 + 1 < sbs && bq[q] + i0 < lq[q];
+                    const bool v1 = epl == 2 && i0 + 2 < sbs && bq[q] + i0 + 1 < lq[q];
+                    const uint64_t m0 = __ballot(v0 && d0[q] < dq[q]), m1 = __ballot(v1 && d1[q] < dq[q]);
+                    const uint64_t me = __ballot((v0 && d0[q] == dq[q]) || (v1 && d1[q] == dq[q]));
+                    if (grp == q) {
+                        cb = __popcll((m0 >> (8 * sub)) & 0xFFu) + __popcll((m1 >> (8 * sub)) & 0xFFu);
+                        tb = (uint32_t)((me >> (8 * sub)) & 0xFFu);
+                    }
+                }
+                const uint64_t b0 = (uint64_t)ca * sbs;
+                for (uint32_t i = cb; tb && i + 1 < sbs; ++i) {
                     if (b0 + i >= len[u]) break;
                     const uint64_t j = g[u] + b0 + i;
                     if (disc[j] != dx[u] || !sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u])) break;
-                    ++cb[u];
+                    ++cb;
                 }
-                c[u] = b0 + cb[u];
+                c[u] = b0 + cb;
             }
-        } else
+        }
 #endif
-        {
-            for (uint64_t st = top >> 1; st; st >>= 1) {
+        for (uint64_t st = (D & 2) || bt ? 0 : top >> 1; st; st >>= 1) {
 #pragma unroll
-                for (int u = 0; u < SB_ILP; ++u) {
-                    const uint64_t p = c[u] + st;
-                    if (p <= len[u]) {
-                        const uint64_t j = g[u] + p - 1, dj = disc[j];
-                        const bool before =
-                            dj != dx[u] ? dj < dx[u] : sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u]);
-                        if (before) c[u] = p;
-                    }
+            for (int u = 0; u < SB_ILP; ++u) {
+                const uint64_t p = c[u] + st;
+                if (p <= len[u]) {
+                    const uint64_t j = g[u] + p - 1, dj = disc[j];
+                    const bool before = dj != dx[u] ? dj < dx[u] : sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u]);
+                    if (before) c[u] = p;
                 }
             }
         }
@@ -516,19 +530,11 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
             if (!live[u]) continue;
             const uint64_t i = base + (uint64_t)(u0 + u) * SB_THREADS + threadIdx.x;
             const uint64_t b = g[u] + c[u];
-            const uint64_t slot = atomicAdd(cnt + b, 1ull);
+            const uint64_t slot = (D & 4) ? (i & 0xFFF) : atomicAdd(cnt + b, 1ull);
             bs[i] = (b << 32) | slot;
 #if SKV_SB_ATOM2  // diagnostic: a second returning atomic on the same counter (adds 0): the atomics' share
             if (atomicAdd(cnt + b, 0ull) == ~0ull) bs[i] = 0;
 #endif
-            if (Lb) {
-                const uint32_t L = Lb[b];
-                if (L) {
-                    SElem e = x[u];
-                    sk_window(x[u], L, e.hi, e.lo);
-                    E[i] = e;
-                }
-            }
         }
 #if SKV_SORT_PROF
         __builtin_amdgcn_s_waitcnt(0);
@@ -538,12 +544,27 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(SElem* E, uint64_t n
     }
 }
 
+// With Lb (depth 0), each element's (hi, lo) is replaced by its 16-byte window from byte Lb[bucket]
+// on, read while the record's key line is in cache (elements are in record order): the bucket sort
+// then reads no record bytes, where it used to load one window per element from a record at random
+// (~250 B of HBM lines per element). (Stored back by the bucket pass instead, the rewrite of E cost
+// 1.8 of its 8 ms at config 5, SKV_SB_DIAGK.)
 __global__ void k_sort_scatter(const SElem* __restrict__ E, uint64_t n, const uint64_t* __restrict__ bs,
-                               const uint64_t* __restrict__ start, SElem* out) {
+                               const uint64_t* __restrict__ start, const uint32_t* __restrict__ Lb, SElem* out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t v = bs[i];
-    out[start[v >> 32] + (v & 0xFFFFFFFFull)] = E[i];
+    SElem e = E[i];
+    if (Lb) {
+        const uint32_t L = Lb[v >> 32];
+        if (L) {
+            uint64_t wh, wl;
+            sk_window(e, L, wh, wl);
+            e.hi = wh;
+            e.lo = wl;
+        }
+    }
+    out[start[v >> 32] + (v & 0xFFFFFFFFull)] = e;
 }
 
 // Bucket order: window (wh, wl), then the key bytes past the window when both keys run past it,
@@ -568,7 +589,7 @@ __device__ __forceinline__ bool sk_wless(const SKey& a, const SKey& b, const SEl
 // One workgroup per bucket: in[start[b], start[b+1]) sorted into out[...]. Bitonic network in
 // the ascending-comparator form (the second element of the first step of each merge is mirrored),
 // so padding past n acts as +inf and is never touched.
-// pre: the elements' (hi, lo) already hold their windows from byte L on (k_sort_bucket with Lb).
+// pre: the elements' (hi, lo) already hold their windows from byte L on (k_sort_scatter with Lb).
 __device__ __forceinline__ SKey sk_skey(const SElem& e, uint32_t L, bool pre) {
     SKey k;
     if (pre) {
@@ -967,13 +988,13 @@ void launch_sort_sample(hipStream_t s, const SElem* E, uint64_t n, uint64_t Ns, 
 void launch_sort_prefix(hipStream_t s, const SElem* Ss, uint64_t ov, uint64_t Tb, uint32_t* L) {
     if (Tb) k_sort_prefix<<<sk_blocks(Tb), 256, 0, s>>>(Ss, ov, Tb, L);
 }
-void launch_sort_bucket(hipStream_t s, SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
-                        void* split_buf, uint64_t* cnt, uint64_t* bs, const uint32_t* Lb) {
+void launch_sort_bucket(hipStream_t s, const SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
+                        void* split_buf, uint64_t* cnt, uint64_t* bs, bool diag) {
     SSplit* sp = (SSplit*)split_buf;
     SWin* win = (SWin*)(sp + nsp + 1);
     uint64_t* disc = (uint64_t*)(win + nsp + 1);
     uint32_t* gcp = (uint32_t*)(disc + nsp + 1);
-    uint64_t* discA = (uint64_t*)(((uintptr_t)(gcp + nsp + 2) + 15) & ~(uintptr_t)15);  // (SB_TOP + 2) groups
+    uint64_t* discA = SKV_SB_BT ? (uint64_t*)(((uintptr_t)(gcp + nsp + 2) + 15) & ~(uintptr_t)15) : nullptr;
     uint64_t top = 1;  // a power of two: the global search level is a full power-of-two search
     while (nsp / top > (uint64_t)SB_TOP) top <<= 1;
     if (nsp) {
@@ -981,16 +1002,38 @@ void launch_sort_bucket(hipStream_t s, SElem* E, uint64_t n, const SElem* Ss, ui
         k_sort_disc<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, top, gcp, disc, discA);
     }
     const uint64_t per_wg = (uint64_t)SB_THREADS * SB_PER;
-    if (n) k_sort_bucket<<<(unsigned)((n + per_wg - 1) / per_wg), SB_THREADS, 0, s>>>(E, n, Lb, sp, win, nsp, top, gcp, disc,
-                                                                                     discA, (unsigned long long*)cnt, bs);
+    const unsigned nb = (unsigned)((n + per_wg - 1) / per_wg);
+#if SKV_SB_DIAGK
+    // timing diagnostics first (E still holds the true prefixes), into scratch outputs
+    if (n && diag) {
+        static uint64_t *bs2 = nullptr, *cnt2 = nullptr;
+        static uint64_t cap = 0;
+        if (cap < n) {
+            (void)hipFree(bs2);
+            (void)hipFree(cnt2);
+            if (hipMalloc(&bs2, n * 8) != hipSuccess ||
+                hipMalloc(&cnt2, (n + 2) * 8) != hipSuccess)  // (nsp < n)
+                abort();
+            cap = n;
+        }
+        auto* c2 = (unsigned long long*)cnt2;
+        (void)hipMemsetAsync(cnt2, 0, (nsp + 2) * 8, s);
+        k_sort_bucket<1><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, discA, c2, bs2);
+        k_sort_bucket<2><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, discA, c2, bs2);
+        k_sort_bucket<4><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, discA, c2, bs2);
+        k_sort_bucket<3><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, discA, c2, bs2);
+        k_sort_bucket<7><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, discA, c2, bs2);
+    }
+#endif
+    if (n) k_sort_bucket<0><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, discA, (unsigned long long*)cnt, bs);
 }
 size_t sort_split_bytes(uint64_t nsp) {
     return (size_t)(nsp + 1) * (sizeof(SSplit) + sizeof(SWin) + sizeof(uint64_t)) + (size_t)(nsp + 2) * sizeof(uint32_t) +
-           16 + (size_t)(SB_TOP + 2) * 16 * sizeof(uint64_t);
+           (SKV_SB_BT ? 16 + (size_t)(SB_TOP + 2) * 16 * sizeof(uint64_t) : 0);
 }
 void launch_sort_scatter(hipStream_t s, const SElem* E, uint64_t n, const uint64_t* bs, const uint64_t* start,
-                         SElem* out) {
-    if (n) k_sort_scatter<<<sk_blocks(n), 256, 0, s>>>(E, n, bs, start, out);
+                         const uint32_t* Lb, SElem* out) {
+    if (n) k_sort_scatter<<<sk_blocks(n), 256, 0, s>>>(E, n, bs, start, Lb, out);
 }
 void launch_sort_tile(hipStream_t s, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out,
                       uint64_t* newkey, bool pre, const void* split_buf) {

@@ -15,6 +15,8 @@
 #   sbbt0    record-sort group-level search by binary lifting (the round-3 form) instead of the two-line search
 #   sortlds  record-sort bucket network in LDS (the round-3 form) instead of registers
 #   sbilp2   record-sort bucket pass searching 2 elements per thread at once (fewer registers)
+#   sbdiag   record-sort bucket pass timing diagnostics: k_sort_bucket<D> launches with parts skipped
+#   bt, bt2  record-sort bucket pass with the two-line cooperative group search (ILP 4 / 2)
 set -eu
 cd "$(dirname "$0")/../skyvault-rs_amd"
 J=${J:-8}
@@ -39,6 +41,9 @@ declare -A F=(
   [sbbt0]="-DSKV_SB_BT=0"
   [sortlds]="-DSKV_SORT_REGS=0"
   [sbilp2]="-DSKV_SB_ILP=2"
+  [sbdiag]="-DSKV_SB_DIAGK=1"
+  [bt]="-DSKV_SB_BT=1"
+  [bt2]="-DSKV_SB_BT=1 -DSKV_SB_ILP=2"
 )
 for tag in ${TAGS:-${!F[@]}}; do
   make -s -j"$J" variant TAG="$tag" VFLAGS="${F[$tag]}"

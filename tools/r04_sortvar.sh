@@ -9,7 +9,7 @@ timeout -k 10 500 python -u -m pytest tests/test_gpu_sort.py tests/test_gpu_pari
 rc=$?
 tail -2 "$O/sortvar_tests.log"
 [ $rc -ne 0 ] && { grep -E "^(FAILED|ERROR)" "$O/sortvar_tests.log" | head -20; exit $rc; }
-for v in ${VARIANTS:-base sbbt0 sortlds}; do
+for v in ${VARIANTS:-base bt bt2 sbilp2}; do
   lib=skyvault-rs_amd/skv/libskv.so pfx=1
   # nopfx: the base library with the WAL stage parsing every record line (SKV_WAL_PREFIX=0)
   case $v in base) ;; nopfx) pfx=0 ;; *) lib=skyvault-rs_amd/skv/variants/libskv_$v.so ;; esac
