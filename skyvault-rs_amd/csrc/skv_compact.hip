@@ -299,6 +299,22 @@ SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth, uint6
     // common prefix on, so the bucket sort reads no record bytes (and restores the true prefixes on
     // output from the bucket's splitter). Sample levels keep their keys.
     const bool pre = depth == 0;
+    const uint64_t top2 = pre ? sort_two_pass_top(Tb - 1) : 0;
+    if (top2) {  // two-pass bucketing (skv_sort.hip): super-buckets, then buckets, both searched in LDS
+        const uint64_t G = sort_two_pass_groups(Tb - 1);
+        uint64_t* scnt = dbuf<uint64_t>(ctx, "sort_scnt", G + 1);
+        uint64_t* sstart = dbuf<uint64_t>(ctx, "sort_sstart", G + 1);
+        uint64_t* sscan = dbuf<uint64_t>(ctx, "sort_sscan", scan_tmp_words(G) + 64);
+        HIPCHK(hipMemsetAsync(scnt, 0, (G + 1) * 8, st));
+        launch_sort_pass_a(st, E, n, Ss, SORT_OV, Tb - 1, split_buf, scnt, bs);
+        launch_scan(st, scnt, G, sstart, sscan);
+        launch_sort_scatter(st, E, n, bs, sstart, sort_super_prefix(split_buf, Tb - 1), T);
+        launch_sort_pass_b(st, T, n, sstart, Tb - 1, split_buf, cnt, bs);
+        launch_scan(st, cnt, Tb, start, scan_tmp);
+        launch_sort_scatter(st, T, n, bs, start, nullptr, E);
+        launch_sort_tile(st, E, start, L, Tb, T, newkey, true, split_buf, top2);
+        return T;
+    }
     launch_sort_bucket(st, E, n, Ss, SORT_OV, Tb - 1, split_buf, cnt, bs, pre);
     launch_scan(st, cnt, Tb, start, scan_tmp);
     launch_sort_scatter(st, E, n, bs, start, pre ? L : nullptr, T);

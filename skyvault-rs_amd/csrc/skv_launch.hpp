@@ -163,7 +163,15 @@ void launch_sort_scatter(hipStream_t, const SElem* E, uint64_t n, const uint64_t
                          const uint32_t* Lb, SElem* out);
 void launch_sort_tile(hipStream_t, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out,
                       uint64_t* newkey, bool pre,
-                      const void* split_buf = nullptr);
+                      const void* split_buf = nullptr, uint64_t two_pass_top = 0);
+// two-pass bucketing at depth 0 (skv_sort.hip): top (the group size) when it applies, else 0
+uint64_t sort_two_pass_top(uint64_t nsp);
+uint64_t sort_two_pass_groups(uint64_t nsp);  // super-buckets
+void launch_sort_pass_a(hipStream_t, const SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
+                        void* split_buf, uint64_t* scnt, uint64_t* as);
+const uint32_t* sort_super_prefix(const void* split_buf, uint64_t nsp);  // per super-bucket common prefix
+void launch_sort_pass_b(hipStream_t, const SElem* T, uint64_t n, const uint64_t* sstart, uint64_t nsp,
+                        const void* split_buf, uint64_t* cnt, uint64_t* bs);
 // skv_search.hip — batched run lookups
 void launch_search_bsearch(hipStream_t, const uint8_t* run, uint64_t len, uint64_t R, const uint64_t* rec_addr,
                            const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,

@@ -282,7 +282,7 @@ __device__ __forceinline__ uint64_t sk_word8(const uint8_t* key, uint32_t klen, 
 // the zero-padded words order as the keys do (the windows' argument), so one 8-byte read decides
 // the step and the 32-byte window is read only on a tie.
 __global__ void k_sort_disc(const SElem* __restrict__ Ss, uint64_t ov, uint64_t nsp, uint64_t top, uint32_t* cp,
-                            uint64_t* disc, uint64_t* discA) {
+                            uint64_t* disc, ulong2* gw) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nsp) return;
     const uint64_t g = j / top, nt = nsp / top;
@@ -291,11 +291,12 @@ __global__ void k_sort_disc(const SElem* __restrict__ Ss, uint64_t ov, uint64_t 
     if (j % top == 0) cp[g] = c;
     if (j + 1 == nsp && (j + 1) % top == 0) cp[g + 1] = 0;  // a last, empty group
     const SElem e = Ss[(j + 1) * ov - 1];
-    const uint64_t d = sk_word8(sk_key(e), e.klen, c);
-    disc[j] = d;
-    // the two-line search's level-A table (SKV_SB_BT): group g's every (top / 16)-th discriminator
-    const uint64_t sbs = top >> 4, jj = j % top;
-    if (discA && sbs && (jj + 1) % sbs == 0) discA[g * 16 + (jj + 1) / sbs - 1] = d;
+    disc[j] = sk_word8(sk_key(e), e.klen, c);
+    if (gw) {  // the two-pass bucket search's group level: the 16-byte window from cp[g] on
+        uint64_t wh, wl;
+        sk_window(e, c, wh, wl);
+        gw[j] = make_ulong2(wh, wl);
+    }
 }
 
 // splitter vs element key order (<0, 0, >0)
@@ -335,9 +336,6 @@ __device__ __forceinline__ bool sk_sbefore(const SWin& w, const SSplit* __restri
 #ifndef SKV_SB_DIAGK
 #define SKV_SB_DIAGK 0
 #endif
-#ifndef SKV_SB_BT
-#define SKV_SB_BT 0  // two-line cooperative group-level search (0: binary lifting)
-#endif
 #ifndef SKV_SB_ATOM2
 #define SKV_SB_ATOM2 0
 #endif
@@ -363,7 +361,6 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restr
                                                             const SWin* __restrict__ win, uint64_t nsp, uint64_t top,
                                                             const uint32_t* __restrict__ gcp,
                                                             const uint64_t* __restrict__ disc,
-                                                            const uint64_t* __restrict__ discA,
                                                             unsigned long long* cnt, uint64_t* bs) {
     __shared__ SWin tt[SB_TOP];
     const uint32_t nt = (uint32_t)(nsp / top);  // top entry j = splitter (j + 1) * top - 1
@@ -421,98 +418,7 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restr
 #pragma unroll
             for (int u = 0; u < SB_ILP; ++u) c[u] = len[u] ? dx[u] % len[u] : 0;
         }
-        bool bt = false;
-#if SKV_SB_BT
-        bt = discA && top >= 64 && top <= 256 && !(D & 2);  // (uniform over the grid)
-        if (bt) {
-            // Two-line search of the group: level A reads the group's every sbs-th discriminator (16
-            // entries, one 128-byte line), level B the sbs - 1 before the entry level A stopped at.
-            // Eight lanes take one element's line together (a 16- or 8-byte load each) and count with
-            // ballots: two line reads per element where the binary lifting's 7 dependent probes read
-            // 7 lines. Every load of a level is issued before its first ballot (a ballot is
-            // convergent: loads are not moved across it). Equal discriminators (rare) are settled by
-            // the owner lane in entry order (the order is monotone).
-            const uint32_t sbs = (uint32_t)(top >> 4), epl = sbs >= 16 ? 2u : 1u;
-            const int ln = threadIdx.x & 63, grp = ln >> 3, sub = ln & 7;
-#pragma unroll
-            for (int u = 0; u < SB_ILP; ++u) {
-                uint32_t aq[8], lq[8];
-                uint64_t dq[8];
-                ulong2 w[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int sl = q * 8 + grp;  // the element's owner lane (its slot u)
-                    aq[q] = __shfl(a[u], sl, 64);
-                    lq[q] = __shfl((uint32_t)len[u], sl, 64);
-                    dq[q] = __shfl(dx[u], sl, 64);
-                }
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const bool v0 = (2 * sub + 1) * sbs - 1 < lq[q];
-                    w[q] = *(const ulong2*)(discA + (uint64_t)(v0 ? aq[q] : 0) * 16 + 2 * sub);
-                }
-                uint32_t ca = 0, te = 0;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const bool v0 = (2 * sub + 1) * sbs - 1 < lq[q], v1 = (2 * sub + 2) * sbs - 1 < lq[q];
-                    const uint64_t m0 = __ballot(v0 && w[q].x < dq[q]), m1 = __ballot(v1 && w[q].y < dq[q]);
-                    const uint64_t me = __ballot((v0 && w[q].x == dq[q]) || (v1 && w[q].y == dq[q]));
-                    if (grp == q) {
-                        ca = __popcll((m0 >> (8 * sub)) & 0xFFu) + __popcll((m1 >> (8 * sub)) & 0xFFu);
-                        te = (uint32_t)((me >> (8 * sub)) & 0xFFu);
-                    }
-                }
-                for (uint32_t k = ca; te && k < 16; ++k) {
-                    const uint64_t idx = (uint64_t)(k + 1) * sbs - 1;
-                    if (idx >= len[u]) break;
-                    const uint64_t j = g[u] + idx;
-                    if (disc[j] != dx[u] || !sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u])) break;
-                    ++ca;
-                }
-                // level B: entries ca * sbs + [0, sbs - 1)
-                uint32_t bq[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) bq[q] = __shfl(ca, q * 8 + grp, 64) * sbs;
-                uint64_t d0[8], d1[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const uint32_t i0 = sub * epl;
-                    const bool v0 = i0 + 1 < sbs && bq[q] + i0 < lq[q];
-                    const uint64_t* pd = disc + (v0 ? (uint64_t)aq[q] * top + bq[q] + i0 : 0);
-                    if (epl == 2) {
-                        const ulong2 t = *(const ulong2*)pd;
-                        d0[q] = t.x;
-                        d1[q] = t.y;
-                    } else {
-                        d0[q] = *pd;
-                        d1[q] = 0;
-                    }
-                }
-                uint32_t cb = 0, tb = 0;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const uint32_t i0 = sub * epl;
-                    const bool v0 = i0 + 1 < sbs && bq[q] + i0 < lq[q];
-                    const bool v1 = epl == 2 && i0 + 2 < sbs && bq[q] + i0 + 1 < lq[q];
-                    const uint64_t m0 = __ballot(v0 && d0[q] < dq[q]), m1 = __ballot(v1 && d1[q] < dq[q]);
-                    const uint64_t me = __ballot((v0 && d0[q] == dq[q]) || (v1 && d1[q] == dq[q]));
-                    if (grp == q) {
-                        cb = __popcll((m0 >> (8 * sub)) & 0xFFu) + __popcll((m1 >> (8 * sub)) & 0xFFu);
-                        tb = (uint32_t)((me >> (8 * sub)) & 0xFFu);
-                    }
-                }
-                const uint64_t b0 = (uint64_t)ca * sbs;
-                for (uint32_t i = cb; tb && i + 1 < sbs; ++i) {
-                    if (b0 + i >= len[u]) break;
-                    const uint64_t j = g[u] + b0 + i;
-                    if (disc[j] != dx[u] || !sk_sbefore(win[j], sp, j, x[u], x0[u], x1[u])) break;
-                    ++cb;
-                }
-                c[u] = b0 + cb;
-            }
-        }
-#endif
-        for (uint64_t st = (D & 2) || bt ? 0 : top >> 1; st; st >>= 1) {
+        for (uint64_t st = (D & 2) ? 0 : top >> 1; st; st >>= 1) {
 #pragma unroll
             for (int u = 0; u < SB_ILP; ++u) {
                 const uint64_t p = c[u] + st;
@@ -541,6 +447,232 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restr
 #endif
         SPROF_T(pe);
         SPROF_ADD(3, pd, pe);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Two-pass bucketing (depth 0 at config-5 sizes). The one-pass search above spends its time in the
+// group level's dependent probes of a global table and in one memory-side returning atomic per
+// element (SKV_SB_DIAGK: 4.1 and 3.1 ms of 8 at 87 M elements). Two passes keep both in LDS:
+//   A  the LDS level only: super-bucket a (group a's range of top buckets), a workgroup-local LDS
+//      count per super-bucket and one global atomic per (workgroup, super-bucket); the scatter
+//      then moves each element to its super-bucket with its window from the super-bucket's common
+//      prefix cp[a] (records read in record order)
+//   B  per chunk of the super-bucket order: the chunk's groups' 16-byte windows from cp[a] in LDS,
+//      the group search there (a tie reads the two records), LDS counts per bucket and one global
+//      atomic per (chunk, bucket); the second scatter then forms the buckets.
+// The bucket sort compares windows from cp[a] (every key of the bucket shares them) and takes its
+// 8-byte sort words from the bucket's own prefix L[b] >= cp[a] on (k_sort_tile's ks).
+constexpr int SA_PER = 32;            // pass A: elements per thread (an LDS slot each, 14 bits)
+constexpr int SBB_PER = 16;           // pass B: elements per thread
+constexpr uint32_t SBB_LW = 1024;     // pass B: group windows in LDS (16 KB), also its bucket bins
+constexpr uint32_t SBB_GMAX = 16;     // pass B: groups a chunk may span on the LDS path
+
+struct SplitLayout {
+    SSplit* sp;
+    SWin* win;
+    uint64_t* disc;
+    uint32_t* gcp;
+    ulong2* gw;
+};
+static SplitLayout split_layout(void* split_buf, uint64_t nsp) {
+    SplitLayout l;
+    l.sp = (SSplit*)split_buf;
+    l.win = (SWin*)(l.sp + nsp + 1);
+    l.disc = (uint64_t*)(l.win + nsp + 1);
+    l.gcp = (uint32_t*)(l.disc + nsp + 1);
+    l.gw = (ulong2*)(((uintptr_t)(l.gcp + nsp + 2) + 15) & ~(uintptr_t)15);
+    return l;
+}
+
+// top-level entries of the bucket search (SKV_SB_NT caps them below SB_TOP: tests reach the group
+// level and the two-pass path at small sizes)
+static uint64_t sb_top(uint64_t nsp) {
+    const char* e = getenv("SKV_SB_NT");
+    uint64_t cap = e ? strtoull(e, nullptr, 10) : (uint64_t)SB_TOP;
+    if (cap == 0 || cap > (uint64_t)SB_TOP) cap = SB_TOP;
+    uint64_t top = 1;  // a power of two: the global search level is a full power-of-two search
+    while (nsp / top > cap) top <<= 1;
+    return top;
+}
+
+__global__ void __launch_bounds__(SB_THREADS) k_sort_pass_a(const SElem* __restrict__ E, uint64_t n,
+                                                            const SSplit* __restrict__ sp,
+                                                            const SWin* __restrict__ win, uint64_t nsp, uint64_t top,
+                                                            unsigned long long* scnt, uint64_t* as) {
+    __shared__ SWin tt[SB_TOP];
+    __shared__ uint32_t hist[SB_TOP + 1];
+    const uint32_t nt = (uint32_t)(nsp / top);
+    for (uint32_t j = threadIdx.x; j < nt; j += SB_THREADS) tt[j] = win[(uint64_t)(j + 1) * top - 1];
+    for (uint32_t j = threadIdx.x; j <= nt; j += SB_THREADS) hist[j] = 0;
+    __syncthreads();
+    uint32_t s1 = 0;
+    if (nt) {
+        s1 = 1;
+        while (s1 * 2 <= nt) s1 *= 2;
+    }
+    const uint64_t base = (uint64_t)blockIdx.x * SB_THREADS * SA_PER;
+    uint32_t pk[SA_PER];  // super-bucket << 14 | workgroup-local slot
+#pragma unroll
+    for (int u0 = 0; u0 < SA_PER; u0 += SB_ILP) {
+        SElem x[SB_ILP];
+        uint64_t x0[SB_ILP], x1[SB_ILP];
+        uint32_t a[SB_ILP];
+#pragma unroll
+        for (int u = 0; u < SB_ILP; ++u) {
+            const uint64_t i = base + (uint64_t)(u0 + u) * SB_THREADS + threadIdx.x;
+            x[u] = E[i < n ? i : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < SB_ILP; ++u) {
+            sk_ext(sk_key(x[u]), x[u].klen, x0[u], x1[u]);
+            a[u] = 0;
+        }
+        for (uint32_t st = s1; st; st >>= 1) {
+#pragma unroll
+            for (int u = 0; u < SB_ILP; ++u) {
+                const uint32_t p = a[u] + st;
+                if (p <= nt && sk_sbefore(tt[p - 1], sp, (uint64_t)p * top - 1, x[u], x0[u], x1[u])) a[u] = p;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < SB_ILP; ++u) {
+            const uint64_t i = base + (uint64_t)(u0 + u) * SB_THREADS + threadIdx.x;
+            pk[u0 + u] = i < n ? (a[u] << 14) | atomicAdd(&hist[a[u]], 1u) : 0u;
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j <= nt; j += SB_THREADS) {
+        const uint32_t h = hist[j];
+        if (h) hist[j] = (uint32_t)atomicAdd(scnt + j, (unsigned long long)h);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < SA_PER; ++u) {
+        const uint64_t i = base + (uint64_t)u * SB_THREADS + threadIdx.x;
+        if (i < n) {
+            const uint32_t a = pk[u] >> 14;
+            as[i] = ((uint64_t)a << 32) | (hist[a] + (pk[u] & 0x3FFFu));
+        }
+    }
+}
+
+// splitter s strictly before element x, given equal 16-byte windows from L (the keys share bytes
+// [0, L + 16) as far as both reach): the bytes past the window, then the key length
+__device__ __noinline__ bool sk_tie_before(const SSplit* __restrict__ s, const SElem& x, uint32_t L) {
+    const uint32_t sk = s->klen;
+    if (sk > L + 16 && x.klen > L + 16) {
+        const uint32_t m = sk < x.klen ? sk : x.klen;
+        const int c = bytes_cmp16((const uint8_t*)s->addr + 5 + L + 16, sk_key(x) + L + 16, m - L - 16);
+        if (c) return c < 0;
+    }
+    return sk < x.klen;
+}
+
+// bucket count c in group a (the group's windows at w: LDS or global)
+template <typename W>
+__device__ __forceinline__ void sb_group_search(W w, const SSplit* __restrict__ spa, uint64_t top, uint64_t len,
+                                                uint32_t L, const SElem& x, uint64_t& c) {
+    c = 0;
+    for (uint64_t st = top >> 1; st; st >>= 1) {
+        const uint64_t p = c + st;
+        if (p <= len) {
+            const ulong2 v = w[p - 1];
+            const bool before = v.x != x.hi ? v.x < x.hi : (v.y != x.lo ? v.y < x.lo : sk_tie_before(spa + p - 1, x, L));
+            if (before) c = p;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(SB_THREADS) k_sort_pass_b(const SElem* __restrict__ T, uint64_t n,
+                                                            const uint64_t* __restrict__ sstart,
+                                                            const ulong2* __restrict__ gw,
+                                                            const SSplit* __restrict__ sp,
+                                                            const uint32_t* __restrict__ gcp, uint64_t nsp,
+                                                            uint64_t top, uint32_t gmax, unsigned long long* cnt,
+                                                            uint64_t* bs) {
+    __shared__ ulong2 lw[SBB_LW];
+    __shared__ uint32_t hist[SBB_LW];
+    __shared__ uint64_t s_st[SBB_GMAX + 1];
+    __shared__ uint32_t s_a0, s_ng;
+    const uint32_t nt = (uint32_t)(nsp / top);
+    const uint64_t p0 = (uint64_t)blockIdx.x * SB_THREADS * SBB_PER;
+    if (p0 >= n) return;
+    const uint64_t p1 = p0 + (uint64_t)SB_THREADS * SBB_PER < n ? p0 + (uint64_t)SB_THREADS * SBB_PER : n;
+    if (threadIdx.x == 0) {  // the chunk's first and last super-buckets (sstart: nt + 2 entries, last = n)
+        uint32_t lo = 0, hi = nt + 1;  // largest a with sstart[a] <= p
+        while (hi - lo > 1) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (sstart[m] <= p0) lo = m;
+            else hi = m;
+        }
+        const uint32_t a0 = lo;
+        hi = nt + 1;
+        while (hi - lo > 1) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (sstart[m] <= p1 - 1) lo = m;
+            else hi = m;
+        }
+        s_a0 = a0;
+        s_ng = lo - a0 + 1;
+    }
+    __syncthreads();
+    const uint32_t a0 = s_a0, ng = s_ng;
+    const bool lds = ng <= gmax && (uint64_t)ng * top <= SBB_LW;  // (uniform; else the global windows)
+    if (lds) {
+        for (uint32_t k = threadIdx.x; k < ng * top; k += SB_THREADS) {
+            const uint64_t j = (uint64_t)a0 * top + k;
+            lw[k] = j < nsp ? gw[j] : make_ulong2(0, 0);
+            hist[k] = 0;
+        }
+        for (uint32_t k = threadIdx.x; k <= ng; k += SB_THREADS) s_st[k] = sstart[a0 + k];
+        __syncthreads();
+    }
+    uint32_t pk[SBB_PER];  // bin (bucket - a0 top) << 13 | workgroup-local slot
+#pragma unroll
+    for (int u = 0; u < SBB_PER; ++u) {
+        const uint64_t p = p0 + (uint64_t)u * SB_THREADS + threadIdx.x;
+        pk[u] = 0;
+        if (p >= p1) continue;
+        const SElem x = T[p];
+        uint32_t a = a0;
+        if (lds) {
+            while (a + 1 < a0 + ng && s_st[a + 1 - a0] <= p) ++a;
+        } else {
+            uint32_t lo = a0, hi = nt + 1;
+            while (hi - lo > 1) {
+                const uint32_t m = (lo + hi) >> 1;
+                if (sstart[m] <= p) lo = m;
+                else hi = m;
+            }
+            a = lo;
+        }
+        const uint64_t len = a < nt ? top - 1 : nsp - (uint64_t)nt * top;
+        uint64_t c;
+        if (lds) sb_group_search(lw + (uint64_t)(a - a0) * top, sp + (uint64_t)a * top, top, len, gcp[a], x, c);
+        else sb_group_search(gw + (uint64_t)a * top, sp + (uint64_t)a * top, top, len, gcp[a], x, c);
+        const uint64_t b = (uint64_t)a * top + c;
+        if (lds) {
+            const uint32_t bin = (uint32_t)(b - (uint64_t)a0 * top);
+            pk[u] = (bin << 13) | atomicAdd(&hist[bin], 1u);
+        } else {
+            bs[p] = (b << 32) | atomicAdd(cnt + b, 1ull);
+        }
+    }
+    if (!lds) return;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < ng * top; k += SB_THREADS) {
+        const uint32_t h = hist[k];
+        if (h) hist[k] = (uint32_t)atomicAdd(cnt + (uint64_t)a0 * top + k, (unsigned long long)h);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < SBB_PER; ++u) {
+        const uint64_t p = p0 + (uint64_t)u * SB_THREADS + threadIdx.x;
+        if (p < p1) {
+            const uint32_t bin = pk[u] >> 13;
+            bs[p] = (((uint64_t)a0 * top + bin) << 32) | (hist[bin] + (pk[u] & 0x1FFFu));
+        }
     }
 }
 
@@ -756,15 +888,25 @@ __device__ __forceinline__ void sk_bitonic_regs(uint64_t (&k)[EPT], uint32_t (&d
     }
 }
 // load the bucket's first words into registers (padding past n), sort, store them by position
+// the bitonic network's 8-byte sort word: the window's first 8 bytes past the ks bytes every key of
+// the bucket shares beyond L (two-pass windows start at the super-bucket's prefix L <= L[b])
+__device__ __forceinline__ uint64_t sk_kw(const SElem& e, uint32_t L, bool pre, uint32_t ks) {
+    const SKey k = sk_skey(e, L, pre);
+    const uint32_t sh = 8 * ks;
+    if (!sh) return k.wh;
+    return sh < 64 ? (k.wh << sh) | (k.wl >> (64 - sh)) : (sh < 128 ? k.wl << (sh - 64) : 0ull);
+}
+
 template <int EPT>
-__device__ void sk_sort_regs(const SElem* bk, uint32_t n, uint32_t L, bool pre, uint64_t* kw, uint16_t* id) {
+__device__ void sk_sort_regs(const SElem* bk, uint32_t n, uint32_t L, bool pre, uint32_t ks, uint64_t* kw,
+                             uint16_t* id) {
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint64_t k[EPT];
     uint32_t d[EPT];
 #pragma unroll
     for (int u = 0; u < EPT; ++u) {
         const uint32_t e = w * 64 * EPT + (uint32_t)u * 64 + l;
-        k[u] = e < n ? sk_skey(bk[e], L, pre).wh : ~0ull;
+        k[u] = e < n ? sk_kw(bk[e], L, pre, ks) : ~0ull;
         d[u] = e < n ? e : 0xFFFFu;
     }
     sk_bitonic_regs<EPT, 1, 0>(k, d, kw, id);
@@ -790,14 +932,19 @@ __device__ void sk_sort_regs(const SElem* bk, uint32_t n, uint32_t L, bool pre, 
 __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uint64_t* __restrict__ start,
                                                             const uint32_t* __restrict__ Lb, uint64_t Tb,
                                                             SElem* out, uint64_t* newkey, bool pre,
-                                                            const SSplit* __restrict__ sp) {
+                                                            const SSplit* __restrict__ sp,
+                                                            const uint32_t* __restrict__ Lsup, uint64_t top) {
     __shared__ uint64_t kw[SORT_CAP];
     __shared__ uint16_t id[SORT_CAP];
     __shared__ uint32_t s_long;
     const uint64_t b = blockIdx.x;
     if (b >= Tb) return;
     const uint64_t s0 = start[b], n = start[b + 1] - s0;
-    const uint32_t L = Lb ? Lb[b] : 0u;
+    // L: where the elements' windows start (Lsup: the two-pass super-bucket's prefix, else the
+    // bucket's own); ks: bytes past L that every key of the bucket shares (sort words skip them)
+    const uint32_t Lt = Lb ? Lb[b] : 0u;
+    const uint32_t L = Lsup ? Lsup[b / top] : Lt;
+    const uint32_t ks = Lt > L ? Lt - L : 0u;
     SElem* bk = in + s0;
     // sp (the records' level, pre): the output elements get their keys' true prefixes back (the WAL
     // stage reads table ids from them). L > 0 only between two splitters: splitter b bounds bucket b.
@@ -812,10 +959,10 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
     if (threadIdx.x == 0) s_long = 0;
 #if SKV_SORT_REGS
     static_assert(SORT_THREADS == 256 && SORT_CAP == 2048, "register network: 256 threads, <= 8 elements each");
-    if (n32 <= 256) sk_sort_regs<1>(bk, n32, L, pre, kw, id);
-    else if (n32 <= 512) sk_sort_regs<2>(bk, n32, L, pre, kw, id);
-    else if (n32 <= 1024) sk_sort_regs<4>(bk, n32, L, pre, kw, id);
-    else sk_sort_regs<8>(bk, n32, L, pre, kw, id);
+    if (n32 <= 256) sk_sort_regs<1>(bk, n32, L, pre, ks, kw, id);
+    else if (n32 <= 512) sk_sort_regs<2>(bk, n32, L, pre, ks, kw, id);
+    else if (n32 <= 1024) sk_sort_regs<4>(bk, n32, L, pre, ks, kw, id);
+    else sk_sort_regs<8>(bk, n32, L, pre, ks, kw, id);
     __syncthreads();
     SPROF_T(q1);
     SPROF_ADD(4, q0, q1);
@@ -823,7 +970,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
     SPROF_ADD(5, q1, q2);
 #else
     for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
-        kw[i] = sk_skey(bk[i], L, pre).wh;
+        kw[i] = sk_kw(bk[i], L, pre, ks);
         id[i] = (uint16_t)i;
     }
     __syncthreads();
@@ -990,16 +1137,15 @@ void launch_sort_prefix(hipStream_t s, const SElem* Ss, uint64_t ov, uint64_t Tb
 }
 void launch_sort_bucket(hipStream_t s, const SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
                         void* split_buf, uint64_t* cnt, uint64_t* bs, bool diag) {
-    SSplit* sp = (SSplit*)split_buf;
-    SWin* win = (SWin*)(sp + nsp + 1);
-    uint64_t* disc = (uint64_t*)(win + nsp + 1);
-    uint32_t* gcp = (uint32_t*)(disc + nsp + 1);
-    uint64_t* discA = SKV_SB_BT ? (uint64_t*)(((uintptr_t)(gcp + nsp + 2) + 15) & ~(uintptr_t)15) : nullptr;
-    uint64_t top = 1;  // a power of two: the global search level is a full power-of-two search
-    while (nsp / top > (uint64_t)SB_TOP) top <<= 1;
+    const SplitLayout l = split_layout(split_buf, nsp);
+    SSplit* sp = l.sp;
+    SWin* win = l.win;
+    uint64_t* disc = l.disc;
+    uint32_t* gcp = l.gcp;
+    const uint64_t top = sb_top(nsp);
     if (nsp) {
         k_sort_splitters<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, sp, win);
-        k_sort_disc<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, top, gcp, disc, discA);
+        k_sort_disc<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, top, gcp, disc, nullptr);
     }
     const uint64_t per_wg = (uint64_t)SB_THREADS * SB_PER;
     const unsigned nb = (unsigned)((n + per_wg - 1) / per_wg);
@@ -1018,28 +1164,64 @@ void launch_sort_bucket(hipStream_t s, const SElem* E, uint64_t n, const SElem* 
         }
         auto* c2 = (unsigned long long*)cnt2;
         (void)hipMemsetAsync(cnt2, 0, (nsp + 2) * 8, s);
-        k_sort_bucket<1><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, discA, c2, bs2);
-        k_sort_bucket<2><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, discA, c2, bs2);
-        k_sort_bucket<4><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, discA, c2, bs2);
-        k_sort_bucket<3><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, discA, c2, bs2);
-        k_sort_bucket<7><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, discA, c2, bs2);
+        k_sort_bucket<1><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, c2, bs2);
+        k_sort_bucket<2><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, c2, bs2);
+        k_sort_bucket<4><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, c2, bs2);
+        k_sort_bucket<3><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, c2, bs2);
+        k_sort_bucket<7><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, c2, bs2);
     }
 #endif
-    if (n) k_sort_bucket<0><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, discA, (unsigned long long*)cnt, bs);
+    if (n) k_sort_bucket<0><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, (unsigned long long*)cnt, bs);
 }
 size_t sort_split_bytes(uint64_t nsp) {
     return (size_t)(nsp + 1) * (sizeof(SSplit) + sizeof(SWin) + sizeof(uint64_t)) + (size_t)(nsp + 2) * sizeof(uint32_t) +
-           (SKV_SB_BT ? 16 + (size_t)(SB_TOP + 2) * 16 * sizeof(uint64_t) : 0);
+           16 + (size_t)(nsp + 1) * sizeof(ulong2);  // (the two-pass search's group windows, 16-aligned)
 }
 void launch_sort_scatter(hipStream_t s, const SElem* E, uint64_t n, const uint64_t* bs, const uint64_t* start,
                          const uint32_t* Lb, SElem* out) {
     if (n) k_sort_scatter<<<sk_blocks(n), 256, 0, s>>>(E, n, bs, start, Lb, out);
 }
 void launch_sort_tile(hipStream_t s, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out,
-                      uint64_t* newkey, bool pre, const void* split_buf) {
+                      uint64_t* newkey, bool pre, const void* split_buf, uint64_t two_pass_top) {
+    const uint32_t* Lsup = two_pass_top ? split_layout((void*)split_buf, Tb - 1).gcp : nullptr;
     if (Tb)
         k_sort_tile<<<(unsigned)Tb, SORT_THREADS, 0, s>>>(in, start, L, Tb, out, newkey, pre,
-                                                         (const SSplit*)split_buf);
+                                                         (const SSplit*)split_buf, Lsup, two_pass_top);
+}
+
+uint64_t sort_two_pass_top(uint64_t nsp) {
+    const char* e = getenv("SKV_SORT_TWO_PASS");  // 0: the one-pass search always
+    if (e && e[0] == '0') return 0;
+    const uint64_t top = sb_top(nsp);
+    return top >= 4 && top <= SBB_LW ? top : 0;
+}
+uint64_t sort_two_pass_groups(uint64_t nsp) { return nsp / sb_top(nsp) + 1; }
+
+void launch_sort_pass_a(hipStream_t s, const SElem* E, uint64_t n, const SElem* Ss, uint64_t ov, uint64_t nsp,
+                        void* split_buf, uint64_t* scnt, uint64_t* as) {
+    const SplitLayout l = split_layout(split_buf, nsp);
+    const uint64_t top = sb_top(nsp);
+    if (nsp) {
+        k_sort_splitters<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, l.sp, l.win);
+        k_sort_disc<<<sk_blocks(nsp), 256, 0, s>>>(Ss, ov, nsp, top, l.gcp, l.disc, l.gw);
+    }
+    const uint64_t per_wg = (uint64_t)SB_THREADS * SA_PER;
+    if (n)
+        k_sort_pass_a<<<(unsigned)((n + per_wg - 1) / per_wg), SB_THREADS, 0, s>>>(E, n, l.sp, l.win, nsp, top,
+                                                                                (unsigned long long*)scnt, as);
+}
+const uint32_t* sort_super_prefix(const void* split_buf, uint64_t nsp) {
+    return split_layout((void*)split_buf, nsp).gcp;
+}
+void launch_sort_pass_b(hipStream_t s, const SElem* T, uint64_t n, const uint64_t* sstart, uint64_t nsp,
+                        const void* split_buf, uint64_t* cnt, uint64_t* bs) {
+    const SplitLayout l = split_layout((void*)split_buf, nsp);
+    const uint64_t per_wg = (uint64_t)SB_THREADS * SBB_PER;
+    const char* e = getenv("SKV_SB_GMAX");  // groups a chunk may span on the LDS path (tests: 0)
+    const uint32_t gmax = e ? (uint32_t)std::min<unsigned long>(strtoul(e, nullptr, 10), SBB_GMAX) : SBB_GMAX;
+    if (n)
+        k_sort_pass_b<<<(unsigned)((n + per_wg - 1) / per_wg), SB_THREADS, 0, s>>>(
+            T, n, sstart, l.gw, l.sp, l.gcp, nsp, sb_top(nsp), gmax, (unsigned long long*)cnt, bs);
 }
 
 }  // namespace skv

@@ -170,6 +170,47 @@ def test_fan_in_tie_runs_past_the_first_word(dev):
     _check(dev, streams, 1 << 15, _abi.SKV_DROP_TOMBSTONES)
 
 
+@pytest.mark.parametrize("nt,two,gmax", [("4", "1", "16"), ("16", "1", "16"), ("16", "1", "0"), ("4", "0", "16")])
+def test_bucket_levels_at_small_sizes(dev, monkeypatch, nt, two, gmax):
+    """SKV_SB_NT caps the bucket search's LDS level at nt entries, so its group level runs at test
+    sizes: with SKV_SORT_TWO_PASS=1 the two-pass bucketing (k_sort_pass_a: super-buckets in LDS;
+    k_sort_pass_b: each chunk's groups' windows from the super-bucket prefix in LDS, or from the
+    global table when a chunk spans more than SKV_SB_GMAX groups), with 0 the one-pass search
+    through the global discriminators. WAL keys, long shared prefixes, tie runs past the sort word,
+    an equal-key flood and variable keys with tombstones, all against the oracle."""
+    monkeypatch.setenv("SKV_SB_NT", nt)
+    monkeypatch.setenv("SKV_SORT_TWO_PASS", two)
+    monkeypatch.setenv("SKV_SB_GMAX", gmax)
+    _check(dev, gen.config5(n_streams=2000), 4 * MiB, _abi.SKV_SPLIT_BY_TABLE)
+    r = random.Random(9)
+    base = "tenant-0001/namespace/partition-000/"
+    streams = []
+    for s in range(1800):
+        ks = {(base + "".join(r.choice("ab") for _ in range(r.randint(0, 50)))).encode()
+              for _ in range(r.randint(1, 8))}
+        streams.append((s + 1, [fmt.encode_run([fmt.put(k, bytes([s & 255])) for k in sorted(ks)])]))
+    _check(dev, streams, 1 << 16, 0)
+    r = random.Random(21)
+    streams = []
+    for s in range(1700):
+        ks = set()
+        for _ in range(r.randint(1, 6)):
+            grp = r.randrange(60)
+            head = f"g{grp:04d}-" + "x" * (grp % 9)
+            ks.add((head + "".join(r.choice("pq") for _ in range(r.randint(0, 6 + grp % 5)))).encode())
+        ops = [fmt.put(k, s.to_bytes(2, "big")) if r.random() < 0.9 else fmt.delete(k) for k in sorted(ks)]
+        streams.append((3 * s + 1, [fmt.encode_run(ops)]))
+    _check(dev, streams, 1 << 15, _abi.SKV_DROP_TOMBSTONES)
+    r = random.Random(5)
+    streams = []
+    for s in range(3000):
+        keys = sorted({f"k{r.randrange(4)}" for _ in range(3)} | {f"u{s:05d}"})
+        ops = [fmt.put(k, s.to_bytes(4, "big")) if r.random() < 0.8 else fmt.delete(k) for k in keys]
+        streams.append((s * 7 - 9000, [fmt.encode_run(ops)]))
+    _check(dev, streams, 1 << 14, 0)
+    _check(dev, gen.config3(n_streams=1700, run_bytes=6000, vsize=16), 256 * 1024, _abi.SKV_DROP_TOMBSTONES)
+
+
 def test_fan_in_errors_surface_like_the_reference(dev):
     """A corrupt or unsorted stream among 1600: the error is resolved before the sort."""
     r = random.Random(3)

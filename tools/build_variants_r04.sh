@@ -12,11 +12,9 @@
 #   sortprof  the record sort's phase ticks (SKV_SORT_PROF_PRINT=1 prints them; diagnostic)
 #   t512     general merge tiles of 4096 elements on 512 threads (8 per thread)
 #   sbatom2  record-sort bucket pass with a second returning atomic per element (diagnostic: their cost)
-#   sbbt0    record-sort group-level search by binary lifting (the round-3 form) instead of the two-line search
 #   sortlds  record-sort bucket network in LDS (the round-3 form) instead of registers
 #   sbilp2   record-sort bucket pass searching 2 elements per thread at once (fewer registers)
 #   sbdiag   record-sort bucket pass timing diagnostics: k_sort_bucket<D> launches with parts skipped
-#   bt, bt2  record-sort bucket pass with the two-line cooperative group search (ILP 4 / 2)
 set -eu
 cd "$(dirname "$0")/../skyvault-rs_amd"
 J=${J:-8}
@@ -38,12 +36,9 @@ declare -A F=(
   [sortprof]="-DSKV_SORT_PROF=1"
   [t512]="-DSKV_TILE_THREADS=512"
   [sbatom2]="-DSKV_SB_ATOM2=1"
-  [sbbt0]="-DSKV_SB_BT=0"
   [sortlds]="-DSKV_SORT_REGS=0"
   [sbilp2]="-DSKV_SB_ILP=2"
   [sbdiag]="-DSKV_SB_DIAGK=1"
-  [bt]="-DSKV_SB_BT=1"
-  [bt2]="-DSKV_SB_BT=1 -DSKV_SB_ILP=2"
 )
 for tag in ${TAGS:-${!F[@]}}; do
   make -s -j"$J" variant TAG="$tag" VFLAGS="${F[$tag]}"
