@@ -889,12 +889,19 @@ __device__ __forceinline__ void sk_bitonic_regs(uint64_t (&k)[EPT], uint32_t (&d
 }
 // load the bucket's first words into registers (padding past n), sort, store them by position
 // the bitonic network's 8-byte sort word: the window's first 8 bytes past the ks bytes every key of
-// the bucket shares beyond L (two-pass windows start at the super-bucket's prefix L <= L[b])
+// the bucket shares beyond L (two-pass windows start at the super-bucket's prefix L <= L[b]). Past
+// 4 shared bytes the word is read from the record instead: a super-bucket that straddles two
+// tables' keys ("17." / "18.") has L = 1 while its buckets share 20+ bytes, and a word of shared
+// bytes would send every such bucket to the global-memory sort.
 __device__ __forceinline__ uint64_t sk_kw(const SElem& e, uint32_t L, bool pre, uint32_t ks) {
+    if (ks > 4) {
+        uint64_t wh, wl;
+        sk_window(e, L + ks, wh, wl);
+        return wh;
+    }
     const SKey k = sk_skey(e, L, pre);
     const uint32_t sh = 8 * ks;
-    if (!sh) return k.wh;
-    return sh < 64 ? (k.wh << sh) | (k.wl >> (64 - sh)) : (sh < 128 ? k.wl << (sh - 64) : 0ull);
+    return sh ? (k.wh << sh) | (k.wl >> (64 - sh)) : k.wh;
 }
 
 template <int EPT>
