@@ -309,14 +309,9 @@ SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth, uint6
         launch_sort_pass_a(st, E, n, Ss, SORT_OV, Tb - 1, split_buf, scnt, bs);
         launch_scan(st, scnt, G, sstart, sscan);
         launch_sort_scatter(st, E, n, bs, sstart, sort_super_prefix(split_buf, Tb - 1), T);
-        const char* se = getenv("SKV_SORT_SUPER");  // 0: pass B over chunks + count scan + scatter
-        if (se && se[0] == '0') {
-            launch_sort_pass_b(st, T, n, sstart, Tb - 1, split_buf, cnt, bs);
-            launch_scan(st, cnt, Tb, start, scan_tmp);
-            launch_sort_scatter(st, T, n, bs, start, nullptr, E);
-        } else {  // one workgroup per super-bucket: bucket starts from its LDS histogram
-            launch_sort_super(st, T, n, sstart, Tb - 1, split_buf, (uint16_t*)bs, E, start);
-        }
+        launch_sort_pass_b(st, T, n, sstart, Tb - 1, split_buf, cnt, bs);
+        launch_scan(st, cnt, Tb, start, scan_tmp);
+        launch_sort_scatter(st, T, n, bs, start, nullptr, E);
         launch_sort_tile(st, E, start, L, Tb, T, newkey, true, split_buf, top2);
         return T;
     }

@@ -172,8 +172,6 @@ void launch_sort_pass_a(hipStream_t, const SElem* E, uint64_t n, const SElem* Ss
 const uint32_t* sort_super_prefix(const void* split_buf, uint64_t nsp);  // per super-bucket common prefix
 void launch_sort_pass_b(hipStream_t, const SElem* T, uint64_t n, const uint64_t* sstart, uint64_t nsp,
                         const void* split_buf, uint64_t* cnt, uint64_t* bs);
-void launch_sort_super(hipStream_t, const SElem* T, uint64_t n, const uint64_t* sstart, uint64_t nsp,
-                       const void* split_buf, uint16_t* cb, SElem* out, uint64_t* start);
 // skv_search.hip — batched run lookups
 void launch_search_bsearch(hipStream_t, const uint8_t* run, uint64_t len, uint64_t R, const uint64_t* rec_addr,
                            const uint64_t* rec_hi, const uint64_t* rec_lo, const uint32_t* rec_klen,

@@ -676,89 +676,6 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_pass_b(const SElem* __restr
     }
 }
 
-// Pass B as one workgroup per super-bucket (the alternative to k_sort_pass_b + scan + scatter): the
-// group's windows in LDS, the bucket of each element (kept as 16 bits in cb), the LDS histogram and
-// its scan give every bucket's start (start[], no global atomics and no bucket-count scan), then
-// the elements are read again and placed. Reads T twice, writes it once.
-constexpr int SBS_THREADS = 1024;
-__global__ void __launch_bounds__(SBS_THREADS) k_sort_super(const SElem* __restrict__ T, uint64_t n,
-                                                             const uint64_t* __restrict__ sstart,
-                                                             const ulong2* __restrict__ gw,
-                                                             const SSplit* __restrict__ sp,
-                                                             const uint32_t* __restrict__ gcp, uint64_t nsp,
-                                                             uint64_t top, uint16_t* cb, SElem* out, uint64_t* start) {
-    __shared__ ulong2 lw[SBB_LW];
-    __shared__ uint32_t hist[SBB_LW];
-    __shared__ uint32_t s_w[SBS_THREADS / 64];
-    const uint32_t nt = (uint32_t)(nsp / top);
-    const uint32_t a = blockIdx.x;  // grid: nt + 1 super-buckets
-    const uint64_t s0 = sstart[a], s1 = sstart[a + 1];
-    const uint64_t len = a < nt ? top - 1 : nsp - (uint64_t)nt * top;
-    const uint32_t L = gcp[a];
-    const SSplit* spa = sp + (uint64_t)a * top;
-    for (uint32_t k = threadIdx.x; k < top; k += SBS_THREADS) {
-        if (k < len) lw[k] = gw[(uint64_t)a * top + k];
-        hist[k] = 0;
-    }
-    __syncthreads();
-    constexpr int U = 4;
-    for (uint64_t p0 = s0 + threadIdx.x; p0 < s1; p0 += (uint64_t)U * SBS_THREADS) {
-        SElem x[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t p = p0 + (uint64_t)u * SBS_THREADS;
-            x[u] = T[p < s1 ? p : s0];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t p = p0 + (uint64_t)u * SBS_THREADS;
-            if (p < s1) {
-                uint64_t c;
-                sb_group_search(lw, spa, top, len, L, x[u], c);
-                cb[p] = (uint16_t)c;
-                atomicAdd(&hist[c], 1u);
-            }
-        }
-    }
-    __syncthreads();
-    // exclusive scan of the len + 1 bucket counts (<= SBS_THREADS): the buckets' starts
-    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const uint32_t v = t <= len ? hist[t] : 0u;
-    uint32_t inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc, d, 64);
-        if (lane >= (uint32_t)d) inc += y;
-    }
-    if (lane == 63) s_w[wv] = inc;
-    __syncthreads();
-    uint32_t off = 0;
-    for (uint32_t w = 0; w < wv; ++w) off += s_w[w];
-    const uint32_t ex = off + inc - v;
-    __syncthreads();
-    if (t <= len) {
-        hist[t] = ex;  // the bucket's cursor
-        start[(uint64_t)a * top + t] = s0 + ex;
-    }
-    if (a == nt && t == 0) start[nsp + 1] = n;
-    __syncthreads();
-    for (uint64_t p0 = s0 + threadIdx.x; p0 < s1; p0 += (uint64_t)U * SBS_THREADS) {
-        SElem x[U];
-        uint32_t c[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t p = p0 + (uint64_t)u * SBS_THREADS;
-            x[u] = T[p < s1 ? p : s0];
-            c[u] = cb[p < s1 ? p : s0];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t p = p0 + (uint64_t)u * SBS_THREADS;
-            if (p < s1) out[s0 + atomicAdd(&hist[c[u]], 1u)] = x[u];
-        }
-    }
-}
-
 // With Lb (depth 0), each element's (hi, lo) is replaced by its 16-byte window from byte Lb[bucket]
 // on, read while the record's key line is in cache (elements are in record order): the bucket sort
 // then reads no record bytes, where it used to load one window per element from a record at random
@@ -1299,13 +1216,6 @@ void launch_sort_pass_a(hipStream_t s, const SElem* E, uint64_t n, const SElem* 
     if (n)
         k_sort_pass_a<<<(unsigned)((n + per_wg - 1) / per_wg), SB_THREADS, 0, s>>>(E, n, l.sp, l.win, nsp, top,
                                                                                 (unsigned long long*)scnt, as);
-}
-void launch_sort_super(hipStream_t s, const SElem* T, uint64_t n, const uint64_t* sstart, uint64_t nsp,
-                       const void* split_buf, uint16_t* cb, SElem* out, uint64_t* start) {
-    const SplitLayout l = split_layout((void*)split_buf, nsp);
-    const uint64_t top = sb_top(nsp);
-    k_sort_super<<<(unsigned)(nsp / top + 1), SBS_THREADS, 0, s>>>(T, n, sstart, l.gw, l.sp, l.gcp, nsp, top, cb, out,
-                                                                    start);
 }
 const uint32_t* sort_super_prefix(const void* split_buf, uint64_t nsp) {
     return split_layout((void*)split_buf, nsp).gcp;

@@ -170,20 +170,17 @@ def test_fan_in_tie_runs_past_the_first_word(dev):
     _check(dev, streams, 1 << 15, _abi.SKV_DROP_TOMBSTONES)
 
 
-@pytest.mark.parametrize("nt,two,gmax,sup", [("4", "1", "16", "1"), ("16", "1", "16", "1"), ("4", "1", "16", "0"),
-                                             ("16", "1", "0", "0"), ("4", "0", "16", "1")])
-def test_bucket_levels_at_small_sizes(dev, monkeypatch, nt, two, gmax, sup):
+@pytest.mark.parametrize("nt,two,gmax", [("4", "1", "16"), ("16", "1", "16"), ("16", "1", "0"), ("4", "0", "16")])
+def test_bucket_levels_at_small_sizes(dev, monkeypatch, nt, two, gmax):
     """SKV_SB_NT caps the bucket search's LDS level at nt entries, so its group level runs at test
     sizes: with SKV_SORT_TWO_PASS=1 the two-pass bucketing (k_sort_pass_a: super-buckets in LDS;
-    then k_sort_super: a workgroup per super-bucket with its group's windows in LDS, or with
-    SKV_SORT_SUPER=0 k_sort_pass_b over chunks, whose windows come from the global table when a
-    chunk spans more than SKV_SB_GMAX groups), with 0 the one-pass search through the global
-    discriminators. WAL keys, long shared prefixes, tie runs past the sort word, an equal-key flood
+    k_sort_pass_b: each chunk's groups' windows from the super-bucket prefix in LDS, or from the
+    global table when a chunk spans more than SKV_SB_GMAX groups), with 0 the one-pass search
+    through the global discriminators. WAL keys, long shared prefixes, tie runs past the sort word, an equal-key flood
     and variable keys with tombstones, all against the oracle."""
     monkeypatch.setenv("SKV_SB_NT", nt)
     monkeypatch.setenv("SKV_SORT_TWO_PASS", two)
     monkeypatch.setenv("SKV_SB_GMAX", gmax)
-    monkeypatch.setenv("SKV_SORT_SUPER", sup)
     _check(dev, gen.config5(n_streams=2000), 4 * MiB, _abi.SKV_SPLIT_BY_TABLE)
     r = random.Random(9)
     base = "tenant-0001/namespace/partition-000/"
