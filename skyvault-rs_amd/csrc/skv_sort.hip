@@ -795,23 +795,21 @@ constexpr uint32_t SORT_TIE_MAX = 32;  // longest run of equal first words sorte
 #ifndef SKV_SORT_REGS
 #define SKV_SORT_REGS 1  // 1: the bucket's bitonic network in registers (shuffles / LDS across waves)
 #endif
-// One compare-exchange of the network on (first word, element id) pairs: the lower index keeps the
-// smaller pair (the ascending-comparator form). Ids are distinct; padding is (~0, 0xFFFF).
-__device__ __forceinline__ void sk_cx(uint64_t& k, uint32_t& d, uint64_t pk, uint32_t pd, bool lower) {
-    const bool pless = pk < k || (pk == k && pd < d);
-    const bool pmore = pk > k || (pk == k && pd > d);
-    if (lower ? pless : pmore) {
-        k = pk;
-        d = pd;
-    }
+// One compare-exchange of the network on packed sort words: the first word's top 53 bits and the
+// element id (11 bits) in one 64-bit value, so a pair moves with one 64-bit shuffle and compares
+// once (ids are distinct; padding is ~0). The lower index keeps the smaller word.
+__device__ __forceinline__ void sk_cx(uint64_t& k, uint64_t pk, bool lower) {
+    const bool take = lower ? pk < k : pk > k;
+    k = take ? pk : k;
 }
+constexpr uint64_t SK_ID_MASK = 0x7FFull;  // SORT_CAP = 2048 ids
 // The bitonic network of k_sort_tile on P = 256 EPT elements held in registers: element
 // e = w * 64 EPT + u * 64 + l (wave w, register u, lane l). A pair inside a wave's span is exchanged
 // through a lane shuffle or between two registers of one lane; a pair across waves through LDS
-// (xk / xd; 3 of the 55 stages at P = 1024). The stages are template instances (LK = log2 of the
-// merge block, LJ = log2 of the pair distance), so every register index is a compile-time constant.
+// (xk; 3 of the 55 stages at P = 1024). The stages are template instances (LK = log2 of the merge
+// block, LJ = log2 of the pair distance), so every register index is a compile-time constant.
 template <int EPT, int LK, int LJ>
-__device__ __forceinline__ void sk_stage(uint64_t (&k)[EPT], uint32_t (&d)[EPT], uint64_t* xk, uint16_t* xd) {
+__device__ __forceinline__ void sk_stage(uint64_t (&k)[EPT], uint64_t* xk) {
     constexpr bool flip = LJ == LK - 1;
     constexpr uint32_t B = 1u << LK, jj = 1u << LJ, WSPAN = 64 * EPT;
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -819,71 +817,52 @@ __device__ __forceinline__ void sk_stage(uint64_t (&k)[EPT], uint32_t (&d)[EPT],
         constexpr uint32_t mask = flip ? B - 1 : jj;
         const bool lower = (l & (flip ? (B >> 1) : jj)) == 0;
 #pragma unroll
-        for (int u = 0; u < EPT; ++u) {
-            const uint64_t pk = __shfl_xor(k[u], (int)mask, 64);
-            const uint32_t pd = __shfl_xor(d[u], (int)mask, 64);
-            sk_cx(k[u], d[u], pk, pd, lower);
-        }
+        for (int u = 0; u < EPT; ++u) sk_cx(k[u], __shfl_xor(k[u], (int)mask, 64), lower);
     } else if constexpr (!flip && jj < WSPAN) {  // same lane, register u ^ jj / 64
         constexpr int jm = (int)(jj >> 6);
 #pragma unroll
         for (int u = 0; u < EPT; ++u) {
             if ((u & jm) == 0) {
                 const int v = u | jm;
-                if (k[v] < k[u] || (k[v] == k[u] && d[v] < d[u])) {
-                    const uint64_t tk = k[u];
-                    const uint32_t td = d[u];
-                    k[u] = k[v];
-                    d[u] = d[v];
-                    k[v] = tk;
-                    d[v] = td;
-                }
+                const uint64_t lo = k[u] < k[v] ? k[u] : k[v], hi = k[u] < k[v] ? k[v] : k[u];
+                k[u] = lo;
+                k[v] = hi;
             }
         }
     } else if constexpr (flip && B <= WSPAN) {  // mirror inside the wave: lane l ^ 63, register u ^ (B / 64 - 1)
         constexpr int mm = (int)(B >> 6) - 1;
         uint64_t pk[EPT];
-        uint32_t pd[EPT];
 #pragma unroll
-        for (int u = 0; u < EPT; ++u) {
-            pk[u] = __shfl_xor(k[u ^ mm], 63, 64);
-            pd[u] = __shfl_xor(d[u ^ mm], 63, 64);
-        }
+        for (int u = 0; u < EPT; ++u) pk[u] = __shfl_xor(k[u ^ mm], 63, 64);
 #pragma unroll
-        for (int u = 0; u < EPT; ++u) sk_cx(k[u], d[u], pk[u], pd[u], (u & (int)(B >> 7)) == 0);
+        for (int u = 0; u < EPT; ++u) sk_cx(k[u], pk[u], (u & (int)(B >> 7)) == 0);
     } else {  // across waves, through LDS
 #pragma unroll
-        for (int u = 0; u < EPT; ++u) {
-            const uint32_t e = w * WSPAN + (uint32_t)u * 64 + l;
-            xk[e] = k[u];
-            xd[e] = (uint16_t)d[u];
-        }
+        for (int u = 0; u < EPT; ++u) xk[w * WSPAN + (uint32_t)u * 64 + l] = k[u];
         __syncthreads();
         uint64_t pk[EPT];
-        uint32_t pd[EPT];
 #pragma unroll
         for (int u = 0; u < EPT; ++u) {
             const uint32_t e = w * WSPAN + (uint32_t)u * 64 + l, p = flip ? (e ^ (B - 1)) : (e ^ jj);
             pk[u] = xk[p];
-            pd[u] = xd[p];
         }
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < EPT; ++u) {
             const uint32_t e = w * WSPAN + (uint32_t)u * 64 + l, p = flip ? (e ^ (B - 1)) : (e ^ jj);
-            sk_cx(k[u], d[u], pk[u], pd[u], e < p);
+            sk_cx(k[u], pk[u], e < p);
         }
     }
 }
 template <int EPT, int LK, int LJ>
-__device__ __forceinline__ void sk_bitonic_regs(uint64_t (&k)[EPT], uint32_t (&d)[EPT], uint64_t* xk, uint16_t* xd) {
+__device__ __forceinline__ void sk_bitonic_regs(uint64_t (&k)[EPT], uint64_t* xk) {
     constexpr int LP = EPT == 1 ? 8 : (EPT == 2 ? 9 : (EPT == 4 ? 10 : 11));  // log2(256 EPT)
     if constexpr (LK <= LP) {
         if constexpr (LJ >= 0) {
-            sk_stage<EPT, LK, LJ>(k, d, xk, xd);
-            sk_bitonic_regs<EPT, LK, LJ - 1>(k, d, xk, xd);
+            sk_stage<EPT, LK, LJ>(k, xk);
+            sk_bitonic_regs<EPT, LK, LJ - 1>(k, xk);
         } else {
-            sk_bitonic_regs<EPT, LK + 1, LK>(k, d, xk, xd);
+            sk_bitonic_regs<EPT, LK + 1, LK>(k, xk);
         }
     }
 }
@@ -908,21 +887,21 @@ template <int EPT>
 __device__ void sk_sort_regs(const SElem* bk, uint32_t n, uint32_t L, bool pre, uint32_t ks, uint64_t* kw,
                              uint16_t* id) {
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint64_t k[EPT];
-    uint32_t d[EPT];
+    uint64_t k[EPT];  // the sort word's top 53 bits | element id (runs of equal 53-bit words go to
+                      // the tie pass like runs of equal words did)
 #pragma unroll
     for (int u = 0; u < EPT; ++u) {
         const uint32_t e = w * 64 * EPT + (uint32_t)u * 64 + l;
-        k[u] = e < n ? sk_kw(bk[e], L, pre, ks) : ~0ull;
-        d[u] = e < n ? e : 0xFFFFu;
+        k[u] = e < n ? (sk_kw(bk[e], L, pre, ks) & ~SK_ID_MASK) | e : ~0ull;
     }
-    sk_bitonic_regs<EPT, 1, 0>(k, d, kw, id);
+    sk_bitonic_regs<EPT, 1, 0>(k, kw);
+    __syncthreads();  // (the last cross-wave stage's reads of kw are done)
 #pragma unroll
     for (int u = 0; u < EPT; ++u) {
         const uint32_t e = w * 64 * EPT + (uint32_t)u * 64 + l;
         if (e < n) {
-            kw[e] = k[u];
-            id[e] = (uint16_t)d[u];
+            kw[e] = k[u] & ~SK_ID_MASK;
+            id[e] = (uint16_t)(k[u] & SK_ID_MASK);
         }
     }
 }
