@@ -681,9 +681,16 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_pass_b(const SElem* __restr
 // then reads no record bytes, where it used to load one window per element from a record at random
 // (~250 B of HBM lines per element). (Stored back by the bucket pass instead, the rewrite of E cost
 // 1.8 of its 8 ms at config 5, SKV_SB_DIAGK.)
+// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs, so each XCD takes a
+// contiguous range of blocks. The elements one counting workgroup placed (k_sort_pass_a: 8,192;
+// k_sort_pass_b: 4,096) own contiguous slot ranges per (super-)bucket; written from one XCD, those
+// ranges' lines are completed in one L2 instead of leaving it as partial lines from eight.
 __global__ void k_sort_scatter(const SElem* __restrict__ E, uint64_t n, const uint64_t* __restrict__ bs,
                                const uint64_t* __restrict__ start, const uint32_t* __restrict__ Lb, SElem* out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nb = gridDim.x, bid = blockIdx.x;
+    const uint32_t xcd = bid & 7, qn = nb >> 3, rn = nb & 7;
+    const uint32_t blk = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
+    const uint64_t i = (uint64_t)blk * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t v = bs[i];
     SElem e = E[i];
