@@ -405,7 +405,16 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         while (chunk < 65536 && job.in_bytes / (2 * chunk) >= (1ull << 16)) chunk *= 2;
     auto n_chunks_of = [chunk](uint64_t len) { return len >= 2 ? (uint32_t)((len - 1 + chunk - 1) / chunk) : 0u; };
     uint64_t n_chunks = 0;
-    {  // blocks of streams (rank order) on host threads: runs and chunks before each block, then fill
+    // one run per stream in a monotone seq_no order, past the splitter merge's fan-in (config 5's
+    // shape, the device-table calls below): the run table is built on the device (k_run_info) from
+    // the caller-order pointer / length arrays, and the host table only if a host path needs it
+    const char* hre = getenv("SKV_HOST_RUNS");  // 1: the host run table always
+    const bool runs_dev = k > (uint32_t)TILE_TARGET / 2 && job.one_run_each && job.caller_order != 0 && !job.scan &&
+                          !job.search && !job.batch && !job.part && !use_span && !getenv("SKV_HOST_TABLES") &&
+                          !(hre && hre[0] == '1');
+    bool host_runs_built = false;
+    auto build_host_runs = [&]() {  // blocks of streams (rank order) on host threads: runs and chunks before each block, then fill
+        runs.resize(job.run_ptr.size());
         const unsigned nb = par_nblocks(k);
         std::vector<uint64_t> rb(nb + 1, 0), cb(nb + 1, 0);
         par_run(k, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
@@ -439,9 +448,22 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             }
         });
         n_chunks = cb[nb];
+        stream_first_run[k] = (uint32_t)runs.size();
+        host_runs_built = true;
+    };
+    const uint32_t n_runs = (uint32_t)job.run_ptr.size();
+    if (runs_dev) {  // chunk count only (8 MB of lengths)
+        const unsigned nb = par_nblocks(n_runs);
+        std::vector<uint64_t> cb(nb, 0);
+        par_run(n_runs, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+            uint64_t nc = 0;
+            for (uint64_t r = lo; r < hi; ++r) nc += n_chunks_of(job.run_len[r]);
+            cb[b] = nc;
+        });
+        for (uint64_t c : cb) n_chunks += c;
+    } else {
+        build_host_runs();
     }
-    stream_first_run[k] = (uint32_t)runs.size();
-    const uint32_t n_runs = (uint32_t)runs.size();
     htrace("run table built");
 
     RunInfo* d_runs = dbuf<RunInfo>(ctx, "runs", n_runs);
@@ -459,7 +481,18 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     RunSummary* d_sum = dbuf<RunSummary>(ctx, "run_sum", n_runs);
     htrace("buffers");
 
-    h2d_up(ctx, d_runs, runs.data(), n_runs * sizeof(RunInfo));
+    if (runs_dev) {
+        uint64_t* d_ptr_in = dbuf<uint64_t>(ctx, "run_ptr_in", n_runs);
+        uint64_t* d_len_in = dbuf<uint64_t>(ctx, "run_len_in", n_runs);
+        uint64_t* d_nch = dbuf<uint64_t>(ctx, "run_nch", n_runs);
+        uint64_t* d_cbase = dbuf<uint64_t>(ctx, "run_cbase", n_runs + 1);
+        h2d_up(ctx, d_ptr_in, job.run_ptr.data(), (size_t)n_runs * 8);
+        h2d_up(ctx, d_len_in, job.run_len.data(), (size_t)n_runs * 8);
+        uint64_t* d_tmp = dbuf<uint64_t>(ctx, "run_info_scan", scan_tmp_words(n_runs) + 64);
+        launch_run_info(st, d_ptr_in, d_len_in, n_runs, job.caller_order < 0, chunk, d_nch, d_cbase, d_tmp, d_runs);
+    } else {
+        h2d_up(ctx, d_runs, runs.data(), n_runs * sizeof(RunInfo));
+    }
     htrace("runs uploaded");
     RunFmt* d_fmt = dbuf<RunFmt>(ctx, "run_fmt", n_runs);
     uint32_t* d_broken = dbuf<uint32_t>(ctx, "run_broken", n_runs);
@@ -493,6 +526,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     uint32_t hflags[4];
     // per stream (rank order): base index, valid record count n_s and the first error
     auto stream_tables = [&]() {  // blocks of streams on host threads (10^6-stream calls)
+        if (!host_runs_built) build_host_runs();  // (a device-built run table: its host copy, same content)
         const unsigned nb = par_nblocks(k);
         std::vector<uint8_t> blk_err(nb, 0);
         const uint64_t acc = par_scan(

@@ -404,7 +404,7 @@ int build_job_impl(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t
     struct Blk {
         uint64_t runs = 0, bytes = 0, bad = ~0ull;
         uint32_t bad_run = ~0u;
-        bool asc = true, desc = true;
+        bool asc = true, desc = true, one = true;
     };
     std::vector<Blk> B(nb);
     par_run(n, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
@@ -424,13 +424,14 @@ int build_job_impl(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t
                 K.bytes += s.run_lens[r];
             }
             K.runs += s.n_runs;
+            K.one = K.one && s.n_runs == 1;
             if (i > 0) {
                 K.asc = K.asc && streams[i - 1].seq_no < s.seq_no;
                 K.desc = K.desc && streams[i - 1].seq_no > s.seq_no;
             }
         }
     });
-    bool asc = true, desc = true;
+    bool asc = true, desc = true, one = true;
     uint64_t total_runs = 0;
     for (unsigned b = 0; b < nb; ++b) {  // the first invalid stream in the caller's order
         if (B[b].bad != ~0ull) {
@@ -444,7 +445,10 @@ int build_job_impl(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t
         job.in_bytes += B[b].bytes;
         asc = asc && B[b].asc;
         desc = desc && B[b].desc;
+        one = one && B[b].one;
     }
+    job.one_run_each = one;
+    job.caller_order = desc ? 1 : (asc ? -1 : 0);
     // pass 2: the tables, streams already in rank order (seq_no descending) when the caller's
     // order is either strict one; resize keeps a lent table's entries (no zero fill per call)
     job.run_ptr.resize(total_runs);

@@ -254,6 +254,10 @@ int derr_to_api(uint32_t e, std::string& msg);
 struct Job {
     std::vector<InStream> ranked;  // streams sorted by seq_no descending
     std::vector<uint64_t> run_ptr, run_len;  // member runs, caller order (flat: 10^6-stream jobs)
+    // build_job's view of the caller's table: every stream holds exactly one run, and its order by
+    // seq_no (1: strictly descending = rank order, -1: strictly ascending = reversed, 0: sorted here)
+    bool one_run_each = false;
+    int caller_order = 0;
     uint64_t max_run_size = 0;
     uint32_t flags = 0;
     uint64_t in_bytes = 0;

@@ -1516,6 +1516,39 @@ void launch_run_tables(hipStream_t s, const RunInfo* runs, const RunFmt* fmt, ui
     if (n_runs) k_run_tables<<<(n_runs + 255) / 256, 256, 0, s>>>(runs, fmt, n_runs, cnt, flags);
 }
 
+// The run table of a call whose streams hold one run each, in a monotone seq_no order, built on the
+// device from the caller-order pointer / length arrays (the host's pass over 10^6 runs and the
+// 32-byte-per-run upload are skipped): rank r is caller stream r (descending seq_no) or n - 1 - r
+// (ascending). Two launches: the chunk counts (scanned into chunk bases between them), then the
+// entries.
+__global__ void k_run_info(const uint64_t* __restrict__ ptr, const uint64_t* __restrict__ len, uint32_t n,
+                           bool reversed, uint64_t chunk, const uint64_t* __restrict__ chunk_base, uint64_t* nch,
+                           RunInfo* runs) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint64_t c = reversed ? n - 1 - r : r;
+    const uint64_t l = len[c];
+    const uint64_t nc = l >= 2 ? (l - 1 + chunk - 1) / chunk : 0;
+    if (!chunk_base) {
+        nch[r] = nc;
+        return;
+    }
+    RunInfo R;
+    R.ptr = ptr[c];
+    R.len = l;
+    R.chunk_base = chunk_base[r];
+    R.n_chunks = (uint32_t)nc;
+    R.stream = (uint32_t)r;
+    runs[r] = R;
+}
+void launch_run_info(hipStream_t s, const uint64_t* ptr, const uint64_t* len, uint32_t n, bool reversed, uint64_t chunk,
+                     uint64_t* nch, uint64_t* chunk_base, uint64_t* scan_tmp, RunInfo* runs) {
+    if (!n) return;
+    k_run_info<<<(n + 255) / 256, 256, 0, s>>>(ptr, len, n, reversed, chunk, nullptr, nch, runs);
+    launch_scan(s, nch, n, chunk_base, scan_tmp);
+    k_run_info<<<(n + 255) / 256, 256, 0, s>>>(ptr, len, n, reversed, chunk, chunk_base, nch, runs);
+}
+
 // largest e in [lo, hi] with P[e] <= v, given P[lo] <= v (64-ary search, exact). Not inlined: k_chain
 // unrolls its resolve step CH_D times, and 32 inlined copies of this rare fallback made the kernel
 // ~50 KB of straight-line code, streamed through the instruction cache on every round.

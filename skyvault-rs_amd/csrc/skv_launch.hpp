@@ -192,6 +192,9 @@ void launch_ingest_slices(hipStream_t, const IngestSlice* slices, uint64_t n, ui
 enum : uint32_t { RT_NOT_FIXED = 0, RT_NOT_UNIFORM = 1, RT_ANY_FIXED = 2, RT_BODYLESS = 3 };
 void launch_run_tables(hipStream_t, const RunInfo* runs, const RunFmt* fmt, uint32_t n_runs, uint64_t* cnt,
                        uint32_t* flags);
+// the run table on the device for one-run streams in monotone seq_no order (chunk_base: n + 1 entries)
+void launch_run_info(hipStream_t, const uint64_t* ptr, const uint64_t* len, uint32_t n, bool reversed, uint64_t chunk,
+                     uint64_t* nch, uint64_t* chunk_base, uint64_t* scan_tmp, RunInfo* runs);
 #if SKV_FX_DIAG == 4
 void launch_fx_keys(hipStream_t, const FxArgs& A, uint64_t R, ulong2* keys);
 #endif
