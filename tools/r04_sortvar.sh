@@ -10,10 +10,11 @@ rc=$?
 tail -2 "$O/sortvar_tests.log"
 [ $rc -ne 0 ] && { grep -E "^(FAILED|ERROR)" "$O/sortvar_tests.log" | head -20; exit $rc; }
 for v in ${VARIANTS:-base one}; do
-  lib=skyvault-rs_amd/skv/libskv.so two=1
-  # one: the base library with the one-pass bucket search (SKV_SORT_TWO_PASS=0)
-  case $v in base) ;; one) two=0 ;; *) lib=skyvault-rs_amd/skv/variants/libskv_$v.so ;; esac
-  SKV_SORT_TWO_PASS=$two SKV_LIB=$lib timeout -k 10 300 python bench.py --config 5 --steps 5 --warmup 1 --no-cpu-baseline --no-host-path \
+  lib=skyvault-rs_amd/skv/libskv.so two=1 hr=0
+  # one: the base library with the one-pass bucket search (SKV_SORT_TWO_PASS=0); hostruns: with the
+  # host-built run table (SKV_HOST_RUNS=1)
+  case $v in base|base2) ;; one) two=0 ;; hostruns|hostruns2) hr=1 ;; *) lib=skyvault-rs_amd/skv/variants/libskv_$v.so ;; esac
+  SKV_HOST_RUNS=$hr SKV_SORT_TWO_PASS=$two SKV_LIB=$lib timeout -k 10 300 python bench.py --config 5 --steps 5 --warmup 1 --no-cpu-baseline --no-host-path \
     > "$O/sortvar_$v.log" 2>&1 || { echo "variant $v failed"; tail -5 "$O/sortvar_$v.log"; exit 1; }
   echo "$v $(grep -o '"ms_per_step": [0-9.]*' $O/sortvar_$v.log) $(grep -o '"phases_ms": {[^}]*' $O/sortvar_$v.log)"
 done
