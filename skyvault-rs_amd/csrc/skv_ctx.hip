@@ -399,14 +399,21 @@ int build_job_impl(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t
     job.max_run_size = max_run_size;
     job.flags = flags;
     // pass 1 (blocks of streams on host threads): NULL checks, run counts, input bytes, and
-    // whether the caller's order is strictly ascending / descending by seq_no
+    // whether the caller's order is strictly ascending / descending by seq_no. A block of one-run
+    // streams in a strict order also writes its tables right away, placed as that order would put
+    // them (spec = -1 ascending / 1 descending); pass 2 then redoes only the blocks whose guess the
+    // whole table's order contradicts (a 10^6-stream WAL flush skips pass 2 entirely).
     const unsigned nb = par_nblocks(n);
     struct Blk {
         uint64_t runs = 0, bytes = 0, bad = ~0ull;
         uint32_t bad_run = ~0u;
         bool asc = true, desc = true, one = true;
+        int spec = 0;
     };
     std::vector<Blk> B(nb);
+    job.run_ptr.resize(n);  // (the one-run size; pass 2 resizes otherwise)
+    job.run_len.resize(n);
+    job.ranked.resize(n);
     par_run(n, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
         Blk& K = B[b];
         for (uint64_t i = lo; i < hi; ++i) {
@@ -430,6 +437,19 @@ int build_job_impl(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t
                 K.desc = K.desc && streams[i - 1].seq_no > s.seq_no;
             }
         }
+        const int dir = K.asc && !K.desc ? -1 : (K.desc && !K.asc ? 1 : 0);
+        if (!K.one || !dir) return;
+        for (uint64_t i = lo; i < hi; ++i) {  // (the block's entries are in cache)
+            const skv_stream& s = streams[i];
+            job.run_ptr[i] = (uint64_t)(uintptr_t)s.runs[0];
+            job.run_len[i] = s.run_lens[0];
+            InStream& S = job.ranked[dir < 0 ? n - 1 - i : i];
+            S.seq = s.seq_no;
+            S.vec_idx = (uint32_t)i;
+            S.n_runs = 1;
+            S.first = i;
+        }
+        K.spec = dir;
     });
     bool asc = true, desc = true, one = true;
     uint64_t total_runs = 0;
@@ -453,8 +473,9 @@ int build_job_impl(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t
     // order is either strict one; resize keeps a lent table's entries (no zero fill per call)
     job.run_ptr.resize(total_runs);
     job.run_len.resize(total_runs);
-    job.ranked.resize(n);
+    const int gdir = asc ? -1 : (desc ? 1 : 0);  // (pass 2's placement below)
     par_run(n, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+        if (one && gdir && B[b].spec == gdir) return;  // written by pass 1
         uint64_t at = B[b].runs;
         for (uint64_t i = lo; i < hi; ++i) {
             const skv_stream& s = streams[i];
