@@ -211,6 +211,27 @@ def test_bucket_levels_at_small_sizes(dev, monkeypatch, nt, two, gmax):
     _check(dev, gen.config3(n_streams=1700, run_bytes=6000, vsize=16), 256 * 1024, _abi.SKV_DROP_TOMBSTONES)
 
 
+@pytest.mark.parametrize("order", ["ascending", "descending", "shuffled"])
+def test_wide_one_run_streams_by_caller_order(dev, order):
+    """70,000 one-run streams (past build_job's 65,536-stream threshold for host-thread blocks):
+    in a strict seq_no order every block writes its tables in pass 1 and the run table is built on
+    the device (k_run_info, reversed for an ascending caller order); shuffled, pass 2 and the host
+    run table do it. Same output and stats as the oracle either way."""
+    r = random.Random(41)
+    n = 70_000
+    streams = []
+    for s in range(n):
+        keys = sorted({f"{r.randrange(8)}.{r.randrange(10 ** 9):09d}" for _ in range(2)})
+        ops = [fmt.put(k, bytes([s & 255, 7])) if r.random() < 0.9 else fmt.delete(k) for k in keys]
+        streams.append((s + 1, [fmt.encode_run(ops)]))
+    if order == "descending":
+        streams.reverse()
+    elif order == "shuffled":
+        r.shuffle(streams)
+    _check(dev, streams, 1 << 20, _abi.SKV_SPLIT_BY_TABLE)
+    _check(dev, streams, 1 << 20, 0)
+
+
 def test_fan_in_errors_surface_like_the_reference(dev):
     """A corrupt or unsorted stream among 1600: the error is resolved before the sort."""
     r = random.Random(3)
