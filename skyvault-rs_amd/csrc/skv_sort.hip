@@ -463,8 +463,15 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restr
 //      atomic per (chunk, bucket); the second scatter then forms the buckets.
 // The bucket sort compares windows from cp[a] (every key of the bucket shares them) and takes its
 // 8-byte sort words from the bucket's own prefix L[b] >= cp[a] on (k_sort_tile's ks).
-constexpr int SA_PER = 32;            // pass A: elements per thread (an LDS slot each, 14 bits)
-constexpr int SBB_PER = 16;           // pass B: elements per thread
+#ifndef SKV_SA_PER
+#define SKV_SA_PER 32
+#endif
+#ifndef SKV_SBB_PER
+#define SKV_SBB_PER 16
+#endif
+constexpr int SA_PER = SKV_SA_PER;    // pass A: elements per thread (workgroup slots < 2^14)
+constexpr int SBB_PER = SKV_SBB_PER;  // pass B: elements per thread (workgroup slots < 2^13)
+static_assert(SA_PER * SB_THREADS <= (1 << 14) && SBB_PER * SB_THREADS <= (1 << 13), "slot bits");
 constexpr uint32_t SBB_LW = 1024;     // pass B: group windows in LDS (16 KB), also its bucket bins
 constexpr uint32_t SBB_GMAX = 16;     // pass B: groups a chunk may span on the LDS path
 
