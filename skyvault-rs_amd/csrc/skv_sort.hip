@@ -464,10 +464,10 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restr
 // The bucket sort compares windows from cp[a] (every key of the bucket shares them) and takes its
 // 8-byte sort words from the bucket's own prefix L[b] >= cp[a] on (k_sort_tile's ks).
 #ifndef SKV_SA_PER
-#define SKV_SA_PER 32
+#define SKV_SA_PER 16
 #endif
 #ifndef SKV_SBB_PER
-#define SKV_SBB_PER 16
+#define SKV_SBB_PER 8
 #endif
 constexpr int SA_PER = SKV_SA_PER;    // pass A: elements per thread (workgroup slots < 2^14)
 constexpr int SBB_PER = SKV_SBB_PER;  // pass B: elements per thread (workgroup slots < 2^13)

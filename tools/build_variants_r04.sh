@@ -15,7 +15,7 @@
 #   sortlds  record-sort bucket network in LDS (the round-3 form) instead of registers
 #   sbilp2   record-sort bucket pass searching 2 elements per thread at once (fewer registers)
 #   sbdiag   record-sort bucket pass timing diagnostics: k_sort_bucket<D> launches with parts skipped
-#   sa16, sa64, sbb8, sbb32  two-pass bucketing: elements per thread of pass A / pass B
+#   sa8, sa32, sbb4, sbb16  two-pass bucketing: elements per thread of pass A / pass B (default 16 / 8)
 set -eu
 cd "$(dirname "$0")/../skyvault-rs_amd"
 J=${J:-8}
@@ -40,10 +40,10 @@ declare -A F=(
   [sortlds]="-DSKV_SORT_REGS=0"
   [sbilp2]="-DSKV_SB_ILP=2"
   [sbdiag]="-DSKV_SB_DIAGK=1"
-  [sa16]="-DSKV_SA_PER=16"
-  [sa64]="-DSKV_SA_PER=64"
-  [sbb8]="-DSKV_SBB_PER=8"
-  [sbb32]="-DSKV_SBB_PER=32"
+  [sa8]="-DSKV_SA_PER=8"
+  [sa32]="-DSKV_SA_PER=32"
+  [sbb4]="-DSKV_SBB_PER=4"
+  [sbb16]="-DSKV_SBB_PER=16"
 )
 for tag in ${TAGS:-${!F[@]}}; do
   make -s -j"$J" variant TAG="$tag" VFLAGS="${F[$tag]}"
