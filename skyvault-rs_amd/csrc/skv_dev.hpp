@@ -252,7 +252,10 @@ struct SElem {
 constexpr int SORT_CAP = 2048;           // elements a bucket sorts in LDS
 constexpr int SORT_THREADS = 256;
 constexpr uint64_t SORT_EVERY = 48;      // one sample per SORT_EVERY elements
-constexpr uint64_t SORT_OV = 16;         // samples per bucket (bucket target SORT_EVERY * SORT_OV = 768)
+#ifndef SKV_SORT_OV
+#define SKV_SORT_OV 16
+#endif
+constexpr uint64_t SORT_OV = SKV_SORT_OV;  // samples per bucket (bucket target SORT_EVERY * SORT_OV = 768)
 
 // Batched run lookups (skv_search.hip): same layout and codes as skv_lookup / SKV_LOOKUP_* /
 // SKV_PANIC_* in include/skv.h

@@ -16,6 +16,7 @@
 #   sbilp2   record-sort bucket pass searching 2 elements per thread at once (fewer registers)
 #   sbdiag   record-sort bucket pass timing diagnostics: k_sort_bucket<D> launches with parts skipped
 #   sa8, sa32, sbb4, sbb16  two-pass bucketing: elements per thread of pass A / pass B (default 16 / 8)
+#   ov12, ov20  record sort: samples per bucket (default 16: 768-element buckets)
 set -eu
 cd "$(dirname "$0")/../skyvault-rs_amd"
 J=${J:-8}
@@ -44,6 +45,8 @@ declare -A F=(
   [sa32]="-DSKV_SA_PER=32"
   [sbb4]="-DSKV_SBB_PER=4"
   [sbb16]="-DSKV_SBB_PER=16"
+  [ov12]="-DSKV_SORT_OV=12"
+  [ov20]="-DSKV_SORT_OV=20"
 )
 for tag in ${TAGS:-${!F[@]}}; do
   make -s -j"$J" variant TAG="$tag" VFLAGS="${F[$tag]}"
