@@ -311,17 +311,9 @@ SElem* sort_elems(skv_ctx* ctx, SElem* E, SElem* T, uint64_t n, int depth, uint6
         launch_sort_scatter(st, E, n, bs, sstart, sort_super_prefix(split_buf, Tb - 1), T);
         launch_sort_pass_b(st, T, n, sstart, Tb - 1, split_buf, cnt, bs);
         launch_scan(st, cnt, Tb, start, scan_tmp);
-        const char* ie = getenv("SKV_SORT_INDEX");  // 0: the second scatter moves the elements
-        if (ie && ie[0] == '0') {
-            launch_sort_scatter(st, T, n, bs, start, nullptr, E);
-            launch_sort_tile(st, E, start, L, Tb, T, newkey, true, split_buf, top2);
-            return T;
-        }
-        // the buckets as an index into the super-bucket order; the bucket sort gathers through it
-        uint32_t* ix = dbuf<uint32_t>(ctx, "sort_ix", n);
-        launch_sort_index(st, n, bs, start, ix);
-        launch_sort_tile(st, T, start, L, Tb, E, newkey, true, split_buf, top2, ix, dbuf<SElem>(ctx, "sort_gs", n));
-        return E;
+        launch_sort_scatter(st, T, n, bs, start, nullptr, E);
+        launch_sort_tile(st, E, start, L, Tb, T, newkey, true, split_buf, top2);
+        return T;
     }
     launch_sort_bucket(st, E, n, Ss, SORT_OV, Tb - 1, split_buf, cnt, bs, pre);
     launch_scan(st, cnt, Tb, start, scan_tmp);

@@ -163,9 +163,7 @@ void launch_sort_scatter(hipStream_t, const SElem* E, uint64_t n, const uint64_t
                          const uint32_t* Lb, SElem* out);
 void launch_sort_tile(hipStream_t, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out,
                       uint64_t* newkey, bool pre,
-                      const void* split_buf = nullptr, uint64_t two_pass_top = 0, const uint32_t* ix = nullptr,
-                      SElem* gs = nullptr);
-void launch_sort_index(hipStream_t, uint64_t n, const uint64_t* bs, const uint64_t* start, uint32_t* ix);
+                      const void* split_buf = nullptr, uint64_t two_pass_top = 0);
 // two-pass bucketing at depth 0 (skv_sort.hip): top (the group size) when it applies, else 0
 uint64_t sort_two_pass_top(uint64_t nsp);
 uint64_t sort_two_pass_groups(uint64_t nsp);  // super-buckets

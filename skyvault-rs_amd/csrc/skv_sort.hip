@@ -719,14 +719,7 @@ struct SKey {
     uint64_t wh, wl;
     uint32_t klen, pos;
 };
-// A bucket's elements: contiguous (p[i]), or in the two-pass order through the bucket's slice of
-// the index written in place of the second scatter (p[ix[i]], p = the super-bucket order)
-struct BkRef {
-    const SElem* p;
-    const uint32_t* ix;
-    __device__ __forceinline__ SElem operator[](uint32_t i) const { return ix ? p[ix[i]] : p[i]; }
-};
-__device__ __forceinline__ bool sk_wless(const SKey& a, const SKey& b, const BkRef& bk, uint32_t ia, uint32_t ib,
+__device__ __forceinline__ bool sk_wless(const SKey& a, const SKey& b, const SElem* bk, uint32_t ia, uint32_t ib,
                                          uint32_t L) {
     if (a.wh != b.wh) return a.wh < b.wh;
     if (a.wl != b.wl) return a.wl < b.wl;
@@ -778,7 +771,7 @@ __device__ void sk_sort_global(SElem* bk, uint64_t n, uint32_t L, bool pre, SEle
                 if (c < n) {
                     if (pre) {
                         const SKey kc = sk_skey(bk[c], L, true), ka = sk_skey(bk[a], L, true);
-                        sw = sk_wless(kc, ka, BkRef{bk, nullptr}, (uint32_t)c, (uint32_t)a, L);
+                        sw = sk_wless(kc, ka, bk, (uint32_t)c, (uint32_t)a, L);
                     } else {
                         sw = sk_less(bk[c], bk[a]);
                     }
@@ -807,7 +800,7 @@ __device__ void sk_sort_global(SElem* bk, uint64_t n, uint32_t L, bool pre, SEle
 }
 
 // full bucket order of elements x and y (indices into the bucket)
-__device__ __forceinline__ bool sk_eless(const BkRef& bk, uint32_t x, uint32_t y, uint32_t L, bool pre) {
+__device__ __forceinline__ bool sk_eless(const SElem* bk, uint32_t x, uint32_t y, uint32_t L, bool pre) {
     return sk_wless(sk_skey(bk[x], L, pre), sk_skey(bk[y], L, pre), bk, x, y, L);
 }
 
@@ -905,7 +898,7 @@ __device__ __forceinline__ uint64_t sk_kw(const SElem& e, uint32_t L, bool pre, 
 }
 
 template <int EPT>
-__device__ void sk_sort_regs(const BkRef& bk, uint32_t n, uint32_t L, bool pre, uint32_t ks, uint64_t* kw,
+__device__ void sk_sort_regs(const SElem* bk, uint32_t n, uint32_t L, bool pre, uint32_t ks, uint64_t* kw,
                              uint16_t* id) {
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint64_t k[EPT];  // the sort word's top 53 bits | element id (runs of equal 53-bit words go to
@@ -940,8 +933,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
                                                             const uint32_t* __restrict__ Lb, uint64_t Tb,
                                                             SElem* out, uint64_t* newkey, bool pre,
                                                             const SSplit* __restrict__ sp,
-                                                            const uint32_t* __restrict__ Lsup, uint64_t top,
-                                                            const uint32_t* __restrict__ ix, SElem* gs) {
+                                                            const uint32_t* __restrict__ Lsup, uint64_t top) {
     __shared__ uint64_t kw[SORT_CAP];
     __shared__ uint16_t id[SORT_CAP];
     __shared__ uint32_t s_long;
@@ -953,22 +945,13 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
     const uint32_t Lt = Lb ? Lb[b] : 0u;
     const uint32_t L = Lsup ? Lsup[b / top] : Lt;
     const uint32_t ks = Lt > L ? Lt - L : 0u;
-    // ix (two-pass): the bucket's elements are in[ix[s0 + i]]; the global-memory sort below works on
-    // a contiguous copy in gs
-    const BkRef bk{ix ? in : in + s0, ix ? ix + s0 : nullptr};
-    auto dense = [&]() -> SElem* {
-        if (!ix) return in + s0;
-        for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) gs[s0 + i] = in[ix[s0 + i]];
-        __threadfence_block();
-        __syncthreads();
-        return gs + s0;
-    };
+    SElem* bk = in + s0;
     // sp (the records' level, pre): the output elements get their keys' true prefixes back (the WAL
     // stage reads table ids from them). L > 0 only between two splitters: splitter b bounds bucket b.
     const SSplit* spb = sp && L ? sp + b : nullptr;
     if (n == 0) return;
     if (n > (uint64_t)SORT_CAP) {
-        sk_sort_global(dense(), n, L, pre, out, s0, newkey, spb);
+        sk_sort_global(bk, n, L, pre, out, s0, newkey, spb);
         return;
     }
     const uint32_t n32 = (uint32_t)n;
@@ -1057,7 +1040,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
     SPROF_T(q3);
     SPROF_ADD(6, q2, q3);
     if (s_long) {  // uniform: every thread read it after the barrier
-        sk_sort_global(dense(), n, L, pre, out, s0, newkey, spb);
+        sk_sort_global(bk, n, L, pre, out, s0, newkey, spb);
         return;
     }
     for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
@@ -1199,25 +1182,11 @@ void launch_sort_scatter(hipStream_t s, const SElem* E, uint64_t n, const uint64
     if (n) k_sort_scatter<<<sk_blocks(n), 256, 0, s>>>(E, n, bs, start, Lb, out);
 }
 void launch_sort_tile(hipStream_t s, SElem* in, const uint64_t* start, const uint32_t* L, uint64_t Tb, SElem* out,
-                      uint64_t* newkey, bool pre, const void* split_buf, uint64_t two_pass_top, const uint32_t* ix,
-                      SElem* gs) {
+                      uint64_t* newkey, bool pre, const void* split_buf, uint64_t two_pass_top) {
     const uint32_t* Lsup = two_pass_top ? split_layout((void*)split_buf, Tb - 1).gcp : nullptr;
     if (Tb)
         k_sort_tile<<<(unsigned)Tb, SORT_THREADS, 0, s>>>(in, start, L, Tb, out, newkey, pre,
-                                                         (const SSplit*)split_buf, Lsup, two_pass_top, ix, gs);
-}
-
-// the second two-pass scatter as an index: ix[start[b] + slot] = the element's position in the
-// super-bucket order (4 bytes written where the scatter moved 32; k_sort_tile gathers)
-__global__ void k_sort_index(uint64_t n, const uint64_t* __restrict__ bs, const uint64_t* __restrict__ start,
-                             uint32_t* ix) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t v = bs[i];
-    ix[start[v >> 32] + (v & 0xFFFFFFFFull)] = (uint32_t)i;
-}
-void launch_sort_index(hipStream_t s, uint64_t n, const uint64_t* bs, const uint64_t* start, uint32_t* ix) {
-    if (n) k_sort_index<<<sk_blocks(n), 256, 0, s>>>(n, bs, start, ix);
+                                                         (const SSplit*)split_buf, Lsup, two_pass_top);
 }
 
 uint64_t sort_two_pass_top(uint64_t nsp) {
