@@ -8,11 +8,13 @@ O="$R/gpurun_out/r04/kvar"
 mkdir -p "$O"
 export TMPDIR=/tmp
 C=${CONFIG:-5}
+# a variant is a library tag (skv/variants/libskv_<tag>.so), base / base<N> (the default library), or
+# NAME=VALUE (the default library with that environment variable)
 for v in ${VARIANTS:-base}; do
-  lib="$R/skyvault-rs_amd/skv/libskv.so"
-  [ "${v%[0-9]}" != base ] && [ "$v" != base ] && lib="$R/skyvault-rs_amd/skv/variants/libskv_${v}.so"
+  lib="$R/skyvault-rs_amd/skv/libskv.so" ev="SKV_KVAR_NONE=1"
+  case $v in base|base[0-9]) ;; *=*) ev="$v" ;; *) lib="$R/skyvault-rs_amd/skv/variants/libskv_${v}.so" ;; esac
   cd /tmp
-  SKV_LIB="$lib" timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/p_$v" -o run -- \
+  env "$ev" SKV_LIB="$lib" timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/p_$v" -o run -- \
     python3 "$R/bench.py" --config $C --steps 3 --warmup 1 --no-cpu-baseline --no-host-path > "$O/b_$v.log" 2>&1 \
     || { echo "variant $v failed"; tail -3 "$O/b_$v.log"; exit 1; }
   cd "$R"
