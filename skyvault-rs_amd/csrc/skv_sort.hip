@@ -23,8 +23,6 @@
 // key, Delete filter, dense output arrays (skv_compact.hip).
 #include "skv_launch.hpp"
 
-#include <type_traits>
-
 namespace skv {
 
 // index of the first differing byte among the first n bytes (n if none)
@@ -811,9 +809,6 @@ constexpr uint32_t SORT_TIE_MAX = 32;  // longest run of equal first words sorte
 #ifndef SKV_SORT_REGS
 #define SKV_SORT_REGS 1  // 1: the bucket's bitonic network in registers (shuffles / LDS across waves)
 #endif
-#ifndef SKV_SORT_REGOUT
-#define SKV_SORT_REGOUT 1  // 1: the loaded elements stay in registers and are written from there
-#endif
 // One compare-exchange of the network on packed sort words: the first word's top 53 bits and the
 // element id (11 bits) in one 64-bit value, so a pair moves with one 64-bit shuffle and compares
 // once (ids are distinct; padding is ~0). The lower index keeps the smaller word.
@@ -926,32 +921,6 @@ __device__ void sk_sort_regs(const SElem* bk, uint32_t n, uint32_t L, bool pre, 
 }
 
 
-// runs of equal sort words into the full order (window, bytes past it, key length, record index) by
-// the thread holding the run's first position; a run longer than SORT_TIE_MAX sets *s_long
-__device__ __forceinline__ void sk_ties(const SElem* bk, uint32_t n32, uint32_t L, bool pre, const uint64_t* kw,
-                                        uint16_t* id, uint32_t* s_long) {
-    for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
-        const uint64_t w = kw[i];
-        if ((i == 0 || kw[i - 1] != w) && i + 1 < n32 && kw[i + 1] == w) {
-            uint32_t e = i + 2;
-            while (e < n32 && kw[e] == w && e - i <= SORT_TIE_MAX) ++e;
-            if (e - i > SORT_TIE_MAX) {
-                *s_long = 1;
-            } else {
-                for (uint32_t t = i + 1; t < e; ++t) {
-                    const uint32_t x = id[t];
-                    uint32_t j = t;
-                    while (j > i && sk_eless(bk, x, id[j - 1], L, pre)) {
-                        id[j] = id[j - 1];
-                        --j;
-                    }
-                    id[j] = (uint16_t)x;
-                }
-            }
-        }
-    }
-}
-
 // One workgroup per bucket: in[start[b], start[b+1]) sorted into out[...]. The bitonic network
 // runs on the first 8 window bytes (kw) and the element ids only, 10 bytes per element where the
 // full window, length and index took 26: the sort is bound by LDS traffic. Runs of equal kw are
@@ -967,9 +936,6 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
                                                             const uint32_t* __restrict__ Lsup, uint64_t top) {
     __shared__ uint64_t kw[SORT_CAP];
     __shared__ uint16_t id[SORT_CAP];
-#if SKV_SORT_REGOUT
-    __shared__ uint16_t posof[SORT_CAP];
-#endif
     __shared__ uint32_t s_long;
     const uint64_t b = blockIdx.x;
     if (b >= Tb) return;
@@ -991,70 +957,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
     const uint32_t n32 = (uint32_t)n;
     SPROF_T(q0);
     if (threadIdx.x == 0) s_long = 0;
-#if SKV_SORT_REGS && SKV_SORT_REGOUT
-    // each thread keeps the elements it loaded in registers and writes them to their sorted positions
-    // (posof, LDS) itself: the output pass reads no element from memory a second time
-    static_assert(SORT_THREADS == 256 && SORT_CAP == 2048, "register network: 256 threads, <= 8 elements each");
-    auto body = [&](auto ept) -> bool {
-        constexpr int EPT = decltype(ept)::value;
-        const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
-        SElem el[EPT];
-        uint64_t k[EPT];
-#pragma unroll
-        for (int u = 0; u < EPT; ++u) {
-            const uint32_t e = w * 64 * EPT + (uint32_t)u * 64 + l;
-            k[u] = ~0ull;
-            if (e < n32) {
-                el[u] = bk[e];
-                k[u] = (sk_kw(el[u], L, pre, ks) & ~SK_ID_MASK) | e;
-            }
-        }
-        sk_bitonic_regs<EPT, 1, 0>(k, kw);
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < EPT; ++u) {
-            const uint32_t e = w * 64 * EPT + (uint32_t)u * 64 + l;
-            if (e < n32) {
-                kw[e] = k[u] & ~SK_ID_MASK;
-                id[e] = (uint16_t)(k[u] & SK_ID_MASK);
-            }
-        }
-        __syncthreads();
-        sk_ties(bk, n32, L, pre, kw, id, &s_long);
-        __syncthreads();
-        if (s_long) return false;
-        for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) posof[id[i]] = (uint16_t)i;
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < EPT; ++u) {
-            const uint32_t e = w * 64 * EPT + (uint32_t)u * 64 + l;
-            if (e < n32) {
-                SElem o = el[u];
-                if (pre && spb) sk_restore(o, L, spb);
-                out[s0 + posof[e]] = o;
-            }
-        }
-        return true;
-    };
-    bool done;
-    if (n32 <= 256) done = body(std::integral_constant<int, 1>{});
-    else if (n32 <= 512) done = body(std::integral_constant<int, 2>{});
-    else if (n32 <= 1024) done = body(std::integral_constant<int, 4>{});
-    else done = body(std::integral_constant<int, 8>{});
-    if (!done) {  // uniform (s_long read after a barrier)
-        sk_sort_global(bk, n, L, pre, out, s0, newkey, spb);
-        return;
-    }
-    for (uint32_t i = threadIdx.x; newkey && i < n32; i += blockDim.x) {
-        bool nk = i == 0 || kw[i - 1] != kw[i];
-        if (!nk) {
-            const uint32_t a = id[i - 1], c = id[i];
-            nk = !sk_wsame(sk_skey(bk[a], L, pre), sk_skey(bk[c], L, pre), bk[a], bk[c], L);
-        }
-        newkey[s0 + i] = nk ? 1 : 0;
-    }
-    return;
-#elif SKV_SORT_REGS
+#if SKV_SORT_REGS
     static_assert(SORT_THREADS == 256 && SORT_CAP == 2048, "register network: 256 threads, <= 8 elements each");
     if (n32 <= 256) sk_sort_regs<1>(bk, n32, L, pre, ks, kw, id);
     else if (n32 <= 512) sk_sort_regs<2>(bk, n32, L, pre, ks, kw, id);
@@ -1112,7 +1015,27 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
     SPROF_T(q2);
     SPROF_ADD(5, q1, q2);
 #endif
-    sk_ties(bk, n32, L, pre, kw, id, &s_long);
+    // runs of equal kw into the full order
+    for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
+        const uint64_t w = kw[i];
+        if ((i == 0 || kw[i - 1] != w) && i + 1 < n32 && kw[i + 1] == w) {
+            uint32_t e = i + 2;
+            while (e < n32 && kw[e] == w && e - i <= SORT_TIE_MAX) ++e;
+            if (e - i > SORT_TIE_MAX) {
+                s_long = 1;
+            } else {
+                for (uint32_t t = i + 1; t < e; ++t) {
+                    const uint32_t x = id[t];
+                    uint32_t j = t;
+                    while (j > i && sk_eless(bk, x, id[j - 1], L, pre)) {
+                        id[j] = id[j - 1];
+                        --j;
+                    }
+                    id[j] = (uint16_t)x;
+                }
+            }
+        }
+    }
     __syncthreads();
     SPROF_T(q3);
     SPROF_ADD(6, q2, q3);

@@ -17,7 +17,6 @@
 #   sbdiag   record-sort bucket pass timing diagnostics: k_sort_bucket<D> launches with parts skipped
 #   sa8, sa32, sbb4, sbb16  two-pass bucketing: elements per thread of pass A / pass B (default 16 / 8)
 #   ov12, ov20  record sort: samples per bucket (default 16: 768-element buckets)
-#   regout0  bucket sort output read back from memory (the round-4 form before register output)
 set -eu
 cd "$(dirname "$0")/../skyvault-rs_amd"
 J=${J:-8}
@@ -48,7 +47,6 @@ declare -A F=(
   [sbb16]="-DSKV_SBB_PER=16"
   [ov12]="-DSKV_SORT_OV=12"
   [ov20]="-DSKV_SORT_OV=20"
-  [regout0]="-DSKV_SORT_REGOUT=0"
 )
 for tag in ${TAGS:-${!F[@]}}; do
   make -s -j"$J" variant TAG="$tag" VFLAGS="${F[$tag]}"
