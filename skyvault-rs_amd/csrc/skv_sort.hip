@@ -216,11 +216,13 @@ struct SSplit {
 // bucket pass, pre): bytes [0, L) are the bucket's common prefix -- its splitter's -- and bytes
 // [L, 16) the window's first 16 - L. Every key of the bucket is longer than L, so no byte of the
 // splitter's part lies past the key's end; the window is zero past it.
-__device__ __forceinline__ void sk_restore(SElem& e, uint32_t L, const SSplit* s) {
+// (shi, slo: the splitter's 16-byte prefix, read once per bucket by the caller -- read per element,
+// the loads were ordered after every output store, which may alias them)
+__device__ __forceinline__ void sk_restore(SElem& e, uint32_t L, uint64_t shi, uint64_t slo) {
     if (!L) return;
     if (L >= 16) {
-        e.hi = s->hi;
-        e.lo = s->lo;
+        e.hi = shi;
+        e.lo = slo;
         return;
     }
     const uint32_t sh = 8 * L;  // 8 .. 120: the window moves right by L bytes
@@ -228,8 +230,8 @@ __device__ __forceinline__ void sk_restore(SElem& e, uint32_t L, const SSplit* s
     const uint64_t rl = sh < 64 ? (e.lo >> sh) | (e.hi << (64 - sh)) : (e.hi >> (sh - 64));
     const uint64_t mh = sh >= 64 ? ~0ull : ~0ull << (64 - sh);
     const uint64_t ml = sh <= 64 ? 0ull : ~0ull << (128 - sh);
-    e.hi = (s->hi & mh) | rh;
-    e.lo = (s->lo & ml) | rl;
+    e.hi = (shi & mh) | rh;
+    e.lo = (slo & ml) | rl;
 }
 
 __device__ __forceinline__ void sk_ext(const uint8_t* key, uint32_t klen, uint64_t& x0, uint64_t& x1) {
@@ -786,9 +788,10 @@ __device__ void sk_sort_global(SElem* bk, uint64_t n, uint32_t L, bool pre, SEle
             __syncthreads();
         }
     }
+    const uint64_t shi = spb ? spb->hi : 0, slo = spb ? spb->lo : 0;
     for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
         SElem o = bk[i];
-        if (pre && spb) sk_restore(o, L, spb);
+        if (pre && spb) sk_restore(o, L, shi, slo);
         out[s0 + i] = o;
         if (newkey) {
             bool nk = i == 0;
@@ -929,9 +932,10 @@ __device__ void sk_sort_regs(const SElem* bk, uint32_t n, uint32_t L, bool pre, 
 // run longer than SORT_TIE_MAX sends the bucket to the global-memory sort instead.
 // The network is the ascending-comparator form (the second element of the first step of each
 // merge is mirrored), so padding past n acts as +inf and is never touched.
-__global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uint64_t* __restrict__ start,
+__global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* __restrict__ in, const uint64_t* __restrict__ start,
                                                             const uint32_t* __restrict__ Lb, uint64_t Tb,
-                                                            SElem* out, uint64_t* newkey, bool pre,
+                                                            SElem* __restrict__ out, uint64_t* __restrict__ newkey,
+                                                            bool pre,
                                                             const SSplit* __restrict__ sp,
                                                             const uint32_t* __restrict__ Lsup, uint64_t top) {
     __shared__ uint64_t kw[SORT_CAP];
@@ -950,6 +954,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
     // stage reads table ids from them). L > 0 only between two splitters: splitter b bounds bucket b.
     const SSplit* spb = sp && L ? sp + b : nullptr;
     if (n == 0) return;
+    const uint64_t shi = spb ? spb->hi : 0, slo = spb ? spb->lo : 0;
     if (n > (uint64_t)SORT_CAP) {
         sk_sort_global(bk, n, L, pre, out, s0, newkey, spb);
         return;
@@ -1046,7 +1051,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* in, const uin
     for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
         const uint32_t c = id[i];
         SElem o = bk[c];
-        if (pre && spb) sk_restore(o, L, spb);
+        if (pre && spb) sk_restore(o, L, shi, slo);
         out[s0 + i] = o;
         if (newkey) {  // a key differing from its predecessor's (buckets never share a key)
             bool nk = i == 0 || kw[i - 1] != kw[i];
