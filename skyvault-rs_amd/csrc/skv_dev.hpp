@@ -642,62 +642,6 @@ __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, ui
     return h;
 }
 
-// parse_rec for a small record (key <= 54 bytes): its first 64 bytes come from one round of five
-// independent aligned loads, so the key length, the key's ASCII check and val_len need no
-// dependent load (parse_rec reads val_len only after the key length, and a key past 27 bytes
-// again). Records outside that shape, non-ASCII keys and every error take parse_rec itself, so
-// the result is parse_rec's. (Fixed-stride runs of small records: config 5's 49-byte WAL records.)
-#ifndef SKV_W64
-#define SKV_W64 1
-#endif
-template <class L = GLoad>
-__device__ __forceinline__ RecHdr parse_rec_w64(const uint8_t* run, uint64_t len, uint64_t p, L ld = L()) {
-    const uintptr_t a = (uintptr_t)(run + p), end = (uintptr_t)(run + len);
-    const uintptr_t base = a & ~(uintptr_t)15;
-    const uint32_t sh = (uint32_t)(a & 15);
-    uint4 blk[5];
-#pragma unroll
-    for (int q = 0; q < 5; ++q) blk[q] = base + 16 * q < end ? ld(base + 16 * q) : make_uint4(0, 0, 0, 0);
-    uint32_t w[16];  // record bytes [p, p + 64)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint4 t = funnel16(blk[q], blk[q + 1], sh);
-        w[4 * q] = t.x;
-        w[4 * q + 1] = t.y;
-        w[4 * q + 2] = t.z;
-        w[4 * q + 3] = t.w;
-    }
-    const uint32_t marker = w[0] & 0xFFu;
-    const uint32_t klen = __builtin_bswap32(__builtin_amdgcn_alignbyte(w[1], w[0], 1));
-    const uint64_t need = p + 5 + (uint64_t)klen + (marker == 1 ? 4u : 0u);
-    bool fb = (marker != 1 && marker != 2) || klen > 54 || need > len;
-    uint32_t acc = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < 16; ++i) acc |= w[i] & dword_mask(5, 5 + klen, i);
-    fb = fb || (acc & 0x80808080u) != 0;  // (a non-ASCII key: the exact UTF-8 check)
-    RecHdr h;
-    h.marker = marker;
-    h.klen = klen;
-    h.err = DERR_NONE;
-    uint32_t kd[7];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) kd[i] = __builtin_amdgcn_alignbyte(w[i + 2], w[i + 1], 1);
-    kd[4] = kd[5] = kd[6] = 0;
-    win_prefix(kd, klen, h.hi, h.lo);
-    const uint32_t o = 5 + (klen > 54 ? 54u : klen), q = o >> 2, r = o & 3;  // o <= 59: dwords q, q + 1 <= 15
-    uint32_t d0 = w[0], d1 = w[1];
-#pragma unroll
-    for (uint32_t i = 1; i < 16; ++i) {
-        d0 = i == q ? w[i] : d0;
-        d1 = i == q + 1 ? w[i] : d1;
-    }
-    const uint64_t vlen = __builtin_bswap32(__builtin_amdgcn_alignbyte(d1, d0, r));
-    h.size = marker == 1 ? 9 + (uint64_t)klen + vlen : 5 + (uint64_t)klen;
-    fb = fb || (marker == 1 && need + vlen > len);
-    if (fb) return parse_rec<true>(run, len, p, ld);  // (one call site)
-    return h;
-}
-
 // walk_checked with vectorized headers: one dependent round trip per record. UTF8 = false: the
 // structure only (k_spec's fast mode; k_emit checks the keys and flags a bad one for an exact rerun)
 // slot (cap > 0, a multiple of 8, 16-byte aligned row): the first cap record starts, as offsets

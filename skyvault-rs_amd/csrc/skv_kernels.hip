@@ -576,7 +576,7 @@ __global__ void k_emit_fixed(const RunInfo* __restrict__ runs, uint32_t n_runs, 
         run = (const uint8_t*)runs[lo].ptr;
         len = runs[lo].len;
         p = 1 + (i - run_recb[lo]) * f.S;
-        h = VERIFY && SKV_W64 && f.S <= 64 ? parse_rec_w64(run, len, p) : parse_rec<true>(run, len, p);
+        h = parse_rec<true>(run, len, p);
         if (VERIFY && (h.err || h.size != f.S || h.size >= (1ull << 31))) {
             atomicOr(&run_broken[lo], 1u);
             atomicOr(flags + 2, 1u);  // poison the speculative merge
