@@ -1194,8 +1194,10 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                 unsigned long long pr[16];
                 sort_prof_read(pr);
                 fprintf(stderr, "[sort prof] bucket: load %llu top %llu group %llu slot+store %llu | tile: load %llu "
-                                "bitonic %llu ties %llu out %llu | tiles %llu (100 MHz ticks, cumulative)\n",
-                        pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], pr[15]);
+                                "bitonic %llu ties %llu out %llu | tiles %llu (100 MHz ticks, cumulative) | tie runs %llu "
+                                "tie elements %llu long %llu record words %llu global %llu\n",
+                        pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], pr[15], pr[8], pr[9], pr[10], pr[11],
+                        pr[12]);
             }
             km = 1;
             list_off = {0, R};

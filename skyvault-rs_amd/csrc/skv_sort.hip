@@ -949,6 +949,10 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* __restrict__ 
     const uint32_t Lt = Lb ? Lb[b] : 0u;
     const uint32_t L = Lsup ? Lsup[b / top] : Lt;
     const uint32_t ks = Lt > L ? Lt - L : 0u;
+#if SKV_SORT_PROF
+    if (threadIdx.x == 0 && ks > 4 && start[b + 1] > start[b]) atomicAdd(&g_sort_prof[11], 1ull);
+    if (threadIdx.x == 0 && start[b + 1] - start[b] > (uint64_t)SORT_CAP) atomicAdd(&g_sort_prof[12], 1ull);
+#endif
     SElem* bk = in + s0;
     // sp (the records' level, pre): the output elements get their keys' true prefixes back (the WAL
     // stage reads table ids from them). L > 0 only between two splitters: splitter b bounds bucket b.
@@ -1027,8 +1031,15 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* __restrict__ 
             uint32_t e = i + 2;
             while (e < n32 && kw[e] == w && e - i <= SORT_TIE_MAX) ++e;
             if (e - i > SORT_TIE_MAX) {
+#if SKV_SORT_PROF
+                atomicAdd(&g_sort_prof[10], 1ull);
+#endif
                 s_long = 1;
             } else {
+#if SKV_SORT_PROF
+                atomicAdd(&g_sort_prof[8], 1ull);
+                atomicAdd(&g_sort_prof[9], (unsigned long long)(e - i));
+#endif
                 for (uint32_t t = i + 1; t < e; ++t) {
                     const uint32_t x = id[t];
                     uint32_t j = t;
