@@ -902,14 +902,19 @@ __device__ __forceinline__ uint64_t sk_kw(const SElem& e, uint32_t L, bool pre, 
 
 template <int EPT>
 __device__ void sk_sort_regs(const SElem* bk, uint32_t n, uint32_t L, bool pre, uint32_t ks, uint64_t* kw,
-                             uint16_t* id) {
+                             uint16_t* id, uint64_t* kwid) {
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint64_t k[EPT];  // the sort word's top 53 bits | element id (runs of equal 53-bit words go to
                       // the tie pass like runs of equal words did)
 #pragma unroll
     for (int u = 0; u < EPT; ++u) {
         const uint32_t e = w * 64 * EPT + (uint32_t)u * 64 + l;
-        k[u] = e < n ? (sk_kw(bk[e], L, pre, ks) & ~SK_ID_MASK) | e : ~0ull;
+        k[u] = ~0ull;
+        if (e < n) {
+            const uint64_t w = sk_kw(bk[e], L, pre, ks);
+            kwid[e] = w;  // the full word by element id: the tie pass orders equal 53-bit words by it
+            k[u] = (w & ~SK_ID_MASK) | e;
+        }
     }
     sk_bitonic_regs<EPT, 1, 0>(k, kw);
     __syncthreads();  // (the last cross-wave stage's reads of kw are done)
@@ -940,6 +945,10 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* __restrict__ 
                                                             const uint32_t* __restrict__ Lsup, uint64_t top) {
     __shared__ uint64_t kw[SORT_CAP];
     __shared__ uint16_t id[SORT_CAP];
+    // full 64-bit sort word by element id: runs of equal 53-bit words (ASCII keys: the dropped low
+    // bits carry most of a byte's information -- ~5 runs per config-5 bucket) are ordered on it in
+    // LDS, and only equal full words read the elements
+    __shared__ uint64_t kwid[SORT_CAP];
     __shared__ uint32_t s_long;
     const uint64_t b = blockIdx.x;
     if (b >= Tb) return;
@@ -968,10 +977,10 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* __restrict__ 
     if (threadIdx.x == 0) s_long = 0;
 #if SKV_SORT_REGS
     static_assert(SORT_THREADS == 256 && SORT_CAP == 2048, "register network: 256 threads, <= 8 elements each");
-    if (n32 <= 256) sk_sort_regs<1>(bk, n32, L, pre, ks, kw, id);
-    else if (n32 <= 512) sk_sort_regs<2>(bk, n32, L, pre, ks, kw, id);
-    else if (n32 <= 1024) sk_sort_regs<4>(bk, n32, L, pre, ks, kw, id);
-    else sk_sort_regs<8>(bk, n32, L, pre, ks, kw, id);
+    if (n32 <= 256) sk_sort_regs<1>(bk, n32, L, pre, ks, kw, id, kwid);
+    else if (n32 <= 512) sk_sort_regs<2>(bk, n32, L, pre, ks, kw, id, kwid);
+    else if (n32 <= 1024) sk_sort_regs<4>(bk, n32, L, pre, ks, kw, id, kwid);
+    else sk_sort_regs<8>(bk, n32, L, pre, ks, kw, id, kwid);
     __syncthreads();
     SPROF_T(q1);
     SPROF_ADD(4, q0, q1);
@@ -979,7 +988,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* __restrict__ 
     SPROF_ADD(5, q1, q2);
 #else
     for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
-        kw[i] = sk_kw(bk[i], L, pre, ks);
+        kw[i] = kwid[i] = sk_kw(bk[i], L, pre, ks);
         id[i] = (uint16_t)i;
     }
     __syncthreads();
@@ -1043,7 +1052,10 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* __restrict__ 
                 for (uint32_t t = i + 1; t < e; ++t) {
                     const uint32_t x = id[t];
                     uint32_t j = t;
-                    while (j > i && sk_eless(bk, x, id[j - 1], L, pre)) {
+                    while (j > i) {
+                        const uint32_t y = id[j - 1];
+                        const uint64_t kx = kwid[x], ky = kwid[y];
+                        if (kx != ky ? kx > ky : !sk_eless(bk, x, y, L, pre)) break;
                         id[j] = id[j - 1];
                         --j;
                     }
@@ -1065,7 +1077,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* __restrict__ 
         if (pre && spb) sk_restore(o, L, shi, slo);
         out[s0 + i] = o;
         if (newkey) {  // a key differing from its predecessor's (buckets never share a key)
-            bool nk = i == 0 || kw[i - 1] != kw[i];
+            bool nk = i == 0 || kw[i - 1] != kw[i] || kwid[id[i - 1]] != kwid[id[i]];
             if (!nk) {
                 const uint32_t a = id[i - 1];
                 nk = !sk_wsame(sk_skey(bk[a], L, pre), sk_skey(bk[c], L, pre), bk[a], bk[c], L);
