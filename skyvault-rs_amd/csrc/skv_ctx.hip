@@ -414,19 +414,9 @@ int build_job_impl(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t
     job.run_ptr.resize(n);  // (the one-run size; pass 2 resizes otherwise)
     job.run_len.resize(n);
     job.ranked.resize(n);
-    static const bool prefetch = [] {  // SKV_JOB_PREFETCH=0: no software prefetch (A/B)
-        const char* e = getenv("SKV_JOB_PREFETCH");
-        return !(e && e[0] == '0');
-    }();
     par_run(n, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
         Blk& K = B[b];
         for (uint64_t i = lo; i < hi; ++i) {
-            if (prefetch && i + 16 < hi) {  // the caller's entries ahead, and the run arrays they point at
-                __builtin_prefetch(&streams[i + 16]);
-                const skv_stream& q = streams[i + 8];
-                __builtin_prefetch(q.run_lens);
-                __builtin_prefetch(q.runs);
-            }
             const skv_stream& s = streams[i];
             if (s.n_runs && (!s.runs || !s.run_lens)) {
                 K.bad = i;
