@@ -17,6 +17,7 @@
 #   sbdiag   record-sort bucket pass timing diagnostics: k_sort_bucket<D> launches with parts skipped
 #   sa8, sa32, sbb4, sbb16  two-pass bucketing: elements per thread of pass A / pass B (default 16 / 8)
 #   ov12, ov20  record sort: samples per bucket (default 16: 768-element buckets)
+#   tileprof merge-tile phase ticks (printed when the ctx is destroyed; diagnostic)
 #   gu4, gu1, gnt0, gpage  k_gather: 4 / 1 blocks per lane in flight, plain stores, the page gather
 set -eu
 cd "$(dirname "$0")/../skyvault-rs_amd"
@@ -48,6 +49,7 @@ declare -A F=(
   [sbb16]="-DSKV_SBB_PER=16"
   [ov12]="-DSKV_SORT_OV=12"
   [ov20]="-DSKV_SORT_OV=20"
+  [tileprof]="-DSKV_TILE_PROF=1"
   [gu4]="-DSKV_GATHER_U=4"
   [gu1]="-DSKV_GATHER_U=1"
   [gnt0]="-DSKV_GATHER_NT=0"
