@@ -807,7 +807,10 @@ __device__ __forceinline__ bool sk_eless(const SElem* bk, uint32_t x, uint32_t y
     return sk_wless(sk_skey(bk[x], L, pre), sk_skey(bk[y], L, pre), bk, x, y, L);
 }
 
-constexpr uint32_t SORT_TIE_MAX = 32;  // longest run of equal first words sorted by one thread
+#ifndef SKV_SORT_TIE_MAX
+#define SKV_SORT_TIE_MAX 32
+#endif
+constexpr uint32_t SORT_TIE_MAX = SKV_SORT_TIE_MAX;  // longest run of equal first words sorted by one thread
 
 #ifndef SKV_SORT_REGS
 #define SKV_SORT_REGS 1  // 1: the bucket's bitonic network in registers (shuffles / LDS across waves)
