@@ -808,7 +808,7 @@ __device__ __forceinline__ bool sk_eless(const SElem* bk, uint32_t x, uint32_t y
 }
 
 #ifndef SKV_SORT_TIE_MAX
-#define SKV_SORT_TIE_MAX 32
+#define SKV_SORT_TIE_MAX 8
 #endif
 constexpr uint32_t SORT_TIE_MAX = SKV_SORT_TIE_MAX;  // longest run of equal first words sorted by one thread
 

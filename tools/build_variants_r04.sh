@@ -17,7 +17,7 @@
 #   sbdiag   record-sort bucket pass timing diagnostics: k_sort_bucket<D> launches with parts skipped
 #   sa8, sa32, sbb4, sbb16  two-pass bucketing: elements per thread of pass A / pass B (default 16 / 8)
 #   ov12, ov20  record sort: samples per bucket (default 16: 768-element buckets)
-#   tie4, tie8, tie16, tie64  bucket sort: longest tie run sorted by one thread (default 32)
+#   tie4, tie8, tie16, tie64  bucket sort: longest tie run sorted by one thread (default 8)
 #   tileprof merge-tile phase ticks (printed when the ctx is destroyed; diagnostic)
 #   gu4, gu1, gnt0, gpage  k_gather: 4 / 1 blocks per lane in flight, plain stores, the page gather
 set -eu
