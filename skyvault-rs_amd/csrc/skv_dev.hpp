@@ -251,7 +251,10 @@ struct SElem {
 };
 constexpr int SORT_CAP = 2048;           // elements a bucket sorts in LDS
 constexpr int SORT_THREADS = 256;
-constexpr uint64_t SORT_EVERY = 48;      // one sample per SORT_EVERY elements
+#ifndef SKV_SORT_EVERY
+#define SKV_SORT_EVERY 48
+#endif
+constexpr uint64_t SORT_EVERY = SKV_SORT_EVERY;  // one sample per SORT_EVERY elements
 #ifndef SKV_SORT_OV
 #define SKV_SORT_OV 16
 #endif

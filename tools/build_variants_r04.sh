@@ -17,6 +17,7 @@
 #   sbdiag   record-sort bucket pass timing diagnostics: k_sort_bucket<D> launches with parts skipped
 #   sa8, sa32, sbb4, sbb16  two-pass bucketing: elements per thread of pass A / pass B (default 16 / 8)
 #   ov12, ov20  record sort: samples per bucket (default 16: 768-element buckets)
+#   ev32, ev24  record sort: one sample per 32 / 24 elements (24 / 32 per bucket: the same 768 target)
 #   tie4, tie8, tie16, tie64  bucket sort: longest tie run sorted by one thread (default 8)
 #   tileprof merge-tile phase ticks (printed when the ctx is destroyed; diagnostic)
 #   gu4, gu1, gnt0, gpage  k_gather: 4 / 1 blocks per lane in flight, plain stores, the page gather
@@ -51,6 +52,8 @@ declare -A F=(
   [ov12]="-DSKV_SORT_OV=12"
   [ov20]="-DSKV_SORT_OV=20"
   [tileprof]="-DSKV_TILE_PROF=1"
+  [ev32]="-DSKV_SORT_EVERY=32 -DSKV_SORT_OV=24"
+  [ev24]="-DSKV_SORT_EVERY=24 -DSKV_SORT_OV=32"
   [tie4]="-DSKV_SORT_TIE_MAX=4"
   [tie8]="-DSKV_SORT_TIE_MAX=8"
   [tie16]="-DSKV_SORT_TIE_MAX=16"
