@@ -137,8 +137,8 @@ typedef struct {
                                 call was rerun with exact key compares (a 64-bit collision) */
     uint32_t host_parts;     /* skv_compact: key-range parts whose H2D, kernels and D2H overlapped
                                 (0: the serial copy -> compact -> copy) */
-    uint32_t span_parse;     /* general path: 1 the one-pass span parse produced the record arrays;
-                                2 | fail_bits << 8: it declined and the chunk-walk parse ran; 0 not tried */
+    uint32_t span_parse;     /* always 0 since ABI 7 (the opt-in one-pass span parse was removed; the
+                                field keeps the struct layout) */
     uint32_t wal_stage;      /* SKV_SPLIT_BY_TABLE: 1 the one-pass stage (every table kept), 2 the exact
                                 stage (the one-pass stage declined or does not apply), 0 no WAL stage */
     uint32_t reserved2;

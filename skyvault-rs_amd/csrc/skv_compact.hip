@@ -391,15 +391,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // big call spends fewer re-synchronising starts per record). Parse of config 3 shapes by walk
     // length (tools/stage_probe.py): 59 GiB 16/32/64 KiB 30.3/26.4/25.2 ms; 3.7 GiB 4/16/32/64 KiB
     // 3.59/2.27/2.14/2.34; 0.23 GiB 4/8/16 KiB 0.50/0.49/0.53; 0.06 GiB 4/16 KiB 0.38/0.47
-    // the one-pass span parse (skv_span.hip) walks SPAN_BYTES spans; the chunk-walk parse behind it
-    // (its fallback, or SKV_SPAN=0) then uses the same chunking
-    // off by default: measured slower than the chunk walks; SKV_SPAN=1 runs it
-    const char* spe = getenv("SKV_SPAN");
-    const bool use_span = spe && spe[0] == '1';
     uint64_t chunk = CHUNK;
-    if (use_span)
-        chunk = SPAN_BYTES;
-    else if (const char* ce = getenv("SKV_CHUNK_BYTES"))  // slot offsets are 16-bit: at most 64 KiB
+    if (const char* ce = getenv("SKV_CHUNK_BYTES"))  // slot offsets are 16-bit: at most 64 KiB
         chunk = std::min<uint64_t>(65536, std::max<uint64_t>(CHUNK, strtoull(ce, nullptr, 10)));
     else
         while (chunk < 65536 && job.in_bytes / (2 * chunk) >= (1ull << 16)) chunk *= 2;
@@ -410,7 +403,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // the caller-order pointer / length arrays, and the host table only if a host path needs it
     const char* hre = getenv("SKV_HOST_RUNS");  // 1: the host run table always
     const bool runs_dev = k > (uint32_t)TILE_TARGET / 2 && job.one_run_each && job.caller_order != 0 && !job.scan &&
-                          !job.search && !job.batch && !job.part && !use_span && !getenv("SKV_HOST_TABLES") &&
+                          !job.search && !job.batch && !job.part && !getenv("SKV_HOST_TABLES") &&
                           !(hre && hre[0] == '1');
     bool host_runs_built = false;
     auto build_host_runs = [&]() {  // blocks of streams (rank order) on host threads: runs and chunks before each block, then fill
@@ -571,15 +564,14 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         HIPCHK(hipMemsetAsync(utf8_bad, 0, 4, st));
         HIPCHK(hipMemsetAsync(d_first_dec, 0xFF, (size_t)k * 8, st));
     };
-    // reset = false: the span parse already produced the verdict words (its order check)
-    auto alloc_records = [&](bool reset = true) {
+    auto alloc_records = [&]() {
         rec_addr = dbuf<uint64_t>(ctx, "rec_addr", R);
         rec_hi = dbuf<uint64_t>(ctx, "rec_hi", R);
         rec_lo = dbuf<uint64_t>(ctx, "rec_lo", R);
         rec_klen = dbuf<uint32_t>(ctx, "rec_klen", R);
         rec_meta = dbuf<uint32_t>(ctx, "rec_meta", R);
         rec_fp = dbuf<uint64_t>(ctx, "rec_fp", R);
-        if (reset) reset_verdict();
+        reset_verdict();
         if (dev_tables)  // one run per stream, rank order: stream bases are the run record bases
             HIPCHK(hipMemcpyAsync(d_stream_base, d_recb, (size_t)(k + 1) * 8, hipMemcpyDeviceToDevice, st));
         else
@@ -597,10 +589,9 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     uint32_t utf8_flag = 0;
     // order check + readback of its result, the record flags and (fast path) the broken-run flags
     // order: ORDER_LAUNCH runs k_order_check here; ORDER_DONE the parse did it (first decreases as
-    // stream-local indices); ORDER_SPAN the span parse did it (global record indices)
-    enum { ORDER_LAUNCH = 0, ORDER_DONE = 1, ORDER_SPAN = 2 };
+    // stream-local indices)
+    enum { ORDER_LAUNCH = 0, ORDER_DONE = 1 };
     auto check_and_read = [&](bool read_broken, int order = ORDER_LAUNCH) -> bool {
-        const bool span_order = order == ORDER_SPAN;
         // the fast path's parse kernel already did the order check
         if (!read_broken && !job.batch && order == ORDER_LAUNCH)  // a writer batch is unsorted by definition
             launch_order_check(st, R, d_stream_base, k, rec_addr, rec_hi, rec_lo, rec_klen, d_first_dec, d_flags + 1);
@@ -622,9 +613,6 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             if (need_broken) d2h(ctx, hq + (size_t)k * 8, d_broken, (size_t)n_runs * 4);
             sync(ctx);
             if (need_dec) memcpy(first_dec.data(), hq, (size_t)k * 8);
-            if (need_dec && span_order)
-                for (uint32_t s = 0; s < k; ++s)
-                    if (first_dec[s] != ~0ull) first_dec[s] -= stream_base[s];
             const uint32_t* b = (const uint32_t*)(hq + (size_t)k * 8);
             for (uint32_t r = 0; need_broken && r < n_runs && !broken; ++r) broken = b[r] != 0;
         }
@@ -647,12 +635,12 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     bool e_direct = false;  // the fixed-stride parse wrote the record sort's elements (sort_e)
     bool any_fixed = false;  // some run is fixed-stride: the general parse also runs k_emit_fixed
     uint32_t uniform_meta = 0;  // every record a Put of one size (the fixed path's runs, one format): its meta
-    uint64_t first_sum = 0, first_n = 0;  // the runs' first-record sizes (record capacity of the span parse)
-    bool any_bodyless = false;            // a run of only a version byte (no span: the chunk-walk parse)
     // the device-table variant: past the splitter merge's fan-in (the fused path cannot apply), one
-    // run per stream, a plain compaction or WAL flush (SKV_HOST_TABLES=1: the host tables always)
-    const bool try_dev_tables = k > (uint32_t)TILE_TARGET / 2 && n_runs == k && !job.scan && !job.search &&
-                                !job.batch && !job.part && !use_span && !getenv("SKV_HOST_TABLES");
+    // run per stream, a plain compaction or WAL flush (SKV_HOST_TABLES=1: the host tables always).
+    // One run per STREAM, not n_runs == k: an empty stream beside a two-member stream also gives
+    // n_runs == k, and the stream bases below are the run record bases.
+    const bool try_dev_tables = k > (uint32_t)TILE_TARGET / 2 && n_runs == k && job.one_run_each && !job.scan && !job.search &&
+                                !job.batch && !job.part && !getenv("SKV_HOST_TABLES");
     if (try_dev_tables) {
         uint64_t* d_cnt = dbuf<uint64_t>(ctx, "run_cnt", n_runs + 1);
         uint32_t* d_rfl = dbuf<uint32_t>(ctx, "run_tflags", 4);
@@ -723,31 +711,18 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         htrace("run formats read");
         // blocks of runs on host threads: every run fixed-stride? one format everywhere?
         const unsigned nbr = par_nblocks(n_runs);
-        std::vector<uint8_t> blk_fixed(nbr, 1), blk_uni(nbr, 1), blk_any(nbr, 0), blk_empty(nbr, 0);
-        std::vector<uint64_t> blk_fs(nbr, 0), blk_fn(nbr, 0);
+        std::vector<uint8_t> blk_fixed(nbr, 1), blk_uni(nbr, 1), blk_any(nbr, 0);
         par_run(n_runs, nbr, [&](unsigned b, uint64_t lo, uint64_t hi) {
-            bool fx = true, un = true, an = false, em = false;
-            uint64_t fs = 0, fc = 0;
+            bool fx = true, un = true, an = false;
             for (uint64_t r = lo; r < hi; ++r) {
                 fx = fx && hf[r].S != 0;
                 an = an || hf[r].S != 0;
                 un = un && hf[r].S == hf[0].S && hf[r].K == hf[0].K;
-                em = em || runs[r].n_chunks == 0;
-                fs += hf[r].first;
-                fc += hf[r].first != 0;
             }
             blk_fixed[b] = fx;
             blk_uni[b] = un;
             blk_any[b] = an;
-            blk_empty[b] = em;
-            blk_fs[b] = fs;
-            blk_fn[b] = fc;
         });
-        for (unsigned b = 0; b < nbr; ++b) {
-            first_sum += blk_fs[b];
-            first_n += blk_fn[b];
-            any_bodyless = any_bodyless || blk_empty[b];
-        }
         bool all_fixed = n_runs > 0, uniform = true;
         for (unsigned b = 0; b < nbr; ++b) {
             all_fixed = all_fixed && blk_fixed[b];
@@ -813,70 +788,6 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                 any_err = false;
                 std::fill(stream_err.begin(), stream_err.end(), 0u);
             }
-        }
-    }
-    // ---- general path, one pass: spans staged in LDS (skv_span.hip) -----------------------------
-    uint32_t span_state = 0;
-    if (!parsed && use_span && n_chunks && !any_bodyless) {
-        const double mean = first_n ? std::max(5.0, (double)first_sum / (double)first_n) : 64.0;
-        const uint64_t cap = std::min<uint64_t>(job.in_bytes / 5 + 1, (uint64_t)(job.in_bytes / mean * 1.5) + 65536);
-        SpanOut so{};
-        so.rec_addr = dbuf<uint64_t>(ctx, "rec_addr", cap);
-        so.rec_hi = dbuf<uint64_t>(ctx, "rec_hi", cap);
-        so.rec_lo = dbuf<uint64_t>(ctx, "rec_lo", cap);
-        so.rec_klen = dbuf<uint32_t>(ctx, "rec_klen", cap);
-        so.rec_meta = dbuf<uint32_t>(ctx, "rec_meta", cap);
-        so.rec_fp = dbuf<uint64_t>(ctx, "rec_fp", cap);
-        so.run_recb = d_recb;
-        so.first = dbuf<uint64_t>(ctx, "span_first", n_chunks);
-        so.exit = dbuf<uint64_t>(ctx, "span_exit", n_chunks);
-        so.tstate = dbuf<uint64_t>(ctx, "span_state", n_chunks);
-        uint32_t* sw = dbuf<uint32_t>(ctx, "span_words", 32);
-        so.ticket = sw;
-        so.fail = sw + 1;
-        so.hdr_err = d_hdr;
-        so.cap = cap;
-        so.sbase = dbuf<uint64_t>(ctx, "span_base", n_chunks);
-        so.first_dec = job.batch ? nullptr : d_first_dec;  // (a writer batch is unsorted by definition)
-        so.any_dec = d_flags + 1;
-        reset_verdict();
-        HIPCHK(hipMemsetAsync(so.tstate, 0, n_chunks * 8, st));
-        HIPCHK(hipMemsetAsync(sw, 0, 128, st));
-        {
-            const char* dg = getenv("SKV_SPAN_DBG");
-            so.dbg = dg && dg[0] == '1' ? sw + 2 : nullptr;
-        }
-        launch_span_parse(st, d_runs, n_runs, n_chunks, so);
-        HIPCHK(hipGetLastError());
-        std::vector<uint64_t>& recb = ctx->s_recb;
-        recb.resize(n_runs + 1);
-        uint8_t* hp = (uint8_t*)pinned(ctx, (n_runs + 1) * 8 + 16);
-        d2h(ctx, hp, so.fail, 4);
-        uint64_t dbgw[16] = {};
-        if (so.dbg) d2h(ctx, (uint8_t*)dbgw, sw, 128);
-        d2h(ctx, hp + 16, d_recb, (n_runs + 1) * 8);
-        sync(ctx);
-        uint32_t fail;
-        memcpy(&fail, hp, 4);
-        span_state = fail ? 2u | (fail << 8) : 1u;
-        ctx->timings.span_parse = span_state;
-        htrace(fail ? "span parse declined" : "span parse done");
-        if (so.dbg)
-            fprintf(stderr, "[span] spans %lu fail %#x ticks/span: stage %.0f walk %.0f lookback %.0f emit %.0f\n",
-                    (unsigned long)n_chunks, fail, (double)dbgw[4] / n_chunks, (double)dbgw[5] / n_chunks,
-                    (double)dbgw[6] / n_chunks, (double)dbgw[7] / n_chunks);
-        if (!fail) {
-            memcpy(recb.data(), hp + 16, (n_runs + 1) * 8);
-            R = recb[n_runs];
-            par_run(n_runs, par_nblocks(n_runs), [&](unsigned, uint64_t lo, uint64_t hi) {
-                for (uint64_t r = lo; r < hi; ++r) sum[r] = RunSummary{recb[r + 1] - recb[r], 0u, 0u};
-            });
-            stream_tables();
-            alloc_records(false);
-            rec_addr = so.rec_addr;
-            mark(ctx, PH_PARSE);
-            check_and_read(false, ORDER_SPAN);
-            parsed = true;
         }
     }
     // ---- general path: speculative chunk walks ----------------------------------------------
@@ -1611,7 +1522,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         t.gather_write_bytes = kept_bytes + n_out_runs;
         t.hot_ms = ms[PH_GATHER];
     }
-    ctx->timings.path = parsed && span_state != 1 ? SKV_PATH_FIXED : SKV_PATH_GENERAL;
+    ctx->timings.path = parsed ? SKV_PATH_FIXED : SKV_PATH_GENERAL;
     ctx->timings.hot_read_bytes = kept_bytes;
     ctx->timings.hot_write_bytes = kept_bytes + n_out_runs;
     ctx->timings.host_syncs = ctx->syncs;

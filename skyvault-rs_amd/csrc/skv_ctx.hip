@@ -11,11 +11,29 @@
 #include <deque>
 #include <exception>
 #include <fstream>
+#include <mutex>
+#include <set>
 #include <sstream>
 
 using namespace skv;
 
 thread_local int skv_tl_device = -1;
+
+namespace skv {
+void lds_limit(const void* kernel) {
+    static std::mutex mu;
+    static std::set<std::pair<int, const void*>> done;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    if (!done.insert({dev, kernel}).second) return;
+    // the ceiling is the CU's LDS less the kernel's static LDS (a larger value is refused)
+    hipFuncAttributes fa{};
+    size_t stat = 0;
+    if (hipFuncGetAttributes(&fa, kernel) == hipSuccess) stat = fa.sharedSizeBytes;
+    (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024 - stat));
+}
+}  // namespace skv
 
 
 int set_err(skv_ctx* ctx, int code, const char* fmt, ...) {

@@ -887,17 +887,6 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
             return SKV_OK;
         }
         const uint64_t n = pres->n_runs;
-        if (getenv("SKV_GPIPE_DEBUG")) {
-            fprintf(stderr, "[gpipe] part %llu/%llu max %llu streams %zu runs %llu bytes %llu open %llu+%llu\n",
-                    (unsigned long long)p, (unsigned long long)P, (unsigned long long)job.max_run_size, sv.size(),
-                    (unsigned long long)n, (unsigned long long)pres->n_bytes, (unsigned long long)open_off,
-                    (unsigned long long)open_len);
-            for (uint64_t r = 0; r < n; ++r)
-                if (r < 3 || r + 3 >= n)
-                    fprintf(stderr, "   run %llu off %llu len %llu recs %llu\n", (unsigned long long)r,
-                            (unsigned long long)pres->runs[r].off, (unsigned long long)pres->runs[r].len,
-                            (unsigned long long)(pres->runs[r].put_count + pres->runs[r].delete_count));
-        }
         if (wal) {
             // whole tables: every run of the part is final at its offset in the call's output
             for (uint64_t r = 0; r < n; ++r) {

@@ -2855,16 +2855,7 @@ hipError_t launch_tile(hipStream_t s, bool l0, const uint64_t* hi, const uint64_
     Elems E{hi, lo, c, klen, poison};
     if (!grid) grid = T;  // level 0 takes tickets: launches of grid < T tiles continue each other
     size_t lds = tile_lds_bytes(k);
-    // raise the dynamic LDS limit once per device and size, not per call
-    static size_t lds_set[64][2] = {};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    size_t& done = lds_set[dev & 63][l0 ? 1 : 0];
-    if (lds > done) {
-        (void)hipFuncSetAttribute(l0 ? (const void*)k_tile<true> : (const void*)k_tile<false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        done = lds;
-    }
+    lds_limit(l0 ? (const void*)k_tile<true> : (const void*)k_tile<false>);
     if (l0) {
         k_tile<true><<<(unsigned)grid, TILE_THREADS, lds, s>>>(E, bounds, k, tile_base, rec_meta, rec_addr, drop, O);
     } else {

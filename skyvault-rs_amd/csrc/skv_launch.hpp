@@ -3,6 +3,10 @@
 #include "skv_dev.hpp"
 
 namespace skv {
+// Raise a kernel's dynamic-LDS limit to the CU's 160 KiB, once per (device, kernel), under a lock:
+// the limit is a ceiling, so one value serves every launch size and concurrent ctxs never lower it
+// between another thread's set and launch (skv_ctx.hip).
+void lds_limit(const void* kernel);
 void launch_run_header(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint32_t* hdr_err, RunFmt* fmt,
                        bool slices = false);
 void launch_spec(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
@@ -212,27 +216,5 @@ void launch_scan_cut(hipStream_t, const uint64_t* d_K, const uint64_t* putx, con
 void launch_scan_gather(hipStream_t, uint64_t R, const uint64_t* info, const uint64_t* keep, const uint64_t* offx,
                         const uint64_t* size, const uint64_t* m_src, uint8_t* out);
 void launch_scan_dn(hipStream_t, const uint64_t* in, const uint64_t* dn, uint64_t max_n, uint64_t* out, uint64_t* tmp);
-// one-pass parse of variable-length runs (skv_span.hip)
-#ifndef SKV_SPAN_BYTES
-#define SKV_SPAN_BYTES 16384
-#endif
-constexpr uint32_t SPAN_BYTES = SKV_SPAN_BYTES;
-struct SpanOut {
-    uint64_t *rec_addr, *rec_hi, *rec_lo, *rec_fp;
-    uint32_t *rec_klen, *rec_meta;
-    uint64_t* run_recb;      // record base of each run with a span; [n_runs] = records in all
-    uint64_t *first, *exit;  // per span: its first record start (NO_POS: none), its last record's end
-    uint64_t* tstate;        // look-back words (zeroed per call)
-    uint32_t* ticket;        // span ticket (zeroed per call)
-    uint32_t* fail;          // SPF_* bits: any -> the chunk-walk parse runs instead (zeroed per call)
-    const uint32_t* hdr_err; // k_run_header's verdict per run
-    uint64_t cap;            // entries the record arrays hold
-    uint32_t* dbg;           // SKV_SPAN_DBG=1: printf the first failing lanes (counter); null: off
-    uint64_t* sbase;         // per span: global index of its first record
-    unsigned long long* first_dec;  // in-stream order check (runs.rs:190-198): per stream, the global
-                                    // index of the record before its first decrease; null: no check
-    uint32_t* any_dec;       // set with any first_dec entry
-};
-void launch_span_parse(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_spans, const SpanOut& O);
 
 }  // namespace skv

@@ -22,6 +22,9 @@
 // reruns the call on the general path, which reproduces the reference's exact outcome.
 #include "skv_launch.hpp"
 
+#include <map>
+#include <mutex>
+
 #ifndef SKV_FX_DIAG
 #define SKV_FX_DIAG 0  // diagnostic builds only (output invalid): 1 skip the copy, 2 skip the merge
                        // rounds, 3 copy only (no key loads, no merge: records in load order);
@@ -1321,25 +1324,24 @@ hipError_t launch_fx_tile(hipStream_t s, const FxArgs& A) {
     // SKV_FX_LDS=<bytes>: pad the tile's LDS request (caps workgroups per CU; occupancy studies)
     static const size_t lds_pad = getenv("SKV_FX_LDS") ? (size_t)atol(getenv("SKV_FX_LDS")) : 0;
     const size_t lds = std::max(fx_tile_lds_bytes(A.k), std::min<size_t>(lds_pad, 160 * 1024));
-    static size_t lds_set[64] = {};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (lds > lds_set[dev & 63]) {
-        (void)hipFuncSetAttribute((const void*)k_fx_tile, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        lds_set[dev & 63] = lds;
-    }
+    lds_limit((const void*)k_fx_tile);
     k_fx_tile<<<(unsigned)A.T, FX_THREADS, lds, s>>>(A);
     return hipGetLastError();
 }
 uint64_t fx_tile_slots(uint32_t k) {  // fused tiles resident at once on the current device
-    static uint64_t cached[64] = {}, cached_k[64] = {};
+    // one entry per (device, k), under a lock: ctxs on other threads call this concurrently
+    static std::mutex mu;
+    static std::map<std::pair<int, uint32_t>, uint64_t> cache;
     int dev = 0, cus = 0, per = 0;
     (void)hipGetDevice(&dev);
-    if (cached[dev & 63] && cached_k[dev & 63] == k) return cached[dev & 63];
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find({dev, k});
+    if (it != cache.end()) return it->second;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_fx_tile, FX_THREADS, fx_tile_lds_bytes(k));
-    cached_k[dev & 63] = k;
-    return cached[dev & 63] = (uint64_t)(cus > 0 ? cus : 256) * (uint64_t)(per > 0 ? per : 1);
+    const uint64_t slots = (uint64_t)(cus > 0 ? cus : 256) * (uint64_t)(per > 0 ? per : 1);
+    cache[{dev, k}] = slots;
+    return slots;
 }
 void launch_ingest(hipStream_t s, const IngestSlice* slices, uint32_t n, uint32_t blocks_per_slice) {
     if (n) k_ingest<<<dim3(blocks_per_slice, n), 256, 0, s>>>(slices);

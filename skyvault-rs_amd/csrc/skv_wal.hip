@@ -654,7 +654,7 @@ void launch_wal_fused(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const u
     // record lines in flight per XCD, so the composition's re-read can hit L2; occupancy studies)
     static const size_t pad = getenv("SKV_WAL_LDS") ? (size_t)atol(getenv("SKV_WAL_LDS")) : 0;
     const size_t lds = std::min<size_t>(pad, 96 * 1024);
-    if (lds) (void)hipFuncSetAttribute((const void*)k_wal_fused, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (lds) lds_limit((const void*)k_wal_fused);
     if (max_K)
         k_wal_fused<<<wal_blocks(max_K, WAL_G), WAL_G, lds, s>>>(Kp, m_src, P, Dp, out, tstate, ticket, fail, tlist,
                                                                   tcount, tcap, tail, diag, S, m_rec);

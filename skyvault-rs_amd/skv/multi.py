@@ -49,14 +49,20 @@ class MultiCompactor:
         for w in self._workers:
             w.start()
 
-    def submit(self, streams, max_run_size: int, flags: int = 0, with_info: bool = False) -> Future:
+    def submit(self, streams, max_run_size: int, flags: int = 0, with_info: bool = False,
+               entry: str = "compact", then: Optional[Callable[[object, object], object]] = None) -> Future:
+        """Queue one compaction. entry: the Compactor method that runs it -- "compact" (host run
+        bytes, the default), "compact_dev" (device pointers: [(seq_no, [(ptr, len)])]) or
+        "compact_host" (pinned host pointers). then(compactor, result), if given, runs on the
+        worker's thread right after the call (e.g. to read the ctx's timings before its next
+        call); the future holds its return value."""
         size = sum(len(r) if isinstance(r, (bytes, bytearray, memoryview)) else r[1]
                    for _, runs in streams for r in runs)
         with self._lock:
             w = min(self._workers, key=lambda x: x.queued_bytes)
             w.queued_bytes += size
         fut: Future = Future()
-        w.q.put((streams, max_run_size, flags, with_info, size, fut))
+        w.q.put((streams, max_run_size, flags, with_info, entry, then, size, fut))
         return fut
 
     def map(self, jobs: Sequence[tuple]) -> List[object]:
@@ -109,11 +115,15 @@ class _Worker(threading.Thread):
             item = self.q.get()
             if item is None:
                 break
-            streams, max_run_size, flags, with_info, size, fut = item
+            streams, max_run_size, flags, with_info, entry, then, size, fut = item
             try:
                 if comp is None:
                     raise self.error
-                fut.set_result(comp.compact(streams, max_run_size, flags, with_info=with_info))
+                if entry == "compact":
+                    res = comp.compact(streams, max_run_size, flags, with_info=with_info)
+                else:
+                    res = getattr(comp, entry)(streams, max_run_size, flags)
+                fut.set_result(then(comp, res) if then is not None else res)
             except BaseException as e:
                 fut.set_exception(e)
             finally:

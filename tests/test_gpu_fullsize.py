@@ -127,6 +127,62 @@ def test_config2_full_size(dev, torch, variant):
 
 
 # ------------------------------------------------------------------------------------------
+# config 4: eight independent config-2A compactions at once (orchestrator_service.rs:119-170
+# schedules per-table / per-level jobs independently), one ctx + worker thread each
+
+
+def test_config4_eight_compactions_at_once(torch):
+    """BASELINE config 4's workload on the visible devices: 8 config-2A compactions (64 x 238,821
+    records, 4 GiB each, the bench's rank seeds 0..7) submitted together to skv.multi.MultiCompactor
+    with one ctx and one worker thread per job (on a one-GPU box all eight share device 0: 32 GiB of
+    inputs and 8 output buffers in HBM, eight calls in flight on eight HIP streams). Every job's
+    bytes and descriptors are compared with its own oracle call."""
+    from skv.devgen import make_cfg2_on_device
+    from skv.multi import MultiCompactor
+
+    n_dev = torch.cuda.device_count()
+    seeds = [SEED + 1000 * j for j in range(8)]  # bench.rank_seed(0..7)
+    inputs = []
+    for j, sd in enumerate(seeds):
+        _progress(f"config 4: generating job {j}")
+        inputs.append(make_cfg2_on_device(torch.device("cuda", j % n_dev), sd, 64, 238821, 256, "A"))
+
+    def keep(comp, res):  # on the worker thread, before any later call on that ctx
+        return res, comp.timings()
+
+    _progress("config 4: 8 jobs submitted")
+    with MultiCompactor([j % n_dev for j in range(8)]) as mc:
+        futs = [mc.submit([(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(runs)], MAX_RUN, 0,
+                          entry="compact_dev", then=keep) for runs in inputs]
+        results = [f.result() for f in futs]
+        try:
+            assert len({w.ident for w in mc._workers}) == 8
+            _progress("config 4: compare")
+
+            def oracle(j):  # the C oracle releases the GIL: two jobs' oracles at a time
+                host = [r.cpu().numpy() for r in inputs[j]]
+                sa = _abi.stream_table(np.arange(1, 65), [h.ctypes.data for h in host], [h.size for h in host])
+                return pyoracle.compact_np(sa, MAX_RUN, 0)
+
+            with ThreadPoolExecutor(2) as ex:
+                pending = {j: ex.submit(oracle, j) for j in range(2)}
+                for j, (res, t) in enumerate(results):
+                    exp, descs, info = pending.pop(j).result()
+                    if j + 2 < 8:
+                        pending[j + 2] = ex.submit(oracle, j + 2)
+                    assert t["path"] == _abi.PATH_FUSED, (j, t)
+                    assert (res.n_bytes, res.n_runs, res.out_records) == (exp.size, len(descs), info["out_records"]), j
+                    _compare_bytes(res, 0, exp, f"config 4 job {j}")
+                    assert res.descs == descs, j
+                    del exp
+                    res.free()
+                    _progress(f"config 4: job {j} bit-exact")
+        finally:
+            for res, _ in results:  # before the workers destroy their ctxs
+                res.free()
+
+
+# ------------------------------------------------------------------------------------------
 # the host-memory entry point (skv_compact) at BASELINE size, default pipeline thresholds
 
 

@@ -170,6 +170,35 @@ def test_heap_order_on_the_record_sort_path(dev):
         assert dev.timings()["sorted"] == 1
 
 
+def test_run_count_equal_to_streams_without_one_run_each(dev):
+    """Past the splitter fan-in, the device-built run tables take the run record bases as the stream
+    bases; that holds only with one run per stream. An empty stream beside a two-member stream also
+    has as many runs as streams: such calls must keep the host tables, so a key decrease or a decode
+    error after the two-member stream is still reported as the oracle reports it."""
+    r = random.Random(61)
+    base = []
+    for s in range(1700):
+        ks = sorted(r.sample(range(10**6), 4))
+        base.append([fmt.put(f"{k:06d}{s:04d}", bytes([s & 255]) * 8) for k in ks])
+    for case in ("ok", "decrease", "decode"):
+        streams = []
+        for s, ops in enumerate(base):
+            if s == 5:
+                streams.append((10**6 - s, []))  # the empty stream
+            elif s == 9:  # two members, ascending across the members
+                streams.append((10**6 - s, [fmt.encode_run(ops[:2]), fmt.encode_run(ops[2:])]))
+            elif s == 40 and case == "decrease":
+                streams.append((10**6 - s, [fmt.encode_run([ops[1], ops[0]] + ops[2:])]))
+            elif s == 40 and case == "decode":
+                streams.append((10**6 - s, [fmt.encode_run(ops)[:-3]]))
+            else:
+                streams.append((10**6 - s, [fmt.encode_run(ops)]))
+        assert sum(len(m) for _, m in streams) == len(streams)
+        for flags in (0, _abi.SKV_SPLIT_BY_TABLE):
+            exp, got = _run_both(dev, streams, 4 * MiB, flags)
+            assert exp == got, (case, flags, _diff(exp, got))
+
+
 def test_wal_split_matches_oracle(dev):
     """WAL compaction (wal_compaction.rs:66-174) on device: table split, prefix strip (incl. the
     format!("{id}.") length quirk), one run per table, swallowed failing tables, bad keys."""
@@ -441,31 +470,6 @@ def test_longer_speculative_walks(dev, chunk):
             os.environ.pop("SKV_CHUNK_BYTES", None)
         else:
             os.environ["SKV_CHUNK_BYTES"] = old
-
-
-def test_span_parse_opt_in(dev):
-    """The one-pass span parse (SKV_SPAN=1, off by default): variable-length shapes it takes
-    (span_parse == 1, incl. a run whose short tail span holds no record start), and shapes it
-    declines for the chunk-walk parse (fake records in values, records longer than a span,
-    corruption) -- every outcome equal to the oracle's."""
-    old = os.environ.get("SKV_SPAN")
-    os.environ["SKV_SPAN"] = "1"
-    try:
-        taken = 0
-        for n, rb in ((4, 200_000), (32, 192 * KiB), (256, 24 * KiB)):
-            s = gen.config3(n_streams=n, run_bytes=rb, vsize=64 if n == 256 else 256)
-            exp, got = _run_both(dev, s, 256 * KiB, 0)
-            assert exp == got, _diff(exp, got)
-            taken += dev.timings()["span_parse"] == 1
-        assert taken >= 2, "the span parse declined the plain config-3 shapes"
-        test_values_with_fake_records(dev)
-        test_records_spanning_many_chunks(dev)
-        test_corruption_at_every_position_class(dev)
-    finally:
-        if old is None:
-            os.environ.pop("SKV_SPAN", None)
-        else:
-            os.environ["SKV_SPAN"] = old
 
 
 def test_device_resident_entry_point(dev):

@@ -163,3 +163,25 @@ def test_multi_two_ctxs_on_one_gpu():
             assert [r.data for r in f.result()] == [r.data for r in pyoracle.compact(streams, mx, fl)]
         with pytest.raises(_abi.RunError):
             futs[-1].result()
+
+
+@pytest.mark.gpu
+def test_concurrent_ctxs_with_different_fan_in():
+    """Two ctxs on one GPU running fused-path compactions of different fan-in k at the same time:
+    the fused tile's LDS size and resident-tile count depend on k, and the host caches of both
+    (the kernel's LDS limit, the per-(device, k) slot count) are shared by every ctx. Each job's
+    output must equal the oracle's, and every job must have taken the fused path."""
+    torch = pytest.importorskip("torch")
+    torch.cuda.init()
+    jobs = [(gen.config2(seed=100 + s, n_streams=(6 if s % 2 else 96), n_records=3000 if s % 2 else 400, vsize=40,
+                         variant="B"), 64 << 10, 0) for s in range(16)]
+
+    def path(comp, res):
+        return res, comp.timings()["path"]
+
+    with MultiCompactor([0, 0]) as mc:
+        futs = [mc.submit(*j, then=path) for j in jobs]
+        for f, (streams, mx, fl) in zip(futs, jobs):
+            runs, p = f.result()
+            assert p == _abi.PATH_FUSED
+            assert [r.data for r in runs] == [r.data for r in pyoracle.compact(streams, mx, fl)]
