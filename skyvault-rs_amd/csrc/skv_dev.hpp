@@ -240,6 +240,14 @@ struct FxArgs {
     const ulong2* keys;           // SKV_FX_DIAG=4 builds only: every record's (hi, lo) key, by record
                                   // index, written before the tiles (the tiles read no record heads)
 };
+// Higher sample levels written by k_fx_sample itself: level-1 sample c of stream j is also level
+// 2's sample c / Sstep when Sstep divides c (and level 3's when Sstep^2 does) -- the same element
+// (key, K << 32 | record) that k_sample would copy from level 1, without its launch per level
+struct FxUpLevels {
+    uint64_t *hi[2], *lo[2], *c[2];
+    const uint64_t* off[2];  // per-stream offsets of the level (k + 1)
+    uint32_t n;              // levels written (0..2)
+};
 // flags[3] reason bits of a poisoned fused call
 enum : uint32_t { FXR_RECORD = 1, FXR_OVERSIZE = 2, FXR_SPLIT = 4, FXR_ORDER = 8, FXR_SAMPLE = 16 };
 

@@ -138,14 +138,29 @@ FxArgs fx_launch(skv_ctx* ctx, uint32_t k, uint32_t n_runs, const RunInfo* d_run
     mark(ctx, PH_PARSE);
     for (size_t li = 1; li < lv.size(); ++li) {
         Level& L = lv[li];
-        const Level& P = lv[li - 1];
         char nm[64];
         snprintf(nm, sizeof nm, "lv%d_hi", (int)li); L.hi = dbuf<uint64_t>(ctx, nm, L.N);
         snprintf(nm, sizeof nm, "lv%d_lo", (int)li); L.lo = dbuf<uint64_t>(ctx, nm, L.N);
         snprintf(nm, sizeof nm, "lv%d_c", (int)li); L.c = dbuf<uint64_t>(ctx, nm, L.N);
         L.d_off = (uint64_t*)(d_blob + lv_off[li]);
-        if (li == 1) launch_fx_sample(st, A, L.d_off, L.S, L.N, L.hi, L.lo, L.c);
-        else launch_sample(st, false, P.hi, P.lo, P.c, nullptr, P.d_off, L.d_off, k, L.S, L.N, L.hi, L.lo, L.c);
+    }
+    // level 1 sampled from the run bytes; levels 2 and 3 written by the same launch (every level
+    // samples the one below with the same step S_step, so level li's sample c is level 1's sample
+    // c * S_step^(li-1)); any higher level from the one below it
+    if (lv.size() > 1) {
+        FxUpLevels up{};
+        for (size_t li = 2; li < lv.size() && up.n < 2; ++li, ++up.n) {
+            up.hi[up.n] = lv[li].hi;
+            up.lo[up.n] = lv[li].lo;
+            up.c[up.n] = lv[li].c;
+            up.off[up.n] = lv[li].d_off;
+        }
+        launch_fx_sample(st, A, lv[1].d_off, lv[1].S, lv[1].N, lv[1].hi, lv[1].lo, lv[1].c, up);
+        for (size_t li = 2 + up.n; li < lv.size(); ++li) {
+            const Level& P = lv[li - 1];
+            Level& L = lv[li];
+            launch_sample(st, false, P.hi, P.lo, P.c, nullptr, P.d_off, L.d_off, k, L.S, L.N, L.hi, L.lo, L.c);
+        }
     }
     for (int li = (int)lv.size() - 1; li >= 1; --li) {
         Level& L = lv[li];

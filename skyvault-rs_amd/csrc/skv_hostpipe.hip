@@ -531,6 +531,75 @@ static bool cut_runs(const Job& job, const std::vector<std::string>& cut, uint64
     return true;
 }
 
+// Cuts of a WAL flush of very many small runs (config 5: 10^6 runs of 83 records): each run is taken
+// as fixed-stride at its first record's size S (record i at 1 + i S) and cut by a binary search over
+// record indices, 32 runs in lockstep per thread with every probe's line prefetched one step ahead.
+// Nothing here is trusted: a cut that is not a record boundary fails its part's decode (the slices
+// are parsed from a true start), and the parts' records are checked to lie inside their key ranges
+// (wal_part_in_range) -- either way the serial path runs. False: a run whose first record does not
+// decode or whose length is not a multiple of it, or a probe whose key would leave the run.
+static bool cut_runs_fixed(const Job& job, const std::vector<std::string>& cut, uint64_t P, std::vector<uint64_t>& bnd) {
+    const uint64_t nr = job.run_ptr.size();
+    bnd.assign((P + 1) * nr, 0);
+    const unsigned nb = par_nblocks(nr, 1u << 12);
+    std::vector<uint8_t> ok(nb, 1);
+    par_run(nr, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+        constexpr int G = 32;
+        const uint8_t* rb[G];
+        uint64_t len[G], S[G], n[G], l[G], h[G];
+        for (uint64_t m0 = lo; m0 < hi && ok[b]; m0 += G) {
+            const int g = (int)std::min<uint64_t>(G, hi - m0);
+            for (int i = 0; i < g; ++i) {
+                rb[i] = (const uint8_t*)(uintptr_t)job.run_ptr[m0 + i];
+                len[i] = job.run_len[m0 + i];
+                __builtin_prefetch(rb[i] + 1);
+            }
+            for (int i = 0; i < g; ++i) {
+                const uint64_t m = m0 + i;
+                bnd[m] = 1;
+                bnd[P * nr + m] = len[i];
+                S[i] = len[i] > 1 ? host_rec_at(rb[i], len[i], 1) : 1;
+                if (!S[i] || (len[i] - 1) % S[i]) {
+                    ok[b] = 0;
+                    return;
+                }
+                n[i] = (len[i] - 1) / S[i];
+                l[i] = 0;
+            }
+            for (uint64_t p = 1; p < P; ++p) {
+                const std::string& c = cut[p - 1];
+                for (int i = 0; i < g; ++i) h[i] = n[i];  // l: the previous cut's index
+                for (;;) {
+                    bool any = false;
+                    for (int i = 0; i < g; ++i)
+                        if (l[i] < h[i]) {
+                            const uint8_t* q = rb[i] + 1 + ((l[i] + h[i]) >> 1) * S[i];
+                            __builtin_prefetch(q);
+                            __builtin_prefetch(q + 40);
+                            any = true;
+                        }
+                    if (!any) break;
+                    for (int i = 0; i < g; ++i)
+                        if (l[i] < h[i]) {
+                            const uint64_t mid = (l[i] + h[i]) >> 1, q = 1 + mid * S[i];
+                            const uint64_t kl = be32(rb[i] + q + 1);
+                            if (kl + 5 > S[i]) {  // not a record of size S here: no key to compare
+                                ok[b] = 0;
+                                return;
+                            }
+                            if (host_key_cmp(rb[i] + q + 5, kl, (const uint8_t*)c.data(), c.size()) < 0) l[i] = mid + 1;
+                            else h[i] = mid;
+                        }
+                }
+                for (int i = 0; i < g; ++i) bnd[p * nr + m0 + i] = 1 + l[i] * S[i];
+            }
+        }
+    });
+    for (uint8_t o : ok)
+        if (!o) return false;
+    return true;
+}
+
 // A stream of several member runs (an L0 or next-level concatenation, table_buffer_compaction.rs:
 // 66-100, table_tree_compaction.rs:103-135) is cut member by member; that is a key range of the
 // stream only when the concatenation ascends: every record of member i below member i + 1's first
@@ -566,6 +635,25 @@ static bool members_ascend(const Job& job) {
     return true;
 }
 
+// The keys of a WAL part's output all lie in [lo, hi) (null: unbounded): its first run's min key
+// and its last run's max key, each the table's canonical prefix "{id}." (every key of a part has
+// one, WAL_STRICT_CANON) + the stripped key in the output bytes (pout: the part's output in HBM).
+// Runs are in key order, so those two bound every key of the part.
+static bool wal_part_in_range(skv_ctx* ctx, const skv_result* pres, const uint8_t* pout, const std::string* lo,
+                              const std::string* hi) {
+    if (!pres->n_runs) return true;
+    const skv_run_desc& f = pres->runs[0];
+    const skv_run_desc& l = pres->runs[pres->n_runs - 1];
+    if (f.min_key_len > (1u << 20) || l.max_key_len > (1u << 20)) return false;
+    uint8_t* hp = (uint8_t*)pinned(ctx, f.min_key_len + l.max_key_len + 16);
+    d2h(ctx, hp, pout + f.min_key_off, f.min_key_len);  // (copy kernels here: no DMA queue behind egress)
+    d2h(ctx, hp + f.min_key_len, pout + l.max_key_off, l.max_key_len);
+    sync(ctx);
+    const std::string mn = std::to_string(f.table_id) + "." + std::string((const char*)hp, f.min_key_len);
+    const std::string mx = std::to_string(l.table_id) + "." + std::string((const char*)hp + f.min_key_len, l.max_key_len);
+    return (!lo || *lo <= mn) && (!hi || mx < *hi);
+}
+
 static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** out, double t_entry, bool& used) {
     used = false;
     const char* pe = getenv("SKV_HOST_PIPE");
@@ -577,11 +665,12 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     const bool wal = (job.flags & SKV_SPLIT_BY_TABLE) != 0;
     if (job.in_bytes < min_bytes || job.batch || job.search || job.scan) return SKV_OK;
     if (k == 0 || nr == 0) return SKV_OK;
-    // Past 2^16 member runs the host's cut search costs what the transfers do: every run is walked up
-    // to its last cut (10^6 config-5 runs: 125-147 ms on 8 threads by a walk or a batched binary
-    // search, measured on a host harness, against ~80 ms for the whole H2D), so such calls (a WAL
-    // flush of 10^6 tiny runs) take the serial path.
-    if (nr > (1u << 16)) return SKV_OK;
+    // Past 2^16 member runs (a WAL flush of 10^6 tiny runs) a walk of every run up to its last cut
+    // costs what the transfers do (125-147 ms on 8 threads for config 5, against ~80 ms for the whole
+    // H2D): such flushes are cut by the fixed-stride search (cut_runs_fixed) and every part's key range
+    // is checked after it (wal_part_in_range); other calls that large take the serial path.
+    const bool many = nr > (1u << 16);
+    if (many && !wal) return SKV_OK;
     // parts of ~1 GiB: each part costs a DMA copy per slice (config 3, 3.7 GiB: 4 parts 99.8 ms, 6
     // parts 102.9, 8 parts 105.0, 10 parts 110.5)
     uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(32, job.in_bytes / (1ull << 30)));
@@ -637,7 +726,7 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     if (P < 2 || (!wal && job.max_run_size > job.in_bytes / (4 * P))) return SKV_OK;
     // ---- bnd[p * nr + m]: byte offset of run m's first record >= cut p (1 / len at the ends)
     std::vector<uint64_t> bnd;
-    if (!cut_runs(job, cut, P, bnd)) {
+    if (!(many ? cut_runs_fixed(job, cut, P, bnd) : cut_runs(job, cut, P, bnd))) {
         htrace("gpipe: a cut not found");
         return SKV_OK;
     }
@@ -887,6 +976,14 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
             return SKV_OK;
         }
         const uint64_t n = pres->n_runs;
+        if (many && !wal_part_in_range(ctx, pres, d_out + wal_off, p == 0 ? nullptr : &cut[p - 1],
+                                       last_part ? nullptr : &cut[p])) {
+            skv_result_free(pres);
+            htrace("gpipe: a part's keys outside its range");
+            drain(ctx);
+            used = false;
+            return SKV_OK;
+        }
         if (wal) {
             // whole tables: every run of the part is final at its offset in the call's output
             for (uint64_t r = 0; r < n; ++r) {

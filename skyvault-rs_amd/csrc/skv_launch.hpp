@@ -117,7 +117,7 @@ void launch_wal_sendfail(hipStream_t, const uint64_t* NTp, uint64_t max_NT, cons
                          const unsigned long long* tfirst, unsigned long long* first_fail);
 // skv_stride.hip — fused stride path
 void launch_fx_sample(hipStream_t, const FxArgs& A, const uint64_t* off_dst, uint64_t Sstep, uint64_t n_dst,
-                      uint64_t* dhi, uint64_t* dlo, uint64_t* dc);
+                      uint64_t* dhi, uint64_t* dlo, uint64_t* dc, const FxUpLevels& up);
 void launch_fx_l1cnt(hipStream_t, const FxArgs& A, const uint64_t* sc, uint64_t N1, uint32_t* posof, uint32_t* cnt);
 void launch_fx_bounds(hipStream_t, const FxArgs& A, const uint64_t* shi, const uint64_t* slo, uint64_t m,
                       const uint64_t* l1hi, const uint64_t* l1lo, const uint64_t* l1off, uint64_t Sstep);

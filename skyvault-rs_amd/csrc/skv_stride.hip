@@ -204,7 +204,7 @@ __device__ __forceinline__ void fx_poison(const FxArgs& A, uint32_t why) {
 // k_tile<false>). Samples out of order inside a stream poison the call before any sample tile
 // merges them (a merge of unsorted lists is not a permutation).
 __global__ void k_fx_sample(FxArgs A, const uint64_t* __restrict__ off_dst, uint64_t Sstep, uint64_t n_dst,
-                            uint64_t* dhi, uint64_t* dlo, uint64_t* dc) {
+                            uint64_t* dhi, uint64_t* dlo, uint64_t* dc, FxUpLevels up) {
     extern __shared__ uint64_t fx_offs[];  // off_dst[0..k], staged once per workgroup
     for (uint32_t x = threadIdx.x; x <= A.k; x += blockDim.x) fx_offs[x] = off_dst[x];
     __syncthreads();
@@ -223,6 +223,14 @@ __global__ void k_fx_sample(FxArgs A, const uint64_t* __restrict__ off_dst, uint
         dhi[i] = h;
         dlo[i] = l;
         dc[i] = ((uint64_t)A.K << 32) | pos;
+        uint64_t c = i - fx_offs[lo];  // this stream's sample index at level 1, then 2
+        for (uint32_t u = 0; u < up.n && c % Sstep == 0; ++u) {
+            c /= Sstep;
+            const uint64_t q = up.off[u][lo] + c;
+            up.hi[u][q] = h;
+            up.lo[u][q] = l;
+            up.c[u][q] = ((uint64_t)A.K << 32) | pos;
+        }
     }
     // per-stream sample order: sample i-1 of the same stream is the previous lane's key (one load
     // per sample; the first lane of each wave loads its predecessor itself)
@@ -1304,8 +1312,8 @@ __global__ void __launch_bounds__(256) k_ingest_slices(const IngestSlice* __rest
 static inline unsigned fx_blocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 void launch_fx_sample(hipStream_t s, const FxArgs& A, const uint64_t* off_dst, uint64_t Sstep, uint64_t n_dst,
-                      uint64_t* dhi, uint64_t* dlo, uint64_t* dc) {
-    if (n_dst) k_fx_sample<<<fx_blocks(n_dst, 256), 256, (A.k + 1) * 8, s>>>(A, off_dst, Sstep, n_dst, dhi, dlo, dc);
+                      uint64_t* dhi, uint64_t* dlo, uint64_t* dc, const FxUpLevels& up) {
+    if (n_dst) k_fx_sample<<<fx_blocks(n_dst, 256), 256, (A.k + 1) * 8, s>>>(A, off_dst, Sstep, n_dst, dhi, dlo, dc, up);
 }
 void launch_fx_l1cnt(hipStream_t s, const FxArgs& A, const uint64_t* sc, uint64_t N1, uint32_t* posof, uint32_t* cnt) {
     if (!N1) return;

@@ -435,3 +435,34 @@ def test_config3_full_size(dev, torch, cfg3_full, flags):
     if flags:
         assert all(d[3] == 0 for d in descs)
     res.free()
+
+
+def test_config5_host_entry_full_size(dev, torch):
+    """config 5 through skv_compact with the 10^6 WAL runs in pinned host memory (storage.rs:183-250
+    get_run -> compact -> put_run, wal_compaction.rs:18-51): past 2^16 runs the flush is cut by the
+    fixed-stride search and pipelined (host_parts > 0, the GPU ingests the parts' slices itself);
+    bytes and descriptors equal to the per-table-group oracle at both max sizes."""
+    from skv.devgen import make_cfg5_on_device
+
+    n_streams = 1_000_000
+    buf = make_cfg5_on_device(torch.device("cuda", 0), SEED + 5, n_streams)
+    host_t = buf.cpu().pin_memory()
+    del buf
+    rl = host_t.shape[1]
+    sa = _abi.stream_table(np.arange(1, n_streams + 1), host_t.data_ptr() + rl * np.arange(n_streams, dtype=np.uint64),
+                           np.full(n_streams, rl))
+    host = host_t.numpy()
+    for max_run in (1 << 62, MAX_RUN):
+        _progress(f"config 5 host entry max {max_run}: device")
+        hr = dev.compact_host(sa, max_run, _abi.SKV_SPLIT_BY_TABLE)
+        t = dev.timings()
+        assert t["host_parts"] >= 2, t
+        _progress(f"config 5 host entry: {t['host_parts']} parts; oracle")
+        exp, descs, dropped, out_records = _wal_oracle(host, max_run)
+        raw = hr._res.contents
+        assert (hr.n_bytes, hr.n_runs, raw.dropped_tables, hr.out_records) == (exp.size, len(descs), dropped, out_records)
+        if exp.size:
+            got = hr.host_bytes(0, exp.size)
+            assert np.array_equal(got, exp), f"config 5 host entry: byte {_first_diff(got, exp)} differs"
+        assert hr.descs == descs
+        hr.free()

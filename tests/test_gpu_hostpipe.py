@@ -423,6 +423,53 @@ def test_wal_flush_of_many_tiny_runs_kernel_ingest(dev, pipe_env):
     assert [r.table_id for r in got] == [r.table_id for r in exp]
 
 
+def _pinned_wal(torch, runs):
+    blob = b"".join(runs)
+    t = torch.empty(len(blob), dtype=torch.uint8).pin_memory()
+    t[:] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+    offs = np.cumsum([0] + [len(r) for r in runs[:-1]])
+    return t, [(s + 1, [(t.data_ptr() + int(o), len(r))]) for s, (o, r) in enumerate(zip(offs, runs))]
+
+
+def test_wal_flush_past_the_walk_threshold(dev, pipe_env):
+    """more than 2^16 WAL runs: cut by the fixed-stride search (each run's records at its first
+    record's size; a binary search per cut), every part's keys checked against its range. Runs of
+    one record size per run (sizes differ between runs), empty runs (a version byte only), Deletes
+    among Puts of the same size; then runs the fixed-stride hypothesis does not fit -- a length that
+    is not a multiple of the first record (the search declines at once), and variable sizes whose
+    total is a multiple of the first (the probes land inside records: a part's decode or its range
+    check fails) -- which take the serial path. Every outcome equal to the oracle's."""
+    torch = pytest.importorskip("torch")
+    rng = random.Random(903)
+    tables = [str(t) for t in range(-5, 60)]
+    runs = []
+    for s in range(70000):
+        if s % 9973 == 5:
+            runs.append(b"\x01")
+            continue
+        keys = sorted({f"{rng.choice(tables)}.{rng.randrange(10 ** 6):06d}" for _ in range(rng.randint(1, 6))})
+        vl = 3 + s % 5
+        runs.append(fmt.encode_run([fmt.put(x + "x" * (11 - len(x)), bytes([s & 0xFF]) * vl) for x in keys]))
+    os.environ["SKV_HOST_PARTS"] = "5"
+    t, pstreams = _pinned_wal(torch, runs)
+    got = dev.compact_host_ptrs(pstreams, 1 << 40, _abi.SKV_SPLIT_BY_TABLE, with_runs=True)
+    assert 2 <= dev.timings()["host_parts"] <= 5
+    exp = pyoracle.compact([(s + 1, [r]) for s, r in enumerate(runs)], 1 << 40, _abi.SKV_SPLIT_BY_TABLE)
+    assert _norm(got) == _norm(exp)
+    # keys padded to one length above, so a Put and a Delete differ in size: a run mixing them
+    mixed = [fmt.put("3.aaaaaaaaaa", b"vvvv"), fmt.delete("3.aaaaaaaaab"), fmt.put("3.aaaaaaaaac", b"vvvv")]
+    # sizes 30, 20, 40: the total (90) is a multiple of the first record's 30
+    odd = fmt.encode_run([fmt.put("4.a", b"v" * 18), fmt.put("4.b", b"v" * 8), fmt.put("4.c", b"v" * 28)])
+    assert len(odd) == 91
+    for extra in ([fmt.encode_run(mixed)], [odd] * 3):
+        bad = runs[:40000] + extra + runs[40000:]
+        t2, p2 = _pinned_wal(torch, bad)
+        got = dev.compact_host_ptrs(p2, 1 << 40, _abi.SKV_SPLIT_BY_TABLE, with_runs=True)
+        assert dev.timings()["host_parts"] == 0
+        exp = pyoracle.compact([(s + 1, [r]) for s, r in enumerate(bad)], 1 << 40, _abi.SKV_SPLIT_BY_TABLE)
+        assert _norm(got) == _norm(exp)
+
+
 @pytest.mark.parametrize("order", ["ascending", "descending", "mixed"])
 def test_serial_path_stages_host_contiguous_runs_as_spans(dev, order):
     """the serial host path (SKV_HOST_PIPE=0) stages runs that tile one host buffer with one copy
