@@ -428,7 +428,9 @@ def main():
     # PCIe-inclusive figure (not `value`): the host entry point skv_compact with the inputs in
     # pinned host memory and the output runs returned in pinned host memory.
     host_path = None
-    if rank == 0 and world == 1 and not args.no_host_path and config != "3F":  # 3F: 64 GB of pinned host memory
+    # 3F at its full 256 MiB runs would pin 64 GB of host memory: its host figure is taken on runs of
+    # at most 64 MiB (--run-mib 64: 256 x 64 MiB = 16 GiB pinned)
+    if rank == 0 and world == 1 and not args.no_host_path and not (config == "3F" and run_mib_used > 64):
         if config == "5":  # one pinned buffer of 10^6 WAL runs; the stream table built once
             host_runs = [buf.cpu().pin_memory()]
             hb0 = host_runs[0].data_ptr()
@@ -532,12 +534,14 @@ def main():
             with open(args.traffic_json) as f:
                 cfgs = json.load(f).get("configs", {})
             kt = cfgs.get(config, {}).get("kernels", {}).get("skv::" + hot_kernel)
+            if config == "3F" and run_mib_used != 256:  # the recorded 3F pass is at 256 MiB runs
+                kt, traffic_note = None, f"no --pmc pass recorded for config 3F at {run_mib_used} MiB runs"
             if kt:
                 traffic = kt["hbm_bytes"]
                 traffic_rw = {"read_bytes": kt["read_bytes"], "write_bytes": kt["write_bytes"],
                               "ratio_to_algorithmic": round(kt["hbm_bytes"] / max(1, gread + gwrite), 3),
                               "source": os.path.relpath(args.traffic_json, ROOT) + f" [configs][{config}]"}
-            else:
+            elif traffic_note is None:
                 traffic_note = f"no --pmc pass recorded for config {config} / {hot_kernel} in {args.traffic_json}"
         except (OSError, ValueError) as e:
             traffic_note = f"traffic file unreadable: {e}"

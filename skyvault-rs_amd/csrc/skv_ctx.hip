@@ -605,6 +605,7 @@ void skv_ctx_destroy(skv_ctx* ctx) {
     for (auto& kv : ctx->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    if (ctx->sl_host) (void)hipHostFree(ctx->sl_host);
     for (auto& c : ctx->up_chunks) (void)hipHostFree(c.first);
     for (int i = 0; i < PH_N; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);

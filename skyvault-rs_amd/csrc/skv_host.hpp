@@ -130,6 +130,8 @@ struct skv_ctx {
     std::vector<hipEvent_t> part_ev;
     uint64_t* part_k = nullptr;
     size_t part_k_cap = 0;
+    void* sl_host = nullptr;  // pinned slice tables of a pipelined call's kernel ingest
+    size_t sl_cap = 0;
     // while a pipelined host call has copies queued on in_stream / out_stream, a buffer that grows
     // keeps its old allocation here until the call has drained (hipFree waits for the whole device,
     // which would serialise the pipeline behind every queued copy)

@@ -532,67 +532,114 @@ static bool cut_runs(const Job& job, const std::vector<std::string>& cut, uint64
 }
 
 // Cuts of a WAL flush of very many small runs (config 5: 10^6 runs of 83 records): each run is taken
-// as fixed-stride at its first record's size S (record i at 1 + i S) and cut by a binary search over
-// record indices, 32 runs in lockstep per thread with every probe's line prefetched one step ahead.
+// as fixed-stride at its first record's size S (record i at 1 + i S); a cut row is found per run by
+// galloping from the position the cut's sample quantile predicts (i0 = frac * records: the cuts are
+// quantiles of evenly spaced samples, so a run's bound lies within a few records of it), touching
+// two or three neighbouring lines instead of a binary search's seven scattered ones. Rows are found
+// one at a time, each while the GPU ingests the part before (the pipeline below).
 // Nothing here is trusted: a cut that is not a record boundary fails its part's decode (the slices
 // are parsed from a true start), and the parts' records are checked to lie inside their key ranges
-// (wal_part_in_range) -- either way the serial path runs. False: a run whose first record does not
-// decode or whose length is not a multiple of it, or a probe whose key would leave the run.
-static bool cut_runs_fixed(const Job& job, const std::vector<std::string>& cut, uint64_t P, std::vector<uint64_t>& bnd) {
+// (wal_part_in_range) -- either way the serial path runs.
+struct FixedRuns {
+    std::vector<uint64_t> S, n;  // per run: the first record's size, records (len - 1) / S
+};
+// false: a run whose first record does not decode or whose length is not a multiple of it
+static bool fixed_prep(const Job& job, FixedRuns& F) {
     const uint64_t nr = job.run_ptr.size();
-    bnd.assign((P + 1) * nr, 0);
+    F.S.resize(nr);
+    F.n.resize(nr);
     const unsigned nb = par_nblocks(nr, 1u << 12);
     std::vector<uint8_t> ok(nb, 1);
     par_run(nr, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
-        constexpr int G = 32;
-        const uint8_t* rb[G];
-        uint64_t len[G], S[G], n[G], l[G], h[G];
-        for (uint64_t m0 = lo; m0 < hi && ok[b]; m0 += G) {
-            const int g = (int)std::min<uint64_t>(G, hi - m0);
-            for (int i = 0; i < g; ++i) {
-                rb[i] = (const uint8_t*)(uintptr_t)job.run_ptr[m0 + i];
-                len[i] = job.run_len[m0 + i];
-                __builtin_prefetch(rb[i] + 1);
+        constexpr uint64_t AHEAD = 16;
+        for (uint64_t m = lo; m < hi && m < lo + AHEAD; ++m) __builtin_prefetch((const uint8_t*)(uintptr_t)job.run_ptr[m] + 1);
+        for (uint64_t m = lo; m < hi; ++m) {
+            if (m + AHEAD < hi) __builtin_prefetch((const uint8_t*)(uintptr_t)job.run_ptr[m + AHEAD] + 1);
+            const uint8_t* rb = (const uint8_t*)(uintptr_t)job.run_ptr[m];
+            const uint64_t len = job.run_len[m];
+            const uint64_t sz = len > 1 ? host_rec_at(rb, len, 1) : 1;
+            if (!sz || (len - 1) % sz) {
+                ok[b] = 0;
+                return;
             }
-            for (int i = 0; i < g; ++i) {
-                const uint64_t m = m0 + i;
-                bnd[m] = 1;
-                bnd[P * nr + m] = len[i];
-                S[i] = len[i] > 1 ? host_rec_at(rb[i], len[i], 1) : 1;
-                if (!S[i] || (len[i] - 1) % S[i]) {
-                    ok[b] = 0;
-                    return;
+            F.S[m] = sz;
+            F.n[m] = (len - 1) / sz;
+        }
+    });
+    for (uint8_t o : ok)
+        if (!o) return false;
+    return true;
+}
+// row[m] = byte offset of run m's first record >= c, at or after prev[m] (both 1 + i S);
+// false: a probed record whose key would not fit a record of size S (not a record start)
+static bool fixed_row(const Job& job, const FixedRuns& F, const std::string& c, double frac, const uint64_t* prev,
+                      uint64_t* row) {
+    const uint64_t nr = job.run_ptr.size();
+    const unsigned nb = par_nblocks(nr, 1u << 12);
+    std::vector<uint8_t> ok(nb, 1);
+    par_run(nr, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
+        constexpr uint64_t AHEAD = 16;
+        auto start = [&](uint64_t m) {
+            const uint64_t a = (prev[m] - 1) / F.S[m];
+            const uint64_t g = std::min<uint64_t>(F.n[m], std::max<uint64_t>(a, (uint64_t)(frac * (double)F.n[m] + 0.5)));
+            return g;
+        };
+        for (uint64_t m = lo; m < hi && m < lo + AHEAD; ++m)
+            __builtin_prefetch((const uint8_t*)(uintptr_t)job.run_ptr[m] + 1 + start(m) * F.S[m]);
+        for (uint64_t m = lo; m < hi; ++m) {
+            if (m + AHEAD < hi)
+                __builtin_prefetch((const uint8_t*)(uintptr_t)job.run_ptr[m + AHEAD] + 1 + start(m + AHEAD) * F.S[m + AHEAD]);
+            const uint8_t* rb = (const uint8_t*)(uintptr_t)job.run_ptr[m];
+            const uint64_t S = F.S[m], n = F.n[m], a = (prev[m] - 1) / S;
+            bool bad = false;
+            auto below = [&](uint64_t i) {  // record i's key < c
+                const uint64_t q = 1 + i * S, kl = be32(rb + q + 1);
+                if (kl + 5 > S) {
+                    bad = true;
+                    return false;
                 }
-                n[i] = (len[i] - 1) / S[i];
-                l[i] = 0;
-            }
-            for (uint64_t p = 1; p < P; ++p) {
-                const std::string& c = cut[p - 1];
-                for (int i = 0; i < g; ++i) h[i] = n[i];  // l: the previous cut's index
-                for (;;) {
-                    bool any = false;
-                    for (int i = 0; i < g; ++i)
-                        if (l[i] < h[i]) {
-                            const uint8_t* q = rb[i] + 1 + ((l[i] + h[i]) >> 1) * S[i];
-                            __builtin_prefetch(q);
-                            __builtin_prefetch(q + 40);
-                            any = true;
-                        }
-                    if (!any) break;
-                    for (int i = 0; i < g; ++i)
-                        if (l[i] < h[i]) {
-                            const uint64_t mid = (l[i] + h[i]) >> 1, q = 1 + mid * S[i];
-                            const uint64_t kl = be32(rb[i] + q + 1);
-                            if (kl + 5 > S[i]) {  // not a record of size S here: no key to compare
-                                ok[b] = 0;
-                                return;
-                            }
-                            if (host_key_cmp(rb[i] + q + 5, kl, (const uint8_t*)c.data(), c.size()) < 0) l[i] = mid + 1;
-                            else h[i] = mid;
-                        }
+                return host_key_cmp(rb + q + 5, kl, (const uint8_t*)c.data(), c.size()) < 0;
+            };
+            // the bound: the first i in [a, n] with i == n or !below(i); gallop from the guess
+            uint64_t g = start(m), l, h;  // invariant: every i < l is below, none of [h, n) is
+            if (g < n && below(g)) {
+                l = g + 1;
+                uint64_t step = 1;
+                h = n;
+                while (l + step - 1 < n && !bad) {
+                    const uint64_t x = l + step - 1;
+                    if (below(x)) {
+                        l = x + 1;
+                        step <<= 1;
+                    } else {
+                        h = x;
+                        break;
+                    }
                 }
-                for (int i = 0; i < g; ++i) bnd[p * nr + m0 + i] = 1 + l[i] * S[i];
+            } else {
+                h = g;
+                l = a;
+                uint64_t step = 1;
+                while (h > a + step - 1 && !bad) {
+                    const uint64_t x = h - step;
+                    if (below(x)) {
+                        l = x + 1;
+                        break;
+                    }
+                    h = x;
+                    step <<= 1;
+                }
             }
+            while (l < h && !bad) {
+                const uint64_t mid = (l + h) >> 1;
+                if (below(mid)) l = mid + 1;
+                else h = mid;
+            }
+            if (bad) {
+                ok[b] = 0;
+                return;
+            }
+            row[m] = 1 + l * S;
         }
     });
     for (uint8_t o : ok)
@@ -669,8 +716,15 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     // costs what the transfers do (125-147 ms on 8 threads for config 5, against ~80 ms for the whole
     // H2D): such flushes are cut by the fixed-stride search (cut_runs_fixed) and every part's key range
     // is checked after it (wal_part_in_range); other calls that large take the serial path.
+    // Measured (round 5, profiles/r05/c5_host.txt): at config 5 the parts' slices (10^6 per part)
+    // can only be ingested by the GPU reading pinned memory, which moves ~26-30 GB/s against ~56 GB/s
+    // for one DMA copy of the whole input, so the pipeline (235-300 ms) loses to the serial path
+    // (169 ms) on the boxes measured: it runs only with SKV_HOST_PIPE_MANY=1.
     const bool many = nr > (1u << 16);
-    if (many && !wal) return SKV_OK;
+    if (many) {
+        const char* me2 = getenv("SKV_HOST_PIPE_MANY");
+        if (!wal || !(me2 && me2[0] == '1')) return SKV_OK;
+    }
     // parts of ~1 GiB: each part costs a DMA copy per slice (config 3, 3.7 GiB: 4 parts 99.8 ms, 6
     // parts 102.9, 8 parts 105.0, 10 parts 110.5)
     uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(32, job.in_bytes / (1ull << 30)));
@@ -726,7 +780,20 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     if (P < 2 || (!wal && job.max_run_size > job.in_bytes / (4 * P))) return SKV_OK;
     // ---- bnd[p * nr + m]: byte offset of run m's first record >= cut p (1 / len at the ends)
     std::vector<uint64_t> bnd;
-    if (!(many ? cut_runs_fixed(job, cut, P, bnd) : cut_runs(job, cut, P, bnd))) {
+    FixedRuns fixed;
+    if (many) {  // rows 0 and P now, row 1 before part 0's slices, row p + 1 while part p - 1 lands
+        if (!fixed_prep(job, fixed)) {
+            htrace("gpipe: a run is not fixed-stride");
+            return SKV_OK;
+        }
+        bnd.assign((P + 1) * nr, 1);
+        for (uint64_t m = 0; m < nr; ++m) bnd[P * nr + m] = job.run_len[m];
+        if (!fixed_row(job, fixed, cut[0], 1.0 / (double)P, bnd.data(), bnd.data() + nr)) {
+            htrace("gpipe: a cut not found");
+            return SKV_OK;
+        }
+        htrace("gpipe: first cut row");
+    } else if (!cut_runs(job, cut, P, bnd)) {
         htrace("gpipe: a cut not found");
         return SKV_OK;
     }
@@ -740,8 +807,12 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     // 130 vs 105 ms: part 0's kernels waited behind the later parts' ingest); a WAL flush of 10^6 tiny
     // runs has millions of slices, each a DMA descriptor with its own fixed cost.
     uint64_t n_slices = 0;
-    for (uint64_t p = 0; p < P; ++p)
-        for (uint64_t m = 0; m < nr; ++m) n_slices += bnd[(p + 1) * nr + m] > bnd[p * nr + m];
+    if (many) {
+        n_slices = P * nr;  // (an upper bound: the rows after the first are not found yet)
+    } else {
+        for (uint64_t p = 0; p < P; ++p)
+            for (uint64_t m = 0; m < nr; ++m) n_slices += bnd[(p + 1) * nr + m] > bnd[p * nr + m];
+    }
     std::vector<uint64_t> hdev;
     bool kernel_ingest = n_slices > (1u << 15);
     {
@@ -818,23 +889,26 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
             if (buf) c->out_pool->give(buf, cap);
         }
     } out_guard{ctx, h_out, cap};
-    // ---- ingest: every part's slices, in part order, on in_stream
+    // ---- ingest: every part's slices, in part order, on in_stream. Kernel ingest: part p's slice
+    // table is built on the host pool into the ctx's pinned slice arena and goes up on in_stream right
+    // before part p's ingest launch; a call past 2^16 runs finds cut row p + 1 first, while the GPU
+    // ingests part p - 1.
     IngestSlice* d_sl = nullptr;
     std::vector<uint64_t> sl_base(P + 1, 0);
+    IngestSlice* h_sl = nullptr;
     if (kernel_ingest) {
-        std::vector<IngestSlice> hsl;
-        hsl.reserve(n_slices);
-        for (uint64_t p = 0; p < P; ++p) {
-            sl_base[p] = hsl.size();
-            for (uint64_t m = 0; m < nr; ++m) {
-                const uint64_t lo = p == 0 ? 0 : bnd[p * nr + m], hi = bnd[(p + 1) * nr + m];
-                if (hi > lo) hsl.push_back(IngestSlice{hdev[m] + lo, (uint64_t)(uintptr_t)(d_in + img[m] + lo), hi - lo});
-            }
+        // capacity: one slice per (part, run) -- part 0's slices start at the version byte, so a run
+        // whose part-0 key range is empty still has one (n_slices does not count those)
+        d_sl = dbuf<IngestSlice>(ctx, "gp_slices", P * nr + 1);
+        const size_t need = (P * nr + 1) * sizeof(IngestSlice);
+        if (ctx->sl_cap < need) {
+            if (ctx->sl_host) ctx->host_graveyard.push_back(ctx->sl_host);  // (defer_free: kio above)
+            ctx->sl_host = nullptr;
+            ctx->sl_cap = 0;
+            HIPCHK(host_alloc_near(ctx->device, &ctx->sl_host, need, hipHostMallocDefault));
+            ctx->sl_cap = need;
         }
-        sl_base[P] = hsl.size();
-        d_sl = dbuf<IngestSlice>(ctx, "gp_slices", hsl.size() + 1);
-        HIPCHK(hipMemcpyAsync(d_sl, hsl.data(), hsl.size() * sizeof(IngestSlice), hipMemcpyHostToDevice, ctx->in_stream));
-        HIPCHK(hipStreamSynchronize(ctx->in_stream));  // (hsl is a local: the copy is from pageable memory)
+        h_sl = (IngestSlice*)ctx->sl_host;
     }
     // a few hundred ingest workgroups in all: the copies are bound by PCIe, and a grid that filled
     // every CU (8 per slice: 2,048 at config 3) held the part kernels off the GPU until the whole
@@ -842,8 +916,46 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     uint32_t igrid = 384;
     if (const char* be = getenv("SKV_INGEST_BLOCKS")) igrid = std::max<uint32_t>(1, (uint32_t)strtoul(be, nullptr, 10));
     for (uint64_t p = 0; p < P; ++p) {
+        if (many && p >= 1 && p + 1 < P) {
+            if (!fixed_row(job, fixed, cut[p], (double)(p + 1) / (double)P, &bnd[p * nr], &bnd[(p + 1) * nr])) {
+                htrace("gpipe: a cut not found");
+                drain(ctx);
+                used = false;
+                return SKV_OK;
+            }
+        }
         if (kernel_ingest) {
-            launch_ingest_slices(ctx->in_stream, d_sl + sl_base[p], sl_base[p + 1] - sl_base[p], igrid);
+            const unsigned nb = par_nblocks(nr, 1u << 14);
+            std::vector<uint64_t> cnt(nb + 1, 0);
+            auto slice = [&](uint64_t m, uint64_t& lo, uint64_t& hi) {
+                lo = p == 0 ? 0 : bnd[p * nr + m];
+                hi = bnd[(p + 1) * nr + m];
+            };
+            par_run(nr, nb, [&](unsigned b, uint64_t lo_m, uint64_t hi_m) {
+                uint64_t c = 0;
+                for (uint64_t m = lo_m; m < hi_m; ++m) {
+                    uint64_t lo, hi;
+                    slice(m, lo, hi);
+                    c += hi > lo;
+                }
+                cnt[b + 1] = c;
+            });
+            for (unsigned b = 0; b < nb; ++b) cnt[b + 1] += cnt[b];
+            sl_base[p + 1] = sl_base[p] + cnt[nb];
+            IngestSlice* out_sl = h_sl + sl_base[p];
+            par_run(nr, nb, [&](unsigned b, uint64_t lo_m, uint64_t hi_m) {
+                uint64_t at = cnt[b];
+                for (uint64_t m = lo_m; m < hi_m; ++m) {
+                    uint64_t lo, hi;
+                    slice(m, lo, hi);
+                    if (hi > lo) out_sl[at++] = IngestSlice{hdev[m] + lo, (uint64_t)(uintptr_t)(d_in + img[m] + lo), hi - lo};
+                }
+            });
+            const uint64_t ns = sl_base[p + 1] - sl_base[p];
+            if (ns)
+                HIPCHK(hipMemcpyAsync(d_sl + sl_base[p], out_sl, ns * sizeof(IngestSlice), hipMemcpyHostToDevice,
+                                      ctx->in_stream));
+            launch_ingest_slices(ctx->in_stream, d_sl + sl_base[p], ns, igrid);
             HIPCHK(hipGetLastError());
         } else {
             for (uint64_t m = 0; m < nr; ++m) {
@@ -853,6 +965,7 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
             }
         }
         HIPCHK(hipEventRecord(ctx->part_ev[2 * p], ctx->in_stream));
+        if (p == 0) htrace("gpipe: part 0 queued");
     }
     htrace("gpipe: ingest queued");
     // ---- egress thread: D2H of every byte range the parts finalize

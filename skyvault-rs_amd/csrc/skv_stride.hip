@@ -1308,6 +1308,33 @@ __global__ void __launch_bounds__(256) k_ingest_slices(const IngestSlice* __rest
     }
 }
 
+// The same with one slice per WAVE (slices of a WAL flush's parts are ~1 KiB: a workgroup per slice
+// left 3 of its 4 waves idle): each wave copies its slice's 16-byte blocks four per lane in flight.
+__global__ void __launch_bounds__(256) k_ingest_waves(const IngestSlice* __restrict__ sl, uint64_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t W = (uint64_t)gridDim.x * 4;
+    for (uint64_t y = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); y < n; y += W) {
+        const IngestSlice S = sl[y];
+        const uint8_t* src = (const uint8_t*)S.src;
+        uint8_t* dst = (uint8_t*)S.dst;
+        const uint64_t head = ((16 - (S.src & 15)) & 15) < S.len ? ((16 - (S.src & 15)) & 15) : S.len;
+        const uint64_t nb = (S.len - head) >> 4, tail0 = head + (nb << 4);
+        if (lane < head) dst[lane] = src[lane];
+        if (lane < S.len - tail0) dst[tail0 + lane] = src[tail0 + lane];
+        const uint4* s4 = (const uint4*)(src + head);
+        uint4* d4 = (uint4*)(dst + head);
+        uint64_t i = lane;
+        for (; i + 192 < nb; i += 256) {
+            const uint4 a = s4[i], b = s4[i + 64], c = s4[i + 128], d = s4[i + 192];
+            d4[i] = a;
+            d4[i + 64] = b;
+            d4[i + 128] = c;
+            d4[i + 192] = d;
+        }
+        for (; i < nb; i += 64) d4[i] = s4[i];
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 static inline unsigned fx_blocks(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
@@ -1355,7 +1382,10 @@ void launch_ingest(hipStream_t s, const IngestSlice* slices, uint32_t n, uint32_
     if (n) k_ingest<<<dim3(blocks_per_slice, n), 256, 0, s>>>(slices);
 }
 void launch_ingest_slices(hipStream_t s, const IngestSlice* slices, uint64_t n, uint32_t grid) {
-    if (n) k_ingest_slices<<<(unsigned)std::min<uint64_t>(n, grid ? grid : 1), 256, 0, s>>>(slices, n);
+    static const bool per_wg = getenv("SKV_INGEST_WG") && getenv("SKV_INGEST_WG")[0] == '1';  // A/B: a workgroup per slice
+    if (!n) return;
+    if (per_wg) k_ingest_slices<<<(unsigned)std::min<uint64_t>(n, grid ? grid : 1), 256, 0, s>>>(slices, n);
+    else k_ingest_waves<<<(unsigned)std::min<uint64_t>((n + 3) / 4, grid ? grid : 1), 256, 0, s>>>(slices, n);
 }
 void launch_copy_bytes(hipStream_t s, uint8_t* dst, const uint8_t* src, uint64_t n) {
     if (n) k_copy_bytes<<<fx_blocks((n + 15) / 16, 256), 256, 0, s>>>(dst, src, n);

@@ -432,13 +432,15 @@ def _pinned_wal(torch, runs):
 
 
 def test_wal_flush_past_the_walk_threshold(dev, pipe_env):
-    """more than 2^16 WAL runs: cut by the fixed-stride search (each run's records at its first
-    record's size; a binary search per cut), every part's keys checked against its range. Runs of
+    """more than 2^16 WAL runs, the many-run pipeline switched on (SKV_HOST_PIPE_MANY=1): cut by the
+    fixed-stride search (each run's records at its first record's size; per cut a gallop from the
+    cut's sample quantile), every part's keys checked against its range. Runs of
     one record size per run (sizes differ between runs), empty runs (a version byte only), Deletes
     among Puts of the same size; then runs the fixed-stride hypothesis does not fit -- a length that
     is not a multiple of the first record (the search declines at once), and variable sizes whose
     total is a multiple of the first (the probes land inside records: a part's decode or its range
-    check fails) -- which take the serial path. Every outcome equal to the oracle's."""
+    check fails) -- which take the serial path; and by default (the knob off) the serial path. Every
+    outcome equal to the oracle's."""
     torch = pytest.importorskip("torch")
     rng = random.Random(903)
     tables = [str(t) for t in range(-5, 60)]
@@ -452,6 +454,16 @@ def test_wal_flush_past_the_walk_threshold(dev, pipe_env):
         runs.append(fmt.encode_run([fmt.put(x + "x" * (11 - len(x)), bytes([s & 0xFF]) * vl) for x in keys]))
     os.environ["SKV_HOST_PARTS"] = "5"
     t, pstreams = _pinned_wal(torch, runs)
+    os.environ["SKV_HOST_PIPE_MANY"] = "1"  # (off by default: it loses to the serial path)
+    try:
+        _many_runs_pipelined(dev, torch, runs, pstreams)
+    finally:
+        os.environ.pop("SKV_HOST_PIPE_MANY", None)
+    got = dev.compact_host_ptrs(pstreams, 1 << 40, _abi.SKV_SPLIT_BY_TABLE, with_runs=True)
+    assert dev.timings()["host_parts"] == 0  # the default: the serial path past 2^16 runs
+
+
+def _many_runs_pipelined(dev, torch, runs, pstreams):
     got = dev.compact_host_ptrs(pstreams, 1 << 40, _abi.SKV_SPLIT_BY_TABLE, with_runs=True)
     assert 2 <= dev.timings()["host_parts"] <= 5
     exp = pyoracle.compact([(s + 1, [r]) for s, r in enumerate(runs)], 1 << 40, _abi.SKV_SPLIT_BY_TABLE)
