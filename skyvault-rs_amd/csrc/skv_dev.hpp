@@ -185,13 +185,7 @@ struct TileOut {
 #ifndef SKV_FX_CAP
 #define SKV_FX_CAP 2048                  // 2048: 63 VGPRs, 4 workgroups per CU (4096: 91 VGPRs, 2 per CU; 3 % slower end to end)
 #endif
-#ifndef SKV_FX_EARLY
-#define SKV_FX_EARLY 1                   // 1: fused tiles publish their survivor count before the merge
-#endif
 constexpr int FX_HSLOTS = 2 * SKV_FX_CAP;  // distinct-key hash slots per fused tile (load <= 1/2)
-#ifndef SKV_FX_NT
-#define SKV_FX_NT 1                      // 1: non-temporal output stores in the fused copy
-#endif
 constexpr int FX_CAP = SKV_FX_CAP;       // max records per fused tile
 constexpr int FX_TARGET = FX_CAP / 4 * 3;  // target records per fused tile (splitter spacing)
 constexpr int FX_THREADS = SKV_FX_THREADS;
@@ -237,8 +231,6 @@ struct FxArgs {
     uint64_t T1, m2;
     const uint32_t* l1cnt;        // (T + 1) x k: stream j's level-1 samples sorted before splitter t
                                   // (k_fx_l1cnt), or null: k_fx_bounds searches them
-    const ulong2* keys;           // SKV_FX_DIAG=4 builds only: every record's (hi, lo) key, by record
-                                  // index, written before the tiles (the tiles read no record heads)
 };
 // Higher sample levels written by k_fx_sample itself: level-1 sample c of stream j is also level
 // 2's sample c / Sstep when Sstep divides c (and level 3's when Sstep^2 does) -- the same element

@@ -84,8 +84,6 @@ FxArgs fx_launch(skv_ctx* ctx, uint32_t k, uint32_t n_runs, const RunInfo* d_run
     uint64_t T0 = 1, m0 = 1;
     if (lv.size() > 1) {
         m0 = std::max<uint64_t>(1, (uint64_t)FX_TARGET / lv[1].S);
-        // SKV_FX_TILE_DIV=d (A/B): tiles of 1/d of the target at the same sample spacing
-        if (const char* de = getenv("SKV_FX_TILE_DIV")) m0 = std::max<uint64_t>(4, m0 / std::max<uint64_t>(1, strtoull(de, nullptr, 10)));
         T0 = std::max<uint64_t>(1, (lv[1].N + m0 - 1) / m0);
     }
     // the last generation of tiles (as many as are resident at once) at half size, so the grid
@@ -209,10 +207,6 @@ FxArgs fx_launch(skv_ctx* ctx, uint32_t k, uint32_t n_runs, const RunInfo* d_run
     A.tstate = (uint64_t*)(d_blob + o_tstate);  // zeroed by the blob upload
     A.tcounter = (uint32_t*)(d_blob + o_tick);
     A.out = io && io->out ? io->out : dbuf<uint8_t>(ctx, "out", out_bytes);
-#if SKV_FX_DIAG == 4
-    A.keys = dbuf<ulong2>(ctx, "fx_keys", R + 1);
-    launch_fx_keys(st, A, R, (ulong2*)A.keys);
-#endif
     mark(ctx, PH_CHECK);
     // ---- the fused tiles
     HIPCHK(launch_fx_tile(st, A));

@@ -199,9 +199,6 @@ void launch_run_tables(hipStream_t, const RunInfo* runs, const RunFmt* fmt, uint
 // the run table on the device for one-run streams in monotone seq_no order (chunk_base: n + 1 entries)
 void launch_run_info(hipStream_t, const uint64_t* ptr, const uint64_t* len, uint32_t n, bool reversed, uint64_t chunk,
                      uint64_t* nch, uint64_t* chunk_base, uint64_t* scan_tmp, RunInfo* runs);
-#if SKV_FX_DIAG == 4
-void launch_fx_keys(hipStream_t, const FxArgs& A, uint64_t R, ulong2* keys);
-#endif
 // skv_scan.hip: ScanFromRun after the merge
 void launch_scan_filter(hipStream_t, uint64_t R, uint32_t k, const uint64_t* stream_base, const uint64_t* a_addr,
                         const uint64_t* a_hi, const uint64_t* a_lo, const uint32_t* a_klen, const uint32_t* a_meta,

@@ -25,14 +25,6 @@
 #include <map>
 #include <mutex>
 
-#ifndef SKV_FX_DIAG
-#define SKV_FX_DIAG 0  // diagnostic builds only (output invalid): 1 skip the copy, 2 skip the merge
-                       // rounds, 3 copy only (no key loads, no merge: records in load order);
-                       // 4 (output valid): the tiles take every key from a compact array written
-                       // before them (k_fx_keys), so they read no record head lines for the keys --
-                       // the price of the key phase's head-line traffic, measured
-#endif
-
 namespace skv {
 
 static_assert(FX_HSLOTS >= 2 * FX_CAP && FX_CAP < 65535, "distinct-key set: 16-bit slots at <= 1/2 load");
@@ -45,11 +37,7 @@ typedef unsigned int fx_u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void fx_store16(uint8_t* p, uint4 v) {
     fx_u32x4 vv = {v.x, v.y, v.z, v.w};
-#if SKV_FX_NT
     __builtin_nontemporal_store(vv, (fx_u32x4*)p);  // written once, never re-read here
-#else
-    *(fx_u32x4*)p = vv;
-#endif
 }
 
 // q = z / d, r = z % d from a double reciprocal and one correction step (z < 2^52)
@@ -131,26 +119,7 @@ __device__ __forceinline__ uint4 fx_ld16(uint64_t a) {  // unaligned: full rate 
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-#ifndef SKV_FX_NTSEL
-#define SKV_FX_NTSEL 0  // 1: the fused copy loads lines that hold no record head non-temporally
-#endif
-#ifndef SKV_FX_INTERP
-#define SKV_FX_INTERP 0  // 1: k_fx_bounds' first probe pair interpolated from the gap's end keys (measured slower: 0.283 vs 0.264 ms splitters; the search is bound by its line fetches, not their latency)
-#endif
-#ifndef SKV_FX_XMASK
-#define SKV_FX_XMASK 1  // 1: the copy's second load only on straddling lanes (exec mask)
-#endif
-#ifndef SKV_FX_NTL
-#define SKV_FX_NTL 0  // 1: non-temporal loads in the copy (the bytes are read once there)
-#endif
-__device__ __forceinline__ uint4 fx_cld16(uint64_t a) {  // the copy's loads
-#if SKV_FX_NTL
-    const fx_v4 v = __builtin_nontemporal_load((fx_g16*)a);
-    return make_uint4(v.x, v.y, v.z, v.w);
-#else
-    return fx_ld16(a);
-#endif
-}
+__device__ __forceinline__ uint4 fx_cld16(uint64_t a) { return fx_ld16(a); }  // the copy's loads
 
 // One record's header pieces: marker + key_len (bytes 0..7), the 16 bytes from the key start,
 // val_len (at 5 + K). All inside the record (S >= 32), issued as three independent loads.
@@ -356,36 +325,6 @@ __device__ __forceinline__ FxBound fx_bound(const FxArgs& A, const uint64_t* __r
             };
             uint64_t b2 = hi;
             a = lo;
-#if SKV_FX_INTERP
-            if (hi - lo >= 4 && q0 + c < q1 && hi < s1) {
-                const uint64_t kh = l1hi[q0 + c];  // sample c = record hi
-                if (kh > pvh) {
-                    const double f = (double)(h - pvh) / (double)(kh - pvh);
-                    const uint64_t span = hi - lo + 1;  // records lo - 1 .. hi
-                    uint64_t g = lo - 1 + (uint64_t)(f * (double)span + 0.5);
-                    g = g < lo + 1 ? lo + 1 : (g > hi - 1 ? hi - 1 : g);
-                    const uint64_t e0 = g - 1;  // probes e0, e0 + 1 inside [lo, hi)
-                    const uint4 k0 = probe(e0), k1 = probe(e0 + 1);
-                    uint64_t h0, l0, h1, l1;
-                    key_of(k0, h0, l0);
-                    key_of(k1, h1, l1);
-                    if (h0 < h || (h0 == h && l0 < l)) {
-                        a = e0 + 1;
-                        pvh = h0;
-                        pvl = l0;
-                        if (h1 < h || (h1 == h && l1 < l)) {
-                            a = e0 + 2;
-                            pvh = h1;
-                            pvl = l1;
-                        } else {
-                            b2 = e0 + 1;
-                        }
-                    } else {
-                        b2 = e0;
-                    }
-                }
-            }
-#endif
             while (a < b2) {
                 const uint64_t i = (a + b2) >> 1;
                 uint64_t eh, el;
@@ -653,30 +592,11 @@ __device__ __forceinline__ void fx_plan(FxBatch<U>& t, FxWalk& w, const uint64_t
             w.o = z ? w.S32 - 1 : w.o - 1;
             w.j = z ? w.j - 1 : w.j;
         }
-#if SKV_FX_NTSEL  // non-temporal loads for the lines no record head shares (read once here)
-        {
-            const uint64_t hEnd = ((s0 + 24) | 127ull) + 1, nHead = (s0 + w.S32) & ~127ull;
-            const bool nt = !vb && !st && aL >= hEnd && aL + 16 <= nHead;
-            if (nt) {
-                const fx_v4 v = __builtin_nontemporal_load((fx_g16*)aL);
-                t.L[u] = make_uint4(v.x, v.y, v.z, v.w);
-            } else {
-                t.L[u] = fx_ld16(aL);
-            }
-        }
-#else
         t.L[u] = fx_cld16(aL);
-#endif
-#if SKV_FX_DIAG_1LD  // diagnostic (output invalid at record ends): no second load
-        t.X[u] = t.L[u];
-        (void)aX;
-#elif SKV_FX_XMASK  // second load only on the lanes that straddle (exec-masked)
+        // the second load only on the lanes that straddle (exec-masked)
         uint4 xv = make_uint4(0, 0, 0, 0);
         if (st && valid) xv = fx_cld16(aX);
         t.X[u] = xv;
-#else
-        t.X[u] = fx_cld16(aX);
-#endif
     }
 }
 __device__ __forceinline__ uint4 fx_sel4(bool c, uint4 a, uint4 b) {  // c ? a : b, per dword
@@ -723,14 +643,7 @@ __device__ __forceinline__ void fx_finish(const FxBatch<U>& t, uint8_t* ob) {
 // LDS: key[FX_CAP] 16 B (by position; after the merge: source addresses by survivor, u64)
 //      | prevk[k] 16 B | segaddr[k] sbase[k] u64 | cb0[k+1] cbA[k+1] cbB[k+1] u32 | id[FX_CAP] u16
 //      | prevok[k] u8
-#ifndef SKV_FX_WAVES
-#define SKV_FX_WAVES 0  // >0: amdgpu_waves_per_eu floor for k_fx_tile (8 caps it at 64 VGPRs)
-#endif
-#if SKV_FX_WAVES
-__global__ void __launch_bounds__(FX_THREADS) __attribute__((amdgpu_waves_per_eu(SKV_FX_WAVES))) k_fx_tile(FxArgs A) {
-#else
 __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
-#endif
     constexpr int PER = FX_CAP / FX_THREADS;
     extern __shared__ __attribute__((aligned(16))) uint64_t fx_smem[];
     const uint32_t k = A.k;
@@ -746,15 +659,11 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     __shared__ uint64_t ws[16];
     __shared__ uint64_t s_t, s_g0;
     __shared__ uint32_t s_dead, s_bad;
-#if SKV_FX_EARLY
     __shared__ uint32_t hs[FX_HSLOTS / 2];  // distinct-key set: 16-bit slots (element + 1), two per word
     __shared__ uint32_t s_early;
-#endif
     const uint32_t tid = threadIdx.x;
     const uint64_t S = A.S;
-#if SKV_FX_EARLY
     for (uint32_t x = tid; x < FX_HSLOTS / 2; x += FX_THREADS) hs[x] = 0;
-#endif
 #if SKV_TILE_PROF
     uint64_t tp_last = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -807,9 +716,6 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     uint32_t bad = 0;
     {
         uint64_t ad[PER];
-#if SKV_FX_DIAG == 4
-        uint64_t gi[PER];
-#endif
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const uint32_t e = tid + u * FX_THREADS;
@@ -818,44 +724,27 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
                 const uint32_t j = fx_seg(cb0, k + 1, e);
                 const uint64_t sa = segaddr[j];
                 ad[u] = sa ? sa + (uint64_t)(e - cb0[j]) * S : fx_addr(A, j, sbase[j] + (e - cb0[j]));
-#if SKV_FX_DIAG == 4
-                gi[u] = sbase[j] + (e - cb0[j]);
-#endif
             }
         }
-#if SKV_FX_DIAG == 4
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            if (ad[u]) {
-                const uint32_t e = tid + u * FX_THREADS;
-                key[e] = A.keys[gi[u]];
-                id[e] = (uint16_t)e;
-            }
-        }
-        if (false)
-#endif
-        {
         FxRec rec[PER];
 #pragma unroll
         for (int u = 0; u < PER; ++u)
-            if (ad[u] && SKV_FX_DIAG != 3) fx_issue(ad[u], A.K, rec[u]);
+            if (ad[u]) fx_issue(ad[u], A.K, rec[u]);
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             if (ad[u]) {
                 const uint32_t e = tid + u * FX_THREADS;
-                uint64_t h = e + 1, l = 0;
-                if (SKV_FX_DIAG != 3 && !fx_check(A, rec[u], ad[u], h, l)) bad |= FXR_RECORD;
+                uint64_t h = 0, l = 0;
+                if (!fx_check(A, rec[u], ad[u], h, l)) bad |= FXR_RECORD;
                 key[e] = make_ulong2(h, l);
                 id[e] = (uint16_t)e;
             }
-        }
         }
     }
     __syncthreads();
     FXPROF(1);
     // ---- order check inside each stream (runs.rs:190-198): against the previous record of the
     // same stream (the previous element of the segment, or the record before the segment).
-#if SKV_FX_EARLY
     // In the same pass, the tile's survivor count before its merge: first-per-key keeps one record
     // per distinct key (k_way.rs:146-151; the fused path holds Puts only, keys <= 16 bytes, so
     // (hi, lo) is the whole key), so the count is the number of distinct keys, found with an LDS
@@ -863,7 +752,6 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     // the merge rounds, successors' look-backs stop waiting on them; the merge's own count is
     // checked against it after the rounds.
     uint32_t distinct = 0;
-#endif
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const uint32_t e = tid + u * FX_THREADS;
@@ -877,8 +765,7 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
                 pv = prevk[j];
                 has = prevok[j] != 0;
             }
-            if (has && !fx_le(pv, c) && SKV_FX_DIAG != 3) bad |= FXR_ORDER;  // a strict decrease
-#if SKV_FX_EARLY
+            if (has && !fx_le(pv, c)) bad |= FXR_ORDER;  // a strict decrease
             uint32_t h = (uint32_t)((c.x * 0x9E3779B97F4A7C15ull ^ c.y * 0xC2B2AE3D27D4EB4Full) >> 40) & (FX_HSLOTS - 1);
             for (;;) {
                 const uint32_t sh = (h & 1u) * 16u;
@@ -895,16 +782,11 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
                 if (o.x == c.x && o.y == c.y) break;  // a duplicate of a key already in the set
                 h = (h + 1) & (FX_HSLOTS - 1);
             }
-#endif
         }
     }
     if (bad) atomicOr(&s_bad, bad);
-#if SKV_FX_EARLY
     uint32_t tot_d;
     fx_block_excl<uint32_t>(distinct, (uint32_t*)ws, tot_d);  // barriers: s_bad is settled after it
-#else
-    __syncthreads();
-#endif
     FXPROF(2);
     if (s_dead || s_bad) {  // publish an empty aggregate so later tiles never wait on this one
         if (tid == 0) {
@@ -914,19 +796,17 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
         }
         break;
     }
-#if SKV_FX_EARLY
     if (tid == 0) {
         s_early = tot_d;
         fx_publish_early(A.tstate, t, tot_d);
     }
-#endif
     // ---- k_way::merge order (k_way.rs:20-27, :113-179): pairwise merge-path rounds over the k
     // stream segments (segment s pairs with s ^ 1, the left one holds newer seq_nos and wins ties,
     // so equal keys end up seq_no-descending, and in stream order within a stream). Each thread
     // produces PER consecutive outputs of a round: one merge-path search, then a sequential merge.
     const uint32_t i0 = tid * PER;
     {
-        uint32_t m = SKV_FX_DIAG >= 2 ? 1 : k;
+        uint32_t m = k;
         const uint32_t* cb = cb0;
         uint32_t* cbn = cbA;
         while (m > 1) {
@@ -1025,19 +905,17 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     const uint32_t cnt = total;
     FXPROF(4);
     if (tid < 64) {
-        const uint64_t g0 = fx_lookback(A.tstate, t, cnt, SKV_FX_EARLY != 0) + (A.gbase ? *A.gbase : 0ull);
+        const uint64_t g0 = fx_lookback(A.tstate, t, cnt, true) + (A.gbase ? *A.gbase : 0ull);
         if (tid == 0) {
             s_g0 = g0;
-#if SKV_FX_EARLY
             if (s_early != cnt) fx_poison(A, FXR_RECORD);  // never: the merge kept another count
-#endif
             if (t == A.T - 1) *A.Kout = g0 + cnt;
             s_dead = __hip_atomic_load(A.flags + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
     FXPROF(5);
-    if (!cnt || s_dead || SKV_FX_DIAG == 1) break;
+    if (!cnt || s_dead) break;
     // ---- output bytes of survivors g0 .. g0+cnt-1 (build_runs' bytes, runs.rs:241-267). The
     // tile's survivors form "pieces": runs of consecutive survivors inside one output run; piece 0
     // starts at survivor 0, piece i >= 1 at survivor jb1 + (i-1) n behind its run's version byte.
@@ -1068,10 +946,7 @@ __global__ void __launch_bounds__(FX_THREADS) k_fx_tile(FxArgs A) {
     // writes its neighbours, so each 128-B output line is completed at once and each input line
     // is read while the neighbouring lanes read it (no partial-line writes, no re-reads).
     // Tiles crossing several runs (small max sizes) take the generic loop.
-#ifndef SKV_FX_GENERIC_COPY
-#define SKV_FX_GENERIC_COPY 0            // 1: every tile takes the generic copy loop (A/B diagnostics)
-#endif
-    const bool multi = SKV_FX_GENERIC_COPY || (jb1 < cnt && cnt - jb1 > nr);
+    const bool multi = jb1 < cnt && cnt - jb1 > nr;
     if (!multi) {
         FxWalk w;
         w.V0 = q0 == 0 ? a0 - 1 : ~0ull;  // version byte before survivor 0
@@ -1229,25 +1104,6 @@ __global__ void k_fx_desc(FxArgs A, DevRunDesc* descs, uint64_t* n_runs_out, uin
     }
 }
 
-#if SKV_FX_DIAG == 4
-// every record's key by record index (rank order), verified as k_fx_tile would (SKV_FX_DIAG=4 only)
-__global__ void k_fx_keys(FxArgs A, uint64_t R, ulong2* keys) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= R) return;
-    uint32_t lo = 0, hi = A.k;  // stream j: stream_base[j] <= i < stream_base[j + 1]
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (A.stream_base[mid] <= i) lo = mid;
-        else hi = mid;
-    }
-    uint64_t h = 0, l = 0;
-    if (!fx_key(A, fx_addr(A, lo, i), h, l)) fx_poison(A, FXR_RECORD);
-    keys[i] = make_ulong2(h, l);
-}
-void launch_fx_keys(hipStream_t s, const FxArgs& A, uint64_t R, ulong2* keys) {
-    if (R) k_fx_keys<<<(unsigned)((R + 255) / 256), 256, 0, s>>>(A, R, keys);
-}
-#endif
 
 // a part's survivor count to host-mapped memory (pipelined host calls): one lane, a vector
 // store with system scope, so the host sees it once the part's completion event has fired
@@ -1290,26 +1146,10 @@ __global__ void __launch_bounds__(256) k_ingest(const IngestSlice* __restrict__ 
     for (; i < nb; i += stride) d4[i] = s4[i];
 }
 
-// The same ingest for calls with many slices (a WAL flush of 10^6 tiny runs: a few KiB each):
-// workgroups stride over the slices, one slice at a time, so the grid stays small (the copies are
-// bound by PCIe) whatever the slice count.
-__global__ void __launch_bounds__(256) k_ingest_slices(const IngestSlice* __restrict__ sl, uint64_t n) {
-    for (uint64_t y = blockIdx.x; y < n; y += gridDim.x) {
-        const IngestSlice S = sl[y];
-        const uint8_t* src = (const uint8_t*)S.src;
-        uint8_t* dst = (uint8_t*)S.dst;
-        const uint64_t head = ((16 - (S.src & 15)) & 15) < S.len ? ((16 - (S.src & 15)) & 15) : S.len;
-        const uint64_t nb = (S.len - head) >> 4, tail0 = head + (nb << 4);
-        if (threadIdx.x < head) dst[threadIdx.x] = src[threadIdx.x];
-        if (threadIdx.x < S.len - tail0) dst[tail0 + threadIdx.x] = src[tail0 + threadIdx.x];
-        const uint4* s4 = (const uint4*)(src + head);
-        uint4* d4 = (uint4*)(dst + head);
-        for (uint64_t i = threadIdx.x; i < nb; i += blockDim.x) d4[i] = s4[i];
-    }
-}
-
-// The same with one slice per WAVE (slices of a WAL flush's parts are ~1 KiB: a workgroup per slice
-// left 3 of its 4 waves idle): each wave copies its slice's 16-byte blocks four per lane in flight.
+// The same ingest for calls with many slices (a WAL flush of 10^6 tiny runs: ~1 KiB slices):
+// workgroups stride over the slices one WAVE per slice (a workgroup per slice left 3 of its 4 waves
+// idle), each wave copying its slice's 16-byte blocks four per lane in flight; the grid stays small
+// (the copies are bound by PCIe) whatever the slice count.
 __global__ void __launch_bounds__(256) k_ingest_waves(const IngestSlice* __restrict__ sl, uint64_t n) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t W = (uint64_t)gridDim.x * 4;
@@ -1356,9 +1196,7 @@ size_t fx_tile_lds_bytes(uint32_t k) {
     return (size_t)FX_CAP * 16 + (size_t)k * 16 + 2 * (size_t)k * 8 + 3 * (size_t)(k + 1) * 4 + (size_t)FX_CAP * 2 + k + 16;
 }
 hipError_t launch_fx_tile(hipStream_t s, const FxArgs& A) {
-    // SKV_FX_LDS=<bytes>: pad the tile's LDS request (caps workgroups per CU; occupancy studies)
-    static const size_t lds_pad = getenv("SKV_FX_LDS") ? (size_t)atol(getenv("SKV_FX_LDS")) : 0;
-    const size_t lds = std::max(fx_tile_lds_bytes(A.k), std::min<size_t>(lds_pad, 160 * 1024));
+    const size_t lds = fx_tile_lds_bytes(A.k);
     lds_limit((const void*)k_fx_tile);
     k_fx_tile<<<(unsigned)A.T, FX_THREADS, lds, s>>>(A);
     return hipGetLastError();
@@ -1382,10 +1220,9 @@ void launch_ingest(hipStream_t s, const IngestSlice* slices, uint32_t n, uint32_
     if (n) k_ingest<<<dim3(blocks_per_slice, n), 256, 0, s>>>(slices);
 }
 void launch_ingest_slices(hipStream_t s, const IngestSlice* slices, uint64_t n, uint32_t grid) {
-    static const bool per_wg = getenv("SKV_INGEST_WG") && getenv("SKV_INGEST_WG")[0] == '1';  // A/B: a workgroup per slice
-    if (!n) return;
-    if (per_wg) k_ingest_slices<<<(unsigned)std::min<uint64_t>(n, grid ? grid : 1), 256, 0, s>>>(slices, n);
-    else k_ingest_waves<<<(unsigned)std::min<uint64_t>((n + 3) / 4, grid ? grid : 1), 256, 0, s>>>(slices, n);
+    // a wave per slice (a workgroup per slice, k_ingest_slices' old shape, measured 12 % slower on
+    // config 5's 10^6-slice parts: profiles/r05/c5_host.txt)
+    if (n) k_ingest_waves<<<(unsigned)std::min<uint64_t>((n + 3) / 4, grid ? grid : 1), 256, 0, s>>>(slices, n);
 }
 void launch_copy_bytes(hipStream_t s, uint8_t* dst, const uint8_t* src, uint64_t n) {
     if (n) k_copy_bytes<<<fx_blocks((n + 15) / 16, 256), 256, 0, s>>>(dst, src, n);
