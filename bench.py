@@ -487,6 +487,28 @@ def main():
         host_path["pipelined_2ctx"] = {
             "value": round(2 * n_jobs * in_bytes / tp / GiB, 3), "unit": "GiB/s",
             "note": f"2 ctxs x {n_jobs} skv_compact calls from 2 host threads, same pinned inputs"}
+        if config in ("2A", "2B", "L0"):
+            # skv_compact_split: the same call as 4 key-range shards on 4 ctxs. Here all
+            # four share this GPU's PCIe link, so the figure is the split's overhead against the
+            # pipelined single-ctx call, not its scaling (G GPUs move G shards over G links)
+            from skv.api import compact_split
+
+            cs = [Compactor(dev_idx) for _ in range(4)]
+            compact_split(cs, hstreams, max_run, flags, keep=True).free()
+            sts = []
+            for _ in range(2):
+                t1 = time.perf_counter()
+                compact_split(cs, hstreams, max_run, flags, keep=True).free()
+                sts.append(time.perf_counter() - t1)
+            st_ = min(sts)
+            sparts = int(cs[0].timings()["host_parts"])
+            for c in cs:
+                c.close()
+            host_path["split_4ctx_1gpu"] = {
+                "value": round(in_bytes / st_ / GiB, 3), "unit": "GiB/s", "ms": round(st_ * 1e3, 3),
+                "parts": sparts,
+                "note": "skv_compact_split over 4 ctxs of this one GPU (one PCIe link shared): each shard's "
+                        "H2D, kernels and D2H in turn; best of 2 after 1 warm-up"}
         del host_runs
         # the ceiling of this figure: the box's PCIe with both directions busy at once (1 GiB H2D on
         # one stream while 1 GiB D2H runs on another, pinned buffers); a host call moves its input

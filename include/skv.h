@@ -35,9 +35,9 @@
 extern "C" {
 #endif
 
-#define SKV_ABI_VERSION 7  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts; 4: skv_scan_runs;
+#define SKV_ABI_VERSION 8  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts; 4: skv_scan_runs;
                               5: skv_timings.span_parse (was reserved); 6: skv_timings.wal_stage;
-                              7: skv_ctx_host_info */
+                              7: skv_ctx_host_info; 8: skv_compact_split */
 
 typedef struct skv_ctx skv_ctx;
 
@@ -182,6 +182,20 @@ int skv_compact(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams,
  */
 int skv_compact_dev(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams,
                     uint64_t max_run_size, uint32_t flags, skv_result** out);
+
+/*
+ * One compaction split across several GPUs by key range: skv_compact's inputs,
+ * semantics, errors and result (pinned host memory, owned by ctxs[0]'s pool), with the work of one
+ * call spread over n_ctx distinct ctxs -- normally one per GPU. Shard g (a key range of every
+ * stream; equal keys never straddle a cut) is staged, merged and deduplicated on ctxs[g]; the
+ * shards exchange only their survivor counts, from which build_runs' greedy split (runs.rs:211-238)
+ * places every shard's survivors in the one output. Taken for calls of one record size with keys of
+ * at most 16 bytes (the fused stride path); every other call, and any shard whose records that path
+ * does not take, runs as skv_compact on ctxs[0]. Errors are reported on ctxs[0]. The ctxs must not
+ * be used by other threads during the call. n_ctx == 1 is skv_compact.
+ */
+int skv_compact_split(skv_ctx* const* ctxs, uint32_t n_ctx, const skv_stream* streams, uint32_t n_streams,
+                      uint64_t max_run_size, uint32_t flags, skv_result** out);
 
 /*
  * Writer-side batch encode (replaces writer_service.rs:148-162 process_batch's BTreeMap + build_runs):

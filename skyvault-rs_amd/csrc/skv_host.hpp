@@ -340,6 +340,19 @@ FxArgs fx_launch(skv_ctx* ctx, uint32_t k, uint32_t n_runs, const RunInfo* d_run
                         const std::vector<uint32_t>& stream_first_run, const RunFmt& f,
                         const std::vector<uint64_t>& recb, uint64_t n, uint64_t out_bytes, const FxPartIO* io,
                         uint64_t*& d_rb_out);
+// Key-range parts of a fused call with host inputs (skv_hostpipe.hip; the pipelined host call and
+// the multi-GPU split, skv_split.hip)
+bool fx_host_shape(const Job& job, RunFmt& f, uint64_t& R);
+bool fx_host_cuts(const Job& job, const RunFmt& f, uint64_t P, std::vector<uint64_t>& lb);
+struct FxPartTables {  // per part i of [p0, p1): runs rows i * nr.., streams, first runs, record bases
+    std::vector<RunInfo> runs;
+    std::vector<uint32_t> kp, np;
+    std::vector<std::vector<uint32_t>> sfr;
+    std::vector<std::vector<uint64_t>> recb;
+};
+void fx_part_tables(const Job& job, const RunFmt& f, uint64_t p0, uint64_t p1, const std::vector<uint64_t>& lb,
+                    const uint8_t* d_in, const std::vector<uint64_t>& img, const std::vector<uint64_t>* base,
+                    FxPartTables& t);
 bool compact_fused(skv_ctx* ctx, const Job& job, const std::vector<RunInfo>& runs, const RunInfo* d_runs,
                           const std::vector<uint32_t>& stream_first_run, const RunFmt& f,
                           const std::vector<uint64_t>& recb, skv_result** out);

@@ -21,13 +21,11 @@ using namespace skv;
 static uint32_t be32(const uint8_t* p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
 
 
-static bool pipe_eligible(const Job& job, RunFmt& f, uint64_t& R) {
-    const char* pe = getenv("SKV_HOST_PIPE");
-    if (pe && pe[0] == '0') return false;
-    const char* me = getenv("SKV_HOST_PIPE_MIN");
-    const uint64_t min_bytes = me ? strtoull(me, nullptr, 10) : (512ull << 20);
+// The fused stride path's shape as the host can see it (one run format, key <= 16 bytes, fan-in
+// within one tile, member runs of a stream ascending as one stream); R = the call's records.
+bool fx_host_shape(const Job& job, RunFmt& f, uint64_t& R) {
     const uint32_t k = (uint32_t)job.ranked.size();
-    if (job.in_bytes < min_bytes || (job.flags & SKV_SPLIT_BY_TABLE) || job.batch || job.search) return false;
+    if ((job.flags & SKV_SPLIT_BY_TABLE) || job.batch || job.search || job.scan) return false;
     const uint64_t nr = job.run_ptr.size();
     if (k == 0 || k > (uint32_t)TILE_TARGET / 2 || nr == 0) return false;
     R = 0;
@@ -59,21 +57,22 @@ static bool pipe_eligible(const Job& job, RunFmt& f, uint64_t& R) {
     return R < 0xFFFFFFFFull;
 }
 
-static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, double t_entry, bool& used) {
-    used = false;
-    RunFmt f{};
-    uint64_t R = 0;
-    if (!pipe_eligible(job, f, R)) return SKV_OK;
-    const uint32_t k = (uint32_t)job.ranked.size();
-    const uint64_t nr = job.run_ptr.size();  // member runs (one per stream unless a stream concatenates)
-    const uint64_t S = f.S, K = f.K;
-    uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(64, job.in_bytes / (256ull << 20)));
-    if (const char* pp = getenv("SKV_HOST_PARTS")) P = std::max<uint64_t>(1, std::min<uint64_t>(256, strtoull(pp, nullptr, 10)));
-    if (R < P * 64) return SKV_OK;
-    htrace("pipe: eligible");
+static bool pipe_eligible(const Job& job, RunFmt& f, uint64_t& R) {
+    const char* pe = getenv("SKV_HOST_PIPE");
+    if (pe && pe[0] == '0') return false;
+    const char* me = getenv("SKV_HOST_PIPE_MIN");
+    const uint64_t min_bytes = me ? strtoull(me, nullptr, 10) : (512ull << 20);
+    if (job.in_bytes < min_bytes) return false;
+    return fx_host_shape(job, f, R);
+}
+
+// P - 1 cut keys (quantiles of an even sample of every run) and lb[p * nr + m] = the first record of
+// run m with key >= cut p (lb[m] = 0, lb[P * nr + m] = its record count). False when a run
+// decreases across a cut: the device checks the order inside each part only.
+bool fx_host_cuts(const Job& job, const RunFmt& f, uint64_t P, std::vector<uint64_t>& lb) {
+    const uint64_t nr = job.run_ptr.size(), S = f.S, K = f.K;
     auto key_at = [&](uint64_t m, uint64_t i) { return (const uint8_t*)(uintptr_t)job.run_ptr[m] + 1 + i * S + 5; };
     auto nrec = [&](uint64_t m) { return (job.run_len[m] - 1) / S; };
-    // ---- cut keys: quantiles of an even sample of every run
     std::vector<std::array<uint8_t, 16>> smp;
     const uint64_t Q = std::max<uint64_t>(2, 4096 / nr);
     for (uint64_t m = 0; m < nr; ++m) {
@@ -85,37 +84,88 @@ static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, doub
         }
     }
     std::sort(smp.begin(), smp.end());
-    std::vector<std::array<uint8_t, 16>> cut;  // P - 1 cut keys B_1..B_{P-1}
+    std::vector<std::array<uint8_t, 16>> cut;  // B_1..B_{P-1}
     for (uint64_t p = 1; p < P; ++p) cut.push_back(smp[p * smp.size() / P]);
-    // ---- lb[p * nr + m]: first record of run m with key >= B_p (binary search in host memory)
-    std::vector<uint64_t> lb((P + 1) * nr);
-    bool cuts_ok = true;
-    {
-        const unsigned nb = par_nblocks(nr, 8);
-        std::vector<uint8_t> ok(nb, 1);
-        par_run(nr, nb, [&](unsigned b, uint64_t lo_m, uint64_t hi_m) {
-            for (uint64_t m = lo_m; m < hi_m; ++m) {
-                const uint64_t nm = nrec(m);
-                lb[m] = 0;
-                lb[P * nr + m] = nm;
-                for (uint64_t p = 1; p < P; ++p) {
-                    uint64_t a = 0, z = nm;
-                    while (a < z) {
-                        const uint64_t mid = (a + z) >> 1;
-                        if (memcmp(key_at(m, mid), cut[p - 1].data(), K) < 0) a = mid + 1;
-                        else z = mid;
-                    }
-                    lb[p * nr + m] = a;
-                    // a run that decreases across a cut is left to the serial path (the device
-                    // checks the order inside each part only)
-                    if (a < lb[(p - 1) * nr + m]) ok[b] = 0;
-                    if (a > 0 && a < nm && memcmp(key_at(m, a - 1), key_at(m, a), K) > 0) ok[b] = 0;
+    lb.assign((P + 1) * nr, 0);
+    const unsigned nb = par_nblocks(nr, 8);
+    std::vector<uint8_t> ok(nb, 1);
+    par_run(nr, nb, [&](unsigned b, uint64_t lo_m, uint64_t hi_m) {
+        for (uint64_t m = lo_m; m < hi_m; ++m) {
+            const uint64_t nm = nrec(m);
+            lb[m] = 0;
+            lb[P * nr + m] = nm;
+            for (uint64_t p = 1; p < P; ++p) {
+                uint64_t a = 0, z = nm;
+                while (a < z) {
+                    const uint64_t mid = (a + z) >> 1;
+                    if (memcmp(key_at(m, mid), cut[p - 1].data(), K) < 0) a = mid + 1;
+                    else z = mid;
                 }
+                lb[p * nr + m] = a;
+                if (a < lb[(p - 1) * nr + m]) ok[b] = 0;
+                if (a > 0 && a < nm && memcmp(key_at(m, a - 1), key_at(m, a), K) > 0) ok[b] = 0;
             }
-        });
-        for (uint8_t o : ok) cuts_ok = cuts_ok && o;
+        }
+    });
+    bool cuts_ok = true;
+    for (uint8_t o : ok) cuts_ok = cuts_ok && o;
+    return cuts_ok;
+}
+
+// Parts [p0, p1) as fused launches: part p's runs (streams in rank order, each stream's member
+// slices in member order, empty slices and streams left out; rows (p - p0) * nr ...), the first run
+// of each stream and the record bases. Slice (p, m) starts at d_in + img[m] + (lb[p][m] - base[m]) * S,
+// the byte before its first record (run m's image holds its records from record base[m] on; no
+// base: from record 0).
+void fx_part_tables(const Job& job, const RunFmt& f, uint64_t p0, uint64_t p1, const std::vector<uint64_t>& lb,
+                    const uint8_t* d_in, const std::vector<uint64_t>& img, const std::vector<uint64_t>* base,
+                    FxPartTables& t) {
+    const uint32_t k = (uint32_t)job.ranked.size();
+    const uint64_t nr = job.run_ptr.size(), S = f.S, Pn = p1 - p0;
+    t.runs.assign(Pn * nr, RunInfo{});
+    t.kp.assign(Pn, 0);
+    t.np.assign(Pn, 0);
+    t.sfr.assign(Pn, {});
+    t.recb.assign(Pn, {});
+    for (uint64_t i = 0; i < Pn; ++i) {
+        const uint64_t p = p0 + i;
+        t.recb[i].assign(1, 0);
+        for (uint32_t s = 0; s < k; ++s) {
+            const InStream& st = job.ranked[s];
+            const uint32_t n0 = t.np[i];
+            for (uint64_t m = st.first; m < st.first + st.n_runs; ++m) {
+                const uint64_t a = lb[p * nr + m], z = lb[(p + 1) * nr + m];
+                if (z == a) continue;
+                RunInfo& ri = t.runs[i * nr + t.np[i]++];
+                ri.ptr = (uint64_t)(uintptr_t)(d_in + img[m] + (a - (base ? (*base)[m] : 0)) * S);
+                ri.len = 1 + (z - a) * S;
+                ri.chunk_base = 0;
+                ri.n_chunks = 0;
+                ri.stream = t.kp[i];
+                t.recb[i].push_back(t.recb[i].back() + (z - a));
+            }
+            if (t.np[i] > n0) {
+                t.sfr[i].push_back(n0);
+                ++t.kp[i];
+            }
+        }
+        t.sfr[i].push_back(t.np[i]);
     }
-    if (!cuts_ok) return SKV_OK;
+}
+
+static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, double t_entry, bool& used) {
+    used = false;
+    RunFmt f{};
+    uint64_t R = 0;
+    if (!pipe_eligible(job, f, R)) return SKV_OK;
+    const uint64_t nr = job.run_ptr.size();  // member runs (one per stream unless a stream concatenates)
+    const uint64_t S = f.S;
+    uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(64, job.in_bytes / (256ull << 20)));
+    if (const char* pp = getenv("SKV_HOST_PARTS")) P = std::max<uint64_t>(1, std::min<uint64_t>(256, strtoull(pp, nullptr, 10)));
+    if (R < P * 64) return SKV_OK;
+    htrace("pipe: eligible");
+    std::vector<uint64_t> lb;  // lb[p * nr + m]: first record of run m with key >= cut p
+    if (!fx_host_cuts(job, f, P, lb)) return SKV_OK;
     htrace("pipe: cuts");
     used = true;
     hipStream_t st = ctx->stream;
@@ -155,38 +205,10 @@ static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, doub
     const uint64_t n = fx_run_records(job.max_run_size, S, R), W = n * S + 1;
     const uint64_t max_runs = (R + n - 1) / n;
     DevRunDesc* d_desc = dbuf<DevRunDesc>(ctx, "descs", max_runs + 1);
-    // per part: its runs (streams in rank order, each stream's member slices in member order, empty
-    // slices and streams left out), the first run of each stream, record bases
-    std::vector<RunInfo> hruns(P * nr);
-    std::vector<uint32_t> kp(P, 0), np(P, 0);
-    std::vector<std::vector<uint32_t>> sfrp(P);
-    std::vector<std::vector<uint64_t>> recbp(P);
-    for (uint64_t p = 0; p < P; ++p) {
-        recbp[p].assign(1, 0);
-        sfrp[p].clear();
-        for (uint32_t s = 0; s < k; ++s) {
-            const InStream& st = job.ranked[s];
-            const uint32_t n0 = np[p];
-            for (uint64_t m = st.first; m < st.first + st.n_runs; ++m) {
-                const uint64_t a = lb[p * nr + m], z = lb[(p + 1) * nr + m];
-                if (z == a) continue;
-                RunInfo& ri = hruns[p * nr + np[p]++];
-                ri.ptr = (uint64_t)(uintptr_t)(d_in + img[m] + a * S);  // the byte before record a
-                ri.len = 1 + (z - a) * S;
-                ri.chunk_base = 0;
-                ri.n_chunks = 0;
-                ri.stream = kp[p];
-                recbp[p].push_back(recbp[p].back() + (z - a));
-            }
-            if (np[p] > n0) {
-                sfrp[p].push_back(n0);
-                ++kp[p];
-            }
-        }
-        sfrp[p].push_back(np[p]);
-    }
+    FxPartTables pt;
+    fx_part_tables(job, f, 0, P, lb, d_in, img, nullptr, pt);
     RunInfo* d_runs = dbuf<RunInfo>(ctx, "hp_runs", P * nr);
-    h2d_up(ctx, d_runs, hruns.data(), P * nr * sizeof(RunInfo));
+    h2d_up(ctx, d_runs, pt.runs.data(), P * nr * sizeof(RunInfo));
     HIPCHK(hipMemsetAsync(d_Kp, 0, P * 8, st));
     HIPCHK(hipMemsetAsync(d_pflags, 0, 16, st));
     size_t cap = 0;
@@ -279,15 +301,14 @@ static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, doub
         }
         HIPCHK(hipEventRecord(ctx->part_ev[2 * p], ctx->in_stream));
         HIPCHK(hipStreamWaitEvent(st, ctx->part_ev[2 * p], 0));
-        if (kp[p]) {
-            const std::vector<uint32_t>& sfr = sfrp[p];
+        if (pt.kp[p]) {
             FxPartIO io;
             io.gbase = p ? d_Kp + p - 1 : nullptr;
             io.Kout = d_Kp + p;
             io.flags = d_pflags;
             io.out = d_out;
             uint64_t* rb_unused = nullptr;
-            Alast = fx_launch(ctx, kp[p], np[p], d_runs + p * nr, sfr, f, recbp[p], n, out_cap, &io, rb_unused);
+            Alast = fx_launch(ctx, pt.kp[p], pt.np[p], d_runs + p * nr, pt.sfr[p], f, pt.recb[p], n, out_cap, &io, rb_unused);
             have_A = true;
         } else if (p) {
             launch_copy_bytes(st, (uint8_t*)(d_Kp + p), (const uint8_t*)(d_Kp + p - 1), 8);

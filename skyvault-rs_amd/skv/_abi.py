@@ -135,6 +135,7 @@ EXPORTED_SYMBOLS = [
     "skv_ctx_host_info",
     "skv_compact",
     "skv_compact_dev",
+    "skv_compact_split",
     "skv_encode_batch",
     "skv_encode_batch_dev",
     "skv_search_run",

@@ -59,6 +59,9 @@ def load():
     for fn in (l.skv_compact, l.skv_compact_dev):
         fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.POINTER(C.POINTER(SkvResult))]
         fn.restype = C.c_int
+    l.skv_compact_split.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
+                                    C.POINTER(C.POINTER(SkvResult))]
+    l.skv_compact_split.restype = C.c_int
     l.skv_search_run.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32,
                                  C.c_void_p]
     l.skv_search_run.restype = C.c_int
@@ -345,6 +348,34 @@ class Compactor:
         t = SkvTimings()
         self.lib.skv_ctx_get_timings(self.ctx, C.byref(t))
         return {f: getattr(t, f) for f, _ in SkvTimings._fields_}
+
+
+def compact_split(compactors: Sequence["Compactor"], streams, max_run_size: int = MAX_RUN_SIZE, flags: int = 0,
+                  keep: bool = False):
+    """skv_compact_split: one compaction spread over the Compactors' GPUs by key range (the first
+    one owns the result and reports errors). streams: [(seq_no, [run_bytes, ...])] (host memory),
+    [(seq_no, [(host_ptr, length)])] or a StreamArgs built with device=True. Returns [OutRun], or,
+    keep=True, the HostResult."""
+    if not compactors:
+        raise ValueError("compact_split needs at least one Compactor")
+    home = compactors[0]
+    if isinstance(streams, StreamArgs):
+        sa = streams
+    elif streams and streams[0][1] and isinstance(streams[0][1][0], tuple):
+        sa = StreamArgs(streams, device=True)
+    else:
+        sa = StreamArgs(streams)
+    ctxs = (C.c_void_p * len(compactors))(*[c.ctx.value for c in compactors])
+    res = C.POINTER(SkvResult)()
+    rc = home.lib.skv_compact_split(ctxs, len(compactors), sa.ptr, sa.n, max_run_size, flags, C.byref(res))
+    if rc != SKV_OK:
+        raise home._err(rc)
+    if keep:
+        return HostResult(home.lib, res, home)
+    try:
+        return result_to_runs(res.contents)
+    finally:
+        home.lib.skv_result_free(res)
 
 
 class RunIndex:

@@ -236,6 +236,36 @@ def test_config2_host_entry_full_size(dev, torch, default_pipe_env):
     hr.free()
 
 
+def test_config2_split_full_size(torch, default_pipe_env):
+    """config 2B (~37 % superseded) through skv_compact_split over 4 ctxs (one
+    compaction as 4 key-range shards, 4 parts each, counts exchanged, survivors placed by the
+    global split): every byte and descriptor equal to the oracle's."""
+    from skv.api import compact_split
+    from skv.devgen import make_cfg2_on_device
+
+    device = torch.device("cuda", 0)
+    _progress("config 2B split: generating")
+    runs = make_cfg2_on_device(device, SEED, 64, 238821, 256, "B")
+    host = _pinned_copies(torch, runs)
+    del runs
+    torch.cuda.empty_cache()
+    streams = [(s + 1, [(h.data_ptr(), h.numel())]) for s, h in enumerate(host)]
+    cs = [Compactor(0) for _ in range(4)]
+    try:
+        hr = compact_split(cs, streams, MAX_RUN, 0, keep=True)
+        t = cs[0].timings()
+        assert t["host_parts"] >= 8 and t["host_parts"] % 4 == 0, t  # 4 shards of parts, not skv_compact
+        _progress("config 2B split: oracle")
+        arrs = [h.numpy() for h in host]
+        sa = _abi.stream_table(np.arange(1, 65), [a.ctypes.data for a in arrs], [a.size for a in arrs])
+        exp, descs, info = pyoracle.compact_np(sa, MAX_RUN, 0)
+        _check_host_result(hr, exp, descs, info, "config 2B split")
+        hr.free()
+    finally:
+        for c in cs:
+            c.close()
+
+
 def test_config3_host_entry_full_size(dev, torch, default_pipe_env):
     """config 3's shape (256 streams, variable 8-128 B keys, 10 % Deletes) at 256 x 16 MiB (3.7 GiB)
     through skv_compact with pinned host inputs: the general key-range pipeline with its own part

@@ -1,0 +1,189 @@
+"""One compaction split across several GPUs by key range (skv_compact_split, skv_split.hip; SURVEY
+§8(e)). On the one-GPU test box the G shards run on G ctxs of device 0, one host thread each: the
+same code as G GPUs (each shard stages, merges and deduplicates its key range on its own ctx and
+stream; only the survivor counts cross between shards; every shard copies its survivors D2H to
+their global places in one output). Outputs must be the oracle's, byte for byte, for any G, any
+max_run_size (run boundaries fall inside shards and at shard edges), equal keys across streams,
+streams absent from some shards, and member-run (L0) streams. Calls outside the split's shape
+(variable-length records) and calls a shard poisons (a key decrease) must end with the oracle's
+outcome through skv_compact on ctxs[0]. `timings()["host_parts"]` on ctxs[0] says whether the call
+was split (G x parts per shard) or not.
+"""
+import os
+import random
+
+import pytest
+
+from skv import _abi
+from skv import format as fmt
+from skv import gen
+from skv.api import Compactor, compact_split
+
+import pyoracle
+from test_gpu_parity import _diff, _norm
+
+pytestmark = pytest.mark.gpu
+MiB = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    torch = pytest.importorskip("torch")
+    torch.cuda.init()
+    cs = [Compactor(0) for _ in range(8)]
+    yield cs
+    for c in cs:
+        c.close()
+
+
+def _fixed_run(keys, vlen, tag):
+    return fmt.encode_run([fmt.put(k, bytes([(tag + i) & 0xFF]) * vlen) for i, k in enumerate(keys)])
+
+
+def _streams(rng, k, n, space, klen=12, vlen=40, same=False):
+    base = sorted(rng.sample(range(space), n)) if same else None
+    out = []
+    for s in range(k):
+        ids = base if same else sorted(rng.sample(range(space), n))
+        out.append((s + 1, [_fixed_run([f"k{i:0{klen - 1}d}" for i in ids], vlen, s)]))
+    return out
+
+
+def _both(cs, streams, max_size, flags=0):
+    try:
+        runs, info = pyoracle.compact(streams, max_size, flags, with_result=True)
+        exp = ("ok", _norm(runs), info["dropped_tables"])
+    except _abi.RunError as e:
+        exp = ("err", e.code, e.message)
+    try:
+        got = ("ok", _norm(compact_split(cs, streams, max_size, flags)), 0)
+    except _abi.RunError as e:
+        got = ("err", e.code, e.message)
+    return exp, got
+
+
+def _check(cs, streams, max_size, flags=0, split=True, parts=1):
+    os.environ["SKV_SPLIT_PARTS"] = str(parts)
+    try:
+        exp, got = _both(cs, streams, max_size, flags)
+    finally:
+        os.environ.pop("SKV_SPLIT_PARTS", None)
+    assert exp == got, _diff(exp, got)
+    hp = cs[0].timings()["host_parts"]
+    if split:
+        assert hp == len(cs) * parts, f"not split (host_parts={hp})"
+    else:
+        assert hp != len(cs) * parts
+
+
+@pytest.mark.parametrize("G", [2, 3, 5, 8])
+@pytest.mark.parametrize("max_size", [4 * MiB, 1000, 7777, 1 << 62])
+def test_split_matches_oracle(ctxs, G, max_size):
+    rng = random.Random(G * 1009 + max_size % 991)
+    _check(ctxs[:G], _streams(rng, 8, 3000, 12000), max_size)
+
+
+@pytest.mark.parametrize("G,parts", [(2, 3), (4, 4), (3, 7)])
+def test_parts_inside_shards(ctxs, G, parts):
+    """several key-range parts per shard: survivor numbering chained through the shard's own parts"""
+    rng = random.Random(G * 31 + parts)
+    _check(ctxs[:G], _streams(rng, 8, 4000, 15000), 3000, parts=parts)
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_equal_keys_in_every_stream(ctxs, G):
+    """every stream holds the same keys: each key has its newest version in stream 1, and the cuts
+    fall between keys, never between versions of one key"""
+    rng = random.Random(77 + G)
+    _check(ctxs[:G], _streams(rng, 6, 4000, 9000, same=True), 2000)
+
+
+def test_streams_absent_from_shards(ctxs):
+    """streams over disjoint key ranges: most shards see only some streams, some see one"""
+    streams = []
+    for s in range(6):
+        keys = [f"k{s:02d}{i:09d}" for i in range(0, 6000, 3)]
+        streams.append((s + 1, [_fixed_run(keys, 24, s)]))
+    _check(ctxs[:4], streams, 3333)
+
+
+def test_member_run_streams(ctxs):
+    """an L0 shape: one stream concatenating many disjoint ascending member runs beside buffer
+    streams; member runs straddle the shard cuts"""
+    rng = random.Random(5)
+    ids = sorted(rng.sample(range(200000), 40000))
+    members = [_fixed_run([f"k{i:011d}" for i in ids[j:j + 1000]], 32, j) for j in range(0, len(ids), 1000)]
+    streams = [(0, members)]
+    for s in range(4):
+        streams.append((s + 1, [_fixed_run([f"k{i:011d}" for i in sorted(rng.sample(range(200000), 5000))], 32, s)]))
+    _check(ctxs[:4], streams, 5000)
+
+
+def test_drop_tombstones_flag(ctxs):
+    rng = random.Random(11)
+    _check(ctxs[:3], _streams(rng, 5, 3000, 8000), 4096, flags=_abi.SKV_DROP_TOMBSTONES)
+
+
+def test_config2_shape_against_one_gpu(ctxs):
+    """a config-2B-shape call (16 streams x 20,000 records, 16-B hex keys, 256-B values, ~37 %
+    superseded at full size): the oracle's bytes through 8 shards of several parts each"""
+    streams = gen.config2(seed=4242, n_streams=16, n_records=20000, vsize=256, variant="B")
+    _check(ctxs[:8], streams, 4 * MiB, parts=3)
+
+
+def test_variable_records_take_one_ctx(ctxs):
+    """records of two sizes: outside the split's shape, the call runs as skv_compact on ctxs[0]"""
+    rng = random.Random(3)
+    streams = _streams(rng, 4, 2000, 6000)
+    ops = [fmt.put(f"k{i:011d}", b"v" * (1 + i % 7)) for i in sorted(rng.sample(range(6000), 1500))]
+    streams.append((9, [fmt.encode_run(ops)]))
+    _check(ctxs[:4], streams, 3000, split=False)
+
+
+def test_poisoned_shard_takes_one_ctx(ctxs):
+    """a key decrease inside one stream (inside one shard, so the host cuts do not see it): the
+    shard's verdict sends the call to skv_compact on ctxs[0], whose outcome is the oracle's"""
+    rng = random.Random(19)
+    streams = _streams(rng, 6, 3000, 12000)
+    keys = [f"k{i:011d}" for i in sorted(rng.sample(range(12000), 3000))]
+    keys[1700], keys[1701] = keys[1701], keys[1700]
+    streams[2] = (3, [_fixed_run(keys, 40, 2)])
+    _check(ctxs[:4], streams, 2500, split=False)
+
+
+def test_corrupt_run_error_text(ctxs):
+    """a truncated run: the error is the reference's, reported on ctxs[0]"""
+    rng = random.Random(23)
+    streams = _streams(rng, 4, 2000, 8000)
+    streams[1] = (2, [streams[1][1][0][:-7]])
+    exp, got = _both(ctxs[:3], streams, 4000)
+    assert exp == got and exp[0] == "err", _diff(exp, got)
+
+
+def test_one_ctx_is_compact(ctxs):
+    rng = random.Random(29)
+    streams = _streams(rng, 4, 2000, 8000)
+    exp, got = _both(ctxs[:1], streams, 4000)
+    assert exp == got, _diff(exp, got)
+
+
+def test_repeated_ctx_is_rejected(ctxs):
+    rng = random.Random(31)
+    streams = _streams(rng, 2, 500, 2000)
+    with pytest.raises(_abi.RunError) as ei:
+        compact_split([ctxs[0], ctxs[1], ctxs[0]], streams, 4000)
+    assert ei.value.code == _abi.SKV_E_INVALID_ARG
+
+
+def test_result_kept_and_freed(ctxs):
+    """keep=True: the result's pinned bytes (ctxs[0]'s pool) outlive the call and read back equal"""
+    rng = random.Random(37)
+    streams = _streams(rng, 5, 3000, 9000)
+    exp = pyoracle.compact(streams, 3000, 0)
+    res = compact_split(ctxs[:4], streams, 3000, keep=True)
+    try:
+        data = bytes(res.host_bytes())
+        assert data == b"".join(r.data for r in exp)
+        assert res.n_runs == len(exp)
+    finally:
+        res.free()
