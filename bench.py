@@ -233,6 +233,46 @@ def reduce_over_ranks(elapsed, in_bytes, dist, device):
     return float(t.item()), float(b.item())
 
 
+def split_extra(devices, hstreams, max_run, flags, in_bytes, reps=2):
+    """skv_compact_split over one ctx per entry of `devices` (pinned host inputs, pinned host output):
+    GiB/s of input bytes, best of `reps` after 1 warm-up, beside the same call through skv_compact
+    on the first device alone. Never the bench's outcome: an error is recorded, not raised."""
+    from skv.api import Compactor, compact_split
+
+    try:
+        cs = [Compactor(d) for d in devices]
+        try:
+            compact_split(cs, hstreams, max_run, flags, keep=True).free()
+            best = None
+            for _ in range(reps):
+                t1 = time.perf_counter()
+                r = compact_split(cs, hstreams, max_run, flags, keep=True)
+                dt = time.perf_counter() - t1
+                best = dt if best is None else min(best, dt)
+                out_b = r.n_bytes
+                r.free()
+            parts = int(cs[0].timings()["host_parts"])
+            cs[0].compact_host_ptrs(hstreams, max_run, flags)
+            one = None
+            for _ in range(reps):
+                t1 = time.perf_counter()
+                cs[0].compact_host_ptrs(hstreams, max_run, flags)
+                dt = time.perf_counter() - t1
+                one = dt if one is None else min(one, dt)
+        finally:
+            for c in cs:
+                c.close()
+        return {"value": round(in_bytes / best / GiB, 3), "unit": "GiB/s", "ms": round(best * 1e3, 3),
+                "ctxs": len(devices), "devices": sorted(set(devices)), "parts": parts, "d2h_bytes": out_b,
+                "one_ctx_value": round(in_bytes / one / GiB, 3),
+                "note": f"skv_compact_split over {len(devices)} ctxs (key-range parts dealt round-robin; each "
+                        "part's H2D and kernels on its ctx, its D2H once the survivor counts of all earlier "
+                        f"parts are in), pinned host in/out, best of {reps} after 1 warm-up; one_ctx_value: "
+                        "skv_compact on the first device alone"}
+    except Exception as e:  # a figure for the record, never the bench's outcome
+        return {"value": None, "error": f"{type(e).__name__}: {e}"}
+
+
 def timed_loop(step, steps, barrier):
     """The bench contract's timed region: barrier (+ device sync) on both sides of exactly `steps`
     calls of step(); returns this rank's elapsed seconds (reduce_over_ranks takes the max)."""
@@ -488,27 +528,12 @@ def main():
             "value": round(2 * n_jobs * in_bytes / tp / GiB, 3), "unit": "GiB/s",
             "note": f"2 ctxs x {n_jobs} skv_compact calls from 2 host threads, same pinned inputs"}
         if config in ("2A", "2B", "L0"):
-            # skv_compact_split: the same call as 4 key-range shards on 4 ctxs. Here all
-            # four share this GPU's PCIe link, so the figure is the split's overhead against the
-            # pipelined single-ctx call, not its scaling (G GPUs move G shards over G links)
-            from skv.api import compact_split
-
-            cs = [Compactor(dev_idx) for _ in range(4)]
-            compact_split(cs, hstreams, max_run, flags, keep=True).free()
-            sts = []
-            for _ in range(2):
-                t1 = time.perf_counter()
-                compact_split(cs, hstreams, max_run, flags, keep=True).free()
-                sts.append(time.perf_counter() - t1)
-            st_ = min(sts)
-            sparts = int(cs[0].timings()["host_parts"])
-            for c in cs:
-                c.close()
-            host_path["split_4ctx_1gpu"] = {
-                "value": round(in_bytes / st_ / GiB, 3), "unit": "GiB/s", "ms": round(st_ * 1e3, 3),
-                "parts": sparts,
-                "note": "skv_compact_split over 4 ctxs of this one GPU (one PCIe link shared): each shard's "
-                        "H2D, kernels and D2H in turn; best of 2 after 1 warm-up"}
+            # skv_compact_split: the same call as key-range parts over 4 ctxs. Here all
+            # four share this GPU's PCIe link (their H2D streams interleave, so every part lands late
+            # and its D2H with it): the figure is the split's worst case against the pipelined
+            # single-ctx call, not its scaling (G GPUs move their parts over G links; the N-GPU runs
+            # report split_ngpu)
+            host_path["split_4ctx_1gpu"] = split_extra([dev_idx] * 4, hstreams, max_run, flags, in_bytes)
         del host_runs
         # the ceiling of this figure: the box's PCIe with both directions busy at once (1 GiB H2D on
         # one stream while 1 GiB D2H runs on another, pinned buffers); a host call moves its input
@@ -537,6 +562,18 @@ def main():
             del dbuf_a, dbuf_b, h_a, h_b
         except Exception as e:  # a figure for the record, never the bench's outcome
             host_path["pcie_bidir_GBps"] = f"unmeasured: {e}"
+
+    # SURVEY §8(e) on N GPUs: rank 0's own input as ONE compaction split over all N GPUs of the node,
+    # after the timed region (the other ranks' timed work is over; skv_compact_split drives every
+    # device from this process, one host thread per shard). Not `value`, not part of the timing.
+    split_ngpu = None
+    # (SKV_BENCH_SHARE_DEVICE=1 rehearsals: N ctxs of device 0)
+    if (rank == 0 and world > 1 and config in ("2A", "2B") and not args.no_host_path
+            and os.environ.get("SKV_BENCH_SPLIT", "1") != "0"):
+        host_runs = [r.cpu().pin_memory() for r in runs]
+        hs = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(host_runs)]
+        split_ngpu = split_extra([0] * world if shared else list(range(world)), hs, max_run, flags, in_bytes)
+        del host_runs
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -616,6 +653,8 @@ def main():
         line["invariants"] = invariants
         if host_path is not None:
             line["host_path"] = host_path
+        if split_ngpu is not None:
+            line["split_ngpu"] = split_ngpu
         if concurrent is not None:
             line["concurrent_2ctx"] = concurrent
         if config4 is not None:

@@ -1,57 +1,107 @@
 // skv_split.hip — one compaction split across several GPUs by key range:
 // skv_compact_split, the host-input entry (skv_compact) over G ctxs at once.
 //
-// The call is cut into G key-range shards, each of P_g key-range parts (the cut keys and per-run
-// bounds of the pipelined host call, fx_host_cuts). Shard g runs on ctxs[g]: the H2D of its slices
-// and the fused stride path over its parts, survivors numbered from 0 within the shard (each
-// part's numbering chained on the device through the shard's earlier parts only, FxPartIO::gbase).
-// Equal keys never straddle a cut, so each shard's merge, dedup and record checks are exactly the
-// whole call's restricted to its keys (k_way.rs:113-171; runs.rs:559-624).
+// The call is cut into P = G x P_g key-range parts (the cut keys and per-run bounds of the pipelined
+// host call, fx_host_cuts), dealt round-robin: part p goes to ctxs[p % G]. Each ctx's worker thread
+// queues, for each of its parts, the H2D of the part's slices (in_stream) and the fused stride path
+// over them (the ctx stream), survivors numbered from 0 within the part, and publishes the part's
+// survivor count and verdict to host-mapped words. Equal keys never straddle a cut, so each part's
+// merge, dedup and record checks are exactly the whole call's restricted to its keys
+// (k_way.rs:113-171; runs.rs:559-624).
 //
 // What does not shard is build_runs' greedy split (runs.rs:211-238): it walks the merged records
 // in order. With one record size it is arithmetic in the global survivor index -- survivor i goes to
-// run i / n, slot i % n (n = fx_run_records) -- so the one exchange between the shards is their
-// survivor counts C_g. The host chains them into bases B_g = C_0 + ... + C_{g-1} (G additions, the
-// "carry" of the split), and every shard copies its survivors D2H straight to their global places
-// in the one pinned output buffer: one copy per output run the shard touches. The host writes the
-// version bytes and the descriptors (StatsV1, runs.rs:102-109) arithmetically, as k_fx_desc does.
+// run i / n, slot i % n (n = fx_run_records) -- so the one exchange between the GPUs is the parts'
+// survivor counts C_p. The host chains them into bases B_p = C_0 + ... + C_{p-1} (the "carry" of the
+// split) as they arrive; once B_p is known the worker of part p copies its survivors D2H straight to
+// their global places in the one pinned output buffer (out_stream; one copy per output run the part
+// touches) while its later parts are still arriving and merging. Round-robin dealing keeps the parts
+// in flight on all GPUs close together in key order, so the D2H of round r overlaps the H2D of
+// round r + 1 on every GPU. The host writes the version bytes and the descriptors (StatsV1,
+// runs.rs:102-109) arithmetically, as k_fx_desc does.
 //
-// A call outside the fused shape, a cut that a run decreases across, or a poisoned shard (a record
+// A call outside the fused shape, a cut that a run decreases across, or a poisoned part (a record
 // the fused path does not take, a key decrease) runs as skv_compact on ctxs[0], which gives the
-// reference's exact outcome. A HIP failure in any shard is SKV_E_DEVICE on ctxs[0].
+// reference's exact outcome. A HIP failure on any ctx is SKV_E_DEVICE on ctxs[0].
 #include "skv_host.hpp"
 
 namespace {
 
-struct Shard {
-    skv_ctx* ctx = nullptr;
-    uint64_t p0 = 0, p1 = 0;    // its key-range parts
-    uint64_t R = 0;             // input records
-    uint64_t C = 0;             // survivors
-    uint64_t B = 0;             // survivors of the earlier shards
-    uint8_t* d_out = nullptr;   // survivors 0..C-1 at 1 + j * S
+constexpr uint64_t NPOS = ~0ull;
+
+// State the workers share: the parts' survivor counts as they arrive and the bases chained from them.
+struct Split {
+    const Job* job = nullptr;
+    RunFmt f{};
+    const std::vector<uint64_t>* lb = nullptr;
+    uint64_t P = 0, G = 0, n = 0;
+    uint8_t* h_out = nullptr;
+    uint64_t out_cap = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<uint64_t> cnt;   // part p's survivors (NPOS: not yet known)
+    std::vector<uint64_t> base;  // base[p] = survivors of parts < p, valid for p <= prefix
+    uint64_t prefix = 0;         // parts [0, prefix) have posted their counts
+    bool stop = false;           // a poisoned part or a failed worker: no more egress
     bool poisoned = false;
-    uint32_t reason = 0;
     std::string err;
-    double merge_ms = 0;
+
+    void post(uint64_t p, uint64_t c) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            cnt[p] = c;
+            while (prefix < P && cnt[prefix] != NPOS) {
+                base[prefix + 1] = base[prefix] + cnt[prefix];
+                ++prefix;
+            }
+        }
+        cv.notify_all();
+    }
+    void halt(bool poison, const std::string& e) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+            poisoned = poisoned || poison;
+            if (!e.empty() && err.empty()) err = e;
+        }
+        cv.notify_all();
+    }
+    // B_p once every earlier part has posted; false once the call has stopped
+    bool wait_base(uint64_t p, uint64_t& B) {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || prefix >= p; });
+        if (stop) return false;
+        B = base[p];
+        return true;
+    }
 };
 
-// Shard g up to its survivor count: H2D of its slices on in_stream, the fused path per part on the
-// ctx stream, one readback of the count and the verdict. Runs on its own host thread.
-void shard_merge(Shard& sh, const Job& job, const RunFmt& f, const std::vector<uint64_t>& lb) {
-    skv_ctx* ctx = sh.ctx;
-    const double t0 = now_ms();
-    const uint64_t nr = job.run_ptr.size(), S = f.S, Pn = sh.p1 - sh.p0;
-    // run m's image holds its records [a_m, z_m) of this shard, after the byte before a_m
-    std::vector<uint64_t> base(nr), img(nr + 1, 0);
-    sh.R = 0;
-    for (uint64_t m = 0; m < nr; ++m) {
-        const uint64_t a = lb[sh.p0 * nr + m], z = lb[sh.p1 * nr + m];
-        base[m] = a;
-        sh.R += z - a;
-        img[m + 1] = img[m] + (z > a ? ((1 + (z - a) * S + 15) & ~15ull) : 0);
+// The worker of ctxs[g]: parts g, g + G, g + 2G, ...
+void split_worker(Split& sp, skv_ctx* ctx, uint64_t g) {
+    const Job& job = *sp.job;
+    const std::vector<uint64_t>& lb = *sp.lb;
+    const RunFmt& f = sp.f;
+    const uint64_t nr = job.run_ptr.size(), S = f.S, W = sp.n * S + 1;
+    std::vector<uint64_t> parts;
+    for (uint64_t p = g; p < sp.P; p += sp.G) parts.push_back(p);
+    const uint64_t np = parts.size();
+    // part i's images: run m's slice [a, z) after the byte before a, at in_off[i] + img[i][m];
+    // its survivors at out_off[i] + 1 + j * S (one local run of R_i records)
+    std::vector<std::vector<uint64_t>> img(np), base(np);
+    std::vector<uint64_t> Rp(np, 0), in_off(np + 1, 0), out_off(np + 1, 0);
+    for (uint64_t i = 0; i < np; ++i) {
+        const uint64_t p = parts[i];
+        img[i].assign(nr + 1, 0);
+        base[i].assign(nr, 0);
+        for (uint64_t m = 0; m < nr; ++m) {
+            const uint64_t a = lb[p * nr + m], z = lb[(p + 1) * nr + m];
+            base[i][m] = a;
+            Rp[i] += z - a;
+            img[i][m + 1] = img[i][m] + (z > a ? ((1 + (z - a) * S + 15) & ~15ull) : 0);
+        }
+        in_off[i + 1] = in_off[i] + ((img[i][nr] + 255) & ~255ull);
+        out_off[i + 1] = out_off[i] + ((1 + Rp[i] * S + 16 + 255) & ~255ull);
     }
-    if (!sh.R) return;
     hipStream_t st = ctx->stream;
     struct KernelUploads {  // table uploads by kernel: a DMA upload would queue behind the bulk H2D
         skv_ctx* c;
@@ -62,92 +112,88 @@ void shard_merge(Shard& sh, const Job& job, const RunFmt& f, const std::vector<u
     ctx->up_chunk = 0;
     ctx->up_off = 0;
     if (!ctx->in_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->in_stream, hipStreamNonBlocking));
-    while (ctx->part_ev.size() < Pn) {
+    if (!ctx->out_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->out_stream, hipStreamNonBlocking));
+    while (ctx->part_ev.size() < 2 * np) {
         hipEvent_t e;
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ctx->part_ev.push_back(e);
     }
+    if (ctx->part_k_cap < 2 * np) {
+        if (ctx->part_k) HIPCHK(hipHostFree(ctx->part_k));
+        ctx->part_k = nullptr;
+        ctx->part_k_cap = 0;
+        HIPCHK(host_alloc_near(ctx->device, (void**)&ctx->part_k, std::max<uint64_t>(2 * np, 64) * 8,
+                               hipHostMallocCoherent));
+        ctx->part_k_cap = std::max<uint64_t>(2 * np, 64);
+    }
+    volatile uint64_t* hK = ctx->part_k;  // [2i] survivors of part i, [2i + 1] its verdict words
     // every buffer sized before the first launch (no buffer moves under queued work)
-    uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", img[nr] + 16);
-    const uint64_t n_loc = sh.R, out_cap = 1 + sh.R * S + 16;  // one local run: survivors at 1 + j * S
-    sh.d_out = dbuf<uint8_t>(ctx, "out", out_cap);
-    uint64_t* d_Kp = dbuf<uint64_t>(ctx, "hp_K", Pn);
+    uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", in_off[np] + 16);
+    uint8_t* d_out = dbuf<uint8_t>(ctx, "out", out_off[np] + 16);
+    uint64_t* d_K = dbuf<uint64_t>(ctx, "hp_K", np);
     uint32_t* d_flags = dbuf<uint32_t>(ctx, "hp_flags", 4);
-    FxPartTables pt;
-    fx_part_tables(job, f, sh.p0, sh.p1, lb, d_in, img, &base, pt);
-    RunInfo* d_runs = dbuf<RunInfo>(ctx, "hp_runs", Pn * nr);
-    uint8_t* hp = (uint8_t*)pinned(ctx, 64);
-    h2d_up(ctx, d_runs, pt.runs.data(), Pn * nr * sizeof(RunInfo));
-    HIPCHK(hipMemsetAsync(d_Kp, 0, Pn * 8, st));
+    RunInfo* d_runs = dbuf<RunInfo>(ctx, "hp_runs", np * nr);
+    std::vector<FxPartTables> pt(np);
+    std::vector<RunInfo> rows(np * nr);
+    for (uint64_t i = 0; i < np; ++i) {
+        fx_part_tables(job, f, parts[i], parts[i] + 1, lb, d_in + in_off[i], img[i], &base[i], pt[i]);
+        std::copy(pt[i].runs.begin(), pt[i].runs.end(), rows.begin() + i * nr);
+    }
+    h2d_up(ctx, d_runs, rows.data(), np * nr * sizeof(RunInfo));
+    HIPCHK(hipMemsetAsync(d_K, 0, np * 8, st));
     HIPCHK(hipMemsetAsync(d_flags, 0, 16, st));
-    for (uint64_t i = 0; i < Pn; ++i) {
-        const uint64_t p = sh.p0 + i;
+    for (uint64_t i = 0; i < np; ++i) {
+        hK[2 * i] = NPOS;
+        hK[2 * i + 1] = NPOS;
+    }
+    // ---- queue every part: H2D, the fused path, the count and verdict to host-mapped words
+    for (uint64_t i = 0; i < np; ++i) {
+        const uint64_t p = parts[i];
         for (uint64_t m = 0; m < nr; ++m) {
             const uint64_t a = lb[p * nr + m], z = lb[(p + 1) * nr + m];
             if (z == a) continue;
-            // the byte before record a rides along with the shard's first slice of the run
-            const uint64_t lo = a == base[m] ? a * S : 1 + a * S, hi = 1 + z * S;
-            HIPCHK(hipMemcpyAsync(d_in + img[m] + (lo - base[m] * S), (const uint8_t*)(uintptr_t)job.run_ptr[m] + lo,
-                                  hi - lo, hipMemcpyHostToDevice, ctx->in_stream));
+            HIPCHK(hipMemcpyAsync(d_in + in_off[i] + img[i][m], (const uint8_t*)(uintptr_t)job.run_ptr[m] + a * S,
+                                  1 + (z - a) * S, hipMemcpyHostToDevice, ctx->in_stream));
         }
-        HIPCHK(hipEventRecord(ctx->part_ev[i], ctx->in_stream));
-        HIPCHK(hipStreamWaitEvent(st, ctx->part_ev[i], 0));
-        if (pt.kp[i]) {
+        HIPCHK(hipEventRecord(ctx->part_ev[2 * i], ctx->in_stream));
+        HIPCHK(hipStreamWaitEvent(st, ctx->part_ev[2 * i], 0));
+        if (pt[i].kp[0]) {
             FxPartIO io;
-            io.gbase = i ? d_Kp + i - 1 : nullptr;
-            io.Kout = d_Kp + i;
+            io.gbase = nullptr;
+            io.Kout = d_K + i;
             io.flags = d_flags;
-            io.out = sh.d_out;
+            io.out = d_out + out_off[i];
             uint64_t* rb_unused = nullptr;
-            (void)fx_launch(ctx, pt.kp[i], pt.np[i], d_runs + i * nr, pt.sfr[i], f, pt.recb[i], n_loc, out_cap, &io,
-                            rb_unused);
-        } else if (i) {
-            launch_copy_bytes(st, (uint8_t*)(d_Kp + i), (const uint8_t*)(d_Kp + i - 1), 8);
+            (void)fx_launch(ctx, pt[i].kp[0], pt[i].np[0], d_runs + i * nr, pt[i].sfr[0], f, pt[i].recb[0], Rp[i],
+                            out_off[i + 1] - out_off[i], &io, rb_unused);
         }
+        launch_fx_publish(st, d_K + i, (uint64_t*)hK + 2 * i);
+        launch_fx_publish(st, (const uint64_t*)(d_flags + 2), (uint64_t*)hK + 2 * i + 1);
         HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ctx->part_ev[2 * i + 1], st));
     }
-    d2h(ctx, hp, d_Kp + Pn - 1, 8);
-    d2h(ctx, hp + 16, d_flags, 16);
-    sync(ctx);
-    uint32_t fl[4];
-    memcpy(&sh.C, hp, 8);
-    memcpy(fl, hp + 16, 16);
-    sh.poisoned = fl[2] != 0 || sh.C > sh.R;
-    sh.reason = fl[3];
-    sh.merge_ms = now_ms() - t0;
-}
-
-// Shard g's survivors to their global places: local survivor j is global survivor B + j.
-void shard_egress(Shard& sh, const RunFmt& f, uint64_t n, uint8_t* h_out) {
-    skv_ctx* ctx = sh.ctx;
-    const uint64_t S = f.S, W = n * S + 1;
-    for (uint64_t j = 0; j < sh.C;) {
-        const uint64_t g = sh.B + j, q = g / n, slot = g % n;
-        const uint64_t c = std::min(n - slot, sh.C - j);
-        HIPCHK(hipMemcpyAsync(h_out + q * W + 1 + slot * S, sh.d_out + 1 + j * S, c * S, hipMemcpyDeviceToHost,
-                              ctx->stream));
-        j += c;
+    // ---- as each part ends: post its count; once its base is known, its survivors to their places
+    for (uint64_t i = 0; i < np; ++i) {
+        HIPCHK(hipEventSynchronize(ctx->part_ev[2 * i + 1]));
+        const uint64_t c = hK[2 * i];
+        const uint32_t poison = (uint32_t)hK[2 * i + 1];  // flags[2]: cumulative over this ctx's parts
+        if (poison != 0 || c > Rp[i]) {
+            sp.halt(true, "");
+            break;
+        }
+        sp.post(parts[i], c);
+        uint64_t B = 0;
+        if (!sp.wait_base(parts[i], B)) break;
+        for (uint64_t j = 0; j < c;) {
+            const uint64_t gi = B + j, q = gi / sp.n, slot = gi % sp.n;
+            const uint64_t cc = std::min(sp.n - slot, c - j);
+            if (q * W + 1 + (slot + cc) * S > sp.out_cap) throw DevError("internal: split egress past the output");
+            HIPCHK(hipMemcpyAsync(sp.h_out + q * W + 1 + slot * S, d_out + out_off[i] + 1 + j * S, cc * S,
+                                  hipMemcpyDeviceToHost, ctx->out_stream));
+            j += cc;
+        }
     }
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-}
-
-// fn(shard) on one host thread per shard, on the shard's device; a throw is kept as the shard's error
-template <typename F>
-void on_shards(std::vector<Shard>& sh, F&& fn) {
-    std::vector<std::thread> th;
-    for (Shard& s : sh)
-        th.emplace_back([&s, &fn] {
-            try {
-                DeviceScope ds(s.ctx->device);
-                if (!ds.ok) throw DevError("hipSetDevice failed");
-                fn(s);
-            } catch (const DevError& e) {
-                s.err = e.msg;
-            } catch (const std::exception& e) {
-                s.err = std::string("host error: ") + e.what();
-            }
-        });
-    for (std::thread& t : th) t.join();
+    HIPCHK(hipStreamSynchronize(ctx->out_stream));
 }
 
 }  // namespace
@@ -174,62 +220,58 @@ int skv_compact_split(skv_ctx* const* ctxs, uint32_t n_ctx, const skv_stream* st
         RunFmt f{};
         uint64_t R = 0;
         const uint64_t G = n_ctx;
-        // shards of P_g parts each (a part is at most ~256 MiB of input, as in the pipelined call)
+        // P_g parts per ctx (a part is at most ~256 MiB of input, as in the pipelined call)
         uint64_t Pg = std::max<uint64_t>(1, std::min<uint64_t>(16, job.in_bytes / G / (256ull << 20)));
         if (const char* e = getenv("SKV_SPLIT_PARTS")) Pg = std::max<uint64_t>(1, std::min<uint64_t>(64, strtoull(e, nullptr, 10)));
         const uint64_t P = G * Pg;
         std::vector<uint64_t> lb;
-        // one D2H copy per output run a shard touches: a split into tiny runs stays on one GPU
+        // one D2H copy per output run a part touches: a split into tiny runs stays on one GPU
         if (fx_host_shape(job, f, R) && R >= P * 64 &&
             R / fx_run_records(max_run_size, f.S, R) <= (1u << 16) && fx_host_cuts(job, f, P, lb)) {
             try {
-                std::vector<Shard> sh(G);
-                for (uint64_t g = 0; g < G; ++g) {
-                    sh[g].ctx = ctxs[g];
-                    sh[g].p0 = g * Pg;
-                    sh[g].p1 = (g + 1) * Pg;
-                }
-                on_shards(sh, [&](Shard& s) { shard_merge(s, job, f, lb); });
-                std::string err;
-                bool poisoned = false;
-                uint64_t C = 0;
-                for (Shard& s : sh) {
-                    if (!s.err.empty() && err.empty()) err = s.err;
-                    poisoned = poisoned || s.poisoned;
-                    s.B = C;  // the carry of build_runs' split: survivors of the earlier shards
-                    C += s.C;
-                }
-                if (!err.empty()) {
-                    for (Shard& s : sh) {
-                        DeviceScope ds(s.ctx->device);
-                        drain(s.ctx);
-                    }
-                    return set_err(home, SKV_E_DEVICE, "split shard: %s", err.c_str());
-                }
-                if (!poisoned) {
-                    const uint64_t n = fx_run_records(max_run_size, f.S, R), W = n * f.S + 1;
-                    const uint64_t runs = (C + n - 1) / n, bytes = C * f.S + runs;
-                    size_t cap = 0;
-                    uint8_t* h_out = (uint8_t*)home->out_pool->take(std::max<uint64_t>(bytes, 1), cap);
-                    if (!h_out) return set_err(home, SKV_E_DEVICE, "pinned host allocation of the output failed");
-                    const double t_eg = now_ms();
-                    on_shards(sh, [&](Shard& s) { shard_egress(s, f, n, h_out); });
-                    for (Shard& s : sh)
-                        if (!s.err.empty()) {
-                            for (Shard& x : sh) {  // no copy still writes h_out once it is back in the pool
-                                DeviceScope ds(x.ctx->device);
-                                drain(x.ctx);
-                            }
-                            home->out_pool->give(h_out, cap);
-                            return set_err(home, SKV_E_DEVICE, "split shard egress: %s", s.err.c_str());
+                const uint64_t n = fx_run_records(max_run_size, f.S, R), W = n * f.S + 1;
+                Split sp;
+                sp.job = &job;
+                sp.f = f;
+                sp.lb = &lb;
+                sp.P = P;
+                sp.G = G;
+                sp.n = n;
+                sp.cnt.assign(P, NPOS);
+                sp.base.assign(P + 1, 0);
+                // sized for every record surviving (the counts arrive while the copies run)
+                sp.out_cap = R * f.S + (R + n - 1) / n;
+                size_t cap = 0;
+                sp.h_out = (uint8_t*)home->out_pool->take(std::max<uint64_t>(sp.out_cap, 1), cap);
+                if (!sp.h_out) return set_err(home, SKV_E_DEVICE, "pinned host allocation of the output failed");
+                std::vector<std::thread> th;
+                for (uint64_t g = 0; g < G; ++g)
+                    th.emplace_back([&sp, ctx = ctxs[g], g] {
+                        DeviceScope ds(ctx->device);
+                        try {
+                            if (!ds.ok) throw DevError("hipSetDevice failed");
+                            split_worker(sp, ctx, g);
+                        } catch (const DevError& e) {
+                            sp.halt(false, e.msg);
+                        } catch (const std::exception& e) {
+                            sp.halt(false, std::string("host error: ") + e.what());
                         }
+                        drain(ctx);  // nothing of this call still runs on the ctx (nor writes h_out)
+                    });
+                for (std::thread& t : th) t.join();
+                if (!sp.err.empty() || sp.poisoned) {
+                    home->out_pool->give(sp.h_out, cap);
+                    if (!sp.err.empty()) return set_err(home, SKV_E_DEVICE, "split: %s", sp.err.c_str());
+                } else {
+                    const uint64_t C = sp.base[P];
+                    const uint64_t runs = (C + n - 1) / n, bytes = C * f.S + runs;
                     ResultBox* box = new ResultBox();
                     skv_result* res = &box->pub;
                     res->runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, runs) * sizeof(skv_run_desc));
                     for (uint64_t r = 0; r < runs; ++r) {
                         const uint64_t c = std::min(n, C - r * n);
                         skv_run_desc& d = res->runs[r];
-                        h_out[r * W] = 1;  // RUN_VERSION_V1 (runs.rs:241-244)
+                        sp.h_out[r * W] = 1;  // RUN_VERSION_V1 (runs.rs:241-244)
                         d.off = r * W;
                         d.len = 1 + c * f.S;
                         d.put_count = c;
@@ -242,7 +284,7 @@ int skv_compact_split(skv_ctx* const* ctxs, uint32_t n_ctx, const skv_stream* st
                         d.reserved = 0;
                     }
                     res->n_runs = runs;
-                    res->bytes = h_out;
+                    res->bytes = sp.h_out;
                     res->n_bytes = bytes;
                     res->in_bytes = job.in_bytes;
                     res->in_records = R;
@@ -253,9 +295,6 @@ int skv_compact_split(skv_ctx* const* ctxs, uint32_t n_ctx, const skv_stream* st
                     skv_timings& t = home->timings;
                     t = skv_timings{};
                     t.path = SKV_PATH_FUSED;
-                    t.merge_ms = 0;
-                    for (const Shard& s : sh) t.merge_ms = std::max(t.merge_ms, s.merge_ms);
-                    t.gather_ms = now_ms() - t_eg;  // the shards' D2H copies to their global places
                     t.hot_read_bytes = R * f.S;
                     t.hot_write_bytes = bytes;
                     t.host_parts = (uint32_t)P;
@@ -270,7 +309,7 @@ int skv_compact_split(skv_ctx* const* ctxs, uint32_t n_ctx, const skv_stream* st
             }
         }
     }
-    // outside the split's shape, or a poisoned shard: the whole call on ctxs[0] (exact outcome)
+    // outside the split's shape, or a poisoned part: the whole call on ctxs[0] (exact outcome)
     return skv_compact(home, streams, n_streams, max_run_size, flags, out);
 }
 

@@ -1,13 +1,13 @@
 """One compaction split across several GPUs by key range (skv_compact_split, skv_split.hip; SURVEY
-§8(e)). On the one-GPU test box the G shards run on G ctxs of device 0, one host thread each: the
-same code as G GPUs (each shard stages, merges and deduplicates its key range on its own ctx and
-stream; only the survivor counts cross between shards; every shard copies its survivors D2H to
-their global places in one output). Outputs must be the oracle's, byte for byte, for any G, any
-max_run_size (run boundaries fall inside shards and at shard edges), equal keys across streams,
-streams absent from some shards, and member-run (L0) streams. Calls outside the split's shape
-(variable-length records) and calls a shard poisons (a key decrease) must end with the oracle's
-outcome through skv_compact on ctxs[0]. `timings()["host_parts"]` on ctxs[0] says whether the call
-was split (G x parts per shard) or not.
+§8(e)). On the one-GPU test box the G ctxs are G ctxs of device 0, one host thread each: the same
+code as G GPUs (key-range parts dealt round-robin over the ctxs; each part staged, merged and
+deduplicated on its ctx and stream; only the parts' survivor counts cross between ctxs; each part's
+survivors copied D2H to their global places once every earlier part's count is in). Outputs must be
+the oracle's, byte for byte, for any G, any parts per ctx, any max_run_size (run boundaries fall
+inside parts and at part edges), equal keys across streams, streams absent from some parts, and
+member-run (L0) streams. Calls outside the split's shape (variable-length records) and calls a part
+poisons (a key decrease) must end with the oracle's outcome through skv_compact on ctxs[0].
+`timings()["host_parts"]` on ctxs[0] says whether the call was split (G x parts per ctx) or not.
 """
 import os
 import random
