@@ -40,4 +40,6 @@ for c in ${CONFIGS:-2A 2B 3 3F 5 L0}; do
     python3 tools/traffic.py "$O/pmc_$c" $c "$O/traffic.json" > "$O/traffic_$c.txt"
     sed -n 1,3p "$O/traffic_$c.txt"
   fi
+  # the per-dispatch CSVs are large (3F: past what a gpurun call brings back); the summaries stay
+  [ "${KEEP_TRACES:-0}" = 1 ] || rm -rf "$O/trace_$c" "$O/pmc_$c"
 done
