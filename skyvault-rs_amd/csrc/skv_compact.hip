@@ -245,14 +245,6 @@ int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, con
             const int code = derr_to_api(d.err, msg);
             ev.push_back({heap->pos_of_original(d.rec), 2, code, msg});
         }
-    if (getenv("SKV_HEAP_DEBUG")) {
-        fprintf(stderr, "[wal] K=%llu heap=%d badkey=%lld sendfail=%lld\n", (unsigned long long)K, heap ? 1 : 0,
-                (long long)h[0], (long long)h[4]);
-        for (const JobEvent& e : ev) fprintf(stderr, "  event pos=%llu sub=%d code=%d %s\n", (unsigned long long)e.pos, e.sub, e.code, e.msg.c_str());
-        if (heap)
-            for (uint64_t r = 0; r < R && r < 64; ++r)
-                fprintf(stderr, "  rec %llu pop=%llu\n", (unsigned long long)r, (unsigned long long)read_dev(heap->pop_pos + r));
-    }
     throw_first(ev);
     const uint64_t n_tables = h[1], n_kept = h[2], n_bytes = h[3];
     skv_run_desc* runs = (skv_run_desc*)malloc(std::max<uint64_t>(1, n_kept) * sizeof(skv_run_desc));
@@ -1363,22 +1355,6 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         HIPCHK(hipGetLastError());
         sync(ctx);  // (read_dev copies on the null stream, which does not wait for the ctx stream)
         const uint64_t v = read_dev((const uint64_t*)first_bad);
-        if (getenv("SKV_HEAP_DEBUG")) {  // diagnostic: the merged sequence of heap-order mode
-            const uint64_t K = read_dev(d_K);
-            fprintf(stderr, "[heap] R=%llu K=%llu first_bad=%lld\n", (unsigned long long)R, (unsigned long long)K,
-                    (long long)v);
-            const uint32_t* effp = (const uint32_t*)ctx->bufs["heap_eff"].p;
-            for (uint64_t i = 0; i < R && i < 40; ++i)
-                fprintf(stderr, "  rec %llu hi=%016llx lo=%016llx klen=%u eff=%u key=%s\n", (unsigned long long)i,
-                        (unsigned long long)read_dev(rec_hi + i), (unsigned long long)read_dev(rec_lo + i),
-                        read_dev(rec_klen + i), effp ? read_dev(effp + i) : 0u, fetch_key(ctx, rec_addr, rec_klen, i).c_str());
-            for (uint64_t g = 0; g < K && g < 200; ++g) {
-                const uint32_t r = read_dev(m_rec + g);
-                fprintf(stderr, "  g=%llu rec=%u pop=%llu key=%s cmpkey=%s\n", (unsigned long long)g, r,
-                        (unsigned long long)read_dev(pop_pos + r), fetch_key(ctx, rec_addr, rec_klen, r).c_str(),
-                        fetch_key(ctx, cmp_addr, cmp_klen, r).c_str());
-            }
-        }
         std::vector<JobEvent> ev;
         if (v != ~0ull)
             ev.push_back({read_dev(pop_pos + read_dev(m_rec + v)), 0, SKV_E_FORMAT,
@@ -1427,7 +1403,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         }
     }
     launch_chain(st, d_K, m_P, job.max_run_size, tile_max, T0, run_b, d_nruns, chain_tbl, R, in_rec_bytes, &sp);
-    if (sp.nseg_cap && getenv("SKV_SPLIT_DEBUG")) {
+    if (sp.nseg_cap && getenv("SKV_SPLIT_DEBUG")) {  // tests/test_gpu_split.py reads which split ran
         sync(ctx);
         SplitPlan pl;
         HIPCHK(hipMemcpy(&pl, sp.plan, sizeof(pl), hipMemcpyDeviceToHost));
