@@ -187,3 +187,9 @@ def test_result_kept_and_freed(ctxs):
         assert res.n_runs == len(exp)
     finally:
         res.free()
+
+
+def test_tiny_call_takes_one_ctx(ctxs):
+    """fewer records than the parts need (64 per part): skv_compact on ctxs[0]"""
+    rng = random.Random(41)
+    _check(ctxs[:4], _streams(rng, 2, 50, 400), 2000, split=False)
