@@ -527,10 +527,9 @@ def main():
             "note": f"2 ctxs x {n_jobs} skv_compact calls from 2 host threads, same pinned inputs"}
         if config in ("2A", "2B", "L0"):
             # skv_compact_split: the same call as key-range parts over 4 ctxs. Here all
-            # four share this GPU's PCIe link (their H2D streams interleave, so every part lands late
-            # and its D2H with it): the figure is the split's worst case against the pipelined
-            # single-ctx call, not its scaling (G GPUs move their parts over G links; the N-GPU runs
-            # report split_ngpu)
+            # four share this GPU's PCIe link, so the figure is the split's overhead against the
+            # pipelined single-ctx call, not its scaling (G GPUs move their parts over G links; the
+            # N-GPU runs report split_ngpu)
             host_path["split_4ctx_1gpu"] = split_extra([dev_idx] * 4, hstreams, max_run, flags, in_bytes)
         del host_runs
         # the ceiling of this figure: the box's PCIe with both directions busy at once (1 GiB H2D on

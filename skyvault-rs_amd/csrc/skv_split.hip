@@ -45,6 +45,10 @@ struct Split {
     bool stop = false;           // a poisoned part or a failed worker: no more egress
     bool poisoned = false;
     std::string err;
+    // ctxs that share a device: their parts' H2D go in part order (each waits for the previous
+    // part of its device), so the first parts land first instead of all parts at once
+    std::vector<int64_t> prev_on_dev;  // the part before p on p's device from another ctx, or -1
+    std::vector<hipEvent_t> h2d_ev;    // part p's H2D-complete event, once its worker recorded it
 
     void post(uint64_t p, uint64_t c) {
         {
@@ -65,6 +69,19 @@ struct Split {
             if (!e.empty() && err.empty()) err = e;
         }
         cv.notify_all();
+    }
+    void h2d_post(uint64_t p, hipEvent_t e) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            h2d_ev[p] = e;
+        }
+        cv.notify_all();
+    }
+    // the H2D event of part q once recorded; null once the call has stopped
+    hipEvent_t h2d_wait(uint64_t q) {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || h2d_ev[q] != nullptr; });
+        return stop ? nullptr : h2d_ev[q];
     }
     // B_p once every earlier part has posted; false once the call has stopped
     bool wait_base(uint64_t p, uint64_t& B) {
@@ -149,6 +166,11 @@ void split_worker(Split& sp, skv_ctx* ctx, uint64_t g) {
     // ---- queue every part: H2D, the fused path, the count and verdict to host-mapped words
     for (uint64_t i = 0; i < np; ++i) {
         const uint64_t p = parts[i];
+        if (sp.prev_on_dev[p] >= 0) {
+            const hipEvent_t e = sp.h2d_wait((uint64_t)sp.prev_on_dev[p]);
+            if (!e) return;  // the call has stopped (a poisoned part or a failed worker)
+            HIPCHK(hipStreamWaitEvent(ctx->in_stream, e, 0));
+        }
         for (uint64_t m = 0; m < nr; ++m) {
             const uint64_t a = lb[p * nr + m], z = lb[(p + 1) * nr + m];
             if (z == a) continue;
@@ -156,6 +178,7 @@ void split_worker(Split& sp, skv_ctx* ctx, uint64_t g) {
                                   1 + (z - a) * S, hipMemcpyHostToDevice, ctx->in_stream));
         }
         HIPCHK(hipEventRecord(ctx->part_ev[2 * i], ctx->in_stream));
+        sp.h2d_post(p, ctx->part_ev[2 * i]);
         HIPCHK(hipStreamWaitEvent(st, ctx->part_ev[2 * i], 0));
         if (pt[i].kp[0]) {
             FxPartIO io;
@@ -239,6 +262,17 @@ int skv_compact_split(skv_ctx* const* ctxs, uint32_t n_ctx, const skv_stream* st
                 sp.n = n;
                 sp.cnt.assign(P, NPOS);
                 sp.base.assign(P + 1, 0);
+                sp.h2d_ev.assign(P, nullptr);
+                sp.prev_on_dev.assign(P, -1);
+                {
+                    std::map<int, uint64_t> last;  // device -> its latest part so far
+                    for (uint64_t p = 0; p < P; ++p) {
+                        const int dv = ctxs[p % G]->device;
+                        auto it = last.find(dv);
+                        if (it != last.end() && it->second % G != p % G) sp.prev_on_dev[p] = (int64_t)it->second;
+                        last[dv] = p;
+                    }
+                }
                 // sized for every record surviving (the counts arrive while the copies run)
                 sp.out_cap = R * f.S + (R + n - 1) / n;
                 size_t cap = 0;
