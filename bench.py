@@ -266,8 +266,8 @@ def split_extra(devices, hstreams, max_run, flags, in_bytes, reps=2):
                 "ctxs": len(devices), "devices": sorted(set(devices)), "parts": parts, "d2h_bytes": out_b,
                 "one_ctx_value": round(in_bytes / one / GiB, 3),
                 "note": f"skv_compact_split over {len(devices)} ctxs (key-range parts dealt round-robin; each "
-                        "part's H2D and kernels on its ctx, its D2H once the survivor counts of all earlier "
-                        f"parts are in), pinned host in/out, best of {reps} after 1 warm-up; one_ctx_value: "
+                        "part's H2D and kernels on its ctx, its D2H once the output size of every earlier part "
+                        f"is known), pinned host in/out, best of {reps} after 1 warm-up; one_ctx_value: "
                         "skv_compact on the first device alone"}
     except Exception as e:  # a figure for the record, never the bench's outcome
         return {"value": None, "error": f"{type(e).__name__}: {e}"}
@@ -525,7 +525,7 @@ def main():
         host_path["pipelined_2ctx"] = {
             "value": round(2 * n_jobs * in_bytes / tp / GiB, 3), "unit": "GiB/s",
             "note": f"2 ctxs x {n_jobs} skv_compact calls from 2 host threads, same pinned inputs"}
-        if config in ("2A", "2B", "L0"):
+        if config in ("2A", "2B", "L0", "3"):
             # skv_compact_split: the same call as key-range parts over 4 ctxs. Here all
             # four share this GPU's PCIe link, so the figure is the split's overhead against the
             # pipelined single-ctx call, not its scaling (G GPUs move their parts over G links; the

@@ -186,13 +186,14 @@ int skv_compact_dev(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams,
 /*
  * One compaction split across several GPUs by key range: skv_compact's inputs,
  * semantics, errors and result (pinned host memory, owned by ctxs[0]'s pool), with the work of one
- * call spread over n_ctx distinct ctxs -- normally one per GPU. Shard g (a key range of every
- * stream; equal keys never straddle a cut) is staged, merged and deduplicated on ctxs[g]; the
- * shards exchange only their survivor counts, from which build_runs' greedy split (runs.rs:211-238)
- * places every shard's survivors in the one output. Taken for calls of one record size with keys of
- * at most 16 bytes (the fused stride path); every other call, and any shard whose records that path
- * does not take, runs as skv_compact on ctxs[0]. Errors are reported on ctxs[0]. The ctxs must not
- * be used by other threads during the call. n_ctx == 1 is skv_compact.
+ * call spread over n_ctx distinct ctxs -- normally one per GPU. The call's key-range parts (equal
+ * keys never straddle a cut) are staged, merged and deduplicated on the ctxs in parallel;
+ * build_runs' greedy split (runs.rs:211-238) is carried across the parts: arithmetically from the
+ * parts' survivor counts for one record size with keys of at most 16 bytes, else by each part's
+ * split continuing the open run the previous part left. WAL flushes (SKV_SPLIT_BY_TABLE), calls of
+ * more than 2^16 member runs, and any call a part finds a data error in run as skv_compact on
+ * ctxs[0], which reports the reference's outcome. Errors are reported on ctxs[0]. The ctxs must
+ * not be used by other threads during the call. n_ctx == 1 is skv_compact.
  */
 int skv_compact_split(skv_ctx* const* ctxs, uint32_t n_ctx, const skv_stream* streams, uint32_t n_streams,
                       uint64_t max_run_size, uint32_t flags, skv_result** out);

@@ -1402,7 +1402,36 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             sp.ends = dbuf<uint32_t>(ctx, "split_ends", (uint64_t)sp.nseg_cap * sp.nc + 4);
         }
     }
-    launch_chain(st, d_K, m_P, job.max_run_size, tile_max, T0, run_b, d_nruns, chain_tbl, R, in_rec_bytes, &sp);
+    // a part of skv_compact_split (variable-length records): the split continues the open run of
+    // the previous part -- records [0, e1) join it (run 0, a continuation), the rest split afresh
+    uint64_t carry_c = 0, carry_e1 = 0;
+    if (job.carry) {
+        if (!job.carry->wait_in(job.carry_part, carry_c)) throw DevError("split stopped");
+        if (carry_c) {
+            uint64_t* d_cf = dbuf<uint64_t>(ctx, "carry_first", 4);
+            launch_carry_first(st, d_K, m_P, job.max_run_size, carry_c, d_cf);
+            uint64_t* hcf = (uint64_t*)pinned(ctx, 16);
+            d2h(ctx, hcf, d_cf, 16);
+            sync(ctx);
+            carry_e1 = hcf[0];
+            if (carry_e1) {
+                const uint64_t K_all = hcf[0] + hcf[1];
+                launch_chain(st, d_cf + 1, m_P + carry_e1, job.max_run_size, tile_max, T0, run_b + 1, d_nruns,
+                             chain_tbl, R, in_rec_bytes, &sp);
+                launch_carry_fix(st, run_b, d_nruns, m_P, carry_e1, K_all);
+            }
+        }
+    }
+    if (!carry_e1)
+        launch_chain(st, d_K, m_P, job.max_run_size, tile_max, T0, run_b, d_nruns, chain_tbl, R, in_rec_bytes, &sp);
+    if (job.carry) {  // the open run this part leaves: the next part's split can start
+        uint64_t* d_co = dbuf<uint64_t>(ctx, "carry_out", 1);
+        launch_carry_out(st, run_b, d_nruns, m_P, carry_c, carry_e1 ? 1u : 0u, d_co);
+        uint64_t* hco = (uint64_t*)pinned(ctx, 16);
+        d2h(ctx, hco, d_co, 8);
+        sync(ctx);
+        job.carry->post_out(job.carry_part, hco[0], carry_e1 != 0);
+    }
     if (sp.nseg_cap && getenv("SKV_SPLIT_DEBUG")) {  // tests/test_gpu_split.py reads which split ran
         sync(ctx);
         SplitPlan pl;

@@ -253,6 +253,16 @@ void sync(skv_ctx* ctx);
 void mark(skv_ctx* ctx, Phase p);
 int derr_to_api(uint32_t e, std::string& msg);
 // ------------------------------------------------------------------------------------------
+// A part of skv_compact_split's split of variable-length records (skv_hostpipe.hip): build_runs'
+// greedy split continues across parts, so each part's split starts from the open run the previous
+// part left (its bytes) and hands its own on. wait_in blocks until that is known (false: the call
+// has stopped); post_out may be called again with the same value (a part that reruns).
+struct CarryHook {
+    virtual ~CarryHook() = default;
+    virtual bool wait_in(uint64_t part, uint64_t& c) = 0;
+    virtual void post_out(uint64_t part, uint64_t c, bool cont) = 0;  // cont: run 0 continues the carried run
+};
+
 struct Job {
     std::vector<InStream> ranked;  // streams sorted by seq_no descending
     std::vector<uint64_t> run_ptr, run_len;  // member runs, caller order (flat: 10^6-stream jobs)
@@ -280,6 +290,8 @@ struct Job {
     // leading byte is not a version byte, and the output goes to dev_out (the call's shared buffer)
     bool part = false;
     uint8_t* dev_out = nullptr;
+    CarryHook* carry = nullptr;  // a part of skv_compact_split's variable-record split
+    uint64_t carry_part = 0;
 };
 
 std::string fetch_key(skv_ctx* ctx, const uint64_t* d_rec_addr, const uint32_t* d_rec_klen, uint64_t rec);
@@ -388,6 +400,10 @@ int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t max_
 void drain(skv_ctx* ctx);
 int run_guarded(skv_ctx* ctx, const Job& job, skv_result** out, double t_entry);
 int compact_host_job(skv_ctx* ctx, Job& job, skv_result** out, double t_entry);
+// skv_compact_split for inputs outside the fused shape (variable-length records, Deletes): key-range
+// parts over the ctxs with build_runs' split carried from part to part (skv_hostpipe.hip). used =
+// false: not taken, or a part hit a data error -- the caller runs skv_compact on ctxs[0]
+int compact_split_general(skv_ctx* const* ctxs, uint32_t G, Job& job, skv_result** out, double t_entry, bool& used);
 // skv_scan_host.hip: the scan's device stage after the merge, and read_run_iter's error text
 struct ScanEvent {  // a run's decode error and the record it surfaces after
     uint32_t s;             // stream (rank order)

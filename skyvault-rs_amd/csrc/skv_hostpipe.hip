@@ -722,6 +722,51 @@ static bool wal_part_in_range(skv_ctx* ctx, const skv_result* pres, const uint8_
     return (!lo || *lo <= mn) && (!hi || mx < *hi);
 }
 
+// Cut keys of a general key-range split: quantiles of records found at evenly spaced offsets of the
+// whole input (about 8192 samples whatever the fan-in: a WAL flush of 10^6 tiny runs samples a subset
+// of them); P - 1 of them, fewer when samples repeat. WAL flushes cut at canonical table prefixes.
+static bool sample_cuts(const Job& job, bool wal, uint64_t P, std::vector<std::string>& cut) {
+    const uint64_t nr = job.run_ptr.size();
+    auto run_b = [&](uint64_t m) { return (const uint8_t*)(uintptr_t)job.run_ptr[m]; };
+    std::vector<uint64_t> rpre(nr + 1, 0);
+    for (uint64_t m = 0; m < nr; ++m) rpre[m + 1] = rpre[m] + job.run_len[m];
+    const uint64_t NS = 8192;
+    std::vector<std::pair<const uint8_t*, uint64_t>> smp(NS, {nullptr, 0});
+    par_run(NS, 16, [&](unsigned, uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi; ++i) {
+            const uint64_t g = (2 * i + 1) * rpre[nr] / (2 * NS);
+            const uint64_t m = (uint64_t)(std::upper_bound(rpre.begin(), rpre.end(), g) - rpre.begin()) - 1;
+            const uint8_t* rb = run_b(m);
+            const uint64_t len = job.run_len[m];
+            const uint64_t q = resync(rb, len, std::max<uint64_t>(1, g - rpre[m]));
+            if (q == NPOS || q >= len) continue;
+            const uint64_t kl = be32(rb + q + 1);
+            if (wal) {
+                const uint64_t pl = wal_canon_prefix(rb + q + 5, kl);
+                if (pl) smp[i] = {rb + q + 5, pl};
+            } else {
+                smp[i] = {rb + q + 5, kl};
+            }
+        }
+    });
+    smp.erase(std::remove_if(smp.begin(), smp.end(), [](const auto& e) { return e.first == nullptr; }), smp.end());
+    htrace("gpipe: sampled");
+    if (smp.size() < P) {
+        htrace("gpipe: too few samples");
+        return false;
+    }
+    std::sort(smp.begin(), smp.end(), [](const auto& a, const auto& c) {
+        return host_key_cmp(a.first, a.second, c.first, c.second) < 0;
+    });
+    cut.clear();
+    for (uint64_t p = 1; p < P; ++p) {
+        const auto& e = smp[p * smp.size() / P];
+        std::string c((const char*)e.first, e.second);
+        if (cut.empty() || cut.back() < c) cut.push_back(c);  // (Rust str order = bytewise = std::string's)
+    }
+    return true;
+}
+
 static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** out, double t_entry, bool& used) {
     used = false;
     const char* pe = getenv("SKV_HOST_PIPE");
@@ -761,42 +806,8 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     // WAL flushes cut at canonical table prefixes "{id}.": every key of a table sorts at or after
     // its prefix and before the next table's, so a part holds whole tables (the one-run rule and the
     // prefix strip stay per table); a key that is not canonical ends the attempt in its part.
-    std::vector<uint64_t> rpre(nr + 1, 0);
-    for (uint64_t m = 0; m < nr; ++m) rpre[m + 1] = rpre[m] + job.run_len[m];
-    const uint64_t NS = 8192;
-    std::vector<std::pair<const uint8_t*, uint64_t>> smp(NS, {nullptr, 0});
-    par_run(NS, 16, [&](unsigned, uint64_t lo, uint64_t hi) {
-        for (uint64_t i = lo; i < hi; ++i) {
-            const uint64_t g = (2 * i + 1) * rpre[nr] / (2 * NS);
-            const uint64_t m = (uint64_t)(std::upper_bound(rpre.begin(), rpre.end(), g) - rpre.begin()) - 1;
-            const uint8_t* rb = run_b(m);
-            const uint64_t len = job.run_len[m];
-            const uint64_t q = resync(rb, len, std::max<uint64_t>(1, g - rpre[m]));
-            if (q == NPOS || q >= len) continue;
-            const uint64_t kl = be32(rb + q + 1);
-            if (wal) {
-                const uint64_t pl = wal_canon_prefix(rb + q + 5, kl);
-                if (pl) smp[i] = {rb + q + 5, pl};
-            } else {
-                smp[i] = {rb + q + 5, kl};
-            }
-        }
-    });
-    smp.erase(std::remove_if(smp.begin(), smp.end(), [](const auto& e) { return e.first == nullptr; }), smp.end());
-    htrace("gpipe: sampled");
-    if (smp.size() < P) {
-        htrace("gpipe: too few samples");
-        return SKV_OK;
-    }
-    std::sort(smp.begin(), smp.end(), [](const auto& a, const auto& c) {
-        return host_key_cmp(a.first, a.second, c.first, c.second) < 0;
-    });
     std::vector<std::string> cut;
-    for (uint64_t p = 1; p < P; ++p) {
-        const auto& e = smp[p * smp.size() / P];
-        std::string c((const char*)e.first, e.second);
-        if (cut.empty() || cut.back() < c) cut.push_back(c);  // (Rust str order = bytewise = std::string's)
-    }
+    if (!sample_cuts(job, wal, P, cut)) return SKV_OK;
     P = cut.size() + 1;
     if (P < 2 || (!wal && job.max_run_size > job.in_bytes / (4 * P))) return SKV_OK;
     // ---- bnd[p * nr + m]: byte offset of run m's first record >= cut p (1 / len at the ends)
@@ -1204,6 +1215,342 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     t.host_total_ms = now_ms() - t_entry;
     t.host_parts = (uint32_t)P;
     t.wal_stage = wal ? 1 : 0;
+    *out = res;
+    return SKV_OK;
+}
+
+// ---- skv_compact_split for variable-length records -----------------------------
+// The call is cut into P key-range parts (sample_cuts / cut_runs, as the general pipeline) dealt
+// round-robin over the ctxs. Each ctx's worker stages its parts' slices (in_stream, all queued up
+// front) and compacts them one by one in part mode, each into its own region of the ctx's output
+// buffer. The merges run in parallel on the GPUs; build_runs' greedy split (runs.rs:211-238) does
+// not, so each part's split waits inside compact_device (Job::carry) for the open run the previous
+// part left, and hands its own on as soon as its split is done (the serial chain SURVEY §8(e)
+// describes: one split pass per part, each a few ms, while later parts still merge). A part whose
+// first run continues the carried run writes it after a version byte that is not copied out; its
+// descriptor is merged into the previous part's last. Once the output bytes of every earlier part
+// are known, a part's bytes go D2H to their place in the one pinned output (out_stream).
+namespace {
+struct GSplit : CarryHook {
+    uint64_t P = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<uint64_t> carry;    // carry[p + 1]: the open run part p leaves (bytes; carry[0] = 0)
+    std::vector<uint8_t> have_c;    // carry[p] known
+    std::vector<uint8_t> cont;      // part p's run 0 continues the carried run
+    std::vector<uint64_t> nbytes;   // part p's output bytes (after the dropped version byte)
+    std::vector<uint8_t> have_b;
+    std::vector<uint64_t> off;      // off[p]: output bytes of parts < p, valid for p <= prefix
+    uint64_t prefix = 0;
+    bool stop = false, data_err = false;
+    std::string err;
+    std::vector<std::vector<skv_run_desc>> descs;  // part p's runs, offsets already global
+    std::vector<uint64_t> in_recs;
+
+    bool wait_in(uint64_t part, uint64_t& c) override {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || have_c[part]; });
+        if (stop) return false;
+        c = carry[part];
+        return true;
+    }
+    void post_out(uint64_t part, uint64_t c, bool is_cont) override {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            carry[part + 1] = c;
+            have_c[part + 1] = 1;
+            cont[part] = is_cont ? 1 : 0;
+        }
+        cv.notify_all();
+    }
+    void post_bytes(uint64_t part, uint64_t n) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            nbytes[part] = n;
+            have_b[part] = 1;
+            while (prefix < P && have_b[prefix]) {
+                off[prefix + 1] = off[prefix] + nbytes[prefix];
+                ++prefix;
+            }
+        }
+        cv.notify_all();
+    }
+    bool wait_off(uint64_t part, uint64_t& o) {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || prefix >= part; });
+        if (stop) return false;
+        o = off[part];
+        return true;
+    }
+    void halt(bool data, const std::string& e) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+            data_err = data_err || data;
+            if (!e.empty() && err.empty()) err = e;
+        }
+        cv.notify_all();
+    }
+};
+
+void gsplit_worker(GSplit& gs, skv_ctx* ctx, uint64_t g, uint64_t G, const Job& job, const std::vector<uint64_t>& bnd,
+                   uint8_t* h_out, uint64_t out_cap) {
+    const uint32_t k = (uint32_t)job.ranked.size();
+    const uint64_t nr = job.run_ptr.size(), P = gs.P;
+    std::vector<uint64_t> parts;
+    for (uint64_t p = g; p < P; p += G) parts.push_back(p);
+    if (parts.empty()) return;
+    const uint64_t np = parts.size();
+    auto run_b = [&](uint64_t m) { return (const uint8_t*)(uintptr_t)job.run_ptr[m]; };
+    struct KernelIO {  // as in compact_host_pipelined_general: no DMA uploads behind the bulk copies
+        skv_ctx* c;
+        explicit KernelIO(skv_ctx* x) : c(x) {
+            c->kernel_uploads = true;
+            c->defer_free = true;
+        }
+        ~KernelIO() {
+            c->kernel_uploads = false;
+            c->defer_free = false;
+            if (c->in_stream) (void)hipStreamSynchronize(c->in_stream);
+            if (c->out_stream) (void)hipStreamSynchronize(c->out_stream);
+            (void)hipStreamSynchronize(c->stream);
+            for (void* q : c->graveyard) (void)hipFree(q);
+            for (void* q : c->host_graveyard) (void)hipHostFree(q);
+            c->graveyard.clear();
+            c->host_graveyard.clear();
+        }
+    } kio(ctx);
+    if (!ctx->in_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->in_stream, hipStreamNonBlocking));
+    if (!ctx->out_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->out_stream, hipStreamNonBlocking));
+    while (ctx->part_ev.size() < np) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->part_ev.push_back(e);
+    }
+    // device images of the runs (congruent mod 16 with their host bytes); only this ctx's slices land
+    std::vector<uint64_t> img(nr + 1, 0);
+    for (uint64_t m = 0; m < nr; ++m) img[m + 1] = img[m] + ((job.run_len[m] + 31) & ~15ull);
+    uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", img[nr] + 16);
+    for (uint64_t m = 0; m < nr; ++m) img[m] += ((uint64_t)(uintptr_t)run_b(m) & 15);
+    uint8_t* d_out = dbuf<uint8_t>(ctx, "gs_out", out_cap);
+    for (uint64_t i = 0; i < np; ++i) {
+        const uint64_t p = parts[i];
+        for (uint64_t m = 0; m < nr; ++m) {
+            // the byte before a slice stands in for its version byte: copied along (it is in the run)
+            const uint64_t lo = bnd[p * nr + m] - 1, hi = bnd[(p + 1) * nr + m];
+            if (hi > lo + 1)
+                HIPCHK(hipMemcpyAsync(d_in + img[m] + lo, run_b(m) + lo, hi - lo, hipMemcpyHostToDevice, ctx->in_stream));
+        }
+        HIPCHK(hipEventRecord(ctx->part_ev[i], ctx->in_stream));
+    }
+    uint64_t dev_off = 0;
+    std::vector<const uint8_t*> ptrs;
+    std::vector<uint64_t> lens;
+    std::vector<skv_stream> sv;
+    for (uint64_t i = 0; i < np; ++i) {
+        const uint64_t p = parts[i];
+        ptrs.clear();
+        lens.clear();
+        sv.clear();
+        std::vector<std::pair<int64_t, uint64_t>> sfirst;
+        for (uint32_t s = 0; s < k; ++s) {
+            const InStream& S = job.ranked[s];
+            const uint64_t f0 = ptrs.size();
+            for (uint64_t m = S.first; m < S.first + S.n_runs; ++m) {
+                const uint64_t lo = bnd[p * nr + m], hi = bnd[(p + 1) * nr + m];
+                if (hi <= lo) continue;
+                ptrs.push_back(d_in + img[m] + lo - 1);
+                lens.push_back(1 + hi - lo);
+            }
+            if (ptrs.size() > f0) sfirst.emplace_back(S.seq, f0);
+        }
+        if (sfirst.empty()) {  // no records in this key range: the carried run passes through
+            uint64_t c = 0;
+            if (!gs.wait_in(p, c)) return;
+            gs.post_out(p, c, false);
+            gs.in_recs[p] = 0;
+            gs.post_bytes(p, 0);
+            continue;
+        }
+        for (size_t q = 0; q < sfirst.size(); ++q) {
+            const uint64_t a = sfirst[q].second, z = q + 1 < sfirst.size() ? sfirst[q + 1].second : ptrs.size();
+            sv.push_back(skv_stream{&ptrs[a], &lens[a], (uint32_t)(z - a), sfirst[q].first});
+        }
+        Job pj;
+        if (build_job(ctx, sv.data(), (uint32_t)sv.size(), job.max_run_size, job.flags, pj) != SKV_OK)
+            throw DevError("internal: split part job: " + ctx->err);
+        pj.part = true;
+        pj.dev_out = d_out + dev_off;
+        pj.carry = &gs;
+        pj.carry_part = p;
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->part_ev[i], 0));
+        skv_result* pres = nullptr;
+        int rc;
+        try {
+            rc = compact_device(ctx, pj, &pres, true);
+        } catch (const ApiError&) {
+            rc = -1;  // a data error: the serial path reports it exactly
+        }
+        if (rc != SKV_OK) {
+            if (pres) skv_result_free(pres);
+            gs.halt(true, "");
+            return;
+        }
+        {  // a part that never reached the split (no runs): the carried run passes through
+            bool posted;
+            {
+                std::lock_guard<std::mutex> lk(gs.mu);
+                posted = gs.have_c[p + 1] != 0;
+            }
+            uint64_t c = 0;
+            if (!posted) {
+                if (!gs.wait_in(p, c)) {
+                    skv_result_free(pres);
+                    return;
+                }
+                gs.post_out(p, c, false);
+            }
+        }
+        bool is_cont;
+        {
+            std::lock_guard<std::mutex> lk(gs.mu);
+            is_cont = gs.cont[p] != 0;
+        }
+        const uint64_t skip = is_cont ? 1 : 0;  // the continuation's version byte stays behind
+        const uint64_t n = pres->n_runs, nb = pres->n_bytes;
+        if (is_cont && (n == 0 || pres->runs[0].off != 0)) {
+            skv_result_free(pres);
+            throw DevError("internal: split part " + std::to_string(p) + " lost its continuation run");
+        }
+        gs.in_recs[p] = pres->in_records;
+        gs.post_bytes(p, nb - skip);
+        uint64_t O = 0;
+        if (!gs.wait_off(p, O)) {
+            skv_result_free(pres);
+            return;
+        }
+        if (O + (nb - skip) > out_cap) {
+            skv_result_free(pres);
+            throw DevError("internal: split output past its buffer");
+        }
+        if (nb > skip)
+            HIPCHK(hipMemcpyAsync(h_out + O, (const uint8_t*)pres->bytes + skip, nb - skip, hipMemcpyDeviceToHost,
+                                  ctx->out_stream));
+        std::vector<skv_run_desc> ds(pres->runs, pres->runs + n);
+        for (skv_run_desc& d : ds) {  // part-relative -> global (the dropped byte before them all)
+            d.off = d.off + O - skip;
+            d.min_key_off = d.min_key_off + O - skip;
+            d.max_key_off = d.max_key_off + O - skip;
+        }
+        {
+            std::lock_guard<std::mutex> lk(gs.mu);
+            gs.descs[p] = std::move(ds);
+        }
+        skv_result_free(pres);
+        dev_off += (nb + 255) & ~255ull;
+    }
+    HIPCHK(hipStreamSynchronize(ctx->out_stream));
+}
+}  // namespace
+
+int compact_split_general(skv_ctx* const* ctxs, uint32_t G, Job& job, skv_result** out, double t_entry, bool& used) {
+    used = false;
+    skv_ctx* home = ctxs[0];
+    const uint32_t k = (uint32_t)job.ranked.size();
+    const uint64_t nr = job.run_ptr.size();
+    if ((job.flags & SKV_SPLIT_BY_TABLE) || job.batch || job.search || job.scan || k == 0 || nr == 0) return SKV_OK;
+    if (nr > (1u << 16)) return SKV_OK;  // the cut walk of every run would cost what the copies do
+    for (uint64_t m = 0; m < nr; ++m)  // a run without a version byte: skv_compact's error
+        if (job.run_len[m] == 0 || ((const uint8_t*)(uintptr_t)job.run_ptr[m])[0] != 1) return SKV_OK;
+    uint64_t Pg = std::max<uint64_t>(1, std::min<uint64_t>(16, job.in_bytes / G / (1ull << 30)));
+    if (const char* e = getenv("SKV_SPLIT_PARTS")) Pg = std::max<uint64_t>(1, std::min<uint64_t>(64, strtoull(e, nullptr, 10)));
+    uint64_t P = (uint64_t)G * Pg;
+    std::vector<std::string> cut;
+    if (!sample_cuts(job, false, P, cut)) return SKV_OK;
+    P = cut.size() + 1;
+    if (P < 2) return SKV_OK;
+    std::vector<uint64_t> bnd;
+    if (!cut_runs(job, cut, P, bnd) || !members_ascend(job)) return SKV_OK;
+    used = true;
+    GSplit gs;
+    gs.P = P;
+    gs.carry.assign(P + 1, 0);
+    gs.have_c.assign(P + 1, 0);
+    gs.have_c[0] = 1;  // the first part starts a fresh run
+    gs.cont.assign(P, 0);
+    gs.nbytes.assign(P, 0);
+    gs.have_b.assign(P, 0);
+    gs.off.assign(P + 1, 0);
+    gs.descs.assign(P, {});
+    gs.in_recs.assign(P, 0);
+    const uint64_t out_cap = job.in_bytes + job.in_bytes / 5 + 64;  // records >= 5 bytes: version bytes <= R
+    size_t cap = 0;
+    uint8_t* h_out = (uint8_t*)home->out_pool->take(out_cap, cap);
+    if (!h_out) throw DevError("pinned host allocation of the output failed");
+    std::vector<std::thread> th;
+    for (uint32_t g = 0; g < G; ++g)
+        th.emplace_back([&, g] {
+            skv_ctx* c = ctxs[g];
+            DeviceScope ds(c->device);
+            try {
+                if (!ds.ok) throw DevError("hipSetDevice failed");
+                gsplit_worker(gs, c, g, G, job, bnd, h_out, out_cap);
+            } catch (const DevError& e) {
+                if (e.msg != "split stopped") gs.halt(false, e.msg);
+            } catch (const std::exception& e) {
+                gs.halt(false, std::string("host error: ") + e.what());
+            }
+            drain(c);  // nothing of this call still runs on the ctx (nor writes h_out)
+        });
+    for (std::thread& t : th) t.join();
+    if (gs.stop) {
+        home->out_pool->give(h_out, cap);
+        if (!gs.err.empty()) throw DevError("split: " + gs.err);
+        used = false;  // a data error in some part: skv_compact reports it exactly
+        return SKV_OK;
+    }
+    // the runs in order; a continuation run 0 extends the run before it
+    std::vector<skv_run_desc> all;
+    uint64_t in_records = 0, out_records = 0;
+    for (uint64_t p = 0; p < P; ++p) {
+        in_records += gs.in_recs[p];
+        for (size_t r = 0; r < gs.descs[p].size(); ++r) {
+            const skv_run_desc& d = gs.descs[p][r];
+            out_records += d.put_count + d.delete_count;
+            if (r == 0 && gs.cont[p]) {
+                if (all.empty()) {
+                    home->out_pool->give(h_out, cap);
+                    throw DevError("internal: a continuation with no run before it");
+                }
+                skv_run_desc& b = all.back();
+                b.len += d.len - 1;
+                b.put_count += d.put_count;
+                b.delete_count += d.delete_count;
+                b.max_key_off = d.max_key_off;
+                b.max_key_len = d.max_key_len;
+            } else {
+                all.push_back(d);
+            }
+        }
+    }
+    ResultBox* box = new ResultBox();
+    skv_result* res = &box->pub;
+    res->runs = (skv_run_desc*)malloc(std::max<size_t>(1, all.size()) * sizeof(skv_run_desc));
+    if (!all.empty()) memcpy(res->runs, all.data(), all.size() * sizeof(skv_run_desc));
+    res->n_runs = all.size();
+    res->bytes = h_out;
+    res->n_bytes = gs.off[P];
+    res->in_bytes = job.in_bytes;
+    res->in_records = in_records;
+    res->out_records = out_records;
+    res->dropped_tables = 0;
+    box->pool = home->out_pool;
+    box->pool_cap = cap;
+    skv_timings& t = home->timings;
+    t = skv_timings{};
+    t.path = SKV_PATH_GENERAL;
+    t.host_total_ms = now_ms() - t_entry;
+    t.host_parts = (uint32_t)P;
     *out = res;
     return SKV_OK;
 }

@@ -2886,6 +2886,59 @@ void launch_chain(hipStream_t s, const uint64_t* Kp, const uint64_t* P, uint64_t
     k_chain<<<1, 64, 0, s>>>(Kp, P, max_size, tile_max, n_tiles, run_b, n_runs, tbl, n_tbl, plan);
 }
 uint64_t chain_table_entries(uint64_t max_bytes) { return (max_bytes >> CH_SHIFT) + 2; }
+// ---- carried open runs (skv_compact_split, variable-length records) -------------------------
+// build_runs (runs.rs:211-238) closes the current run before a record that would take it past max;
+// a run carried in with c bytes (version byte included) keeps taking this part's records while
+// c + their bytes <= max. One lane: a binary search of P.
+__global__ void k_carry_first(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ P, uint64_t max_size,
+                              uint64_t c, uint64_t* out) {
+    if (threadIdx.x) return;
+    const uint64_t K = *Kp;
+    uint64_t e = 0;
+    if (c < max_size) {
+        const uint64_t v = P[0] + (max_size - c);  // record j joins iff P[j + 1] <= v
+        uint64_t lo = 0, hi = K;                   // largest e in [0, K] with P[e] <= v
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi + 1) >> 1;
+            if (P[mid] <= v) lo = mid;
+            else hi = mid - 1;
+        }
+        e = lo;
+    }
+    out[0] = e;
+    out[1] = K - e;
+}
+__global__ void __launch_bounds__(1024) k_carry_fix(uint64_t* run_b, uint64_t* n_runs_out, const uint64_t* __restrict__ P,
+                                                    uint64_t e1, uint64_t K) {
+    const uint64_t m = n_runs_out[0];  // runs of the suffix; run_b[1 .. m + 1] its starts and end
+    __syncthreads();
+    for (uint64_t i = 1 + threadIdx.x; i <= m + 1; i += blockDim.x) run_b[i] += e1;
+    if (threadIdx.x == 0) {
+        run_b[0] = 0;
+        n_runs_out[0] = m + 1;
+        n_runs_out[1] = K;
+        n_runs_out[2] = P[K];  // (an empty suffix left 0 here)
+    }
+}
+__global__ void k_carry_out(const uint64_t* __restrict__ run_b, const uint64_t* __restrict__ n_runs_out,
+                            const uint64_t* __restrict__ P, uint64_t c, uint32_t cont, uint64_t* out) {
+    if (threadIdx.x) return;
+    const uint64_t n = n_runs_out[0], K = n_runs_out[1];
+    if (n == 0) *out = c;  // no records: the carried run stays open as it came
+    else if (cont && n == 1) *out = c + (P[K] - P[0]);
+    else *out = 1 + (P[K] - P[run_b[n - 1]]);
+}
+void launch_carry_first(hipStream_t s, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, uint64_t c,
+                        uint64_t* out) {
+    k_carry_first<<<1, 64, 0, s>>>(Kp, P, max_size, c, out);
+}
+void launch_carry_fix(hipStream_t s, uint64_t* run_b, uint64_t* n_runs_out, const uint64_t* P, uint64_t e1, uint64_t K) {
+    k_carry_fix<<<1, 1024, 0, s>>>(run_b, n_runs_out, P, e1, K);
+}
+void launch_carry_out(hipStream_t s, const uint64_t* run_b, const uint64_t* n_runs_out, const uint64_t* P, uint64_t c,
+                      uint32_t cont, uint64_t* out) {
+    k_carry_out<<<1, 64, 0, s>>>(run_b, n_runs_out, P, c, cont, out);
+}
 void launch_run_stats(hipStream_t s, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
                       const uint64_t* Dp, const uint32_t* m_rec, const uint32_t* rec_klen, DevRunDesc* descs,
                       uint64_t* seg_r0, uint64_t max_runs) {

@@ -61,6 +61,16 @@ void launch_chain(hipStream_t, const uint64_t* Kp, const uint64_t* P, uint64_t m
                   uint64_t n_tiles, uint64_t* run_b, uint64_t* n_runs, uint32_t* tbl, uint64_t max_K,
                   uint64_t max_bytes, const SplitBufs* sp = nullptr);
 uint64_t chain_table_entries(uint64_t max_bytes);
+// A part of a compaction split over several GPUs (skv_compact_split) that continues the previous
+// part's open run of c bytes: out[0] = e1, the records [0, e1) that still join that run, out[1] = K - e1
+void launch_carry_first(hipStream_t, const uint64_t* Kp, const uint64_t* P, uint64_t max_size, uint64_t c,
+                        uint64_t* out);
+// the split of records [e1, K) (written at run_b + 1, relative to e1) turned into the part's split:
+// run 0 = the continuation [0, e1), the others shifted by e1
+void launch_carry_fix(hipStream_t, uint64_t* run_b, uint64_t* n_runs_out, const uint64_t* P, uint64_t e1, uint64_t K);
+// the open run the part leaves to the next one: its bytes (version byte included)
+void launch_carry_out(hipStream_t, const uint64_t* run_b, const uint64_t* n_runs_out, const uint64_t* P,
+                      uint64_t c, uint32_t cont, uint64_t* out);
 void launch_run_stats(hipStream_t, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
                       const uint64_t* Dp, const uint32_t* m_rec, const uint32_t* rec_klen, DevRunDesc* descs,
                       uint64_t* seg_r0, uint64_t max_runs);

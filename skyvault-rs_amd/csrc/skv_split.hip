@@ -248,9 +248,21 @@ int skv_compact_split(skv_ctx* const* ctxs, uint32_t n_ctx, const skv_stream* st
         if (const char* e = getenv("SKV_SPLIT_PARTS")) Pg = std::max<uint64_t>(1, std::min<uint64_t>(64, strtoull(e, nullptr, 10)));
         const uint64_t P = G * Pg;
         std::vector<uint64_t> lb;
-        // one D2H copy per output run a part touches: a split into tiny runs stays on one GPU
-        if (fx_host_shape(job, f, R) && R >= P * 64 &&
-            R / fx_run_records(max_run_size, f.S, R) <= (1u << 16) && fx_host_cuts(job, f, P, lb)) {
+        // the fused shape's arithmetic split; one D2H copy per output run a part touches, so a split
+        // into tiny runs takes the general split below
+        const bool fused = fx_host_shape(job, f, R) && R >= P * 64 &&
+                           R / fx_run_records(max_run_size, f.S, R) <= (1u << 16) && fx_host_cuts(job, f, P, lb);
+        if (!fused) {  // variable-length records: the split with build_runs' carry (skv_hostpipe.hip)
+            bool used = false;
+            try {
+                const int rc = compact_split_general(ctxs, n_ctx, job, out, t_entry, used);
+                if (used) return rc;
+            } catch (const DevError& e) {
+                return set_err(home, SKV_E_DEVICE, "%s", e.msg.c_str());
+            } catch (const std::exception& e) {
+                return set_err(home, SKV_E_DEVICE, "host error: %s", e.what());
+            }
+        } else {
             try {
                 const uint64_t n = fx_run_records(max_run_size, f.S, R), W = n * f.S + 1;
                 Split sp;

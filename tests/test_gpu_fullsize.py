@@ -292,6 +292,39 @@ def test_config3_host_entry_full_size(dev, torch, default_pipe_env):
         hr.free()
 
 
+def test_config3_split_full_size(torch, default_pipe_env):
+    """config 3's shape at 256 x 16 MiB (3.7 GiB) through skv_compact_split over 4 ctxs with 3 parts
+    each (SURVEY §8(e) for variable-length records: parallel merges, build_runs' split carried from
+    part to part). Flags 0 and the Delete filter; every byte and descriptor equal to the oracle's."""
+    from skv.api import compact_split
+    from skv.devgen import make_cfg3_on_device
+
+    device = torch.device("cuda", 0)
+    _progress("config 3 split: generating")
+    runs = make_cfg3_on_device(device, SEED + 7, 256, 16)
+    host = _pinned_copies(torch, runs)
+    del runs
+    torch.cuda.empty_cache()
+    streams = [(s + 1, [(h.data_ptr(), h.numel())]) for s, h in enumerate(host)]
+    arrs = [h.numpy() for h in host]
+    sa = _abi.stream_table(np.arange(1, 257), [a.ctypes.data for a in arrs], [a.size for a in arrs])
+    cs = [Compactor(0) for _ in range(4)]
+    os.environ["SKV_SPLIT_PARTS"] = "3"
+    try:
+        for flags in (0, _abi.SKV_DROP_TOMBSTONES):
+            hr = compact_split(cs, streams, MAX_RUN, flags, keep=True)
+            t = cs[0].timings()
+            assert t["host_parts"] >= 8 and t["path"] == _abi.PATH_GENERAL, t
+            _progress(f"config 3 split flags {flags}: {t['host_parts']} parts; oracle")
+            exp, descs, info = pyoracle.compact_np(sa, MAX_RUN, flags)
+            _check_host_result(hr, exp, descs, info, f"config 3 split flags {flags}")
+            hr.free()
+    finally:
+        os.environ.pop("SKV_SPLIT_PARTS", None)
+        for c in cs:
+            c.close()
+
+
 # ------------------------------------------------------------------------------------------
 # config 5: 10^6 WAL runs, oracle per group of whole tables
 

@@ -1,13 +1,18 @@
-"""One compaction split across several GPUs by key range (skv_compact_split, skv_split.hip; SURVEY
-§8(e)). On the one-GPU test box the G ctxs are G ctxs of device 0, one host thread each: the same
-code as G GPUs (key-range parts dealt round-robin over the ctxs; each part staged, merged and
-deduplicated on its ctx and stream; only the parts' survivor counts cross between ctxs; each part's
-survivors copied D2H to their global places once every earlier part's count is in). Outputs must be
-the oracle's, byte for byte, for any G, any parts per ctx, any max_run_size (run boundaries fall
-inside parts and at part edges), equal keys across streams, streams absent from some parts, and
-member-run (L0) streams. Calls outside the split's shape (variable-length records) and calls a part
-poisons (a key decrease) must end with the oracle's outcome through skv_compact on ctxs[0].
-`timings()["host_parts"]` on ctxs[0] says whether the call was split (G x parts per ctx) or not.
+"""One compaction split across several GPUs by key range (skv_compact_split, skv_split.hip and
+skv_hostpipe.hip). On the one-GPU test box the G ctxs are G ctxs of device 0, one host
+thread each: the same code as G GPUs (key-range parts dealt round-robin over the ctxs; each part
+staged, merged and deduplicated on its ctx and stream; each part's bytes copied D2H to their global
+place once every earlier part's output size is known). Two splits:
+  - one record size, keys <= 16 B (the fused path): build_runs' split is arithmetic in the global
+    survivor index, so only the parts' survivor counts cross between ctxs;
+  - anything else (variable-length records, Deletes, the Delete filter): each part's split continues
+    the open run the previous part left (Job::carry), a continuation's descriptor merged into the
+    run before it.
+Outputs must be the oracle's, byte for byte, for any G, any parts per ctx, any max_run_size (runs
+of one record, runs over max, run boundaries inside parts and at part edges), equal keys across
+streams, streams absent from parts, parts of only tombstones, member-run (L0) streams. Calls a part
+finds a data error in (a key decrease, a truncated run) must end with the oracle's outcome through
+skv_compact on ctxs[0]. `timings()` on ctxs[0] says which split ran (`host_parts`, `path`).
 """
 import os
 import random
@@ -62,16 +67,21 @@ def _both(cs, streams, max_size, flags=0):
     return exp, got
 
 
-def _check(cs, streams, max_size, flags=0, split=True, parts=1):
+def _check(cs, streams, max_size, flags=0, split=True, parts=1, general=False):
+    """split: the fused split (exactly G x parts parts); general: the split with the carried open
+    run (parts from sampled cut keys: at least 2); neither: skv_compact on ctxs[0]"""
     os.environ["SKV_SPLIT_PARTS"] = str(parts)
     try:
         exp, got = _both(cs, streams, max_size, flags)
     finally:
         os.environ.pop("SKV_SPLIT_PARTS", None)
     assert exp == got, _diff(exp, got)
-    hp = cs[0].timings()["host_parts"]
-    if split:
-        assert hp == len(cs) * parts, f"not split (host_parts={hp})"
+    t = cs[0].timings()
+    hp = t["host_parts"]
+    if general:
+        assert hp >= 2 and t["path"] == _abi.PATH_GENERAL, f"not the general split ({t})"
+    elif split:
+        assert hp == len(cs) * parts and t["path"] == _abi.PATH_FUSED, f"not split ({t})"
     else:
         assert hp != len(cs) * parts
 
@@ -131,13 +141,13 @@ def test_config2_shape_against_one_gpu(ctxs):
     _check(ctxs[:8], streams, 4 * MiB, parts=3)
 
 
-def test_variable_records_take_one_ctx(ctxs):
-    """records of two sizes: outside the split's shape, the call runs as skv_compact on ctxs[0]"""
+def test_mixed_record_sizes_take_the_general_split(ctxs):
+    """records of several sizes: outside the fused shape, the split with the carried open run"""
     rng = random.Random(3)
     streams = _streams(rng, 4, 2000, 6000)
     ops = [fmt.put(f"k{i:011d}", b"v" * (1 + i % 7)) for i in sorted(rng.sample(range(6000), 1500))]
     streams.append((9, [fmt.encode_run(ops)]))
-    _check(ctxs[:4], streams, 3000, split=False)
+    _check(ctxs[:4], streams, 3000, general=True)
 
 
 def test_poisoned_shard_takes_one_ctx(ctxs):
@@ -189,7 +199,69 @@ def test_result_kept_and_freed(ctxs):
         res.free()
 
 
-def test_tiny_call_takes_one_ctx(ctxs):
-    """fewer records than the parts need (64 per part): skv_compact on ctxs[0]"""
+def test_tiny_call(ctxs):
+    """fewer records than the fused split's parts need (64 per part): the general split"""
     rng = random.Random(41)
-    _check(ctxs[:4], _streams(rng, 2, 50, 400), 2000, split=False)
+    _check(ctxs[:4], _streams(rng, 2, 50, 400), 2000, general=True)
+
+
+# ---- variable-length records: build_runs' split carried from part to part ----------------------
+
+
+@pytest.mark.parametrize("G", [2, 3, 8])
+@pytest.mark.parametrize("max_size", [4096, 1000, 64 * 1024, 1 << 62])
+@pytest.mark.parametrize("flags", [0, _abi.SKV_DROP_TOMBSTONES], ids=["flags0", "drop"])
+def test_general_split_matches_oracle(ctxs, G, max_size, flags):
+    """config 3's shape (8-128 B keys, 10 % Deletes): runs continue across part edges"""
+    streams = gen.config3(seed=900 + G, n_streams=12, run_bytes=96 * 1024)
+    _check(ctxs[:G], streams, max_size, flags, general=True)
+
+
+@pytest.mark.parametrize("parts", [2, 5])
+def test_general_split_parts_per_ctx(ctxs, parts):
+    streams = gen.config3(seed=77, n_streams=8, run_bytes=128 * 1024)
+    _check(ctxs[:3], streams, 5000, 0, general=True, parts=parts)
+
+
+@pytest.mark.parametrize("max_size", [1, 200, 400])
+def test_general_split_runs_of_one_record(ctxs, max_size):
+    """max below most records: nearly every record its own run, carried runs already over max"""
+    streams = gen.config3(seed=31, n_streams=6, run_bytes=32 * 1024)
+    _check(ctxs[:4], streams, max_size, 0, general=True)
+
+
+def test_general_split_part_of_only_tombstones(ctxs):
+    """a key range holding only Deletes: with the filter, a part with no survivors passes the
+    carried run on unchanged"""
+    rng = random.Random(8)
+    streams = []
+    for s in range(4):
+        ids = sorted(rng.sample(range(40000), 3000))
+        ops = [fmt.delete(f"k{i:06d}") if 10000 <= i < 30000 else fmt.put(f"k{i:06d}", b"x" * (i % 50))
+               for i in ids]
+        streams.append((s + 1, [fmt.encode_run(ops)]))
+    _check(ctxs[:4], streams, 3000, _abi.SKV_DROP_TOMBSTONES, general=True, parts=3)
+
+
+def test_general_split_member_runs(ctxs):
+    """an L0 shape with variable records: a stream of many ascending member runs"""
+    rng = random.Random(12)
+    ids = sorted(rng.sample(range(300000), 30000))
+    members = [fmt.encode_run([fmt.put(f"key{i:07d}", b"v" * (i % 97)) for i in ids[j:j + 1500]])
+               for j in range(0, len(ids), 1500)]
+    streams = [(0, members)] + [
+        (s + 1, [fmt.encode_run([fmt.put(f"key{i:07d}", b"w" * (i % 31)) for i in sorted(rng.sample(range(300000), 4000))])])
+        for s in range(3)]
+    _check(ctxs[:4], streams, 8000, general=True)
+
+
+def test_general_split_unsorted_stream(ctxs):
+    """a key decrease inside a part: the part's decode check stops the split, skv_compact on
+    ctxs[0] gives the oracle's outcome"""
+    streams = gen.config3(seed=5, n_streams=6, run_bytes=48 * 1024)
+    rng = random.Random(6)
+    ids = sorted(rng.sample(range(100000), 2000))
+    ops = [fmt.put(f"key{i:07d}", b"z" * (i % 40)) for i in ids]
+    ops[900], ops[901] = ops[901], ops[900]
+    streams[2] = (streams[2][0], [fmt.encode_run(ops)])
+    _check(ctxs[:4], streams, 4096, split=False)
