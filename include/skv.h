@@ -190,8 +190,9 @@ int skv_compact_dev(skv_ctx* ctx, const skv_stream* streams, uint32_t n_streams,
  * keys never straddle a cut) are staged, merged and deduplicated on the ctxs in parallel;
  * build_runs' greedy split (runs.rs:211-238) is carried across the parts: arithmetically from the
  * parts' survivor counts for one record size with keys of at most 16 bytes, else by each part's
- * split continuing the open run the previous part left. WAL flushes (SKV_SPLIT_BY_TABLE), calls of
- * more than 2^16 member runs, and any call a part finds a data error in run as skv_compact on
+ * split continuing the open run the previous part left; a WAL flush (SKV_SPLIT_BY_TABLE) is cut at
+ * table prefixes, so its parts carry nothing. Calls of more than 2^16 member runs, a WAL flush that
+ * needs the exact WAL stage, and any call a part finds a data error in run as skv_compact on
  * ctxs[0], which reports the reference's outcome. Errors are reported on ctxs[0]. The ctxs must
  * not be used by other threads during the call. n_ctx == 1 is skv_compact.
  */

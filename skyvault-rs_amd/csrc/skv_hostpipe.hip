@@ -1245,7 +1245,8 @@ struct GSplit : CarryHook {
     bool stop = false, data_err = false;
     std::string err;
     std::vector<std::vector<skv_run_desc>> descs;  // part p's runs, offsets already global
-    std::vector<uint64_t> in_recs;
+    std::vector<uint64_t> in_recs, dropped;
+    bool wal = false;  // WAL flush: parts hold whole tables, nothing is carried
 
     bool wait_in(uint64_t part, uint64_t& c) override {
         std::unique_lock<std::mutex> g(mu);
@@ -1366,8 +1367,10 @@ void gsplit_worker(GSplit& gs, skv_ctx* ctx, uint64_t g, uint64_t G, const Job& 
         }
         if (sfirst.empty()) {  // no records in this key range: the carried run passes through
             uint64_t c = 0;
-            if (!gs.wait_in(p, c)) return;
-            gs.post_out(p, c, false);
+            if (!gs.wal) {
+                if (!gs.wait_in(p, c)) return;
+                gs.post_out(p, c, false);
+            }
             gs.in_recs[p] = 0;
             gs.post_bytes(p, 0);
             continue;
@@ -1381,7 +1384,7 @@ void gsplit_worker(GSplit& gs, skv_ctx* ctx, uint64_t g, uint64_t G, const Job& 
             throw DevError("internal: split part job: " + ctx->err);
         pj.part = true;
         pj.dev_out = d_out + dev_off;
-        pj.carry = &gs;
+        pj.carry = gs.wal ? nullptr : &gs;
         pj.carry_part = p;
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->part_ev[i], 0));
         skv_result* pres = nullptr;
@@ -1396,7 +1399,7 @@ void gsplit_worker(GSplit& gs, skv_ctx* ctx, uint64_t g, uint64_t G, const Job& 
             gs.halt(true, "");
             return;
         }
-        {  // a part that never reached the split (no runs): the carried run passes through
+        if (!gs.wal) {  // a part that never reached the split (no runs): the carried run passes through
             bool posted;
             {
                 std::lock_guard<std::mutex> lk(gs.mu);
@@ -1423,6 +1426,7 @@ void gsplit_worker(GSplit& gs, skv_ctx* ctx, uint64_t g, uint64_t G, const Job& 
             throw DevError("internal: split part " + std::to_string(p) + " lost its continuation run");
         }
         gs.in_recs[p] = pres->in_records;
+        gs.dropped[p] = pres->dropped_tables;
         gs.post_bytes(p, nb - skip);
         uint64_t O = 0;
         if (!gs.wait_off(p, O)) {
@@ -1458,7 +1462,8 @@ int compact_split_general(skv_ctx* const* ctxs, uint32_t G, Job& job, skv_result
     skv_ctx* home = ctxs[0];
     const uint32_t k = (uint32_t)job.ranked.size();
     const uint64_t nr = job.run_ptr.size();
-    if ((job.flags & SKV_SPLIT_BY_TABLE) || job.batch || job.search || job.scan || k == 0 || nr == 0) return SKV_OK;
+    const bool wal = (job.flags & SKV_SPLIT_BY_TABLE) != 0;
+    if (job.batch || job.search || job.scan || k == 0 || nr == 0) return SKV_OK;
     if (nr > (1u << 16)) return SKV_OK;  // the cut walk of every run would cost what the copies do
     for (uint64_t m = 0; m < nr; ++m)  // a run without a version byte: skv_compact's error
         if (job.run_len[m] == 0 || ((const uint8_t*)(uintptr_t)job.run_ptr[m])[0] != 1) return SKV_OK;
@@ -1466,7 +1471,7 @@ int compact_split_general(skv_ctx* const* ctxs, uint32_t G, Job& job, skv_result
     if (const char* e = getenv("SKV_SPLIT_PARTS")) Pg = std::max<uint64_t>(1, std::min<uint64_t>(64, strtoull(e, nullptr, 10)));
     uint64_t P = (uint64_t)G * Pg;
     std::vector<std::string> cut;
-    if (!sample_cuts(job, false, P, cut)) return SKV_OK;
+    if (!sample_cuts(job, wal, P, cut)) return SKV_OK;  // (WAL flushes: cuts at table prefixes)
     P = cut.size() + 1;
     if (P < 2) return SKV_OK;
     std::vector<uint64_t> bnd;
@@ -1483,6 +1488,8 @@ int compact_split_general(skv_ctx* const* ctxs, uint32_t G, Job& job, skv_result
     gs.off.assign(P + 1, 0);
     gs.descs.assign(P, {});
     gs.in_recs.assign(P, 0);
+    gs.dropped.assign(P, 0);
+    gs.wal = wal;
     const uint64_t out_cap = job.in_bytes + job.in_bytes / 5 + 64;  // records >= 5 bytes: version bytes <= R
     size_t cap = 0;
     uint8_t* h_out = (uint8_t*)home->out_pool->take(out_cap, cap);
@@ -1511,9 +1518,10 @@ int compact_split_general(skv_ctx* const* ctxs, uint32_t G, Job& job, skv_result
     }
     // the runs in order; a continuation run 0 extends the run before it
     std::vector<skv_run_desc> all;
-    uint64_t in_records = 0, out_records = 0;
+    uint64_t in_records = 0, out_records = 0, dropped = 0;
     for (uint64_t p = 0; p < P; ++p) {
         in_records += gs.in_recs[p];
+        dropped += gs.dropped[p];
         for (size_t r = 0; r < gs.descs[p].size(); ++r) {
             const skv_run_desc& d = gs.descs[p][r];
             out_records += d.put_count + d.delete_count;
@@ -1543,7 +1551,7 @@ int compact_split_general(skv_ctx* const* ctxs, uint32_t G, Job& job, skv_result
     res->in_bytes = job.in_bytes;
     res->in_records = in_records;
     res->out_records = out_records;
-    res->dropped_tables = 0;
+    res->dropped_tables = dropped;
     box->pool = home->out_pool;
     box->pool_cap = cap;
     skv_timings& t = home->timings;
@@ -1551,6 +1559,7 @@ int compact_split_general(skv_ctx* const* ctxs, uint32_t G, Job& job, skv_result
     t.path = SKV_PATH_GENERAL;
     t.host_total_ms = now_ms() - t_entry;
     t.host_parts = (uint32_t)P;
+    t.wal_stage = wal ? 1 : 0;
     *out = res;
     return SKV_OK;
 }

@@ -351,11 +351,11 @@ class Compactor:
 
 
 def compact_split(compactors: Sequence["Compactor"], streams, max_run_size: int = MAX_RUN_SIZE, flags: int = 0,
-                  keep: bool = False):
+                  keep: bool = False, with_info: bool = False):
     """skv_compact_split: one compaction spread over the Compactors' GPUs by key range (the first
     one owns the result and reports errors). streams: [(seq_no, [run_bytes, ...])] (host memory),
-    [(seq_no, [(host_ptr, length)])] or a StreamArgs built with device=True. Returns [OutRun], or,
-    keep=True, the HostResult."""
+    [(seq_no, [(host_ptr, length)])] or a StreamArgs built with device=True. Returns [OutRun] (with
+    with_info, ([OutRun], info) as Compactor.compact), or, keep=True, the HostResult."""
     if not compactors:
         raise ValueError("compact_split needs at least one Compactor")
     home = compactors[0]
@@ -373,9 +373,13 @@ def compact_split(compactors: Sequence["Compactor"], streams, max_run_size: int 
     if keep:
         return HostResult(home.lib, res, home)
     try:
-        return result_to_runs(res.contents)
+        runs = result_to_runs(res.contents)
+        info = dict(in_bytes=res.contents.in_bytes, in_records=res.contents.in_records,
+                    out_records=res.contents.out_records, dropped_tables=res.contents.dropped_tables,
+                    n_bytes=res.contents.n_bytes)
     finally:
         home.lib.skv_result_free(res)
+    return (runs, info) if with_info else runs
 
 
 class RunIndex:

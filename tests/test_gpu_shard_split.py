@@ -61,7 +61,8 @@ def _both(cs, streams, max_size, flags=0):
     except _abi.RunError as e:
         exp = ("err", e.code, e.message)
     try:
-        got = ("ok", _norm(compact_split(cs, streams, max_size, flags)), 0)
+        runs, info = compact_split(cs, streams, max_size, flags, with_info=True)
+        got = ("ok", _norm(runs), info["dropped_tables"])
     except _abi.RunError as e:
         got = ("err", e.code, e.message)
     return exp, got
@@ -265,3 +266,14 @@ def test_general_split_unsorted_stream(ctxs):
     ops[900], ops[901] = ops[901], ops[900]
     streams[2] = (streams[2][0], [fmt.encode_run(ops)])
     _check(ctxs[:4], streams, 4096, split=False)
+
+
+@pytest.mark.parametrize("G", [2, 4])
+@pytest.mark.parametrize("max_size", [1 << 62, 16 * 1024])
+def test_wal_flush_split(ctxs, G, max_size):
+    """a WAL flush (SKV_SPLIT_BY_TABLE, 3,000 runs over 64 tables): parts cut at table prefixes hold
+    whole tables, so nothing is carried. At 16 KiB every table breaks the one-run rule: the exact WAL
+    stage, which a part does not run, so the call is skv_compact's (dropped_tables compared too)"""
+    streams = [(s + 1, [gen.wal_run(700 + s).tobytes()]) for s in range(3000)]
+    one_run = max_size == 1 << 62
+    _check(ctxs[:G], streams, max_size, _abi.SKV_SPLIT_BY_TABLE, split=False, general=one_run)
