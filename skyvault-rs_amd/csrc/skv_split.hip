@@ -20,9 +20,11 @@
 // round r + 1 on every GPU. The host writes the version bytes and the descriptors (StatsV1,
 // runs.rs:102-109) arithmetically, as k_fx_desc does.
 //
-// A call outside the fused shape, a cut that a run decreases across, or a poisoned part (a record
-// the fused path does not take, a key decrease) runs as skv_compact on ctxs[0], which gives the
-// reference's exact outcome. A HIP failure on any ctx is SKV_E_DEVICE on ctxs[0].
+// A call outside the fused shape (variable-length records, Deletes, WAL flushes), or one whose
+// survivors would need more than 2^16 D2H copies, takes the split with build_runs' carry
+// (compact_split_general, skv_hostpipe.hip). A poisoned part (a record the fused path does not
+// take, a key decrease) runs the call as skv_compact on ctxs[0], which gives the reference's exact
+// outcome. A HIP failure on any ctx is SKV_E_DEVICE on ctxs[0].
 #include "skv_host.hpp"
 
 namespace {
