@@ -1328,19 +1328,35 @@ void gsplit_worker(GSplit& gs, skv_ctx* ctx, uint64_t g, uint64_t G, const Job& 
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ctx->part_ev.push_back(e);
     }
-    // device images of the runs (congruent mod 16 with their host bytes); only this ctx's slices land
-    std::vector<uint64_t> img(nr + 1, 0);
-    for (uint64_t m = 0; m < nr; ++m) img[m + 1] = img[m] + ((job.run_len[m] + 31) & ~15ull);
-    uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", img[nr] + 16);
-    for (uint64_t m = 0; m < nr; ++m) img[m] += ((uint64_t)(uintptr_t)run_b(m) & 15);
-    uint8_t* d_out = dbuf<uint8_t>(ctx, "gs_out", out_cap);
+    // this ctx's slices only: slice (i, m) = run m's bytes [lo - 1, hi) of part i (the byte before
+    // the slice stands in for its version byte), at d_in + soff[i * nr + m], congruent mod 16 with
+    // its host bytes; the output regions of its parts (a part writes at most its record bytes plus
+    // a version byte per record of >= 5 bytes)
+    std::vector<uint64_t> soff(np * nr, 0), ocap(np, 0);
+    uint64_t in_total = 0, out_total = 0;
+    for (uint64_t i = 0; i < np; ++i) {
+        const uint64_t p = parts[i];
+        uint64_t pb = 0;
+        for (uint64_t m = 0; m < nr; ++m) {
+            const uint64_t lo = bnd[p * nr + m] - 1, hi = bnd[(p + 1) * nr + m];
+            if (hi <= lo + 1) continue;
+            in_total = ((in_total + 15) & ~15ull) + (((uint64_t)(uintptr_t)run_b(m) + lo) & 15);
+            soff[i * nr + m] = in_total;
+            in_total += hi - lo;
+            pb += hi - lo - 1;
+        }
+        ocap[i] = (pb + pb / 5 + 64 + 255) & ~255ull;
+        out_total += ocap[i];
+    }
+    uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", in_total + 32);
+    uint8_t* d_out = dbuf<uint8_t>(ctx, "gs_out", out_total + 256);
     for (uint64_t i = 0; i < np; ++i) {
         const uint64_t p = parts[i];
         for (uint64_t m = 0; m < nr; ++m) {
-            // the byte before a slice stands in for its version byte: copied along (it is in the run)
             const uint64_t lo = bnd[p * nr + m] - 1, hi = bnd[(p + 1) * nr + m];
             if (hi > lo + 1)
-                HIPCHK(hipMemcpyAsync(d_in + img[m] + lo, run_b(m) + lo, hi - lo, hipMemcpyHostToDevice, ctx->in_stream));
+                HIPCHK(hipMemcpyAsync(d_in + soff[i * nr + m], run_b(m) + lo, hi - lo, hipMemcpyHostToDevice,
+                                      ctx->in_stream));
         }
         HIPCHK(hipEventRecord(ctx->part_ev[i], ctx->in_stream));
     }
@@ -1360,7 +1376,7 @@ void gsplit_worker(GSplit& gs, skv_ctx* ctx, uint64_t g, uint64_t G, const Job& 
             for (uint64_t m = S.first; m < S.first + S.n_runs; ++m) {
                 const uint64_t lo = bnd[p * nr + m], hi = bnd[(p + 1) * nr + m];
                 if (hi <= lo) continue;
-                ptrs.push_back(d_in + img[m] + lo - 1);
+                ptrs.push_back(d_in + soff[i * nr + m]);
                 lens.push_back(1 + hi - lo);
             }
             if (ptrs.size() > f0) sfirst.emplace_back(S.seq, f0);
@@ -1451,7 +1467,7 @@ void gsplit_worker(GSplit& gs, skv_ctx* ctx, uint64_t g, uint64_t G, const Job& 
             gs.descs[p] = std::move(ds);
         }
         skv_result_free(pres);
-        dev_off += (nb + 255) & ~255ull;
+        dev_off += ocap[i];
     }
     HIPCHK(hipStreamSynchronize(ctx->out_stream));
 }
