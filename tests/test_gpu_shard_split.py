@@ -277,3 +277,46 @@ def test_wal_flush_split(ctxs, G, max_size):
     streams = [(s + 1, [gen.wal_run(700 + s).tobytes()]) for s in range(3000)]
     one_run = max_size == 1 << 62
     _check(ctxs[:G], streams, max_size, _abi.SKV_SPLIT_BY_TABLE, split=False, general=one_run)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_split_random_shapes(ctxs, seed):
+    """random calls: G, parts per ctx, record sizes (fixed or variable, with or without Deletes),
+    fan-in, member runs, max_run_size and flags drawn per seed; either split, same bytes as the
+    oracle"""
+    rng = random.Random(10007 * seed + 3)
+    G = rng.choice([2, 3, 4, 5, 8])
+    parts = rng.choice([1, 1, 2, 3])
+    flags = rng.choice([0, 0, _abi.SKV_DROP_TOMBSTONES])
+    fixed = rng.random() < 0.4
+    vlen = rng.choice([0, 8, 40, 200])
+    space = rng.choice([2000, 20000, 200000])
+    streams = []
+    for s in range(rng.randint(1, 12)):
+        n = rng.randint(0, 3000)
+        ids = sorted(rng.sample(range(space), min(n, space)))
+        if not ids:
+            continue
+        n_members = rng.choice([1, 1, 1, 3])
+        cuts = sorted(rng.sample(range(1, len(ids)), min(n_members - 1, len(ids) - 1))) if len(ids) > 1 else []
+        bounds = [0] + cuts + [len(ids)]
+        members = []
+        for a, b in zip(bounds, bounds[1:]):
+            ops = []
+            for i in ids[a:b]:
+                key = f"k{i:09d}" if fixed else f"k{i:09d}" + "x" * (i % 13)  # (order-preserving)
+                if not fixed and rng.random() < 0.1:
+                    ops.append(fmt.delete(key))
+                else:
+                    ops.append(fmt.put(key, bytes([i & 0xFF]) * (vlen if fixed else (i * 7) % (vlen + 1))))
+            members.append(fmt.encode_run(ops))
+        streams.append((s + 1, members))
+    if not streams:
+        return
+    max_size = rng.choice([1, 100, 1000, 4096, 1 << 20, 1 << 62])
+    os.environ["SKV_SPLIT_PARTS"] = str(parts)
+    try:
+        exp, got = _both(ctxs[:G], streams, max_size, flags)
+    finally:
+        os.environ.pop("SKV_SPLIT_PARTS", None)
+    assert exp == got, _diff(exp, got)
