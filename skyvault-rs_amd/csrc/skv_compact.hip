@@ -1424,7 +1424,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     }
     if (!carry_e1)
         launch_chain(st, d_K, m_P, job.max_run_size, tile_max, T0, run_b, d_nruns, chain_tbl, R, in_rec_bytes, &sp);
-    if (job.carry) {  // the open run this part leaves: the next part's split can start
+    if (job.carry) {  // the open run this part leaves, staged (handed on once the part's result is final)
         uint64_t* d_co = dbuf<uint64_t>(ctx, "carry_out", 1);
         launch_carry_out(st, run_b, d_nruns, m_P, carry_c, carry_e1 ? 1u : 0u, d_co);
         uint64_t* hco = (uint64_t*)pinned(ctx, 16);

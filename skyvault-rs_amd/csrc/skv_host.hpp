@@ -255,8 +255,10 @@ int derr_to_api(uint32_t e, std::string& msg);
 // ------------------------------------------------------------------------------------------
 // A part of skv_compact_split's split of variable-length records (skv_hostpipe.hip): build_runs'
 // greedy split continues across parts, so each part's split starts from the open run the previous
-// part left (its bytes) and hands its own on. wait_in blocks until that is known (false: the call
-// has stopped); post_out may be called again with the same value (a part that reruns).
+// part left (its bytes) and posts its own. wait_in blocks until that is known (false: the call
+// has stopped); post_out only stages the value -- a part may rerun after its split (a deferred
+// verification that fails, a fingerprint collision) and post again -- and the split hands it on
+// once the part's result is final.
 struct CarryHook {
     virtual ~CarryHook() = default;
     virtual bool wait_in(uint64_t part, uint64_t& c) = 0;

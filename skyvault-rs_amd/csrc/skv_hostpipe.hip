@@ -1236,7 +1236,12 @@ struct GSplit : CarryHook {
     std::mutex mu;
     std::condition_variable cv;
     std::vector<uint64_t> carry;    // carry[p + 1]: the open run part p leaves (bytes; carry[0] = 0)
-    std::vector<uint8_t> have_c;    // carry[p] known
+    std::vector<uint8_t> have_c;    // carry[p] committed (the next part may split)
+    // what compact_device posts at its split (post_out) is only staged: a part can rerun after its
+    // split (a deferred verification that fails, a fingerprint collision) and post again; its
+    // worker commits the value once the part's result is final
+    std::vector<uint64_t> carry_st;
+    std::vector<uint8_t> staged;
     std::vector<uint8_t> cont;      // part p's run 0 continues the carried run
     std::vector<uint64_t> nbytes;   // part p's output bytes (after the dropped version byte)
     std::vector<uint8_t> have_b;
@@ -1256,11 +1261,16 @@ struct GSplit : CarryHook {
         return true;
     }
     void post_out(uint64_t part, uint64_t c, bool is_cont) override {
+        std::lock_guard<std::mutex> g(mu);
+        carry_st[part + 1] = c;
+        staged[part + 1] = 1;
+        cont[part] = is_cont ? 1 : 0;
+    }
+    void commit(uint64_t part) {
         {
             std::lock_guard<std::mutex> g(mu);
-            carry[part + 1] = c;
+            carry[part + 1] = carry_st[part + 1];
             have_c[part + 1] = 1;
-            cont[part] = is_cont ? 1 : 0;
         }
         cv.notify_all();
     }
@@ -1386,6 +1396,7 @@ void gsplit_worker(GSplit& gs, skv_ctx* ctx, uint64_t g, uint64_t G, const Job& 
             if (!gs.wal) {
                 if (!gs.wait_in(p, c)) return;
                 gs.post_out(p, c, false);
+                gs.commit(p);
             }
             gs.in_recs[p] = 0;
             gs.post_bytes(p, 0);
@@ -1415,20 +1426,21 @@ void gsplit_worker(GSplit& gs, skv_ctx* ctx, uint64_t g, uint64_t G, const Job& 
             gs.halt(true, "");
             return;
         }
-        if (!gs.wal) {  // a part that never reached the split (no runs): the carried run passes through
+        if (!gs.wal) {  // the part's result is final: its open run goes to the next part
             bool posted;
             {
                 std::lock_guard<std::mutex> lk(gs.mu);
-                posted = gs.have_c[p + 1] != 0;
+                posted = gs.staged[p + 1] != 0;
             }
             uint64_t c = 0;
-            if (!posted) {
+            if (!posted) {  // it never reached the split (no runs): the carried run passes through
                 if (!gs.wait_in(p, c)) {
                     skv_result_free(pres);
                     return;
                 }
                 gs.post_out(p, c, false);
             }
+            gs.commit(p);
         }
         bool is_cont;
         {
@@ -1498,6 +1510,8 @@ int compact_split_general(skv_ctx* const* ctxs, uint32_t G, Job& job, skv_result
     gs.carry.assign(P + 1, 0);
     gs.have_c.assign(P + 1, 0);
     gs.have_c[0] = 1;  // the first part starts a fresh run
+    gs.carry_st.assign(P + 1, 0);
+    gs.staged.assign(P + 1, 0);
     gs.cont.assign(P, 0);
     gs.nbytes.assign(P, 0);
     gs.have_b.assign(P, 0);
