@@ -35,9 +35,10 @@
 extern "C" {
 #endif
 
-#define SKV_ABI_VERSION 8  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts; 4: skv_scan_runs;
+#define SKV_ABI_VERSION 9  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts; 4: skv_scan_runs;
                               5: skv_timings.span_parse (was reserved); 6: skv_timings.wal_stage;
-                              7: skv_ctx_host_info; 8: skv_compact_split */
+                              7: skv_ctx_host_info; 8: skv_compact_split; 9: skv_host_plan,
+                              skv_split_deal */
 
 typedef struct skv_ctx skv_ctx;
 
@@ -166,6 +167,28 @@ int skv_ctx_get_timings(const skv_ctx* ctx, skv_timings* out);
  * device has its own pool, bound to the CPUs of that node, and a ctx's pinned staging and output
  * buffers are allocated on that node. */
 int skv_ctx_host_info(const skv_ctx* ctx, int* numa_node, int* host_threads);
+
+/*
+ * The placement plans behind the multi-GPU entry points, as pure functions (no HIP device needed:
+ * schedulers that place jobs across the GPUs of a node, and CPU tests, call them directly).
+ *
+ * skv_host_plan: the host side the library gives the GPU whose PCI bus id is `pci_bus_id`
+ * ("0000:c1:00.0"), read from `sysfs_root` ("/sys" on a live system; NULL = "/sys") on a machine of
+ * `n_devices` GPUs and `hw_threads` CPUs: its NUMA node (-1: unknown), the size of its host pool
+ * (the caller + pool_threads - 1 workers, SKV_HOST_THREADS capped at hw_threads / n_devices) and the
+ * node's CPUs the pool is bound to (at most max_cpus written). Returns the node's CPU count, or -1
+ * when the node is unknown. skv_ctx_host_info reports the same plan for a live ctx.
+ *
+ * skv_split_deal: how skv_compact_split deals its n_parts key-range parts over n_ctx ctxs whose
+ * devices are ctx_device[g]: ctx_of_part[p] = p % n_ctx (the ctx, hence the GPU, that merges part
+ * p); h2d_after[p] = the latest earlier part dealt to ANOTHER ctx of the same device, whose H2D copy
+ * must land first (ctxs sharing one PCIe link take their inputs in part order), or -1.
+ * (orchestrator_service.rs:119-170 places independent jobs; this places one job's parts.)
+ */
+int skv_host_plan(const char* sysfs_root, const char* pci_bus_id, int n_devices, int hw_threads, int* numa_node,
+                  int* pool_threads, int* cpus, int max_cpus);
+int skv_split_deal(const int* ctx_device, uint32_t n_ctx, uint64_t n_parts, uint32_t* ctx_of_part,
+                   int64_t* h2d_after);
 
 /*
  * Host-memory entry point: the shape skyvault's jobs have (Bytes in from get_run,

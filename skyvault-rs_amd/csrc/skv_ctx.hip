@@ -26,12 +26,27 @@ void lds_limit(const void* kernel) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> g(mu);
-    if (!done.insert({dev, kernel}).second) return;
-    // the ceiling is the CU's LDS less the kernel's static LDS (a larger value is refused)
+    if (done.count({dev, kernel})) return;
+    // the ceiling is the device's per-workgroup LDS opt-in limit (the CU's 160 KiB on gfx950) less
+    // the kernel's static LDS (a larger value is refused); recorded only once the device took it,
+    // so a refused or failed call is tried again by the next launch
+    int cap = 0;
+    if (hipDeviceGetAttribute(&cap, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess || cap <= 0) {
+        (void)hipGetLastError();
+        if (hipDeviceGetAttribute(&cap, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+    }
     hipFuncAttributes fa{};
     size_t stat = 0;
     if (hipFuncGetAttributes(&fa, kernel) == hipSuccess) stat = fa.sharedSizeBytes;
-    (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024 - stat));
+    else (void)hipGetLastError();
+    if ((size_t)cap <= stat) return;
+    if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)((size_t)cap - stat)) == hipSuccess)
+        done.insert({dev, kernel});
+    else
+        (void)hipGetLastError();
 }
 }  // namespace skv
 
@@ -166,6 +181,31 @@ struct DevHost {
     unsigned threads = 1;  // the caller + threads - 1 workers
     HostPool* pool = nullptr;
 };
+// The plan of one device's host side from sysfs (root "/sys" on a live system): its NUMA node (the PCI
+// device's numa_node), that node's CPUs, and the pool size for a machine of hw CPUs and ndev GPUs.
+struct HostPlan {
+    int numa = -1;
+    std::vector<int> cpus;
+    unsigned threads = 1;
+};
+HostPlan host_plan(const std::string& root, const char* bus_id, int ndev, unsigned hw) {
+    HostPlan p;
+    if (bus_id && *bus_id) {
+        std::string bus(bus_id);
+        for (char& c : bus) c = (char)tolower(c);
+        const std::string nn = read_text(root + "/bus/pci/devices/" + bus + "/numa_node");
+        try {
+            p.numa = nn.empty() ? -1 : std::stoi(nn);
+        } catch (...) {
+            p.numa = -1;
+        }
+        if (p.numa >= 0) p.cpus = parse_cpulist(read_text(root + "/devices/system/node/node" + std::to_string(p.numa) + "/cpulist"));
+    }
+    if (ndev < 1) ndev = 1;
+    hw = std::max(1u, hw);
+    p.threads = std::max(1u, std::min(host_threads_cap(), std::max(1u, hw / (unsigned)ndev)));
+    return p;
+}
 DevHost& dev_host(int device) {  // created on first use, never torn down (like the workers)
     static std::mutex mu;
     static std::map<int, DevHost*> hosts;
@@ -175,23 +215,16 @@ DevHost& dev_host(int device) {  // created on first use, never torn down (like 
     if (it != hosts.end()) return *it->second;
     DevHost* d = new DevHost();
     char bus[64] = {};
-    if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, device) == hipSuccess) {
-        for (char* c = bus; *c; ++c) *c = (char)tolower(*c);
-        const std::string nn = read_text(std::string("/sys/bus/pci/devices/") + bus + "/numa_node");
-        try {
-            d->numa = nn.empty() ? -1 : std::stoi(nn);
-        } catch (...) {
-            d->numa = -1;
-        }
-        if (d->numa >= 0)
-            d->cpus = parse_cpulist(read_text("/sys/devices/system/node/node" + std::to_string(d->numa) + "/cpulist"));
-    } else {
+    if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, device) != hipSuccess) {
         (void)hipGetLastError();
+        bus[0] = 0;
     }
     int ndev = 1;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) ndev = 1;
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    d->threads = std::max(1u, std::min(host_threads_cap(), std::max(1u, hw / (unsigned)ndev)));
+    const HostPlan p = host_plan("/sys", bus, ndev, std::thread::hardware_concurrency());
+    d->numa = p.numa;
+    d->cpus = p.cpus;
+    d->threads = p.threads;
     d->pool = new HostPool(d->threads > 1 ? d->threads - 1 : 1, d->cpus);
     hosts[device] = d;
     return *d;
@@ -635,6 +668,20 @@ int skv_ctx_set_profiling(skv_ctx* ctx, int enable) {
     if (!ctx) return SKV_E_INVALID_ARG;
     ctx->profiling = enable != 0;
     return SKV_OK;
+}
+
+int skv_host_plan(const char* sysfs_root, const char* pci_bus_id, int n_devices, int hw_threads, int* numa_node,
+                  int* pool_threads, int* cpus, int max_cpus) {
+    try {
+        const HostPlan p = host_plan(sysfs_root && *sysfs_root ? sysfs_root : "/sys", pci_bus_id, n_devices,
+                                     hw_threads > 0 ? (unsigned)hw_threads : 1u);
+        if (numa_node) *numa_node = p.numa;
+        if (pool_threads) *pool_threads = (int)p.threads;
+        for (int i = 0; cpus && i < max_cpus && i < (int)p.cpus.size(); ++i) cpus[i] = p.cpus[i];
+        return p.numa < 0 ? -1 : (int)p.cpus.size();
+    } catch (...) {
+        return -1;
+    }
 }
 
 int skv_ctx_host_info(const skv_ctx* ctx, int* numa_node, int* host_threads) {

@@ -333,6 +333,40 @@ __device__ __forceinline__ void bitonic_pair(uint32_t i, uint32_t lk, uint32_t l
     }
 }
 
+// v of lane (lane ^ M) inside a wave, without the LDS crossbar (ds_bpermute, which __shfl_xor
+// lowers to): DPP quad permutes for 1 and 2, row rotates for 4 and 8, the gfx950 half-row / half-wave
+// swaps for 16 and 32. M is a compile-time constant.
+template <int M>
+__device__ __forceinline__ uint32_t xshfl(uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63;
+    if constexpr (M == 1) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    } else if constexpr (M == 2) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    } else if constexpr (M == 4) {
+        const uint32_t a = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+        const uint32_t b = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x12C, 0xF, 0xF, false);  // row_ror:12
+        return (lane & 4) ? a : b;
+    } else if constexpr (M == 8) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    } else if constexpr (M == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);  // odd rows <-> even rows
+        return (lane & 16) ? r[0] : r[1];
+    } else {
+        static_assert(M == 32, "xshfl: M in {1, 2, 4, 8, 16, 32}");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);  // upper half <-> lower half
+        return (lane & 32) ? r[0] : r[1];
+    }
+}
+template <int M>
+__device__ __forceinline__ uint64_t xshfl64(uint64_t v) {
+    return ((uint64_t)xshfl<M>((uint32_t)(v >> 32)) << 32) | xshfl<M>((uint32_t)v);
+}
+
+// a + b, saturating at 2^64 - 1 (a run's byte budget P[b] + max - 1 with max near 2^64: runs.rs:219
+// compares u64 sizes without overflow)
+__device__ __forceinline__ uint64_t sat_add_u64(uint64_t a, uint64_t b) { return b > ~0ull - a ? ~0ull : a + b; }
+
 struct WalkRes {
     uint64_t end;   // first record start >= stop, or the erroring record's start
     uint32_t cnt;   // records decoded

@@ -400,6 +400,55 @@ int search_stage(skv_ctx* ctx, const Job& job, const RunInfo& run, uint64_t R, u
 void ensure_aux(skv_ctx* ctx);
 int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t max_run_size, uint32_t flags, Job& job);
 void drain(skv_ctx* ctx);
+
+// A pipelined or split call on one ctx (skv_hostpipe.hip, skv_split.hip): table uploads and readbacks
+// by copy kernels, not DMA copies that would queue behind the bulk copies; buffers that grow keep
+// their old allocation (the graveyards) until the ctx's three streams have drained, as a hipFree in
+// between would synchronise the whole device under every other ctx's queued work.
+struct PipeIO {
+    skv_ctx* c;
+    explicit PipeIO(skv_ctx* x) : c(x) {
+        c->kernel_uploads = true;
+        c->defer_free = true;
+    }
+    ~PipeIO() {
+        c->kernel_uploads = false;
+        c->defer_free = false;
+        if (!c->graveyard.empty() || !c->host_graveyard.empty()) {
+            if (c->in_stream) (void)hipStreamSynchronize(c->in_stream);
+            if (c->out_stream) (void)hipStreamSynchronize(c->out_stream);
+            (void)hipStreamSynchronize(c->stream);
+            for (void* q : c->graveyard) (void)hipFree(q);
+            for (void* q : c->host_graveyard) (void)hipHostFree(q);
+            c->graveyard.clear();
+            c->host_graveyard.clear();
+        }
+    }
+};
+
+// Worker threads of a multi-ctx call, joined on every path: a std::thread constructor that throws
+// after some workers started must not destroy joinable threads (std::terminate); the caller's
+// stop() is asked to halt the started workers before they are joined.
+struct WorkerSet {
+    std::vector<std::thread> th;
+    template <class F, class Stop>
+    bool spawn(unsigned n, F&& body, Stop&& stop) {
+        try {
+            for (unsigned g = 0; g < n; ++g) th.emplace_back(body, g);
+        } catch (...) {
+            stop();
+            join();
+            return false;
+        }
+        return true;
+    }
+    void join() {
+        for (std::thread& t : th)
+            if (t.joinable()) t.join();
+        th.clear();
+    }
+    ~WorkerSet() { join(); }
+};
 int run_guarded(skv_ctx* ctx, const Job& job, skv_result** out, double t_entry);
 int compact_host_job(skv_ctx* ctx, Job& job, skv_result** out, double t_entry);
 // skv_compact_split for inputs outside the fused shape (variable-length records, Deletes): key-range

@@ -871,27 +871,7 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     }
     htrace("gpipe: cuts");
     used = true;
-    struct KernelIO {  // table uploads and readbacks by copy kernels, not DMA behind the bulk copies;
-                       // buffers that grow keep their old allocation until the streams have drained
-        skv_ctx* c;
-        explicit KernelIO(skv_ctx* x) : c(x) {
-            c->kernel_uploads = true;
-            c->defer_free = true;
-        }
-        ~KernelIO() {
-            c->kernel_uploads = false;
-            c->defer_free = false;
-            if (!c->graveyard.empty() || !c->host_graveyard.empty()) {
-                if (c->in_stream) (void)hipStreamSynchronize(c->in_stream);
-                if (c->out_stream) (void)hipStreamSynchronize(c->out_stream);
-                (void)hipStreamSynchronize(c->stream);
-                for (void* q : c->graveyard) (void)hipFree(q);
-                for (void* q : c->host_graveyard) (void)hipHostFree(q);
-                c->graveyard.clear();
-                c->host_graveyard.clear();
-            }
-        }
-    } kio(ctx);
+    PipeIO kio(ctx);
     if (!ctx->in_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->in_stream, hipStreamNonBlocking));
     if (!ctx->out_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->out_stream, hipStreamNonBlocking));
     while (ctx->part_ev.size() < 2 * P) {
@@ -1313,24 +1293,7 @@ void gsplit_worker(GSplit& gs, skv_ctx* ctx, uint64_t g, uint64_t G, const Job& 
     if (parts.empty()) return;
     const uint64_t np = parts.size();
     auto run_b = [&](uint64_t m) { return (const uint8_t*)(uintptr_t)job.run_ptr[m]; };
-    struct KernelIO {  // as in compact_host_pipelined_general: no DMA uploads behind the bulk copies
-        skv_ctx* c;
-        explicit KernelIO(skv_ctx* x) : c(x) {
-            c->kernel_uploads = true;
-            c->defer_free = true;
-        }
-        ~KernelIO() {
-            c->kernel_uploads = false;
-            c->defer_free = false;
-            if (c->in_stream) (void)hipStreamSynchronize(c->in_stream);
-            if (c->out_stream) (void)hipStreamSynchronize(c->out_stream);
-            (void)hipStreamSynchronize(c->stream);
-            for (void* q : c->graveyard) (void)hipFree(q);
-            for (void* q : c->host_graveyard) (void)hipHostFree(q);
-            c->graveyard.clear();
-            c->host_graveyard.clear();
-        }
-    } kio(ctx);
+    PipeIO kio(ctx);  // as in compact_host_pipelined_general
     if (!ctx->in_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->in_stream, hipStreamNonBlocking));
     if (!ctx->out_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->out_stream, hipStreamNonBlocking));
     while (ctx->part_ev.size() < np) {
@@ -1524,9 +1487,8 @@ int compact_split_general(skv_ctx* const* ctxs, uint32_t G, Job& job, skv_result
     size_t cap = 0;
     uint8_t* h_out = (uint8_t*)home->out_pool->take(out_cap, cap);
     if (!h_out) throw DevError("pinned host allocation of the output failed");
-    std::vector<std::thread> th;
-    for (uint32_t g = 0; g < G; ++g)
-        th.emplace_back([&, g] {
+    WorkerSet ws;
+    const bool spawned = ws.spawn(G, [&](unsigned g) {
             skv_ctx* c = ctxs[g];
             DeviceScope ds(c->device);
             try {
@@ -1538,8 +1500,9 @@ int compact_split_general(skv_ctx* const* ctxs, uint32_t G, Job& job, skv_result
                 gs.halt(false, std::string("host error: ") + e.what());
             }
             drain(c);  // nothing of this call still runs on the ctx (nor writes h_out)
-        });
-    for (std::thread& t : th) t.join();
+        }, [&] { gs.halt(false, "worker thread creation failed"); });
+    ws.join();
+    if (!spawned && !gs.stop) gs.halt(false, "worker thread creation failed");
     if (gs.stop) {
         home->out_pool->give(h_out, cap);
         if (!gs.err.empty()) throw DevError("split: " + gs.err);

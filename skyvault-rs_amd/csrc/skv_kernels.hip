@@ -1096,6 +1096,206 @@ __device__ void tile_big(Elems E, const uint64_t* bounds, uint32_t k, uint64_t t
     }
 }
 
+// ---- the level-0 tile's merge as a sort of (16-byte prefix, element id) --------------------------
+// k_way::merge's order inside a tile (key asc, then seq_no desc = rec_idx asc) is the sort of the
+// tile's elements by (key, element id): ids follow (stream rank, position). The 16-byte prefix
+// decides almost every compare, and equal prefixes fall back to the id, which is the right order
+// for equal keys; the groups it gets wrong (equal prefixes of different keys: a length or a tail
+// past 16 bytes differs) are re-sorted with the full compare afterwards (tile_fix_ties).
+// Each wave sorts 256 consecutive positions in registers (a bitonic network, 4 elements per lane at
+// index 4 lane + r: 15 stages inside a lane, 21 across lanes over DPP / permlane swaps, no LDS and
+// no barrier); then LDS merge-path rounds merge the 16 sorted runs of 256 (4 rounds instead of
+// log2(k) rounds over the streams' segments, 8 at k = 256).
+struct WK {
+    uint64_t h, l;
+    uint32_t id;
+};
+__device__ __forceinline__ bool wk_less(const WK& a, const WK& b) {
+    return a.h < b.h || (a.h == b.h && (a.l < b.l || (a.l == b.l && a.id < b.id)));
+}
+template <int LM>
+__device__ __forceinline__ WK wk_shfl(const WK& x) {
+    return WK{xshfl64<LM>(x.h), xshfl64<LM>(x.l), xshfl<LM>(x.id)};
+}
+// compare-exchange stage (block 2^KK, distance 2^JJ) of the ascending bitonic sort
+template <int KK, int JJ>
+__device__ __forceinline__ void wk_stage(WK (&x)[4], uint32_t lane) {
+    constexpr uint32_t K2 = 1u << KK, D = 1u << JJ;
+    if constexpr (D < 4) {  // partners in the same lane: registers r and r | D
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+            if (r & D) continue;
+            const bool asc = ((4 * lane + r) & K2) == 0;
+            WK a = x[r], b = x[r | D];
+            const bool sw = asc ? wk_less(b, a) : wk_less(a, b);
+            x[r] = sw ? b : a;
+            x[r | D] = sw ? a : b;
+        }
+    } else {  // partner lane ^ D / 4, same register
+        constexpr int LM = (int)(D / 4);
+        const bool take_min = ((lane & LM) == 0) == (((4 * lane) & K2) == 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const WK y = wk_shfl<LM>(x[r]);
+            if (take_min == wk_less(y, x[r])) x[r] = y;
+        }
+    }
+}
+template <int KK, int JJ>
+__device__ __forceinline__ void wk_merge(WK (&x)[4], uint32_t lane) {
+    wk_stage<KK, JJ>(x, lane);
+    if constexpr (JJ > 0) wk_merge<KK, JJ - 1>(x, lane);
+}
+template <int KK>
+__device__ __forceinline__ void wk_sort(WK (&x)[4], uint32_t lane) {
+    if constexpr (KK > 1) wk_sort<KK - 1>(x, lane);
+    wk_merge<KK, KK - 1>(x, lane);
+}
+__device__ __forceinline__ bool k16_less(const ulong2& a, uint32_t ia, const ulong2& b, uint32_t ib) {
+    return a.x < b.x || (a.x == b.x && (a.y < b.y || (a.y == b.y && ia < ib)));
+}
+
+// (16-byte prefix by position, element id by position) -> sorted by (prefix, id). key16 / mi hold the
+// elements at their load positions (id == position) on entry.
+__device__ void tile_sort_wave(ulong2* key16, uint16_t* mi, uint32_t n) {
+    static_assert(TILE_THREADS * 4 == TILE_CAP && TILE_CAP <= 4096, "one 256-position run per wave");
+    constexpr int PER = 4;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    {
+        WK x[4];
+        const uint32_t p0 = 256 * w + 4 * lane;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t p = p0 + r;
+            if (p < n) {
+                const ulong2 k = key16[p];
+                x[r] = WK{k.x, k.y, p};
+            } else {
+                x[r] = WK{~0ull, ~0ull, 0xFFFFu};  // padding sorts last
+            }
+        }
+        if (256 * w < n) wk_sort<8>(x, lane);  // (waves past n idle: no barrier inside the sort)
+        if (256 * w < n) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t p = p0 + r;
+                if (p < n) {
+                    key16[p] = make_ulong2(x[r].h, x[r].l);
+                    mi[p] = (uint16_t)x[r].id;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // merge-path rounds over the sorted runs (length L, pairs of 2L; a thread's PER outputs lie in
+    // one pair because 2L is a multiple of PER)
+    const uint32_t o0 = threadIdx.x * PER;
+    for (uint32_t L = 256; L < n; L <<= 1) {
+        ulong2 ok[PER];
+        uint32_t ox[PER];
+        if (o0 < n) {
+            const uint32_t a0 = o0 & ~(2 * L - 1);
+            const uint32_t a1 = a0 + L < n ? a0 + L : n, b1 = a0 + 2 * L < n ? a0 + 2 * L : n;
+            const uint32_t lenA = a1 - a0, lenB = b1 - a1, d = o0 - a0;
+            uint32_t l = d > lenB ? d - lenB : 0, h = d < lenA ? d : lenA;
+            while (l < h) {  // how many of the first d outputs come from A
+                const uint32_t mid = (l + h) >> 1, pa = a0 + mid, pb = a1 + d - mid - 1;
+                if (k16_less(key16[pa], mi[pa], key16[pb], mi[pb])) l = mid + 1;
+                else h = mid;
+            }
+            uint32_t ia = a0 + l, ib = a1 + (d - l);
+            ulong2 hA = make_ulong2(0, 0), hB = make_ulong2(0, 0);
+            uint32_t xA = 0, xB = 0;
+            if (ia < a1) {
+                hA = key16[ia];
+                xA = mi[ia];
+            }
+            if (ib < b1) {
+                hB = key16[ib];
+                xB = mi[ib];
+            }
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const bool takeA = ia < a1 && (ib >= b1 || k16_less(hA, xA, hB, xB));
+                if (takeA) {
+                    ok[q] = hA;
+                    ox[q] = xA;
+                    if (++ia < a1) {
+                        hA = key16[ia];
+                        xA = mi[ia];
+                    }
+                } else {
+                    ok[q] = hB;
+                    ox[q] = xB;
+                    if (++ib < b1) {
+                        hB = key16[ib];
+                        xB = mi[ib];
+                    }
+                }
+            }
+        }
+        __syncthreads();  // every thread has read its inputs of this round
+#pragma unroll
+        for (int q = 0; q < PER; ++q)
+            if (o0 + q < n) {
+                key16[o0 + q] = ok[q];
+                mi[o0 + q] = (uint16_t)ox[q];
+            }
+        __syncthreads();
+    }
+}
+
+// Groups of positions with one 16-byte prefix are in id order after tile_sort_wave. That is the
+// merge order when the group's keys are equal (one length and, past 16 bytes, one fingerprint: the
+// fingerprint shortcut's "equal"); a group with two lengths or two fingerprints (or any key past 16
+// bytes in exact mode) is re-sorted with the full compare (elem_less_fp), by one thread per group.
+__device__ void tile_fix_ties(const ulong2* key16, uint16_t* mi, uint32_t n, const uint64_t* el_c,
+                              const uint64_t* el_fp, const uint64_t* kfp, const uint64_t* rec_addr, uint32_t* s_cx) {
+    constexpr int PER = 4;
+    const uint32_t o0 = threadIdx.x * PER;
+    if (threadIdx.x == 0) *s_cx = 0;
+    __syncthreads();
+    bool cx = false;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = o0 + q;
+        if (i > 0 && i < n) {
+            const ulong2 a = key16[i - 1], b = key16[i];
+            if (a.x == b.x && a.y == b.y) {
+                const uint32_t p = mi[i - 1], e = mi[i];
+                const uint32_t kp = (uint32_t)(el_c[p] >> 32), ke = (uint32_t)(el_c[e] >> 32);
+                cx |= kp != ke || (ke > 16 && (!kfp || el_fp[p] != el_fp[e]));
+            }
+        }
+    }
+    if (cx) *s_cx = 1;
+    __syncthreads();
+    if (!*s_cx) return;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t g0 = o0 + q;
+        if (g0 + 1 >= n) continue;
+        const ulong2 k = key16[g0];
+        if (g0 > 0 && key16[g0 - 1].x == k.x && key16[g0 - 1].y == k.y) continue;  // not a group start
+        uint32_t g1 = g0 + 1;
+        while (g1 < n && key16[g1].x == k.x && key16[g1].y == k.y) ++g1;
+        if (g1 - g0 < 2) continue;
+        for (uint32_t i = g0 + 1; i < g1; ++i) {  // insertion sort of the group's ids
+            const uint32_t e = mi[i];
+            uint32_t j = i;
+            while (j > g0) {
+                const uint32_t p = mi[j - 1];
+                if (!elem_less_fp(kfp != nullptr, el_fp[e], rec_addr, k.x, k.y, el_c[e], k.x, k.y, el_c[p], el_fp[p]))
+                    break;
+                mi[j] = (uint16_t)p;
+                --j;
+            }
+            mi[j] = (uint16_t)e;
+        }
+    }
+    __syncthreads();
+}
+
 #if SKV_TILE_PROF
 #define TPROF(i)                                                                 \
     do {                                                                         \
@@ -1126,6 +1326,13 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     uint64_t* el_fp = el_c + TILE_CAP;
     uint16_t* mi = (uint16_t*)(el_fp + TILE_CAP);
     uint16_t* posof = mi + TILE_CAP;  // after the rounds: merged position of each element
+    // level-0 tiles outside heap-order mode: hp / el_lo hold {hp, lo} by position instead (key16),
+    // sorted by tile_sort_wave
+    ulong2* key16 = (ulong2*)smem;
+#ifndef SKV_TILE_WAVE
+#define SKV_TILE_WAVE 1
+#endif
+    const bool wpath = SKV_TILE_WAVE && L0 && O.act_hi == nullptr;
     uint32_t* cbA = (uint32_t*)(posof + TILE_CAP);
     uint32_t* cbB = cbA + (k + 1);
     uint64_t* ws = (uint64_t*)(((uintptr_t)(cbB + (k + 1)) + 15) & ~(uintptr_t)15);
@@ -1197,8 +1404,12 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                 raddr[u] = (O.pay_addr ? O.pay_addr : rec_addr)[pos];  // coalesced here, not gathered later
                 if (kfp) fp = kfp[pos];
             }
-            hp[e] = rh[u];
-            el_lo[e] = lo;
+            if (wpath) {
+                key16[e] = make_ulong2(rh[u], lo);
+            } else {
+                hp[e] = rh[u];
+                el_lo[e] = lo;
+            }
             el_c[e] = rc[u];
             el_fp[e] = fp;
             mi[e] = (uint16_t)e;
@@ -1216,7 +1427,17 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                                  el_c[xb], el_fp[xb])
                   : elem_less(rec_addr, ha, el_lo[xa], el_c[xa], hb, el_lo[xb], el_c[xb]);
     };
-    {
+    if (wpath) {
+        tile_sort_wave(key16, mi, n);
+        tile_fix_ties(key16, mi, n, el_c, el_fp, kfp, rec_addr, s_flag + 30);
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) posof[mi[i]] = (uint16_t)i;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const uint32_t e = threadIdx.x + u * TILE_THREADS;
+            if (e < n) rpos[u] = posof[e];
+        }
+    } else {
         const uint32_t o0 = threadIdx.x * PER;
         uint32_t m = k;
         uint32_t* cb = cbA;
@@ -1340,8 +1561,9 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                 if (i > 0) first = act_key_cmp(O, (uint32_t)el_c[mi[i - 1]], (uint32_t)c) != 0;
             } else if (i > 0) {
                 const uint32_t p = mi[i - 1];
-                if (hp[i - 1] == hp[i]) {
-                    const uint64_t lp = el_lo[p], le = el_lo[e], cp = el_c[p];
+                if (wpath ? key16[i - 1].x == key16[i].x : hp[i - 1] == hp[i]) {
+                    const uint64_t lp = wpath ? key16[i - 1].y : el_lo[p], le = wpath ? key16[i].y : el_lo[e];
+                    const uint64_t cp = el_c[p];
                     int kc = lp != le ? (lp < le ? -1 : 1) : 0;
                     const uint32_t kp = (uint32_t)(cp >> 32), ke = (uint32_t)(c >> 32);
                     if (!kc && kp > 16 && ke > 16) {
@@ -1707,7 +1929,8 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
         {
             uint64_t wl;
             if (tbl && all_fit) {
-                const uint64_t low = Pb + (uint64_t)(lane + 1) * (max_size - 1 - mr);
+                const uint64_t step = max_size - 1 - mr;  // (saturating: max may be near 2^64)
+                const uint64_t low = step > (~0ull - Pb) / (uint64_t)(lane + 1) ? ~0ull : Pb + (uint64_t)(lane + 1) * step;
                 wl = (low >= PK || lane >= ch_d) ? K : (uint64_t)tbl[low >> CH_SHIFT];
             } else {
                 const uint64_t c = b + (uint64_t)(lane + 1) * L;
@@ -1746,7 +1969,7 @@ __global__ void __launch_bounds__(64) k_chain(const uint64_t* __restrict__ Kp, c
                 e = b + 1;  // a run of one record that alone exceeds max (runs.rs:219 needs !first)
                 Pe = P[e];
             } else {
-                const uint64_t v = Pb + max_size - 1;  // record j fits iff P[j+1] <= v
+                const uint64_t v = sat_add_u64(Pb, max_size - 1);  // record j fits iff P[j+1] <= v
                 const uint64_t ws = wsd[d];
                 // predicate P[pos] <= v is monotone in pos = ws + 4*lane + q: the last true
                 // position is found from four wave ballots with scalar bit ops
@@ -1881,7 +2104,7 @@ __device__ __forceinline__ uint64_t sp_step(const uint64_t* __restrict__ P, uint
         Pe = PK;
         return K;
     }
-    const uint64_t v = Pb + M - 1;  // record j fits iff P[j + 1] <= v
+    const uint64_t v = sat_add_u64(Pb, M - 1);  // record j fits iff P[j + 1] <= v
     if (PK <= v) {
         Pe = PK;
         return K;
@@ -2896,7 +3119,7 @@ __global__ void k_carry_first(const uint64_t* __restrict__ Kp, const uint64_t* _
     const uint64_t K = *Kp;
     uint64_t e = 0;
     if (c < max_size) {
-        const uint64_t v = P[0] + (max_size - c);  // record j joins iff P[j + 1] <= v
+        const uint64_t v = sat_add_u64(P[0], max_size - c);  // record j joins iff P[j + 1] <= v
         uint64_t lo = 0, hi = K;                   // largest e in [0, K] with P[e] <= v
         while (lo < hi) {
             const uint64_t mid = (lo + hi + 1) >> 1;

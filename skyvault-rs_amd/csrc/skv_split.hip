@@ -122,11 +122,9 @@ void split_worker(Split& sp, skv_ctx* ctx, uint64_t g) {
         out_off[i + 1] = out_off[i] + ((1 + Rp[i] * S + 16 + 255) & ~255ull);
     }
     hipStream_t st = ctx->stream;
-    struct KernelUploads {  // table uploads by kernel: a DMA upload would queue behind the bulk H2D
-        skv_ctx* c;
-        explicit KernelUploads(skv_ctx* x) : c(x) { c->kernel_uploads = true; }
-        ~KernelUploads() { c->kernel_uploads = false; }
-    } ku(ctx);
+    // table uploads by kernel (a DMA upload would queue behind the bulk H2D); fx_launch's own buffers
+    // are sized per part and may grow mid-queue: their old allocations wait for the streams to drain
+    PipeIO kio(ctx);
     ctx->syncs = 0;
     ctx->up_chunk = 0;
     ctx->up_off = 0;
@@ -146,7 +144,7 @@ void split_worker(Split& sp, skv_ctx* ctx, uint64_t g) {
         ctx->part_k_cap = std::max<uint64_t>(2 * np, 64);
     }
     volatile uint64_t* hK = ctx->part_k;  // [2i] survivors of part i, [2i + 1] its verdict words
-    // every buffer sized before the first launch (no buffer moves under queued work)
+    // the call's own buffers sized before the first launch (fx_launch's per-part ones: PipeIO above)
     uint8_t* d_in = dbuf<uint8_t>(ctx, "host_in", in_off[np] + 16);
     uint8_t* d_out = dbuf<uint8_t>(ctx, "out", out_off[np] + 16);
     uint64_t* d_K = dbuf<uint64_t>(ctx, "hp_K", np);
@@ -225,6 +223,25 @@ void split_worker(Split& sp, skv_ctx* ctx, uint64_t g) {
 
 extern "C" {
 
+// The deal of skv_compact_split's key-range parts (include/skv.h): part p on ctxs[p % n_ctx]; ctxs that
+// share a device take their parts' H2D in part order, so part p waits for the H2D of the latest
+// earlier part dealt to another ctx of its device (h2d_after[p], -1: none).
+int skv_split_deal(const int* ctx_device, uint32_t n_ctx, uint64_t n_parts, uint32_t* ctx_of_part,
+                   int64_t* h2d_after) {
+    if (!ctx_device || !n_ctx || (n_parts && (!ctx_of_part || !h2d_after))) return SKV_E_INVALID_ARG;
+    std::map<int, uint64_t> last;  // device -> its latest part so far
+    for (uint64_t p = 0; p < n_parts; ++p) {
+        const uint32_t g = (uint32_t)(p % n_ctx);
+        const int dv = ctx_device[g];
+        ctx_of_part[p] = g;
+        h2d_after[p] = -1;
+        auto it = last.find(dv);
+        if (it != last.end() && it->second % n_ctx != g) h2d_after[p] = (int64_t)it->second;
+        last[dv] = p;
+    }
+    return SKV_OK;
+}
+
 int skv_compact_split(skv_ctx* const* ctxs, uint32_t n_ctx, const skv_stream* streams, uint32_t n_streams,
                       uint64_t max_run_size, uint32_t flags, skv_result** out) {
     const double t_entry = now_ms();
@@ -279,22 +296,19 @@ int skv_compact_split(skv_ctx* const* ctxs, uint32_t n_ctx, const skv_stream* st
                 sp.h2d_ev.assign(P, nullptr);
                 sp.prev_on_dev.assign(P, -1);
                 {
-                    std::map<int, uint64_t> last;  // device -> its latest part so far
-                    for (uint64_t p = 0; p < P; ++p) {
-                        const int dv = ctxs[p % G]->device;
-                        auto it = last.find(dv);
-                        if (it != last.end() && it->second % G != p % G) sp.prev_on_dev[p] = (int64_t)it->second;
-                        last[dv] = p;
-                    }
+                    std::vector<int> dev(G);
+                    std::vector<uint32_t> ctx_of(P);
+                    for (uint64_t g = 0; g < G; ++g) dev[g] = ctxs[g]->device;
+                    (void)skv_split_deal(dev.data(), (uint32_t)G, P, ctx_of.data(), sp.prev_on_dev.data());
                 }
                 // sized for every record surviving (the counts arrive while the copies run)
                 sp.out_cap = R * f.S + (R + n - 1) / n;
                 size_t cap = 0;
                 sp.h_out = (uint8_t*)home->out_pool->take(std::max<uint64_t>(sp.out_cap, 1), cap);
                 if (!sp.h_out) return set_err(home, SKV_E_DEVICE, "pinned host allocation of the output failed");
-                std::vector<std::thread> th;
-                for (uint64_t g = 0; g < G; ++g)
-                    th.emplace_back([&sp, ctx = ctxs[g], g] {
+                WorkerSet ws;
+                const bool spawned = ws.spawn((unsigned)G, [&sp, ctxs](unsigned g) {
+                        skv_ctx* ctx = ctxs[g];
                         DeviceScope ds(ctx->device);
                         try {
                             if (!ds.ok) throw DevError("hipSetDevice failed");
@@ -305,8 +319,9 @@ int skv_compact_split(skv_ctx* const* ctxs, uint32_t n_ctx, const skv_stream* st
                             sp.halt(false, std::string("host error: ") + e.what());
                         }
                         drain(ctx);  // nothing of this call still runs on the ctx (nor writes h_out)
-                    });
-                for (std::thread& t : th) t.join();
+                    }, [&sp] { sp.halt(false, "worker thread creation failed"); });
+                ws.join();
+                if (!spawned && sp.err.empty()) sp.halt(false, "worker thread creation failed");
                 if (!sp.err.empty() || sp.poisoned) {
                     home->out_pool->give(sp.h_out, cap);
                     if (!sp.err.empty()) return set_err(home, SKV_E_DEVICE, "split: %s", sp.err.c_str());

@@ -133,6 +133,8 @@ EXPORTED_SYMBOLS = [
     "skv_ctx_set_profiling",
     "skv_ctx_get_timings",
     "skv_ctx_host_info",
+    "skv_host_plan",
+    "skv_split_deal",
     "skv_compact",
     "skv_compact_dev",
     "skv_compact_split",

@@ -56,6 +56,12 @@ def load():
     l.skv_ctx_get_timings.argtypes = [C.c_void_p, C.POINTER(SkvTimings)]
     l.skv_ctx_host_info.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     l.skv_ctx_host_info.restype = C.c_int
+    l.skv_host_plan.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                C.POINTER(C.c_int), C.c_int]
+    l.skv_host_plan.restype = C.c_int
+    l.skv_split_deal.argtypes = [C.POINTER(C.c_int), C.c_uint32, C.c_uint64, C.POINTER(C.c_uint32),
+                                 C.POINTER(C.c_int64)]
+    l.skv_split_deal.restype = C.c_int
     for fn in (l.skv_compact, l.skv_compact_dev):
         fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.POINTER(C.POINTER(SkvResult))]
         fn.restype = C.c_int
@@ -411,3 +417,28 @@ def device_count() -> int:
     n = C.c_int(0)
     load().skv_device_count(C.byref(n))
     return n.value
+
+
+def host_plan(pci_bus_id: str, n_devices: int, hw_threads: int, sysfs_root: str = "/sys") -> dict:
+    """skv_host_plan: the NUMA node, host-pool size and CPUs the library gives the GPU at `pci_bus_id`
+    (no device needed; a stub sysfs tree may stand in for /sys)."""
+    l = load()
+    node, threads = C.c_int(-1), C.c_int(0)
+    cpus = (C.c_int * 4096)()
+    n = l.skv_host_plan(sysfs_root.encode(), pci_bus_id.encode(), n_devices, hw_threads, C.byref(node),
+                        C.byref(threads), cpus, 4096)
+    return {"numa_node": node.value, "pool_threads": threads.value, "cpus": sorted(cpus[:max(n, 0)])}
+
+
+def split_deal(ctx_devices: Sequence[int], n_parts: int) -> tuple:
+    """skv_split_deal: (ctx of each part, the part whose H2D each part waits for or -1) for
+    skv_compact_split over ctxs on the devices `ctx_devices` (no device needed)."""
+    l = load()
+    g = len(ctx_devices)
+    dev = (C.c_int * g)(*ctx_devices)
+    ctx_of = (C.c_uint32 * max(n_parts, 1))()
+    after = (C.c_int64 * max(n_parts, 1))()
+    rc = l.skv_split_deal(dev, g, n_parts, ctx_of, after)
+    if rc != SKV_OK:
+        raise RunError(rc, "skv_split_deal: invalid arguments")
+    return list(ctx_of[:n_parts]), list(after[:n_parts])

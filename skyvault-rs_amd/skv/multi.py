@@ -17,10 +17,13 @@ from concurrent.futures import Future
 from typing import Callable, List, Optional, Sequence, Set
 
 
+SYSFS_ROOT = "/sys"  # tests point this at a stub tree (the library's skv_host_plan takes the same root)
+
+
 def numa_cpus(node: int) -> Set[int]:
     """CPUs of NUMA node `node` that this process may run on (sysfs cpulist; empty if unknown)."""
     try:
-        with open(f"/sys/devices/system/node/node{int(node)}/cpulist") as f:
+        with open(f"{SYSFS_ROOT}/devices/system/node/node{int(node)}/cpulist") as f:
             text = f.read().strip()
     except OSError:
         return set()
@@ -55,7 +58,16 @@ class MultiCompactor:
         bytes, the default), "compact_dev" (device pointers: [(seq_no, [(ptr, len)])]) or
         "compact_host" (pinned host pointers). then(compactor, result), if given, runs on the
         worker's thread right after the call (e.g. to read the ctx's timings before its next
-        call); the future holds its return value."""
+        call); the future holds its return value.
+
+        A "compact_dev" result lives in the ctx's device output buffer, which the worker's next
+        call on the same ctx overwrites (include/skv.h: valid until the next call on the ctx), so
+        that entry requires `then`: read or copy the result there, before the worker moves on."""
+        if entry not in ("compact", "compact_dev", "compact_host"):
+            raise ValueError(f"unknown entry {entry!r}")
+        if entry == "compact_dev" and then is None:
+            raise ValueError('entry="compact_dev" needs then=: its DeviceResult is valid only until the '
+                             "worker's next call on the same ctx")
         size = sum(len(r) if isinstance(r, (bytes, bytearray, memoryview)) else r[1]
                    for _, runs in streams for r in runs)
         with self._lock:

@@ -21,7 +21,7 @@ def test_header_declares_exactly_the_bound_symbols():
 def test_library_exports_every_symbol():
     api.build()
     assert api.exported_symbols_present() == _abi.EXPORTED_SYMBOLS
-    assert api.load().skv_abi_version() == 8
+    assert api.load().skv_abi_version() == 9
 
 
 def test_struct_layouts_match_header():

@@ -313,6 +313,23 @@ def test_greedy_split_random_sizes_with_oversized_records(dev):
     assert not bad, bad[:5]
 
 
+@pytest.mark.parametrize("max_size", [(1 << 64) - 1, (1 << 64) - 2, (1 << 63) + 5])
+@pytest.mark.parametrize("flags", [0, _abi.SKV_DROP_TOMBSTONES], ids=["flags0", "drop"])
+def test_max_run_size_near_two_to_the_64(dev, max_size, flags):
+    """build_runs compares u64 sizes without overflow (runs.rs:219): with max near 2^64 every record
+    joins one run. The chain's byte budget P[b] + max - 1 and its byte-table windows saturate
+    instead of wrapping: variable sizes (the general split), one size (arithmetic) and
+    the fused shape."""
+    streams = gen.config3(seed=4242, n_streams=10, run_bytes=64 * 1024)
+    exp, got = _run_both(dev, streams, max_size, flags)
+    assert exp == got, _diff(exp, got)
+    r = random.Random(17)
+    fixed = [(s + 1, [fmt.encode_run([fmt.put(f"k{k:07d}", bytes([s]) * 40)
+                                      for k in sorted(r.sample(range(50000), 3000))])]) for s in range(5)]
+    exp, got = _run_both(dev, fixed, max_size, flags)
+    assert exp == got, _diff(exp, got)
+
+
 def test_wal_one_pass_stage_many_tables(dev):
     """k_wal_fused's table-start list past the readback it reads with the verdict (WF_GUESS = 1024
     starts: the rest comes in a second copy) and past its capacity (WF_TCAP = 65536: the exact stage

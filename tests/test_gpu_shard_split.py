@@ -88,7 +88,7 @@ def _check(cs, streams, max_size, flags=0, split=True, parts=1, general=False):
 
 
 @pytest.mark.parametrize("G", [2, 3, 5, 8])
-@pytest.mark.parametrize("max_size", [4 * MiB, 1000, 7777, 1 << 62])
+@pytest.mark.parametrize("max_size", [4 * MiB, 1000, 7777, 1 << 62, (1 << 64) - 1])
 def test_split_matches_oracle(ctxs, G, max_size):
     rng = random.Random(G * 1009 + max_size % 991)
     _check(ctxs[:G], _streams(rng, 8, 3000, 12000), max_size)
@@ -210,7 +210,7 @@ def test_tiny_call(ctxs):
 
 
 @pytest.mark.parametrize("G", [2, 3, 8])
-@pytest.mark.parametrize("max_size", [4096, 1000, 64 * 1024, 1 << 62])
+@pytest.mark.parametrize("max_size", [4096, 1000, 64 * 1024, 1 << 62, (1 << 64) - 1])
 @pytest.mark.parametrize("flags", [0, _abi.SKV_DROP_TOMBSTONES], ids=["flags0", "drop"])
 def test_general_split_matches_oracle(ctxs, G, max_size, flags):
     """config 3's shape (8-128 B keys, 10 % Deletes): runs continue across part edges"""
