@@ -1096,38 +1096,31 @@ __device__ void tile_big(Elems E, const uint64_t* bounds, uint32_t k, uint64_t t
     }
 }
 
-// ---- the level-0 tile's merge as a sort of (16-byte prefix, element id) --------------------------
+// ---- the level-0 tile's merge as a sort of packed 64-bit words ------------------------------------
 // k_way::merge's order inside a tile (key asc, then seq_no desc = rec_idx asc) is the sort of the
-// tile's elements by (key, element id): ids follow (stream rank, position). The 16-byte prefix
-// decides almost every compare, and equal prefixes fall back to the id, which is the right order
-// for equal keys; the groups it gets wrong (equal prefixes of different keys: a length or a tail
-// past 16 bytes differs) are re-sorted with the full compare afterwards (tile_fix_ties).
-// Each wave sorts 256 consecutive positions in registers (a bitonic network, 4 elements per lane at
-// index 4 lane + r: 15 stages inside a lane, 21 across lanes over DPP / permlane swaps, no LDS and
-// no barrier); then LDS merge-path rounds merge the 16 sorted runs of 256 (4 rounds instead of
-// log2(k) rounds over the streams' segments, 8 at k = 256).
-struct WK {
-    uint64_t h, l;
-    uint32_t id;
-};
-__device__ __forceinline__ bool wk_less(const WK& a, const WK& b) {
-    return a.h < b.h || (a.h == b.h && (a.l < b.l || (a.l == b.l && a.id < b.id)));
-}
-template <int LM>
-__device__ __forceinline__ WK wk_shfl(const WK& x) {
-    return WK{xshfl64<LM>(x.h), xshfl64<LM>(x.l), xshfl<LM>(x.id)};
-}
-// compare-exchange stage (block 2^KK, distance 2^JJ) of the ascending bitonic sort
+// tile's elements by (key, element id): ids follow (stream rank, position). Each element becomes ONE
+// 64-bit word: the 52 key bits that follow the tile's common key prefix (c bytes, c <= 8, from the
+// OR of every key XOR the first one: the tile is a key range, so its keys often share bytes), then
+// the 12-bit id. Words order as the keys do, except inside a group of equal 52-bit windows, which
+// comes out in id order: the merge order when the group's keys are equal (one 16-byte prefix, one
+// length, one fingerprint past 16 bytes: the fingerprint shortcut's "equal"), and re-sorted with the
+// full compare otherwise (tile_fix_groups). Equal keys across streams (config 3: a third of the
+// records) are the common group; keys that differ only past the window are rare.
+// Each wave sorts 256 consecutive positions in registers (a bitonic network, 4 words per lane at
+// index 4 lane + r: 15 stages inside a lane, 21 across lanes over DPP / permlane swaps, no LDS, no
+// barrier); then LDS merge-path rounds over the words merge the 16 sorted runs of 256 (4 rounds,
+// one 8-byte read per probe, in place of log2(k) rounds over the streams' segments, 8 at k = 256,
+// reading 8-byte prefixes + ids + by-id key words on ties).
 template <int KK, int JJ>
-__device__ __forceinline__ void wk_stage(WK (&x)[4], uint32_t lane) {
+__device__ __forceinline__ void wd_stage(uint64_t (&x)[4], uint32_t lane) {
     constexpr uint32_t K2 = 1u << KK, D = 1u << JJ;
     if constexpr (D < 4) {  // partners in the same lane: registers r and r | D
 #pragma unroll
         for (uint32_t r = 0; r < 4; ++r) {
             if (r & D) continue;
             const bool asc = ((4 * lane + r) & K2) == 0;
-            WK a = x[r], b = x[r | D];
-            const bool sw = asc ? wk_less(b, a) : wk_less(a, b);
+            const uint64_t a = x[r], b = x[r | D];
+            const bool sw = asc ? b < a : a < b;
             x[r] = sw ? b : a;
             x[r | D] = sw ? a : b;
         }
@@ -1136,164 +1129,215 @@ __device__ __forceinline__ void wk_stage(WK (&x)[4], uint32_t lane) {
         const bool take_min = ((lane & LM) == 0) == (((4 * lane) & K2) == 0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const WK y = wk_shfl<LM>(x[r]);
-            if (take_min == wk_less(y, x[r])) x[r] = y;
+            const uint64_t y = xshfl64<LM>(x[r]);
+            if (take_min == (y < x[r])) x[r] = y;
         }
     }
 }
 template <int KK, int JJ>
-__device__ __forceinline__ void wk_merge(WK (&x)[4], uint32_t lane) {
-    wk_stage<KK, JJ>(x, lane);
-    if constexpr (JJ > 0) wk_merge<KK, JJ - 1>(x, lane);
+__device__ __forceinline__ void wd_merge(uint64_t (&x)[4], uint32_t lane) {
+    wd_stage<KK, JJ>(x, lane);
+    if constexpr (JJ > 0) wd_merge<KK, JJ - 1>(x, lane);
 }
 template <int KK>
-__device__ __forceinline__ void wk_sort(WK (&x)[4], uint32_t lane) {
-    if constexpr (KK > 1) wk_sort<KK - 1>(x, lane);
-    wk_merge<KK, KK - 1>(x, lane);
-}
-__device__ __forceinline__ bool k16_less(const ulong2& a, uint32_t ia, const ulong2& b, uint32_t ib) {
-    return a.x < b.x || (a.x == b.x && (a.y < b.y || (a.y == b.y && ia < ib)));
+__device__ __forceinline__ void wd_sort(uint64_t (&x)[4], uint32_t lane) {
+    if constexpr (KK > 1) wd_sort<KK - 1>(x, lane);
+    wd_merge<KK, KK - 1>(x, lane);
 }
 
-// (16-byte prefix by position, element id by position) -> sorted by (prefix, id). key16 / mi hold the
-// elements at their load positions (id == position) on entry.
-__device__ void tile_sort_wave(ulong2* key16, uint16_t* mi, uint32_t n) {
-    static_assert(TILE_THREADS * 4 == TILE_CAP && TILE_CAP <= 4096, "one 256-position run per wave");
-    constexpr int PER = 4;
+constexpr uint32_t WD_ID = 12;  // id bits of a sort word (TILE_CAP <= 4096)
+static_assert(TILE_CAP <= (1 << WD_ID), "element ids fit the sort word");
+
+// the 8 key bytes that follow c common bytes (0 <= c <= 8) of a 16-byte prefix
+__device__ __forceinline__ uint64_t wd_window(uint64_t hi, uint64_t lo, uint32_t c) {
+    return c == 0 ? hi : (c >= 8 ? lo : (hi << (8 * c)) | (lo >> (64 - 8 * c)));
+}
+
+// key16 (by id, id == load position), n elements -> wd[] by position: runs of 256 sorted words.
+// c: common prefix bytes of the tile's keys (<= 8).
+__device__ void tile_sort_words(const ulong2* key16, uint64_t* wd, uint32_t n, uint32_t c) {
+    static_assert(TILE_THREADS * 4 == TILE_CAP, "one 256-position run per wave");
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    {
-        WK x[4];
+    if (256 * w < n) {  // waves past n idle (no barrier inside the sort)
+        uint64_t x[4];
         const uint32_t p0 = 256 * w + 4 * lane;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t p = p0 + r;
             if (p < n) {
                 const ulong2 k = key16[p];
-                x[r] = WK{k.x, k.y, p};
+                x[r] = (wd_window(k.x, k.y, c) >> WD_ID << WD_ID) | p;
             } else {
-                x[r] = WK{~0ull, ~0ull, 0xFFFFu};  // padding sorts last
+                x[r] = ~0ull;  // padding sorts last
             }
         }
-        if (256 * w < n) wk_sort<8>(x, lane);  // (waves past n idle: no barrier inside the sort)
-        if (256 * w < n) {
+        wd_sort<8>(x, lane);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint32_t p = p0 + r;
-                if (p < n) {
-                    key16[p] = make_ulong2(x[r].h, x[r].l);
-                    mi[p] = (uint16_t)x[r].id;
-                }
-            }
-        }
+        for (int r = 0; r < 4; ++r)
+            if (p0 + r < n) wd[p0 + r] = x[r];
     }
     __syncthreads();
-    // merge-path rounds over the sorted runs (length L, pairs of 2L; a thread's PER outputs lie in
-    // one pair because 2L is a multiple of PER)
+}
+// merge-path rounds over the sorted runs of 256 words (length L, pairs of 2L; a thread's 4 outputs lie
+// in one pair because 2L is a multiple of 4); words are distinct (the id), so no tie rule. ow: this
+// thread's final words (positions 4 tid .. 4 tid + 3, valid below n), for the caller's epilogue.
+__device__ void tile_merge_runs(uint64_t* wd, uint32_t n, uint64_t (&ow)[4]) {
+    constexpr int PER = 4;
     const uint32_t o0 = threadIdx.x * PER;
+    bool rounds = false;
     for (uint32_t L = 256; L < n; L <<= 1) {
-        ulong2 ok[PER];
-        uint32_t ox[PER];
+        rounds = true;
         if (o0 < n) {
             const uint32_t a0 = o0 & ~(2 * L - 1);
             const uint32_t a1 = a0 + L < n ? a0 + L : n, b1 = a0 + 2 * L < n ? a0 + 2 * L : n;
             const uint32_t lenA = a1 - a0, lenB = b1 - a1, d = o0 - a0;
             uint32_t l = d > lenB ? d - lenB : 0, h = d < lenA ? d : lenA;
             while (l < h) {  // how many of the first d outputs come from A
-                const uint32_t mid = (l + h) >> 1, pa = a0 + mid, pb = a1 + d - mid - 1;
-                if (k16_less(key16[pa], mi[pa], key16[pb], mi[pb])) l = mid + 1;
+                const uint32_t mid = (l + h) >> 1;
+                if (wd[a0 + mid] < wd[a1 + d - mid - 1]) l = mid + 1;
                 else h = mid;
             }
             uint32_t ia = a0 + l, ib = a1 + (d - l);
-            ulong2 hA = make_ulong2(0, 0), hB = make_ulong2(0, 0);
-            uint32_t xA = 0, xB = 0;
-            if (ia < a1) {
-                hA = key16[ia];
-                xA = mi[ia];
-            }
-            if (ib < b1) {
-                hB = key16[ib];
-                xB = mi[ib];
-            }
+            uint64_t hA = ia < a1 ? wd[ia] : ~0ull, hB = ib < b1 ? wd[ib] : ~0ull;
 #pragma unroll
             for (int q = 0; q < PER; ++q) {
-                const bool takeA = ia < a1 && (ib >= b1 || k16_less(hA, xA, hB, xB));
-                if (takeA) {
-                    ok[q] = hA;
-                    ox[q] = xA;
-                    if (++ia < a1) {
-                        hA = key16[ia];
-                        xA = mi[ia];
-                    }
-                } else {
-                    ok[q] = hB;
-                    ox[q] = xB;
-                    if (++ib < b1) {
-                        hB = key16[ib];
-                        xB = mi[ib];
-                    }
-                }
+                const bool takeA = hA < hB;  // exhausted sides read as ~0 (above every real word)
+                ow[q] = takeA ? hA : hB;
+                if (takeA) hA = ++ia < a1 ? wd[ia] : ~0ull;
+                else hB = ++ib < b1 ? wd[ib] : ~0ull;
             }
         }
         __syncthreads();  // every thread has read its inputs of this round
 #pragma unroll
         for (int q = 0; q < PER; ++q)
-            if (o0 + q < n) {
-                key16[o0 + q] = ok[q];
-                mi[o0 + q] = (uint16_t)ox[q];
-            }
+            if (o0 + q < n) wd[o0 + q] = ow[q];
         __syncthreads();
+    }
+    if (!rounds) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) ow[q] = o0 + q < n ? wd[o0 + q] : ~0ull;
     }
 }
 
-// Groups of positions with one 16-byte prefix are in id order after tile_sort_wave. That is the
-// merge order when the group's keys are equal (one length and, past 16 bytes, one fingerprint: the
-// fingerprint shortcut's "equal"); a group with two lengths or two fingerprints (or any key past 16
-// bytes in exact mode) is re-sorted with the full compare (elem_less_fp), by one thread per group.
-__device__ void tile_fix_ties(const ulong2* key16, uint16_t* mi, uint32_t n, const uint64_t* el_c,
-                              const uint64_t* el_fp, const uint64_t* kfp, const uint64_t* rec_addr, uint32_t* s_cx) {
+// fingerprint of element e's key bytes past 16 (O.key_fp by record index), 0 in exact mode
+__device__ __forceinline__ uint64_t el_fp_of(const uint64_t* kfp, uint64_t c) {
+    return kfp ? kfp[(uint32_t)c] : 0;
+}
+// the full element order (elem_less_fp over key16 / el_c by id, fingerprints from global memory)
+__device__ __forceinline__ bool el_less_full(const ulong2* key16, const uint64_t* el_c, const uint64_t* kfp,
+                                             const uint64_t* rec_addr, uint32_t a, uint32_t b) {
+    const ulong2 ka = key16[a], kb = key16[b];
+    const uint64_t ca = el_c[a], cb = el_c[b];
+    if (ka.x != kb.x) return ka.x < kb.x;
+    if (ka.y != kb.y) return ka.y < kb.y;
+    return elem_less_fp(kfp != nullptr, el_fp_of(kfp, ca), rec_addr, ka.x, ka.y, ca, kb.x, kb.y, cb,
+                        el_fp_of(kfp, cb));
+}
+// two elements with the same key under the fingerprint shortcut (their id order is the merge order)
+__device__ __forceinline__ bool el_same_key(const ulong2* key16, const uint64_t* el_c, const uint64_t* kfp,
+                                            uint32_t a, uint32_t b) {
+    const ulong2 ka = key16[a], kb = key16[b];
+    const uint32_t la = (uint32_t)(el_c[a] >> 32), lb = (uint32_t)(el_c[b] >> 32);
+    if (ka.x != kb.x || ka.y != kb.y || la != lb) return false;
+    return la <= 16 || (kfp && el_fp_of(kfp, el_c[a]) == el_fp_of(kfp, el_c[b]));
+}
+
+// Groups of equal 52-bit windows after tile_merge_runs (wd by position) whose keys are not all one
+// key: re-sorted by the full compare, one thread per group (insertion sort; groups hold a handful of
+// elements). Returns false when such a group is larger than 64: the caller then merges the tile
+// exactly. The rare path: the caller found a mixed pair first.
+__device__ bool tile_fix_groups(const ulong2* key16, const uint64_t* wd, uint16_t* mi, uint32_t n, const uint64_t* el_c,
+                                const uint64_t* kfp, const uint64_t* rec_addr, uint32_t* s_big) {
     constexpr int PER = 4;
     const uint32_t o0 = threadIdx.x * PER;
-    if (threadIdx.x == 0) *s_cx = 0;
-    __syncthreads();
-    bool cx = false;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const uint32_t i = o0 + q;
-        if (i > 0 && i < n) {
-            const ulong2 a = key16[i - 1], b = key16[i];
-            if (a.x == b.x && a.y == b.y) {
-                const uint32_t p = mi[i - 1], e = mi[i];
-                const uint32_t kp = (uint32_t)(el_c[p] >> 32), ke = (uint32_t)(el_c[e] >> 32);
-                cx |= kp != ke || (ke > 16 && (!kfp || el_fp[p] != el_fp[e]));
-            }
-        }
-    }
-    if (cx) *s_cx = 1;
-    __syncthreads();
-    if (!*s_cx) return;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t g0 = o0 + q;
         if (g0 + 1 >= n) continue;
-        const ulong2 k = key16[g0];
-        if (g0 > 0 && key16[g0 - 1].x == k.x && key16[g0 - 1].y == k.y) continue;  // not a group start
+        const uint64_t gw = wd[g0] >> WD_ID;
+        if (g0 > 0 && (wd[g0 - 1] >> WD_ID) == gw) continue;  // not a group start
         uint32_t g1 = g0 + 1;
-        while (g1 < n && key16[g1].x == k.x && key16[g1].y == k.y) ++g1;
-        if (g1 - g0 < 2) continue;
+        bool mixed = false;
+        while (g1 < n && (wd[g1] >> WD_ID) == gw) {
+            mixed |= !el_same_key(key16, el_c, kfp, mi[g1 - 1], mi[g1]);
+            ++g1;
+        }
+        if (!mixed) continue;
+        if (g1 - g0 > 64) {
+            *s_big = 1;  // the exact merge takes the whole tile
+            continue;
+        }
         for (uint32_t i = g0 + 1; i < g1; ++i) {  // insertion sort of the group's ids
             const uint32_t e = mi[i];
             uint32_t j = i;
-            while (j > g0) {
-                const uint32_t p = mi[j - 1];
-                if (!elem_less_fp(kfp != nullptr, el_fp[e], rec_addr, k.x, k.y, el_c[e], k.x, k.y, el_c[p], el_fp[p]))
-                    break;
-                mi[j] = (uint16_t)p;
+            while (j > g0 && el_less_full(key16, el_c, kfp, rec_addr, e, mi[j - 1])) {
+                mi[j] = mi[j - 1];
                 --j;
             }
             mi[j] = (uint16_t)e;
         }
     }
     __syncthreads();
+    return *s_big == 0;
+}
+
+// The exact merge of a tile (any keys): pairwise merge-path rounds over the streams' segments (cb:
+// segment starts, k + 1 entries, scratch cbn) with the full compare, elements by id through mi.
+// Rare: a tile whose keys share more than the sort word sees (tile_fix_groups' large groups).
+__device__ void tile_merge_exact(const ulong2* key16, const uint64_t* el_c, const uint64_t* kfp, const uint64_t* rec_addr,
+                                 uint16_t* mi, uint32_t n, uint32_t k, uint32_t* cb, uint32_t* cbn) {
+    constexpr int PER = 4;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) mi[i] = (uint16_t)i;
+    __syncthreads();
+    const uint32_t o0 = threadIdx.x * PER;
+    uint32_t m = k;
+    while (m > 1) {
+        const uint32_t mp = (m + 1) >> 1;
+        uint32_t ox[PER];
+        uint32_t pos = o0, ia = 0, a1 = 0, ib = 0, b1 = 0;
+        bool setup = true;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            ox[q] = 0;
+            if (pos < n) {
+                if (setup || pos >= b1) {
+                    uint32_t lo = 0, hi = mp;  // pair p with cb[2p] <= pos
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (cb[2 * mid] <= pos) lo = mid;
+                        else hi = mid;
+                    }
+                    const uint32_t a0 = cb[2 * lo];
+                    a1 = cb[2 * lo + 1 < m ? 2 * lo + 1 : m];
+                    b1 = cb[2 * lo + 2 < m ? 2 * lo + 2 : m];
+                    const uint32_t lenA = a1 - a0, lenB = b1 - a1, d = pos - a0;
+                    uint32_t l = d > lenB ? d - lenB : 0, h = d < lenA ? d : lenA;
+                    while (l < h) {
+                        const uint32_t mid = (l + h) >> 1;
+                        if (el_less_full(key16, el_c, kfp, rec_addr, mi[a0 + mid], mi[a1 + d - mid - 1])) l = mid + 1;
+                        else h = mid;
+                    }
+                    ia = a0 + l;
+                    ib = a1 + (d - l);
+                    setup = false;
+                }
+                const bool takeA =
+                    ia < a1 && (ib >= b1 || el_less_full(key16, el_c, kfp, rec_addr, mi[ia], mi[ib]));
+                ox[q] = takeA ? mi[ia++] : mi[ib++];
+                ++pos;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; ++q)
+            if (o0 + q < n) mi[o0 + q] = (uint16_t)ox[q];
+        for (uint32_t p = threadIdx.x; p <= mp; p += blockDim.x) cbn[p] = p < mp ? cb[2 * p] : cb[m];
+        __syncthreads();
+        uint32_t* t = cb;
+        cb = cbn;
+        cbn = t;
+        m = mp;
+    }
 }
 
 #if SKV_TILE_PROF
@@ -1326,13 +1370,11 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     uint64_t* el_fp = el_c + TILE_CAP;
     uint16_t* mi = (uint16_t*)(el_fp + TILE_CAP);
     uint16_t* posof = mi + TILE_CAP;  // after the rounds: merged position of each element
-    // level-0 tiles outside heap-order mode: hp / el_lo hold {hp, lo} by position instead (key16),
-    // sorted by tile_sort_wave
+    // level-0 tiles outside heap-order mode (tile_sort_words): hp / el_lo hold {hp, lo} by id instead
+    // (key16), el_fp the sort words by position (wd; fingerprints are read from O.key_fp on ties)
     ulong2* key16 = (ulong2*)smem;
-#ifndef SKV_TILE_WAVE
-#define SKV_TILE_WAVE 1
-#endif
-    const bool wpath = SKV_TILE_WAVE && L0 && O.act_hi == nullptr;
+    uint64_t* wd = el_fp;
+    const bool wpath = L0 && O.act_hi == nullptr;
     uint32_t* cbA = (uint32_t*)(posof + TILE_CAP);
     uint32_t* cbB = cbA + (k + 1);
     uint64_t* ws = (uint64_t*)(((uintptr_t)(cbB + (k + 1)) + 15) & ~(uintptr_t)15);
@@ -1348,7 +1390,11 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     }
     uint64_t t = blockIdx.x;
     if (L0) {  // level 0 tiles take tickets in start order (tile_lookback's progress guarantee)
-        if (threadIdx.x == 0) s_tk = atomicAdd(O.tcounter, 1u);
+        if (threadIdx.x == 0) {
+            s_tk = atomicAdd(O.tcounter, 1u);
+            s_flag[24] = s_flag[25] = 0;  // mixed groups / a group too large (tile_fix_groups)
+            s_flag[26] = s_flag[27] = 0;  // the common-prefix OR (tile_sort_words' window)
+        }
         __syncthreads();
         t = s_tk;
     }
@@ -1385,7 +1431,7 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     // Thread owns elements e = threadIdx.x + u*TILE_THREADS for the loads (payload stays in
     // registers) and output positions threadIdx.x * PER + q in the merge rounds.
     constexpr int PER = TILE_CAP / TILE_THREADS;
-    uint64_t rh[PER], rc[PER], raddr[PER];
+    uint64_t rh[PER], rl[PER], rc[PER], raddr[PER];
     uint32_t rpos[PER], rmeta[PER];
     const uint64_t* kfp = L0 ? O.key_fp : nullptr;
 #pragma unroll
@@ -1404,14 +1450,15 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                 raddr[u] = (O.pay_addr ? O.pay_addr : rec_addr)[pos];  // coalesced here, not gathered later
                 if (kfp) fp = kfp[pos];
             }
+            rl[u] = lo;
             if (wpath) {
                 key16[e] = make_ulong2(rh[u], lo);
             } else {
                 hp[e] = rh[u];
                 el_lo[e] = lo;
+                el_fp[e] = fp;
             }
             el_c[e] = rc[u];
-            el_fp[e] = fp;
             mi[e] = (uint16_t)e;
         }
     }
@@ -1428,10 +1475,53 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                   : elem_less(rec_addr, ha, el_lo[xa], el_c[xa], hb, el_lo[xb], el_c[xb]);
     };
     if (wpath) {
-        tile_sort_wave(key16, mi, n);
-        tile_fix_ties(key16, mi, n, el_c, el_fp, kfp, rec_addr, s_flag + 30);
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) posof[mi[i]] = (uint16_t)i;
+        // c = the bytes every key of the tile shares (<= 8): the OR of each key's first 8 bytes XOR
+        // element 0's, over the block
+        const uint64_t k0 = key16[0].x;
+        uint64_t dh = 0;
+#pragma unroll
+        for (int u = 0; u < PER; ++u)
+            if (threadIdx.x + u * TILE_THREADS < n) dh |= rh[u] ^ k0;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) dh |= __shfl_xor(dh, d, 64);
+        if ((threadIdx.x & 63) == 0 && dh) {
+            atomicOr(s_flag + 26, (uint32_t)(dh >> 32));
+            atomicOr(s_flag + 27, (uint32_t)dh);
+        }
         __syncthreads();
+        const uint64_t D = ((uint64_t)s_flag[26] << 32) | s_flag[27];
+        const uint32_t cpx = D ? (uint32_t)__builtin_clzll(D) >> 3 : 8u;
+        tile_sort_words(key16, wd, n, cpx);
+        TPROF(8);
+        uint64_t ow[4];
+        tile_merge_runs(wd, n, ow);
+        TPROF(9);
+        // epilogue from registers: ids by position, positions by id, and the pairs of equal windows
+        // (one LDS read: the word before this thread's first); a pair whose keys differ sends the
+        // tile to tile_fix_groups
+        constexpr uint32_t IDM = (1u << WD_ID) - 1;
+        const uint32_t o0 = threadIdx.x * 4;
+        uint64_t prevw = o0 > 0 && o0 < n ? wd[o0 - 1] : ~0ull;
+        bool mixed = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (o0 + q < n) {
+                const uint32_t id = (uint32_t)(ow[q] & IDM);
+                mi[o0 + q] = (uint16_t)id;
+                posof[id] = (uint16_t)(o0 + q);
+                if (prevw != ~0ull && (prevw >> WD_ID) == (ow[q] >> WD_ID))
+                    mixed |= !el_same_key(key16, el_c, kfp, (uint32_t)(prevw & IDM), id);
+                prevw = ow[q];
+            }
+        }
+        if (mixed) s_flag[24] = 1;
+        __syncthreads();
+        if (s_flag[24]) {  // rare: re-sort the mixed groups (or the whole tile), then positions again
+            if (!tile_fix_groups(key16, wd, mi, n, el_c, kfp, rec_addr, s_flag + 25))
+                tile_merge_exact(key16, el_c, kfp, rec_addr, mi, n, k, cbA, cbB);
+            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) posof[mi[i]] = (uint16_t)i;
+            __syncthreads();
+        }
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const uint32_t e = threadIdx.x + u * TILE_THREADS;
@@ -1561,14 +1651,15 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                 if (i > 0) first = act_key_cmp(O, (uint32_t)el_c[mi[i - 1]], (uint32_t)c) != 0;
             } else if (i > 0) {
                 const uint32_t p = mi[i - 1];
-                if (wpath ? key16[i - 1].x == key16[i].x : hp[i - 1] == hp[i]) {
-                    const uint64_t lp = wpath ? key16[i - 1].y : el_lo[p], le = wpath ? key16[i].y : el_lo[e];
+                if (wpath ? key16[p].x == key16[e].x : hp[i - 1] == hp[i]) {
+                    const uint64_t lp = wpath ? key16[p].y : el_lo[p], le = wpath ? key16[e].y : el_lo[e];
                     const uint64_t cp = el_c[p];
                     int kc = lp != le ? (lp < le ? -1 : 1) : 0;
                     const uint32_t kp = (uint32_t)(cp >> 32), ke = (uint32_t)(c >> 32);
                     if (!kc && kp > 16 && ke > 16) {
                         if (kfp) {
-                            const int same = kp == ke && el_fp[p] == el_fp[e];
+                            const int same = kp == ke && (wpath ? el_fp_of(kfp, cp) == el_fp_of(kfp, c)
+                                                                : el_fp[p] == el_fp[e]);
                             kc = same ? 0 : 1;
                             if (same) vmask |= 1u << q;
                         } else {

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/xchk tools/ubench/xshfl_check.hip 2>/dev/null
 timeout -k 10 60 /tmp/xchk || { echo "xshfl check failed"; exit 1; }
 timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m "gpu and not slow" \
-  tests/test_gpu_parity.py tests/test_gpu_kat.py tests/test_gpu_split.py tests/test_gpu_scan.py tests/test_gpu_search.py \
+  tests/test_gpu_parity.py tests/test_gpu_kat.py tests/test_gpu_split.py tests/test_gpu_scan.py tests/test_gpu_search.py tests/test_gpu_shard_split.py \
   > "$O/pytest.log" 2>&1; rc=$?; tail -5 "$O/pytest.log"; [ $rc -ne 0 ] && exit 1
 for c in ${CONFIGS:-3 3F}; do
   extra="--steps 10 --warmup 2"; [ "$c" = 3F ] && extra="--steps 5 --warmup 1"
