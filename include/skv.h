@@ -38,7 +38,7 @@ extern "C" {
 #define SKV_ABI_VERSION 9  /* 2: skv_timings gained sorted, fp_rerun; 3: host_parts; 4: skv_scan_runs;
                               5: skv_timings.span_parse (was reserved); 6: skv_timings.wal_stage;
                               7: skv_ctx_host_info; 8: skv_compact_split; 9: skv_host_plan,
-                              skv_split_deal */
+                              skv_split_deal, skv_test_option */
 
 typedef struct skv_ctx skv_ctx;
 
@@ -189,6 +189,22 @@ int skv_host_plan(const char* sysfs_root, const char* pci_bus_id, int n_devices,
                   int* pool_threads, int* cpus, int max_cpus);
 int skv_split_deal(const int* ctx_device, uint32_t n_ctx, uint64_t n_parts, uint32_t* ctx_of_part,
                    int64_t* h2d_after);
+
+/*
+ * Test hooks, for the parity suite only: they force the rare paths a call would otherwise take only
+ * on rare data (the general path where the fused one applies, the record sort at small fan-in, a
+ * fingerprint collision and its exact rerun, small parse chunks, the exact WAL stage, kernel ingest,
+ * an injected failure after a pipeline part, split modes, sort search variants, a small grid's worth
+ * of fused tile slots). Names: SKV_FUSED, SKV_SORT, SKV_FP_TEST, SKV_FP_GATHER, SKV_CHUNK_BYTES,
+ * SKV_WAL_FUSED, SKV_INGEST, SKV_TEST_FAIL_PART, SKV_PAR_COPY_MIN, SKV_HI_STEP, SKV_SPLIT,
+ * SKV_SPLIT_DEBUG, SKV_SPLIT_SEG, SKV_SPLIT_NC, SKV_SORT_TWO_PASS, SKV_SB_NT, SKV_SB_GMAX,
+ * SKV_FX_TAIL_SLOTS. value NULL clears one hook, name NULL clears every hook; an unknown name is
+ * SKV_E_INVALID_ARG. Process-wide. The library reads none of them from the environment; the only
+ * environment variables it reads are the host-pipeline thresholds (SKV_HOST_PIPE, SKV_HOST_PIPE_MIN,
+ * SKV_HOST_PARTS, SKV_SPLIT_PARTS), the host pool size (SKV_HOST_THREADS) and two profiling
+ * switches (SKV_HOST_TRACE, SKV_SORT_PROF_PRINT).
+ */
+int skv_test_option(const char* name, const char* value);
 
 /*
  * Host-memory entry point: the shape skyvault's jobs have (Bytes in from get_run,

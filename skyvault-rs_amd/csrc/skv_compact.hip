@@ -80,11 +80,10 @@ static int wal_fused(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d
     HIPCHK(hipMemsetAsync(words, 0, 16, st));
     HIPCHK(hipMemsetAsync(tail, 0, 64, st));
     mark(ctx, PH_CHAIN);
-    const char* fe = getenv("SKV_WAL_FUSED");
     // in a key-range part every key must carry the canonical "{id}." prefix: the cuts are canonical
     // prefixes, so only then does no table straddle two parts (WAL_STRICT_CANON)
     launch_wal_fused(st, d_K, R, m_src, m_P, m_Dp, d_out, tstate, words, words + 1, tl, words + 2, WF_TCAP, tail,
-                     (fe && fe[0] == '2' ? 2u : 0u) | (job.part ? WAL_STRICT_CANON : 0u), S, m_rec);
+                     job.part ? WAL_STRICT_CANON : 0u, S, m_rec);
     HIPCHK(hipGetLastError());
     mark(ctx, PH_GATHER);
     uint8_t* hp = (uint8_t*)pinned(ctx, 128 + WF_GUESS * sizeof(WalTStart));
@@ -147,12 +146,10 @@ int wal_stage(skv_ctx* ctx, const Job& job, uint64_t R, const uint64_t* d_K, con
                      const uint32_t* rec_klen, const uint32_t* fp_bad, const HeapRes* heap, skv_result** out,
                      const SElem* sorted) {
     hipStream_t st = ctx->stream;
-    const char* fe = getenv("SKV_WAL_FUSED");
+    const char* fe = test_opt("SKV_WAL_FUSED");
     if (!heap && !(fe && fe[0] == '0') && R > 0) {
         // sorted: the record sort's output, its elements' true key prefixes by sorted position (m_rec)
-        const char* pe = getenv("SKV_WAL_PREFIX");
-        const int rc = wal_fused(ctx, job, R, d_K, m_src, m_P, m_Dp, fp_bad, out,
-                                 pe && pe[0] == '0' ? nullptr : sorted, m_rec);
+        const int rc = wal_fused(ctx, job, R, d_K, m_src, m_P, m_Dp, fp_bad, out, sorted, m_rec);
         if (rc != RC_DECLINED) {
             ctx->timings.wal_stage = 1;
             return rc;
@@ -384,7 +381,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // length (tools/stage_probe.py): 59 GiB 16/32/64 KiB 30.3/26.4/25.2 ms; 3.7 GiB 4/16/32/64 KiB
     // 3.59/2.27/2.14/2.34; 0.23 GiB 4/8/16 KiB 0.50/0.49/0.53; 0.06 GiB 4/16 KiB 0.38/0.47
     uint64_t chunk = CHUNK;
-    if (const char* ce = getenv("SKV_CHUNK_BYTES"))  // slot offsets are 16-bit: at most 64 KiB
+    if (const char* ce = test_opt("SKV_CHUNK_BYTES"))  // slot offsets are 16-bit: at most 64 KiB
         chunk = std::min<uint64_t>(65536, std::max<uint64_t>(CHUNK, strtoull(ce, nullptr, 10)));
     else
         while (chunk < 65536 && job.in_bytes / (2 * chunk) >= (1ull << 16)) chunk *= 2;
@@ -393,10 +390,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // one run per stream in a monotone seq_no order, past the splitter merge's fan-in (config 5's
     // shape, the device-table calls below): the run table is built on the device (k_run_info) from
     // the caller-order pointer / length arrays, and the host table only if a host path needs it
-    const char* hre = getenv("SKV_HOST_RUNS");  // 1: the host run table always
     const bool runs_dev = k > (uint32_t)TILE_TARGET / 2 && job.one_run_each && job.caller_order != 0 && !job.scan &&
-                          !job.search && !job.batch && !job.part && !getenv("SKV_HOST_TABLES") &&
-                          !(hre && hre[0] == '1');
+                          !job.search && !job.batch && !job.part;
     bool host_runs_built = false;
     auto build_host_runs = [&]() {  // blocks of streams (rank order) on host threads: runs and chunks before each block, then fill
         runs.resize(job.run_ptr.size());
@@ -618,7 +613,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // Made where the fixed-stride parse decides whether to write key fingerprints, and kept: a parse
     // that skipped them (fp_skipped) commits the call to the sort, which merges on dense ranks -- the
     // splitter merge would read unwritten fingerprints (a scan's key filter can shrink R in between).
-    const char* sort_env = getenv("SKV_SORT");
+    const char* sort_env = test_opt("SKV_SORT");
     auto sort_by_fan_in = [&](uint64_t nrec) {
         return (k > (uint32_t)TILE_TARGET / 2 && nrec > (uint64_t)TILE_CAP) || (sort_env && sort_env[0] == '1') ||
                job.batch;
@@ -632,7 +627,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // One run per STREAM, not n_runs == k: an empty stream beside a two-member stream also gives
     // n_runs == k, and the stream bases below are the run record bases.
     const bool try_dev_tables = k > (uint32_t)TILE_TARGET / 2 && n_runs == k && job.one_run_each && !job.scan && !job.search &&
-                                !job.batch && !job.part && !getenv("SKV_HOST_TABLES");
+                                !job.batch && !job.part;
     if (try_dev_tables) {
         uint64_t* d_cnt = dbuf<uint64_t>(ctx, "run_cnt", n_runs + 1);
         uint32_t* d_rfl = dbuf<uint32_t>(ctx, "run_tflags", 4);
@@ -661,8 +656,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             fp_skipped = will_sort;
             // the record sort follows: the parse writes the sort's elements itself (no k_sort_load
             // pass; the record arrays are filled from them only if a key decrease needs them)
-            const char* sde = getenv("SKV_SORT_DIRECT");
-            e_direct = will_sort && !job.batch && !job.scan && !job.search && !(sde && sde[0] == '0');
+            e_direct = will_sort && !job.batch && !job.scan && !job.search;
             launch_parse_fixed(st, d_runs, n_runs, d_fmt, d_broken, d_recb, R, rec_addr, rec_hi, rec_lo, rec_klen,
                                rec_meta, d_flags, d_stream_base, d_first_dec, will_sort ? nullptr : rec_fp,
                                dbuf<uint32_t>(ctx, "wave_run", (R + 63) / 64 + 1),
@@ -743,7 +737,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
                 });
             // one record size and one key length <= 16 everywhere: the fused stride path
             const RunFmt f0 = hf[0];
-            const char* fenv = getenv("SKV_FUSED");
+            const char* fenv = test_opt("SKV_FUSED");
             if (allow_deferred && uniform && !job.batch && !job.search && !job.scan && !job.part &&
                 !(job.flags & SKV_SPLIT_BY_TABLE) &&
                 !(fenv && fenv[0] == '0') &&
@@ -813,9 +807,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         alloc_records();
         // the order check fused into k_emit (+ k_chunk_order at chunk edges) when every record comes from
         // it (fixed-stride runs' records, from k_emit_fixed<false>, are not checked there; a writer batch is
-        // unsorted by definition; SKV_EMIT_ORDER=0: k_order_check)
-        const char* eo = getenv("SKV_EMIT_ORDER");
-        const bool emit_order = !any_fixed && !job.batch && !(eo && eo[0] == '0');
+        // unsorted by definition)
+        const bool emit_order = !any_fixed && !job.batch;
         launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, any_fixed ? R : 0,
                     rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad, ch_slots, slot_cap, chunk,
                     ch_end, emit_order ? d_stream_base : nullptr, emit_order ? d_first_dec : nullptr);
@@ -1069,10 +1062,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             } else {
                 // Without the Delete filter (and outside writer batches and scans) the survivors of the
                 // one sorted list are the first record of each key: the sort's store emits the merged
-                // arrays itself and the level-0 merge tiles are skipped (SKV_SORT_MERGED=0: the tiles)
-                const char* sme = getenv("SKV_SORT_MERGED");
-                const bool direct = !(job.flags & SKV_DROP_TOMBSTONES) && !job.batch && !job.scan &&
-                                    !(sme && sme[0] == '0');
+                // arrays itself and the level-0 merge tiles are skipped
+                const bool direct = !(job.flags & SKV_DROP_TOMBSTONES) && !job.batch && !job.scan;
                 SortMerged M{};
                 if (direct) {
                     M.m_rec = dbuf<uint32_t>(ctx, "m_rec", R + 1);
@@ -1120,14 +1111,13 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // SKV_HI_STEP=f: levels >= 2 (they only pick splitters for the sample sorts) at an f times
     // coarser step. Measured at config 3 with f = 2: one sample level fewer, but the merge phase
     // 4.02 vs 3.26 ms (the level-1 sample tiles lose their balance), so the default is 1.
-    const char* hse = getenv("SKV_HI_STEP");
+    const char* hse = test_opt("SKV_HI_STEP");
     const uint64_t hi_f = hse ? std::max<uint64_t>(1, strtoull(hse, nullptr, 10)) : 1;
     // Level 1 (the level-0 tiles' splitters) at twice the step from 128 lists on: a tile's size
     // spreads by ~sqrt(k) x step / 2.4 records around TILE_TARGET, which at k >= 128 stays under
     // 1/4.6 of the TILE_CAP margin, and half the samples halve their sort (3F merge 27.3 -> 25.7 ms,
-    // config 3 2.22 -> 1.92 ms; a step of 3 unbalanced the tiles: 31.4 ms). SKV_L1_STEP=f overrides.
-    const char* l1e = getenv("SKV_L1_STEP");
-    const uint64_t l1_f = l1e ? std::max<uint64_t>(1, strtoull(l1e, nullptr, 10)) : (km >= 128 ? 2 : 1);
+    // config 3 2.22 -> 1.92 ms; a step of 3 unbalanced the tiles: 31.4 ms).
+    const uint64_t l1_f = km >= 128 ? 2 : 1;
     while (lv.back().N > (uint64_t)TILE_CAP) {
         const Level& P = lv.back();
         Level L;
@@ -1174,7 +1164,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     const unsigned long long* verify_lo = nullptr;  // pairs before it verified beside the merge
     bool verify_pending = false;
     if (km > 1 && !ctx->exact_keys && !heap && !job.scan) {  // (the scan's filtered arrays carry no fingerprints)
-        const char* te = getenv("SKV_FP_TEST");
+        const char* te = test_opt("SKV_FP_TEST");
         if (te && te[0] == '1') {
             uint64_t* f = dbuf<uint64_t>(ctx, "rec_fp_test", R);
             HIPCHK(hipMemsetAsync(f, 0, R * 8, st));
@@ -1182,8 +1172,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         } else {
             key_fp = rec_fp;  // written by the emit kernels with the record arrays
         }
-        const char* ge = getenv("SKV_FP_GATHER");
-        if (!SKV_PAGE_GATHER && !(ge && ge[0] == '0') && !(job.flags & (SKV_SPLIT_BY_TABLE | SKV_DROP_TOMBSTONES)))
+        const char* ge = test_opt("SKV_FP_GATHER");
+        if (!(ge && ge[0] == '0') && !(job.flags & (SKV_SPLIT_BY_TABLE | SKV_DROP_TOMBSTONES)))
             m_dup = dbuf<uint64_t>(ctx, "m_dup", R + 1);
     }
     if (sorted_merged) {  // m_P / m_Dp: exclusive scans of the survivors' sizes / Delete bits
@@ -1269,40 +1259,10 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
             snprintf(nm, sizeof nm, "s%d_c", li); L.sc = O.oc = dbuf<uint64_t>(ctx, nm, L.N);
         }
         const uint32_t drop = (job.flags & SKV_DROP_TOMBSTONES) ? 1u : 0u;
-        // SKV_FP_PIECE_MIN=T: split level 0 from T tiles on (off by default: at 3F the verify beside
-        // the merge pieces slowed the merge by what it saved beside the gather, 89.6 vs 89.3 ms)
-        const char* pme = getenv("SKV_FP_PIECE_MIN");
-        const uint64_t piece_min = pme ? std::max<uint64_t>(1, strtoull(pme, nullptr, 10)) : ~0ull;
-        if (l0 && key_fp && T >= piece_min && T >= 4) {
-            // Level 0 in FP_PIECES launches (tickets continue across them): after each piece but
-            // the last, a one-lane kernel snapshots the pair count, and k_fp_verify checks that
-            // piece's pairs on the aux stream while the next piece merges; the last piece's pairs
-            // are checked beside the gather. Measured neutral: the verify's random record reads
-            // cost the LDS-bound merge about what they cost the gather.
-            constexpr int FP_PIECES = 4;
-            uint64_t* snap = dbuf<uint64_t>(ctx, "fp_vsnap", FP_PIECES);
-            ensure_aux(ctx);
-            uint64_t done = 0;
-            for (int p = 0; p < FP_PIECES; ++p) {
-                const uint64_t upto = T * (uint64_t)(p + 1) / FP_PIECES;
-                HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, cmp_klen, bounds, km, T, tile_base, rec_meta, cmp_addr,
-                                   drop, O, d_flags + 2, upto - done));
-                done = upto;
-                if (p + 1 < FP_PIECES) {
-                    launch_fx_publish(st, (const uint64_t*)O.vcount, snap + p);
-                    HIPCHK(hipEventRecord(ctx->aux_ev[0], st));
-                    HIPCHK(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_ev[0], 0));
-                    launch_fp_verify(ctx->aux_stream, p ? (const unsigned long long*)(snap + p - 1) : nullptr,
-                                     (const unsigned long long*)(snap + p), O.vpairs, R, fp_bad, 1024);
-                    verify_pending = true;
-                }
-            }
-            HIPCHK(hipEventRecord(ctx->aux_ev[1], ctx->aux_stream));
-            verify_lo = (const unsigned long long*)(snap + FP_PIECES - 2);
-        } else {
-            HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, cmp_klen, bounds, km, T, tile_base, rec_meta, cmp_addr, drop,
-                               O, d_flags + 2));
-        }
+        // (round 4-5 also split level 0 into pieces whose pairs k_fp_verify checked beside the next
+        // piece's merge: measured neutral at 3F, 89.6 vs 89.3 ms, and removed in round 6)
+        HIPCHK(launch_tile(st, l0, L.hi, L.lo, L.c, cmp_klen, bounds, km, T, tile_base, rec_meta, cmp_addr, drop, O,
+                           d_flags + 2));
         if (l0 && key_fp) verify_args = {O.vcount, O.vpairs};
         if (l0) T0 = T;
     }
@@ -1378,13 +1338,13 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     // candidates per window, runs per segment (tests shrink the window to exercise the stitch's walks)
     SplitBufs sp{};
     {
-        const char* mode = getenv("SKV_SPLIT");
+        const char* mode = test_opt("SKV_SPLIT");
         const bool serial = mode && !strcmp(mode, "serial");
         sp.segr = 16;
         sp.nc = 512;
         sp.min_runs = mode && !strcmp(mode, "par") ? 0 : 1024;
-        if (const char* e = getenv("SKV_SPLIT_NC")) sp.nc = (uint32_t)std::min<uint64_t>(8192, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
-        if (const char* e = getenv("SKV_SPLIT_SEG")) sp.segr = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
+        if (const char* e = test_opt("SKV_SPLIT_NC")) sp.nc = (uint32_t)std::min<uint64_t>(8192, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
+        if (const char* e = test_opt("SKV_SPLIT_SEG")) sp.segr = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
         const uint64_t M = job.max_run_size;
         if (!serial && M > 8 && R < 0xFFFFFFF0ull) {
             // runs of >= 8 records (the plan's gate) hold > 7/8 (max - 1) bytes each
@@ -1432,7 +1392,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         sync(ctx);
         job.carry->post_out(job.carry_part, hco[0], carry_e1 != 0);
     }
-    if (sp.nseg_cap && getenv("SKV_SPLIT_DEBUG")) {  // tests/test_gpu_split.py reads which split ran
+    if (sp.nseg_cap && test_opt("SKV_SPLIT_DEBUG")) {  // tests/test_gpu_split.py reads which split ran
         sync(ctx);
         SplitPlan pl;
         HIPCHK(hipMemcpy(&pl, sp.plan, sizeof(pl), hipMemcpyDeviceToHost));
@@ -1446,18 +1406,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
     const uint64_t total_rec_bytes = job.in_bytes;
     // a part of a pipelined host call writes into the call's shared output buffer (job.dev_out)
     uint8_t* d_out = job.dev_out ? job.dev_out : dbuf<uint8_t>(ctx, "out", total_rec_bytes + R + 16);
-#if SKV_PAGE_GATHER
-    {
-        const uint64_t max_out = total_rec_bytes + R + 16;
-        uint64_t* Dst = dbuf<uint64_t>(ctx, "g_dst", R + 1);
-        uint32_t* page_first = dbuf<uint32_t>(ctx, "g_page_first", max_out / PAGE_BYTES + 2);
-        launch_page_prep(st, d_K, d_nruns, run_b, m_P, seg_r0, Dst, page_first, R);
-        mark(ctx, PH_CHAIN);
-        launch_gather_pages(st, d_K, d_nruns, m_P, Dst, m_src, page_first, d_out, max_out);
-    }
-#else
     launch_gather(st, d_K, d_nruns, run_b, m_P, m_src, seg_r0, d_out, R, m_dup, fp_bad);
-#endif
     HIPCHK(hipGetLastError());
     mark(ctx, PH_GATHER);
     // ---- readback: summary + descriptors in one sync (descriptor count guessed from sizes) -------

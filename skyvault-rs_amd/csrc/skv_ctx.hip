@@ -233,9 +233,47 @@ DevHost& dev_host(int device) {  // created on first use, never torn down (like 
 
 int device_numa_node(int device) { return dev_host(device).numa; }
 
+// the test hooks' table (skv_test_option): fixed names, values copied in under a lock; test_opt hands
+// a caller a thread-local copy, so a hook set from another thread never tears a value being parsed
+namespace {
+struct TestOpt {
+    const char* name;
+    bool set;
+    char value[48];
+};
+std::mutex& test_opt_mu() {
+    static std::mutex mu;
+    return mu;
+}
+std::vector<TestOpt>& test_opts() {
+    static std::vector<TestOpt> t = [] {
+        std::vector<TestOpt> v;
+        for (const char* n : {"SKV_FUSED", "SKV_SORT", "SKV_FP_TEST", "SKV_FP_GATHER", "SKV_CHUNK_BYTES",
+                              "SKV_WAL_FUSED", "SKV_INGEST", "SKV_TEST_FAIL_PART", "SKV_PAR_COPY_MIN", "SKV_HI_STEP",
+                              "SKV_SPLIT", "SKV_SPLIT_DEBUG", "SKV_SPLIT_SEG", "SKV_SPLIT_NC", "SKV_SORT_TWO_PASS",
+                              "SKV_SB_NT", "SKV_SB_GMAX", "SKV_FX_TAIL_SLOTS"})
+            v.push_back(TestOpt{n, false, {}});
+        return v;
+    }();
+    return t;
+}
+}  // namespace
+const char* test_opt(const char* name) {
+    thread_local char buf[8][48];
+    thread_local unsigned next = 0;
+    std::lock_guard<std::mutex> g(test_opt_mu());
+    for (const TestOpt& o : test_opts()) {
+        if (strcmp(o.name, name)) continue;
+        if (!o.set) return nullptr;
+        char* b = buf[next++ & 7];
+        memcpy(b, o.value, sizeof o.value);
+        return b;
+    }
+    return nullptr;
+}
+
 hipError_t host_alloc_near(int device, void** p, size_t bytes, unsigned flags) {
-    const char* ne = getenv("SKV_NUMA");
-    const int node = device >= 0 && !(ne && ne[0] == '0') ? dev_host(device).numa : -1;
+    const int node = device >= 0 ? dev_host(device).numa : -1;
     if (node < 0 || node >= 1024) return hipHostMalloc(p, bytes, flags);
     // prefer the GPU's node for this thread while the pages are allocated (and pinned), then put the
     // thread's own policy back; hipHostMallocNumaUser makes the allocation follow it
@@ -275,7 +313,7 @@ void par_exec(unsigned nb, void (*run)(void*, unsigned), void* arg) {
 
 // host copy into pinned staging; large tables (10^6-run calls: tens of MB) on the host pool
 void stage_copy(void* dst, const void* src, size_t bytes) {
-    const char* pe = getenv("SKV_PAR_COPY_MIN");  // tests: split small tables too
+    const char* pe = test_opt("SKV_PAR_COPY_MIN");  // tests: split small tables too
     const size_t kPar = pe ? (size_t)strtoull(pe, nullptr, 10) : (8u << 20);
     const unsigned nt = dev_host(skv_tl_device).threads;
     if (bytes < kPar || nt < 2) {
@@ -668,6 +706,23 @@ int skv_ctx_set_profiling(skv_ctx* ctx, int enable) {
     if (!ctx) return SKV_E_INVALID_ARG;
     ctx->profiling = enable != 0;
     return SKV_OK;
+}
+
+int skv_test_option(const char* name, const char* value) {
+    if (!name) {  // clear every hook
+        std::lock_guard<std::mutex> g(test_opt_mu());
+        for (TestOpt& o : test_opts()) o.set = false;
+        return SKV_OK;
+    }
+    std::lock_guard<std::mutex> g(test_opt_mu());
+    for (TestOpt& o : test_opts()) {
+        if (strcmp(o.name, name)) continue;
+        if (value && strlen(value) >= sizeof o.value) return SKV_E_INVALID_ARG;
+        if (value) memcpy(o.value, value, strlen(value) + 1);
+        o.set = value != nullptr;
+        return SKV_OK;
+    }
+    return SKV_E_INVALID_ARG;
 }
 
 int skv_host_plan(const char* sysfs_root, const char* pci_bus_id, int n_devices, int hw_threads, int* numa_node,

@@ -16,50 +16,24 @@
 
 namespace skv {
 
-#ifndef SKV_CHUNK
 #define SKV_CHUNK 4096
-#endif
 constexpr uint64_t CHUNK = SKV_CHUNK;     // bytes of run body per speculative walk lane
-#ifndef SKV_TILE_CAP
 #define SKV_TILE_CAP 4096
 #define SKV_TILE_TARGET 3072
 #define SKV_TILE_THREADS 1024
-#endif
 constexpr int TILE_CAP = SKV_TILE_CAP;          // max elements a merge tile sorts in LDS
 constexpr int TILE_TARGET = SKV_TILE_TARGET;    // target elements per merge tile
 constexpr int TILE_THREADS = SKV_TILE_THREADS;
-#ifndef SKV_GATHER_SEG
 #define SKV_GATHER_SEG 256
-#endif
 constexpr int GATHER_SEG = SKV_GATHER_SEG;      // surviving records per gather workgroup
-#ifndef SKV_GATHER_THREADS
 #define SKV_GATHER_THREADS SKV_GATHER_SEG
-#endif
 constexpr int GATHER_THREADS = SKV_GATHER_THREADS;  // >= GATHER_SEG: one lane per record in the setup
 static_assert(SKV_GATHER_THREADS >= SKV_GATHER_SEG && SKV_GATHER_THREADS % 64 == 0, "gather block shape");
 constexpr int GATHER_TBL = 23 * SKV_GATHER_SEG; // output 16-byte blocks per gather workgroup with a direct piece table
-#ifndef SKV_GATHER_U
 #define SKV_GATHER_U 2                   // output blocks per lane in flight in k_gather
-#endif
-#ifndef SKV_GATHER_WAVES
 #define SKV_GATHER_WAVES 8               // k_gather register budget: waves per SIMD (64 VGPRs at 8)
-#endif
 #ifndef SKV_TILE_PROF
 #define SKV_TILE_PROF 0                  // 1: k_tile<true> accumulates per-phase times (diagnostic builds)
-#endif
-#ifndef SKV_PAGE_U
-#define SKV_PAGE_U 4                     // page gather: 16-byte output blocks per lane
-#endif
-#ifndef SKV_PAGE_WAVES
-#define SKV_PAGE_WAVES 5                 // k_gather_pages register budget (waves per SIMD)
-#endif
-#ifndef SKV_PAGE_GATHER
-#define SKV_PAGE_GATHER 0                // 1: page gather (k_page_prep + k_gather_pages), 0: segment gather
-#endif
-constexpr int PAGE_U = SKV_PAGE_U;
-constexpr uint64_t PAGE_BYTES = 16ull * 256 * SKV_PAGE_U;
-#ifndef SKV_GATHER_NT
-#define SKV_GATHER_NT 1                  // 1: non-temporal output stores (written once, never re-read)
 #endif
 constexpr uint32_t NO_POS32 = 0xFFFFFFFFu;
 constexpr uint64_t NO_POS = ~0ull;
@@ -176,15 +150,9 @@ struct TileOut {
 
 // Fused stride path (skv_stride.hip): every input record is a Put of one size S with one key
 // length K <= 16, so record addresses, output offsets and the greedy split are arithmetic.
-#ifndef SKV_FX_THREADS
 #define SKV_FX_THREADS 512
-#endif
-#ifndef SKV_FX_U
 #define SKV_FX_U 2                       // output blocks per lane per batch in the fused copy (two batches in flight)
-#endif
-#ifndef SKV_FX_CAP
 #define SKV_FX_CAP 2048                  // 2048: 63 VGPRs, 4 workgroups per CU (4096: 91 VGPRs, 2 per CU; 3 % slower end to end)
-#endif
 constexpr int FX_HSLOTS = 2 * SKV_FX_CAP;  // distinct-key hash slots per fused tile (load <= 1/2)
 constexpr int FX_CAP = SKV_FX_CAP;       // max records per fused tile
 constexpr int FX_TARGET = FX_CAP / 4 * 3;  // target records per fused tile (splitter spacing)
@@ -251,13 +219,9 @@ struct SElem {
 };
 constexpr int SORT_CAP = 2048;           // elements a bucket sorts in LDS
 constexpr int SORT_THREADS = 256;
-#ifndef SKV_SORT_EVERY
 #define SKV_SORT_EVERY 48
-#endif
 constexpr uint64_t SORT_EVERY = SKV_SORT_EVERY;  // one sample per SORT_EVERY elements
-#ifndef SKV_SORT_OV
 #define SKV_SORT_OV 16
-#endif
 constexpr uint64_t SORT_OV = SKV_SORT_OV;  // samples per bucket (bucket target SORT_EVERY * SORT_OV = 768)
 
 // Batched run lookups (skv_search.hip): same layout and codes as skv_lookup / SKV_LOOKUP_* /

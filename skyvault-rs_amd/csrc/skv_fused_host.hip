@@ -90,9 +90,8 @@ FxArgs fx_launch(skv_ctx* ctx, uint32_t k, uint32_t n_runs, const RunInfo* d_run
     // drains in half a tile time (SKV_FX_TAIL=0: uniform tiles)
     uint64_t T1 = T0, m2 = m0;
     {
-        const char* te = getenv("SKV_FX_TAIL");
-        if (lv.size() > 1 && m0 >= 4 && !(te && te[0] == '0')) {
-            const char* se = getenv("SKV_FX_TAIL_SLOTS");  // tests: a small grid's worth of slots
+        if (lv.size() > 1 && m0 >= 4) {
+            const char* se = test_opt("SKV_FX_TAIL_SLOTS");  // tests: a small grid's worth of slots
             const uint64_t slots = se ? std::max<uint64_t>(1, strtoull(se, nullptr, 10)) : fx_tile_slots(k);
             const uint64_t h = m0 / 2;
             if (T0 > 3 * slots) {

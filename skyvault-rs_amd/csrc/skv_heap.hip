@@ -69,12 +69,6 @@ __global__ void __launch_bounds__(PM_T) k_pmax_block(uint64_t R, const uint64_t*
             if (head || c > 0) v = (uint32_t)i;
             if (head) f = 1;
             loc[q] = v;
-#if SKV_HEAP_PRINTF
-            if (blockIdx.x == 0 && threadIdx.x < 3)
-                printf("t%u q%d i=%llu s=%u base=%llu v=%u hi_i=%llx hi_v=%llx cmp=%d\n", threadIdx.x, q,
-                       (unsigned long long)i, s, (unsigned long long)base[s], v, (unsigned long long)hi[i],
-                       (unsigned long long)hi[v], rec_cmp(hi, lo, klen, addr, (uint32_t)i, v));
-#endif
         }
     }
     // block-wide inclusive segmented scan of the thread aggregates (Hillis-Steele)

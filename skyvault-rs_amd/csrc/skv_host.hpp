@@ -401,6 +401,11 @@ void ensure_aux(skv_ctx* ctx);
 int build_job(skv_ctx* ctx, const skv_stream* streams, uint32_t n, uint64_t max_run_size, uint32_t flags, Job& job);
 void drain(skv_ctx* ctx);
 
+// Test hooks (include/skv.h skv_test_option): the parity suite forces rare paths through named
+// values set on the library (the fused path off, the record sort on, fingerprint collisions, small
+// chunks, ...). Never read from the environment: production behaviour depends only on the call.
+// test_opt(name): the value set for `name`, or null (declared in skv_launch.hpp).
+
 // A pipelined or split call on one ctx (skv_hostpipe.hip, skv_split.hip): table uploads and readbacks
 // by copy kernels, not DMA copies that would queue behind the bulk copies; buffers that grow keep
 // their old allocation (the graveyards) until the ctx's three streams have drained, as a hipFree in

@@ -288,7 +288,7 @@ static int compact_host_pipelined(skv_ctx* ctx, Job& job, skv_result** out, doub
     // ---- ingest + kernels, part by part
     FxArgs Alast{};
     bool have_A = false;
-    const char* fail_env = getenv("SKV_TEST_FAIL_PART");  // tests: a failure after part p was queued
+    const char* fail_env = test_opt("SKV_TEST_FAIL_PART");  // tests: a failure after part p was queued
     const uint64_t fail_at = fail_env ? strtoull(fail_env, nullptr, 10) : ~0ull;
     for (uint64_t p = 0; p < P; ++p) {
         if (p == fail_at) throw DevError("injected failure before part " + std::to_string(p));
@@ -552,122 +552,6 @@ static bool cut_runs(const Job& job, const std::vector<std::string>& cut, uint64
     return true;
 }
 
-// Cuts of a WAL flush of very many small runs (config 5: 10^6 runs of 83 records): each run is taken
-// as fixed-stride at its first record's size S (record i at 1 + i S); a cut row is found per run by
-// galloping from the position the cut's sample quantile predicts (i0 = frac * records: the cuts are
-// quantiles of evenly spaced samples, so a run's bound lies within a few records of it), touching
-// two or three neighbouring lines instead of a binary search's seven scattered ones. Rows are found
-// one at a time, each while the GPU ingests the part before (the pipeline below).
-// Nothing here is trusted: a cut that is not a record boundary fails its part's decode (the slices
-// are parsed from a true start), and the parts' records are checked to lie inside their key ranges
-// (wal_part_in_range) -- either way the serial path runs.
-struct FixedRuns {
-    std::vector<uint64_t> S, n;  // per run: the first record's size, records (len - 1) / S
-};
-// false: a run whose first record does not decode or whose length is not a multiple of it
-static bool fixed_prep(const Job& job, FixedRuns& F) {
-    const uint64_t nr = job.run_ptr.size();
-    F.S.resize(nr);
-    F.n.resize(nr);
-    const unsigned nb = par_nblocks(nr, 1u << 12);
-    std::vector<uint8_t> ok(nb, 1);
-    par_run(nr, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
-        constexpr uint64_t AHEAD = 16;
-        for (uint64_t m = lo; m < hi && m < lo + AHEAD; ++m) __builtin_prefetch((const uint8_t*)(uintptr_t)job.run_ptr[m] + 1);
-        for (uint64_t m = lo; m < hi; ++m) {
-            if (m + AHEAD < hi) __builtin_prefetch((const uint8_t*)(uintptr_t)job.run_ptr[m + AHEAD] + 1);
-            const uint8_t* rb = (const uint8_t*)(uintptr_t)job.run_ptr[m];
-            const uint64_t len = job.run_len[m];
-            const uint64_t sz = len > 1 ? host_rec_at(rb, len, 1) : 1;
-            if (!sz || (len - 1) % sz) {
-                ok[b] = 0;
-                return;
-            }
-            F.S[m] = sz;
-            F.n[m] = (len - 1) / sz;
-        }
-    });
-    for (uint8_t o : ok)
-        if (!o) return false;
-    return true;
-}
-// row[m] = byte offset of run m's first record >= c, at or after prev[m] (both 1 + i S);
-// false: a probed record whose key would not fit a record of size S (not a record start)
-static bool fixed_row(const Job& job, const FixedRuns& F, const std::string& c, double frac, const uint64_t* prev,
-                      uint64_t* row) {
-    const uint64_t nr = job.run_ptr.size();
-    const unsigned nb = par_nblocks(nr, 1u << 12);
-    std::vector<uint8_t> ok(nb, 1);
-    par_run(nr, nb, [&](unsigned b, uint64_t lo, uint64_t hi) {
-        constexpr uint64_t AHEAD = 16;
-        auto start = [&](uint64_t m) {
-            const uint64_t a = (prev[m] - 1) / F.S[m];
-            const uint64_t g = std::min<uint64_t>(F.n[m], std::max<uint64_t>(a, (uint64_t)(frac * (double)F.n[m] + 0.5)));
-            return g;
-        };
-        for (uint64_t m = lo; m < hi && m < lo + AHEAD; ++m)
-            __builtin_prefetch((const uint8_t*)(uintptr_t)job.run_ptr[m] + 1 + start(m) * F.S[m]);
-        for (uint64_t m = lo; m < hi; ++m) {
-            if (m + AHEAD < hi)
-                __builtin_prefetch((const uint8_t*)(uintptr_t)job.run_ptr[m + AHEAD] + 1 + start(m + AHEAD) * F.S[m + AHEAD]);
-            const uint8_t* rb = (const uint8_t*)(uintptr_t)job.run_ptr[m];
-            const uint64_t S = F.S[m], n = F.n[m], a = (prev[m] - 1) / S;
-            bool bad = false;
-            auto below = [&](uint64_t i) {  // record i's key < c
-                const uint64_t q = 1 + i * S, kl = be32(rb + q + 1);
-                if (kl + 5 > S) {
-                    bad = true;
-                    return false;
-                }
-                return host_key_cmp(rb + q + 5, kl, (const uint8_t*)c.data(), c.size()) < 0;
-            };
-            // the bound: the first i in [a, n] with i == n or !below(i); gallop from the guess
-            uint64_t g = start(m), l, h;  // invariant: every i < l is below, none of [h, n) is
-            if (g < n && below(g)) {
-                l = g + 1;
-                uint64_t step = 1;
-                h = n;
-                while (l + step - 1 < n && !bad) {
-                    const uint64_t x = l + step - 1;
-                    if (below(x)) {
-                        l = x + 1;
-                        step <<= 1;
-                    } else {
-                        h = x;
-                        break;
-                    }
-                }
-            } else {
-                h = g;
-                l = a;
-                uint64_t step = 1;
-                while (h > a + step - 1 && !bad) {
-                    const uint64_t x = h - step;
-                    if (below(x)) {
-                        l = x + 1;
-                        break;
-                    }
-                    h = x;
-                    step <<= 1;
-                }
-            }
-            while (l < h && !bad) {
-                const uint64_t mid = (l + h) >> 1;
-                if (below(mid)) l = mid + 1;
-                else h = mid;
-            }
-            if (bad) {
-                ok[b] = 0;
-                return;
-            }
-            row[m] = 1 + l * S;
-        }
-    });
-    for (uint8_t o : ok)
-        if (!o) return false;
-    return true;
-}
-
 // A stream of several member runs (an L0 or next-level concatenation, table_buffer_compaction.rs:
 // 66-100, table_tree_compaction.rs:103-135) is cut member by member; that is a key range of the
 // stream only when the concatenation ascends: every record of member i below member i + 1's first
@@ -701,25 +585,6 @@ static bool members_ascend(const Job& job) {
     for (uint8_t o : ok)
         if (!o) return false;
     return true;
-}
-
-// The keys of a WAL part's output all lie in [lo, hi) (null: unbounded): its first run's min key
-// and its last run's max key, each the table's canonical prefix "{id}." (every key of a part has
-// one, WAL_STRICT_CANON) + the stripped key in the output bytes (pout: the part's output in HBM).
-// Runs are in key order, so those two bound every key of the part.
-static bool wal_part_in_range(skv_ctx* ctx, const skv_result* pres, const uint8_t* pout, const std::string* lo,
-                              const std::string* hi) {
-    if (!pres->n_runs) return true;
-    const skv_run_desc& f = pres->runs[0];
-    const skv_run_desc& l = pres->runs[pres->n_runs - 1];
-    if (f.min_key_len > (1u << 20) || l.max_key_len > (1u << 20)) return false;
-    uint8_t* hp = (uint8_t*)pinned(ctx, f.min_key_len + l.max_key_len + 16);
-    d2h(ctx, hp, pout + f.min_key_off, f.min_key_len);  // (copy kernels here: no DMA queue behind egress)
-    d2h(ctx, hp + f.min_key_len, pout + l.max_key_off, l.max_key_len);
-    sync(ctx);
-    const std::string mn = std::to_string(f.table_id) + "." + std::string((const char*)hp, f.min_key_len);
-    const std::string mx = std::to_string(l.table_id) + "." + std::string((const char*)hp + f.min_key_len, l.max_key_len);
-    return (!lo || *lo <= mn) && (!hi || mx < *hi);
 }
 
 // Cut keys of a general key-range split: quantiles of records found at evenly spaced offsets of the
@@ -778,19 +643,13 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     const bool wal = (job.flags & SKV_SPLIT_BY_TABLE) != 0;
     if (job.in_bytes < min_bytes || job.batch || job.search || job.scan) return SKV_OK;
     if (k == 0 || nr == 0) return SKV_OK;
-    // Past 2^16 member runs (a WAL flush of 10^6 tiny runs) a walk of every run up to its last cut
-    // costs what the transfers do (125-147 ms on 8 threads for config 5, against ~80 ms for the whole
-    // H2D): such flushes are cut by the fixed-stride search (cut_runs_fixed) and every part's key range
-    // is checked after it (wal_part_in_range); other calls that large take the serial path.
-    // Measured (round 5, profiles/r05/c5_host.txt): at config 5 the parts' slices (10^6 per part)
-    // can only be ingested by the GPU reading pinned memory, which moves ~26-30 GB/s against ~56 GB/s
-    // for one DMA copy of the whole input, so the pipeline (235-300 ms) loses to the serial path
-    // (169 ms) on the boxes measured: it runs only with SKV_HOST_PIPE_MANY=1.
-    const bool many = nr > (1u << 16);
-    if (many) {
-        const char* me2 = getenv("SKV_HOST_PIPE_MANY");
-        if (!wal || !(me2 && me2[0] == '1')) return SKV_OK;
-    }
+    // Past 2^16 member runs (a WAL flush of 10^6 tiny runs) the call takes the serial path: a walk of
+    // every run up to its last cut costs what the transfers do (125-147 ms on 8 threads for config 5,
+    // against ~80 ms for the whole H2D), and the parts' 10^6 scattered slices move at ~26-30 GB/s (the
+    // GPU reading pinned memory) against ~56 GB/s for one DMA copy of the whole input. Round 5 built
+    // a pipeline for them (a fixed-stride cut search, cut rows found while the GPU ingests) and
+    // measured it slower (235-300 vs 169 ms, profiles/r05/c5_host.txt); round 6 removed it.
+    if (nr > (1u << 16)) return SKV_OK;
     // parts of ~1 GiB: each part costs a DMA copy per slice (config 3, 3.7 GiB: 4 parts 99.8 ms, 6
     // parts 102.9, 8 parts 105.0, 10 parts 110.5)
     uint64_t P = std::max<uint64_t>(2, std::min<uint64_t>(32, job.in_bytes / (1ull << 30)));
@@ -812,20 +671,7 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     if (P < 2 || (!wal && job.max_run_size > job.in_bytes / (4 * P))) return SKV_OK;
     // ---- bnd[p * nr + m]: byte offset of run m's first record >= cut p (1 / len at the ends)
     std::vector<uint64_t> bnd;
-    FixedRuns fixed;
-    if (many) {  // rows 0 and P now, row 1 before part 0's slices, row p + 1 while part p - 1 lands
-        if (!fixed_prep(job, fixed)) {
-            htrace("gpipe: a run is not fixed-stride");
-            return SKV_OK;
-        }
-        bnd.assign((P + 1) * nr, 1);
-        for (uint64_t m = 0; m < nr; ++m) bnd[P * nr + m] = job.run_len[m];
-        if (!fixed_row(job, fixed, cut[0], 1.0 / (double)P, bnd.data(), bnd.data() + nr)) {
-            htrace("gpipe: a cut not found");
-            return SKV_OK;
-        }
-        htrace("gpipe: first cut row");
-    } else if (!cut_runs(job, cut, P, bnd)) {
+    if (!cut_runs(job, cut, P, bnd)) {
         htrace("gpipe: a cut not found");
         return SKV_OK;
     }
@@ -839,16 +685,12 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     // 130 vs 105 ms: part 0's kernels waited behind the later parts' ingest); a WAL flush of 10^6 tiny
     // runs has millions of slices, each a DMA descriptor with its own fixed cost.
     uint64_t n_slices = 0;
-    if (many) {
-        n_slices = P * nr;  // (an upper bound: the rows after the first are not found yet)
-    } else {
-        for (uint64_t p = 0; p < P; ++p)
-            for (uint64_t m = 0; m < nr; ++m) n_slices += bnd[(p + 1) * nr + m] > bnd[p * nr + m];
-    }
+    for (uint64_t p = 0; p < P; ++p)
+        for (uint64_t m = 0; m < nr; ++m) n_slices += bnd[(p + 1) * nr + m] > bnd[p * nr + m];
     std::vector<uint64_t> hdev;
     bool kernel_ingest = n_slices > (1u << 15);
     {
-        const char* ie = getenv("SKV_INGEST");
+        const char* ie = test_opt("SKV_INGEST");
         if (ie && !strcmp(ie, "kernel")) kernel_ingest = true;
         if (kernel_ingest) {
             hdev.assign(nr, 0);
@@ -903,8 +745,7 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     } out_guard{ctx, h_out, cap};
     // ---- ingest: every part's slices, in part order, on in_stream. Kernel ingest: part p's slice
     // table is built on the host pool into the ctx's pinned slice arena and goes up on in_stream right
-    // before part p's ingest launch; a call past 2^16 runs finds cut row p + 1 first, while the GPU
-    // ingests part p - 1.
+    // before part p's ingest launch.
     IngestSlice* d_sl = nullptr;
     std::vector<uint64_t> sl_base(P + 1, 0);
     IngestSlice* h_sl = nullptr;
@@ -925,17 +766,8 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
     // a few hundred ingest workgroups in all: the copies are bound by PCIe, and a grid that filled
     // every CU (8 per slice: 2,048 at config 3) held the part kernels off the GPU until the whole
     // input had landed (part 0 finished after 77 ms, parts 1-7 in 3 ms each behind it)
-    uint32_t igrid = 384;
-    if (const char* be = getenv("SKV_INGEST_BLOCKS")) igrid = std::max<uint32_t>(1, (uint32_t)strtoul(be, nullptr, 10));
+    const uint32_t igrid = 384;
     for (uint64_t p = 0; p < P; ++p) {
-        if (many && p >= 1 && p + 1 < P) {
-            if (!fixed_row(job, fixed, cut[p], (double)(p + 1) / (double)P, &bnd[p * nr], &bnd[(p + 1) * nr])) {
-                htrace("gpipe: a cut not found");
-                drain(ctx);
-                used = false;
-                return SKV_OK;
-            }
-        }
         if (kernel_ingest) {
             const unsigned nb = par_nblocks(nr, 1u << 14);
             std::vector<uint64_t> cnt(nb + 1, 0);
@@ -1101,14 +933,6 @@ static int compact_host_pipelined_general(skv_ctx* ctx, Job& job, skv_result** o
             return SKV_OK;
         }
         const uint64_t n = pres->n_runs;
-        if (many && !wal_part_in_range(ctx, pres, d_out + wal_off, p == 0 ? nullptr : &cut[p - 1],
-                                       last_part ? nullptr : &cut[p])) {
-            skv_result_free(pres);
-            htrace("gpipe: a part's keys outside its range");
-            drain(ctx);
-            used = false;
-            return SKV_OK;
-        }
         if (wal) {
             // whole tables: every run of the part is final at its offset in the call's output
             for (uint64_t r = 0; r < n; ++r) {

@@ -361,10 +361,7 @@ __device__ __forceinline__ void put_rec(uint64_t o, const uint8_t* rp, const Rec
 // starts in its slot row, so EM_G lanes per chunk parse one record each with independent loads and
 // store consecutive records side by side; a chunk with more records than slots is walked by one
 // lane from its validated start.
-#ifndef SKV_EM_G
-#define SKV_EM_G 16
-#endif
-constexpr uint32_t EM_G = SKV_EM_G;  // lanes per chunk
+constexpr uint32_t EM_G = 16;  // lanes per chunk
 __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
                        const RunFmt* __restrict__ fmt, const uint32_t* __restrict__ run_broken,
                        const uint64_t* __restrict__ ch_start, const uint64_t* __restrict__ ch_rec_base,
@@ -682,11 +679,7 @@ __device__ __forceinline__ void load_elem(const Elems& E, uint64_t pos, uint64_t
     c = L0 ? (((uint64_t)E.klen[pos] << 32) | pos) : E.c[pos];
 }
 
-#ifndef SKV_DIAG_NOSUFFIX
-#define SKV_DIAG_NOSUFFIX 0  // diagnostic builds only (wrong order): skip key bytes past 16
-#endif
 __device__ __forceinline__ int suffix_cmp(const uint64_t* rec_addr, uint64_t ca, uint64_t cb) {
-    if (SKV_DIAG_NOSUFFIX) return 0;
     uint32_t la = (uint32_t)(ca >> 32), lb = (uint32_t)(cb >> 32);
     if (la > 16 && lb > 16) {
         const uint8_t* a = (const uint8_t*)rec_addr[(uint32_t)ca] + 5;
@@ -1865,15 +1858,7 @@ void launch_run_info(hipStream_t s, const uint64_t* ptr, const uint64_t* len, ui
 // largest e in [lo, hi] with P[e] <= v, given P[lo] <= v (64-ary search, exact). Not inlined: k_chain
 // unrolls its resolve step CH_D times, and 32 inlined copies of this rare fallback made the kernel
 // ~50 KB of straight-line code, streamed through the instruction cache on every round.
-#ifndef SKV_CH_INLINE
-#define SKV_CH_INLINE 0
-#endif
-#if SKV_CH_INLINE
-#define SKV_CH_SEARCH_ATTR
-#else
-#define SKV_CH_SEARCH_ATTR __noinline__
-#endif
-__device__ SKV_CH_SEARCH_ATTR uint64_t chain_search(const uint64_t* P, uint64_t lo, uint64_t hi, uint64_t v, int lane) {
+__device__ __noinline__ uint64_t chain_search(const uint64_t* P, uint64_t lo, uint64_t hi, uint64_t v, int lane) {
     while (lo < hi) {
         uint64_t span = hi - lo;
         uint64_t step = (span + 63) / 64;
@@ -1889,20 +1874,14 @@ __device__ SKV_CH_SEARCH_ATTR uint64_t chain_search(const uint64_t* P, uint64_t 
     return lo;
 }
 
-#ifndef SKV_CH_D
-#define SKV_CH_D 32
-#endif
-#ifndef SKV_CH_Q
-#define SKV_CH_Q 1
-#endif
 // Predicted windows in flight and entries per lane per window. With every record fitting a run,
 // run d+1 from a known start ends within (d+1) x (largest record) bytes of its lower bound, so
 // 32 windows of 64 consecutive P entries (one load per lane each, all independent) cover 32 run
 // ends per round for records of ~300 B (config 3: 3F chain 26.6 ms with 8 x 512-entry windows,
 // whose 64 loads per lane per round kept one wave latency-bound); rounds shrink to fewer
 // windows when the records are small relative to the largest (see ch_d below).
-constexpr int CH_D = SKV_CH_D;
-constexpr int CH_Q = SKV_CH_Q;
+constexpr int CH_D = 32;
+constexpr int CH_Q = 1;
 constexpr uint32_t CH_SHIFT = 10;  // byte -> record table granularity (1 KiB)
 
 // tbl[t] = the surviving record j with P[j] <= t * 2^CH_SHIFT < P[j+1] (K past the end): lets the
@@ -2746,13 +2725,9 @@ __global__ void __launch_bounds__(GATHER_THREADS, SKV_GATHER_WAVES) k_gather(con
             const uint4 v = two[u] ? funnel16(L[u], X[u], sh[u] & 15u) : L[u];
             if (ok[u]) {
                 uint8_t* o = out + ((q0 + qi + u * step) << 4);
-#if SKV_GATHER_NT
                 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
                 u32x4 vv = {v.x, v.y, v.z, v.w};
                 __builtin_nontemporal_store(vv, (u32x4*)o);
-#else
-                *(uint4*)o = v;
-#endif
             }
         }
     }
@@ -2782,211 +2757,6 @@ __global__ void __launch_bounds__(GATHER_THREADS, SKV_GATHER_WAVES) k_gather(con
         const uint32_t kl = __builtin_bswap32(load_window16(ra + 1, 4).x);
         if (!key_tails_equal(ra, (const uint8_t*)dupj, kl)) atomicOr(fp_bad, 1u);
     }
-}
-
-// ---------------------------------------------------------------------------------------
-// page gather: the output is cut into PAGE_BYTES pages, one workgroup each, every lane writes
-// PAGE_U aligned 16-byte blocks of its page with loads issued before stores and no loop — the
-// shape of the fastest plain copy on gfx950 (short workgroups, one pass). A prepass gives each
-// record its output address (bit 63: first record of a run, i.e. preceded by the run's version
-// byte) and each page the record holding its first byte.
-
-__global__ void k_page_prep(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ n_runs_p,
-                            const uint64_t* __restrict__ run_b, const uint64_t* __restrict__ P,
-                            const uint64_t* __restrict__ seg_r0, uint64_t* Dst, uint32_t* page_first) {
-    const uint64_t K = *Kp;
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= K) return;
-    const uint64_t n_runs = *n_runs_p;
-    uint64_t r = seg_r0[j / GATHER_SEG];  // run holding the segment's first record
-    while (r + 1 < n_runs && run_b[r + 1] <= j) ++r;
-    const bool start = run_b[r] == j;
-    const uint64_t d = P[j] + r + 1;
-    Dst[j] = d | (start ? (1ull << 63) : 0ull);
-    const uint64_t lo = start ? d - 1 : d, hi = d + (P[j + 1] - P[j]);
-    for (uint64_t pg = (lo + PAGE_BYTES - 1) / PAGE_BYTES; pg * PAGE_BYTES < hi; ++pg) page_first[pg] = (uint32_t)j;
-}
-
-// positions inside a workgroup are 32-bit, relative to its page: rel(v) = v - page_lo + 2^31,
-// clamped. Every compared position lies within a record (< 2^31 bytes) of the page, so
-// clamping never changes an outcome.
-__device__ __forceinline__ uint32_t page_rel(uint64_t v, uint64_t page_lo) {
-    const int64_t d = (int64_t)(v - page_lo) + 0x80000000ll;
-    return d < 0 ? 0u : (d > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)d);
-}
-
-// An output block [B, B+16) of a page (page-relative positions) assembled from the pieces that
-// cover its bytes [x0, x1): version bytes and record slices; bytewise store unless full.
-__device__ __noinline__ void page_block_slow(uint32_t B, uint32_t x0, uint32_t x1, uint32_t e, const uint32_t* s_x,
-                                             const uint32_t* s_d, const uint64_t* s_s, uint8_t* o) {
-    uint4 acc = make_uint4(0, 0, 0, 0);
-    uint32_t x = x0;
-    while (x < x1) {
-        const uint32_t d = s_d[e], nx = s_x[e + 1];
-        if (x < d) {  // the run's version byte at d - 1
-            const uint32_t a = x - B;
-            acc.x |= dword_mask(a, a + 1, 0) & 0x01010101u;
-            acc.y |= dword_mask(a, a + 1, 1) & 0x01010101u;
-            acc.z |= dword_mask(a, a + 1, 2) & 0x01010101u;
-            acc.w |= dword_mask(a, a + 1, 3) & 0x01010101u;
-            x += 1;
-            continue;
-        }
-        const uint32_t ee = nx < x1 ? nx : x1;
-        const uint32_t a = x - B, b = ee - B;
-        uint4 wv = load_window16((const uint8_t*)s_s[e] + (x - d), b - a);
-        wv = shl_bytes(wv, a);
-        acc.x |= wv.x & dword_mask(a, b, 0);
-        acc.y |= wv.y & dword_mask(a, b, 1);
-        acc.z |= wv.z & dword_mask(a, b, 2);
-        acc.w |= wv.w & dword_mask(a, b, 3);
-        x = ee;
-        ++e;
-    }
-    if (x0 == B && x1 == B + 16) *(uint4*)o = acc;
-    else for (uint32_t y = x0; y < x1; ++y) o[y - B] = (uint8_t)byte_of(acc, y - B);
-}
-
-__global__ void __launch_bounds__(256, SKV_PAGE_WAVES) k_gather_pages(const uint64_t* __restrict__ Kp,
-                                                                    const uint64_t* __restrict__ n_runs_p,
-                                                                    const uint64_t* __restrict__ P,
-                                                                    const uint64_t* __restrict__ Dst,
-                                                                    const uint64_t* __restrict__ m_src,
-                                                                    const uint32_t* __restrict__ page_first,
-                                                                    uint8_t* __restrict__ out) {
-    constexpr uint32_t NE = 256;      // records staged per round
-    constexpr uint32_t ORG = 0x80000000u;
-    __shared__ uint32_t s_x[NE + 1];  // extended start: version byte (if any) else first record byte
-    __shared__ uint32_t s_d[NE];      // first record byte
-    __shared__ uint64_t s_s[NE];      // source address
-    __shared__ uint16_t s_slow[PAGE_BYTES / 16];
-    __shared__ uint32_t s_nslow;
-    const uint32_t nb = gridDim.x, bid = blockIdx.x;
-    const uint32_t xcd = bid & 7, qn = nb >> 3, rn = nb & 7;
-    const uint32_t w = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
-    const uint64_t K = *Kp;
-    if (K == 0) return;
-    const uint64_t total = P[K] + *n_runs_p;
-    const uint64_t page_lo = (uint64_t)w * PAGE_BYTES;
-    if (page_lo >= total) return;
-    const uint32_t page_hi = page_rel(page_lo + PAGE_BYTES < total ? page_lo + PAGE_BYTES : total, page_lo);
-    const uint32_t tot_r = page_rel(total, page_lo);
-    uint8_t* const obase = out + page_lo;
-    uint64_t j0 = page_first[w];
-    const uint32_t t = threadIdx.x;
-    for (;;) {  // one round unless the page holds more than NE records (records < PAGE/NE bytes)
-        {
-            const uint64_t j = j0 + t;
-            if (j < K) {
-                const uint64_t dv = Dst[j];
-                const uint64_t d = dv & ~(1ull << 63);
-                s_d[t] = page_rel(d, page_lo);
-                s_x[t] = page_rel((dv >> 63) ? d - 1 : d, page_lo);
-                s_s[t] = m_src[j];
-            } else {
-                s_x[t] = tot_r;
-                s_d[t] = tot_r;
-                s_s[t] = 0;
-            }
-            if (t == 0) {
-                s_nslow = 0;
-                const uint64_t jn = j0 + NE;
-                uint32_t xn = tot_r;
-                if (jn < K) {
-                    const uint64_t dv = Dst[jn];
-                    const uint64_t d = dv & ~(1ull << 63);
-                    xn = page_rel((dv >> 63) ? d - 1 : d, page_lo);
-                }
-                s_x[NE] = xn;
-            }
-        }
-        __syncthreads();
-        const uint32_t cover = s_x[NE];  // this round covers output positions [.., cover)
-        const uint32_t r_lo = s_x[0] > ORG ? s_x[0] : ORG;
-        const uint32_t r_hi = cover < page_hi ? cover : page_hi;
-        // blocks of the page intersecting [r_lo, r_hi); one crossing r_lo / r_hi (several rounds,
-        // or the end of the output) is assembled bytewise for its in-range bytes
-        const uint32_t q0 = (r_lo - ORG) >> 4, q1 = (r_hi - ORG + 15) >> 4;
-        auto find = [&](uint32_t x) {  // last entry with extended start <= x
-            uint32_t lo = 0, hi = NE;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_x[mid] <= x) lo = mid;
-                else hi = mid;
-            }
-            return lo;
-        };
-        uint4 v[PAGE_U];
-        uint32_t fast = 0;
-#pragma unroll
-        for (int u = 0; u < PAGE_U; ++u) {
-            const uint32_t q = q0 + t + u * 256;
-            v[u] = make_uint4(0, 0, 0, 0);
-            if (q < q1) {
-                const uint32_t B = ORG + (q << 4);
-                bool ok = false;
-                if (B >= r_lo && B + 16 <= r_hi) {
-                    const uint32_t lo = find(B);
-                    const uint32_t d = s_d[lo], e = s_x[lo + 1];
-                    const uint8_t* src = (const uint8_t*)s_s[lo];
-                    if (B >= d && B + 16 <= e) {
-                        v[u] = *(const uint4*)(src + (B - d));
-                        ok = true;
-                    } else if (B >= d && lo + 2 <= NE && e - d >= 16 && s_d[lo + 1] == e) {
-                        // straddle into the next record (no version byte between them)
-                        const uint32_t e2 = s_x[lo + 2];
-                        if (e2 >= B + 16 && e2 - e >= 16) {
-                            const uint32_t k = e - B;  // bytes from the first record
-                            const uint4 L = *(const uint4*)(src + (e - d) - 16);
-                            const uint4 F = *(const uint4*)((const uint8_t*)s_s[lo + 1]);
-                            v[u] = funnel16(L, F, 16 - k);
-                            ok = true;
-                        }
-                    }
-                }
-                if (ok) fast |= 1u << u;
-                else s_slow[atomicAdd(&s_nslow, 1u)] = (uint16_t)q;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < PAGE_U; ++u) {
-            if (fast & (1u << u)) {
-                uint8_t* o = obase + ((q0 + t + u * 256) << 4);
-#if SKV_GATHER_NT
-                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                u32x4 vv = {v[u].x, v[u].y, v[u].z, v[u].w};
-                __builtin_nontemporal_store(vv, (u32x4*)o);
-#else
-                *(uint4*)o = v[u];
-#endif
-            }
-        }
-        // slow blocks (version bytes, records < 16 B, round / output edges), queued in LDS
-        __syncthreads();
-        const uint32_t n_slow = s_nslow;
-        for (uint32_t i = t; i < n_slow; i += 256) {
-            const uint32_t B = ORG + ((uint32_t)s_slow[i] << 4);
-            const uint32_t x0 = B > r_lo ? B : r_lo;
-            const uint32_t x1 = B + 16 < r_hi ? B + 16 : r_hi;
-            page_block_slow(B, x0, x1, find(x0), s_x, s_d, s_s, obase + (B - ORG));
-        }
-        if (cover >= page_hi) break;
-        __syncthreads();  // LDS reuse for the next round
-        j0 += NE;
-    }
-}
-
-void launch_page_prep(hipStream_t s, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
-                      const uint64_t* seg_r0, uint64_t* Dst, uint32_t* page_first, uint64_t max_K) {
-    if (!max_K) return;
-    k_page_prep<<<(unsigned)((max_K + 255) / 256), 256, 0, s>>>(Kp, n_runs, run_b, P, seg_r0, Dst, page_first);
-}
-void launch_gather_pages(hipStream_t s, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* P,
-                         const uint64_t* Dst, const uint64_t* m_src, const uint32_t* page_first, uint8_t* out,
-                         uint64_t max_out_bytes) {
-    if (!max_out_bytes) return;
-    k_gather_pages<<<(unsigned)((max_out_bytes + PAGE_BYTES - 1) / PAGE_BYTES), 256, 0, s>>>(Kp, n_runs, P, Dst, m_src,
-                                                                                             page_first, out);
 }
 
 // ---------------------------------------------------------------------------------------

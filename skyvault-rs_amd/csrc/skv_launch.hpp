@@ -2,6 +2,9 @@
 #pragma once
 #include "skv_dev.hpp"
 
+// a test hook's value (include/skv.h skv_test_option; skv_ctx.hip), or null
+const char* test_opt(const char* name);
+
 namespace skv {
 // Raise a kernel's dynamic-LDS limit to the CU's 160 KiB, once per (device, kernel), under a lock:
 // the limit is a ceiling, so one value serves every launch size and concurrent ctxs never lower it
@@ -109,10 +112,6 @@ void launch_wal_desc(hipStream_t, const uint64_t* NTp, uint64_t max_NT, const ui
 void launch_wal_gather(hipStream_t, const uint64_t* Kp, uint64_t max_K, const uint32_t* tix, const uint64_t* tstart,
                        const uint64_t* keep, const uint64_t* run_off, const uint64_t* Pw, const uint32_t* strip,
                        const uint64_t* m_src, const uint32_t* wnk, const uint8_t* canon, uint8_t* out);
-void launch_page_prep(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* run_b, const uint64_t* P,
-                      const uint64_t* seg_r0, uint64_t* Dst, uint32_t* page_first, uint64_t max_K);
-void launch_gather_pages(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, const uint64_t* P, const uint64_t* Dst,
-                         const uint64_t* m_src, const uint32_t* page_first, uint8_t* out, uint64_t max_out_bytes);
 // skv_heap.hip — k_way::merge's heap pop order for unsorted streams (heap-order mode)
 void launch_heap_keys(hipStream_t, uint64_t R, const uint64_t* base, uint32_t k, const uint64_t* hi,
                       const uint64_t* lo, const uint32_t* klen, const uint64_t* addr, uint32_t* eff, uint64_t* blk_agg,

@@ -335,24 +335,10 @@ __device__ __forceinline__ bool sk_sbefore(const SWin& w, const SSplit* __restri
 // table (32 B per splitter: 3.4 MB at config 5's 10^5 splitters, L2-resident, where the 48-byte
 // SSplit table was not). Both levels are branch-free power-of-two searches with a step count
 // uniform over the wave, run for SB_ILP elements at once so their loads overlap.
-#ifndef SKV_SB_DIAGK
-#define SKV_SB_DIAGK 0
-#endif
-#ifndef SKV_SB_ATOM2
-#define SKV_SB_ATOM2 0
-#endif
-#ifndef SKV_SB_THREADS
 #define SKV_SB_THREADS 256
-#endif
-#ifndef SKV_SB_PER
 #define SKV_SB_PER 16
-#endif
-#ifndef SKV_SB_TOP
 #define SKV_SB_TOP 1024
-#endif
-#ifndef SKV_SB_ILP
 #define SKV_SB_ILP 4  // elements a thread searches at once
-#endif
 constexpr int SB_THREADS = SKV_SB_THREADS, SB_PER = SKV_SB_PER, SB_TOP = SKV_SB_TOP, SB_ILP = SKV_SB_ILP;
 static_assert(SB_PER % SB_ILP == 0, "a workgroup's elements in whole ILP batches");
 // D (SKV_SB_DIAGK builds only, timing diagnostics with scratch outputs): bit 0 skips the LDS level
@@ -440,9 +426,6 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restr
             const uint64_t b = g[u] + c[u];
             const uint64_t slot = (D & 4) ? (i & 0xFFF) : atomicAdd(cnt + b, 1ull);
             bs[i] = (b << 32) | slot;
-#if SKV_SB_ATOM2  // diagnostic: a second returning atomic on the same counter (adds 0): the atomics' share
-            if (atomicAdd(cnt + b, 0ull) == ~0ull) bs[i] = 0;
-#endif
         }
 #if SKV_SORT_PROF
         __builtin_amdgcn_s_waitcnt(0);
@@ -465,12 +448,8 @@ __global__ void __launch_bounds__(SB_THREADS) k_sort_bucket(const SElem* __restr
 //      atomic per (chunk, bucket); the second scatter then forms the buckets.
 // The bucket sort compares windows from cp[a] (every key of the bucket shares them) and takes its
 // 8-byte sort words from the bucket's own prefix L[b] >= cp[a] on (k_sort_tile's ks).
-#ifndef SKV_SA_PER
 #define SKV_SA_PER 16
-#endif
-#ifndef SKV_SBB_PER
 #define SKV_SBB_PER 8
-#endif
 constexpr int SA_PER = SKV_SA_PER;    // pass A: elements per thread (workgroup slots < 2^14)
 constexpr int SBB_PER = SKV_SBB_PER;  // pass B: elements per thread (workgroup slots < 2^13)
 static_assert(SA_PER * SB_THREADS <= (1 << 14) && SBB_PER * SB_THREADS <= (1 << 13), "slot bits");
@@ -497,7 +476,7 @@ static SplitLayout split_layout(void* split_buf, uint64_t nsp) {
 // top-level entries of the bucket search (SKV_SB_NT caps them below SB_TOP: tests reach the group
 // level and the two-pass path at small sizes)
 static uint64_t sb_top(uint64_t nsp) {
-    const char* e = getenv("SKV_SB_NT");
+    const char* e = test_opt("SKV_SB_NT");
     uint64_t cap = e ? strtoull(e, nullptr, 10) : (uint64_t)SB_TOP;
     if (cap == 0 || cap > (uint64_t)SB_TOP) cap = SB_TOP;
     uint64_t top = 1;  // a power of two: the global search level is a full power-of-two search
@@ -807,14 +786,9 @@ __device__ __forceinline__ bool sk_eless(const SElem* bk, uint32_t x, uint32_t y
     return sk_wless(sk_skey(bk[x], L, pre), sk_skey(bk[y], L, pre), bk, x, y, L);
 }
 
-#ifndef SKV_SORT_TIE_MAX
 #define SKV_SORT_TIE_MAX 8
-#endif
 constexpr uint32_t SORT_TIE_MAX = SKV_SORT_TIE_MAX;  // longest run of equal first words sorted by one thread
 
-#ifndef SKV_SORT_REGS
-#define SKV_SORT_REGS 1  // 1: the bucket's bitonic network in registers (shuffles / LDS across waves)
-#endif
 // One compare-exchange of the network on packed sort words: the first word's top 53 bits and the
 // element id (11 bits) in one 64-bit value, so a pair moves with one 64-bit shuffle and compares
 // once (ids are distinct; padding is ~0). The lower index keeps the smaller word.
@@ -978,7 +952,6 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* __restrict__ 
     const uint32_t n32 = (uint32_t)n;
     SPROF_T(q0);
     if (threadIdx.x == 0) s_long = 0;
-#if SKV_SORT_REGS
     static_assert(SORT_THREADS == 256 && SORT_CAP == 2048, "register network: 256 threads, <= 8 elements each");
     if (n32 <= 256) sk_sort_regs<1>(bk, n32, L, pre, ks, kw, id, kwid);
     else if (n32 <= 512) sk_sort_regs<2>(bk, n32, L, pre, ks, kw, id, kwid);
@@ -989,53 +962,6 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_tile(SElem* __restrict__ 
     SPROF_ADD(4, q0, q1);
     SPROF_T(q2);
     SPROF_ADD(5, q1, q2);
-#else
-    for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
-        kw[i] = kwid[i] = sk_kw(bk[i], L, pre, ks);
-        id[i] = (uint16_t)i;
-    }
-    __syncthreads();
-    SPROF_T(q1);
-    SPROF_ADD(4, q0, q1);
-    uint32_t P = 1, lp = 0;
-    while (P < n32) {
-        P <<= 1;
-        ++lp;
-    }
-    // A stage with jj <= 64 pairs elements inside one 128-element chunk, and compare-exchange i
-    // touches chunk i / 64, which is always handled by the same wave (i = threadIdx.x + m *
-    // SORT_THREADS). Those stages need no workgroup barrier: a wave's LDS operations complete in
-    // issue order, so only the stages with jj >= 128 are bracketed by __syncthreads (55 -> 9
-    // barriers for a 1024-element bucket).
-    static_assert(SORT_THREADS % 64 == 0, "whole waves per workgroup");
-    bool local_last = false;
-    for (uint32_t lk = 1; lk <= lp; ++lk) {
-        for (int lj = (int)lk - 1; lj >= 0; --lj) {
-            const bool wide = lj >= 6 + 1;
-            if (wide && local_last) __syncthreads();
-            for (uint32_t i = threadIdx.x; i < P / 2; i += blockDim.x) {
-                uint32_t a, c;
-                bitonic_pair(i, lk, (uint32_t)lj, a, c);
-                if (c < n32) {
-                    const uint64_t ka = kw[a], kc = kw[c];
-                    if (kc < ka) {
-                        const uint16_t ia = id[a], ic = id[c];
-                        kw[a] = kc;
-                        kw[c] = ka;
-                        id[a] = ic;
-                        id[c] = ia;
-                    }
-                }
-            }
-            if (wide) __syncthreads();
-            else __builtin_amdgcn_wave_barrier();
-            local_last = !wide;
-        }
-    }
-    if (local_last) __syncthreads();
-    SPROF_T(q2);
-    SPROF_ADD(5, q1, q2);
-#endif
     // runs of equal kw into the full order
     for (uint32_t i = threadIdx.x; i < n32; i += blockDim.x) {
         const uint64_t w = kw[i];
@@ -1180,28 +1106,6 @@ void launch_sort_bucket(hipStream_t s, const SElem* E, uint64_t n, const SElem* 
     }
     const uint64_t per_wg = (uint64_t)SB_THREADS * SB_PER;
     const unsigned nb = (unsigned)((n + per_wg - 1) / per_wg);
-#if SKV_SB_DIAGK
-    // timing diagnostics first (E still holds the true prefixes), into scratch outputs
-    if (n && diag) {
-        static uint64_t *bs2 = nullptr, *cnt2 = nullptr;
-        static uint64_t cap = 0;
-        if (cap < n) {
-            (void)hipFree(bs2);
-            (void)hipFree(cnt2);
-            if (hipMalloc(&bs2, n * 8) != hipSuccess ||
-                hipMalloc(&cnt2, (n + 2) * 8) != hipSuccess)  // (nsp < n)
-                abort();
-            cap = n;
-        }
-        auto* c2 = (unsigned long long*)cnt2;
-        (void)hipMemsetAsync(cnt2, 0, (nsp + 2) * 8, s);
-        k_sort_bucket<1><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, c2, bs2);
-        k_sort_bucket<2><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, c2, bs2);
-        k_sort_bucket<4><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, c2, bs2);
-        k_sort_bucket<3><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, c2, bs2);
-        k_sort_bucket<7><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, c2, bs2);
-    }
-#endif
     if (n) k_sort_bucket<0><<<nb, SB_THREADS, 0, s>>>(E, n, sp, win, nsp, top, gcp, disc, (unsigned long long*)cnt, bs);
 }
 size_t sort_split_bytes(uint64_t nsp) {
@@ -1221,7 +1125,7 @@ void launch_sort_tile(hipStream_t s, SElem* in, const uint64_t* start, const uin
 }
 
 uint64_t sort_two_pass_top(uint64_t nsp) {
-    const char* e = getenv("SKV_SORT_TWO_PASS");  // 0: the one-pass search always
+    const char* e = test_opt("SKV_SORT_TWO_PASS");  // 0: the one-pass search always
     if (e && e[0] == '0') return 0;
     const uint64_t top = sb_top(nsp);
     return top >= 4 && top <= SBB_LW ? top : 0;
@@ -1248,7 +1152,7 @@ void launch_sort_pass_b(hipStream_t s, const SElem* T, uint64_t n, const uint64_
                         const void* split_buf, uint64_t* cnt, uint64_t* bs) {
     const SplitLayout l = split_layout((void*)split_buf, nsp);
     const uint64_t per_wg = (uint64_t)SB_THREADS * SBB_PER;
-    const char* e = getenv("SKV_SB_GMAX");  // groups a chunk may span on the LDS path (tests: 0)
+    const char* e = test_opt("SKV_SB_GMAX");  // groups a chunk may span on the LDS path (tests: 0)
     const uint32_t gmax = e ? (uint32_t)std::min<unsigned long>(strtoul(e, nullptr, 10), SBB_GMAX) : SBB_GMAX;
     if (n)
         k_sort_pass_b<<<(unsigned)((n + per_wg - 1) / per_wg), SB_THREADS, 0, s>>>(

@@ -604,7 +604,6 @@ __global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict_
         if (j + 1 == K || threadIdx.x + 1 == WAL_G) os[threadIdx.x + 1] = ostart + wo;
     }
     __syncthreads();
-    if ((diag & 3) == 2) return;  // SKV_WAL_FUSED=2 (diagnostic, wrong output): everything but the output bytes
     // consecutive threads compose consecutive aligned output blocks (coalesced stores; a thread per
     // record instead, its blocks in a loop, measured slower: 10.1 vs 8.9 ms at config 5)
     const uint32_t c = (uint32_t)(K - j0 < WAL_G ? K - j0 : WAL_G);
@@ -652,11 +651,8 @@ void launch_wal_fused(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const u
                       const SElem* S, const uint32_t* m_rec) {
     // SKV_WAL_LDS=<bytes>: pad the workgroup's LDS request (caps workgroups per CU: a smaller set of
     // record lines in flight per XCD, so the composition's re-read can hit L2; occupancy studies)
-    static const size_t pad = getenv("SKV_WAL_LDS") ? (size_t)atol(getenv("SKV_WAL_LDS")) : 0;
-    const size_t lds = std::min<size_t>(pad, 96 * 1024);
-    if (lds) lds_limit((const void*)k_wal_fused);
     if (max_K)
-        k_wal_fused<<<wal_blocks(max_K, WAL_G), WAL_G, lds, s>>>(Kp, m_src, P, Dp, out, tstate, ticket, fail, tlist,
+        k_wal_fused<<<wal_blocks(max_K, WAL_G), WAL_G, 0, s>>>(Kp, m_src, P, Dp, out, tstate, ticket, fail, tlist,
                                                                   tcount, tcap, tail, diag, S, m_rec);
 }
 

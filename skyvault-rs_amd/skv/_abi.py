@@ -135,6 +135,7 @@ EXPORTED_SYMBOLS = [
     "skv_ctx_host_info",
     "skv_host_plan",
     "skv_split_deal",
+    "skv_test_option",
     "skv_compact",
     "skv_compact_dev",
     "skv_compact_split",

@@ -62,6 +62,8 @@ def load():
     l.skv_split_deal.argtypes = [C.POINTER(C.c_int), C.c_uint32, C.c_uint64, C.POINTER(C.c_uint32),
                                  C.POINTER(C.c_int64)]
     l.skv_split_deal.restype = C.c_int
+    l.skv_test_option.argtypes = [C.c_char_p, C.c_char_p]
+    l.skv_test_option.restype = C.c_int
     for fn in (l.skv_compact, l.skv_compact_dev):
         fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.POINTER(C.POINTER(SkvResult))]
         fn.restype = C.c_int
@@ -442,3 +444,27 @@ def split_deal(ctx_devices: Sequence[int], n_parts: int) -> tuple:
     if rc != SKV_OK:
         raise RunError(rc, "skv_split_deal: invalid arguments")
     return list(ctx_of[:n_parts]), list(after[:n_parts])
+
+
+_test_opts: dict = {}
+
+
+def test_option(name: Optional[str], value=None) -> None:
+    """skv_test_option: set (value: str / int) or clear (None) one of the library's test hooks (tests
+    only, include/skv.h); name None clears every hook."""
+    l = load()
+    rc = l.skv_test_option(name.encode() if name is not None else None,
+                           str(value).encode() if value is not None else None)
+    if rc != SKV_OK:
+        raise RunError(rc, f"skv_test_option: unknown hook {name!r}")
+    if name is None:
+        _test_opts.clear()
+    elif value is None:
+        _test_opts.pop(name, None)
+    else:
+        _test_opts[name] = str(value)
+
+
+def test_option_get(name: str) -> Optional[str]:
+    """the value this process set for a test hook through test_option (None: unset)"""
+    return _test_opts.get(name)

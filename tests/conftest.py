@@ -20,3 +20,12 @@ def oracle():
 
     pyoracle.build()
     return pyoracle
+
+
+@pytest.fixture(autouse=True)
+def _clear_test_hooks():
+    """the library's test hooks (skv_test_option) are process-wide: none outlives its test"""
+    yield
+    api = sys.modules.get("skv.api")
+    if api is not None and getattr(api, "_lib", None) is not None:
+        api.test_option(None)

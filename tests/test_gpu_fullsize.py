@@ -189,7 +189,7 @@ def test_config4_eight_compactions_at_once(torch):
 @pytest.fixture
 def default_pipe_env():
     """skv_compact with its shipped thresholds: no SKV_HOST_PIPE* / SKV_HOST_PARTS override."""
-    keys = ("SKV_HOST_PIPE", "SKV_HOST_PIPE_MIN", "SKV_HOST_PARTS", "SKV_INGEST")
+    keys = ("SKV_HOST_PIPE", "SKV_HOST_PIPE_MIN", "SKV_HOST_PARTS")  # (test hooks are cleared per test)
     old = {k: os.environ.pop(k, None) for k in keys}
     yield
     for k, v in old.items():
@@ -502,10 +502,9 @@ def test_config3_full_size(dev, torch, cfg3_full, flags):
 
 def test_config5_host_entry_full_size(dev, torch):
     """config 5 through skv_compact with the 10^6 WAL runs in pinned host memory (storage.rs:183-250
-    get_run -> compact -> put_run, wal_compaction.rs:18-51), with the many-run pipeline switched on
-    (SKV_HOST_PIPE_MANY=1): the flush is cut by the fixed-stride search and pipelined (host_parts >
-    0, the GPU ingests the parts' slices itself); bytes and descriptors equal to the per-table-group
-    oracle at both max sizes."""
+    get_run -> compact -> put_run, wal_compaction.rs:18-51): past 2^16 runs the call takes the serial
+    path (the many-run pipeline measured slower and was removed in round 6); bytes
+    and descriptors equal to the per-table-group oracle at both max sizes."""
     from skv.devgen import make_cfg5_on_device
 
     n_streams = 1_000_000
@@ -516,11 +515,7 @@ def test_config5_host_entry_full_size(dev, torch):
     sa = _abi.stream_table(np.arange(1, n_streams + 1), host_t.data_ptr() + rl * np.arange(n_streams, dtype=np.uint64),
                            np.full(n_streams, rl))
     host = host_t.numpy()
-    os.environ["SKV_HOST_PIPE_MANY"] = "1"  # the pipeline past 2^16 runs (off by default)
-    try:
-        _config5_host(dev, sa, host)
-    finally:
-        os.environ.pop("SKV_HOST_PIPE_MANY", None)
+    _config5_host(dev, sa, host)
 
 
 def _config5_host(dev, sa, host):
@@ -528,8 +523,7 @@ def _config5_host(dev, sa, host):
         _progress(f"config 5 host entry max {max_run}: device")
         hr = dev.compact_host(sa, max_run, _abi.SKV_SPLIT_BY_TABLE)
         t = dev.timings()
-        # at 4 MiB the one-run rule drops every table, which a part cannot decide alone: serial path
-        assert (t["host_parts"] >= 2) == (max_run != MAX_RUN), t
+        assert t["host_parts"] == 0, t  # past 2^16 runs: the serial path
         _progress(f"config 5 host entry: {t['host_parts']} parts; oracle")
         exp, descs, dropped, out_records = _wal_oracle(host, max_run)
         raw = hr._res.contents

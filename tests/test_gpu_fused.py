@@ -22,6 +22,7 @@ from skv.api import Compactor
 
 import pyoracle
 from test_gpu_parity import _diff, _run_both
+from knobs import knob, knob_get  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 KiB, MiB = 1 << 10, 1 << 20
@@ -180,12 +181,12 @@ def test_fused_matches_unfused(dev):
     streams = gen.config2(n_streams=64, n_records=2500, vsize=256, variant="B")
     a = dev.compact(streams, 4 * MiB, 0)
     assert dev.timings()["path"] == _abi.PATH_FUSED
-    os.environ["SKV_FUSED"] = "0"
+    knob("SKV_FUSED", "0")
     try:
         b = dev.compact(streams, 4 * MiB, 0)
         assert dev.timings()["path"] == _abi.PATH_FIXED
     finally:
-        del os.environ["SKV_FUSED"]
+        knob("SKV_FUSED", None)
     assert [(x.data, x.stats.min_key, x.stats.max_key) for x in a] == \
         [(y.data, y.stats.min_key, y.stats.max_key) for y in b]
 
@@ -241,7 +242,7 @@ def test_fused_short_tail_tiles(dev, slots):
     """The last generation of tiles at half size (splitter t at sorted sample t*m up to T1, then
     T1*m + (t - T1)*m/2): forced on small inputs by pretending only `slots` tiles fit the GPU at
     once; same bytes as the oracle, and the fused path is still the one taken."""
-    os.environ["SKV_FX_TAIL_SLOTS"] = slots
+    knob("SKV_FX_TAIL_SLOTS", slots)
     try:
         r = random.Random(int(slots))
         for trial in range(6):
@@ -251,4 +252,4 @@ def test_fused_short_tail_tiles(dev, slots):
             streams = [(s + 1, [_run(7000 + 100 * trial + s, n, 16, 40, uni)]) for s in range(k)]
             _check(dev, streams, r.choice([4 * MiB, 5000, 64 * KiB]))
     finally:
-        del os.environ["SKV_FX_TAIL_SLOTS"]
+        knob("SKV_FX_TAIL_SLOTS", None)

@@ -16,6 +16,7 @@ from skv.api import Compactor
 
 import pyoracle
 from test_oracle_vs_pyref import _case
+from knobs import knob, knob_get  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -252,17 +253,17 @@ def test_wal_one_pass_stage(dev):
         exp, got = _run_both(dev, sts, 4 * MiB, _abi.SKV_SPLIT_BY_TABLE)
         assert exp == got, _diff(exp, got)
         assert dev.timings()["wal_stage"] == 2
-    old = os.environ.get("SKV_WAL_FUSED")
-    os.environ["SKV_WAL_FUSED"] = "0"
+    old = knob_get("SKV_WAL_FUSED")
+    knob("SKV_WAL_FUSED", "0")
     try:
         exp, got = _run_both(dev, streams, 4 * MiB, _abi.SKV_SPLIT_BY_TABLE)
         assert exp == got, _diff(exp, got)
         assert dev.timings()["wal_stage"] == 2
     finally:
         if old is None:
-            os.environ.pop("SKV_WAL_FUSED", None)
+            knob("SKV_WAL_FUSED", None)
         else:
-            os.environ["SKV_WAL_FUSED"] = old
+            knob("SKV_WAL_FUSED", old)
 
 
 def test_chain_window_predicted_past_the_end(dev):
@@ -476,17 +477,17 @@ def test_longer_speculative_walks(dev, chunk):
     """Big calls walk 8-64 KiB per speculative chunk (skv_compact.hip picks the length from the call
     size); SKV_CHUNK_BYTES forces a length on small inputs: fake records in values, records
     spanning chunks, and corruption everywhere must still give the reference's outcome."""
-    old = os.environ.get("SKV_CHUNK_BYTES")
-    os.environ["SKV_CHUNK_BYTES"] = str(chunk)
+    old = knob_get("SKV_CHUNK_BYTES")
+    knob("SKV_CHUNK_BYTES", str(chunk))
     try:
         test_values_with_fake_records(dev)
         test_records_spanning_many_chunks(dev)
         test_corruption_at_every_position_class(dev)
     finally:
         if old is None:
-            os.environ.pop("SKV_CHUNK_BYTES", None)
+            knob("SKV_CHUNK_BYTES", None)
         else:
-            os.environ["SKV_CHUNK_BYTES"] = old
+            knob("SKV_CHUNK_BYTES", old)
 
 
 def test_device_resident_entry_point(dev):
@@ -606,11 +607,11 @@ def test_coarse_sample_levels_same_bytes(dev):
     streams = gen.config3(seed=77, n_streams=300, run_bytes=160 * KiB, vsize=32)
     ref = dev.compact(streams, 1 * MiB, 0)
     for f in ("2", "4"):
-        os.environ["SKV_HI_STEP"] = f
+        knob("SKV_HI_STEP", f)
         try:
             got = dev.compact(streams, 1 * MiB, 0)
         finally:
-            del os.environ["SKV_HI_STEP"]
+            knob("SKV_HI_STEP", None)
         assert [r.data for r in got] == [r.data for r in ref], f
 
 
@@ -618,14 +619,14 @@ def test_threaded_table_staging(dev):
     """Host tables above SKV_PAR_COPY_MIN bytes are copied into the pinned upload arena by
     several threads (10^6-run calls); forced down to 4 KiB here, a 1000-run WAL call and a
     256-way call still match the oracle."""
-    os.environ["SKV_PAR_COPY_MIN"] = "4096"
+    knob("SKV_PAR_COPY_MIN", "4096")
     try:
         for streams, flags in ((gen.config5(n_streams=1000), _abi.SKV_SPLIT_BY_TABLE),
                                (gen.config3(n_streams=256, run_bytes=24 * KiB, vsize=64), 0)):
             exp, got = _run_both(dev, streams, 4 * MiB, flags)
             assert exp == got, _diff(exp, got)
     finally:
-        del os.environ["SKV_PAR_COPY_MIN"]
+        knob("SKV_PAR_COPY_MIN", None)
 
 
 def test_device_entry_reuse_across_calls(dev):

@@ -14,6 +14,7 @@ from skv.api import Compactor
 
 import pyoracle
 from test_scan_oracle import KATS, _ops, norm_oracle, scan_case
+from knobs import knob, knob_get  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -106,17 +107,17 @@ def test_scan_record_sort_path(dev):
     rng = random.Random(9)
     runs = _big_runs(rng, 5, 2000, 8000)
     runs.append(fmt.encode_run(list(reversed([(True, f"user{i:08d}".encode(), b"q") for i in range(300)]))))
-    old = os.environ.get("SKV_SORT")
-    os.environ["SKV_SORT"] = "1"
+    old = knob_get("SKV_SORT")
+    knob("SKV_SORT", "1")
     try:
         for mx in (3, 500, 10000):
             for start in (b"", b"user00004000"):
                 assert norm_dev(dev, runs, start, mx) == norm_oracle(pyoracle, runs, start, mx), (mx, start)
     finally:
         if old is None:
-            os.environ.pop("SKV_SORT", None)
+            knob("SKV_SORT", None)
         else:
-            os.environ["SKV_SORT"] = old
+            knob("SKV_SORT", old)
 
 
 def test_scan_more_runs_than_the_splitter_merge_takes(dev):

@@ -16,6 +16,7 @@ from skv import format as fmt
 from skv.api import Compactor
 
 from test_gpu_parity import _case, _diff, _run_both
+from knobs import knob, knob_get  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -35,8 +36,8 @@ def dev():
 
 @pytest.fixture
 def forced_sort(monkeypatch):
-    monkeypatch.setenv("SKV_SORT", "1")
-    monkeypatch.setenv("SKV_FUSED", "0")
+    knob("SKV_SORT", "1")
+    knob("SKV_FUSED", "0")
 
 
 def _check(dev, streams, max_size, flags, expect_sorted=True):
@@ -178,9 +179,9 @@ def test_bucket_levels_at_small_sizes(dev, monkeypatch, nt, two, gmax):
     global table when a chunk spans more than SKV_SB_GMAX groups), with 0 the one-pass search
     through the global discriminators. WAL keys, long shared prefixes, tie runs past the sort word, an equal-key flood
     and variable keys with tombstones, all against the oracle."""
-    monkeypatch.setenv("SKV_SB_NT", nt)
-    monkeypatch.setenv("SKV_SORT_TWO_PASS", two)
-    monkeypatch.setenv("SKV_SB_GMAX", gmax)
+    knob("SKV_SB_NT", nt)
+    knob("SKV_SORT_TWO_PASS", two)
+    knob("SKV_SB_GMAX", gmax)
     _check(dev, gen.config5(n_streams=2000), 4 * MiB, _abi.SKV_SPLIT_BY_TABLE)
     r = random.Random(9)
     base = "tenant-0001/namespace/partition-000/"
@@ -263,8 +264,8 @@ def _prefix_keys_streams(n_streams=12, per=300, seed=11):
 
 
 def test_fp_shortcut_collisions_are_caught(dev, monkeypatch):
-    monkeypatch.setenv("SKV_FUSED", "0")
-    monkeypatch.setenv("SKV_FP_TEST", "1")
+    knob("SKV_FUSED", "0")
+    knob("SKV_FP_TEST", "1")
     streams = _prefix_keys_streams()
     _check(dev, streams, 1 << 16, 0, expect_sorted=False)
     assert dev.timings()["fp_rerun"] == 1, "forced collisions were not detected"
@@ -275,7 +276,7 @@ def test_fp_collisions_caught_by_the_gather(dev, monkeypatch):
     """Every forced collision pairs a survivor with the one record dropped after it (two keys per
     16-byte prefix, in different streams): only k_gather's in-gather verify (TileOut::m_dup) sees
     them. With SKV_FP_GATHER=0 the same pairs go to k_fp_verify. Both detect and rerun exactly."""
-    monkeypatch.setenv("SKV_FUSED", "0")
+    knob("SKV_FUSED", "0")
     r = random.Random(21)
     prefixes = sorted({f"p{r.randrange(10**12):015d}" for _ in range(3000)})
     a = fmt.encode_run([fmt.put(p + "aaaa", b"A") for p in prefixes])
@@ -283,17 +284,17 @@ def test_fp_collisions_caught_by_the_gather(dev, monkeypatch):
     c = fmt.encode_run([fmt.put(p + "aaaa", b"C") for p in prefixes[1::2]])  # real duplicates, other prefixes
     streams = [(3, [a]), (2, [b]), (1, [c])]
     for gather in ("1", "0"):
-        monkeypatch.setenv("SKV_FP_GATHER", gather)
-        monkeypatch.setenv("SKV_FP_TEST", "1")
+        knob("SKV_FP_GATHER", gather)
+        knob("SKV_FP_TEST", "1")
         _check(dev, streams, 1 << 16, 0, expect_sorted=False)
         assert dev.timings()["fp_rerun"] == 1, f"SKV_FP_GATHER={gather}: forced collisions not detected"
-        monkeypatch.setenv("SKV_FP_TEST", "0")
+        knob("SKV_FP_TEST", "0")
         _check(dev, streams, 1 << 16, 0, expect_sorted=False)
         assert dev.timings()["fp_rerun"] == 0
 
 
 def test_fp_shortcut_no_rerun_on_real_fingerprints(dev, monkeypatch):
-    monkeypatch.setenv("SKV_FUSED", "0")
+    knob("SKV_FUSED", "0")
     for streams, mx, fl in ((_prefix_keys_streams(), 1 << 16, 0),
                             (gen.config3(n_streams=32, run_bytes=64 * 1024, vsize=16), 1 << 18, 0),
                             (gen.config3(n_streams=32, run_bytes=64 * 1024, vsize=16), 1 << 18, 1),
@@ -305,28 +306,6 @@ def test_fp_shortcut_no_rerun_on_real_fingerprints(dev, monkeypatch):
 def test_fp_shortcut_wal_collisions(dev, monkeypatch):
     """WAL split after a merge whose fingerprints all collide (config-5 keys: one 16-byte prefix
     per table): the WAL stage must see the rerun's exact merge."""
-    monkeypatch.setenv("SKV_FP_TEST", "1")
+    knob("SKV_FP_TEST", "1")
     _check(dev, gen.config5(n_streams=40), 4 * MiB, _abi.SKV_SPLIT_BY_TABLE, expect_sorted=False)
     assert dev.timings()["fp_rerun"] == 1
-
-
-def test_fp_verify_in_pieces(dev, monkeypatch):
-    """Level 0 merged in four launches with each piece's pairs verified beside the next piece
-    (SKV_FP_PIECE_MIN=1 forces the split on small calls): exact output with real fingerprints,
-    and forced collisions (SKV_FP_TEST=1) caught wherever the colliding pairs fall."""
-    monkeypatch.setenv("SKV_FUSED", "0")
-    monkeypatch.setenv("SKV_FP_PIECE_MIN", "1")
-    cases = ((gen.config3(n_streams=64, run_bytes=256 * 1024, vsize=16), 1 << 18, 0),
-             (gen.config3(n_streams=64, run_bytes=256 * 1024, vsize=16), 1 << 18, _abi.SKV_DROP_TOMBSTONES),
-             (_prefix_keys_streams(), 1 << 16, 0))
-    for streams, mx, fl in cases:
-        _check(dev, streams, mx, fl, expect_sorted=False)
-        assert dev.timings()["fp_rerun"] == 0
-    monkeypatch.setenv("SKV_FP_TEST", "1")
-    for streams, mx, fl in cases:  # (config 3 keys rarely tie on prefix and length: exact either way)
-        _check(dev, streams, mx, fl, expect_sorted=False)
-    many = _prefix_keys_streams(n_streams=64, per=1000, seed=12)  # ~20 tiles, colliding everywhere
-    for fl in (0, _abi.SKV_DROP_TOMBSTONES):
-        _check(dev, many, 1 << 16, fl, expect_sorted=False)
-        assert dev.timings()["fp_rerun"] == 1, "forced collisions were not detected"
-    _check(dev, gen.config5(n_streams=40), 4 * MiB, _abi.SKV_SPLIT_BY_TABLE, expect_sorted=False)

@@ -14,6 +14,7 @@ from skv.api import Compactor
 
 import pyoracle
 from test_gpu_parity import _diff, _run_both
+from knobs import knob, knob_get  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 KiB, MiB = 1 << 10, 1 << 20
@@ -33,15 +34,13 @@ class _env:
         self.kv = {k: str(v) for k, v in kv.items()}
 
     def __enter__(self):
-        self.old = {k: os.environ.get(k) for k in self.kv}
-        os.environ.update(self.kv)
+        self.old = {k: knob_get(k) for k in self.kv}
+        for k, v in self.kv.items():
+            knob(k, v)
 
     def __exit__(self, *a):
         for k, v in self.old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+            knob(k, v)
 
 
 def _plan(err):

@@ -1,4 +1,4 @@
-"""k_tile<true> phase ticks (a SKV_TILE_PROF=1 build, SKV_LIB=...): config 3 (256 streams x
+"""k_tile<true> (or, with a second argument 2A / 2B, k_fx_tile) phase ticks (a SKV_TILE_PROF=1 build, SKV_LIB=...): config 3 (256 streams x
 --run-mib MiB, built in HBM), 1 warm-up + 3 calls of skv_compact_dev; the phase sums are printed
 by skv_ctx_destroy on stderr (100 MHz ticks summed over tiles; phases: 0 segments, 1 loads,
 2 merge, 3 first-per-key, 4 meta/address by position, 5 filter + scans, 6 look-back, 7 emit)."""
@@ -16,7 +16,12 @@ from skv.devgen import make_cfg3_full_on_device  # noqa: E402
 
 run_mib = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 dev = torch.device("cuda:0")
-runs = make_cfg3_full_on_device(dev, 0x5EEDC0DE, 256, run_mib)
+if len(sys.argv) > 2 and sys.argv[2] in ("2A", "2B"):  # the fused path (k_fx_tile's phases)
+    from skv.devgen import make_cfg2_on_device
+
+    runs = make_cfg2_on_device(dev, 0x5EEDC0DE, 64, 238821, 256, sys.argv[2][1])
+else:
+    runs = make_cfg3_full_on_device(dev, 0x5EEDC0DE, 256, run_mib)
 table = [(s + 1, [(r.data_ptr(), r.numel())]) for s, r in enumerate(runs)]
 comp = Compactor(0, profiling=True)
 for i in range(4):
