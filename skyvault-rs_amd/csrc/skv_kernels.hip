@@ -1367,7 +1367,7 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
     // (key16), el_fp the sort words by position (wd; fingerprints are read from O.key_fp on ties)
     ulong2* key16 = (ulong2*)smem;
     uint64_t* wd = el_fp;
-    const bool wpath = L0 && O.act_hi == nullptr;
+    const bool wpath = !L0 || O.act_hi == nullptr;  // (sample tiles too: level > 0, exact compares)
     uint32_t* cbA = (uint32_t*)(posof + TILE_CAP);
     uint32_t* cbB = cbA + (k + 1);
     uint64_t* ws = (uint64_t*)(((uintptr_t)(cbB + (k + 1)) + 15) & ~(uintptr_t)15);
@@ -1382,6 +1382,7 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         return;
     }
     uint64_t t = blockIdx.x;
+    if (!L0 && threadIdx.x == 0) s_flag[24] = s_flag[25] = s_flag[26] = s_flag[27] = 0;  // (barriers follow)
     if (L0) {  // level 0 tiles take tickets in start order (tile_lookback's progress guarantee)
         if (threadIdx.x == 0) {
             s_tk = atomicAdd(O.tcounter, 1u);
@@ -1614,7 +1615,17 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         }
     }
     if (!L0) {
-        tile_output_samples(n, hp, mi, el_lo, el_c, base, O);
+        if (wpath) {  // sorted samples from key16 / el_c by id
+            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+                const uint32_t e = mi[i];
+                const ulong2 kk = key16[e];
+                O.ohi[base + i] = kk.x;
+                O.olo[base + i] = kk.y;
+                O.oc[base + i] = el_c[e];
+            }
+        } else {
+            tile_output_samples(n, hp, mi, el_lo, el_c, base, O);
+        }
         return;
     }
     TPROF(2);
