@@ -226,12 +226,12 @@ __global__ void k_wal_desc(const uint64_t* __restrict__ NTp, const uint64_t* __r
 // [version byte,] marker, key_len and the source body after the prefix) go to LDS; the
 // workgroup's output span is contiguous (kept tables are), and each lane then composes whole
 // 16-byte output blocks from the pieces (bytewise only at the span's two edges).
-constexpr int WAL_G = 256;
-static_assert(WAL_G == (int)WAL_FUSED_G, "k_wal_fused's workgroup size (host look-back sizing)");
+constexpr int WAL_G = 256;  // k_wal_gather's merged records (and threads) per workgroup
 
 // bytes [x0, x1) of output block B, starting inside kept record r
+template <typename HL>
 __device__ uint4 wal_compose(uint64_t B, uint64_t x0, uint64_t x1, uint32_t r, const uint64_t* os,
-                             const uint64_t* src, const uint64_t* head, const uint32_t* hl) {
+                             const uint64_t* src, const uint64_t* head, const HL* hl) {
     uint4 acc = make_uint4(0, 0, 0, 0);
     uint64_t x = x0;
     while (x < x1) {
@@ -428,9 +428,45 @@ __device__ __forceinline__ WalRec wal_parse_pfx(uint64_t hi, uint64_t lo, uint32
     return r;
 }
 
+// SKV_WAL_PROBE (diagnostic builds, output invalid by design): phase knockouts of k_wal_fused --
+// 1 no look-back wait (the predecessor's slot as read once: offsets stay in bounds), 2 no output
+// bytes, 4 no key parse (the element's fields as a canonical key)
+#ifndef SKV_WAL_PROBE
+#define SKV_WAL_PROBE 0
+#endif
 constexpr uint32_t WF_BADKEY = 1, WF_ORDER = 2, WF_TABLES = 4;
+// WF_R merged records per thread, strided (record k*WAL_T + tid of the workgroup's WF_G): one
+// look-back per WF_G records (at one record per thread the look-back wait was 1.85 of 7.0 ms at
+// config 5, profiles/r06/wal_probe.txt)
+constexpr int WAL_T = 256, WF_R = SKV_WAL_RPT, WF_G = WAL_T * WF_R;
+static_assert(WF_G == (int)WAL_FUSED_G, "k_wal_fused's records per workgroup (host look-back sizing)");
 constexpr uint32_t WF_TBL = 4096;  // output blocks of a workgroup's span with a piece table (64 KiB)
-static_assert(WAL_G <= 256, "piece ids in the block table are bytes");
+static_assert(WF_G <= 65536, "piece ids in the block table are 16-bit");
+#ifndef SKV_WAL_WPE
+#define SKV_WAL_WPE 4  // k_wal_fused's waves per SIMD asked of the register allocator
+#endif
+constexpr int WF_NB = 4;                 // a body's aligned 16-byte blocks loaded before the look-back
+constexpr uint32_t WF_STAGE = 64 * WF_G;  // LDS staging bytes (64 per record); the piece arrays share it
+static_assert(8 * (WF_G + 1) + 16 * WF_G + 2 * WF_TBL + WF_G <= WF_STAGE, "piece arrays fit the stage area");
+
+// bytes 0..n-1 of v (n <= 16) to LDS bytes d..d+n-1 of a zeroed area: dwords a neighbouring piece
+// shares are ORed in, whole dwords stored
+__device__ __forceinline__ void lds_or16(uint32_t* buf, uint32_t d, uint4 v, uint32_t n) {
+    const uint32_t sh = d & 3;
+    uint32_t* p = buf + (d >> 2);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t x[5];
+    x[0] = w[0] << (8 * sh);
+#pragma unroll
+    for (int i = 1; i < 4; ++i) x[i] = (uint32_t)((((uint64_t)w[i] << 32) | w[i - 1]) >> (32 - 8 * sh));
+    x[4] = sh ? w[3] >> (32 - 8 * sh) : 0u;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t m = dword_mask(sh, sh + n, (uint32_t)i);
+        if (m == 0xFFFFFFFFu) p[i] = x[i];
+        else if (m) atomicOr(&p[i], x[i] & m);
+    }
+}
 struct WalPrev {
     int64_t tid;
     uint64_t size, rp;
@@ -438,115 +474,209 @@ struct WalPrev {
     bool canon;
 };
 
-__global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ m_src,
+__global__ void __launch_bounds__(WAL_T) __attribute__((amdgpu_waves_per_eu(SKV_WAL_WPE))) k_wal_fused(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ m_src,
                                                      const uint64_t* __restrict__ P, const uint64_t* __restrict__ Dp,
                                                      uint8_t* out, uint64_t* tstate, uint32_t* ticket, uint32_t* fail,
                                                      WalTStart* tlist, uint32_t* tcount, uint32_t tcap,
                                                      uint64_t* tail, uint32_t diag,
                                                      const SElem* __restrict__ S, const uint32_t* __restrict__ m_rec) {
-    __shared__ uint64_t os[WAL_G + 1], src[WAL_G], head[WAL_G];
-    __shared__ uint32_t hl[WAL_G];
-    __shared__ uint64_t s_w[WAL_G / 64], s_base[1];
-    __shared__ WalPrev s_prev[WAL_G / 64];  // each wave's last record, for the next wave's lane 0
-    __shared__ uint8_t s_tbl[WF_TBL];
+    constexpr int NW = WAL_T / 64;
+    // the output staging area; a span too long for it composes from the pieces (arrays carved from it)
+    __shared__ uint4 s_stage[WF_STAGE / 16];
+    uint64_t* os = (uint64_t*)s_stage;  // [WF_G + 1]
+    uint64_t* src = os + WF_G + 1;
+    uint64_t* head = src + WF_G;
+    uint16_t* s_tbl = (uint16_t*)(head + WF_G);  // [WF_TBL]
+    uint8_t* hl = (uint8_t*)(s_tbl + WF_TBL);    // [WF_G]
+    __shared__ uint64_t s_w[WF_R][NW], s_base[1];
+    __shared__ WalPrev s_prev[WF_R][NW];  // each wave's last record (per k), for the next wave's lane 0
     __shared__ uint32_t s_t;
     const uint64_t K = *Kp;
     if (threadIdx.x == 0) s_t = atomicAdd(ticket, 1u);
     __syncthreads();
     const uint64_t t = s_t;
-    const uint64_t j0 = t * WAL_G;
+    const uint64_t j0 = t * WF_G;
     if (j0 >= K) return;  // (tickets past the last workgroup: nothing to publish)
-    const uint64_t j = j0 + threadIdx.x;
-    const bool live = j < K;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    WalRec r{};
-    const uint8_t* rp = nullptr;
+    WalRec r[WF_R];
+    const uint8_t* rp[WF_R];
+    uint64_t p0[WF_R], p1[WF_R], d0[WF_R], d1[WF_R];
     uint32_t bad = 0;
-    if (live) {
-        rp = (const uint8_t*)m_src[j];
-        bool ok = false;
-        if (S) {  // the record sort's element: its key prefix, no record line read for the parse
-            const SElem e = S[m_rec[j]];
-            r = wal_parse_pfx(e.hi, e.lo, e.klen, Dp[j + 1] != Dp[j] ? 2u : 1u, P[j + 1] - P[j], ok);
+    // every load of the WF_R records first (independent), then the parses
+#pragma unroll
+    for (int k = 0; k < WF_R; ++k) {
+        const uint64_t j = j0 + (uint64_t)k * WAL_T + threadIdx.x;
+        rp[k] = nullptr;
+        p0[k] = p1[k] = d0[k] = d1[k] = 0;
+        if (j < K) {
+            rp[k] = (const uint8_t*)m_src[j];
+            p0[k] = P[j];
+            p1[k] = P[j + 1];
+            d0[k] = Dp[j];
+            d1[k] = Dp[j + 1];
         }
-        if (!ok) r = wal_parse(rp, P[j + 1] - P[j]);
-        if (r.err || ((diag & WAL_STRICT_CANON) && !r.canon)) bad |= WF_BADKEY;
     }
-    // the record before: the neighbouring lane; a wave's lane 0 takes the previous wave's last lane
-    // through LDS, and only the workgroup's first record parses its predecessor again
-    if (lane == 63) {
-        s_prev[wv].tid = r.tid;
-        s_prev[wv].strip = r.strip;
-        s_prev[wv].klen = r.klen;
-        s_prev[wv].canon = r.canon;
-        s_prev[wv].size = r.size;
-        s_prev[wv].rp = (uint64_t)rp;
+    SElem e[WF_R];
+    uint4 pb[WF_R][WF_NB];
+    bool pre[WF_R];
+    if (S) {
+#pragma unroll
+        for (int k = 0; k < WF_R; ++k) {
+            const uint64_t j = j0 + (uint64_t)k * WAL_T + threadIdx.x;
+            if (j < K) e[k] = S[m_rec[j]];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < WF_R; ++k) {
+        const uint64_t j = j0 + (uint64_t)k * WAL_T + threadIdx.x;
+        r[k] = WalRec{};
+        if (j < K) {
+            bool ok = false;
+            if (S) {  // the record sort's element: its key prefix, no record line read for the parse
+                if (SKV_WAL_PROBE & 4) {
+                    r[k].size = p1[k] - p0[k];
+                    r[k].marker = d1[k] != d0[k] ? 2u : 1u;
+                    r[k].klen = e[k].klen;
+                    r[k].tid = (int64_t)(e[k].hi >> 56);
+                    r[k].strip = 2;
+                    r[k].canon = true;
+                    r[k].err = 0;
+                    ok = true;
+                } else {
+                    r[k] = wal_parse_pfx(e[k].hi, e[k].lo, e[k].klen, d1[k] != d0[k] ? 2u : 1u, p1[k] - p0[k], ok);
+                }
+            }
+            if (!ok) r[k] = wal_parse(rp[k], p1[k] - p0[k]);
+            if (r[k].err || ((diag & WAL_STRICT_CANON) && !r[k].canon)) bad |= WF_BADKEY;
+        }
+        // the record before: the neighbouring lane; a wave's lane 0 takes the previous wave's last
+        // lane (of the same k, or of k - 1 for the workgroup's thread 0) through LDS
+        if (lane == 63) {
+            WalPrev& q = s_prev[k][wv];
+            q.tid = r[k].tid;
+            q.strip = r[k].strip;
+            q.klen = r[k].klen;
+            q.canon = r[k].canon;
+            q.size = r[k].size;
+            q.rp = (uint64_t)rp[k];
+        }
     }
     __syncthreads();
-    int64_t ptid = __shfl_up(r.tid, 1, 64);
-    uint32_t pstrip = __shfl_up(r.strip, 1, 64), pklen = __shfl_up(r.klen, 1, 64);
-    bool pcanon = __shfl_up(r.canon ? 1 : 0, 1, 64) != 0;
-    uint64_t psize = __shfl_up(r.size, 1, 64);
-    const uint8_t* prp = (const uint8_t*)__shfl_up((uint64_t)rp, 1, 64);
-    if (lane == 0 && wv > 0) {
-        const WalPrev& q = s_prev[wv - 1];
-        ptid = q.tid;
-        pstrip = q.strip;
-        pklen = q.klen;
-        pcanon = q.canon;
-        psize = q.size;
-        prp = (const uint8_t*)q.rp;
-    }
-    if (live && threadIdx.x == 0 && j > 0) {
-        prp = (const uint8_t*)m_src[j - 1];
-        const WalRec q = wal_parse(prp, P[j] - P[j - 1]);
-        ptid = q.tid;
-        pstrip = q.strip;
-        pklen = q.klen;
-        pcanon = q.canon;
-        psize = q.size;
-        if (q.err) bad |= WF_BADKEY;
-    }
-    const bool nw = live && (j == 0 || ptid != r.tid);
-    if (live && !nw && !(pcanon && r.canon)) {  // stripped keys must ascend inside a table
-        const uint8_t* ka = prp + 5 + pstrip;
-        const uint8_t* kb = rp + 5 + r.strip;
-        const uint64_t la = pklen - pstrip, lb = r.klen - r.strip;
-        const uint64_t n = la < lb ? la : lb;
-        int c = bytes_cmp16(ka, kb, n);
-        if (!c) c = la < lb ? -1 : (la > lb ? 1 : 0);
-        if (c >= 0) bad |= WF_ORDER;
+    uint64_t wo[WF_R], wi[WF_R];
+    bool nw[WF_R];
+#pragma unroll
+    for (int k = 0; k < WF_R; ++k) {
+        const uint64_t j = j0 + (uint64_t)k * WAL_T + threadIdx.x;
+        const bool live = j < K;
+        int64_t ptid = __shfl_up(r[k].tid, 1, 64);
+        uint32_t pstrip = __shfl_up(r[k].strip, 1, 64), pklen = __shfl_up(r[k].klen, 1, 64);
+        bool pcanon = __shfl_up(r[k].canon ? 1 : 0, 1, 64) != 0;
+        uint64_t psize = __shfl_up(r[k].size, 1, 64);
+        const uint8_t* prp = (const uint8_t*)__shfl_up((uint64_t)rp[k], 1, 64);
+        if (lane == 0 && (wv > 0 || k > 0)) {
+            const WalPrev& q = wv > 0 ? s_prev[k][wv - 1] : s_prev[k > 0 ? k - 1 : 0][NW - 1];
+            ptid = q.tid;
+            pstrip = q.strip;
+            pklen = q.klen;
+            pcanon = q.canon;
+            psize = q.size;
+            prp = (const uint8_t*)q.rp;
+        }
+        if (live && threadIdx.x == 0 && k == 0 && j > 0) {  // only the workgroup's first record parses its predecessor
+            prp = (const uint8_t*)m_src[j - 1];
+            const WalRec q = wal_parse(prp, P[j] - P[j - 1]);
+            ptid = q.tid;
+            pstrip = q.strip;
+            pklen = q.klen;
+            pcanon = q.canon;
+            psize = q.size;
+            if (q.err) bad |= WF_BADKEY;
+        }
+        nw[k] = live && (j == 0 || ptid != r[k].tid);
+        if (live && !nw[k] && !(pcanon && r[k].canon)) {  // stripped keys must ascend inside a table
+            const uint8_t* ka = prp + 5 + pstrip;
+            const uint8_t* kb = rp[k] + 5 + r[k].strip;
+            const uint64_t la = pklen - pstrip, lb = r[k].klen - r[k].strip;
+            const uint64_t n = la < lb ? la : lb;
+            int c = bytes_cmp16(ka, kb, n);
+            if (!c) c = la < lb ? -1 : (la > lb ? 1 : 0);
+            if (c >= 0) bad |= WF_ORDER;
+        }
+        if (nw[k] && live) {  // table starts go to the unordered list
+            const uint32_t x = atomicAdd(tcount, 1u);
+            if (x < tcap) {
+                WalTStart ts;
+                ts.b = j;
+                ts.W = 0;  // (filled below, once the output offset is known)
+                ts.Dp = d0[k];
+                ts.tid = r[k].tid;
+                ts.nk = r[k].klen - r[k].strip;
+                ts.prev_nk = j ? pklen - pstrip : 0;
+                ts.prev_ws = j ? psize - pstrip : 0;
+                tlist[x] = ts;
+                p0[k] = x;  // (p0 no longer needed: the list slot)
+            } else {
+                atomicOr(fail, WF_TABLES);
+                p0[k] = ~0ull;
+            }
+        }
+        // output bytes of record j: its version byte (a table start) + its stripped record. The
+        // exclusive prefix of those is where its piece starts, and a table's version byte sits where
+        // its first record's piece starts, so one sum places everything (no separate table-start count).
+        wo[k] = live ? r[k].size - r[k].strip + (nw[k] ? 1 : 0) : 0;
+        wi[k] = wo[k];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t a = __shfl_up(wi[k], d, 64);
+            if (lane >= d) wi[k] += a;
+        }
+        if (lane == 63) s_w[k][wv] = wi[k];
     }
     if (bad) atomicOr(fail, bad);
-    const uint64_t ws = live ? r.size - r.strip : 0;
-    // output bytes of record j: its version byte (a table start) + its stripped record. The exclusive
-    // prefix of those is where its piece starts, and a table's version byte sits where its first
-    // record's piece starts, so one sum places everything (no separate table-start count).
-    const uint64_t wo = ws + (nw ? 1 : 0);
-    uint64_t wi = wo;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t a = __shfl_up(wi, d, 64);
-        if (lane >= d) wi += a;
-    }
-    if (lane == 63) s_w[wv] = wi;
     __syncthreads();
-    uint64_t wb = 0, wt = 0;
-    for (int w = 0; w < WAL_G / 64; ++w) {
-        if (w < wv) wb += s_w[w];
-        wt += s_w[w];
+    uint64_t wb[WF_R], wt = 0;
+#pragma unroll
+    for (int k = 0; k < WF_R; ++k) {
+        wb[k] = wt;
+        for (int w = 0; w < NW; ++w) {
+            if (w < wv) wb[k] += s_w[k][w];
+            wt += s_w[k][w];
+        }
     }
-    // decoupled look-back over workgroups (ticket order); wave 0 reads 64 predecessors per step --
-    // workgroups are short, so chains of aggregates are long
+    const bool staged = wt + 32 <= WF_STAGE;
+    if (staged)
+        for (uint32_t i = threadIdx.x; i < WF_STAGE / 16; i += WAL_T) s_stage[i] = make_uint4(0, 0, 0, 0);
+    // decoupled look-back over workgroups (ticket order); wave 0 reads 64 predecessors per step.
+    // The aggregate goes out before any record body is read: a successor's look-back waits on it
+    constexpr uint64_t FA = 1ull << 62, FI = 2ull << 62, VM = FA - 1;
+    if (threadIdx.x == 0) __hip_atomic_store(&tstate[t], (t == 0 ? FI : FA) | wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the bodies' aligned 16-byte blocks, loaded now so their lines arrive during the look-back (a
+    // body of more than WF_NB blocks is loaded when it is written)
+#pragma unroll
+    for (int k = 0; k < WF_R; ++k) {
+        const uint64_t j = j0 + (uint64_t)k * WAL_T + threadIdx.x;
+        pre[k] = false;
+        if (staged && j < K) {
+            const uintptr_t sa = (uintptr_t)rp[k] + 5 + r[k].strip, a0 = sa & ~(uintptr_t)15;
+            const uint64_t L = r[k].size - 5 - r[k].strip;
+            pre[k] = (sa & 15) + L <= 16 * WF_NB;
+            if (pre[k]) {
+#pragma unroll
+                for (int i = 0; i < WF_NB; ++i)
+                    if (a0 + 16 * i < sa + L) pb[k][i] = *(const uint4*)(a0 + 16 * i);
+            }
+        }
+    }
     if (threadIdx.x < 64) {
-        constexpr uint64_t FA = 1ull << 62, FI = 2ull << 62, VM = FA - 1;
         uint64_t acc = 0;
-        if (t == 0) {
-            if (lane == 0) __hip_atomic_store(&tstate[0], FI | wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0) __hip_atomic_store(&tstate[t], FA | wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t > 0) {
             int64_t top = (int64_t)t - 1;
-            for (;;) {
+            if (SKV_WAL_PROBE & 1) {  // one read: an inclusive, an aggregate or 0, all <= the true prefix
+                acc = lane == 0 ? (__hip_atomic_load(&tstate[top], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & VM) : 0;
+                acc = __shfl(acc, 0, 64);
+                top = -1;
+            }
+            for (; top >= 0;) {
                 const int64_t p = top - lane;
                 const uint64_t v = p >= 0 ? __hip_atomic_load(&tstate[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : FI;
                 const uint64_t f = v >> 62;
@@ -569,61 +699,94 @@ __global__ void __launch_bounds__(WAL_G) k_wal_fused(const uint64_t* __restrict_
         if (lane == 0) s_base[0] = acc;
     }
     __syncthreads();
-    const uint64_t ostart = s_base[0] + wb + wi - wo;  // this record's piece (version byte first if nw)
-    if (live && j + 1 == K) {
-        tail[0] = ostart + wo;  // output bytes of the whole call
-        tail[1] = ws;
-        tail[2] = r.klen - r.strip;
-        tail[4] = Dp[j + 1];    // deletes of all records
-    }
-    if (nw) {
-        const uint32_t e = atomicAdd(tcount, 1u);
-        if (e < tcap) {
-            WalTStart x;
-            x.b = j;
-            x.W = ostart;
-            x.Dp = Dp[j];
-            x.tid = r.tid;
-            x.nk = r.klen - r.strip;
-            x.prev_nk = j ? pklen - pstrip : 0;
-            x.prev_ws = j ? psize - pstrip : 0;
-            tlist[e] = x;
+    const uint32_t c = (uint32_t)(K - j0 < (uint64_t)WF_G ? K - j0 : (uint64_t)WF_G);
+    const uint64_t Blo = s_base[0] & ~15ull;
+    uint32_t* stg = (uint32_t*)s_stage;
+#pragma unroll
+    for (int k = 0; k < WF_R; ++k) {
+        const uint64_t j = j0 + (uint64_t)k * WAL_T + threadIdx.x;
+        if (j >= K) continue;
+        const uint32_t q = (uint32_t)k * WAL_T + threadIdx.x;
+        const uint64_t ostart = s_base[0] + wb[k] + wi[k] - wo[k];  // this record's piece (version byte first if nw)
+        if (j + 1 == K) {
+            tail[0] = ostart + wo[k];  // output bytes of the whole call
+            tail[1] = r[k].size - r[k].strip;
+            tail[2] = r[k].klen - r[k].strip;
+            tail[4] = d1[k];           // deletes of all records
+        }
+        if (nw[k] && p0[k] != ~0ull) tlist[p0[k]].W = ostart;
+        // the output piece: [version byte,] marker, new key_len, then the record body past the prefix
+        const uint32_t nk = r[k].klen - r[k].strip;
+        const uint64_t h5 = (uint64_t)r[k].marker | ((uint64_t)(nk >> 24) << 8) | ((uint64_t)((nk >> 16) & 0xFF) << 16) |
+                            ((uint64_t)((nk >> 8) & 0xFF) << 24) | ((uint64_t)(nk & 0xFF) << 32);
+        const uint64_t hd = nw[k] ? (1ull | (h5 << 8)) : h5;
+        const uint32_t hn = nw[k] ? 6u : 5u;
+        const uintptr_t sa = (uintptr_t)rp[k] + 5 + r[k].strip;
+        if (staged) {
+            const uint32_t d = (uint32_t)(ostart - Blo), db = d + hn;
+            const uint64_t L = r[k].size - 5 - r[k].strip;
+            lds_or16(stg, d, make_uint4((uint32_t)hd, (uint32_t)(hd >> 32), 0u, 0u), hn);
+            if (pre[k]) {
+                const uint32_t s0 = (uint32_t)(sa & 15);
+#pragma unroll
+                for (int i = 0; i < WF_NB; ++i) {
+                    const uint64_t gs = 16 * (uint64_t)i;  // block i's first byte, relative to sa's block
+                    if (gs >= s0 + L) break;
+                    const uint32_t lb = i == 0 ? s0 : 0u;
+                    const uint32_t hb = (uint32_t)(s0 + L - gs < 16 ? s0 + L - gs : 16);
+                    lds_or16(stg, (uint32_t)(db + gs + lb - s0), i == 0 ? funnel16(pb[k][0], make_uint4(0, 0, 0, 0), s0) : pb[k][i],
+                             hb - lb);
+                }
+            } else {
+                for (uint64_t o = 0; o < L; o += 16) {
+                    const uint32_t m = (uint32_t)(L - o < 16 ? L - o : 16);
+                    lds_or16(stg, (uint32_t)(db + o), load_window16((const uint8_t*)sa + o, m), m);
+                }
+            }
         } else {
-            atomicOr(fail, WF_TABLES);
+            os[q] = ostart;
+            src[q] = sa;
+            head[q] = hd;
+            hl[q] = (uint8_t)hn;
+            if (q + 1 == c) os[q + 1] = ostart + wo[k];
         }
     }
-    // the output pieces: [version byte,] marker, new key_len, then the record body past the prefix
-    if (live) {
-        const uint32_t nk = r.klen - r.strip;
-        const uint64_t h5 = (uint64_t)r.marker | ((uint64_t)(nk >> 24) << 8) | ((uint64_t)((nk >> 16) & 0xFF) << 16) |
-                            ((uint64_t)((nk >> 8) & 0xFF) << 24) | ((uint64_t)(nk & 0xFF) << 32);
-        os[threadIdx.x] = ostart;
-        src[threadIdx.x] = (uint64_t)rp + 5 + r.strip;
-        head[threadIdx.x] = nw ? (1ull | (h5 << 8)) : h5;
-        hl[threadIdx.x] = nw ? 6u : 5u;
-        if (j + 1 == K || threadIdx.x + 1 == WAL_G) os[threadIdx.x + 1] = ostart + wo;
+    if (staged) {
+        __syncthreads();
+        if (SKV_WAL_PROBE & 2) return;
+        const uint64_t lo = s_base[0], hi = lo + wt, Bhi = (hi + 15) & ~15ull;
+        for (uint64_t B = Blo + 16ull * threadIdx.x; B < Bhi; B += 16ull * WAL_T) {
+            const uint64_t x0 = B > lo ? B : lo, x1 = B + 16 < hi ? B + 16 : hi;
+            const uint4 v = s_stage[(B - Blo) >> 4];
+            if (x0 == B && x1 == B + 16) {
+                *(uint4*)(out + B) = v;
+            } else {  // span edge: this workgroup's bytes only
+                for (uint64_t y = x0; y < x1; ++y) out[y] = (uint8_t)byte_of(v, (uint32_t)(y - B));
+            }
+        }
+        return;
     }
     __syncthreads();
+    if (SKV_WAL_PROBE & 2) return;
     // consecutive threads compose consecutive aligned output blocks (coalesced stores; a thread per
     // record instead, its blocks in a loop, measured slower: 10.1 vs 8.9 ms at config 5)
-    const uint32_t c = (uint32_t)(K - j0 < WAL_G ? K - j0 : WAL_G);
-    const uint64_t lo = os[0], hi = os[c];
-    const uint64_t Blo = lo & ~15ull, Bhi = (hi + 15) & ~15ull;
+    const uint64_t lo = os[0], hi = os[c];  // (lo = s_base: Blo as above)
+    const uint64_t Bhi = (hi + 15) & ~15ull;
     // block -> piece holding its first byte (lo for the first block), marked by the pieces
     // themselves when the span fits the table; else a binary search over the pieces per block
     const uint64_t q0 = Blo >> 4;
     const bool use_tbl = (Bhi >> 4) - q0 <= WF_TBL;
     if (use_tbl) {
-        if (live) {
-            uint64_t qs = (ostart + 15) >> 4;
-            const uint64_t qe = (ostart + wo + 15) >> 4;
-            if (threadIdx.x == 0) s_tbl[0] = 0;
+        if (threadIdx.x == 0) s_tbl[0] = 0;
+        for (uint32_t q = threadIdx.x; q < c; q += WAL_T) {
+            uint64_t qs = (os[q] + 15) >> 4;
+            const uint64_t qe = (os[q + 1] + 15) >> 4;
             if (qs <= q0) qs = q0 + 1;
-            for (uint64_t q = qs; q < qe; ++q) s_tbl[q - q0] = (uint8_t)threadIdx.x;
+            for (uint64_t b = qs; b < qe; ++b) s_tbl[b - q0] = (uint16_t)q;
         }
         __syncthreads();
     }
-    for (uint64_t B = Blo + 16ull * threadIdx.x; B < Bhi; B += 16ull * WAL_G) {
+    for (uint64_t B = Blo + 16ull * threadIdx.x; B < Bhi; B += 16ull * WAL_T) {
         const uint64_t x0 = B > lo ? B : lo, x1 = B + 16 < hi ? B + 16 : hi;
         uint32_t a = 0;  // last record with os <= x0
         if (use_tbl) {
@@ -649,11 +812,9 @@ void launch_wal_fused(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const u
                       const uint64_t* Dp, uint8_t* out, uint64_t* tstate, uint32_t* ticket, uint32_t* fail,
                       WalTStart* tlist, uint32_t* tcount, uint32_t tcap, uint64_t* tail, uint32_t diag,
                       const SElem* S, const uint32_t* m_rec) {
-    // SKV_WAL_LDS=<bytes>: pad the workgroup's LDS request (caps workgroups per CU: a smaller set of
-    // record lines in flight per XCD, so the composition's re-read can hit L2; occupancy studies)
     if (max_K)
-        k_wal_fused<<<wal_blocks(max_K, WAL_G), WAL_G, 0, s>>>(Kp, m_src, P, Dp, out, tstate, ticket, fail, tlist,
-                                                                  tcount, tcap, tail, diag, S, m_rec);
+        k_wal_fused<<<wal_blocks(max_K, WF_G), WAL_T, 0, s>>>(Kp, m_src, P, Dp, out, tstate, ticket, fail, tlist,
+                                                               tcount, tcap, tail, diag, S, m_rec);
 }
 
 void launch_wal_keys(hipStream_t s, const uint64_t* Kp, uint64_t max_K, const uint64_t* m_src, const uint64_t* P,

@@ -229,7 +229,8 @@ def test_wal_split_matches_oracle(dev):
 def test_wal_one_pass_stage(dev):
     """The one-pass WAL stage (k_wal_fused) where it applies -- sorted streams, good keys, ascending
     stripped keys, every table within max -- and the exact stage where it declines: many tables across
-    many 256-record workgroups, short and long records, Deletes, tables of one record, a table over
+    many 512-record workgroups, short and long records (output staged in LDS, or composed from the
+    record lines where a workgroup's span is past the stage), Deletes, tables of one record, a table over
     max, a bad key, "007.a"
     next to "7.0" (one table whose stripped keys decrease). Every outcome equal to the oracle's."""
     r = random.Random(29)
@@ -243,7 +244,15 @@ def test_wal_one_pass_stage(dev):
                if r.random() < .9 else fmt.delete(k) for k in keys]
         streams.append((s + 1, [fmt.encode_run(ops)]))
     single = [(100, [fmt.encode_run([fmt.put("777.x", b"only")])])]
-    for sts, max_size, stage in ((streams, 4 * MiB, 1), (streams + single, 4 * MiB, 1), (streams, 600, 2)):
+    # long records only: every workgroup's span is past the LDS stage and the block table (the
+    # pieces are composed from the record lines, a binary search per block)
+    longs = []
+    for s in range(3):
+        keys = sorted({f"{r.choice(tables)}.{r.randrange(10**6):06d}" for _ in range(1500)})
+        longs.append((50 + s, [fmt.encode_run([fmt.put(k, bytes(r.randrange(256) for _ in range(r.randrange(150, 400))))
+                                               for k in keys])]))
+    for sts, max_size, stage in ((streams, 4 * MiB, 1), (streams + single, 4 * MiB, 1), (streams, 600, 2),
+                                 (longs, 64 * MiB, 1)):
         exp, got = _run_both(dev, sts, max_size, _abi.SKV_SPLIT_BY_TABLE)
         assert exp == got, _diff(exp, got)
         assert dev.timings()["wal_stage"] == stage
@@ -334,7 +343,7 @@ def test_max_run_size_near_two_to_the_64(dev, max_size, flags):
 def test_wal_one_pass_stage_many_tables(dev):
     """k_wal_fused's table-start list past the readback it reads with the verdict (WF_GUESS = 1024
     starts: the rest comes in a second copy) and past its capacity (WF_TCAP = 65536: the exact stage
-    runs). Tables of one to three records, spread over several streams and many 256-record
+    runs). Tables of one to three records, spread over several streams and many 512-record
     workgroups; the descriptors' min/max key offsets come from the list, so both are compared with
     the oracle byte for byte."""
     r = random.Random(31)
