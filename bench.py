@@ -592,10 +592,18 @@ def main():
         # PMC counters of THIS config's dominant kernel (tools/traffic.py keys them by config and
         # kernel); none recorded -> null with the reason, never another config's counters
         traffic, traffic_note, traffic_rw = None, None, None
+        call_traffic = None
         try:
             with open(args.traffic_json) as f:
                 cfgs = json.load(f).get("configs", {})
             kt = cfgs.get(config, {}).get("kernels", {}).get("skv::" + hot_kernel)
+            ct = cfgs.get(config, {}).get("call")
+            if ct and not (config == "3F" and run_mib_used != 256):
+                # every skv kernel's corrected PMC bytes over one whole call, against the call's I + O
+                call_traffic = {"hbm_bytes": ct["hbm_bytes"], "read_bytes": ct["read_bytes"],
+                                "write_bytes": ct["write_bytes"], "launches": ct["launches"],
+                                "ratio_to_io": round(ct["hbm_bytes"] / max(1, in_bytes + out_bytes), 3),
+                                "source": os.path.relpath(args.traffic_json, ROOT) + f" [configs][{config}][call]"}
             if config == "3F" and run_mib_used != 256:  # the recorded 3F pass is at 256 MiB runs
                 kt, traffic_note = None, f"no --pmc pass recorded for config 3F at {run_mib_used} MiB runs"
             if kt:
@@ -652,6 +660,7 @@ def main():
                 "pipeline_achieved": round((in_bytes + out_bytes) / (ms_per_step * 1e-3) / 1e9, 1),
                 "pipeline_frac": round((in_bytes + out_bytes) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             },
+            "call_traffic": call_traffic,
         }
         line["invariants"] = invariants
         if host_path is not None:

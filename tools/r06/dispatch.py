@@ -5,8 +5,9 @@ restricted to the bench's TIMED compactions (measurement hygiene, VERDICT r05 it
 The bench runs W warm-up compactions, K timed ones and one invariant-check call (bench.py
 timed_loop / check_invariants). Compactions are told apart by the first kernel of each call (the
 kernel named by --first, default: the first skv kernel of the trace): dispatch i starts a new
-compaction when it is that kernel. The first W compactions and everything after the K-th timed one
-are dropped, so per-kernel totals can never exceed the traced ms_per_step.
+compaction when it is that kernel (every m-th occurrence when each call launches it m times,
+m = its count / (W + K + 1)). The first W compactions and everything after the K-th timed one are
+dropped, so per-kernel totals can never exceed the traced ms_per_step.
 
 usage: dispatch.py run_kernel_trace.csv W K [--first NAME] [--out stats.csv] [--top N]"""
 import argparse
@@ -45,9 +46,14 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
     rows.sort()
     first = a.first or rows[0][2]
-    calls, cur = [], None
+    # a call that launches its first kernel m times (config 5: k_run_info twice) starts at every m-th
+    # occurrence; the bench's calls are W warm-ups, K timed and one invariant check
+    m = 1 if a.first else max(1, sum(1 for r in rows if r[2] == first) // (a.W + a.K + 1))
+    calls, cur, seen = [], None, 0
     for s, e, n in rows:
-        if n == first or cur is None:
+        if n == first:
+            seen += 1
+        if (n == first and (seen - 1) % m == 0) or cur is None:
             cur = []
             calls.append(cur)
         cur.append((s, e, n))
