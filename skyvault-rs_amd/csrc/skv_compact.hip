@@ -782,14 +782,19 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         // k_emit parses the records of a chunk in parallel instead of walking its chain again
         const uint32_t slot_cap = (uint32_t)((chunk / 64 + 7) & ~7ull);  // rows of 16-byte groups (walk_fast)
         uint16_t* ch_slots = dbuf<uint16_t>(ctx, "ch_slots", n_chunks * slot_cap);
+        // the walks' staged record arrays (32 bytes per record, chunk / 128 per chunk: a chunk of
+        // shorter records is emitted from the records as before)
+        const uint32_t stg_cap = (uint32_t)((chunk / 128 + 7) & ~7ull);
+        StgRec* ch_stg_rec = dbuf<StgRec>(ctx, "ch_stg_rec", (n_chunks + STG_W - 1) / STG_W * STG_W * stg_cap);
+        uint8_t* ch_stg = dbuf<uint8_t>(ctx, "ch_stg", n_chunks);
         HIPCHK(hipMemsetAsync(bad_bits, 0, (n_chunks / 64 + 1) * 8, st));
         HIPCHK(hipMemsetAsync(first_bad, 0xFF, n_runs * 4, st));
         HIPCHK(hipMemsetAsync(err_chunk, 0xFF, n_runs * 4, st));
         launch_spec(st, d_runs, n_runs, n_chunks, d_hdr, d_fmt, d_broken, ch_start, ch_end, ch_cnt, ch_err,
-                    ctx->exact_utf8, chunk, ch_slots, slot_cap);
+                    ctx->exact_utf8, chunk, ch_slots, slot_cap, ch_stg_rec, stg_cap, ch_stg);
         launch_validate(st, d_runs, n_runs, n_chunks, d_hdr, ch_start, ch_end, ch_err, bad_bits, first_bad);
         launch_fixup(st, d_runs, n_runs, d_hdr, first_bad, bad_bits, ch_start, ch_end, ch_cnt, ch_err,
-                     ctx->exact_utf8, chunk, ch_slots, slot_cap);
+                     ctx->exact_utf8, chunk, ch_slots, slot_cap, ch_stg);
         launch_err_chunk(st, d_runs, n_runs, n_chunks, d_hdr, ch_err, err_chunk);
         launch_mask(st, d_runs, n_runs, n_chunks, d_hdr, err_chunk, ch_cnt, cnt64);
         launch_scan(st, cnt64, n_chunks, ch_rec_base, scan_tmp);
@@ -811,7 +816,8 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         const bool emit_order = !any_fixed && !job.batch;
         launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, any_fixed ? R : 0,
                     rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad, ch_slots, slot_cap, chunk,
-                    ch_end, emit_order ? d_stream_base : nullptr, emit_order ? d_first_dec : nullptr);
+                    ch_end, emit_order ? d_stream_base : nullptr, emit_order ? d_first_dec : nullptr, ch_stg_rec,
+                    stg_cap, ch_stg);
         mark(ctx, PH_PARSE);
         check_and_read(false, emit_order ? ORDER_DONE : ORDER_LAUNCH);
         if (utf8_flag && !ctx->exact_utf8) {  // a key the chunk walks did not check: exact walks

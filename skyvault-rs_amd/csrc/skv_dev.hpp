@@ -335,7 +335,27 @@ struct WalkRes {
     uint64_t end;   // first record start >= stop, or the erroring record's start
     uint32_t cnt;   // records decoded
     uint32_t err;   // DERR_* | extra << 8
+    uint32_t nst;   // records staged (walk_fast<.., true>): the first nst of the chunk
 };
+struct StgRec {  // a walked record's arrays, staged by its chunk slot (32 bytes, two 16-byte stores)
+    uint64_t hi, lo;    // key prefix words
+    uint64_t fp;        // fingerprint of the key bytes past 16
+    uint32_t klen_del;  // key length | Delete << 31
+    uint32_t ascii;     // 1: every key byte is ASCII (else k_emit checks the key's UTF-8)
+};
+// Staged entry i of chunk c sits at ((c / STG_W) * scap + i) * STG_W + c % STG_W: the walks of a
+// wave (consecutive chunks, one record per step each) store one contiguous 2 KiB block per step.
+// (A row per chunk put the lanes of a store 16 KiB apart: k_spec 1.2 s instead of 10 ms at 3F.)
+// SKV_STG_PROBE (diagnostic builds, output invalid): 1 no fingerprint in the staging walk, 2 no
+// staged stores (the entries computed, not written)
+#ifndef SKV_STG_PROBE
+#define SKV_STG_PROBE 0
+#endif
+constexpr uint32_t STG_W = 64;
+constexpr uint64_t STG_KMAX = 144;  // longest key the walks stage (two fingerprint steps)
+__device__ __forceinline__ uint64_t stg_base(uint64_t c, uint32_t scap) {
+    return (c / STG_W) * scap * STG_W + c % STG_W;
+}
 
 // runs::read_run_stream's per-record loop (runs.rs:559-626) over [p, stop) of one run, in the
 // reference's check order. max_recs bounds the walk (probe mode).
@@ -525,9 +545,14 @@ __device__ __forceinline__ void window32(const uint8_t* run, uint64_t len, uint6
 }
 
 __device__ __forceinline__ uint32_t sel8(const uint32_t w[8], uint32_t i) {
-    uint32_t r = w[0];
-#pragma unroll
-    for (uint32_t k = 1; k < 8; ++k) r = i == k ? w[k] : r;
+    // the words as register values first: a select chain over the array's loads was folded into one
+    // load at a variable index, which kept the window in scratch (two stores and a dependent load in
+    // every walk step)
+    uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4], x5 = w[5], x6 = w[6], x7 = w[7];
+    asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7));
+    const uint32_t a = (i & 1) ? x1 : x0, b = (i & 1) ? x3 : x2, c = (i & 1) ? x5 : x4, d = (i & 1) ? x7 : x6;
+    const uint32_t e = (i & 2) ? b : a, f = (i & 2) ? d : c;
+    const uint32_t r = (i & 4) ? f : e;
     return i < 8 ? r : 0u;
 }
 
@@ -643,44 +668,6 @@ __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, ui
     return h;
 }
 
-// walk_checked with vectorized headers: one dependent round trip per record. UTF8 = false: the
-// structure only (k_spec's fast mode; k_emit checks the keys and flags a bad one for an exact rerun)
-// slot (cap > 0, a multiple of 8, 16-byte aligned row): the first cap record starts, as offsets
-// from cs (k_emit reads them back), stored eight at a time (one 16-byte store instead of eight
-// 2-byte ones: the single-lane stores were written back as separate partial lines, 7.8 GB at 3F)
-template <int UTF8 = 1, class L = GLoad>
-__device__ inline WalkRes walk_fast(const uint8_t* run, uint64_t len, uint64_t p, uint64_t stop, uint32_t max_recs,
-                                   L ld = L(), uint16_t* slot = nullptr, uint32_t cap = 0, uint64_t cs = 0) {
-    uint32_t cnt = 0;
-    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    auto flush = [&]() {  // the group holding slot cnt - 1 (positions past cnt: unread)
-        if (cap && (cnt & 7) && (cnt & ~7u) < cap) *(uint4*)(slot + (cnt & ~7u)) = make_uint4(s0, s1, s2, s3);
-    };
-    while (p < stop && cnt < max_recs) {
-        RecHdr h = parse_rec<false, UTF8>(run, len, p, ld);
-        if (h.err) {
-            flush();
-            return {p, cnt, h.err};
-        }
-        if (cnt < cap) {
-            const uint32_t j = cnt & 7, v = (uint32_t)(uint16_t)(p - cs) << (16 * (j & 1)), q = j >> 1;
-            s0 |= q == 0 ? v : 0u;
-            s1 |= q == 1 ? v : 0u;
-            s2 |= q == 2 ? v : 0u;
-            s3 |= q == 3 ? v : 0u;
-            if (j == 7) {
-                *(uint4*)(slot + (cnt & ~7u)) = make_uint4(s0, s1, s2, s3);
-                s0 = s1 = s2 = s3 = 0;
-            }
-        }
-        ++cnt;
-        p += h.size;
-    }
-    flush();
-    return {p, cnt, DERR_NONE};
-}
-
-
 // 64-bit fingerprint of the key bytes past the 16-byte prefix (0 for keys of at most 16 bytes),
 // a function of the bytes alone; ascii: those bytes have no high bit
 __device__ __forceinline__ uint64_t fp_mix(uint64_t x) {
@@ -726,6 +713,142 @@ __device__ inline uint64_t key_tail_fp(const uint8_t* key, uint32_t klen, bool& 
     ascii = (acc & 0x80808080u) == 0;
     return h;
 }
+
+// key_tail_fp for a key of at most STG_KMAX bytes with every block load issued up front (the
+// walk's staging: these loads go out with the value length's, so the chain stays one round trip
+// past the header per record); the same function of the bytes as key_tail_fp
+template <class L = GLoad>
+__device__ __forceinline__ uint64_t key_tail_fp_short(const uint8_t* key, uint32_t klen, bool& ascii, L ld = L()) {
+    ascii = true;
+    if (klen <= 16) return 0;
+    const uint32_t n = klen - 16;  // <= STG_KMAX - 16 = 128
+    const uintptr_t a = (uintptr_t)(key + 16);
+    const uintptr_t base = a & ~(uintptr_t)15;
+    const uint32_t sh = (uint32_t)(a & 15);
+    const uint32_t nblk = (sh + n + 15) >> 4;
+    uint4 B[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) B[i] = (uint32_t)i < nblk ? ld(base + 16ull * i) : make_uint4(0, 0, 0, 0);
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        if (16u * w < n) {
+            const uint32_t m = n - 16 * w < 16 ? n - 16 * w : 16;
+            const uint4 v = funnel16(B[w], B[w + 1], sh);
+            const uint32_t a0 = v.x & dword_mask(0, m, 0), a1 = v.y & dword_mask(0, m, 1);
+            const uint32_t a2 = v.z & dword_mask(0, m, 2), a3 = v.w & dword_mask(0, m, 3);
+            acc |= a0 | a1 | a2 | a3;
+            h = fp_mix(h ^ (((uint64_t)a1 << 32) | a0));
+            h = fp_mix(h ^ (((uint64_t)a3 << 32) | a2) ^ 0x2545F4914F6CDD1Dull);
+        }
+    }
+    ascii = (acc & 0x80808080u) == 0;
+    return h;
+}
+
+// parse_rec<true, 0> for the staging walks: the value length's load and the key tail's loads are
+// issued together after the header window; fpv / ascii as key_tail_fp gives them, for keys of at
+// most STG_KMAX bytes (longer keys end the chunk's staging, their fingerprint is not computed)
+template <class L = GLoad>
+__device__ __forceinline__ RecHdr parse_rec_stg(const uint8_t* run, uint64_t len, uint64_t p, uint64_t& fpv,
+                                                bool& ascii, L ld = L()) {
+    RecHdr h;
+    h.size = 0;
+    h.hi = h.lo = 0;
+    fpv = 0;
+    ascii = true;
+    uint32_t w[8];
+    window32(run, len, p, w, ld);
+    h.marker = w[0] & 0xFFu;
+    if (p + 5 > len) { h.err = DERR_IO; h.klen = 0; return h; }
+    h.klen = __builtin_bswap32(__builtin_amdgcn_alignbyte(w[1], w[0], 1));
+    const uint64_t kp = p + 5;
+    if (kp + h.klen > len) { h.err = DERR_KEY; return h; }
+    const uint64_t vo = 5 + h.klen;
+    const bool vload = h.marker == 1 && kp + h.klen + 4 <= len && vo + 4 > 32;
+    const uint4 vv = vload ? load_window16(run + p + vo, 4, ld) : make_uint4(0, 0, 0, 0);
+    if (h.klen <= STG_KMAX && !(SKV_STG_PROBE & 1)) fpv = key_tail_fp_short(run + kp, (uint32_t)h.klen, ascii, ld);
+    uint32_t kd[7];
+    win_key(w, kd);
+    win_prefix(kd, h.klen, h.hi, h.lo);
+    ascii = ascii && ((h.hi | h.lo) & 0x8080808080808080ull) == 0;
+    if (h.marker == 1) {
+        if (kp + h.klen + 4 > len) { h.err = DERR_IO; return h; }
+        const uint64_t vlen = vo + 4 <= 32 ? win_be32(w, (uint32_t)vo) : __builtin_bswap32(vv.x);
+        if (kp + h.klen + 4 + vlen > len) { h.err = DERR_VAL; return h; }
+        h.size = 9 + h.klen + vlen;
+    } else if (h.marker == 2) {
+        h.size = 5 + h.klen;
+    } else {
+        h.err = !utf8_valid_fast(run + kp, h.klen, ld) ? DERR_UTF8 : DERR_MARKER | (h.marker << 8);
+        return h;
+    }
+    h.err = DERR_NONE;
+    return h;
+}
+
+// walk_checked with vectorized headers: one dependent round trip per record. UTF8 = false: the
+// structure only (k_spec's fast mode; k_emit checks the keys and flags a bad one for an exact rerun)
+// slot (cap > 0, a multiple of 8, 16-byte aligned row): the first cap record starts, as offsets
+// from cs (k_emit reads them back), stored eight at a time (one 16-byte store instead of eight
+// 2-byte ones: the single-lane stores were written back as separate partial lines, 7.8 GB at 3F)
+// STG: the walk also stages each record's arrays (key prefix, key length, Delete bit, fingerprint of
+// the key past 16 bytes, an ASCII bit) in its chunk's StgRec row (scap entries), so that k_emit
+// copies them to record order without reading the record again (the parse reads the input once)
+template <int UTF8 = 1, bool STG = false, class L = GLoad>
+__device__ inline WalkRes walk_fast(const uint8_t* run, uint64_t len, uint64_t p, uint64_t stop, uint32_t max_recs,
+                                   L ld = L(), uint16_t* slot = nullptr, uint32_t cap = 0, uint64_t cs = 0,
+                                   StgRec* stg = nullptr, uint32_t scap = 0) {
+    uint32_t cnt = 0, nst = 0;
+    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    auto flush = [&]() {  // the group holding slot cnt - 1 (positions past cnt: unread)
+        if (cap && (cnt & 7) && (cnt & ~7u) < cap) *(uint4*)(slot + (cnt & ~7u)) = make_uint4(s0, s1, s2, s3);
+    };
+    while (p < stop && cnt < max_recs) {
+        uint64_t fpv = 0;
+        bool ascii = true;
+        RecHdr h;
+        if (STG && UTF8 == 0) {
+            h = parse_rec_stg(run, len, p, fpv, ascii, ld);
+        } else {
+            h = parse_rec<STG, UTF8>(run, len, p, ld);
+            if (STG && h.klen <= STG_KMAX) {
+                fpv = key_tail_fp(run + p + 5, (uint32_t)h.klen, ascii, ld);
+                ascii = ascii && ((h.hi | h.lo) & 0x8080808080808080ull) == 0;
+            }
+        }
+        if (h.err) {
+            flush();
+            return {p, cnt, h.err, nst};
+        }
+        // (a key past STG_KMAX bytes ends the staging: its fingerprint would lengthen the walk's
+        // chain -- a wrong speculative chain can read a run-sized "key" -- and k_emit parses the chunk)
+        if (STG && cnt < scap && nst == cnt && h.klen <= STG_KMAX && (!(SKV_STG_PROBE & 2) || (fpv ^ h.hi) == 42)) {
+            ++nst;
+            const uint32_t kd = (uint32_t)h.klen | (h.marker == 2 ? 0x80000000u : 0u);
+            uint4* e = (uint4*)(stg + (uint64_t)cnt * STG_W);
+            e[0] = make_uint4((uint32_t)h.hi, (uint32_t)(h.hi >> 32), (uint32_t)h.lo, (uint32_t)(h.lo >> 32));
+            e[1] = make_uint4((uint32_t)fpv, (uint32_t)(fpv >> 32), kd, ascii ? 1u : 0u);
+        }
+        if (cnt < cap) {
+            const uint32_t j = cnt & 7, v = (uint32_t)(uint16_t)(p - cs) << (16 * (j & 1)), q = j >> 1;
+            s0 |= q == 0 ? v : 0u;
+            s1 |= q == 1 ? v : 0u;
+            s2 |= q == 2 ? v : 0u;
+            s3 |= q == 3 ? v : 0u;
+            if (j == 7) {
+                *(uint4*)(slot + (cnt & ~7u)) = make_uint4(s0, s1, s2, s3);
+                s0 = s1 = s2 = s3 = 0;
+            }
+        }
+        ++cnt;
+        p += h.size;
+    }
+    flush();
+    return {p, cnt, DERR_NONE, nst};
+}
+
 
 __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t k) {
     uint32_t d = (k >> 2) == 0 ? v.x : ((k >> 2) == 1 ? v.y : ((k >> 2) == 2 ? v.z : v.w));

@@ -163,9 +163,10 @@ template <int UTF8>
 __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
                        const uint32_t* __restrict__ hdr_err, const RunFmt* __restrict__ fmt, uint32_t* run_broken,
                        uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, uint64_t chunk,
-                       uint16_t* slots, uint32_t cap) {
+                       uint16_t* slots, uint32_t cap, StgRec* stg, uint32_t scap, uint8_t* ch_stg) {
     uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
+    ch_stg[c] = 0;  // (a walked chunk's records are staged)
     uint32_t r = find_run(runs, n_runs, c);
     RunInfo R = runs[r];
     uint64_t local = c - R.chunk_base;
@@ -228,7 +229,9 @@ __global__ void k_spec(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         ch_err[c] = 0;
         return;
     }
-    const WalkRes w = walk_fast<UTF8>(run, R.len, start, ce, 0xFFFFFFFFu, GLoad(), slots + c * cap, cap, cs);
+    const WalkRes w = walk_fast<UTF8, true>(run, R.len, start, ce, 0xFFFFFFFFu, GLoad(), slots + c * cap, cap, cs,
+                                            stg + stg_base(c, scap), scap);
+    ch_stg[c] = w.nst == w.cnt ? 1 : 0;
     ch_start[c] = start;
     ch_end[c] = w.end;
     ch_cnt[c] = w.cnt;
@@ -270,7 +273,7 @@ __device__ uint64_t next_bad(const unsigned long long* bits, uint64_t from, uint
 __global__ void k_fixup(const RunInfo* __restrict__ runs, uint32_t n_runs, const uint32_t* __restrict__ hdr_err,
                         const uint32_t* __restrict__ run_first_bad, const unsigned long long* __restrict__ bad_bits,
                         uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, bool utf8,
-                        uint64_t chunk, uint16_t* slots, uint32_t cap) {
+                        uint64_t chunk, uint16_t* slots, uint32_t cap, uint8_t* ch_stg) {
     uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_runs) return;
     uint32_t fb = run_first_bad[r];
@@ -289,8 +292,11 @@ __global__ void k_fixup(const RunInfo* __restrict__ runs, uint32_t n_runs, const
         uint32_t cnt = 0, err = 0;
         if (E < ce) {
             uint16_t* sl = slots + g * cap;
+            // (no staging: one lane walks a run's repaired chunks in sequence, the fingerprints' ALU
+            // work would sit in that chain -- 2.0 against 0.84 ms at 3F; k_emit parses these chunks)
             WalkRes w = utf8 ? walk_fast<1>(run, R.len, E, ce, 0xFFFFFFFFu, GLoad(), sl, cap, cs)
                              : walk_fast<0>(run, R.len, E, ce, 0xFFFFFFFFu, GLoad(), sl, cap, cs);
+            ch_stg[g] = 0;
             end = w.end;
             cnt = w.cnt;
             err = w.err;
@@ -369,7 +375,8 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
                        uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags,
                        uint64_t* __restrict__ rec_fp, uint32_t* utf8_bad, const uint16_t* __restrict__ slots,
                        uint32_t cap, uint64_t chunk, const uint64_t* __restrict__ ch_end,
-                       const uint64_t* __restrict__ stream_base, unsigned long long* first_dec) {
+                       const uint64_t* __restrict__ stream_base, unsigned long long* first_dec,
+                       const StgRec* __restrict__ stg, uint32_t scap, const uint8_t* __restrict__ ch_stg) {
     const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t c = gi / EM_G;
     const uint32_t j0 = (uint32_t)(gi % EM_G);
@@ -435,6 +442,28 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         h.size = pn - p;
         return h;
     };
+    // a chunk whose walk staged every record: its arrays come from the staged row (coalesced 32-byte
+    // entries), the record itself is read only for a non-ASCII key's UTF-8 check
+    const bool staged = ch_stg[c] && cnt <= scap;
+    const StgRec* sg = stg + stg_base(c, scap);
+    auto shdr = [&](uint64_t i, uint64_t p, uint64_t pn) {
+        RecHdr h;
+        const uint4* e = (const uint4*)(sg + i * STG_W);
+        const uint4 a = e[0], b = e[1];
+        h.hi = ((uint64_t)a.y << 32) | a.x;
+        h.lo = ((uint64_t)a.w << 32) | a.z;
+        h.klen = b.z & 0x7FFFFFFFu;
+        h.marker = (b.z >> 31) ? 2u : 1u;
+        h.err = b.w;  // (the ASCII bit, carried to semit)
+        h.size = pn - p;
+        return h;
+    };
+    auto semit = [&](uint64_t i, uint64_t p, const RecHdr& h) {
+        const uint4 b = ((const uint4*)(sg + i * STG_W))[1];
+        if (!h.err && !utf8_valid(run + p + 5, h.klen)) atomicOr(utf8_bad, 1u);
+        put_rec(b0 + i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp,
+                ((uint64_t)b.y << 32) | b.x);
+    };
     // steps are uniform over the chunk's EM_G lanes (the order check shuffles inside the group)
     const uint64_t nit = (cnt + 2 * EM_G - 1) / (2 * EM_G);
     uint64_t c_hi = 0, c_lo = 0, c_ad = 0;  // lane EM_G - 1's second record of the previous step
@@ -447,10 +476,10 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         const uint64_t pn = ia + 1 < cnt ? cs + sl[ia + 1] : cend;
         const uint64_t q = two ? cs + sl[i2] : p;
         const uint64_t qn = two ? (i2 + 1 < cnt ? cs + sl[i2 + 1] : cend) : pn;
-        const RecHdr ha = hdr(p, pn);
-        const RecHdr hb = hdr(q, qn);
-        if (one) emit(i, p, ha);
-        if (two) emit(i2, q, hb);
+        const RecHdr ha = staged ? shdr(ia, p, pn) : hdr(p, pn);
+        const RecHdr hb = staged ? shdr(two ? i2 : ia, q, qn) : hdr(q, qn);
+        if (one) staged ? semit(i, p, ha) : emit(i, p, ha);
+        if (two) staged ? semit(i2, q, hb) : emit(i2, q, hb);
         if (first_dec) {
             const uint64_t pa = (uint64_t)(uintptr_t)(run + p), pb = (uint64_t)(uintptr_t)(run + q);
             const uint32_t ka = (uint32_t)ha.klen, kb = (uint32_t)hb.klen;
@@ -2823,14 +2852,15 @@ void launch_run_header(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint
 }
 void launch_spec(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                  const RunFmt* fmt, uint32_t* run_broken, uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt,
-                 uint32_t* ch_err, bool utf8, uint64_t chunk, uint16_t* slots, uint32_t cap) {
+                 uint32_t* ch_err, bool utf8, uint64_t chunk, uint16_t* slots, uint32_t cap, StgRec* stg,
+                 uint32_t scap, uint8_t* ch_stg) {
     if (!n_chunks) return;
     if (utf8)
         k_spec<1><<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, fmt, run_broken, ch_start,
-                                                            ch_end, ch_cnt, ch_err, chunk, slots, cap);
+                                                            ch_end, ch_cnt, ch_err, chunk, slots, cap, stg, scap, ch_stg);
     else
         k_spec<0><<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, hdr_err, fmt, run_broken, ch_start,
-                                                            ch_end, ch_cnt, ch_err, chunk, slots, cap);
+                                                            ch_end, ch_cnt, ch_err, chunk, slots, cap, stg, scap, ch_stg);
 }
 void launch_validate(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                      const uint64_t* ch_start, const uint64_t* ch_end, const uint32_t* ch_err,
@@ -2842,10 +2872,10 @@ void launch_validate(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64
 void launch_fixup(hipStream_t s, const RunInfo* runs, uint32_t n_runs, const uint32_t* hdr_err,
                   const uint32_t* run_first_bad, const unsigned long long* bad_bits, uint64_t* ch_start,
                   uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, bool utf8, uint64_t chunk, uint16_t* slots,
-                  uint32_t cap) {
+                  uint32_t cap, uint8_t* ch_stg) {
     if (n_runs)
         k_fixup<<<blocks_for(n_runs, 64), 64, 0, s>>>(runs, n_runs, hdr_err, run_first_bad, bad_bits, ch_start, ch_end,
-                                                       ch_cnt, ch_err, utf8, chunk, slots, cap);
+                                                       ch_cnt, ch_err, utf8, chunk, slots, cap, ch_stg);
 }
 void launch_err_chunk(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                       const uint32_t* ch_err, uint32_t* run_err_chunk) {
@@ -2867,12 +2897,13 @@ void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n
                  const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                  uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, uint64_t* rec_fp, uint32_t* utf8_bad,
                  const uint16_t* slots, uint32_t cap, uint64_t chunk, const uint64_t* ch_end,
-                 const uint64_t* stream_base, unsigned long long* first_dec) {
+                 const uint64_t* stream_base, unsigned long long* first_dec, const StgRec* stg, uint32_t scap,
+                 const uint8_t* ch_stg) {
     if (n_chunks)
         k_emit<<<blocks_for(n_chunks * EM_G, 256), 256, 0, s>>>(runs, n_runs, n_chunks, fmt, run_broken, ch_start,
                                                                 ch_rec_base, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
                                                                 flags, rec_fp, utf8_bad, slots, cap, chunk, ch_end,
-                                                                stream_base, first_dec);
+                                                                stream_base, first_dec, stg, scap, ch_stg);
     if (R)
         k_emit_fixed<false><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, nullptr, R, fmt, (uint32_t*)run_broken, run_recb,
                                                                rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags,

@@ -14,14 +14,15 @@ void launch_run_header(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint32
                        bool slices = false);
 void launch_spec(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                  const RunFmt* fmt, uint32_t* run_broken, uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt,
-                 uint32_t* ch_err, bool utf8, uint64_t chunk, uint16_t* slots, uint32_t cap);
+                 uint32_t* ch_err, bool utf8, uint64_t chunk, uint16_t* slots, uint32_t cap, StgRec* stg,
+                 uint32_t scap, uint8_t* ch_stg);
 void launch_validate(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                      const uint64_t* ch_start, const uint64_t* ch_end, const uint32_t* ch_err,
                      unsigned long long* bad_bits, uint32_t* run_first_bad);
 void launch_fixup(hipStream_t, const RunInfo* runs, uint32_t n_runs, const uint32_t* hdr_err,
                   const uint32_t* run_first_bad, const unsigned long long* bad_bits, uint64_t* ch_start,
                   uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, bool utf8, uint64_t chunk, uint16_t* slots,
-                  uint32_t cap);
+                  uint32_t cap, uint8_t* ch_stg);
 void launch_err_chunk(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                       const uint32_t* ch_err, uint32_t* run_err_chunk);
 void launch_mask(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
@@ -34,7 +35,8 @@ void launch_emit(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_c
                  const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                  uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, uint64_t* rec_fp, uint32_t* utf8_bad,
                  const uint16_t* slots, uint32_t cap, uint64_t chunk, const uint64_t* ch_end,
-                 const uint64_t* stream_base = nullptr, unsigned long long* first_dec = nullptr);
+                 const uint64_t* stream_base, unsigned long long* first_dec, const StgRec* stg, uint32_t scap,
+                 const uint8_t* ch_stg);
 void launch_parse_fixed(hipStream_t, const RunInfo* runs, uint32_t n_runs, const RunFmt* fmt, uint32_t* run_broken,
                         const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                         uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, const uint64_t* stream_base,

@@ -610,6 +610,47 @@ def test_invalid_utf8_key_in_variable_runs(dev):
         assert exp == got, _diff(exp, got)
 
 
+def test_staged_chunk_walks(dev):
+    """The chunk walks stage each record's arrays (key prefix, length, Delete bit, fingerprint, ASCII
+    bit) for k_emit, which then reads no record (skv_dev.hpp walk_fast<.., true>): records long
+    enough that chunks are staged, with non-ASCII keys (k_emit checks their UTF-8), keys past the
+    staged limit (144 B: the chunk's staging stops there, k_emit parses it from the records), short
+    records among long ones (a chunk past its staged capacity), Deletes, and an invalid UTF-8 key
+    (the exact rerun). Every outcome equal to the oracle's."""
+    r = random.Random(61)
+    for trial in range(8):
+        streams = []
+        for s in range(6):
+            keys = set()
+            for _ in range(400):
+                kind = r.random()
+                tail = ("x" * r.randint(0, 60) if kind < .6 else "é" * r.randint(1, 40) if kind < .85
+                        else "y" * r.randint(140, 300))
+                keys.add("k%05d" % r.randrange(10**5) + tail)
+            ops = []
+            for k in sorted(keys):
+                if r.random() < .1:
+                    ops.append(fmt.delete(k))
+                else:
+                    # (trial 2: short records only -- chunks past the staged capacity)
+                    long_ok = trial != 2 and ((trial & 1) or r.random() < .7)
+                    vlen = r.randint(150, 400) if long_ok else r.randint(0, 8)
+                    ops.append(fmt.put(k, bytes(r.randrange(256) for _ in range(vlen))))
+            run = bytearray(fmt.encode_run(ops))
+            if trial >= 6 and s == 2:  # one key byte made invalid UTF-8
+                p, i = 1, 0
+                target = r.randrange(len(ops))
+                while i < target:
+                    kl = int.from_bytes(run[p + 1:p + 5], "big")
+                    p += 5 + kl + (4 + int.from_bytes(run[p + 5 + kl:p + 9 + kl], "big") if run[p] == 1 else 0)
+                    i += 1
+                run[p + 5 + 2] = 0xFF
+            streams.append((s + 1, [bytes(run)]))
+        for flags in (0, _abi.SKV_DROP_TOMBSTONES):
+            exp, got = _run_both(dev, streams, 1 << 18, flags)
+            assert exp == got, (trial, flags, _diff(exp, got))
+
+
 def test_coarse_sample_levels_same_bytes(dev):
     """The sample levels above the first only pick splitters: with a 2x or 4x coarser step there
     (SKV_HI_STEP; tiles past TILE_CAP take the oversized-tile path) the output is the same."""
