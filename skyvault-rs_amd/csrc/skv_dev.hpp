@@ -714,42 +714,26 @@ __device__ inline uint64_t key_tail_fp(const uint8_t* key, uint32_t klen, bool& 
     return h;
 }
 
-// key_tail_fp for a key of at most STG_KMAX bytes with every block load issued up front (the
-// walk's staging: these loads go out with the value length's, so the chain stays one round trip
-// past the header per record); the same function of the bytes as key_tail_fp
-template <class L = GLoad>
-__device__ __forceinline__ uint64_t key_tail_fp_short(const uint8_t* key, uint32_t klen, bool& ascii, L ld = L()) {
-    ascii = true;
-    if (klen <= 16) return 0;
-    const uint32_t n = klen - 16;  // <= STG_KMAX - 16 = 128
-    const uintptr_t a = (uintptr_t)(key + 16);
-    const uintptr_t base = a & ~(uintptr_t)15;
-    const uint32_t sh = (uint32_t)(a & 15);
-    const uint32_t nblk = (sh + n + 15) >> 4;
-    uint4 B[9];
+// uint4 b[i] for a dynamic i < N, as a select tree over register values (no array in memory)
+template <int N>
+__device__ __forceinline__ uint4 sel_blk(const uint4 (&b)[N], uint32_t i) {
+    uint4 r = b[0];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) B[i] = (uint32_t)i < nblk ? ld(base + 16ull * i) : make_uint4(0, 0, 0, 0);
-    uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
-    uint32_t acc = 0;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-        if (16u * w < n) {
-            const uint32_t m = n - 16 * w < 16 ? n - 16 * w : 16;
-            const uint4 v = funnel16(B[w], B[w + 1], sh);
-            const uint32_t a0 = v.x & dword_mask(0, m, 0), a1 = v.y & dword_mask(0, m, 1);
-            const uint32_t a2 = v.z & dword_mask(0, m, 2), a3 = v.w & dword_mask(0, m, 3);
-            acc |= a0 | a1 | a2 | a3;
-            h = fp_mix(h ^ (((uint64_t)a1 << 32) | a0));
-            h = fp_mix(h ^ (((uint64_t)a3 << 32) | a2) ^ 0x2545F4914F6CDD1Dull);
-        }
+    for (int k = 1; k < N; ++k) {
+        const bool t = i == (uint32_t)k;
+        r.x = t ? b[k].x : r.x;
+        r.y = t ? b[k].y : r.y;
+        r.z = t ? b[k].z : r.z;
+        r.w = t ? b[k].w : r.w;
     }
-    ascii = (acc & 0x80808080u) == 0;
-    return h;
+    return r;
 }
 
-// parse_rec<true, 0> for the staging walks: the value length's load and the key tail's loads are
-// issued together after the header window; fpv / ascii as key_tail_fp gives them, for keys of at
-// most STG_KMAX bytes (longer keys end the chunk's staging, their fingerprint is not computed)
+// parse_rec<true, 0> for the staging walks, reading each byte of the record's header, key and value
+// length once: the header window's aligned blocks, then (past them, issued together) the blocks up
+// to the value length, from which the value length and the fingerprint of the key past 16 bytes
+// (key_tail_fp's function of the bytes) are taken. Keys of at most STG_KMAX bytes (longer keys end
+// the chunk's staging, their fingerprint is not computed: fpv 0).
 template <class L = GLoad>
 __device__ __forceinline__ RecHdr parse_rec_stg(const uint8_t* run, uint64_t len, uint64_t p, uint64_t& fpv,
                                                 bool& ascii, L ld = L()) {
@@ -758,24 +742,84 @@ __device__ __forceinline__ RecHdr parse_rec_stg(const uint8_t* run, uint64_t len
     h.hi = h.lo = 0;
     fpv = 0;
     ascii = true;
+    const uintptr_t a = (uintptr_t)(run + p), end = (uintptr_t)(run + len);
+    const uintptr_t base = a & ~(uintptr_t)15;
+    const uint32_t sh = (uint32_t)(a & 15);
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const uint4 b0 = ld(base);
+    const uint4 b1 = base + 16 < end ? ld(base + 16) : z;
+    const bool b2ok = sh && base + 32 < end;
+    const uint4 b2 = b2ok ? ld(base + 32) : z;
     uint32_t w[8];
-    window32(run, len, p, w, ld);
+    {
+        const uint4 lo = funnel16(b0, b1, sh), hi = funnel16(b1, b2, sh);
+        w[0] = lo.x; w[1] = lo.y; w[2] = lo.z; w[3] = lo.w;
+        w[4] = hi.x; w[5] = hi.y; w[6] = hi.z; w[7] = hi.w;
+        if (p + 32 > len) {
+            const uint32_t valid = (uint32_t)(len - p);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) w[i] &= dword_mask(0, valid, i) | (4u * i + 4 <= valid ? 0xFFFFFFFFu : 0u);
+        }
+    }
     h.marker = w[0] & 0xFFu;
     if (p + 5 > len) { h.err = DERR_IO; h.klen = 0; return h; }
     h.klen = __builtin_bswap32(__builtin_amdgcn_alignbyte(w[1], w[0], 1));
     const uint64_t kp = p + 5;
     if (kp + h.klen > len) { h.err = DERR_KEY; return h; }
     const uint64_t vo = 5 + h.klen;
-    const bool vload = h.marker == 1 && kp + h.klen + 4 <= len && vo + 4 > 32;
-    const uint4 vv = vload ? load_window16(run + p + vo, 4, ld) : make_uint4(0, 0, 0, 0);
-    if (h.klen <= STG_KMAX && !(SKV_STG_PROBE & 1)) fpv = key_tail_fp_short(run + kp, (uint32_t)h.klen, ascii, ld);
+    const bool put = h.marker == 1;
+    const bool vin = put && kp + h.klen + 4 <= len;  // (else the IO error below)
+    // the region past the window: key bytes 16.. (fingerprint) and the value length, in aligned
+    // blocks from tb; blocks the window already holds are taken from it
+    const bool tail = h.klen > 16 && h.klen <= STG_KMAX;
+    const bool vfar = vin && vo + 4 > 32 && h.klen <= STG_KMAX;
+    uint4 B[10];
+    const uintptr_t tb = (a + 21) & ~(uintptr_t)15;  // base + 16 or base + 32
+    const uint32_t tsh = (uint32_t)((a + 21) & 15);
+    const uint64_t rend = vfar ? vo + 4 : (tail ? vo : 21);  // region end, relative to p
+    const uint32_t nblk = rend > 21 ? (uint32_t)((tsh + (rend - 21) + 15) >> 4) : 0u;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uintptr_t ba = tb + 16ull * i;
+        B[i] = (uint32_t)i >= nblk ? z : (ba == base + 16 ? b1 : (ba == base + 32 && b2ok ? b2 : ld(ba)));
+    }
+    uint4 vv = z;
+    if (vin && vo + 4 > 32 && h.klen > STG_KMAX) vv = load_window16(run + p + vo, 4, ld);  // (unstaged key)
+    if (tail && !(SKV_STG_PROBE & 1)) {
+        const uint32_t n = (uint32_t)h.klen - 16;
+        uint64_t hh = 0x9E3779B97F4A7C15ull ^ n;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (16u * q < n) {
+                const uint32_t m = n - 16 * q < 16 ? n - 16 * q : 16;
+                const uint4 v = funnel16(B[q], B[q + 1], tsh);
+                const uint32_t a0 = v.x & dword_mask(0, m, 0), a1 = v.y & dword_mask(0, m, 1);
+                const uint32_t a2 = v.z & dword_mask(0, m, 2), a3 = v.w & dword_mask(0, m, 3);
+                acc |= a0 | a1 | a2 | a3;
+                hh = fp_mix(hh ^ (((uint64_t)a1 << 32) | a0));
+                hh = fp_mix(hh ^ (((uint64_t)a3 << 32) | a2) ^ 0x2545F4914F6CDD1Dull);
+            }
+        }
+        ascii = (acc & 0x80808080u) == 0;
+        fpv = hh;
+    }
     uint32_t kd[7];
     win_key(w, kd);
     win_prefix(kd, h.klen, h.hi, h.lo);
     ascii = ascii && ((h.hi | h.lo) & 0x8080808080808080ull) == 0;
-    if (h.marker == 1) {
+    if (put) {
         if (kp + h.klen + 4 > len) { h.err = DERR_IO; return h; }
-        const uint64_t vlen = vo + 4 <= 32 ? win_be32(w, (uint32_t)vo) : __builtin_bswap32(vv.x);
+        uint64_t vlen;
+        if (vo + 4 <= 32) {
+            vlen = win_be32(w, (uint32_t)vo);
+        } else if (h.klen <= STG_KMAX) {
+            const uint32_t off = tsh + (uint32_t)(vo - 21);  // the value length's offset from tb
+            const uint4 v = funnel16(sel_blk(B, off >> 4), sel_blk(B, (off >> 4) + 1), off & 15);
+            vlen = __builtin_bswap32(v.x);
+        } else {
+            vlen = __builtin_bswap32(vv.x);
+        }
         if (kp + h.klen + 4 + vlen > len) { h.err = DERR_VAL; return h; }
         h.size = 9 + h.klen + vlen;
     } else if (h.marker == 2) {

@@ -383,6 +383,7 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
     if (c >= n_chunks) return;
     uint64_t b0 = ch_rec_base[c], cnt = ch_rec_base[c + 1] - b0;
     if (!cnt) return;
+    if (ch_stg[c] && cnt <= scap) return;  // k_emit_stg
     uint32_t r = find_run(runs, n_runs, c);
     if (fmt[r].S && !run_broken[r]) return;  // k_emit_fixed
     const uint8_t* run = (const uint8_t*)runs[r].ptr;
@@ -442,28 +443,6 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         h.size = pn - p;
         return h;
     };
-    // a chunk whose walk staged every record: its arrays come from the staged row (coalesced 32-byte
-    // entries), the record itself is read only for a non-ASCII key's UTF-8 check
-    const bool staged = ch_stg[c] && cnt <= scap;
-    const StgRec* sg = stg + stg_base(c, scap);
-    auto shdr = [&](uint64_t i, uint64_t p, uint64_t pn) {
-        RecHdr h;
-        const uint4* e = (const uint4*)(sg + i * STG_W);
-        const uint4 a = e[0], b = e[1];
-        h.hi = ((uint64_t)a.y << 32) | a.x;
-        h.lo = ((uint64_t)a.w << 32) | a.z;
-        h.klen = b.z & 0x7FFFFFFFu;
-        h.marker = (b.z >> 31) ? 2u : 1u;
-        h.err = b.w;  // (the ASCII bit, carried to semit)
-        h.size = pn - p;
-        return h;
-    };
-    auto semit = [&](uint64_t i, uint64_t p, const RecHdr& h) {
-        const uint4 b = ((const uint4*)(sg + i * STG_W))[1];
-        if (!h.err && !utf8_valid(run + p + 5, h.klen)) atomicOr(utf8_bad, 1u);
-        put_rec(b0 + i, run + p, h, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags, rec_fp,
-                ((uint64_t)b.y << 32) | b.x);
-    };
     // steps are uniform over the chunk's EM_G lanes (the order check shuffles inside the group)
     const uint64_t nit = (cnt + 2 * EM_G - 1) / (2 * EM_G);
     uint64_t c_hi = 0, c_lo = 0, c_ad = 0;  // lane EM_G - 1's second record of the previous step
@@ -476,10 +455,10 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
         const uint64_t pn = ia + 1 < cnt ? cs + sl[ia + 1] : cend;
         const uint64_t q = two ? cs + sl[i2] : p;
         const uint64_t qn = two ? (i2 + 1 < cnt ? cs + sl[i2 + 1] : cend) : pn;
-        const RecHdr ha = staged ? shdr(ia, p, pn) : hdr(p, pn);
-        const RecHdr hb = staged ? shdr(two ? i2 : ia, q, qn) : hdr(q, qn);
-        if (one) staged ? semit(i, p, ha) : emit(i, p, ha);
-        if (two) staged ? semit(i2, q, hb) : emit(i2, q, hb);
+        const RecHdr ha = hdr(p, pn);
+        const RecHdr hb = hdr(q, qn);
+        if (one) emit(i, p, ha);
+        if (two) emit(i2, q, hb);
         if (first_dec) {
             const uint64_t pa = (uint64_t)(uintptr_t)(run + p), pb = (uint64_t)(uintptr_t)(run + q);
             const uint32_t ka = (uint32_t)ha.klen, kb = (uint32_t)hb.klen;
@@ -505,6 +484,81 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
                 decrease(i);
             if (two && key_cmp(y_hi, y_lo, y_kl, (const uint8_t*)y_ad + 5, hb.hi, hb.lo, kb, run + q + 5) > 0)
                 decrease(i2);
+        }
+    }
+}
+
+// k_emit for the chunks whose walk staged every record (k_spec): the arrays are copied from the
+// staged entries (one record per lane per step, 32 lanes per chunk: a store instruction writes 32
+// consecutive records per chunk; 16 / 32 / 64 lanes measured 5.63 / 4.40 / 4.76 ms at 3F), the
+// record itself is read only for a non-ASCII key's UTF-8 check and for the order check of two keys
+// with equal prefixes
+#ifndef SKV_EMS_G
+#define SKV_EMS_G 32
+#endif
+constexpr uint32_t EMS_G = SKV_EMS_G;  // lanes per staged chunk
+__global__ void __launch_bounds__(256) k_emit_stg(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
+                           const uint64_t* __restrict__ ch_rec_base, uint64_t* __restrict__ rec_addr,
+                           uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo, uint32_t* __restrict__ rec_klen,
+                           uint32_t* __restrict__ rec_meta, uint32_t* flags, uint64_t* __restrict__ rec_fp,
+                           uint32_t* utf8_bad, const uint16_t* __restrict__ slots, uint32_t cap, uint64_t chunk,
+                           const uint64_t* __restrict__ ch_end, const uint64_t* __restrict__ stream_base,
+                           unsigned long long* first_dec, const StgRec* __restrict__ stg, uint32_t scap,
+                           const uint8_t* __restrict__ ch_stg) {
+    const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t c = gi / EMS_G;
+    const uint32_t j0 = (uint32_t)(gi % EMS_G);
+    if (c >= n_chunks) return;
+    const uint64_t b0 = ch_rec_base[c], cnt = ch_rec_base[c + 1] - b0;
+    if (!cnt || !ch_stg[c] || cnt > scap) return;
+    const uint32_t r = find_run(runs, n_runs, c);
+    const uint8_t* run = (const uint8_t*)runs[r].ptr;
+    const uint64_t cs = 1 + (c - runs[r].chunk_base) * chunk;
+    const uint16_t* sl = slots + c * cap;
+    const StgRec* sg = stg + stg_base(c, scap);
+    const uint64_t cend = ch_end[c];
+    const uint32_t sidx = runs[r].stream;
+    const uint64_t sbase = first_dec ? stream_base[sidx] : 0;
+    uint64_t c_hi = 0, c_lo = 0, c_ad = 0;  // lane EMS_G - 1's record of the previous step
+    uint32_t c_kl = 0;
+    const uint64_t nit = (cnt + EMS_G - 1) / EMS_G;
+    for (uint64_t t = 0; t < nit; ++t) {
+        const uint64_t i = j0 + t * EMS_G;
+        const bool live = i < cnt;
+        const uint64_t ia = live ? i : cnt - 1;
+        const uint64_t p = cs + sl[ia];
+        const uint64_t pn = ia + 1 < cnt ? cs + sl[ia + 1] : cend;
+        const uint4* e = (const uint4*)(sg + ia * STG_W);
+        const uint4 x = e[0], y = e[1];
+        const uint64_t hi = ((uint64_t)x.y << 32) | x.x, lo = ((uint64_t)x.w << 32) | x.z;
+        const uint32_t kl = y.z & 0x7FFFFFFFu;
+        const uint64_t ad = (uint64_t)(uintptr_t)(run + p);
+        if (live) {
+            const uint64_t size = pn - p;
+            const uint64_t o = b0 + i;
+            rec_addr[o] = ad;
+            rec_fp[o] = ((uint64_t)y.y << 32) | y.x;
+            rec_hi[o] = hi;
+            rec_lo[o] = lo;
+            rec_klen[o] = kl;
+            if (size >= (1ull << 31)) atomicOr(flags, 1u);  // record too large for this build
+            rec_meta[o] = (uint32_t)size | (y.z & 0x80000000u);
+            if (!y.w && !utf8_valid(run + p + 5, kl)) atomicOr(utf8_bad, 1u);
+        }
+        if (first_dec) {  // the in-stream order check against the record before (k_emit's)
+            uint64_t x_hi = __shfl_up(hi, 1, EMS_G), x_lo = __shfl_up(lo, 1, EMS_G), x_ad = __shfl_up(ad, 1, EMS_G);
+            uint32_t x_kl = __shfl_up(kl, 1, EMS_G);
+            if (j0 == 0) {
+                x_hi = c_hi; x_lo = c_lo; x_ad = c_ad; x_kl = c_kl;
+            }
+            c_hi = __shfl(hi, EMS_G - 1, EMS_G);
+            c_lo = __shfl(lo, EMS_G - 1, EMS_G);
+            c_ad = __shfl(ad, EMS_G - 1, EMS_G);
+            c_kl = __shfl(kl, EMS_G - 1, EMS_G);
+            if (live && i > 0 && key_cmp(x_hi, x_lo, x_kl, (const uint8_t*)x_ad + 5, hi, lo, kl, run + p + 5) > 0) {
+                atomicMin(&first_dec[sidx], (unsigned long long)(b0 + i - 1 - sbase));
+                atomicOr(flags + 1, 1u);
+            }
         }
     }
 }
@@ -2904,6 +2958,11 @@ void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n
                                                                 ch_rec_base, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
                                                                 flags, rec_fp, utf8_bad, slots, cap, chunk, ch_end,
                                                                 stream_base, first_dec, stg, scap, ch_stg);
+    if (n_chunks)
+        k_emit_stg<<<blocks_for(n_chunks * EMS_G, 256), 256, 0, s>>>(runs, n_runs, n_chunks, ch_rec_base, rec_addr, rec_hi,
+                                                                    rec_lo, rec_klen, rec_meta, flags, rec_fp, utf8_bad,
+                                                                    slots, cap, chunk, ch_end, stream_base, first_dec,
+                                                                    stg, scap, ch_stg);
     if (R)
         k_emit_fixed<false><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, nullptr, R, fmt, (uint32_t*)run_broken, run_recb,
                                                                rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags,
