@@ -638,6 +638,11 @@ __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, ui
     h.klen = __builtin_bswap32(__builtin_amdgcn_alignbyte(w[1], w[0], 1));
     const uint64_t kp = p + 5;
     if (kp + h.klen > len) { h.err = DERR_KEY; return h; }
+    // the value length past the window is loaded before the key's UTF-8 check, so that the two
+    // round trips overlap (the checks keep the reference's order)
+    const uint64_t vo = 5 + h.klen;
+    const bool vfar = h.marker == 1 && vo + 4 > 32 && kp + h.klen + 4 <= len;
+    const uint4 vv = vfar ? load_window16(run + p + vo, 4, ld) : make_uint4(0, 0, 0, 0);
     uint32_t kd[7];
     win_key(w, kd);
     bool ok = UTF8 == 0 || (UTF8 == 2 ? ascii_prefix(kd, h.klen < 27 ? (uint32_t)h.klen : 27u)
@@ -647,13 +652,7 @@ __device__ __forceinline__ RecHdr parse_rec(const uint8_t* run, uint64_t len, ui
     if (PREFIX) win_prefix(kd, h.klen, h.hi, h.lo);
     if (h.marker == 1) {
         if (kp + h.klen + 4 > len) { h.err = DERR_IO; return h; }
-        uint64_t vo = 5 + h.klen;
-        uint64_t vlen;
-        if (vo + 4 <= 32) vlen = win_be32(w, (uint32_t)vo);
-        else {
-            uint4 v = load_window16(run + p + vo, 4, ld);
-            vlen = __builtin_bswap32(v.x);
-        }
+        const uint64_t vlen = vo + 4 <= 32 ? win_be32(w, (uint32_t)vo) : __builtin_bswap32(vv.x);
         if (kp + h.klen + 4 + vlen > len) { h.err = DERR_VAL; return h; }
         h.size = 9 + h.klen + vlen;
     } else if (h.marker == 2) {
