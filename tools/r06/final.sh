@@ -10,6 +10,7 @@ R="$PWD"; O="$R/gpurun_out/r06/final"; mkdir -p "$O"
 export TMPDIR=/tmp
 for c in ${CONFIGS:-2A 2B 3 3F 5 L0}; do
   W=3; K=${STEPS:-20}; extra=""
+  if [ "${BENCH:-1}" = 1 ]; then
   [ "$c" = 3F ] && { W=1; K=5; extra="--no-host-path"; }
   [ "$c" = 5 ] && { W=2; K=10; }
   timeout -k 10 600 python3 bench.py --config $c --steps $K --warmup $W $extra > "$O/bench_$c.log" 2>&1
@@ -27,6 +28,7 @@ for c in ${CONFIGS:-2A 2B 3 3F 5 L0}; do
   cp "$f" "$O/rocprof_stats_$c.csv"
   sed -n 1,6p "$O/kernel_stats_$c.txt"
   echo "$c: $(grep -o '"value": [0-9.]*' $O/bench_$c.json | head -1) $(grep -o '"ms_per_step": [0-9.]*' $O/bench_$c.json)"
+  fi
   if [ "${PMC:-1}" = 1 ]; then
     pe="--steps 1 --warmup 1 --no-cpu-baseline --no-host-path"
     for ctr in FETCH_SIZE WRITE_SIZE; do
@@ -35,7 +37,8 @@ for c in ${CONFIGS:-2A 2B 3 3F 5 L0}; do
         python3 "$R/bench.py" --config $c $pe > "$O/pmc_${c}_$ctr.log" 2>&1
       rc=$?; cd "$R"; [ $rc -ne 0 ] && { echo "pmc $c $ctr rc=$rc"; tail -3 "$O/pmc_${c}_$ctr.log"; exit $rc; }
     done
-    python3 tools/traffic.py "$O/pmc_$c" $c "$O/traffic.json" 3 > "$O/traffic_$c.txt"
+    # (one traffic file per config: a call's gpurun_out merge must not replace another call's)
+    python3 tools/traffic.py "$O/pmc_$c" $c "$O/traffic_$c.json" 3 > "$O/traffic_$c.txt"
     sed -n 1,3p "$O/traffic_$c.txt"
   fi
   [ "${KEEP_TRACES:-0}" = 1 ] || rm -rf "$O/trace_$c" "$O/pmc_$c"
