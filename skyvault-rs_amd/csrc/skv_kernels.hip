@@ -1226,11 +1226,11 @@ static_assert(TILE_CAP <= (1 << WD_ID), "element ids fit the sort word");
 
 // the 8 key bytes that follow c common bytes (0 <= c <= 8) of a 16-byte prefix
 __device__ __forceinline__ uint64_t wd_window(uint64_t hi, uint64_t lo, uint32_t c) {
-    return c == 0 ? hi : (c >= 8 ? lo : (hi << (8 * c)) | (lo >> (64 - 8 * c)));
+    return c == 0 ? hi : (c >= 8 ? lo << (8 * (c - 8)) : (hi << (8 * c)) | (lo >> (64 - 8 * c)));
 }
 
 // key16 (by id, id == load position), n elements -> wd[] by position: runs of 256 sorted words.
-// c: common prefix bytes of the tile's keys (<= 8).
+// c: common prefix bytes of the tile's keys (<= 15).
 __device__ void tile_sort_words(const ulong2* key16, uint64_t* wd, uint32_t n, uint32_t c) {
     static_assert(TILE_THREADS * 4 == TILE_CAP, "one 256-position run per wave");
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1465,12 +1465,12 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
         return;
     }
     uint64_t t = blockIdx.x;
-    if (!L0 && threadIdx.x == 0) s_flag[24] = s_flag[25] = s_flag[26] = s_flag[27] = 0;  // (barriers follow)
+    if (!L0 && threadIdx.x == 0) s_flag[24] = s_flag[25] = s_flag[26] = s_flag[27] = s_flag[28] = s_flag[29] = 0;
     if (L0) {  // level 0 tiles take tickets in start order (tile_lookback's progress guarantee)
         if (threadIdx.x == 0) {
             s_tk = atomicAdd(O.tcounter, 1u);
             s_flag[24] = s_flag[25] = 0;  // mixed groups / a group too large (tile_fix_groups)
-            s_flag[26] = s_flag[27] = 0;  // the common-prefix OR (tile_sort_words' window)
+            s_flag[26] = s_flag[27] = s_flag[28] = s_flag[29] = 0;  // the common-prefix ORs (tile_sort_words)
         }
         __syncthreads();
         t = s_tk;
@@ -1552,22 +1552,33 @@ __global__ void __launch_bounds__(TILE_THREADS) k_tile(Elems E, const uint64_t* 
                   : elem_less(rec_addr, ha, el_lo[xa], el_c[xa], hb, el_lo[xb], el_c[xb]);
     };
     if (wpath) {
-        // c = the bytes every key of the tile shares (<= 8): the OR of each key's first 8 bytes XOR
-        // element 0's, over the block
-        const uint64_t k0 = key16[0].x;
-        uint64_t dh = 0;
+        // c = the bytes every key of the tile shares (<= 15): the OR of each key's prefix words XOR
+        // element 0's, over the block (keys sharing their first 8 bytes -- 2B's zero-padded hex ids --
+        // take the window from the second word: from the first, 16 ids shared one, and the sample
+        // tiles went to the exact merge: 287 against 41 us)
+        const ulong2 k0 = key16[0];
+        uint64_t dh = 0, dl = 0;
 #pragma unroll
         for (int u = 0; u < PER; ++u)
-            if (threadIdx.x + u * TILE_THREADS < n) dh |= rh[u] ^ k0;
+            if (threadIdx.x + u * TILE_THREADS < n) {
+                dh |= rh[u] ^ k0.x;
+                dl |= rl[u] ^ k0.y;
+            }
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) dh |= __shfl_xor(dh, d, 64);
-        if ((threadIdx.x & 63) == 0 && dh) {
+        for (int d = 32; d >= 1; d >>= 1) {
+            dh |= __shfl_xor(dh, d, 64);
+            dl |= __shfl_xor(dl, d, 64);
+        }
+        if ((threadIdx.x & 63) == 0 && (dh | dl)) {
             atomicOr(s_flag + 26, (uint32_t)(dh >> 32));
             atomicOr(s_flag + 27, (uint32_t)dh);
+            atomicOr(s_flag + 28, (uint32_t)(dl >> 32));
+            atomicOr(s_flag + 29, (uint32_t)dl);
         }
         __syncthreads();
         const uint64_t D = ((uint64_t)s_flag[26] << 32) | s_flag[27];
-        const uint32_t cpx = D ? (uint32_t)__builtin_clzll(D) >> 3 : 8u;
+        const uint64_t DL = ((uint64_t)s_flag[28] << 32) | s_flag[29];
+        const uint32_t cpx = D ? (uint32_t)__builtin_clzll(D) >> 3 : (DL ? 8u + ((uint32_t)__builtin_clzll(DL) >> 3) : 15u);
         tile_sort_words(key16, wd, n, cpx);
         TPROF(8);
         uint64_t ow[4];
