@@ -817,7 +817,7 @@ int compact_device(skv_ctx* ctx, const Job& job, skv_result** out, bool allow_de
         launch_emit(st, d_runs, n_runs, n_chunks, d_fmt, d_broken, ch_start, ch_rec_base, d_recb, any_fixed ? R : 0,
                     rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, d_flags, rec_fp, utf8_bad, ch_slots, slot_cap, chunk,
                     ch_end, emit_order ? d_stream_base : nullptr, emit_order ? d_first_dec : nullptr, ch_stg_rec,
-                    stg_cap, ch_stg);
+                    stg_cap, ch_stg, R, dbuf<uint32_t>(ctx, "blk_chunk", R / 64 + 1 + n_chunks));
         mark(ctx, PH_PARSE);
         check_and_read(false, emit_order ? ORDER_DONE : ORDER_LAUNCH);
         if (utf8_flag && !ctx->exact_utf8) {  // a key the chunk walks did not check: exact walks

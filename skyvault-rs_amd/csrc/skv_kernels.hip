@@ -488,54 +488,74 @@ __global__ void k_emit(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64
     }
 }
 
-// k_emit for the chunks whose walk staged every record (k_spec): the arrays are copied from the
-// staged entries (one record per lane per step, 32 lanes per chunk: a store instruction writes 32
-// consecutive records per chunk; 16 / 32 / 64 lanes measured 5.63 / 4.40 / 4.76 ms at 3F), the
-// record itself is read only for a non-ASCII key's UTF-8 check and for the order check of two keys
-// with equal prefixes
-#ifndef SKV_EMS_G
-#define SKV_EMS_G 32
-#endif
-constexpr uint32_t EMS_G = SKV_EMS_G;  // lanes per staged chunk
-__global__ void __launch_bounds__(256) k_emit_stg(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
-                           const uint64_t* __restrict__ ch_rec_base, uint64_t* __restrict__ rec_addr,
-                           uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo, uint32_t* __restrict__ rec_klen,
-                           uint32_t* __restrict__ rec_meta, uint32_t* flags, uint64_t* __restrict__ rec_fp,
-                           uint32_t* utf8_bad, const uint16_t* __restrict__ slots, uint32_t cap, uint64_t chunk,
-                           const uint64_t* __restrict__ ch_end, const uint64_t* __restrict__ stream_base,
-                           unsigned long long* first_dec, const StgRec* __restrict__ stg, uint32_t scap,
-                           const uint8_t* __restrict__ ch_stg) {
-    const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t c = gi / EMS_G;
-    const uint32_t j0 = (uint32_t)(gi % EMS_G);
+// k_emit_stg: 64-record groups per wave (1 / 2 / 4 / 8 measured 3.73 / 4.12 / 4.27 / 4.90 ms at 3F)
+constexpr int EMS_R = 1;
+// blk_chunk[q] = the chunk holding record 64 q (k_emit_stg's starting point for a wave);
+// chunk_run[c] = the run of chunk c (one search per chunk instead of one per record)
+__global__ void k_blk_chunk(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t n_chunks,
+                            const uint64_t* __restrict__ ch_rec_base, uint32_t* blk_chunk, uint32_t* chunk_run) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
-    const uint64_t b0 = ch_rec_base[c], cnt = ch_rec_base[c + 1] - b0;
-    if (!cnt || !ch_stg[c] || cnt > scap) return;
-    const uint32_t r = find_run(runs, n_runs, c);
-    const uint8_t* run = (const uint8_t*)runs[r].ptr;
-    const uint64_t cs = 1 + (c - runs[r].chunk_base) * chunk;
-    const uint16_t* sl = slots + c * cap;
-    const StgRec* sg = stg + stg_base(c, scap);
-    const uint64_t cend = ch_end[c];
-    const uint32_t sidx = runs[r].stream;
-    const uint64_t sbase = first_dec ? stream_base[sidx] : 0;
-    uint64_t c_hi = 0, c_lo = 0, c_ad = 0;  // lane EMS_G - 1's record of the previous step
-    uint32_t c_kl = 0;
-    const uint64_t nit = (cnt + EMS_G - 1) / EMS_G;
-    for (uint64_t t = 0; t < nit; ++t) {
-        const uint64_t i = j0 + t * EMS_G;
-        const bool live = i < cnt;
-        const uint64_t ia = live ? i : cnt - 1;
-        const uint64_t p = cs + sl[ia];
-        const uint64_t pn = ia + 1 < cnt ? cs + sl[ia + 1] : cend;
-        const uint4* e = (const uint4*)(sg + ia * STG_W);
-        const uint4 x = e[0], y = e[1];
-        const uint64_t hi = ((uint64_t)x.y << 32) | x.x, lo = ((uint64_t)x.w << 32) | x.z;
-        const uint32_t kl = y.z & 0x7FFFFFFFu;
-        const uint64_t ad = (uint64_t)(uintptr_t)(run + p);
+    chunk_run[c] = find_run(runs, n_runs, c);
+    const uint64_t b0 = ch_rec_base[c], b1 = ch_rec_base[c + 1];
+    for (uint64_t q = (b0 + 63) >> 6; (q << 6) < b1; ++q) blk_chunk[q] = (uint32_t)c;
+}
+
+// k_emit for the chunks whose walk staged every record (k_spec): the arrays are copied from the
+// staged entries, one thread per record in record order, so a wave stores 64 consecutive records
+// of every array (whole lines; a chunk's lanes storing 32 records each wrote 12.2 GB for 8.2 GB of
+// arrays at 3F). The record itself is read only for a non-ASCII key's UTF-8 check and for the
+// order check of two keys with equal prefixes.
+__global__ void __launch_bounds__(256) k_emit_stg(const RunInfo* __restrict__ runs, uint32_t n_runs, uint64_t R,
+                           const uint64_t* __restrict__ ch_rec_base, const uint32_t* __restrict__ blk_chunk,
+                           const uint32_t* __restrict__ chunk_run, uint64_t* __restrict__ rec_addr, uint64_t* __restrict__ rec_hi, uint64_t* __restrict__ rec_lo,
+                           uint32_t* __restrict__ rec_klen, uint32_t* __restrict__ rec_meta, uint32_t* flags,
+                           uint64_t* __restrict__ rec_fp, uint32_t* utf8_bad, const uint16_t* __restrict__ slots,
+                           uint32_t cap, uint64_t chunk, const uint64_t* __restrict__ ch_end,
+                           const uint64_t* __restrict__ stream_base, unsigned long long* first_dec,
+                           const StgRec* __restrict__ stg, uint32_t scap, const uint8_t* __restrict__ ch_stg) {
+    // XCD-aware block order (workgroup b runs on XCD b % 8): each XCD takes one contiguous eighth of
+    // the records, so the staged lines a wave reads 32 bytes of (the rest: its neighbouring chunks'
+    // entries) are read again from that XCD's L2 by the waves that follow (24.1 -> 7.3 GB read at 3F)
+    const uint32_t nb = gridDim.x, bid = blockIdx.x, xcd = bid & 7, qn = nb >> 3, rn = nb & 7;
+    const uint32_t blk = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
+    // a wave takes EMS_R x 64 consecutive records
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t w0 = ((uint64_t)blk * (blockDim.x >> 6) + wv) * (64 * EMS_R);
+#pragma unroll
+    for (int k = 0; k < EMS_R; ++k) {
+        const uint64_t o = w0 + 64 * k + lane;
+        const bool inr = o < R;
+        uint64_t c = 0, b0 = 0, cnt = 0;
+        if (inr) {
+            c = blk_chunk[o >> 6];
+            while (ch_rec_base[c + 1] <= o) ++c;  // (64 consecutive records span few chunks)
+            b0 = ch_rec_base[c];
+            cnt = ch_rec_base[c + 1] - b0;
+        }
+        const bool live = inr && ch_stg[c] && cnt <= scap;  // (else k_emit / k_emit_fixed)
+        const uint64_t i = o - b0;
+        uint64_t hi = 0, lo = 0, ad = 0, cs = 0;
+        uint32_t kl = 0, sidx = 0;
+        const uint8_t* run = nullptr;
+        const uint16_t* sl = nullptr;
+        const StgRec* sg = nullptr;
         if (live) {
+            const uint32_t r = chunk_run[c];
+            run = (const uint8_t*)runs[r].ptr;
+            sidx = runs[r].stream;
+            cs = 1 + (c - runs[r].chunk_base) * chunk;
+            sl = slots + c * cap;
+            sg = stg + stg_base(c, scap);
+            const uint64_t p = cs + sl[i];
+            const uint64_t pn = i + 1 < cnt ? cs + sl[i + 1] : ch_end[c];
+            const uint4* e = (const uint4*)(sg + i * STG_W);
+            const uint4 x = e[0], y = e[1];
+            hi = ((uint64_t)x.y << 32) | x.x;
+            lo = ((uint64_t)x.w << 32) | x.z;
+            kl = y.z & 0x7FFFFFFFu;
+            ad = (uint64_t)(uintptr_t)(run + p);
             const uint64_t size = pn - p;
-            const uint64_t o = b0 + i;
             rec_addr[o] = ad;
             rec_fp[o] = ((uint64_t)y.y << 32) | y.x;
             rec_hi[o] = hi;
@@ -545,20 +565,23 @@ __global__ void __launch_bounds__(256) k_emit_stg(const RunInfo* __restrict__ ru
             rec_meta[o] = (uint32_t)size | (y.z & 0x80000000u);
             if (!y.w && !utf8_valid(run + p + 5, kl)) atomicOr(utf8_bad, 1u);
         }
-        if (first_dec) {  // the in-stream order check against the record before (k_emit's)
-            uint64_t x_hi = __shfl_up(hi, 1, EMS_G), x_lo = __shfl_up(lo, 1, EMS_G), x_ad = __shfl_up(ad, 1, EMS_G);
-            uint32_t x_kl = __shfl_up(kl, 1, EMS_G);
-            if (j0 == 0) {
-                x_hi = c_hi; x_lo = c_lo; x_ad = c_ad; x_kl = c_kl;
-            }
-            c_hi = __shfl(hi, EMS_G - 1, EMS_G);
-            c_lo = __shfl(lo, EMS_G - 1, EMS_G);
-            c_ad = __shfl(ad, EMS_G - 1, EMS_G);
-            c_kl = __shfl(kl, EMS_G - 1, EMS_G);
-            if (live && i > 0 && key_cmp(x_hi, x_lo, x_kl, (const uint8_t*)x_ad + 5, hi, lo, kl, run + p + 5) > 0) {
-                atomicMin(&first_dec[sidx], (unsigned long long)(b0 + i - 1 - sbase));
-                atomicOr(flags + 1, 1u);
-            }
+        if (!first_dec) continue;
+        // the in-stream order check against the record before in the chunk: the lane before holds
+        // it (record o - 1), except at lane 0; a chunk's first record is k_chunk_order's
+        uint64_t x_hi = __shfl_up(hi, 1, 64), x_lo = __shfl_up(lo, 1, 64), x_ad = __shfl_up(ad, 1, 64);
+        uint32_t x_kl = __shfl_up(kl, 1, 64);
+        if (!live || i == 0) continue;
+        if (lane == 0) {
+            const uint4* ep = (const uint4*)(sg + (i - 1) * STG_W);
+            const uint4 x = ep[0];
+            x_hi = ((uint64_t)x.y << 32) | x.x;
+            x_lo = ((uint64_t)x.w << 32) | x.z;
+            x_kl = ep[1].z & 0x7FFFFFFFu;
+            x_ad = (uint64_t)(uintptr_t)(run + cs + sl[i - 1]);
+        }
+        if (key_cmp(x_hi, x_lo, x_kl, (const uint8_t*)x_ad + 5, hi, lo, kl, (const uint8_t*)ad + 5) > 0) {
+            atomicMin(&first_dec[sidx], (unsigned long long)(o - 1 - stream_base[sidx]));
+            atomicOr(flags + 1, 1u);
         }
     }
 }
@@ -2963,17 +2986,19 @@ void launch_emit(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n
                  uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, uint64_t* rec_fp, uint32_t* utf8_bad,
                  const uint16_t* slots, uint32_t cap, uint64_t chunk, const uint64_t* ch_end,
                  const uint64_t* stream_base, unsigned long long* first_dec, const StgRec* stg, uint32_t scap,
-                 const uint8_t* ch_stg) {
+                 const uint8_t* ch_stg, uint64_t R_all, uint32_t* blk_chunk) {
     if (n_chunks)
         k_emit<<<blocks_for(n_chunks * EM_G, 256), 256, 0, s>>>(runs, n_runs, n_chunks, fmt, run_broken, ch_start,
                                                                 ch_rec_base, rec_addr, rec_hi, rec_lo, rec_klen, rec_meta,
                                                                 flags, rec_fp, utf8_bad, slots, cap, chunk, ch_end,
                                                                 stream_base, first_dec, stg, scap, ch_stg);
-    if (n_chunks)
-        k_emit_stg<<<blocks_for(n_chunks * EMS_G, 256), 256, 0, s>>>(runs, n_runs, n_chunks, ch_rec_base, rec_addr, rec_hi,
-                                                                    rec_lo, rec_klen, rec_meta, flags, rec_fp, utf8_bad,
-                                                                    slots, cap, chunk, ch_end, stream_base, first_dec,
-                                                                    stg, scap, ch_stg);
+    if (n_chunks && R_all) {
+        uint32_t* chunk_run = blk_chunk + R_all / 64 + 1;
+        k_blk_chunk<<<blocks_for(n_chunks, 256), 256, 0, s>>>(runs, n_runs, n_chunks, ch_rec_base, blk_chunk, chunk_run);
+        k_emit_stg<<<blocks_for(R_all, 256 * EMS_R), 256, 0, s>>>(runs, n_runs, R_all, ch_rec_base, blk_chunk, chunk_run, rec_addr, rec_hi,
+                                                           rec_lo, rec_klen, rec_meta, flags, rec_fp, utf8_bad, slots, cap,
+                                                           chunk, ch_end, stream_base, first_dec, stg, scap, ch_stg);
+    }
     if (R)
         k_emit_fixed<false><<<blocks_for(R, 256), 256, 0, s>>>(runs, n_runs, nullptr, R, fmt, (uint32_t*)run_broken, run_recb,
                                                                rec_addr, rec_hi, rec_lo, rec_klen, rec_meta, flags,

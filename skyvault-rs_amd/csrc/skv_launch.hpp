@@ -36,7 +36,7 @@ void launch_emit(hipStream_t, const RunInfo* runs, uint32_t n_runs, uint64_t n_c
                  uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, uint64_t* rec_fp, uint32_t* utf8_bad,
                  const uint16_t* slots, uint32_t cap, uint64_t chunk, const uint64_t* ch_end,
                  const uint64_t* stream_base, unsigned long long* first_dec, const StgRec* stg, uint32_t scap,
-                 const uint8_t* ch_stg);
+                 const uint8_t* ch_stg, uint64_t R_all, uint32_t* blk_chunk);  // blk_chunk: R_all / 64 + 1 + n_chunks
 void launch_parse_fixed(hipStream_t, const RunInfo* runs, uint32_t n_runs, const RunFmt* fmt, uint32_t* run_broken,
                         const uint64_t* run_recb, uint64_t R, uint64_t* rec_addr, uint64_t* rec_hi, uint64_t* rec_lo,
                         uint32_t* rec_klen, uint32_t* rec_meta, uint32_t* flags, const uint64_t* stream_base,
