@@ -83,10 +83,8 @@ void launch_gather(hipStream_t, const uint64_t* Kp, const uint64_t* n_runs, cons
                    const uint64_t* m_src, const uint64_t* seg_r0, uint8_t* out, uint64_t max_K,
                    const uint64_t* m_dup = nullptr, uint32_t* fp_bad = nullptr);
 // skv_wal.hip — SKV_SPLIT_BY_TABLE (wal_compaction.rs:66-174)
-#ifndef SKV_WAL_RPT
-#define SKV_WAL_RPT 2  // merged records per k_wal_fused thread
-#endif
-constexpr uint32_t WAL_FUSED_G = 256 * SKV_WAL_RPT;  // merged records per k_wal_fused workgroup
+constexpr uint32_t WAL_FUSED_RPT = 2;                 // merged records per k_wal_fused thread
+constexpr uint32_t WAL_FUSED_G = 256 * WAL_FUSED_RPT;  // merged records per k_wal_fused workgroup
 // k_wal_fused's mode word: bits 0-1 diagnostics (2: no output bytes); WAL_STRICT_CANON: a key whose
 // prefix is not the canonical "{id}." fails the stage (key-range parts of a pipelined host call)
 constexpr uint32_t WAL_STRICT_CANON = 4;

@@ -438,13 +438,10 @@ constexpr uint32_t WF_BADKEY = 1, WF_ORDER = 2, WF_TABLES = 4;
 // WF_R merged records per thread, strided (record k*WAL_T + tid of the workgroup's WF_G): one
 // look-back per WF_G records (at one record per thread the look-back wait was 1.85 of 7.0 ms at
 // config 5, profiles/r06/wal_probe.txt)
-constexpr int WAL_T = 256, WF_R = SKV_WAL_RPT, WF_G = WAL_T * WF_R;
+constexpr int WAL_T = 256, WF_R = (int)WAL_FUSED_RPT, WF_G = WAL_T * WF_R;
 static_assert(WF_G == (int)WAL_FUSED_G, "k_wal_fused's records per workgroup (host look-back sizing)");
 constexpr uint32_t WF_TBL = 4096;  // output blocks of a workgroup's span with a piece table (64 KiB)
 static_assert(WF_G <= 65536, "piece ids in the block table are 16-bit");
-#ifndef SKV_WAL_WPE
-#define SKV_WAL_WPE 4  // k_wal_fused's waves per SIMD asked of the register allocator
-#endif
 constexpr int WF_NB = 4;                 // a body's aligned 16-byte blocks loaded before the look-back
 constexpr uint32_t WF_STAGE = 64 * WF_G;  // LDS staging bytes (64 per record); the piece arrays share it
 static_assert(8 * (WF_G + 1) + 16 * WF_G + 2 * WF_TBL + WF_G <= WF_STAGE, "piece arrays fit the stage area");
@@ -474,7 +471,9 @@ struct WalPrev {
     bool canon;
 };
 
-__global__ void __launch_bounds__(WAL_T) __attribute__((amdgpu_waves_per_eu(SKV_WAL_WPE))) k_wal_fused(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ m_src,
+// (4 waves per SIMD asked of the register allocator: 128 VGPRs with a few spills, 5.55 ms at config 5,
+// against 134 VGPRs at 3 waves, 5.86 ms)
+__global__ void __launch_bounds__(WAL_T) __attribute__((amdgpu_waves_per_eu(4))) k_wal_fused(const uint64_t* __restrict__ Kp, const uint64_t* __restrict__ m_src,
                                                      const uint64_t* __restrict__ P, const uint64_t* __restrict__ Dp,
                                                      uint8_t* out, uint64_t* tstate, uint32_t* ticket, uint32_t* fail,
                                                      WalTStart* tlist, uint32_t* tcount, uint32_t tcap,
