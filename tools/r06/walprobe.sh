@@ -1,6 +1,7 @@
 #!/bin/bash
 # config 5: k_wal_fused phase knockouts (SKV_WAL_PROBE builds, output invalid: --no-check) and the
-# product, timed dispatches of k_wal_fused per variant (VARIANTS="base wp1 ...", base = libskv.so)
+# product, timed dispatches of k_wal_fused per variant (VARIANTS="base wp1 wp2", base = libskv.so;
+# build wpN with: make -C skyvault-rs_amd variant TAG=wpN VFLAGS=-DSKV_WAL_PROBE=N)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R="$PWD"; O="$R/gpurun_out/r06/wal"; mkdir -p "$O"
@@ -11,7 +12,7 @@ if [ "${PARITY:-1}" = 1 ]; then
     tests/test_gpu_hostpipe.py "tests/test_gpu_fullsize.py::test_config5_full_size" > "$O/pytest.log" 2>&1
   rc=$?; tail -4 "$O/pytest.log"; [ $rc -ne 0 ] && exit 1
 fi
-for v in ${VARIANTS:-base rpt1 rpt2 wp1 wp2}; do
+for v in ${VARIANTS:-base wp1 wp2}; do
   lib="$R/skyvault-rs_amd/skv/libskv.so"; chk=""
   [ "$v" != base ] && lib="$R/skyvault-rs_amd/skv/variants/libskv_$v.so"
   case $v in wp*) chk="--no-check";; esac
