@@ -269,42 +269,90 @@ __device__ uint64_t next_bad(const unsigned long long* bits, uint64_t from, uint
     return to;
 }
 
-// Sequential repair of each run's bad chunks from the true chain (exact; rare on real data).
-__global__ void k_fixup(const RunInfo* __restrict__ runs, uint32_t n_runs, const uint32_t* __restrict__ hdr_err,
+// Repair of each run's bad chunks from the true chain (exact; rare on real data): one wave per run,
+// its bad chunks in order. A bad chunk is re-speculated across the wave -- lane l takes 1/64 of it,
+// lane 0 from the true start E, the others from a speculative start in their sub-range (as k_spec
+// does over chunks) -- the links are checked in lane order (a lane whose start is not its
+// predecessor's end walks again from that end), and the starts are written at their scanned
+// offsets. (One lane walking a whole 64 KiB chunk took 0.8 ms at 3F for 51 bad chunks.)
+template <int UTF8>
+__device__ void fix_chunk(const uint8_t* run, uint64_t len, uint64_t E, uint64_t cs, uint64_t ce, uint16_t* sl,
+                          uint32_t cap, uint64_t& end, uint32_t& cnt, uint32_t& err) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t sub = (ce - cs + 63) / 64;
+    const uint64_t lo = cs + sub * lane < ce ? cs + sub * lane : ce;
+    const uint64_t hi = lane == 63 || lo + sub > ce ? ce : lo + sub;
+    uint64_t st = lane == 0 ? E : (lo < hi ? spec_start<UTF8>(run, len, lo, hi) : hi);
+    WalkRes w{st, 0, 0};
+    if (st != NO_POS && st < hi) w = walk_fast<UTF8>(run, len, st, hi, 0xFFFFFFFFu);
+    else if (st != NO_POS) w = WalkRes{st, 0, 0};
+    uint32_t last = 63;  // the last lane on the true chain
+    for (uint32_t l = 1; l < 64; ++l) {  // wave-uniform: every value below is a shuffle result
+        const uint32_t perr = __shfl(w.err, l - 1, 64);
+        if (perr) {
+            last = l - 1;
+            break;
+        }
+        const uint64_t pe = __shfl(w.end, l - 1, 64);
+        if (__shfl(st, l, 64) != pe && lane == l) {  // walk again from the true chain's position
+            st = pe;
+            w = pe < hi ? walk_fast<UTF8>(run, len, pe, hi, 0xFFFFFFFFu) : WalkRes{pe, 0, 0};
+        }
+    }
+    const uint32_t mine = lane <= last ? w.cnt : 0u;
+    uint32_t ex = mine;  // inclusive scan of the counts
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t v = __shfl_up(ex, d, 64);
+        if (lane >= (uint32_t)d) ex += v;
+    }
+    cnt = __shfl(ex, 63, 64);
+    end = __shfl(w.end, last, 64);
+    err = __shfl(w.err, last, 64);
+    ex -= mine;
+    if (mine && ex < cap) {  // the starts of this lane's records at their chunk positions
+        uint64_t p = st;
+        for (uint32_t i = 0; i < mine && ex + i < cap; ++i) {
+            sl[ex + i] = (uint16_t)(p - cs);
+            p += parse_rec<false, UTF8>(run, len, p).size;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64) k_fixup(const RunInfo* __restrict__ runs, uint32_t n_runs, const uint32_t* __restrict__ hdr_err,
                         const uint32_t* __restrict__ run_first_bad, const unsigned long long* __restrict__ bad_bits,
                         uint64_t* ch_start, uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, bool utf8,
                         uint64_t chunk, uint16_t* slots, uint32_t cap, uint8_t* ch_stg) {
-    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t r = blockIdx.x;  // one wave per run
     if (r >= n_runs) return;
-    uint32_t fb = run_first_bad[r];
+    const uint32_t fb = run_first_bad[r];
     if (fb == NO_POS32 || hdr_err[r]) return;
-    RunInfo R = runs[r];
+    const RunInfo R = runs[r];
     const uint8_t* run = (const uint8_t*)R.ptr;
-    uint64_t n = R.n_chunks, base = R.chunk_base;
+    const uint64_t n = R.n_chunks, base = R.chunk_base;
     uint64_t c = fb;
     while (c < n) {
-        uint64_t g = base + c;
+        const uint64_t g = base + c;
         if (ch_err[g - 1]) break;  // a real error in a valid chunk ends the run
-        uint64_t E = ch_end[g - 1];
-        uint64_t cs = 1 + c * chunk;
-        uint64_t ce = cs + chunk < R.len ? cs + chunk : R.len;
+        const uint64_t E = ch_end[g - 1];
+        const uint64_t cs = 1 + c * chunk;
+        const uint64_t ce = cs + chunk < R.len ? cs + chunk : R.len;
         uint64_t end = E;
         uint32_t cnt = 0, err = 0;
         if (E < ce) {
             uint16_t* sl = slots + g * cap;
-            // (no staging: one lane walks a run's repaired chunks in sequence, the fingerprints' ALU
-            // work would sit in that chain -- 2.0 against 0.84 ms at 3F; k_emit parses these chunks)
-            WalkRes w = utf8 ? walk_fast<1>(run, R.len, E, ce, 0xFFFFFFFFu, GLoad(), sl, cap, cs)
-                             : walk_fast<0>(run, R.len, E, ce, 0xFFFFFFFFu, GLoad(), sl, cap, cs);
-            ch_stg[g] = 0;
-            end = w.end;
-            cnt = w.cnt;
-            err = w.err;
+            if (utf8) fix_chunk<1>(run, R.len, E, cs, ce, sl, cap, end, cnt, err);
+            else fix_chunk<0>(run, R.len, E, cs, ce, sl, cap, end, cnt, err);
         }
-        ch_start[g] = E;
-        ch_end[g] = end;
-        ch_cnt[g] = cnt;
-        ch_err[g] = err;
+        __syncthreads();  // (every lane's reads of this chunk's old state are done)
+        if (threadIdx.x == 0) {
+            ch_stg[g] = 0;  // (k_emit parses a repaired chunk from its record starts)
+            ch_start[g] = E;
+            ch_end[g] = end;
+            ch_cnt[g] = cnt;
+            ch_err[g] = err;
+        }
+        __syncthreads();
         if (err) break;
         ++c;
         if (c >= n) break;
@@ -2962,8 +3010,8 @@ void launch_fixup(hipStream_t s, const RunInfo* runs, uint32_t n_runs, const uin
                   uint64_t* ch_end, uint32_t* ch_cnt, uint32_t* ch_err, bool utf8, uint64_t chunk, uint16_t* slots,
                   uint32_t cap, uint8_t* ch_stg) {
     if (n_runs)
-        k_fixup<<<blocks_for(n_runs, 64), 64, 0, s>>>(runs, n_runs, hdr_err, run_first_bad, bad_bits, ch_start, ch_end,
-                                                       ch_cnt, ch_err, utf8, chunk, slots, cap, ch_stg);
+        k_fixup<<<n_runs, 64, 0, s>>>(runs, n_runs, hdr_err, run_first_bad, bad_bits, ch_start, ch_end, ch_cnt, ch_err,
+                                       utf8, chunk, slots, cap, ch_stg);
 }
 void launch_err_chunk(hipStream_t s, const RunInfo* runs, uint32_t n_runs, uint64_t n_chunks, const uint32_t* hdr_err,
                       const uint32_t* ch_err, uint32_t* run_err_chunk) {
